@@ -1,0 +1,426 @@
+"""Host-side family formation: RawRecords -> the device family batch (include/bsdc.h).
+
+Everything here is record bookkeeping that needs no base or quality value -- which records the two
+tools keep, soft-clip stripping, MI grouping, the 4-record pairing plan and the template mates --
+so the kernel only ever sees records that reach the vote:
+
+* tool 1 dispatch (tools/1.convert_AG_to_CT.py:70-80): flags {0,99,147} pass, {1,83,163} are
+  converted unless their cigar has I, D or H, every other flag is dropped;
+* tool 2 (tools/2.extend_gap.py:155-186): hard-clipped records dropped (:160-161), soft clips
+  stripped (:168-176, identical to tool 1's own strip at :81-83), a missing/empty MI raises
+  (:179-180), groups keyed by MI.split('/')[0] in first-seen order; groups of exactly four
+  (:114-115) pair (99,163) and (83,147) and are emitted in the order 163, 99, 83, 147 with any
+  other flag dropped (:123-138);
+* family formation for the vote: one family per tool-2 group (DESIGN.md section 3.7 on how this
+  relates to fgbio's TemplateCoordinate grouping).
+"""
+from __future__ import annotations
+
+from dataclasses import dataclass
+from typing import List, Optional
+
+import numpy as np
+
+from . import records as R
+
+LINK_MATE_NONE = 0xFFFF
+LINK_AB = 1 << 16
+LINK_BA = 1 << 17
+LINK_COMPLEX = 1 << 18
+LINK_RT = 1 << 19
+LINK_CONVERT = 1 << 20
+LINK_EXT_RIGHT = 1 << 21
+LINK_EXT_LEFT = 1 << 22
+LINK_PARTNER_SHIFT = 23
+LINK_RD_IN = 1 << 25
+LINK_USABLE = 1 << 26
+
+MODE_CONVERT, MODE_EXTEND, MODE_VOTE, MODE_DUMP = 1, 2, 4, 8
+
+# families whose arena fits this many bytes run one per wavefront with the arena in LDS
+SMALL_ARENA_CAP = 8192
+LDS_TABLES = 2048 + 384
+LARGE_LDS_CAP = 64 * 1024 - LDS_TABLES
+
+
+def round16(x):
+    return (np.asarray(x, dtype=np.int64) + 15) & ~np.int64(15)
+
+
+def arena_bytes(n, sum_len, max_len, complex_ops):
+    """Mirror of ArenaLayout (csrc/bsdc_kernels.hip) / bsdc_family_arena_bytes."""
+    n = np.asarray(n, dtype=np.int64)
+    ssw = round16(np.asarray(max_len, dtype=np.int64) + 2)
+    total = round16(n * 48) + round16(n * 8) + 8 * ssw
+    cops = np.asarray(complex_ops, dtype=np.int64)
+    total = total + np.where(cops > 0, round16(4 * (cops + 4 * n)), 0)
+    total = total + round16(2 * np.asarray(sum_len, dtype=np.int64) + 4 * n)
+    return total
+
+
+class MissingMITag(ValueError):
+    pass
+
+
+@dataclass
+class FamilyBatch:
+    # ---- device arrays ----
+    fam_off: np.ndarray      # u32 [F+1]
+    rec_off: np.ndarray      # u32 [R]
+    rec_pos: np.ndarray      # i32
+    rec_lenflag: np.ndarray  # u32
+    rec_tid: np.ndarray      # i32
+    rec_link: np.ndarray     # u32
+    cig_off: np.ndarray      # u32
+    cig_info: np.ndarray     # u32
+    cigar: np.ndarray        # u32
+    rt: np.ndarray           # i32 [4R]
+    seq: np.ndarray          # u8 packed nt16
+    qual: np.ndarray         # u8
+    small_fams: np.ndarray   # u32
+    large_fams: np.ndarray   # u32
+    max_len: int
+    small_arena: int
+    large_arena: int
+    # ---- host bookkeeping ----
+    src: np.ndarray          # i64 [R] input record index
+    fam_mi: np.ndarray       # i32 [F] MI id of each family
+    n_bases: int
+
+    @property
+    def n_rec(self) -> int:
+        return int(self.rec_off.shape[0])
+
+    @property
+    def n_fam(self) -> int:
+        return int(self.fam_off.shape[0]) - 1
+
+    @property
+    def stride(self) -> int:
+        return int(round16(self.max_len + 2))
+
+    def device_arrays(self):
+        return {k: getattr(self, k) for k in (
+            "fam_off", "rec_off", "rec_pos", "rec_lenflag", "rec_tid", "rec_link", "cig_off",
+            "cig_info", "cigar", "rt", "seq", "qual", "small_fams", "large_fams")}
+
+
+def _per_record_ops(raw: R.RawRecords):
+    n = raw.n
+    rec = np.repeat(np.arange(n, dtype=np.int64), raw.n_cig)
+    ops = (raw.cigar & 0xF).astype(np.int64)
+    lens = (raw.cigar >> 4).astype(np.int64)
+    j = np.arange(ops.shape[0], dtype=np.int64) - raw.cig_off[rec] if ops.shape[0] else np.zeros(0, np.int64)
+    return rec, ops, lens, j
+
+
+def _has_op(rec, ops, n, op):
+    return np.bincount(rec[ops == op], minlength=n)[:n] > 0
+
+
+def tool1_plan(raw: R.RawRecords):
+    """tools/1.convert_AG_to_CT.py:70-80 -> (pass_through, convert) masks."""
+    n = raw.n
+    rec, ops, _, _ = _per_record_ops(raw)
+    f = raw.flag.astype(np.int64)
+    idh = _has_op(rec, ops, n, R.OP_I) | _has_op(rec, ops, n, R.OP_D) | _has_op(rec, ops, n, R.OP_H)
+    pas = np.isin(f, (0, 99, 147))
+    conv = np.isin(f, (1, 83, 163)) & ~idh
+    return pas, conv
+
+
+def _softclip_strip(raw: R.RawRecords):
+    """remove_softclips (tools/2.extend_gap.py:30-52): (lead S, trailing S, first kept op, kept op count)."""
+    n = raw.n
+    nc = raw.n_cig.astype(np.int64)
+    has = nc > 0
+    co = raw.cig_off.astype(np.int64)
+    first = np.where(has, raw.cigar[np.minimum(co, max(raw.cigar.shape[0] - 1, 0))] if raw.cigar.shape[0] else 0, 0)
+    first = np.asarray(first, dtype=np.int64)
+    fS = has & ((first & 0xF) == R.OP_S)
+    sL = np.where(fS, first >> 4, 0)
+    rem = nc - fS
+    lasti = co + nc - 1
+    last = np.where(has, raw.cigar[np.clip(lasti, 0, max(raw.cigar.shape[0] - 1, 0))] if raw.cigar.shape[0] else 0, 0)
+    last = np.asarray(last, dtype=np.int64)
+    lS = (rem > 0) & ((last & 0xF) == R.OP_S)
+    sR = np.where(lS, last >> 4, 0)
+    l0 = raw.l_seq.astype(np.int64)
+    a = np.maximum(l0 - sL, 0)
+    L = np.where(sR > 0, np.maximum(a - sR, 0), a)
+    kfirst = fS.astype(np.int64)
+    kn = rem - lS
+    return sL, L, kfirst, kn
+
+
+def build_family_batch(raw: R.RawRecords, mode: str = "full", small_cap: int = SMALL_ARENA_CAP) -> FamilyBatch:
+    """mode: 'full' (raw step-5 input: tools 1+2 then the vote), 'convert' (tool 1 alone: one
+    family per converted record), 'extend' (tool-1 output: tool 2 alone), 'vote' (tool-2 output)."""
+    n = raw.n
+    f = raw.flag.astype(np.int64)
+    rec, ops, lens, jop = _per_record_ops(raw)
+    hasH = _has_op(rec, ops, n, R.OP_H)
+
+    if mode in ("full", "convert"):
+        pas, conv = tool1_plan(raw)
+        keep1 = pas | conv
+    else:
+        conv = np.zeros(n, bool)
+        keep1 = np.ones(n, bool)
+    if mode == "convert":
+        keep2 = conv
+    elif mode in ("full", "extend"):
+        keep2 = keep1 & ~hasH
+    else:
+        keep2 = keep1
+
+    if mode != "convert":
+        miss = keep2 & (raw.mi_id < 0)
+        if miss.any():
+            k = int(np.nonzero(miss)[0][0])
+            raise MissingMITag("%s does not have MI tag." % raw.qname(k).decode())
+
+    sL, L, kfirst, kn = _softclip_strip(raw)
+    if mode == "vote":  # tool-2 output has no clips left; keep records as they are
+        sL = np.zeros(n, np.int64)
+        L = raw.l_seq.astype(np.int64)
+        kfirst = np.zeros(n, np.int64)
+        kn = raw.n_cig.astype(np.int64)
+
+    idx2 = np.nonzero(keep2)[0].astype(np.int64)
+    ext_right = np.zeros(n, bool)
+    ext_left = np.zeros(n, bool)
+    partner_local = np.zeros(n, np.int64)
+    rd_in = np.zeros(n, bool)
+
+    if mode == "convert":
+        order = idx2
+        fam_sizes = np.ones(idx2.shape[0], np.int64)
+        fam_mi = np.full(idx2.shape[0], -1, np.int32)
+    else:
+        keys = raw.mi_id[idx2].astype(np.int64)
+        if idx2.shape[0]:
+            uniq, first, inv = np.unique(keys, return_index=True, return_inverse=True)
+            rank = np.empty(uniq.shape[0], np.int64)
+            rank[np.argsort(first, kind="stable")] = np.arange(uniq.shape[0])
+            grp = rank[inv]
+            perm = np.argsort(grp, kind="stable")
+            members = idx2[perm]
+            gsz = np.bincount(grp, minlength=uniq.shape[0])
+            fam_mi = uniq[np.argsort(rank)].astype(np.int32)
+        else:
+            members = idx2
+            gsz = np.zeros(0, np.int64)
+            fam_mi = np.zeros(0, np.int32)
+        goff = np.zeros(gsz.shape[0] + 1, np.int64)
+        goff[1:] = np.cumsum(gsz)
+        keep_rec = np.ones(members.shape[0], bool)
+        out_members = members.copy()
+        fam_sizes = gsz.copy()
+        if mode in ("full", "extend"):
+            g4 = np.nonzero(gsz == 4)[0]
+            if g4.shape[0]:
+                base = goff[g4]
+                M = members[base[:, None] + np.arange(4)[None, :]]
+                Fl = f[M]
+                slot = np.full(Fl.shape, 4, np.int64)
+                for s, fl in enumerate((99, 163, 83, 147)):
+                    slot[Fl == fl] = s
+                key = slot * 4 + np.arange(4)[None, :]
+                ordr = np.argsort(key, axis=1, kind="stable")
+                outm = np.take_along_axis(M, ordr, axis=1)
+                outs = np.take_along_axis(slot, ordr, axis=1)
+                cnt = np.stack([(slot == s).sum(1) for s in range(4)], axis=1)
+                start = np.zeros_like(cnt)
+                start[:, 1:] = np.cumsum(cnt, axis=1)[:, :-1]
+                rows = np.arange(g4.shape[0])
+                # pair (99, 163): left = the 163 record, right = the 99 record; swapped in the
+                # output (tools/2.extend_gap.py:124-126 assigns process_read_pair's (left, right))
+                p1 = (cnt[:, 0] > 0) & (cnt[:, 1] > 0)
+                start = np.minimum(start, 3)  # only read where the pair exists
+                a_pos, b_pos = start[:, 0], start[:, 1]
+                a_rec = outm[rows, a_pos]
+                b_rec = outm[rows, b_pos]
+                outm[rows[p1], a_pos[p1]] = b_rec[p1]
+                outm[rows[p1], b_pos[p1]] = a_rec[p1]
+                # pair (83, 147): left = 83, right = 147
+                p2 = (cnt[:, 2] > 0) & (cnt[:, 3] > 0)
+                c_pos, d_pos = start[:, 2], start[:, 3]
+                c_rec = outm[rows, c_pos]
+                d_rec = outm[rows, d_pos]
+                # LA / RD of the left (converted) record
+                if mode == "full":
+                    la_b = np.ones(g4.shape[0], bool)
+                    la_c = np.ones(g4.shape[0], bool)
+                else:
+                    la = raw.la_tag if raw.la_tag is not None else np.full(n, -1, np.int32)
+                    rd = raw.rd_tag if raw.rd_tag is not None else np.full(n, -1, np.int32)
+                    for pm, lrec in ((p1, b_rec), (p2, c_rec)):
+                        bad = pm & ((la[lrec] < 0) | (rd[lrec] < 0))
+                        if bad.any():
+                            k = int(lrec[np.nonzero(bad)[0][0]])
+                            raise KeyError("%s: tag 'LA'/'RD' not present" % raw.qname(k).decode())
+                    la_b = la[b_rec] == 1
+                    la_c = la[c_rec] == 1
+                    rd_in[b_rec[p1]] = rd[b_rec[p1]] == 1
+                    rd_in[c_rec[p2]] = rd[c_rec[p2]] == 1
+                # number of kept records per group and their local positions
+                nkeep = (outs < 4).sum(1)
+                # roles; local indices are positions within the group's output list
+                q = p1 & la_b
+                ext_right[a_rec[q]] = True
+                partner_local[a_rec[q]] = a_pos[q]
+                ext_left[b_rec[p1]] = True
+                partner_local[b_rec[p1]] = b_pos[p1]
+                q = p2 & la_c
+                ext_right[d_rec[q]] = True
+                partner_local[d_rec[q]] = c_pos[q]
+                ext_left[c_rec[p2]] = True
+                partner_local[c_rec[p2]] = d_pos[p2]
+                # write back the new order; dropped flags go to the tail and are masked out
+                out_members[base[:, None] + np.arange(4)[None, :]] = outm
+                kr = np.arange(4)[None, :] < nkeep[:, None]
+                keep_rec[base[:, None] + np.arange(4)[None, :]] = kr
+                fam_sizes[g4] = nkeep
+        order = out_members[keep_rec]
+    nr = int(order.shape[0])
+    nf = int(fam_sizes.shape[0])
+    fam_off = np.zeros(nf + 1, np.int64)
+    fam_off[1:] = np.cumsum(fam_sizes)
+    fam_of = np.repeat(np.arange(nf, dtype=np.int64), fam_sizes)
+    local = np.arange(nr, dtype=np.int64) - fam_off[fam_of]
+
+    # ---- per batch record ----
+    Lb = L[order]
+    if nr and Lb.max() > 0xFFFF:
+        raise ValueError("record longer than 65535 bases")
+    rec_off = np.zeros(nr, np.int64)
+    if nr:
+        rec_off[1:] = np.cumsum(Lb)[:-1]
+    total = int(Lb.sum()) if nr else 0
+    if total >= 1 << 32:
+        raise ValueError("batch too large for 32-bit offsets; split it")
+    # gather stripped bases / quals
+    srcpos = np.repeat(raw.seq_off[order] + sL[order] - rec_off, Lb) + np.arange(total, dtype=np.int64)
+    codes = raw.seq[srcpos] if total else np.zeros(0, np.uint8)
+    qual = raw.qual[srcpos] if total else np.zeros(0, np.uint8)
+    seq = R.pack_nibbles(codes)
+
+    # stripped cigars, complex records
+    nops = kn[order]
+    cfirst = raw.cig_off[order] + kfirst[order]
+    opid = np.repeat(cfirst - np.concatenate([[0], np.cumsum(nops)[:-1]]) if nr else np.zeros(0, np.int64), nops) \
+        + np.arange(int(nops.sum()) if nr else 0, dtype=np.int64)
+    sc = raw.cigar[opid] if opid.shape[0] else np.zeros(0, np.uint32)
+    sc_rec = np.repeat(np.arange(nr, dtype=np.int64), nops)
+    sc_op = (sc & 0xF).astype(np.int64)
+    sc_len = (sc >> 4).astype(np.int64)
+    not_m = ~np.isin(sc_op, (R.OP_M, R.OP_EQ, R.OP_X))
+    complex_ = np.bincount(sc_rec[not_m], minlength=nr)[:nr] > 0 if nr else np.zeros(0, bool)
+    refc = np.isin(sc_op, R.REF_CONSUMING)
+    reflen = np.bincount(sc_rec[refc], weights=sc_len[refc], minlength=nr)[:nr].astype(np.int64) if nr else np.zeros(0, np.int64)
+    if mode == "vote":
+        reflen = np.where(complex_, reflen, Lb)
+    # compact cigar array holding only complex records' ops
+    keep_op = complex_[sc_rec] if nr else np.zeros(0, bool)
+    cigar_c = sc[keep_op].astype(np.uint32)
+    cnt_c = np.where(complex_, nops, 0)
+    cig_off = np.zeros(nr, np.int64)
+    if nr:
+        cig_off[1:] = np.cumsum(cnt_c)[:-1]
+    if complex_.any() and (nops[complex_].max() > 0xFFFF or reflen[complex_].max() > 0xFFFF):
+        raise ValueError("cigar too long")
+    cig_info = np.where(complex_, nops | (reflen << 16), 0).astype(np.uint32)
+
+    # link word
+    fo = f[order]
+    strand = raw.mi_strand[order].astype(np.int64)
+    usable = ((fo & 1) != 0) & ((fo & 0x900) == 0) & (strand >= 0)
+    link = np.full(nr, LINK_MATE_NONE, np.int64)
+    # template mates: first usable R1 of a name -> first usable R2 of the name, within a family
+    name = raw.name_id[order].astype(np.int64)
+    key = fam_of * (int(name.max()) + 1 if nr else 1) + name
+    r1 = usable & ((fo & 0x40) != 0)
+    r2 = usable & ((fo & 0x80) != 0)
+    i1 = np.nonzero(r1)[0]
+    i2 = np.nonzero(r2)[0]
+    if i1.shape[0] and i2.shape[0]:
+        u1, f1 = np.unique(key[i1], return_index=True)
+        u2, f2 = np.unique(key[i2], return_index=True)
+        _, ia, ib = np.intersect1d(u1, u2, assume_unique=True, return_indices=True)
+        a = i1[f1[ia]]
+        b = i2[f2[ib]]
+        link[a] = local[b]
+    link |= np.where(strand == 0, LINK_AB, 0) | np.where(strand == 1, LINK_BA, 0)
+    link |= np.where(complex_, LINK_COMPLEX, 0)
+    link |= np.where(conv[order], LINK_CONVERT, 0)
+    link |= np.where(ext_right[order], LINK_EXT_RIGHT, 0)
+    link |= np.where(ext_left[order], LINK_EXT_LEFT, 0)
+    link |= np.where(ext_right[order] | ext_left[order], partner_local[order] << LINK_PARTNER_SHIFT, 0)
+    link |= np.where(rd_in[order], LINK_RD_IN, 0)
+    link |= np.where(usable, LINK_USABLE, 0)
+
+    # read-through candidates (stale mate fields, MC tag)
+    rt = np.zeros((nr, 4), np.int64)
+    has_mc = raw.mc_off[order] >= 0
+    base_rt = usable & ((fo & 0xC) == 0) & (raw.next_tid[order] == raw.tid[order]) & has_mc
+    if base_rt.any():
+        # MC cigars are stored contiguously in record order (records.py / synth.py invariant)
+        mcn = np.where(raw.mc_off >= 0, raw.mc_n, 0).astype(np.int64)
+        mrec = np.repeat(np.arange(raw.n, dtype=np.int64), mcn)
+        mo = raw.mc_cigar[:mrec.shape[0]]
+        mop = (mo & 0xF).astype(np.int64)
+        mln = (mo >> 4).astype(np.int64)
+        refm = np.isin(mop, R.REF_CONSUMING)
+        mref = np.bincount(mrec[refm], weights=mln[refm], minlength=raw.n)[:raw.n].astype(np.int64)
+        clip = np.isin(mop, (R.OP_S, R.OP_H))
+        ncum = np.cumsum(~clip)
+        mstart = np.zeros(raw.n, np.int64)
+        mstart[1:] = np.cumsum(mcn)[:-1]
+        base = np.where(mstart > 0, ncum[np.maximum(mstart - 1, 0)], 0) if ncum.shape[0] else np.zeros(raw.n, np.int64)
+        upto = ncum - base[mrec]                       # non-clip ops up to and including this one
+        before = upto - (~clip)
+        rtot = np.bincount(mrec[~clip], minlength=raw.n)[:raw.n]
+        after = rtot[mrec] - upto
+        lm = clip & (before == 0)
+        tm = clip & (after == 0)
+        lead = np.bincount(mrec[lm], weights=mln[lm], minlength=raw.n)[:raw.n].astype(np.int64)
+        trail = np.bincount(mrec[tm], weights=mln[tm], minlength=raw.n)[:raw.n].astype(np.int64)
+        np_ = raw.next_pos[order].astype(np.int64)
+        mate_us = np_ - lead[order]
+        mate_ue = np_ + mref[order] - 1 + trail[order]
+        pos = raw.pos[order].astype(np.int64)
+        rl = np.where(complex_, reflen, Lb)
+        neg = (fo & 16) != 0
+        cand = base_rt & np.where(neg, pos - 2 < mate_us, pos + rl - 1 + 2 > mate_ue)
+        link |= np.where(cand, LINK_RT, 0)
+        rt[:, 0] = np_
+        rt[:, 1] = raw.tlen[order]
+        rt[:, 2] = mate_us
+        rt[:, 3] = mate_ue
+        rt[~cand] = 0
+
+    # ---- family classes ----
+    sum_len = np.bincount(fam_of, weights=Lb, minlength=nf)[:nf].astype(np.int64) if nr else np.zeros(nf, np.int64)
+    max_len_f = np.zeros(nf, np.int64)
+    if nr:
+        np.maximum.at(max_len_f, fam_of, Lb)
+    cops = np.bincount(fam_of, weights=cnt_c, minlength=nf)[:nf].astype(np.int64) if nr else np.zeros(nf, np.int64)
+    need = arena_bytes(fam_sizes, sum_len, max_len_f, cops)
+    small = need <= small_cap
+    small_fams = np.nonzero(small)[0].astype(np.uint32)
+    large_fams = np.nonzero(~small)[0].astype(np.uint32)
+    small_arena = int(round16(need[small].max())) if small.any() else 16
+    large_arena = int(round16(need[~small].max())) if (~small).any() else 16
+
+    return FamilyBatch(
+        fam_off=fam_off.astype(np.uint32), rec_off=rec_off.astype(np.uint32),
+        rec_pos=raw.pos[order].astype(np.int32),
+        rec_lenflag=(Lb | (fo << 16)).astype(np.uint32), rec_tid=raw.tid[order].astype(np.int32),
+        rec_link=link.astype(np.uint32), cig_off=cig_off.astype(np.uint32), cig_info=cig_info,
+        cigar=cigar_c if cigar_c.shape[0] else np.zeros(1, np.uint32),
+        rt=rt.reshape(-1).astype(np.int32), seq=seq if seq.shape[0] else np.zeros(1, np.uint8),
+        qual=qual if qual.shape[0] else np.zeros(1, np.uint8),
+        small_fams=small_fams, large_fams=large_fams, max_len=int(Lb.max()) if nr else 0,
+        small_arena=small_arena, large_arena=large_arena, src=order.astype(np.int64),
+        fam_mi=fam_mi.astype(np.int32), n_bases=total)

@@ -1,0 +1,165 @@
+"""Device side of the step: family batches in HBM (torch tensors as plumbing), libbsdc launches.
+
+The Engine owns one libbsdc context per GPU.  ``upload`` copies a FamilyBatch into HBM once;
+``run`` enqueues the kernels on the current torch stream (so torch events time exactly them) and
+``fetch`` brings the consensus (and the optional stage dump) back to the host.
+"""
+from __future__ import annotations
+
+import ctypes as C
+from dataclasses import dataclass
+from typing import Dict, Optional
+
+import numpy as np
+import torch
+
+from . import _lib
+from .batch import FamilyBatch
+from .records import Reference
+
+
+@dataclass
+class ConsensusParams:
+    """fgbio CallDuplexConsensusReads options, defaults from main.snake.py:163."""
+
+    error_rate_pre_umi: float = 45.0
+    error_rate_post_umi: float = 30.0
+    min_input_base_quality: int = 0
+    consensus_call_overlapping_bases: bool = True
+    min_reads: int = 0
+
+
+def _dptr(t: torch.Tensor) -> int:
+    return int(t.data_ptr())
+
+
+class DeviceBatch:
+    """A FamilyBatch resident in HBM plus its output buffers."""
+
+    def __init__(self, fb: FamilyBatch, device: torch.device, dump: bool = False):
+        self.fb = fb
+        self.device = device
+        self.t: Dict[str, torch.Tensor] = {}
+        for k, v in fb.device_arrays().items():
+            a = np.ascontiguousarray(v)
+            if a.size == 0:
+                a = np.zeros(1, dtype=a.dtype)
+            # torch has no uint32/uint16 arithmetic we need; move raw bytes
+            self.t[k] = torch.from_numpy(a.view(np.uint8)).to(device, non_blocking=False)
+        F, Rn = fb.n_fam, fb.n_rec
+        self.stride = fb.stride
+        self.status = torch.zeros(max(F, 1), dtype=torch.uint8, device=device)
+        self.len = torch.zeros(max(2 * F, 1), dtype=torch.int16, device=device)
+        self.seq = torch.zeros(max(F * self.stride, 16), dtype=torch.uint8, device=device)
+        self.qual = torch.zeros(max(2 * F * self.stride, 16), dtype=torch.uint8, device=device)
+        self.dump = dump
+        if dump:
+            cap = fb.n_bases + 2 * Rn + 16
+            self.dump_pos = torch.zeros(max(Rn, 1), dtype=torch.int32, device=device)
+            self.dump_len = torch.zeros(max(Rn, 1), dtype=torch.int16, device=device)
+            self.dump_tags = torch.zeros(max(Rn, 1), dtype=torch.uint8, device=device)
+            self.dump_seq = torch.zeros(cap, dtype=torch.uint8, device=device)
+            self.dump_qual = torch.zeros(cap, dtype=torch.uint8, device=device)
+        lds_cap = 64 * 1024 - (2048 + 384)
+        nl = int(fb.large_fams.shape[0])
+        self.scratch = None
+        if nl and fb.large_arena > lds_cap:
+            self.scratch = torch.zeros(nl * fb.large_arena, dtype=torch.uint8, device=device)
+        self._b = _lib.FamilyBatchC()
+        b = self._b
+        b.n_rec, b.n_fam = Rn, F
+        for k in ("fam_off", "rec_off", "rec_pos", "rec_lenflag", "rec_tid", "rec_link", "cig_off",
+                  "cig_info", "cigar", "rt", "seq", "qual", "small_fams", "large_fams"):
+            setattr(b, k, _dptr(self.t[k]))
+        b.n_small = int(fb.small_fams.shape[0])
+        b.n_large = nl
+        b.max_len = fb.max_len
+        b.small_arena = fb.small_arena
+        b.large_arena = fb.large_arena
+        self._o = _lib.ConsensusC()
+        o = self._o
+        o.stride = self.stride
+        o.status, o.len, o.seq, o.qual = _dptr(self.status), _dptr(self.len), _dptr(self.seq), _dptr(self.qual)
+        if dump:
+            o.dump_pos, o.dump_len, o.dump_tags = _dptr(self.dump_pos), _dptr(self.dump_len), _dptr(self.dump_tags)
+            o.dump_seq, o.dump_qual = _dptr(self.dump_seq), _dptr(self.dump_qual)
+        o.scratch = _dptr(self.scratch) if self.scratch is not None else None
+
+    def fetch(self):
+        """-> dict of numpy arrays (consensus and, if dumped, the post-tool records)."""
+        F = self.fb.n_fam
+        out = {
+            "status": self.status[:F].cpu().numpy(),
+            "len": self.len[:2 * F].cpu().numpy().view(np.uint16).astype(np.int32).reshape(F, 2),
+            "seq": self.seq[:F * self.stride].cpu().numpy().reshape(F, 2, self.stride // 2),
+            "qual": self.qual[:2 * F * self.stride].cpu().numpy().reshape(F, 2, self.stride),
+            "stride": self.stride,
+        }
+        if self.dump:
+            Rn = self.fb.n_rec
+            out["dump_pos"] = self.dump_pos[:Rn].cpu().numpy()
+            out["dump_len"] = self.dump_len[:Rn].cpu().numpy().view(np.uint16).astype(np.int32)
+            out["dump_tags"] = self.dump_tags[:Rn].cpu().numpy()
+            out["dump_seq"] = self.dump_seq.cpu().numpy()
+            out["dump_qual"] = self.dump_qual.cpu().numpy()
+        return out
+
+
+class Engine:
+    """One libbsdc context on one GPU."""
+
+    def __init__(self, device_index: int = 0, params: Optional[ConsensusParams] = None):
+        if not torch.cuda.is_available():
+            raise RuntimeError("no GPU: the bsdc product path runs on MI355X only (no CPU fallback)")
+        self.lib = _lib.load()
+        self.device_index = device_index
+        self.device = torch.device("cuda", device_index)
+        self.params = params or ConsensusParams()
+        p = _lib.Params(self.params.error_rate_pre_umi, self.params.error_rate_post_umi,
+                        self.params.min_input_base_quality, int(self.params.consensus_call_overlapping_bases),
+                        self.params.min_reads, 0)
+        h = C.c_void_p()
+        rc = self.lib.bsdc_ctx_create(device_index, C.byref(p), C.byref(h))
+        if rc != 0:
+            raise RuntimeError("bsdc_ctx_create failed (%d)" % rc)
+        self.ctx = h
+        self.ref: Optional[Reference] = None
+
+    def close(self):
+        if self.ctx:
+            self.lib.bsdc_ctx_destroy(self.ctx)
+            self.ctx = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+    def _check(self, rc: int, what: str):
+        if rc != 0:
+            raise RuntimeError("%s failed (%d): %s" % (what, rc, self.lib.bsdc_last_error(self.ctx).decode()))
+
+    def load_reference(self, ref: Reference):
+        packed = np.ascontiguousarray(ref.packed)
+        off = np.ascontiguousarray(ref.contig_off, dtype=np.int64)
+        ln = np.ascontiguousarray(ref.contig_len, dtype=np.int64)
+        rc = self.lib.bsdc_load_reference(self.ctx, packed.ctypes.data, ref.n_nibbles, off.ctypes.data,
+                                          ln.ctypes.data, len(ref.names))
+        self._check(rc, "bsdc_load_reference")
+        self.ref = ref
+
+    def upload(self, fb: FamilyBatch, dump: bool = False) -> DeviceBatch:
+        with torch.cuda.device(self.device):
+            return DeviceBatch(fb, self.device, dump)
+
+    def run(self, db: DeviceBatch, mode: int, stream: Optional[torch.cuda.Stream] = None):
+        s = stream if stream is not None else torch.cuda.current_stream(self.device)
+        rc = self.lib.bsdc_run(self.ctx, C.byref(db._b), C.byref(db._o), mode, C.c_void_p(s.cuda_stream))
+        self._check(rc, "bsdc_run")
+
+    def tables(self):
+        lr = np.zeros(256, np.int64)
+        thr = np.zeros(94, np.float32)
+        self._check(self.lib.bsdc_get_tables(self.ctx, lr.ctypes.data, thr.ctypes.data), "bsdc_get_tables")
+        return lr, thr

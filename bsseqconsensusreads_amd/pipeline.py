@@ -1,0 +1,206 @@
+"""The step-5 path as the reference's stages see it, on top of the Engine.
+
+* ``run_tool1``  -- tools/1.convert_AG_to_CT.py semantics: input order, pass-through records
+  unchanged, converted records replaced, every other record dropped.
+* ``run_tool2``  -- tools/2.extend_gap.py semantics on tool-1 output (RD/LA tags from the input).
+* ``run_step5``  -- convert_Bstrain -> extend -> groupsort_convert -> callduplex in one device pass;
+  returns the consensus pair per family and, on request, the tool-2 records (parity dump).
+* ``run_duplex`` -- callduplex alone on already converted + extended records.
+"""
+from __future__ import annotations
+
+from dataclasses import dataclass
+from typing import List, Optional
+
+import numpy as np
+
+from . import records as R
+from .batch import FamilyBatch, build_family_batch
+from .device import Engine
+from ._lib import MODE_CONVERT, MODE_DUMP, MODE_EXTEND, MODE_VOTE
+
+
+@dataclass
+class OutRecords:
+    """Output records of a tool stage; everything not listed is the input record's (``src``)."""
+
+    src: np.ndarray      # i64 input record index
+    pos: np.ndarray
+    l_seq: np.ndarray
+    seq_off: np.ndarray
+    seq: np.ndarray      # nt16 codes
+    qual: np.ndarray
+    n_cig: np.ndarray
+    cig_off: np.ndarray
+    cigar: np.ndarray
+    rd: np.ndarray       # -1 = tag untouched by this stage
+    la: np.ndarray
+
+    @property
+    def n(self):
+        return int(self.src.shape[0])
+
+    def record(self, k: int):
+        o, l = int(self.seq_off[k]), int(self.l_seq[k])
+        c, m = int(self.cig_off[k]), int(self.n_cig[k])
+        return dict(src=int(self.src[k]), pos=int(self.pos[k]), seq=self.seq[o:o + l], qual=self.qual[o:o + l],
+                    cigar=self.cigar[c:c + m], rd=int(self.rd[k]), la=int(self.la[k]))
+
+
+@dataclass
+class Consensus:
+    fam_mi: np.ndarray     # i32 MI id per family (RawRecords.mi_names index)
+    status: np.ndarray     # u8 bit0 emitted, bit1 AB used, bit2 BA used
+    length: np.ndarray     # [F, 2]
+    seq: np.ndarray        # [F, 2, stride] nt16 codes
+    qual: np.ndarray       # [F, 2, stride]
+
+
+def _stripped_cigar(raw: R.RawRecords, k: int, strip: bool) -> List[int]:
+    ops = [int(x) for x in raw.record_cigar(k)]
+    if strip:
+        if ops and (ops[0] & 0xF) == R.OP_S:
+            ops = ops[1:]
+        if ops and (ops[-1] & 0xF) == R.OP_S:
+            ops = ops[:-1]
+    return ops
+
+
+def _records_from_dump(raw: R.RawRecords, fb: FamilyBatch, out: dict, strip: bool) -> OutRecords:
+    n = fb.n_rec
+    lens = out["dump_len"][:n].astype(np.int64)
+    seq_off = np.zeros(n, np.int64)
+    if n:
+        seq_off[1:] = np.cumsum(lens)[:-1]
+    d = fb.rec_off.astype(np.int64) + 2 * np.arange(n, dtype=np.int64)
+    idx = np.repeat(d - seq_off, lens) + np.arange(int(lens.sum()), dtype=np.int64)
+    seq = out["dump_seq"][idx]
+    qual = out["dump_qual"][idx]
+    tags = out["dump_tags"][:n]
+    cig, ncig = [], []
+    rd = np.full(n, -1, np.int32)
+    la = np.full(n, -1, np.int32)
+    for b in range(n):
+        k = int(fb.src[b])
+        ops = _stripped_cigar(raw, k, strip)
+        t = int(tags[b])
+        if t & 2:  # converted in this launch: [(M,1)] + cigar, RD trims the last op
+            ops = [(1 << 4)] + ops
+            if t & 1:
+                last = ops[-1]
+                if (last >> 4) > 1:
+                    ops[-1] = last - (1 << 4)
+                else:
+                    ops.pop()
+            rd[b] = t & 1
+            la[b] = 1
+        elif t & 4:
+            ops = [(1 << 4)] + ops
+        if t & 8:
+            ops = ops + [(1 << 4)]
+        cig.extend(ops)
+        ncig.append(len(ops))
+    n_cig = np.asarray(ncig, np.int32)
+    cig_off = np.zeros(n, np.int64)
+    if n:
+        cig_off[1:] = np.cumsum(n_cig)[:-1]
+    return OutRecords(fb.src.copy(), out["dump_pos"][:n].astype(np.int32), lens.astype(np.int32), seq_off, seq, qual,
+                      n_cig, cig_off, np.asarray(cig, np.uint32), rd, la)
+
+
+def _concat_records(parts: List[OutRecords], order: np.ndarray) -> OutRecords:
+    """Merge record sets and put them in `order` of src."""
+    src = np.concatenate([p.src for p in parts])
+    where = {int(s): (pi, k) for pi, p in enumerate(parts) for k, s in enumerate(p.src)}
+    pos, l_seq, seqs, quals, ncig, cigs, rd, la = [], [], [], [], [], [], [], []
+    for s in order:
+        pi, k = where[int(s)]
+        r = parts[pi].record(k)
+        pos.append(r["pos"])
+        l_seq.append(len(r["seq"]))
+        seqs.append(r["seq"])
+        quals.append(r["qual"])
+        ncig.append(len(r["cigar"]))
+        cigs.append(r["cigar"])
+        rd.append(r["rd"])
+        la.append(r["la"])
+    l_seq = np.asarray(l_seq, np.int32)
+    so = np.zeros(len(order), np.int64)
+    if len(order):
+        so[1:] = np.cumsum(l_seq)[:-1]
+    ncig = np.asarray(ncig, np.int32)
+    co = np.zeros(len(order), np.int64)
+    if len(order):
+        co[1:] = np.cumsum(ncig)[:-1]
+    cat = lambda xs, dt: np.concatenate(xs).astype(dt) if xs else np.zeros(0, dt)
+    return OutRecords(np.asarray(order, np.int64), np.asarray(pos, np.int32), l_seq, so, cat(seqs, np.uint8),
+                      cat(quals, np.uint8), ncig, co, cat(cigs, np.uint32), np.asarray(rd, np.int32),
+                      np.asarray(la, np.int32))
+
+
+def _passthrough(raw: R.RawRecords, idx: np.ndarray) -> OutRecords:
+    parts_seq = [raw.record_seq(int(k)) for k in idx]
+    parts_q = [raw.record_qual(int(k)) for k in idx]
+    parts_c = [raw.record_cigar(int(k)) for k in idx]
+    l = np.asarray([len(x) for x in parts_seq], np.int32)
+    so = np.zeros(len(idx), np.int64)
+    if len(idx):
+        so[1:] = np.cumsum(l)[:-1]
+    nc = np.asarray([len(x) for x in parts_c], np.int32)
+    co = np.zeros(len(idx), np.int64)
+    if len(idx):
+        co[1:] = np.cumsum(nc)[:-1]
+    cat = lambda xs, dt: np.concatenate(xs).astype(dt) if xs else np.zeros(0, dt)
+    return OutRecords(np.asarray(idx, np.int64), raw.pos[idx].astype(np.int32), l, so, cat(parts_seq, np.uint8),
+                      cat(parts_q, np.uint8), nc, co, cat(parts_c, np.uint32), np.full(len(idx), -1, np.int32),
+                      np.full(len(idx), -1, np.int32))
+
+
+def run_tool1(engine: Engine, raw: R.RawRecords) -> OutRecords:
+    """tools/1.convert_AG_to_CT.py:67-186 over a record stream (reference must be loaded)."""
+    from .batch import tool1_plan
+    pas, conv = tool1_plan(raw)
+    fb = build_family_batch(raw, "convert")
+    db = engine.upload(fb, dump=True)
+    engine.run(db, MODE_CONVERT | MODE_DUMP)
+    out = db.fetch()
+    converted = _records_from_dump(raw, fb, out, strip=True)
+    passed = _passthrough(raw, np.nonzero(pas)[0])
+    order = np.nonzero(pas | conv)[0]
+    return _concat_records([passed, converted], order)
+
+
+def run_tool2(engine: Engine, raw: R.RawRecords) -> OutRecords:
+    """tools/2.extend_gap.py:145-190 on tool-1 output (LA / RD tags in the input)."""
+    fb = build_family_batch(raw, "extend")
+    db = engine.upload(fb, dump=True)
+    engine.run(db, MODE_EXTEND | MODE_DUMP)
+    return _records_from_dump(raw, fb, db.fetch(), strip=True)
+
+
+def consensus_from_output(fb: FamilyBatch, out: dict) -> Consensus:
+    F = fb.n_fam
+    stride = out["stride"]
+    packed = out["seq"].reshape(F, 2, stride // 2)
+    seq = np.empty((F, 2, stride), np.uint8)
+    seq[:, :, 0::2] = packed >> 4
+    seq[:, :, 1::2] = packed & 0xF
+    return Consensus(fb.fam_mi.copy(), out["status"], out["len"], seq, out["qual"])
+
+
+def run_step5(engine: Engine, raw: R.RawRecords, dump: bool = False):
+    """Rules convert_Bstrain .. callduplex (main.snake.py:121-164) -> (Consensus, tool-2 records or None)."""
+    fb = build_family_batch(raw, "full")
+    db = engine.upload(fb, dump=dump)
+    engine.run(db, MODE_CONVERT | MODE_EXTEND | MODE_VOTE | (MODE_DUMP if dump else 0))
+    out = db.fetch()
+    t2 = _records_from_dump(raw, fb, out, strip=True) if dump else None
+    return consensus_from_output(fb, out), t2
+
+
+def run_duplex(engine: Engine, raw: R.RawRecords) -> Consensus:
+    """callduplex alone (main.snake.py:155-164) on converted + extended records."""
+    fb = build_family_batch(raw, "vote")
+    db = engine.upload(fb)
+    engine.run(db, MODE_VOTE)
+    return consensus_from_output(fb, db.fetch())

@@ -1,0 +1,141 @@
+/* bsdc.h -- C-ABI of libbsdc, the MI355X (gfx950) step-5 duplex path.
+ *
+ * The reference has no plugin API: its boundary is the file contract of the four Snakemake rules
+ * convert_Bstrain -> extend -> groupsort_convert -> callduplex (main.snake.py:121-164).  Each entry
+ * point below replaces one piece of that contract; INTEGRATION.md shows the ctypes binding the
+ * Python host (bsseqconsensusreads_amd/_lib.py) uses, which is also what a maintainer of the
+ * reference would add in place of the `python3 tools/...` / `fgbio ...` shell lines.
+ *
+ *   bsdc_convert      replaces tools/1.convert_AG_to_CT.py:69-186 (per-record B-strand conversion)
+ *   bsdc_extend       replaces tools/2.extend_gap.py:112-140       (4-record gap extension)
+ *   bsdc_duplex_call  replaces main.snake.py:155-164 fgbio CallDuplexConsensusReads (and, with
+ *                     BSDC_MODE_CONVERT|BSDC_MODE_EXTEND in `mode`, the two tools in front of it)
+ *
+ * Conventions: every function returns 0 on success and a negative errno-style code on failure
+ * (message via bsdc_last_error).  Batch and output pointers are DEVICE pointers owned by the
+ * caller; work is enqueued on `stream` (a hipStream_t, NULL = the null stream) and is
+ * asynchronous.  The reference genome is copied into library-owned device memory.  One context
+ * per GPU per host thread; no global mutable state.  Output order == input family order.
+ */
+#ifndef BSDC_H
+#define BSDC_H
+#include <stdint.h>
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define BSDC_ABI_VERSION 1
+
+#define BSDC_EINVAL (-22)
+#define BSDC_ENOMEM (-12)
+#define BSDC_EDEVICE (-5)
+
+/* fgbio CallDuplexConsensusReads flags as the pipeline passes them (main.snake.py:163) */
+typedef struct {
+    double error_rate_pre_umi;                /* --error-rate-pre-umi=45 */
+    double error_rate_post_umi;               /* --error-rate-post-umi=30 */
+    int32_t min_input_base_quality;           /* --min-input-base-quality=0 */
+    int32_t consensus_call_overlapping_bases; /* --consensus-call-overlapping-bases=true */
+    int32_t min_reads;                        /* --min-reads=0 (only 0 is supported) */
+    int32_t reserved;
+} bsdc_params;
+
+/* Per-record `link` word (host-built) */
+#define BSDC_LINK_MATE_MASK 0xFFFFu   /* template mate (R2 of this R1) index within family; 0xFFFF = none */
+#define BSDC_LINK_AB (1u << 16)       /* MI ends in /A */
+#define BSDC_LINK_BA (1u << 17)       /* MI ends in /B */
+#define BSDC_LINK_COMPLEX (1u << 18)  /* cigar is not a single M-like run: read cig_* */
+#define BSDC_LINK_RT (1u << 19)       /* read-through trim candidate: read rt[] */
+#define BSDC_LINK_CONVERT (1u << 20)  /* tool 1 converts this record (flag 1/83/163) */
+#define BSDC_LINK_EXT_RIGHT (1u << 21) /* tool 2: gets the partner's first base prepended */
+#define BSDC_LINK_EXT_LEFT (1u << 22) /* tool 2: gets the partner's last base appended if RD=1 */
+#define BSDC_LINK_PARTNER_SHIFT 23    /* 2 bits: tool-2 partner index within the family */
+#define BSDC_LINK_RD_IN (1u << 25)    /* RD tag of an already-converted input (extend-only mode) */
+#define BSDC_LINK_USABLE (1u << 26)   /* paired primary record with an /A or /B MI */
+
+/* A batch of MI families in HBM, structure-of-arrays.  Record r of family f is
+ * fam_off[f] <= r < fam_off[f+1]; its bases are nibbles rec_off[r] .. rec_off[r]+len-1 of `seq`
+ * (nt16 codes "=ACMGRSVTWYHKDBN", two per byte, high nibble first, as in BAM) and its quals the
+ * same indices of `qual`.  Soft clips are already stripped by the host (tools 1 and 2 both strip
+ * them before anything else).  rec_off must be the running sum of the lengths. */
+typedef struct {
+    int64_t n_rec;
+    int64_t n_fam;
+    const uint32_t *fam_off;     /* [n_fam+1] */
+    const uint32_t *rec_off;     /* [n_rec]   */
+    const int32_t *rec_pos;      /* [n_rec]   0-based leftmost aligned position */
+    const uint32_t *rec_lenflag; /* [n_rec]   length | flag << 16 */
+    const int32_t *rec_tid;      /* [n_rec]   */
+    const uint32_t *rec_link;    /* [n_rec]   BSDC_LINK_* */
+    const uint32_t *cig_off;     /* [n_rec]   complex records only: first op in `cigar` */
+    const uint32_t *cig_info;    /* [n_rec]   complex only: n_ops | reflen << 16 */
+    const uint32_t *cigar;       /*           BAM-encoded ops (soft/hard clips removed) */
+    const int32_t *rt;           /* [4*n_rec] RT records only: next_pos, tlen, mate unclipped start, end */
+    const uint8_t *seq;
+    const uint8_t *qual;
+    const uint32_t *small_fams;  /* families processed one wavefront each (LDS arena) */
+    int64_t n_small;
+    const uint32_t *large_fams;  /* families processed one workgroup each */
+    int64_t n_large;
+    int32_t max_len;             /* max record length */
+    int32_t small_arena;         /* LDS bytes per wavefront for small families (multiple of 16) */
+    int32_t large_arena;         /* bytes per workgroup for large families */
+    int32_t reserved;
+} bsdc_family_batch;
+
+/* Outputs (device pointers).  Consensus slot (f, end) holds `stride` bases. */
+typedef struct {
+    int32_t stride;              /* >= max_len + 2, multiple of 16 */
+    int32_t reserved;
+    uint8_t *status;             /* [n_fam] bit0 pair emitted, bit1 AB strand used, bit2 BA strand used */
+    uint16_t *len;               /* [2*n_fam] R1, R2 lengths */
+    uint8_t *seq;                /* [2*n_fam*stride/2] packed nt16 */
+    uint8_t *qual;               /* [2*n_fam*stride] */
+    /* optional stage dump (NULL = off): the records after tool 1 + tool 2 */
+    int32_t *dump_pos;           /* [n_rec] */
+    uint16_t *dump_len;          /* [n_rec] */
+    uint8_t *dump_tags;          /* [n_rec] bit0 RD=1, bit1 LA present, bit2 prepended M, bit3 appended M */
+    uint8_t *dump_seq;           /* [rec_off[r] + 2r ...] one nt16 code per byte */
+    uint8_t *dump_qual;
+    uint8_t *scratch;            /* large-family arenas when large_arena exceeds LDS: n_large * large_arena bytes */
+} bsdc_consensus;
+
+#define BSDC_MODE_CONVERT 1
+#define BSDC_MODE_EXTEND 2
+#define BSDC_MODE_VOTE 4
+#define BSDC_MODE_DUMP 8
+
+typedef struct bsdc_ctx bsdc_ctx;
+
+int32_t bsdc_abi_version(void);
+int32_t bsdc_ctx_create(int32_t device, const bsdc_params *params, bsdc_ctx **out);
+void bsdc_ctx_destroy(bsdc_ctx *ctx);
+const char *bsdc_last_error(const bsdc_ctx *ctx);
+
+/* Reference genome, host pointers: nt16 codes of the upper-cased FASTA, packed two per byte;
+ * contig_off[tid] = first nibble of contig tid (-1 = contig absent from the FASTA). */
+int32_t bsdc_load_reference(bsdc_ctx *ctx, const uint8_t *packed_nt16, int64_t n_nibbles,
+                            const int64_t *contig_off, const int64_t *contig_len, int32_t n_contig);
+
+/* The one launcher.  mode = OR of BSDC_MODE_*. */
+int32_t bsdc_run(bsdc_ctx *ctx, const bsdc_family_batch *batch, bsdc_consensus *out, int32_t mode,
+                 void *stream);
+
+/* Named entry points of the three reference stages (== bsdc_run with a fixed mode). */
+int32_t bsdc_convert(bsdc_ctx *ctx, const bsdc_family_batch *batch, bsdc_consensus *out, void *stream);
+int32_t bsdc_extend(bsdc_ctx *ctx, const bsdc_family_batch *batch, bsdc_consensus *out, void *stream);
+int32_t bsdc_duplex_call(bsdc_ctx *ctx, const bsdc_family_batch *batch, bsdc_consensus *out,
+                         int32_t with_tools, void *stream);
+
+/* Arena bytes one family needs (host-side helper shared with the batch builder). */
+int64_t bsdc_family_arena_bytes(int32_t n_rec, int64_t sum_len, int32_t max_len, int64_t complex_ops);
+
+/* The likelihood tables the vote kernel uses (host copies), for cross-checks. */
+int32_t bsdc_get_tables(const bsdc_ctx *ctx, int64_t *lr256, float *thresh94);
+/* Same tables for given error rates, without a context (no GPU needed). */
+void bsdc_model_tables(double error_rate_pre_umi, double error_rate_post_umi, int64_t *lr256, float *thresh94);
+
+#ifdef __cplusplus
+}
+#endif
+#endif

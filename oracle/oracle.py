@@ -1,0 +1,234 @@
+"""ctypes wrapper of the CPU restatement (oracle/bsdc_oracle.c).
+
+TEST INFRASTRUCTURE ONLY: imported by tests/, __graft_entry__.smoke() and bench.py's cpu_baseline
+leg, as the checker.  The product path (bsseqconsensusreads_amd) never imports this module.
+"""
+from __future__ import annotations
+
+import ctypes as C
+import os
+import subprocess
+from dataclasses import dataclass
+from typing import Dict, List, Optional
+
+import numpy as np
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+LIB = os.path.join(HERE, "build", "liboracle.so")
+
+NT16 = "=ACMGRSVTWYHKDBN"
+_NT16_ASCII = np.frombuffer(NT16.encode(), dtype=np.uint8)
+_ASCII_NT16 = np.full(256, 15, np.uint8)
+for _i, _c in enumerate(NT16):
+    _ASCII_NT16[ord(_c)] = _i
+    _ASCII_NT16[ord(_c.lower())] = _i
+_ASCII_NT16[ord("U")] = _ASCII_NT16[ord("u")] = 8
+
+
+class _Records(C.Structure):
+    _fields_ = [("n", C.c_int64)] + [(k, C.c_void_p) for k in (
+        "flag", "tid", "pos", "l_seq", "seq_off", "seq", "qual", "cig_off", "n_cig", "cigar", "mi_id",
+        "mi_strand", "name_id", "next_tid", "next_pos", "tlen", "mc_off", "mc_n", "mc_cigar")]
+
+
+class _Reference(C.Structure):
+    _fields_ = [("n_contig", C.c_int32), ("off", C.c_void_p), ("len", C.c_void_p), ("seq", C.c_void_p)]
+
+
+class _Params(C.Structure):
+    _fields_ = [("error_rate_pre_umi", C.c_double), ("error_rate_post_umi", C.c_double),
+                ("min_input_base_quality", C.c_int32), ("consensus_call_overlapping_bases", C.c_int32),
+                ("run_tools", C.c_int32), ("n_threads", C.c_int32)]
+
+
+_lib = None
+
+
+def build():
+    subprocess.run(["make", "-s", "-C", HERE], check=True)
+
+
+def load():
+    global _lib
+    if _lib is None:
+        if not os.path.exists(LIB):
+            build()
+        lib = C.CDLL(LIB)
+        lib.orc_run.restype = C.c_void_p
+        lib.orc_run.argtypes = [C.POINTER(_Records), C.POINTER(_Reference), C.POINTER(_Params)]
+        lib.orc_last_error.restype = C.c_char_p
+        lib.orc_free.argtypes = [C.c_void_p]
+        for fn in ("orc_n_records", "orc_total_bases", "orc_total_cigar"):
+            getattr(lib, fn).restype = C.c_int64
+            getattr(lib, fn).argtypes = [C.c_void_p, C.c_int]
+        lib.orc_get_records.argtypes = [C.c_void_p, C.c_int] + [C.c_void_p] * 9
+        lib.orc_n_families.restype = C.c_int64
+        lib.orc_n_families.argtypes = [C.c_void_p]
+        lib.orc_max_cons_len.restype = C.c_int32
+        lib.orc_max_cons_len.argtypes = [C.c_void_p]
+        lib.orc_get_consensus.argtypes = [C.c_void_p, C.c_int32] + [C.c_void_p] * 6
+        lib.orc_tables.argtypes = [C.c_double, C.c_double, C.c_void_p, C.c_void_p]
+        lib.orc_det_expf.restype = C.c_float
+        lib.orc_det_expf.argtypes = [C.c_float]
+        _lib = lib
+    return _lib
+
+
+class OracleError(RuntimeError):
+    pass
+
+
+@dataclass
+class OracleRecords:
+    src: np.ndarray
+    pos: np.ndarray
+    l_seq: np.ndarray
+    seq_off: np.ndarray
+    seq: np.ndarray   # nt16 codes
+    qual: np.ndarray
+    n_cig: np.ndarray
+    cig_off: np.ndarray
+    cigar: np.ndarray
+    rd: np.ndarray
+    la: np.ndarray
+
+    def record(self, k: int):
+        o, l = int(self.seq_off[k]), int(self.l_seq[k])
+        c, m = int(self.cig_off[k]), int(self.n_cig[k])
+        return dict(src=int(self.src[k]), pos=int(self.pos[k]), seq=self.seq[o:o + l], qual=self.qual[o:o + l],
+                    cigar=self.cigar[c:c + m], rd=int(self.rd[k]), la=int(self.la[k]))
+
+
+@dataclass
+class OracleResult:
+    tool1: OracleRecords
+    tool2: OracleRecords
+    fam_mi: np.ndarray
+    status: np.ndarray      # 1 = consensus pair emitted
+    cons_len: np.ndarray    # [F, 2]
+    cons_seq: np.ndarray    # [F, 2, stride] nt16 codes
+    cons_qual: np.ndarray   # [F, 2, stride]
+    n_reads: np.ndarray
+
+
+def _ptr(a):
+    return a.ctypes.data
+
+
+def run(raw, ref, pre=45.0, post=30.0, overlap=True, run_tools=True, threads=0) -> OracleResult:
+    """raw: bsseqconsensusreads_amd.records.RawRecords; ref: records.Reference."""
+    lib = load()
+    keep = []
+
+    def arr(x, dt):
+        a = np.ascontiguousarray(x, dtype=dt)
+        if a.size == 0:
+            a = np.zeros(1, dt)
+        keep.append(a)
+        return _ptr(a)
+
+    rr = _Records()
+    rr.n = raw.n
+    rr.flag = arr(raw.flag, np.uint16)
+    rr.tid = arr(raw.tid, np.int32)
+    rr.pos = arr(raw.pos, np.int32)
+    rr.l_seq = arr(raw.l_seq, np.int32)
+    rr.seq_off = arr(raw.seq_off, np.int64)
+    rr.seq = arr(_NT16_ASCII[raw.seq], np.uint8)
+    rr.qual = arr(raw.qual, np.uint8)
+    rr.cig_off = arr(raw.cig_off, np.int64)
+    rr.n_cig = arr(raw.n_cig, np.int32)
+    rr.cigar = arr(raw.cigar, np.uint32)
+    rr.mi_id = arr(raw.mi_id, np.int32)
+    rr.mi_strand = arr(raw.mi_strand, np.int8)
+    rr.name_id = arr(raw.name_id, np.int32)
+    rr.next_tid = arr(raw.next_tid, np.int32)
+    rr.next_pos = arr(raw.next_pos, np.int32)
+    rr.tlen = arr(raw.tlen, np.int32)
+    rr.mc_off = arr(raw.mc_off, np.int64)
+    rr.mc_n = arr(raw.mc_n, np.int32)
+    rr.mc_cigar = arr(raw.mc_cigar, np.uint32)
+
+    # reference letters: the FASTA's own when kept, else the nt16 letters
+    offs, lens, parts, o = [], [], [], 0
+    for t, name in enumerate(ref.names):
+        if ref.contig_off[t] < 0:
+            offs.append(-1)
+            lens.append(0)
+            continue
+        if name in ref.letters:
+            b = np.frombuffer(ref.letters[name], dtype=np.uint8)
+        else:
+            co, cl = int(ref.contig_off[t]), int(ref.contig_len[t])
+            lo, hi = co // 2, (co + cl + 1) // 2 + 1
+            pk = ref.packed[lo:hi]
+            codes = np.empty(2 * pk.shape[0], np.uint8)
+            codes[0::2] = pk >> 4
+            codes[1::2] = pk & 0xF
+            codes = codes[co - 2 * lo: co - 2 * lo + cl]
+            b = _NT16_ASCII[codes]
+        offs.append(o)
+        lens.append(len(b))
+        parts.append(b)
+        o += len(b)
+    rf = _Reference()
+    rf.n_contig = len(ref.names)
+    rf.off = arr(np.asarray(offs, np.int64), np.int64)
+    rf.len = arr(np.asarray(lens, np.int64), np.int64)
+    rf.seq = arr(np.concatenate(parts) if parts else np.zeros(1, np.uint8), np.uint8)
+
+    p = _Params(pre, post, 0, int(overlap), int(run_tools), int(threads))
+    h = lib.orc_run(C.byref(rr), C.byref(rf), C.byref(p))
+    if not h:
+        raise OracleError(lib.orc_last_error().decode())
+    try:
+        outs = []
+        for which in (1, 2):
+            n = lib.orc_n_records(h, which)
+            nb = lib.orc_total_bases(h, which)
+            nc = lib.orc_total_cigar(h, which)
+            src = np.zeros(max(n, 1), np.int64)
+            pos = np.zeros(max(n, 1), np.int32)
+            l_seq = np.zeros(max(n, 1), np.int32)
+            seq = np.zeros(max(nb, 1), np.uint8)
+            qual = np.zeros(max(nb, 1), np.uint8)
+            n_cig = np.zeros(max(n, 1), np.int32)
+            cig = np.zeros(max(nc, 1), np.uint32)
+            rd = np.zeros(max(n, 1), np.int32)
+            la = np.zeros(max(n, 1), np.int32)
+            lib.orc_get_records(h, which, _ptr(src), _ptr(pos), _ptr(l_seq), _ptr(seq), _ptr(qual), _ptr(n_cig),
+                                _ptr(cig), _ptr(rd), _ptr(la))
+            so = np.zeros(n, np.int64)
+            if n:
+                so[1:] = np.cumsum(l_seq[:n])[:-1]
+            co = np.zeros(n, np.int64)
+            if n:
+                co[1:] = np.cumsum(n_cig[:n])[:-1]
+            outs.append(OracleRecords(src[:n], pos[:n], l_seq[:n], so, _ASCII_NT16[seq[:nb]], qual[:nb], n_cig[:n],
+                                      co, cig[:nc], rd[:n], la[:n]))
+        F = lib.orc_n_families(h)
+        stride = max(int(lib.orc_max_cons_len(h)), 1)
+        mi = np.zeros(max(F, 1), np.int32)
+        st = np.zeros(max(F, 1), np.int32)
+        ln = np.zeros(max(2 * F, 1), np.int32)
+        bs = np.zeros(max(2 * F * stride, 1), np.uint8)
+        qs = np.zeros(max(2 * F * stride, 1), np.uint8)
+        nr = np.zeros(max(F, 1), np.int32)
+        lib.orc_get_consensus(h, stride, _ptr(mi), _ptr(st), _ptr(ln), _ptr(bs), _ptr(qs), _ptr(nr))
+        return OracleResult(outs[0], outs[1], mi[:F], st[:F], ln[:2 * F].reshape(F, 2),
+                            _ASCII_NT16[bs[:2 * F * stride]].reshape(F, 2, stride) if F else np.zeros((0, 2, stride), np.uint8),
+                            qs[:2 * F * stride].reshape(F, 2, stride), nr[:F])
+    finally:
+        lib.orc_free(h)
+
+
+def tables(pre=45.0, post=30.0):
+    lib = load()
+    lr = np.zeros(256, np.int64)
+    thr = np.zeros(94, np.float32)
+    lib.orc_tables(pre, post, _ptr(lr), _ptr(thr))
+    return lr, thr
+
+
+def det_expf(x: float) -> float:
+    return float(load().orc_det_expf(x))

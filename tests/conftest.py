@@ -1,0 +1,21 @@
+import os
+import sys
+
+import pytest
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+if ROOT not in sys.path:
+    sys.path.insert(0, ROOT)
+
+
+def pytest_configure(config):
+    config.addinivalue_line("markers", "gpu: needs an MI355X (runs the HIP path through the C-ABI)")
+
+
+@pytest.fixture(scope="session")
+def engine():
+    from bsseqconsensusreads_amd.device import Engine
+
+    e = Engine(0)
+    yield e
+    e.close()

@@ -1,0 +1,51 @@
+"""Shared test helpers: golden fixtures and record comparisons."""
+import gzip
+import json
+import os
+
+import numpy as np
+
+from bsseqconsensusreads_amd import records as R
+
+GOLDEN = os.path.join(os.path.dirname(os.path.abspath(__file__)), "golden")
+
+
+def load_golden(name):
+    with gzip.open(os.path.join(GOLDEN, name), "rt") as fh:
+        return json.load(fh)
+
+
+def golden_inputs(g):
+    raw = R.records_from_dicts(g["input"])
+    names = [c["name"] for c in g["header"]["references"]]
+    ref = R.Reference.from_contigs(names, g["contigs"], header_lengths=[c["length"] for c in g["header"]["references"]])
+    return raw, ref
+
+
+def compare_records(golden_out, produced, raw, inputs, what=""):
+    """golden_out: list of fixture dicts (reference tool output, in order);
+    produced: an OracleRecords / OutRecords with .record(k); inputs: fixture input dicts."""
+    n = len(produced.src)
+    assert n == len(golden_out), "%s: %d records vs golden %d" % (what, n, len(golden_out))
+    for k in range(n):
+        g = golden_out[k]
+        p = produced.record(k)
+        src = inputs[p["src"]]
+        ctx = "%s record %d (%s flag %d)" % (what, k, g["name"], g["flag"])
+        assert src["name"] == g["name"] and src["flag"] == g["flag"], ctx + ": wrong record/order"
+        assert p["pos"] == g["pos"], ctx + ": pos %d vs %d" % (p["pos"], g["pos"])
+        gc = [(l << 4) | op for op, l in g["cigar"]]
+        assert [int(x) for x in p["cigar"]] == gc, ctx + ": cigar %s vs %s" % (
+            R.cigar_string(p["cigar"]), R.cigar_string(gc))
+        gs = R.encode_seq(g["seq"]) if g["seq"] else np.zeros(0, np.uint8)
+        assert np.array_equal(p["seq"], gs), ctx + ": seq\n%s\n%s" % (R.decode_seq(p["seq"]), g["seq"])
+        gq = np.frombuffer(g["qual"].encode(), np.uint8) - 33 if g["qual"] is not None else None
+        assert gq is not None and np.array_equal(p["qual"], gq), ctx + ": qual"
+        gt = {t[0]: t[2] for t in g["tags"]}
+        st = {t[0]: t[2] for t in src["tags"]}
+        for t in ("RD", "LA"):
+            exp = gt.get(t, None)
+            got = p[t.lower()] if p[t.lower()] >= 0 else st.get(t, None)
+            assert exp == got, ctx + ": tag %s %r vs %r" % (t, got, exp)
+        # every other tag passes through
+        assert {k: v for k, v in gt.items() if k not in ("RD", "LA")} == {k: v for k, v in st.items() if k not in ("RD", "LA")}, ctx

@@ -1,0 +1,66 @@
+"""CPU checks of the C-ABI library: it loads without a GPU, exports what include/bsdc.h declares,
+and its host-side model tables / arena sizes agree with the oracle and the batch builder."""
+import re
+import os
+
+import numpy as np
+
+from bsseqconsensusreads_amd import _lib, batch
+from oracle import oracle
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+
+
+def test_library_exports_every_declared_symbol():
+    lib = _lib.load()
+    hdr = open(os.path.join(ROOT, "include", "bsdc.h")).read()
+    declared = set(re.findall(r"\b(bsdc_[a-z_0-9]+)\s*\(", hdr))
+    assert declared == set(_lib.EXPORTS), declared ^ set(_lib.EXPORTS)
+    for name in declared:
+        assert hasattr(lib, name), name
+    assert lib.bsdc_abi_version() == _lib.BSDC_ABI_VERSION
+
+
+def test_model_tables_bit_identical_to_oracle():
+    lib = _lib.load()
+    for pre, post in ((45.0, 30.0), (40.0, 25.0), (60.0, 40.0)):
+        lr = np.zeros(256, np.int64)
+        thr = np.zeros(94, np.float32)
+        lib.bsdc_model_tables(pre, post, lr.ctypes.data, thr.ctypes.data)
+        olr, othr = oracle.tables(pre, post)
+        assert np.array_equal(lr, olr)
+        assert np.array_equal(thr.view(np.uint32), othr.view(np.uint32))
+
+
+def test_model_tables_follow_fgbio_formula():
+    """lr[q] = ln(1-a) - ln(a/3), a = e_post + e(q) - 4/3 e_post e(q) (fixed point 2^40);
+    threshold k: S <= thr[k] <=> floor(-10 log10 p' + 0.001) >= k."""
+    lr, thr = oracle.tables(45.0, 30.0)
+    ep, epre = 10 ** -3.0, 10 ** -4.5
+    for q in (0, 2, 10, 20, 30, 37, 40, 60, 93):
+        e = 10 ** (-q / 10)
+        a = ep + e - 4 / 3 * ep * e
+        assert abs(lr[q] / 2.0 ** 40 - (np.log1p(-a) - np.log(a / 3))) < 1e-9
+    # worked value: one Q37 read -> S = 3 e^-lr[37] -> Q29
+    S = 3 * np.exp(-lr[37] / 2.0 ** 40)
+    Q = max(k for k in range(94) if k == 0 or S <= thr[k])
+    p = S / (1 + S)
+    pp = epre + p - 4 / 3 * epre * p
+    assert Q == 29 == int(np.floor(-10 * np.log10(pp) + 0.001))
+
+
+def test_det_expf_accuracy():
+    for x in np.linspace(-80, 0, 2001).astype(np.float32):
+        v = oracle.det_expf(float(x))
+        assert abs(v / np.exp(np.float64(x)) - 1) < 1e-6, x
+
+
+def test_arena_formula_matches_library():
+    lib = _lib.load()
+    rng = np.random.default_rng(0)
+    for _ in range(200):
+        n = int(rng.integers(1, 600))
+        sl = int(rng.integers(0, 200 * n))
+        ml = int(rng.integers(0, 400))
+        co = int(rng.integers(0, 3)) * int(rng.integers(0, 50))
+        assert lib.bsdc_family_arena_bytes(n, sl, ml, co) == int(batch.arena_bytes(n, sl, ml, co))

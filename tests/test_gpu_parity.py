@@ -1,0 +1,151 @@
+"""HIP path (through the C-ABI) against the reference tools' golden outputs and the CPU restatement.
+
+Bar: bit-exact everywhere -- tool 1 / tool 2 records (seq, qual, pos, cigar, tags) against the
+reference's own outputs, consensus bases AND qualities against oracle/ (the vote's fixed-point
+sums and shared phred thresholds make the qualities exact too; north_star allows +-1).
+"""
+import numpy as np
+import pytest
+
+from bsseqconsensusreads_amd import batch, pipeline, synth
+from bsseqconsensusreads_amd import records as R
+from helpers import compare_records, golden_inputs, load_golden
+from oracle import oracle
+
+pytestmark = pytest.mark.gpu
+
+
+def assert_consensus_equal(cons, ref, what=""):
+    assert np.array_equal(cons.fam_mi, ref.fam_mi), what + ": family order"
+    st = (cons.status & 1).astype(np.int32)
+    bad = np.nonzero(st != ref.status)[0]
+    assert bad.size == 0, "%s: status differs at families %s" % (what, bad[:10])
+    assert np.array_equal(cons.length, ref.cons_len), what + ": lengths"
+    F = len(ref.status)
+    for f in range(F):
+        for e in range(2):
+            n = int(ref.cons_len[f, e])
+            if not np.array_equal(cons.seq[f, e, :n], ref.cons_seq[f, e, :n]):
+                d = np.nonzero(cons.seq[f, e, :n] != ref.cons_seq[f, e, :n])[0]
+                raise AssertionError("%s: family %d end %d bases differ at %s: gpu %s oracle %s" % (
+                    what, f, e, d[:8], cons.seq[f, e, d[:8]], ref.cons_seq[f, e, d[:8]]))
+            if not np.array_equal(cons.qual[f, e, :n], ref.cons_qual[f, e, :n]):
+                d = np.nonzero(cons.qual[f, e, :n] != ref.cons_qual[f, e, :n])[0]
+                raise AssertionError("%s: family %d end %d quals differ at %s: gpu %s oracle %s" % (
+                    what, f, e, d[:8], cons.qual[f, e, d[:8]], ref.cons_qual[f, e, d[:8]]))
+
+
+def test_tool1_fuzz_matches_reference(engine):
+    g = load_golden("tool1_fuzz.json.gz")
+    raw, ref = golden_inputs(g)
+    engine.load_reference(ref)
+    out = pipeline.run_tool1(engine, raw)
+    compare_records(g["tool1"], out, raw, g["input"], "gpu tool1 fuzz")
+
+
+def test_tools12_families_match_reference(engine):
+    g = load_golden("tool12_families.json.gz")
+    raw, ref = golden_inputs(g)
+    engine.load_reference(ref)
+    compare_records(g["tool1"], pipeline.run_tool1(engine, raw), raw, g["input"], "gpu tool1 families")
+    cons, t2 = pipeline.run_step5(engine, raw, dump=True)
+    compare_records(g["tool2"], t2, raw, g["input"], "gpu fused tool2 dump")
+    assert_consensus_equal(cons, oracle.run(raw, ref), "golden families consensus")
+
+
+def test_tool2_alone_on_reference_tool1_output(engine):
+    g = load_golden("tool12_families.json.gz")
+    raw1 = R.records_from_dicts(g["tool1"])
+    out = pipeline.run_tool2(engine, raw1)
+    compare_records(g["tool2"], out, raw1, g["tool1"], "gpu tool2 alone")
+
+
+def test_missing_mi_raises(engine):
+    g = load_golden("tool2_missing_mi.json.gz")
+    raw, ref = golden_inputs(g)
+    with pytest.raises(ValueError, match="does not have MI tag"):
+        pipeline.run_step5(engine, raw)
+
+
+@pytest.mark.parametrize("cfg", ["C0", "C1", "C2", "C3", "C4"])
+def test_synthetic_configs_vs_oracle(engine, cfg):
+    n = {"C0": 3000, "C1": 1500, "C2": 3000, "C3": 150, "C4": 1200}[cfg]
+    s = synth.generate(cfg, n, seed=11, device="cpu", genome_len=400_000)
+    engine.load_reference(s.ref)
+    cons, t2 = pipeline.run_step5(engine, s.raw, dump=True)
+    ref = oracle.run(s.raw, s.ref)
+    assert_consensus_equal(cons, ref, cfg)
+    # the fused kernel's tool-2 state equals the restatement's tool-2 records
+    assert np.array_equal(t2.src, ref.tool2.src)
+    assert np.array_equal(t2.pos, ref.tool2.pos)
+    assert np.array_equal(t2.seq, ref.tool2.seq)
+    assert np.array_equal(t2.qual, ref.tool2.qual)
+    assert np.array_equal(t2.cigar, ref.tool2.cigar)
+
+
+def test_messy_records_vs_oracle(engine):
+    """soft/hard clips, I/D ops (complex cigars, alignment filter), N runs, trailing Ns."""
+    s = synth.generate("C2", 800, seed=5, device="cpu", genome_len=200_000)
+    raw = synth.messify(s.raw, frac=0.25, seed=9)
+    engine.load_reference(s.ref)
+    cons, _ = pipeline.run_step5(engine, raw)
+    assert_consensus_equal(cons, oracle.run(raw, s.ref), "messy")
+
+
+def test_read_through_trim_vs_oracle(engine):
+    """short inserts: reads run past the (stale) mate end, fgbio trims them."""
+    s = synth.generate("C1", 600, seed=6, device="cpu", genome_len=200_000, frag=(140, 40, 60))
+    fb = batch.build_family_batch(s.raw, "full")
+    assert (fb.rec_link & batch.LINK_RT).any()
+    engine.load_reference(s.ref)
+    cons, _ = pipeline.run_step5(engine, s.raw)
+    assert_consensus_equal(cons, oracle.run(s.raw, s.ref), "read-through")
+
+
+@pytest.mark.parametrize("where", ["lds", "global"])
+def test_large_family_kernel(engine, where, monkeypatch):
+    """every family through the workgroup-per-family kernel (arena in LDS, or in HBM scratch)."""
+    s = synth.generate("C2", 700, seed=12, device="cpu", genome_len=200_000)
+    raw = synth.messify(s.raw, frac=0.1, seed=2)
+    real = batch.build_family_batch
+
+    def forced(r, mode="full", small_cap=0):
+        fb = real(r, mode, small_cap=0)
+        if where == "global":
+            fb.large_arena = max(fb.large_arena, 70000)
+        return fb
+
+    monkeypatch.setattr(pipeline, "build_family_batch", forced)
+    engine.load_reference(s.ref)
+    cons, _ = pipeline.run_step5(engine, raw)
+    assert_consensus_equal(cons, oracle.run(raw, s.ref), "large-" + where)
+
+
+def test_vote_only_on_tool2_output(engine):
+    """callduplex alone (main.snake.py:155-164) on the restatement's own tool-2 records."""
+    s = synth.generate("C0", 1000, seed=13, device="cpu", genome_len=200_000)
+    ref = oracle.run(s.raw, s.ref)
+    t2 = ref.tool2
+    b = R._Builder()
+    for k in range(len(t2.src)):
+        r = t2.record(k)
+        src = r["src"]
+        tags = [("MI", "Z", "%d/%s" % (s.raw.mi_id[src], "A" if s.raw.mi_strand[src] == 0 else "B")),
+                ("MC", "Z", "%dM" % s.raw.l_seq[src])]
+        b.add(("t%d" % s.raw.name_id[src]).encode(), int(s.raw.flag[src]), 0, r["pos"], 60, [int(x) for x in r["cigar"]],
+              r["seq"], r["qual"], 0, int(s.raw.next_pos[src]), int(s.raw.tlen[src]), R.encode_aux(tags), tags)
+    raw2 = b.finish()
+    cons = pipeline.run_duplex(engine, raw2)
+    ref2 = oracle.run(raw2, s.ref, run_tools=False)
+    assert_consensus_equal(cons, ref2, "vote-only")
+
+
+def test_empty_and_repeatable(engine):
+    s = synth.generate("C2", 300, seed=14, device="cpu", genome_len=100_000)
+    engine.load_reference(s.ref)
+    a, _ = pipeline.run_step5(engine, s.raw)
+    b, _ = pipeline.run_step5(engine, s.raw)
+    assert np.array_equal(a.seq, b.seq) and np.array_equal(a.qual, b.qual)
+    empty = R.records_from_dicts([])
+    c, _ = pipeline.run_step5(engine, empty)
+    assert c.status.shape[0] == 0
