@@ -7,8 +7,9 @@ import os
 HERE = os.path.dirname(os.path.abspath(__file__))
 LIB_PATH = os.path.join(HERE, "libbsdc.so")
 
-BSDC_ABI_VERSION = 1
+BSDC_ABI_VERSION = 2
 MODE_CONVERT, MODE_EXTEND, MODE_VOTE, MODE_DUMP = 1, 2, 4, 8
+MODE_SKIP_SMALL, MODE_SKIP_LARGE = 16, 32
 
 
 class Params(C.Structure):
@@ -19,14 +20,12 @@ class Params(C.Structure):
 
 class FamilyBatchC(C.Structure):
     _fields_ = [("n_rec", C.c_int64), ("n_fam", C.c_int64),
-                ("fam_off", C.c_void_p), ("rec_off", C.c_void_p), ("rec_pos", C.c_void_p),
-                ("rec_lenflag", C.c_void_p), ("rec_tid", C.c_void_p), ("rec_link", C.c_void_p),
+                ("fam_off", C.c_void_p), ("rec", C.c_void_p), ("rec_win", C.c_void_p),
                 ("cig_off", C.c_void_p), ("cig_info", C.c_void_p), ("cigar", C.c_void_p),
                 ("rt", C.c_void_p), ("seq", C.c_void_p), ("qual", C.c_void_p),
-                ("small_fams", C.c_void_p), ("n_small", C.c_int64),
-                ("large_fams", C.c_void_p), ("n_large", C.c_int64),
-                ("max_len", C.c_int32), ("small_arena", C.c_int32), ("large_arena", C.c_int32),
-                ("reserved", C.c_int32)]
+                ("small_fams", C.c_void_p), ("n_small", C.c_int64 * 4), ("small_arena", C.c_int32 * 4),
+                ("large_fams", C.c_void_p), ("n_large", C.c_int64), ("large_arena", C.c_int32),
+                ("max_len", C.c_int32)]
 
 
 class ConsensusC(C.Structure):
@@ -38,7 +37,8 @@ class ConsensusC(C.Structure):
 
 EXPORTS = ("bsdc_abi_version", "bsdc_ctx_create", "bsdc_ctx_destroy", "bsdc_last_error",
            "bsdc_load_reference", "bsdc_run", "bsdc_convert", "bsdc_extend", "bsdc_duplex_call",
-           "bsdc_family_arena_bytes", "bsdc_get_tables", "bsdc_model_tables")
+           "bsdc_family_arena_bytes", "bsdc_small_arena_bytes", "bsdc_get_tables", "bsdc_model_tables",
+           "bsdc_agree_tables")
 
 _lib = None
 
@@ -69,10 +69,14 @@ def load(path: str = LIB_PATH):
     lib.bsdc_duplex_call.restype = C.c_int32
     lib.bsdc_family_arena_bytes.argtypes = [C.c_int32, C.c_int64, C.c_int32, C.c_int64]
     lib.bsdc_family_arena_bytes.restype = C.c_int64
+    lib.bsdc_small_arena_bytes.argtypes = [C.c_int32, C.c_int64, C.c_int32, C.c_int64, C.c_int32]
+    lib.bsdc_small_arena_bytes.restype = C.c_int64
     lib.bsdc_get_tables.argtypes = [C.c_void_p, C.c_void_p, C.c_void_p]
     lib.bsdc_get_tables.restype = C.c_int32
     lib.bsdc_model_tables.argtypes = [C.c_double, C.c_double, C.c_void_p, C.c_void_p]
     lib.bsdc_model_tables.restype = None
+    lib.bsdc_agree_tables.argtypes = [C.c_double, C.c_double, C.c_void_p, C.c_void_p]
+    lib.bsdc_agree_tables.restype = None
     if lib.bsdc_abi_version() != BSDC_ABI_VERSION:
         raise RuntimeError("libbsdc ABI %d != %d" % (lib.bsdc_abi_version(), BSDC_ABI_VERSION))
     if path == LIB_PATH:

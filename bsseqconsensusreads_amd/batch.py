@@ -37,9 +37,10 @@ LINK_USABLE = 1 << 26
 
 MODE_CONVERT, MODE_EXTEND, MODE_VOTE, MODE_DUMP = 1, 2, 4, 8
 
-# families whose arena fits this many bytes run one per wavefront with the arena in LDS
-SMALL_ARENA_CAP = 8192
-LDS_TABLES = 2048 + 384
+# small families run one per wavefront with their arena in LDS, in buckets of these arena sizes
+SMALL_BUCKETS = (4096, 6144, 8192, 12288)
+SMALL_ARENA_CAP = 12288
+LDS_TABLES = 1024 + 384 + 2048 + 192
 LARGE_LDS_CAP = 64 * 1024 - LDS_TABLES
 
 
@@ -47,14 +48,35 @@ def round16(x):
     return (np.asarray(x, dtype=np.int64) + 15) & ~np.int64(15)
 
 
-def arena_bytes(n, sum_len, max_len, complex_ops):
+def ref_chunks(max_len):
+    """16-B chunks that cover one converted record's packed reference window (mirror of the kernel)."""
+    return (15 + (int(max_len) + 4) // 2 + 15) // 16
+
+
+def small_chunks(img, nconv, max_len):
+    img = np.asarray(img, dtype=np.int64)
+    return img // 16 + img // 32 + np.asarray(nconv, dtype=np.int64) * ref_chunks(max_len)
+
+
+def small_arena_bytes(n, img, nconv, complex_ops, max_len):
+    """Mirror of SmallLayout (csrc/bsdc_kernels.hip) / bsdc_small_arena_bytes."""
+    n = np.asarray(n, dtype=np.int64)
+    ws = 32 * ref_chunks(max_len)
+    cops = np.asarray(complex_ops, dtype=np.int64)
+    ow = int(round16(int(max_len) + 2))
+    total = 2 * np.asarray(img, dtype=np.int64) + np.asarray(nconv, dtype=np.int64) * ws + 256 \
+        + round16(16 * n) + 160 + 8 * ow + 256
+    return total + np.where(cops > 0, round16(4 * (cops + 4 * n)), 0)
+
+
+def large_arena_bytes(n, slot_bytes, max_len, complex_ops):
     """Mirror of ArenaLayout (csrc/bsdc_kernels.hip) / bsdc_family_arena_bytes."""
     n = np.asarray(n, dtype=np.int64)
     ssw = round16(np.asarray(max_len, dtype=np.int64) + 2)
     total = round16(n * 48) + round16(n * 8) + 8 * ssw
     cops = np.asarray(complex_ops, dtype=np.int64)
     total = total + np.where(cops > 0, round16(4 * (cops + 4 * n)), 0)
-    total = total + round16(2 * np.asarray(sum_len, dtype=np.int64) + 4 * n)
+    total = total + round16(np.asarray(slot_bytes, dtype=np.int64))
     return total
 
 
@@ -64,28 +86,30 @@ class MissingMITag(ValueError):
 
 @dataclass
 class FamilyBatch:
-    # ---- device arrays ----
+    # ---- device arrays (include/bsdc.h bsdc_family_batch) ----
     fam_off: np.ndarray      # u32 [F+1]
-    rec_off: np.ndarray      # u32 [R]
+    rec_off: np.ndarray      # u32 [R] slot start (nibble index into seq == byte index into qual)
     rec_pos: np.ndarray      # i32
     rec_lenflag: np.ndarray  # u32
-    rec_tid: np.ndarray      # i32
+    rec_tid: np.ndarray      # i32 (host only)
     rec_link: np.ndarray     # u32
+    rec_win: np.ndarray      # u32 [R, 2] converted records: reference window start nibble, valid nibbles
     cig_off: np.ndarray      # u32
     cig_info: np.ndarray     # u32
     cigar: np.ndarray        # u32
     rt: np.ndarray           # i32 [4R]
-    seq: np.ndarray          # u8 packed nt16
-    qual: np.ndarray         # u8
-    small_fams: np.ndarray   # u32
+    seq: np.ndarray          # u8 packed nt16, slot layout
+    qual: np.ndarray         # u8, slot layout
+    small_buckets: List[np.ndarray]  # 4 lists of family ids (u32), one per LDS arena size
+    small_arenas: List[int]
     large_fams: np.ndarray   # u32
     max_len: int
-    small_arena: int
     large_arena: int
     # ---- host bookkeeping ----
     src: np.ndarray          # i64 [R] input record index
     fam_mi: np.ndarray       # i32 [F] MI id of each family
     n_bases: int
+    n_slots: int
 
     @property
     def n_rec(self) -> int:
@@ -99,10 +123,18 @@ class FamilyBatch:
     def stride(self) -> int:
         return int(round16(self.max_len + 2))
 
+    @property
+    def small_fams(self) -> np.ndarray:
+        return np.concatenate(self.small_buckets).astype(np.uint32)
+
     def device_arrays(self):
-        return {k: getattr(self, k) for k in (
-            "fam_off", "rec_off", "rec_pos", "rec_lenflag", "rec_tid", "rec_link", "cig_off",
-            "cig_info", "cigar", "rt", "seq", "qual", "small_fams", "large_fams")}
+        rec = np.stack([self.rec_off, self.rec_pos.view(np.uint32), self.rec_lenflag, self.rec_link], axis=1)
+        d = {"fam_off": self.fam_off, "rec": np.ascontiguousarray(rec, dtype=np.uint32),
+             "rec_win": np.ascontiguousarray(self.rec_win, dtype=np.uint32)}
+        for k in ("cig_off", "cig_info", "cigar", "rt", "seq", "qual", "large_fams"):
+            d[k] = getattr(self, k)
+        d["small_fams"] = self.small_fams
+        return d
 
 
 def _per_record_ops(raw: R.RawRecords):
@@ -153,7 +185,8 @@ def _softclip_strip(raw: R.RawRecords):
     return sL, L, kfirst, kn
 
 
-def build_family_batch(raw: R.RawRecords, mode: str = "full", small_cap: int = SMALL_ARENA_CAP) -> FamilyBatch:
+def build_family_batch(raw: R.RawRecords, mode: str = "full", ref: Optional[R.Reference] = None,
+                       small_cap: int = SMALL_ARENA_CAP) -> FamilyBatch:
     """mode: 'full' (raw step-5 input: tools 1+2 then the vote), 'convert' (tool 1 alone: one
     family per converted record), 'extend' (tool-1 output: tool 2 alone), 'vote' (tool-2 output)."""
     n = raw.n
@@ -292,18 +325,37 @@ def build_family_batch(raw: R.RawRecords, mode: str = "full", small_cap: int = S
 
     # ---- per batch record ----
     Lb = L[order]
-    if nr and Lb.max() > 0xFFFF:
-        raise ValueError("record longer than 65535 bases")
-    rec_off = np.zeros(nr, np.int64)
+    if nr and Lb.max() > 0xFFFF - 8:
+        raise ValueError("record longer than 65527 bases")
+    # HBM layout: record slots of cap4 = round4(L+2) (prepend / append room, dword aligned), the
+    # record's bases at slot+1; every family image starts on a 32-nibble boundary
+    cap4 = (Lb + 2 + 3) & ~np.int64(3)
+    span = np.bincount(fam_of, weights=cap4, minlength=nf)[:nf].astype(np.int64) if nr else np.zeros(nf, np.int64)
+    img = (span + 31) & ~np.int64(31)
+    fam_base = np.zeros(nf + 1, np.int64)
+    fam_base[1:] = np.cumsum(img)
+    within = np.zeros(nr, np.int64)
     if nr:
-        rec_off[1:] = np.cumsum(Lb)[:-1]
-    total = int(Lb.sum()) if nr else 0
-    if total >= 1 << 32:
+        cs = np.cumsum(cap4) - cap4
+        within = cs - cs[fam_off[fam_of]]
+    rec_off = fam_base[fam_of] + within if nr else np.zeros(0, np.int64)
+    n_slots = int(fam_base[-1]) + 64
+    if n_slots >= 1 << 32:
         raise ValueError("batch too large for 32-bit offsets; split it")
-    # gather stripped bases / quals
-    srcpos = np.repeat(raw.seq_off[order] + sL[order] - rec_off, Lb) + np.arange(total, dtype=np.int64)
-    codes = raw.seq[srcpos] if total else np.zeros(0, np.uint8)
-    qual = raw.qual[srcpos] if total else np.zeros(0, np.uint8)
+    total = int(Lb.sum()) if nr else 0
+    codes = np.zeros(n_slots, np.uint8)
+    qual = np.zeros(n_slots, np.uint8)
+    shift = raw.seq_off[order] + sL[order]
+    step = 1 << 18
+    for c0 in range(0, nr, step):
+        c1 = min(nr, c0 + step)
+        ln = Lb[c0:c1]
+        m = int(ln.sum())
+        rel = np.arange(m, dtype=np.int64) - np.repeat(np.cumsum(ln) - ln, ln)
+        srcpos = np.repeat(shift[c0:c1], ln) + rel
+        dst = np.repeat(rec_off[c0:c1] + 1, ln) + rel
+        codes[dst] = raw.seq[srcpos]
+        qual[dst] = raw.qual[srcpos]
     seq = R.pack_nibbles(codes)
 
     # stripped cigars, complex records
@@ -334,10 +386,12 @@ def build_family_batch(raw: R.RawRecords, mode: str = "full", small_cap: int = S
 
     # link word
     fo = f[order]
+    tid = raw.tid[order].astype(np.int64)
     strand = raw.mi_strand[order].astype(np.int64)
     usable = ((fo & 1) != 0) & ((fo & 0x900) == 0) & (strand >= 0)
     link = np.full(nr, LINK_MATE_NONE, np.int64)
-    # template mates: first usable R1 of a name -> first usable R2 of the name, within a family
+    # template mates: first usable R1 of a name -> first usable R2 of the name, within a family;
+    # only mates that can overlap (both mapped, one contig) are linked
     name = raw.name_id[order].astype(np.int64)
     key = fam_of * (int(name.max()) + 1 if nr else 1) + name
     r1 = usable & ((fo & 0x40) != 0)
@@ -350,7 +404,8 @@ def build_family_batch(raw: R.RawRecords, mode: str = "full", small_cap: int = S
         _, ia, ib = np.intersect1d(u1, u2, assume_unique=True, return_indices=True)
         a = i1[f1[ia]]
         b = i2[f2[ib]]
-        link[a] = local[b]
+        ok = (tid[a] == tid[b]) & ((fo[a] & 4) == 0) & ((fo[b] & 4) == 0)
+        link[a[ok]] = local[b[ok]]
     link |= np.where(strand == 0, LINK_AB, 0) | np.where(strand == 1, LINK_BA, 0)
     link |= np.where(complex_, LINK_COMPLEX, 0)
     link |= np.where(conv[order], LINK_CONVERT, 0)
@@ -359,6 +414,23 @@ def build_family_batch(raw: R.RawRecords, mode: str = "full", small_cap: int = S
     link |= np.where(ext_right[order] | ext_left[order], partner_local[order] << LINK_PARTNER_SHIFT, 0)
     link |= np.where(rd_in[order], LINK_RD_IN, 0)
     link |= np.where(usable, LINK_USABLE, 0)
+
+    # tool-1 reference window of converted records: nibbles [max(pos-1,0), +L+2) of the contig,
+    # N past the contig end or for a contig the FASTA lacks (tools/1.convert_AG_to_CT.py:103-117)
+    rec_win = np.zeros((nr, 2), np.int64)
+    convb = conv[order]
+    if convb.any():
+        if ref is None:
+            raise ValueError("converting records needs the reference")
+        np0 = np.maximum(raw.pos[order].astype(np.int64) - 1, 0)
+        okt = (tid >= 0) & (tid < len(ref.names))
+        coff = np.where(okt, ref.contig_off[np.clip(tid, 0, max(len(ref.names) - 1, 0))], -1) if len(ref.names) else np.full(nr, -1)
+        clen = np.where(okt, ref.contig_len[np.clip(tid, 0, max(len(ref.names) - 1, 0))], 0) if len(ref.names) else np.zeros(nr, np.int64)
+        present = coff >= 0
+        rec_win[:, 0] = np.where(convb & present, coff + np0, 0)
+        rec_win[:, 1] = np.where(convb & present, np.clip(clen - np0, 0, Lb + 2), 0)
+        if rec_win[:, 0].max() >= 1 << 32:
+            raise ValueError("reference too large for 32-bit nibble offsets")
 
     # read-through candidates (stale mate fields, MC tag)
     rt = np.zeros((nr, 4), np.int64)
@@ -400,27 +472,42 @@ def build_family_batch(raw: R.RawRecords, mode: str = "full", small_cap: int = S
         rt[:, 3] = mate_ue
         rt[~cand] = 0
 
-    # ---- family classes ----
-    sum_len = np.bincount(fam_of, weights=Lb, minlength=nf)[:nf].astype(np.int64) if nr else np.zeros(nf, np.int64)
+    # ---- family classes: small (one wavefront, LDS) by arena bucket, or large (one workgroup) ----
+    max_len = int(Lb.max()) if nr else 0
     max_len_f = np.zeros(nf, np.int64)
     if nr:
         np.maximum.at(max_len_f, fam_of, Lb)
     cops = np.bincount(fam_of, weights=cnt_c, minlength=nf)[:nf].astype(np.int64) if nr else np.zeros(nf, np.int64)
-    need = arena_bytes(fam_sizes, sum_len, max_len_f, cops)
-    small = need <= small_cap
-    small_fams = np.nonzero(small)[0].astype(np.uint32)
+    nconv = np.bincount(fam_of, weights=convb.astype(np.int64), minlength=nf)[:nf].astype(np.int64) if nr else np.zeros(nf, np.int64)
+    need_s = small_arena_bytes(fam_sizes, img, nconv, cops, max_len)
+    chunks = small_chunks(img, nconv, max_len)
+    need_l = large_arena_bytes(fam_sizes, 2 * span, max_len_f, cops)
+    small = (fam_sizes <= 64) & (chunks <= 256) & (need_s <= small_cap)
+    buckets, arenas = [], []
+    lo = -1
+    for cap in SMALL_BUCKETS:
+        if cap > small_cap:
+            cap = small_cap
+        sel = small & (need_s > lo) & (need_s <= cap)
+        buckets.append(np.nonzero(sel)[0].astype(np.uint32))
+        arenas.append(int(cap))
+        lo = cap
+        if cap == small_cap:
+            break
+    while len(buckets) < 4:
+        buckets.append(np.zeros(0, np.uint32))
+        arenas.append(16)
     large_fams = np.nonzero(~small)[0].astype(np.uint32)
-    small_arena = int(round16(need[small].max())) if small.any() else 16
-    large_arena = int(round16(need[~small].max())) if (~small).any() else 16
+    large_arena = int(round16(need_l[~small].max())) if (~small).any() else 16
 
     return FamilyBatch(
         fam_off=fam_off.astype(np.uint32), rec_off=rec_off.astype(np.uint32),
         rec_pos=raw.pos[order].astype(np.int32),
         rec_lenflag=(Lb | (fo << 16)).astype(np.uint32), rec_tid=raw.tid[order].astype(np.int32),
-        rec_link=link.astype(np.uint32), cig_off=cig_off.astype(np.uint32), cig_info=cig_info,
+        rec_link=link.astype(np.uint32), rec_win=rec_win.astype(np.uint32),
+        cig_off=cig_off.astype(np.uint32), cig_info=cig_info,
         cigar=cigar_c if cigar_c.shape[0] else np.zeros(1, np.uint32),
-        rt=rt.reshape(-1).astype(np.int32), seq=seq if seq.shape[0] else np.zeros(1, np.uint8),
-        qual=qual if qual.shape[0] else np.zeros(1, np.uint8),
-        small_fams=small_fams, large_fams=large_fams, max_len=int(Lb.max()) if nr else 0,
-        small_arena=small_arena, large_arena=large_arena, src=order.astype(np.int64),
-        fam_mi=fam_mi.astype(np.int32), n_bases=total)
+        rt=rt.reshape(-1).astype(np.int32), seq=seq, qual=qual,
+        small_buckets=buckets, small_arenas=arenas, large_fams=large_fams, max_len=max_len,
+        large_arena=large_arena, src=order.astype(np.int64), fam_mi=fam_mi.astype(np.int32),
+        n_bases=total, n_slots=n_slots)

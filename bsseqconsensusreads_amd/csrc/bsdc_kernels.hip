@@ -2,20 +2,25 @@
 //
 // One launch does, per MI family, everything rules convert_Bstrain -> extend -> groupsort_convert
 // -> callduplex do (main.snake.py:121-164) after the host has formed the families:
-//   phase 1  B-strand conversion        tools/1.convert_AG_to_CT.py:84-183
-//   phase 2  gap extension              tools/2.extend_gap.py:58-110 (4-record groups, :112-140)
-//   phase 3  overlapping-bases consensus    fgbio, --consensus-call-overlapping-bases=true
-//   phase 4  source reads                   fgbio toSourceRead (orientation, read-through, trailing N)
-//   phase 5  most-common-alignment filter   fgbio filterToMostCommonAlignment
-//   phase 6  single-strand likelihood vote  fgbio VanillaUmiConsensusCaller (pre 45 / post 30)
-//   phase 7  duplex combine                 fgbio DuplexConsensusCaller.duplexConsensus
+//   B-strand conversion        tools/1.convert_AG_to_CT.py:84-183
+//   gap extension              tools/2.extend_gap.py:58-110 (4-record groups, :112-140)
+//   overlapping-bases consensus    fgbio, --consensus-call-overlapping-bases=true
+//   source reads                   fgbio toSourceRead (orientation, read-through, trailing N)
+//   most-common-alignment filter   fgbio filterToMostCommonAlignment
+//   single-strand likelihood vote  fgbio VanillaUmiConsensusCaller (pre 45 / post 30)
+//   duplex combine                 fgbio DuplexConsensusCaller.duplexConsensus
 // The fgbio rows are restated from its public behaviour (parity unpinned).
 //
-// Layout: a family's records are staged once from HBM into an arena (LDS for the small-family
-// kernel: one wavefront per family; LDS or global scratch for the large-family kernel: one
-// 256-thread workgroup per family), every phase works in the arena, and only the consensus pair
-// (packed nt16 + quals) goes back to HBM.  All integer / byte work; the vote's likelihood sums
-// are exact fixed-point int64 so any summation order is bit-identical to the CPU restatement.
+// Two kernels:
+//  * k_small -- one wavefront per family (families of <= 64 records whose arena fits the
+//    bucket's LDS budget).  The family's slots are ONE contiguous, 32-aligned image in HBM
+//    (include/bsdc.h); every 16-byte chunk of it (quals, packed bases) and of the converted
+//    records' reference windows is requested up front (<= 4 loads in flight per lane), unpacked
+//    into LDS, and everything after that is LDS + registers.  Per-record metadata lives in the
+//    record's lane; loops over records are wave-uniform and read it with readlane.
+//  * k_large -- one 256-thread workgroup per family, generic (arena in LDS or HBM scratch).
+// All integer / byte work; the vote's likelihood sums are exact fixed-point integers (2^-20 nats),
+// so any summation order is bit-identical to the CPU restatement (oracle/).
 #include <hip/hip_runtime.h>
 
 #include <cmath>
@@ -23,7 +28,6 @@
 #include <cstdlib>
 #include <cstring>
 #include <string>
-#include <vector>
 
 #include "../../include/bsdc.h"
 
@@ -31,110 +35,36 @@ namespace {
 
 constexpr int kWave = 64;
 constexpr int kLargeThreads = 256;
-constexpr int kSmallWaves = 4;  // wavefronts (families) per small-kernel workgroup
-constexpr double kLrScale = 1099511627776.0;  // 2^40
-constexpr double kLrInvScale = 9.094947017729282379150390625e-13;
+constexpr int kSmallWaves = 4;                 // wavefronts (families) per small-kernel workgroup
+constexpr double kLrScale = 1048576.0;          // 2^20
+constexpr int kTabBytes = 1024 + 384 + 2048 + 192;  // the Tables image in LDS
+constexpr uint32_t kLinkRdDev = 1u << 27;       // device-internal: tool 1 trimmed a base (RD=1)
 
 // nt16 codes
-constexpr uint8_t kA = 1, kC = 2, kG = 4, kT = 8, kN = 15;
-
-struct RecMeta {  // 48 B, one per record of the family, in the arena
-    int32_t pos;     // current leftmost position
-    int32_t len;     // current length
-    uint32_t slot;   // arena offset of the base slot (quals at slot + cap)
-    int32_t cap;     // slot capacity (input length + 2)
-    int32_t start;   // index of the first base inside the slot
-    uint32_t link;
-    uint32_t gidx;   // global record index
-    int32_t tid;
-    int32_t srclen;  // source-read length (phase 4)
-    int32_t reflen;  // current reference length
-    uint16_t flag;
-    uint8_t rd;
-    uint8_t set;     // 0 AB-R1, 1 AB-R2, 2 BA-R1, 3 BA-R2, 0xFF none
-    int32_t in_len;
-};
-static_assert(sizeof(RecMeta) == 48, "RecMeta layout");
+constexpr uint32_t kA = 1, kC = 2, kG = 4, kT = 8, kN = 15;
 
 struct Tables {
-    long long lr[256];
-    float thr[96];
+    int32_t lr[256];    // round((ln(1-a) - ln(a/3)) * 2^20), a = P(error) of a Q base after the post-UMI step
+    float thr[96];      // Q >= k  <=>  S <= thr[k]
+    uint8_t qlo[2048];  // agreement case (S = 3 e^-D): Q at D = 2^16 k
+    int32_t dthr[48];   // agreement case: smallest D with Q >= q (INT32_MAX: never)
 };
 
 __host__ __device__ inline int64_t round16(int64_t x) { return (x + 15) & ~int64_t(15); }
-
-// Arena layout of one family (offsets from the arena base).
-struct ArenaLayout {
-    uint32_t meta, lists, ssb, ssq, simp, slots, total;
-    int32_t ssw;
-    __host__ __device__ ArenaLayout(int n, int64_t sum_len, int max_len, int64_t complex_ops) {
-        ssw = (int32_t)round16(max_len + 2);
-        int64_t o = 0;
-        meta = (uint32_t)o;
-        o += round16((int64_t)n * (int64_t)sizeof(RecMeta));
-        lists = (uint32_t)o;
-        o += round16((int64_t)n * 8);
-        ssb = (uint32_t)o;
-        o += 4 * (int64_t)ssw;
-        ssq = (uint32_t)o;
-        o += 4 * (int64_t)ssw;
-        simp = (uint32_t)o;
-        if (complex_ops > 0) o += round16(4 * (complex_ops + 4 * (int64_t)n));
-        slots = (uint32_t)o;
-        o += round16(2 * sum_len + 4 * (int64_t)n);
-        total = (uint32_t)o;
-    }
-};
+__host__ __device__ inline int ref_chunks(int max_len) { return (15 + (max_len + 4) / 2 + 15) / 16; }
 
 // ------------------------------------------------------------------------------------------
-// group abstraction: a wavefront (G = 64) or a workgroup (G = 256)
+// shared device helpers
 // ------------------------------------------------------------------------------------------
-template <int G>
-struct Grp {
-    int t;
-    int *red;  // LDS scratch of G/64 ints (G > 64 only)
-    __device__ __forceinline__ void sync() const {
-        if constexpr (G == kWave) {
-            __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
-            __builtin_amdgcn_wave_barrier();
-            __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
-        } else {
-            __syncthreads();
-        }
-    }
-    __device__ __forceinline__ int max(int v) const {
-#pragma unroll
-        for (int o = 32; o >= 1; o >>= 1) v = ::max(v, __shfl_xor(v, o, kWave));
-        if constexpr (G == kWave) {
-            return v;
-        } else {
-            sync();
-            if ((t & 63) == 0) red[t >> 6] = v;
-            sync();
-            int r = red[0];
-#pragma unroll
-            for (int w = 1; w < G / kWave; w++) r = ::max(r, red[w]);
-            sync();
-            return r;
-        }
-    }
-    __device__ __forceinline__ int any(int v) const { return max(v ? 1 : 0); }
-};
-
-// ------------------------------------------------------------------------------------------
-// small helpers
-// ------------------------------------------------------------------------------------------
-__device__ __forceinline__ uint8_t nib(const uint8_t *p, int64_t k) {
-    const uint8_t b = p[k >> 1];
+__device__ __forceinline__ uint32_t nib(const uint8_t *p, int64_t k) {
+    const uint32_t b = p[k >> 1];
     return (k & 1) ? (b & 0xF) : (b >> 4);
 }
-// htsjdk complement: A<->T, C<->G, everything else unchanged
-__device__ __forceinline__ uint8_t comp_nt16(uint8_t b) {
-    return b == kA ? kT : b == kT ? kA : b == kC ? kG : b == kG ? kC : b;
-}
-__device__ __forceinline__ int base_idx(uint8_t b) {
-    return b == kA ? 0 : b == kC ? 1 : b == kG ? 2 : b == kT ? 3 : -1;
-}
+// htsjdk complement (A<->T, C<->G); other codes only need to stay non-ACGT: nt16 4-bit reversal
+__device__ __forceinline__ uint32_t comp_nt16(uint32_t b) { return __builtin_bitreverse32(b) >> 28; }
+__device__ __forceinline__ bool is_acgt(uint32_t b) { return b != 0 && (b & (b - 1)) == 0 && b < 16; }
+__device__ __forceinline__ int acgt_idx(uint32_t b) { return __builtin_ctz(b); }
+
 __device__ __forceinline__ float det_expf(float x) {
     // keep in step with oracle/bsdc_oracle.c orc_det_expf: same reduction, same fma chain
     const float t = x * 1.44269504088896341f;
@@ -151,30 +81,57 @@ __device__ __forceinline__ float det_expf(float x) {
     return ldexpf(p, (int)n);
 }
 
-struct RefView {
-    const uint8_t *seq;
-    const int64_t *off;
-    const int64_t *len;
-    int32_t n;
-};
+// S = sum over the three other bases of e^(D_b - D_best), each term skipped below e^-80
+__device__ __forceinline__ float term(long long d) {
+    const float x = (float)((double)d * 9.5367431640625e-07);
+    return x < -80.0f ? 0.0f : det_expf(x);
+}
 
-// reference nibble at contig position p (N past the contig end or for an absent contig)
-__device__ __forceinline__ uint8_t ref_at(const RefView &R, int32_t tid, int64_t p) {
-    if (tid < 0 || tid >= R.n) return kN;
-    const int64_t o = R.off[tid];
-    if (o < 0 || p < 0 || p >= R.len[tid]) return kN;
-    return nib(R.seq, o + p);
+// Q = max k with S <= thr[k] (thr is non-increasing), binary search over 1..93
+__device__ __forceinline__ int phred_of(float S, const float *thr) {
+    int lo = 0, hi = 93;
+#pragma unroll
+    for (int it = 0; it < 7; it++) {
+        const int mid = (lo + hi + 1) >> 1;
+        if (lo < hi) {
+            if (S <= thr[mid])
+                lo = mid;
+            else
+                hi = mid - 1;
+        }
+    }
+    return lo;
 }
 
 // tool 1 per-base rule (tools/1.convert_AG_to_CT.py:123-150), in its local form: the value at i
 // depends on m[i], m[i+1], ref[i], ref[i+1] only (the skip at :140 writes what the A rule would)
-__device__ __forceinline__ uint8_t convert_rule(uint8_t m0, uint8_t m1, bool has_next, uint8_t f0, uint8_t f1) {
+__device__ __forceinline__ uint32_t convert_rule(uint32_t m0, uint32_t m1, bool has_next, uint32_t f0, uint32_t f1) {
     if (m0 == kA) return f0 == kG ? kG : kA;
     if (m0 == kC) {
         if (f0 == kC && f1 == kG) return (has_next && m1 == kA) ? kT : kC;
         return kT;
     }
     return m0;
+}
+
+// ---- SWAR: four nt16 codes, one per byte ----
+__device__ __forceinline__ uint32_t eq4(uint32_t x, uint32_t code) {
+    // 0x0F in every byte equal to `code`, 0 elsewhere (bytes hold 0..15)
+    const uint32_t t = x ^ (code * 0x01010101u);
+    const uint32_t z = ((t + 0x0F0F0F0Fu) & 0x10101010u) ^ 0x10101010u;
+    return z - (z >> 4);
+}
+__device__ __forceinline__ uint32_t sel4(uint32_t m, uint32_t a, uint32_t b) { return (m & a) | (~m & b); }
+
+// the conversion rule on four positions: m = m[j..j+3], m1 = m[j+1..j+4], f0 = ref[j..j+3],
+// f1 = ref[j+1..j+4], nxt = 0x0F where position j+k has a next base
+__device__ __forceinline__ uint32_t convert4(uint32_t m, uint32_t m1, uint32_t f0, uint32_t f1, uint32_t nxt) {
+    const uint32_t mA = eq4(m, kA), mC = eq4(m, kC);
+    const uint32_t cpg = eq4(f0, kC) & eq4(f1, kG);
+    const uint32_t nA = eq4(m1, kA) & nxt;
+    const uint32_t selA = sel4(eq4(f0, kG), 0x04040404u, 0x01010101u);
+    const uint32_t selC = sel4(cpg, sel4(nA, 0x08080808u, 0x02020202u), 0x08080808u);
+    return sel4(mA, selA, sel4(mC, selC, m));
 }
 
 // Cigar of the current record for complex records: [npre x M1] + input ops (the last one
@@ -226,233 +183,1051 @@ __device__ int read_at_ref(const CigView &c, int32_t pos, int32_t len, int64_t p
     return -1;
 }
 
+__device__ __forceinline__ CigView make_cigview(const bsdc_family_batch &B, uint32_t gidx, uint32_t link, bool conv,
+                                                bool rd, bool do_extend) {
+    CigView c;
+    c.ops = B.cigar + B.cig_off[gidx];
+    c.n = (int)(B.cig_info[gidx] & 0xFFFF);
+    c.npre = (conv || (do_extend && (link & BSDC_LINK_EXT_RIGHT))) ? 1 : 0;
+    c.nsuf = (do_extend && (link & BSDC_LINK_EXT_LEFT) && rd) ? 1 : 0;
+    c.rdtrim = (conv && rd) ? 1 : 0;
+    return c;
+}
+
+// fgbio toSourceRead's read-through trim (isFrPair + the stale mate fields), on a record of
+// current position `pos`, length `len`, reference length `reflen`
+__device__ int32_t readthrough_keep(const bsdc_family_batch &B, uint32_t gidx, uint32_t flag, int32_t pos,
+                                    int32_t len, int32_t reflen, bool complex_, const CigView *cv) {
+    const int32_t *rt = B.rt + 4 * (int64_t)gidx;
+    const int32_t next_pos = rt[0], tlen = rt[1], mate_us = rt[2], mate_ue = rt[3];
+    const bool neg = flag & 16, mneg = flag & 32;
+    if (neg == mneg) return len;
+    const int64_t posfive = neg ? (int64_t)next_pos : (int64_t)pos;
+    const int64_t negfive = neg ? (int64_t)pos + reflen - 1 : (int64_t)pos + tlen;
+    if (!(posfive < negfive)) return len;
+    int32_t keep = len;
+    if (!neg) {
+        const int64_t end = (int64_t)pos + reflen - 1;
+        if (end > mate_ue) {
+            int32_t kk;
+            if (!complex_) {
+                kk = (int32_t)::min<int64_t>((int64_t)mate_ue - pos + 1, len);
+                if (kk < 0) kk = 0;
+            } else {
+                int last = -1;
+                for (int64_t p = pos; p <= mate_ue && p < (int64_t)pos + reflen; p++) {
+                    const int q = read_at_ref(*cv, pos, len, p);
+                    if (q >= 0) last = q;
+                }
+                kk = last + 1;
+            }
+            keep = ::min(keep, kk);
+        }
+    } else if ((int64_t)pos < mate_us) {
+        int32_t kk;
+        if (!complex_) {
+            const int64_t first = (int64_t)mate_us - pos;
+            kk = first >= len ? 0 : (int32_t)(len - first);
+        } else {
+            int first = len;
+            for (int64_t p = (int64_t)pos + reflen - 1; p >= mate_us && p >= pos; p--) {
+                const int q = read_at_ref(*cv, pos, len, p);
+                if (q >= 0) first = q;
+            }
+            kk = len - first;
+        }
+        keep = ::min(keep, kk);
+    }
+    return keep;
+}
+
+// Simplified cigar of a source read (sequencing orientation, M/=/X -> M, merged, truncated to
+// srclen query bases) into `so`; returns the op count.
+__device__ int simplified_cigar(const CigView *cv, bool complex_, bool neg, int32_t srclen, uint32_t *so) {
+    if (!complex_) {
+        so[0] = ((uint32_t)srclen << 4) | 0u;
+        return 1;
+    }
+    int cnt = 0;
+    const int tot = cv->count();
+    int32_t q = 0;
+    for (int j = 0; j < tot && q < srclen; j++) {
+        const int k = neg ? tot - 1 - j : j;
+        int op;
+        int32_t l;
+        cv->at(k, op, l);
+        if (l <= 0) continue;
+        if (op == 7 || op == 8) op = 0;
+        if (op == 4 || op == 5) continue;
+        if (op == 0 || op == 1) {
+            if (q + l > srclen) l = srclen - q;
+            q += l;
+        }
+        if (cnt > 0 && (int)(so[cnt - 1] & 0xF) == op)
+            so[cnt - 1] = (((so[cnt - 1] >> 4) + (uint32_t)l) << 4) | (uint32_t)op;
+        else
+            so[cnt++] = ((uint32_t)l << 4) | (uint32_t)op;
+    }
+    return cnt;
+}
+
+__device__ __forceinline__ bool cigar_prefix(const uint32_t *ac, int an, const uint32_t *bc, int bn) {
+    bool pre = an <= bn;
+    for (int k = 0; pre && k < an - 1; k++) pre = ac[k] == bc[k];
+    if (pre && an > 0) pre = (ac[an - 1] & 0xF) == (bc[an - 1] & 0xF) && (ac[an - 1] >> 4) <= (bc[an - 1] >> 4);
+    return pre;
+}
+
+// fgbio filterToMostCommonAlignment on one of X / Y, single thread.  `ord` (scratch, n entries)
+// holds the candidate records; srclen[] / sofs[] / so[] describe them; rejected ones get set 0xFF.
+__device__ void filter_group(uint16_t *ord, int cnt, const uint16_t *srclen, const uint32_t *sofs, const uint32_t *so,
+                             uint8_t *set) {
+    if (cnt < 2) return;
+    for (int i = 1; i < cnt; i++) {  // stable sort by source length, descending
+        const uint16_t x = ord[i];
+        int j = i - 1;
+        while (j >= 0 && srclen[ord[j]] < srclen[x]) {
+            ord[j + 1] = ord[j];
+            j--;
+        }
+        ord[j + 1] = x;
+    }
+    int ng = 0;
+    uint16_t gdef[64];
+    int gsize[64];
+    for (int i = 0; i < cnt; i++) {
+        const uint32_t ai = sofs[ord[i]];
+        bool found = false;
+        for (int gi = 0; gi < ng; gi++) {
+            const uint32_t bi = sofs[gdef[gi]];
+            if (cigar_prefix(so + (ai & 0xFFFF), (int)(ai >> 16), so + (bi & 0xFFFF), (int)(bi >> 16))) {
+                gsize[gi]++;
+                found = true;
+            }
+        }
+        if (!found && ng < 64) {
+            gdef[ng] = ord[i];
+            gsize[ng] = 1;
+            ng++;
+        }
+    }
+    if (ng <= 1) return;
+    int best = 0;
+    for (int gi = 1; gi < ng; gi++)
+        if (gsize[gi] > gsize[best]) best = gi;
+    const uint32_t bi = sofs[gdef[best]];
+    for (int i = 0; i < cnt; i++) {
+        const uint32_t ai = sofs[ord[i]];
+        if (!cigar_prefix(so + (ai & 0xFFFF), (int)(ai >> 16), so + (bi & 0xFFFF), (int)(bi >> 16))) set[ord[i]] = 0xFF;
+    }
+}
+
 struct KParams {
     bsdc_family_batch B;
     bsdc_consensus O;
-    RefView R;
+    const uint8_t *ref;  // packed nt16 genome
     const Tables *tab;
     int32_t mode;
     int32_t overlap;
 };
 
-// ------------------------------------------------------------------------------------------
-// one family, processed by group g in arena A
-// ------------------------------------------------------------------------------------------
-template <int G>
-__device__ void process_family(const KParams &P, const Grp<G> &g, uint8_t *A, const long long *lr,
-                               const float *thr, uint32_t fam) {
+__device__ __forceinline__ void load_tables(const Tables *tab, uint8_t *dst) {
+    static_assert(sizeof(Tables) == kTabBytes, "Tables image");
+    const uint4 *src = reinterpret_cast<const uint4 *>(tab);
+    uint4 *d = reinterpret_cast<uint4 *>(dst);
+    for (int i = threadIdx.x; i < kTabBytes / 16; i += blockDim.x) d[i] = src[i];
+    __syncthreads();
+}
+
+// duplex combine of two SS columns (fgbio DuplexConsensusCaller.duplexConsensus)
+__device__ __forceinline__ void duplex_col(uint32_t xb, uint32_t xq, uint32_t yb, uint32_t yq, uint32_t &ob, uint32_t &oq) {
+    uint32_t rb;
+    int rq;
+    if (xb == yb) {
+        rb = xb;
+        rq = (int)(xq + yq);
+    } else if (xq > yq) {
+        rb = xb;
+        rq = (int)(xq - yq);
+    } else if (yq > xq) {
+        rb = yb;
+        rq = (int)(yq - xq);
+    } else {
+        rb = xb;
+        rq = 2;
+    }
+    if (rq > 93) rq = 93;
+    if (xb == kN || yb == kN || rq == 2) {
+        rb = kN;
+        rq = 2;
+    }
+    ob = rb;
+    oq = (uint32_t)rq;
+}
+
+// ==========================================================================================
+// k_small: one wavefront per family, everything in LDS
+// ==========================================================================================
+struct SmallLayout {
+    uint32_t bimg, qimg, ref, lists, meta, misc, outb, outq, squeue, descs, simp, total;
+    int32_t ws, ow;
+    __host__ __device__ SmallLayout(int n, int64_t img, int nconv, int64_t cops, int max_len) {
+        ws = 32 * ref_chunks(max_len);
+        ow = (int32_t)round16(max_len + 2);
+        int64_t o = 0;
+        bimg = (uint32_t)o;
+        o += img;
+        qimg = (uint32_t)o;
+        o += img;
+        ref = (uint32_t)o;
+        o += (int64_t)nconv * ws;
+        lists = (uint32_t)o;  // 4 x 64 record indices (u8)
+        o += 256;
+        meta = (uint32_t)o;   // SMeta per record (serial filter only)
+        o += round16(16 * (int64_t)n);
+        misc = (uint32_t)o;   // lc[4] u32 | srclen[64] u16 (serial filter only)
+        o += 160;
+        outb = (uint32_t)o;   // duplex bases, 2 ends
+        o += 2 * (int64_t)ow;
+        outq = (uint32_t)o;   // duplex quals, 2 ends
+        o += 2 * (int64_t)ow;
+        squeue = (uint32_t)o; // queued (end, column) of disagreeing columns
+        o += 4 * (int64_t)ow;
+        descs = (uint32_t)o;  // per-record source descriptor (queued path)
+        o += 256;
+        simp = (uint32_t)o;   // simplified cigars (serial filter only)
+        if (cops > 0) o += round16(4 * (cops + 4 * (int64_t)n));
+        total = (uint32_t)o;
+    }
+};
+
+struct SMeta {  // 16 B, LDS copy of a record's registers (only for the rare serial path)
+    uint32_t gidx;
+    int32_t pos;
+    uint32_t link;
+    uint16_t len;
+    uint16_t flag;
+};
+
+__device__ __forceinline__ void wave_sync() {
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+    __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+}
+__device__ __forceinline__ uint64_t ballot(bool p) { return __ballot(p); }
+__device__ __forceinline__ int mbcnt(uint64_t m) {
+    return (int)__builtin_amdgcn_mbcnt_hi((uint32_t)(m >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)m, 0));
+}
+// value of a per-lane register held by `lane` (wave-uniform lane index)
+__device__ __forceinline__ int32_t rl(int32_t v, int lane) { return __builtin_amdgcn_readlane(v, lane); }
+__device__ __forceinline__ uint32_t rlu(uint32_t v, int lane) { return (uint32_t)__builtin_amdgcn_readlane((int)v, lane); }
+__device__ __forceinline__ uint32_t lds32(const uint8_t *p) { return *reinterpret_cast<const uint32_t *>(p); }
+__device__ __forceinline__ void st32(uint8_t *p, uint32_t v) { *reinterpret_cast<uint32_t *>(p) = v; }
+__device__ __forceinline__ uint32_t alignbyte(uint32_t hi, uint32_t lo, uint32_t s) {
+    return __builtin_amdgcn_alignbyte(hi, lo, s);
+}
+// 16 packed bytes (32 nibbles, high first) -> 32 bytes
+__device__ __forceinline__ void unpack32(uint4 v, uint8_t *dst) {
+    const uint32_t w[4] = {v.x, v.y, v.z, v.w};
+    uint32_t o[8];
+#pragma unroll
+    for (int k = 0; k < 4; k++) {
+        const uint32_t lo = w[k] & 0x0F0F0F0Fu;
+        const uint32_t hi = (w[k] >> 4) & 0x0F0F0F0Fu;
+        o[2 * k] = __builtin_amdgcn_perm(lo, hi, 0x05010400u);
+        o[2 * k + 1] = __builtin_amdgcn_perm(lo, hi, 0x07030602u);
+    }
+    uint4 *d = reinterpret_cast<uint4 *>(dst);
+    d[0] = make_uint4(o[0], o[1], o[2], o[3]);
+    d[1] = make_uint4(o[4], o[5], o[6], o[7]);
+}
+
+__global__ __launch_bounds__(kWave *kSmallWaves) void k_small(KParams P, const uint32_t *fams, int64_t nfams,
+                                                              int32_t arena) {
+    extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
+    const Tables *T = reinterpret_cast<const Tables *>(smem);
+    const int32_t *lr = T->lr;
+    const float *thr = T->thr;
+    const uint8_t *qlo = T->qlo;
+    const int32_t *dthr = T->dthr;
+    load_tables(P.tab, smem);
+    const int w = threadIdx.x >> 6;
+    const int t = threadIdx.x & 63;
+    const int64_t fi = (int64_t)blockIdx.x * kSmallWaves + w;
+    if (fi >= nfams) return;
+    uint8_t *A = smem + kTabBytes + (size_t)w * (size_t)arena;
     const bsdc_family_batch &B = P.B;
-    const uint32_t r0 = B.fam_off[fam];
-    const int n = (int)(B.fam_off[fam + 1] - r0);
-    const uint32_t off0 = n > 0 ? B.rec_off[r0] : 0u;
     const bool do_convert = P.mode & BSDC_MODE_CONVERT;
     const bool do_extend = P.mode & BSDC_MODE_EXTEND;
     const bool do_vote = P.mode & BSDC_MODE_VOTE;
+    const int max_len = B.max_len;
+    const int stop = (P.mode >> BSDC_MODE_STOP_SHIFT) & 15;  // profiling ablation (0 = full kernel)
 
-    // complex-cigar op count of the family (sizes the arena's simplified-cigar region)
-    int64_t cops = 0;
-    int maxlen_f = 0;
-    {
-        int c = 0, ml = 0;
-        for (int r = g.t; r < n; r += G) {
-            const uint32_t lk = B.rec_link[r0 + r];
-            if (lk & BSDC_LINK_COMPLEX) c += (int)(B.cig_info[r0 + r] & 0xFFFF);
-            ml = ::max(ml, (int)(B.rec_lenflag[r0 + r] & 0xFFFF));
-        }
-        // sum via max-of-prefix is not available; complex families are rare: use a group sum by max trick
-        // (sum over lanes with shuffles)
+    const uint32_t fam = __builtin_amdgcn_readfirstlane(fams[fi]);
+    const uint32_t r0 = __builtin_amdgcn_readfirstlane(B.fam_off[fam]);
+    const int n = (int)(__builtin_amdgcn_readfirstlane(B.fam_off[fam + 1]) - r0);
+
+    // ---- record metadata: lane t owns record t ----
+    const bool has = t < n;
+    uint4 rc = make_uint4(0, 0, 0, 0);
+    if (has) rc = reinterpret_cast<const uint4 *>(B.rec)[r0 + t];
+    const uint32_t gslot = rc.x;
+    int32_t pos = (int32_t)rc.y;
+    const int32_t L = (int32_t)(rc.z & 0xFFFF);
+    const uint32_t flag = rc.z >> 16;
+    uint32_t link = rc.w;
+    const bool conv = has && do_convert && (link & BSDC_LINK_CONVERT);
+    uint2 win = make_uint2(0, 0);
+    if (conv) win = reinterpret_cast<const uint2 *>(B.rec_win)[r0 + t];
+    const bool cplx = has && (link & BSDC_LINK_COMPLEX);
+    const uint32_t cinfo = cplx ? B.cig_info[r0 + t] : 0;
+
+    const uint64_t conv_mask = ballot(conv);
+    const int nconv = __builtin_popcountll(conv_mask);
+    const int ci = mbcnt(conv_mask);
+    const uint32_t base_g = rlu(gslot, 0);
+    const uint32_t cap4 = (uint32_t)((L + 2 + 3) & ~3);
+    const uint32_t end_g = rlu(gslot + cap4, n - 1);
+    const uint32_t img = (end_g - base_g + 31u) & ~31u;
+    int cops = (int)(cinfo & 0xFFFF);
 #pragma unroll
-        for (int o = 32; o >= 1; o >>= 1) c += __shfl_xor(c, o, kWave);
-        if constexpr (G > kWave) {
-            g.sync();
-            if ((g.t & 63) == 0) g.red[g.t >> 6] = c;
-            g.sync();
-            int s = 0;
-            for (int w = 0; w < G / kWave; w++) s += g.red[w];
-            c = s;
-            g.sync();
-        }
-        cops = c;
-        maxlen_f = g.max(ml);
-    }
-    const ArenaLayout L(n, 0, maxlen_f, cops);  // slot region placed last; its size is not needed here
-    RecMeta *M = reinterpret_cast<RecMeta *>(A + L.meta);
-    uint16_t *lists = reinterpret_cast<uint16_t *>(A + L.lists);
-    uint8_t *ssb = A + L.ssb;
-    uint8_t *ssq = A + L.ssq;
-    uint32_t *simp = reinterpret_cast<uint32_t *>(A + L.simp);
-    uint8_t *slots = A + L.slots;
-    const int ssw = L.ssw;
+    for (int o = 32; o >= 1; o >>= 1) cops += __shfl_xor(cops, o, kWave);
+    const SmallLayout Lo(n, img, nconv, cops, max_len);
+    uint8_t *bimg = A + Lo.bimg;
+    uint8_t *qimg = A + Lo.qimg;
+    uint8_t *refw = A + Lo.ref;
+    const int ws = Lo.ws;
+    uint32_t *lc = reinterpret_cast<uint32_t *>(A + Lo.misc);
+    uint16_t *srcl = reinterpret_cast<uint16_t *>(A + Lo.misc + 16);
+    uint32_t *convwin = reinterpret_cast<uint32_t *>(A + Lo.lists);  // temporary, before the lists exist
+    const uint32_t slot = gslot - base_g;                              // record slot in the image
+    if (conv) convwin[ci] = win.x;
+    if (t < 4) lc[t] = 0;
+    wave_sync();
 
-    // ---- phase 0: record metadata ----
-    for (int r = g.t; r < n; r += G) {
+    // ---- stage the family image: every chunk load in flight at once ----
+    {
+        const int rcn = ref_chunks(max_len);
+        const int nq = (int)(img >> 4), ns = (int)(img >> 5);
+        const int total = nq + ns + nconv * rcn;
+        uint4 v[4];
+#pragma unroll
+        for (int u = 0; u < 4; u++) {
+            const int k = t + 64 * u;
+            v[u] = make_uint4(0, 0, 0, 0);
+            if (k < nq) {
+                v[u] = *reinterpret_cast<const uint4 *>(B.qual + base_g + 16 * (uint32_t)k);
+            } else if (k < nq + ns) {
+                v[u] = *reinterpret_cast<const uint4 *>(B.seq + (base_g >> 1) + 16 * (uint32_t)(k - nq));
+            } else if (k < total) {
+                const int kk = k - nq - ns;
+                const int cr = kk / rcn, part = kk - cr * rcn;
+                const uint32_t wb = (convwin[cr] >> 1) & ~15u;
+                v[u] = *reinterpret_cast<const uint4 *>(P.ref + wb + 16 * (uint32_t)part);
+            }
+        }
+#pragma unroll
+        for (int u = 0; u < 4; u++) {
+            const int k = t + 64 * u;
+            if (k < nq) {
+                *reinterpret_cast<uint4 *>(qimg + 16 * k) = v[u];
+            } else if (k < nq + ns) {
+                unpack32(v[u], bimg + 32 * (k - nq));
+            } else if (k < total) {
+                const int kk = k - nq - ns;
+                const int cr = kk / rcn, part = kk - cr * rcn;
+                unpack32(v[u], refw + cr * ws + 32 * part);
+            }
+        }
+    }
+    wave_sync();
+    if (stop == 1) return;
+
+    // ---- tool 1: convert, one converted record at a time, 4 positions per lane ----
+    int32_t start = 1, len = L;
+    bool rd = false;
+    {
+        uint64_t cm = conv_mask;
+        while (cm) {
+            const int r = __builtin_ctzll(cm);
+            cm &= cm - 1;
+            const uint32_t s_slot = rlu(slot, r);
+            const int32_t s_L = rl(L, r);
+            const int s_ci = rl(ci, r);
+            const uint32_t s_win = rlu(win.x, r);
+            const int32_t s_avail = (int32_t)rlu(win.y, r);
+            const int32_t Lm = s_L + 1;
+            const uint32_t ph = s_win & 31u;
+            bool my_rd = false;
+            for (int j4 = 4 * t; j4 < Lm; j4 += 256) {
+                uint32_t m = lds32(bimg + s_slot + j4);
+                const uint32_t mn = lds32(bimg + s_slot + j4 + 4);
+                const uint32_t a = (uint32_t)(s_ci * ws) + ph + (uint32_t)j4;
+                const uint32_t d0 = lds32(refw + (a & ~3u)), d1 = lds32(refw + (a & ~3u) + 4);
+                const uint32_t sh = a & 3u;
+                uint32_t f0 = alignbyte(d1, d0, sh);
+                uint32_t f1 = sh == 3 ? d1 : alignbyte(d1, d0, sh + 1);
+                if (j4 + 5 > s_avail) {  // past the contig end / absent contig: N
+#pragma unroll
+                    for (int k = 0; k < 4; k++) {
+                        if (j4 + k >= s_avail) f0 = (f0 & ~(0xFFu << (8 * k))) | (kN << (8 * k));
+                        if (j4 + k + 1 >= s_avail) f1 = (f1 & ~(0xFFu << (8 * k))) | (kN << (8 * k));
+                    }
+                }
+                if (j4 == 0) m = (m & ~0xFFu) | (f0 & 0xFFu);  // :121 seed, m[0] = ref[0]
+                const uint32_t m1 = alignbyte(mn, m, 1);
+                uint32_t nxt = 0x0F0F0F0Fu;
+                const int last = Lm - 1 - j4;  // the record's last position has no next base
+                if (last >= 0 && last < 4) nxt &= ~(0xFFu << (8 * last));
+                const uint32_t out = convert4(m, m1, f0, f1, nxt);
+                st32(bimg + s_slot + j4, out);
+                if (last >= 0 && last < 4) {  // :157-170 a final C before a reference G is trimmed
+                    my_rd = ((out >> (8 * last)) & 0xFF) == kC && ((f1 >> (8 * last)) & 0xFF) == kG;
+                }
+            }
+            const bool s_rd = ballot(my_rd) != 0;
+            if (t == 0) qimg[s_slot] = 40;  // :174-177 'I' + quals
+            if (t == r) rd = s_rd;
+        }
+        if (conv) {
+            start = 0;
+            len = L + 1 - (rd ? 1 : 0);
+            pos = pos - 1 > 0 ? pos - 1 : 0;
+        }
+    }
+    if (!do_convert && has && (link & BSDC_LINK_RD_IN)) rd = true;
+    if (rd) link |= kLinkRdDev;
+    wave_sync();
+    if (stop == 2) return;
+
+    // ---- tool 2: gap extension of 4-record groups (tools/2.extend_gap.py:58-110) ----
+    if (do_extend) {
+        const int p = (int)((link >> BSDC_LINK_PARTNER_SHIFT) & 3u);
+        const uint32_t p_slot = (uint32_t)__shfl((int)slot, p, kWave);
+        const int32_t p_start = __shfl(start, p, kWave);
+        const int32_t p_len = __shfl(len, p, kWave);
+        const bool er = has && (link & BSDC_LINK_EXT_RIGHT);
+        const bool el = has && (link & BSDC_LINK_EXT_LEFT) && rd;
+        uint32_t b0 = 0, q0 = 0, bl = 0, ql = 0;
+        if (er) {  // :70-80 the converted partner's first base / qual
+            b0 = bimg[p_slot + p_start];
+            q0 = qimg[p_slot + p_start];
+        }
+        if (el) {  // :92-101 the partner's last base / qual, after its own prepend
+            if (p_len > 0) {
+                bl = bimg[p_slot + p_start + p_len - 1];
+                ql = qimg[p_slot + p_start + p_len - 1];
+            } else {
+                bl = bimg[slot + start];
+                ql = qimg[slot + start];
+            }
+        }
+        if (er) {
+            bimg[slot + start - 1] = (uint8_t)b0;
+            qimg[slot + start - 1] = (uint8_t)q0;
+            start -= 1;
+            len += 1;
+            pos -= 1;
+        }
+        if (el) {
+            bimg[slot + start + len] = (uint8_t)bl;
+            qimg[slot + start + len] = (uint8_t)ql;
+            len += 1;
+        }
+        wave_sync();
+    }
+
+    // current reference length
+    int32_t reflen = len;
+    if (cplx) {
+        reflen = (int32_t)(cinfo >> 16) + (conv ? 1 : 0) - ((conv && rd) ? 1 : 0) +
+                 ((do_extend && (link & BSDC_LINK_EXT_RIGHT)) ? 1 : 0) +
+                 ((do_extend && (link & BSDC_LINK_EXT_LEFT) && rd) ? 1 : 0);
+    }
+
+    // ---- stage dump ----
+    if (P.mode & BSDC_MODE_DUMP) {
+        for (int r = 0; r < n; r++) {
+            const uint32_t s_slot = rlu(slot, r), s_g = rlu(gslot, r);
+            const int32_t s_start = rl(start, r), s_len = rl(len, r);
+            for (int j = t; j < s_len; j += 64) {
+                P.O.dump_seq[s_g + j] = bimg[s_slot + s_start + j];
+                P.O.dump_qual[s_g + j] = qimg[s_slot + s_start + j];
+            }
+        }
+        if (has) {
+            const uint32_t gi = r0 + t;
+            P.O.dump_pos[gi] = pos;
+            P.O.dump_len[gi] = (uint16_t)len;
+            uint8_t tg = 0;
+            if (rd) tg |= 1;
+            if (conv) tg |= 2 | 4;
+            if (do_extend && (link & BSDC_LINK_EXT_RIGHT)) tg |= 4;
+            if (do_extend && (link & BSDC_LINK_EXT_LEFT) && rd) tg |= 8;
+            P.O.dump_tags[gi] = tg;
+        }
+    }
+    if (!do_vote || stop == 3) return;
+
+    // ---- overlapping-bases consensus, one template at a time ----
+    const uint32_t mate = link & BSDC_LINK_MATE_MASK;
+    const bool usable = has && (link & BSDC_LINK_USABLE);
+    if (P.overlap) {
+        const bool mate_ok = usable && mate != BSDC_LINK_MATE_MASK && !(flag & 4);
+        uint64_t tm = ballot(mate_ok);
+        while (tm) {
+            const int a = __builtin_ctzll(tm);
+            tm &= tm - 1;
+            const int b = (int)rlu(mate, a);
+            const uint32_t la_ = rlu(link, a), lb_ = rlu(link, b);
+            if (!(lb_ & BSDC_LINK_USABLE) || (rlu(flag, b) & 4)) continue;
+            const int32_t pa = rl(pos, a), pb = rl(pos, b), la = rl(len, a), lb = rl(len, b);
+            const int32_t ra = rl(reflen, a), rbn = rl(reflen, b);
+            if (ra <= 0 || rbn <= 0) continue;
+            const int32_t s0 = ::max(pa, pb);
+            const int32_t e0 = ::min(pa + ra - 1, pb + rbn - 1);
+            if (s0 > e0) continue;
+            const uint32_t sa = rlu(slot, a) + (uint32_t)rl(start, a), sb = rlu(slot, b) + (uint32_t)rl(start, b);
+            const bool ca = la_ & BSDC_LINK_COMPLEX, cb = lb_ & BSDC_LINK_COMPLEX;
+            CigView va, vb;
+            if (ca) va = make_cigview(B, r0 + a, la_, do_convert && (la_ & BSDC_LINK_CONVERT), (la_ & kLinkRdDev) != 0, do_extend);
+            if (cb) vb = make_cigview(B, r0 + b, lb_, do_convert && (lb_ & BSDC_LINK_CONVERT), (lb_ & kLinkRdDev) != 0, do_extend);
+            for (int32_t p = s0 + t; p <= e0; p += 64) {
+                const int ia = ca ? read_at_ref(va, pa, la, p) : (p - pa < la ? p - pa : -1);
+                const int ib = cb ? read_at_ref(vb, pb, lb, p) : (p - pb < lb ? p - pb : -1);
+                if (ia < 0 || ib < 0) continue;
+                const uint32_t x = bimg[sa + ia], y = bimg[sb + ib];
+                if (x == kN || y == kN) continue;
+                const int qa = qimg[sa + ia], qb = qimg[sb + ib];
+                if (x == y) {
+                    const uint8_t q = (uint8_t)::min(qa + qb, 93);
+                    qimg[sa + ia] = q;
+                    qimg[sb + ib] = q;
+                } else if (qa > qb) {
+                    bimg[sb + ib] = (uint8_t)x;
+                    qimg[sa + ia] = qimg[sb + ib] = (uint8_t)(qa - qb);
+                } else if (qb > qa) {
+                    bimg[sa + ia] = (uint8_t)y;
+                    qimg[sa + ia] = qimg[sb + ib] = (uint8_t)(qb - qa);
+                } else {
+                    bimg[sa + ia] = bimg[sb + ib] = (uint8_t)kN;
+                    qimg[sa + ia] = qimg[sb + ib] = 2;
+                }
+            }
+        }
+        wave_sync();
+    }
+
+    if (stop == 4) return;
+    // ---- source reads: read-through trim, trailing-N trim, strand/end set ----
+    const bool neg = flag & 16;
+    int32_t srclen = 0;
+    uint32_t set = 0xFF;
+    if (usable) {
+        int32_t keep = len;
+        CigView cv;
+        if (cplx) cv = make_cigview(B, r0 + t, link, conv, rd, do_extend);
+        if (link & BSDC_LINK_RT) keep = readthrough_keep(B, r0 + t, flag, pos, len, reflen, cplx, &cv);
+        const uint8_t *sbp = bimg + slot + start;
+        while (keep > 0) {
+            const uint32_t bb = neg ? sbp[len - keep] : sbp[keep - 1];
+            if (bb != kN) break;
+            keep--;
+        }
+        srclen = keep;
+        if (keep > 0) {
+            const bool r1 = flag & 0x40;
+            set = (link & BSDC_LINK_AB) ? (r1 ? 0u : 1u) : (r1 ? 2u : 3u);
+        }
+    }
+
+    // ---- most-common-alignment filter (only families with a non-M-only cigar; serial) ----
+    if (ballot(cplx && set != 0xFF)) {
+        SMeta *meta = reinterpret_cast<SMeta *>(A + Lo.meta);
+        uint8_t *setv = A + Lo.lists;                                      // 64 B scratch
+        uint16_t *ordv = reinterpret_cast<uint16_t *>(A + Lo.lists + 64);  // 64 x u16 scratch
+        if (has) {
+            meta[t].gidx = r0 + t;
+            meta[t].pos = pos;
+            meta[t].link = link;
+            meta[t].len = (uint16_t)len;
+            meta[t].flag = (uint16_t)flag;
+            srcl[t] = (uint16_t)srclen;
+            setv[t] = (uint8_t)set;
+        }
+        wave_sync();
+        if (t == 0) {
+            uint32_t *so = reinterpret_cast<uint32_t *>(A + Lo.simp);
+            uint32_t *sofs = so + cops + 2 * n;
+            uint32_t fill = 0;
+            for (int r = 0; r < n; r++) {
+                sofs[r] = 0;
+                if (setv[r] == 0xFF) continue;
+                const SMeta m = meta[r];
+                const bool mc = m.link & BSDC_LINK_COMPLEX;
+                const bool mconv = do_convert && (m.link & BSDC_LINK_CONVERT);
+                CigView v;
+                if (mc) v = make_cigview(B, m.gidx, m.link, mconv, (m.link & kLinkRdDev) != 0, do_extend);
+                const int c = simplified_cigar(&v, mc, m.flag & 16, srcl[r], so + fill);
+                sofs[r] = fill | ((uint32_t)c << 16);
+                fill += (uint32_t)c;
+            }
+            for (int xy = 0; xy < 2; xy++) {
+                const int s1 = xy == 0 ? 0 : 1, s2 = xy == 0 ? 3 : 2;
+                int cnt = 0;
+                for (int r = 0; r < n; r++)
+                    if (setv[r] == s1) ordv[cnt++] = (uint16_t)r;
+                for (int r = 0; r < n; r++)
+                    if (setv[r] == s2) ordv[cnt++] = (uint16_t)r;
+                filter_group(ordv, cnt, srcl, sofs, so, setv);
+            }
+        }
+        wave_sync();
+        if (has) set = setv[t];
+        wave_sync();
+    }
+
+    // ---- per-set read lists (family order) and consensus lengths ----
+    uint8_t *lists = A + Lo.lists;  // 4 x 64 record indices
+    int cnt[4];
+#pragma unroll
+    for (int s = 0; s < 4; s++) {
+        const uint64_t ms = ballot(set == (uint32_t)s);
+        cnt[s] = __builtin_popcountll(ms);
+        if (set == (uint32_t)s) lists[s * 64 + mbcnt(ms)] = (uint8_t)t;
+    }
+    if (set != 0xFF) atomicMax(&lc[set], (uint32_t)srclen);
+    wave_sync();
+    int lcs[4];
+#pragma unroll
+    for (int s = 0; s < 4; s++) lcs[s] = (int)__builtin_amdgcn_readfirstlane(lc[s]);
+    if (stop == 5) return;
+
+    // ---- single-strand vote + duplex combine, per end; lane = consensus column ----
+    // R1 = AB-R1 + BA-R2, R2 = AB-R2 + BA-R1.  A read's source position c is image byte
+    // sbase + c (forward) or sbase - c (reverse).  Fast path: every read that covers the column
+    // shows the same base (OR of one-hot codes has <= 1 bit) -> the vote is a function of the
+    // likelihood sum alone, looked up exactly (Tables::qlo / dthr).  Columns where reads disagree
+    // are queued and run through the general four-likelihood path once per family.
+    const uint32_t sbase = slot + start + (neg ? (uint32_t)(len - 1) : 0u);
+    const uint32_t desc = sbase | ((uint32_t)srclen << 16) | (neg ? 0x80000000u : 0u);  // srclen < 2^15
+    uint32_t *descs = reinterpret_cast<uint32_t *>(A + Lo.descs);
+    descs[t] = desc;  // published for the queued path (ds_bpermute cannot read inactive lanes)
+    bool hs[4];
+#pragma unroll
+    for (int s = 0; s < 4; s++) hs[s] = cnt[s] > 0;
+    const bool emit = (hs[0] || hs[3]) && (hs[1] || hs[2]);
+    const int32_t stride = P.O.stride;
+    int olen[2];
+#pragma unroll
+    for (int e = 0; e < 2; e++) {
+        const int sa = e == 0 ? 0 : 1, sb = e == 0 ? 3 : 2;
+        olen[e] = (hs[sa] && hs[sb]) ? ::min(lcs[sa], lcs[sb]) : hs[sa] ? lcs[sa] : hs[sb] ? lcs[sb] : 0;
+    }
+    if (emit && stop != 6) {
+        const int ow = Lo.ow;
+        uint8_t *outb = A + Lo.outb;  // [2][ow] duplex bases
+        uint8_t *outq = A + Lo.outq;  // [2][ow] duplex quals
+        uint16_t *sq = reinterpret_cast<uint16_t *>(A + Lo.squeue);
+        int nq = 0;
+        for (int e = 0; e < 2; e++) {
+            const int sa = e == 0 ? 0 : 1, sb = e == 0 ? 3 : 2;
+            const int ol = olen[e];
+            for (int c = t; c < ((ol + 63) & ~63); c += 64) {
+                const bool col = c < ol;
+                uint32_t vb[2] = {0, 0}, vq[2] = {0, 0};
+                bool slow = false;
+#pragma unroll
+                for (int side = 0; side < 2; side++) {
+                    const int s = side == 0 ? sa : sb;
+                    if (!hs[s]) continue;
+                    int32_t dsum = 0;
+                    uint32_t bm = 0;
+                    const int ns = cnt[s];
+                    for (int i = 0; i < ns; i += 2) {  // two reads per iteration, loads in flight together
+                        const int ra = (int)__builtin_amdgcn_readfirstlane(lists[s * 64 + i]);
+                        const bool two = i + 1 < ns;
+                        const int rb = two ? (int)__builtin_amdgcn_readfirstlane(lists[s * 64 + i + 1]) : ra;
+                        const uint32_t da = rlu(desc, ra), db = rlu(desc, rb);
+                        const bool va = col && c < (int)((da >> 16) & 0x7FFF);
+                        const bool vbb = two && col && c < (int)((db >> 16) & 0x7FFF);
+                        const uint32_t ia = (da & 0x80000000u) ? (da & 0xFFFF) - c : (da & 0xFFFF) + c;
+                        const uint32_t ib = (db & 0x80000000u) ? (db & 0xFFFF) - c : (db & 0xFFFF) + c;
+                        uint32_t ba = va ? bimg[ia] : kN, qa = va ? qimg[ia] : 0u;
+                        uint32_t bb = vbb ? bimg[ib] : kN, qb = vbb ? qimg[ib] : 0u;
+                        if (da & 0x80000000u) ba = comp_nt16(ba);
+                        if (db & 0x80000000u) bb = comp_nt16(bb);
+                        const bool oka = is_acgt(ba), okb = is_acgt(bb);
+                        const int32_t xa = lr[qa], xb = lr[qb];
+                        bm |= (oka ? ba : 0u) | (okb ? bb : 0u);
+                        dsum += (oka ? xa : 0) + (okb ? xb : 0);
+                    }
+                    if (__builtin_popcount(bm) > 1 || dsum < 0) {
+                        slow = true;
+                    } else {
+                        const int32_t d = ::min(dsum, (int32_t)((1 << 27) - 1));
+                        const int q0 = qlo[d >> 16];
+                        const int Q = q0 + (d >= dthr[q0 + 1] ? 1 : 0);
+                        vb[side] = Q < 2 ? kN : bm;
+                        vq[side] = Q < 2 ? 2u : (uint32_t)Q;
+                    }
+                }
+                if (col && !slow) {
+                    uint32_t ob, oq;
+                    if (hs[sa] && hs[sb]) {
+                        duplex_col(vb[0], vq[0], vb[1], vq[1], ob, oq);
+                    } else {
+                        ob = hs[sa] ? vb[0] : vb[1];
+                        oq = hs[sa] ? vq[0] : vq[1];
+                    }
+                    outb[e * ow + c] = (uint8_t)ob;
+                    outq[e * ow + c] = (uint8_t)oq;
+                }
+                const uint64_t ms = ballot(col && slow);
+                if (col && slow) sq[nq + mbcnt(ms)] = (uint16_t)((e << 15) | c);
+                nq += __builtin_popcountll(ms);
+            }
+        }
+        // queued columns: the general path (all four likelihoods, up to three exp terms)
+        wave_sync();
+        for (int k0 = 0; k0 < nq; k0 += 64) {
+            const int k = k0 + t;
+            const bool act = k < nq;
+            const uint32_t ent = act ? sq[k] : 0u;
+            const int e = (int)(ent >> 15), c = (int)(ent & 0x7FFF);
+            const int sa = e == 0 ? 0 : 1, sb = e == 0 ? 3 : 2;
+            uint32_t vb[2] = {0, 0}, vq[2] = {0, 0};
+            for (int side = 0; side < 2; side++) {
+                const int s = side == 0 ? sa : sb;  // per lane: lanes of both ends mix here
+                if (!act || !hs[s]) continue;
+                int32_t D0 = 0, D1 = 0, D2 = 0, D3 = 0;
+                for (int i = 0; i < cnt[s]; i++) {
+                    const int r = lists[s * 64 + i];
+                    const uint32_t d = descs[r];
+                    if (c >= (int)((d >> 16) & 0x7FFF)) continue;
+                    const uint32_t idx = (d & 0x80000000u) ? (d & 0xFFFF) - c : (d & 0xFFFF) + c;
+                    uint32_t bb = bimg[idx];
+                    if (d & 0x80000000u) bb = comp_nt16(bb);
+                    const int32_t v = lr[qimg[idx]];
+                    D0 += bb == kA ? v : 0;
+                    D1 += bb == kC ? v : 0;
+                    D2 += bb == kG ? v : 0;
+                    D3 += bb == kT ? v : 0;
+                }
+                int best = 0;
+                int32_t Db = D0;
+                if (D1 > Db) { best = 1; Db = D1; }
+                if (D2 > Db) { best = 2; Db = D2; }
+                if (D3 > Db) { best = 3; Db = D3; }
+                float S = 0.0f;
+                if (best != 0) S += term((long long)D0 - Db);
+                if (best != 1) S += term((long long)D1 - Db);
+                if (best != 2) S += term((long long)D2 - Db);
+                if (best != 3) S += term((long long)D3 - Db);
+                const int Q = phred_of(S, thr);
+                vb[side] = Q < 2 ? kN : (1u << best);
+                vq[side] = Q < 2 ? 2u : (uint32_t)Q;
+            }
+            if (act) {
+                uint32_t ob, oq;
+                if (hs[sa] && hs[sb]) {
+                    duplex_col(vb[0], vq[0], vb[1], vq[1], ob, oq);
+                } else {
+                    ob = hs[sa] ? vb[0] : vb[1];
+                    oq = hs[sa] ? vq[0] : vq[1];
+                }
+                outb[e * ow + c] = (uint8_t)ob;
+                outq[e * ow + c] = (uint8_t)oq;
+            }
+        }
+        wave_sync();
+        // pack and store: lanes 0-31 end 0, lanes 32-63 end 1, 8 columns per lane
+        {
+            const int e = t >> 5;
+            const int ol = olen[e];
+            for (int c0 = 8 * (t & 31); c0 < ol; c0 += 256) {
+                const uint2 bv = *reinterpret_cast<const uint2 *>(outb + e * ow + c0);
+                const uint2 qv = *reinterpret_cast<const uint2 *>(outq + e * ow + c0);
+                uint32_t pk = 0, qlo2 = qv.x, qhi2 = qv.y;
+#pragma unroll
+                for (int k = 0; k < 8; k++) {
+                    uint32_t ob = ((k < 4 ? bv.x : bv.y) >> (8 * (k & 3))) & 0xFF;
+                    if (c0 + k >= ol) {
+                        ob = 0;
+                        if (k < 4)
+                            qlo2 &= ~(0xFFu << (8 * k));
+                        else
+                            qhi2 &= ~(0xFFu << (8 * (k - 4)));
+                    }
+                    pk |= ob << (8 * (k >> 1) + ((k & 1) ? 0 : 4));
+                }
+                const int64_t so = (2 * (int64_t)fam + e) * stride;
+                *reinterpret_cast<uint32_t *>(P.O.seq + so / 2 + c0 / 2) = pk;
+                *reinterpret_cast<uint2 *>(P.O.qual + so + c0) = make_uint2(qlo2, qhi2);
+            }
+        }
+    }
+    if (t == 0) {
+        uint8_t st = emit ? 1 : 0;
+        if (hs[0] || hs[1]) st |= 2;
+        if (hs[2] || hs[3]) st |= 4;
+        P.O.status[fam] = st;
+        P.O.len[2 * fam] = (uint16_t)(emit ? olen[0] : 0);
+        P.O.len[2 * fam + 1] = (uint16_t)(emit ? olen[1] : 0);
+    }
+}
+
+// ==========================================================================================
+// k_large: one 256-thread workgroup per family (arena in LDS or in HBM scratch)
+// ==========================================================================================
+struct RecMeta {  // 48 B, one per record of the family, in the arena
+    int32_t pos;     // current leftmost position
+    int32_t len;     // current length
+    uint32_t slot;   // arena offset of the base slot (quals at slot + cap)
+    int32_t cap;     // slot capacity (input length + 2)
+    int32_t start;   // index of the first base inside the slot
+    uint32_t link;
+    uint32_t gidx;   // global record index
+    uint32_t win;    // converted: reference window start nibble
+    int32_t srclen;  // source-read length
+    int32_t reflen;  // current reference length
+    uint16_t flag;
+    uint8_t rd;
+    uint8_t set;     // 0 AB-R1, 1 AB-R2, 2 BA-R1, 3 BA-R2, 0xFF none
+    int32_t in_len;
+};
+static_assert(sizeof(RecMeta) == 48, "RecMeta layout");
+
+// Arena layout of one large family (offsets from the arena base).
+struct ArenaLayout {
+    uint32_t meta, lists, ssb, ssq, simp, slots, total;
+    int32_t ssw;
+    __host__ __device__ ArenaLayout(int n, int64_t slot_bytes, int max_len, int64_t complex_ops) {
+        ssw = (int32_t)round16(max_len + 2);
+        int64_t o = 0;
+        meta = (uint32_t)o;
+        o += round16((int64_t)n * (int64_t)sizeof(RecMeta));
+        lists = (uint32_t)o;
+        o += round16((int64_t)n * 8);
+        ssb = (uint32_t)o;
+        o += 4 * (int64_t)ssw;
+        ssq = (uint32_t)o;
+        o += 4 * (int64_t)ssw;
+        simp = (uint32_t)o;
+        if (complex_ops > 0) o += round16(4 * (complex_ops + 4 * (int64_t)n));
+        slots = (uint32_t)o;
+        o += round16(slot_bytes);
+        total = (uint32_t)o;
+    }
+};
+
+__device__ __forceinline__ int block_sum(int v, int *red) {
+#pragma unroll
+    for (int o = 32; o >= 1; o >>= 1) v += __shfl_xor(v, o, kWave);
+    __syncthreads();
+    if ((threadIdx.x & 63) == 0) red[threadIdx.x >> 6] = v;
+    __syncthreads();
+    int s = 0;
+    for (int w = 0; w < kLargeThreads / kWave; w++) s += red[w];
+    __syncthreads();
+    return s;
+}
+__device__ __forceinline__ int block_max(int v, int *red) {
+#pragma unroll
+    for (int o = 32; o >= 1; o >>= 1) v = ::max(v, __shfl_xor(v, o, kWave));
+    __syncthreads();
+    if ((threadIdx.x & 63) == 0) red[threadIdx.x >> 6] = v;
+    __syncthreads();
+    int s = red[0];
+    for (int w = 1; w < kLargeThreads / kWave; w++) s = ::max(s, red[w]);
+    __syncthreads();
+    return s;
+}
+
+__device__ void process_large(const KParams &P, uint8_t *A, const int32_t *lr, const float *thr, uint32_t fam, int *red,
+                              int *s_cnt, int *s_lc) {
+    constexpr int G = kLargeThreads;
+    const int tt = threadIdx.x;
+    const bsdc_family_batch &B = P.B;
+    const uint32_t r0 = B.fam_off[fam];
+    const int n = (int)(B.fam_off[fam + 1] - r0);
+    const bool do_convert = P.mode & BSDC_MODE_CONVERT;
+    const bool do_extend = P.mode & BSDC_MODE_EXTEND;
+    const bool do_vote = P.mode & BSDC_MODE_VOTE;
+    const uint4 *REC = reinterpret_cast<const uint4 *>(B.rec);
+    const uint32_t off0 = n > 0 ? REC[r0].x : 0u;
+
+    int c = 0, ml = 0;
+    for (int r = tt; r < n; r += G) {
+        const uint4 rc = REC[r0 + r];
+        if (rc.w & BSDC_LINK_COMPLEX) c += (int)(B.cig_info[r0 + r] & 0xFFFF);
+        ml = ::max(ml, (int)(rc.z & 0xFFFF));
+    }
+    const int cops = block_sum(c, red);
+    const int maxlen_f = block_max(ml, red);
+    const ArenaLayout Lo(n, 0, maxlen_f, cops);
+    RecMeta *M = reinterpret_cast<RecMeta *>(A + Lo.meta);
+    uint16_t *lists = reinterpret_cast<uint16_t *>(A + Lo.lists);
+    uint8_t *ssb = A + Lo.ssb;
+    uint8_t *ssq = A + Lo.ssq;
+    uint32_t *simp = reinterpret_cast<uint32_t *>(A + Lo.simp);
+    uint8_t *slots = A + Lo.slots;
+    const int ssw = Lo.ssw;
+
+    // ---- record metadata ----
+    for (int r = tt; r < n; r += G) {
         const uint32_t gi = r0 + r;
-        const uint32_t lf = B.rec_lenflag[gi];
+        const uint4 rc = REC[gi];
         RecMeta m;
-        m.in_len = (int32_t)(lf & 0xFFFF);
-        m.flag = (uint16_t)(lf >> 16);
-        m.pos = B.rec_pos[gi];
+        m.in_len = (int32_t)(rc.z & 0xFFFF);
+        m.flag = (uint16_t)(rc.z >> 16);
+        m.pos = (int32_t)rc.y;
         m.len = m.in_len;
         m.cap = m.in_len + 2;
-        m.slot = 2u * (B.rec_off[gi] - off0) + 4u * (uint32_t)r;
+        m.slot = 2u * (rc.x - off0);
         m.start = 1;
-        m.link = B.rec_link[gi];
+        m.link = rc.w;
         m.gidx = gi;
-        m.tid = B.rec_tid[gi];
+        m.win = (do_convert && (m.link & BSDC_LINK_CONVERT)) ? B.rec_win[2 * (size_t)gi] : 0u;
         m.srclen = 0;
         m.reflen = (m.link & BSDC_LINK_COMPLEX) ? (int32_t)(B.cig_info[gi] >> 16) : m.in_len;
         m.rd = 0;
         m.set = 0xFF;
         M[r] = m;
     }
-    g.sync();
+    __syncthreads();
 
-    // ---- phase 1: stage bases + tool-1 conversion (tools/1.convert_AG_to_CT.py:84-183) ----
+    // ---- stage bases + tool-1 conversion ----
     for (int r = 0; r < n; r++) {
         const RecMeta m = M[r];
         const int32_t Lin = m.in_len;
-        const int64_t ib = (int64_t)B.rec_off[m.gidx];
+        const int64_t ib = (int64_t)B.rec[4 * (size_t)m.gidx] + 1;  // the record's first base
         uint8_t *sb = slots + m.slot;
         uint8_t *sq = sb + m.cap;
         if (do_convert && (m.link & BSDC_LINK_CONVERT)) {
-            const int32_t Lm = Lin + 1;                       // 'N' + seq
-            const int32_t np = m.pos - 1 > 0 ? m.pos - 1 : 0; // :92
-            for (int j = g.t; j < Lm; j += G) {
-                const uint8_t f0 = ref_at(P.R, m.tid, (int64_t)np + j);
-                const uint8_t f1 = ref_at(P.R, m.tid, (int64_t)np + j + 1);
-                const uint8_t m0 = j == 0 ? f0 : nib(B.seq, ib + j - 1);  // :121 seed
+            const int32_t Lm = Lin + 1;
+            const int32_t np = m.pos - 1 > 0 ? m.pos - 1 : 0;
+            const int32_t avail = (int32_t)B.rec_win[2 * (size_t)m.gidx + 1];
+            for (int j = tt; j < Lm; j += G) {
+                const uint32_t f0 = j < avail ? nib(P.ref, (int64_t)m.win + j) : kN;
+                const uint32_t f1 = j + 1 < avail ? nib(P.ref, (int64_t)m.win + j + 1) : kN;
+                const uint32_t m0 = j == 0 ? f0 : nib(B.seq, ib + j - 1);
                 const bool has_next = j + 1 < Lm;
-                const uint8_t m1 = has_next ? nib(B.seq, ib + j) : kN;
-                const uint8_t o = convert_rule(m0, m1, has_next, f0, f1);
-                sb[j] = o;
-                sq[j] = j == 0 ? (uint8_t)40 : B.qual[ib + j - 1];     // :174-177 'I' + quals
+                const uint32_t m1 = has_next ? nib(B.seq, ib + j) : kN;
+                const uint32_t o = convert_rule(m0, m1, has_next, f0, f1);
+                sb[j] = (uint8_t)o;
+                sq[j] = j == 0 ? (uint8_t)40 : B.qual[ib + j - 1];
                 if (j == Lm - 1) {
-                    // :157-170 trailing C before a reference G is trimmed
-                    const uint8_t f2 = ref_at(P.R, m.tid, (int64_t)np + Lm);
-                    const uint8_t rd = (f2 == kG && o == kC) ? 1 : 0;
+                    const uint32_t f2 = Lm < avail ? nib(P.ref, (int64_t)m.win + Lm) : kN;
+                    const uint8_t rdv = (f2 == kG && o == kC) ? 1 : 0;
                     RecMeta &w = M[r];
-                    w.rd = rd;
-                    w.len = Lm - rd;
+                    w.rd = rdv;
+                    w.len = Lm - rdv;
                     w.start = 0;
                     w.pos = np;
-                    w.reflen = m.reflen + 1 - ((rd && m.reflen > 0) ? 1 : 0);
+                    w.reflen = m.reflen + 1 - ((rdv && m.reflen > 0) ? 1 : 0);
                 }
             }
         } else {
-            for (int j = g.t; j < Lin; j += G) {
-                sb[1 + j] = nib(B.seq, ib + j);
+            for (int j = tt; j < Lin; j += G) {
+                sb[1 + j] = (uint8_t)nib(B.seq, ib + j);
                 sq[1 + j] = B.qual[ib + j];
             }
         }
     }
-    g.sync();
-
-    // ---- phase 2: gap extension of 4-record groups (tools/2.extend_gap.py:58-110) ----
-    if (do_extend) {
-        for (int r = g.t; r < n; r += G) {
-            const RecMeta m = M[r];
-            const int p = (int)((m.link >> BSDC_LINK_PARTNER_SHIFT) & 3u);
-            const RecMeta pm = M[p];
-            const uint8_t *pb = slots + pm.slot;
-            const uint8_t *pq = pb + pm.cap;
-            if (m.link & BSDC_LINK_EXT_RIGHT) {
-                // :70-80 the converted partner's first base / qual, POS-1, [(M,1)] + cigar
-                // the partner is converted (start 0 when converted in this launch, else 1); its
-                // first base is never touched by its own append (length >= 1)
-                const int ps = (do_convert && (pm.link & BSDC_LINK_CONVERT)) ? 0 : 1;
-                uint8_t *sb = slots + m.slot;
-                sb[0] = pb[ps];
-                sb[m.cap] = pq[ps];
-                RecMeta &w = M[r];
-                w.start = 0;
-                w.len = m.len + 1;
-                w.pos = m.pos - 1;
-                w.reflen = m.reflen + 1;
-            }
-        }
-        g.sync();
-        for (int r = g.t; r < n; r += G) {
-            const RecMeta m = M[r];
-            const int p = (int)((m.link >> BSDC_LINK_PARTNER_SHIFT) & 3u);
-            const bool rd = (do_convert && (m.link & BSDC_LINK_CONVERT)) ? (m.rd != 0) : ((m.link & BSDC_LINK_RD_IN) != 0);
-            if ((m.link & BSDC_LINK_EXT_LEFT) && rd) {
-                // :92-101 the partner's last base / qual (after its prepend), cigar + [(M,1)]
-                const RecMeta pm = M[p];
-                const uint8_t *pb = slots + pm.slot;
-                uint8_t *sb = slots + m.slot;
-                const int li = pm.start + pm.len - 1;
-                sb[m.start + m.len] = pb[li];
-                sb[m.cap + m.start + m.len] = pb[pm.cap + li];
-                RecMeta &w = M[r];
-                w.len = m.len + 1;
-                w.reflen = m.reflen + 1;
-            }
-        }
-        g.sync();
+    __syncthreads();
+    if (!do_convert) {
+        for (int r = tt; r < n; r += G)
+            if (M[r].link & BSDC_LINK_RD_IN) M[r].rd = 1;
+        __syncthreads();
     }
 
-    // ---- stage dump: the records as tool 2 writes them ----
+    // ---- gap extension ----
+    if (do_extend) {
+        for (int r = tt; r < n; r += G) {
+            const RecMeta m = M[r];
+            if (!(m.link & BSDC_LINK_EXT_RIGHT)) continue;
+            const int p = (int)((m.link >> BSDC_LINK_PARTNER_SHIFT) & 3u);
+            const RecMeta pm = M[p];
+            uint8_t *sb = slots + m.slot;
+            sb[0] = slots[pm.slot + pm.start];
+            sb[m.cap] = slots[pm.slot + pm.cap + pm.start];
+            RecMeta &w = M[r];
+            w.start = 0;
+            w.len = m.len + 1;
+            w.pos = m.pos - 1;
+            w.reflen = m.reflen + 1;
+        }
+        __syncthreads();
+        for (int r = tt; r < n; r += G) {
+            const RecMeta m = M[r];
+            if (!((m.link & BSDC_LINK_EXT_LEFT) && m.rd)) continue;
+            const int p = (int)((m.link >> BSDC_LINK_PARTNER_SHIFT) & 3u);
+            const RecMeta pm = M[p];
+            uint8_t *sb = slots + m.slot;
+            const int li = pm.start + pm.len - 1;
+            sb[m.start + m.len] = slots[pm.slot + li];
+            sb[m.cap + m.start + m.len] = slots[pm.slot + pm.cap + li];
+            RecMeta &w = M[r];
+            w.len = m.len + 1;
+            w.reflen = m.reflen + 1;
+        }
+        __syncthreads();
+    }
+
     if (P.mode & BSDC_MODE_DUMP) {
         for (int r = 0; r < n; r++) {
             const RecMeta m = M[r];
-            const int64_t d = (int64_t)B.rec_off[m.gidx] + 2 * (int64_t)m.gidx;
+            const int64_t d = (int64_t)B.rec[4 * (size_t)m.gidx];
             const uint8_t *sb = slots + m.slot + m.start;
-            for (int j = g.t; j < m.len; j += G) {
+            for (int j = tt; j < m.len; j += G) {
                 P.O.dump_seq[d + j] = sb[j];
                 P.O.dump_qual[d + j] = sb[m.cap + j];
             }
-            if (g.t == 0) {
+            if (tt == 0) {
                 P.O.dump_pos[m.gidx] = m.pos;
                 P.O.dump_len[m.gidx] = (uint16_t)m.len;
                 const bool conv = do_convert && (m.link & BSDC_LINK_CONVERT);
-                const bool rd = conv ? (m.rd != 0) : ((m.link & BSDC_LINK_RD_IN) != 0);
                 uint8_t tg = 0;
-                if (rd) tg |= 1;
+                if (m.rd) tg |= 1;
                 if (conv) tg |= 2 | 4;
                 if (do_extend && (m.link & BSDC_LINK_EXT_RIGHT)) tg |= 4;
-                if (do_extend && (m.link & BSDC_LINK_EXT_LEFT) && rd) tg |= 8;
+                if (do_extend && (m.link & BSDC_LINK_EXT_LEFT) && m.rd) tg |= 8;
                 P.O.dump_tags[m.gidx] = tg;
             }
         }
     }
     if (!do_vote) return;
 
-    // complex-cigar view of record r in its current state
-    auto cigview = [&](const RecMeta &m) {
-        CigView c;
-        c.ops = B.cigar + B.cig_off[m.gidx];
-        c.n = (int)(B.cig_info[m.gidx] & 0xFFFF);
-        const bool conv = do_convert && (m.link & BSDC_LINK_CONVERT);
-        const bool rd = conv ? (m.rd != 0) : ((m.link & BSDC_LINK_RD_IN) != 0);
-        c.npre = (conv || (do_extend && (m.link & BSDC_LINK_EXT_RIGHT))) ? 1 : 0;
-        c.nsuf = (do_extend && (m.link & BSDC_LINK_EXT_LEFT) && rd) ? 1 : 0;
-        c.rdtrim = (conv && rd) ? 1 : 0;
-        return c;
+    auto cigv = [&](const RecMeta &m) {
+        return make_cigview(B, m.gidx, m.link, do_convert && (m.link & BSDC_LINK_CONVERT), m.rd != 0, do_extend);
     };
 
-    // ---- phase 3: overlapping-bases consensus, per template ----
+    // ---- overlapping-bases consensus ----
     if (P.overlap) {
         for (int r = 0; r < n; r++) {
             const RecMeta a = M[r];
             const uint32_t mate = a.link & BSDC_LINK_MATE_MASK;
             if (mate == BSDC_LINK_MATE_MASK || !(a.link & BSDC_LINK_USABLE)) continue;
             const RecMeta b = M[mate];
-            if (!(b.link & BSDC_LINK_USABLE)) continue;
-            if ((a.flag & 4) || (b.flag & 4) || a.tid != b.tid) continue;
+            if (!(b.link & BSDC_LINK_USABLE) || (a.flag & 4) || (b.flag & 4)) continue;
             if (a.reflen <= 0 || b.reflen <= 0) continue;
             const int32_t s = ::max(a.pos, b.pos);
             const int32_t e = ::min(a.pos + a.reflen - 1, b.pos + b.reflen - 1);
             if (s > e) continue;
             const bool ca = a.link & BSDC_LINK_COMPLEX, cb = b.link & BSDC_LINK_COMPLEX;
+            CigView va, vb;
+            if (ca) va = cigv(a);
+            if (cb) vb = cigv(b);
             uint8_t *ab = slots + a.slot + a.start;
             uint8_t *aq = slots + a.slot + a.cap + a.start;
             uint8_t *bb = slots + b.slot + b.start;
             uint8_t *bq = slots + b.slot + b.cap + b.start;
-            for (int32_t p = s + g.t; p <= e; p += G) {
-                const int ia = ca ? read_at_ref(cigview(a), a.pos, a.len, p) : (p - a.pos < a.len ? p - a.pos : -1);
-                const int ibb = cb ? read_at_ref(cigview(b), b.pos, b.len, p) : (p - b.pos < b.len ? p - b.pos : -1);
+            for (int32_t p = s + tt; p <= e; p += G) {
+                const int ia = ca ? read_at_ref(va, a.pos, a.len, p) : (p - a.pos < a.len ? p - a.pos : -1);
+                const int ibb = cb ? read_at_ref(vb, b.pos, b.len, p) : (p - b.pos < b.len ? p - b.pos : -1);
                 if (ia < 0 || ibb < 0) continue;
-                const uint8_t x = ab[ia], y = bb[ibb];
+                const uint32_t x = ab[ia], y = bb[ibb];
                 if (x == kN || y == kN) continue;
                 const int qa = aq[ia], qb = bq[ibb];
                 if (x == y) {
@@ -460,257 +1235,122 @@ __device__ void process_family(const KParams &P, const Grp<G> &g, uint8_t *A, co
                     aq[ia] = q;
                     bq[ibb] = q;
                 } else if (qa > qb) {
-                    bb[ibb] = x;
+                    bb[ibb] = (uint8_t)x;
                     aq[ia] = bq[ibb] = (uint8_t)(qa - qb);
                 } else if (qb > qa) {
-                    ab[ia] = y;
+                    ab[ia] = (uint8_t)y;
                     aq[ia] = bq[ibb] = (uint8_t)(qb - qa);
                 } else {
-                    ab[ia] = bb[ibb] = kN;
+                    ab[ia] = bb[ibb] = (uint8_t)kN;
                     aq[ia] = bq[ibb] = 2;
                 }
             }
         }
-        g.sync();
+        __syncthreads();
     }
 
-    // ---- phase 4: source reads (orientation, read-through trim, trailing-N trim) ----
-    for (int r = g.t; r < n; r += G) {
+    // ---- source reads ----
+    for (int r = tt; r < n; r += G) {
         RecMeta &m = M[r];
         if (!(m.link & BSDC_LINK_USABLE)) continue;
-        const bool neg = m.flag & 16;
+        const bool negr = m.flag & 16;
         int32_t keep = m.len;
-        if (m.link & BSDC_LINK_RT) {
-            const int32_t *rt = B.rt + 4 * (int64_t)m.gidx;
-            const int32_t next_pos = rt[0], tlen = rt[1], mate_us = rt[2], mate_ue = rt[3];
-            // fgbio isFrPair (htsjdk getPairOrientation == FR); RT is only set on records that are
-            // paired, mapped, mate mapped, on the mate's contig and carry an MC tag
-            const bool mneg = m.flag & 32;
-            bool fr = false;
-            if (neg != mneg) {
-                const int64_t posfive = neg ? (int64_t)next_pos : (int64_t)m.pos;
-                const int64_t negfive = neg ? (int64_t)m.pos + m.reflen - 1 : (int64_t)m.pos + tlen;
-                fr = posfive < negfive;
-            }
-            if (fr) {
-                const bool cx = m.link & BSDC_LINK_COMPLEX;
-                if (!neg) {
-                    const int64_t end = (int64_t)m.pos + m.reflen - 1;
-                    if (end > mate_ue) {
-                        int32_t kk;
-                        if (!cx) {
-                            kk = (int32_t)::min<int64_t>((int64_t)mate_ue - m.pos + 1, m.len);
-                            if (kk < 0) kk = 0;
-                        } else {
-                            int last = -1;
-                            const CigView c = cigview(m);
-                            for (int64_t p = m.pos; p <= mate_ue && p < (int64_t)m.pos + m.reflen; p++) {
-                                const int q = read_at_ref(c, m.pos, m.len, p);
-                                if (q >= 0) last = q;
-                            }
-                            kk = last + 1;
-                        }
-                        keep = ::min(keep, kk);
-                    }
-                } else {
-                    if ((int64_t)m.pos < mate_us) {
-                        int32_t kk;
-                        if (!cx) {
-                            const int64_t first = (int64_t)mate_us - m.pos;
-                            kk = first >= m.len ? 0 : (int32_t)(m.len - first);
-                        } else {
-                            int first = m.len;
-                            const CigView c = cigview(m);
-                            for (int64_t p = (int64_t)m.pos + m.reflen - 1; p >= mate_us && p >= m.pos; p--) {
-                                const int q = read_at_ref(c, m.pos, m.len, p);
-                                if (q >= 0) first = q;
-                            }
-                            kk = m.len - first;
-                        }
-                        keep = ::min(keep, kk);
-                    }
-                }
-            }
-        }
+        const bool cx = m.link & BSDC_LINK_COMPLEX;
+        CigView cv;
+        if (cx) cv = cigv(m);
+        if (m.link & BSDC_LINK_RT) keep = readthrough_keep(B, m.gidx, m.flag, m.pos, m.len, m.reflen, cx, &cv);
         const uint8_t *sb = slots + m.slot + m.start;
         while (keep > 0) {
-            const uint8_t b = neg ? sb[m.len - keep] : sb[keep - 1];
+            const uint32_t b = negr ? sb[m.len - keep] : sb[keep - 1];
             if (b != kN) break;
             keep--;
         }
         m.srclen = keep;
         if (keep > 0) {
             const bool r1 = m.flag & 0x40;
-            const bool ab = m.link & BSDC_LINK_AB;
-            m.set = ab ? (r1 ? 0 : 1) : (r1 ? 2 : 3);
+            const bool abs_ = m.link & BSDC_LINK_AB;
+            m.set = abs_ ? (r1 ? 0 : 1) : (r1 ? 2 : 3);
         }
     }
-    g.sync();
+    __syncthreads();
 
-    // ---- phase 5: most-common-alignment filter (only families with a non-M-only cigar) ----
-    int has_complex = 0;
-    for (int r = g.t; r < n; r += G) has_complex |= (M[r].link & BSDC_LINK_COMPLEX) && M[r].set != 0xFF;
-    if (g.any(has_complex)) {
-        if (g.t == 0) {
-            // simplified cigars (sequencing orientation, M/=/X -> M, merged, truncated)
-            uint32_t *so = simp;                 // ops
-            uint32_t *sofs = simp + cops + 2 * n; // per record: offset | count << 16 (n entries)
+    // ---- most-common-alignment filter ----
+    int hc = 0;
+    for (int r = tt; r < n; r += G) hc |= (M[r].link & BSDC_LINK_COMPLEX) && M[r].set != 0xFF;
+    if (block_max(hc, red)) {
+        if (tt == 0) {
+            uint32_t *so = simp;
+            uint32_t *sofs = simp + cops + 2 * n;
+            uint16_t *srcl = reinterpret_cast<uint16_t *>(simp + cops + 3 * n);  // n u16 in the last n words
+            uint8_t *setv = reinterpret_cast<uint8_t *>(srcl + n);               // ... and n bytes after them
             uint32_t fill = 0;
             for (int r = 0; r < n; r++) {
-                const RecMeta &m = M[r];
                 sofs[r] = 0;
-                if (m.set == 0xFF) continue;
-                const uint32_t base = fill;
-                int cnt = 0;
-                if (!(m.link & BSDC_LINK_COMPLEX)) {
-                    so[fill++] = ((uint32_t)m.srclen << 4) | 0u;
-                    cnt = 1;
-                } else {
-                    const CigView c = cigview(m);
-                    const bool neg = m.flag & 16;
-                    const int tot = c.count();
-                    int32_t q = 0;
-                    for (int j = 0; j < tot && q < m.srclen; j++) {
-                        const int k = neg ? tot - 1 - j : j;
-                        int op;
-                        int32_t l;
-                        c.at(k, op, l);
-                        if (l <= 0) continue;
-                        if (op == 7 || op == 8) op = 0;
-                        if (op == 4 || op == 5) continue;
-                        if (op == 0 || op == 1) {
-                            if (q + l > m.srclen) l = m.srclen - q;
-                            q += l;
-                        }
-                        if (cnt > 0 && (int)(so[fill - 1] & 0xF) == op) {
-                            so[fill - 1] = ((((so[fill - 1] >> 4) + (uint32_t)l)) << 4) | (uint32_t)op;
-                        } else {
-                            so[fill++] = ((uint32_t)l << 4) | (uint32_t)op;
-                            cnt++;
-                        }
-                    }
-                }
-                sofs[r] = base | ((uint32_t)cnt << 16);
+                srcl[r] = (uint16_t)M[r].srclen;
+                setv[r] = M[r].set;
+                if (M[r].set == 0xFF) continue;
+                const RecMeta &m = M[r];
+                const bool mc = m.link & BSDC_LINK_COMPLEX;
+                CigView v;
+                if (mc) v = cigv(m);
+                const int c2 = simplified_cigar(&v, mc, m.flag & 16, m.srclen, so + fill);
+                sofs[r] = fill | ((uint32_t)c2 << 16);
+                fill += (uint32_t)c2;
             }
-            // X = {AB-R1, BA-R2} (sets 0, 3), Y = {AB-R2, BA-R1} (sets 1, 2); AB records first
-            uint16_t *ord = lists;  // scratch: n entries
-            uint8_t *member = ssb;  // scratch bitmap rows are too big in general: use group ids
-            (void)member;
             for (int xy = 0; xy < 2; xy++) {
-                const int sa = xy == 0 ? 0 : 1, sbb = xy == 0 ? 3 : 2;
+                const int s1 = xy == 0 ? 0 : 1, s2 = xy == 0 ? 3 : 2;
                 int cnt = 0;
                 for (int r = 0; r < n; r++)
-                    if (M[r].set == sa) ord[cnt++] = (uint16_t)r;
+                    if (setv[r] == s1) lists[cnt++] = (uint16_t)r;
                 for (int r = 0; r < n; r++)
-                    if (M[r].set == sbb) ord[cnt++] = (uint16_t)r;
-                if (cnt < 2) continue;
-                // stable sort by srclen descending
-                for (int i = 1; i < cnt; i++) {
-                    const uint16_t x = ord[i];
-                    int j = i - 1;
-                    while (j >= 0 && M[ord[j]].srclen < M[x].srclen) {
-                        ord[j + 1] = ord[j];
-                        j--;
-                    }
-                    ord[j + 1] = x;
-                }
-                // groups: defining read + size; membership recomputed for the winner below
-                int ng = 0;
-                uint16_t gdef[64];
-                int gsize[64];
-                bool overflow = false;
-                for (int i = 0; i < cnt; i++) {
-                    const uint32_t ai = sofs[ord[i]];
-                    const uint32_t *ac = so + (ai & 0xFFFF);
-                    const int an = (int)(ai >> 16);
-                    bool found = false;
-                    for (int gi = 0; gi < ng; gi++) {
-                        const uint32_t bi = sofs[gdef[gi]];
-                        const uint32_t *bc = so + (bi & 0xFFFF);
-                        const int bn = (int)(bi >> 16);
-                        bool pre = an <= bn;
-                        for (int k = 0; pre && k < an - 1; k++) pre = ac[k] == bc[k];
-                        if (pre && an > 0) pre = (ac[an - 1] & 0xF) == (bc[an - 1] & 0xF) && (ac[an - 1] >> 4) <= (bc[an - 1] >> 4);
-                        if (pre) {
-                            gsize[gi]++;
-                            found = true;
-                        }
-                    }
-                    if (!found) {
-                        if (ng < 64) {
-                            gdef[ng] = ord[i];
-                            gsize[ng] = 1;
-                            ng++;
-                        } else {
-                            overflow = true;
-                        }
-                    }
-                }
-                (void)overflow;
-                if (ng <= 1) continue;
-                int best = 0;
-                for (int gi = 1; gi < ng; gi++)
-                    if (gsize[gi] > gsize[best]) best = gi;
-                const uint32_t bi = sofs[gdef[best]];
-                const uint32_t *bc = so + (bi & 0xFFFF);
-                const int bn = (int)(bi >> 16);
-                for (int i = 0; i < cnt; i++) {
-                    const uint32_t ai = sofs[ord[i]];
-                    const uint32_t *ac = so + (ai & 0xFFFF);
-                    const int an = (int)(ai >> 16);
-                    bool pre = an <= bn;
-                    for (int k = 0; pre && k < an - 1; k++) pre = ac[k] == bc[k];
-                    if (pre && an > 0) pre = (ac[an - 1] & 0xF) == (bc[an - 1] & 0xF) && (ac[an - 1] >> 4) <= (bc[an - 1] >> 4);
-                    if (!pre) M[ord[i]].set = 0xFF;
-                }
+                    if (setv[r] == s2) lists[cnt++] = (uint16_t)r;
+                filter_group(lists, cnt, srcl, sofs, so, setv);
             }
+            for (int r = 0; r < n; r++) M[r].set = setv[r];
         }
-        g.sync();
+        __syncthreads();
     }
 
-    // ---- phase 6a: per-set read lists (family order) and consensus lengths ----
-    __shared__ int s_cnt[kLargeThreads / kWave > kSmallWaves ? kLargeThreads / kWave : kSmallWaves][4];
-    __shared__ int s_lc[kLargeThreads / kWave > kSmallWaves ? kLargeThreads / kWave : kSmallWaves][4];
-    const int wslot = G == kWave ? (int)(threadIdx.x >> 6) : 0;
-    if (g.t == 0) {
-        int cnt[4] = {0, 0, 0, 0}, lc[4] = {0, 0, 0, 0};
+    // ---- lists and consensus lengths ----
+    if (tt == 0) {
+        int cnt[4] = {0, 0, 0, 0}, lcv[4] = {0, 0, 0, 0};
         for (int r = 0; r < n; r++) {
             const int s = M[r].set;
             if (s == 0xFF) continue;
             lists[s * n + cnt[s]++] = (uint16_t)r;
-            lc[s] = ::max(lc[s], M[r].srclen);
+            lcv[s] = ::max(lcv[s], M[r].srclen);
         }
         for (int s = 0; s < 4; s++) {
-            s_cnt[wslot][s] = cnt[s];
-            s_lc[wslot][s] = lc[s];
+            s_cnt[s] = cnt[s];
+            s_lc[s] = lcv[s];
         }
     }
-    g.sync();
-    int cnt[4], lc[4];
+    __syncthreads();
+    int cnt[4], lcv[4];
     for (int s = 0; s < 4; s++) {
-        cnt[s] = s_cnt[wslot][s];
-        lc[s] = s_lc[wslot][s];
+        cnt[s] = s_cnt[s];
+        lcv[s] = s_lc[s];
     }
-    g.sync();
+    __syncthreads();
 
-    // ---- phase 6b: single-strand vote, lane = (set, column) ----
-    const int tot = lc[0] + lc[1] + lc[2] + lc[3];
-    for (int k = g.t; k < tot; k += G) {
-        int s = 0, c = k;
-        while (c >= lc[s]) {
-            c -= lc[s];
+    // ---- single-strand vote (int64 sums: sets can exceed 250 reads) ----
+    const int tot = lcv[0] + lcv[1] + lcv[2] + lcv[3];
+    for (int k = tt; k < tot; k += G) {
+        int s = 0, col = k;
+        while (col >= lcv[s]) {
+            col -= lcv[s];
             s++;
         }
         long long D0 = 0, D1 = 0, D2 = 0, D3 = 0;
         const uint16_t *lst = lists + s * n;
         for (int i = 0; i < cnt[s]; i++) {
             const RecMeta &m = M[lst[i]];
-            if (c >= m.srclen) continue;
-            const bool neg = m.flag & 16;
-            const int j = neg ? m.len - 1 - c : c;
-            uint8_t b = slots[m.slot + m.start + j];
-            const uint8_t q = slots[m.slot + m.cap + m.start + j];
-            if (neg) b = comp_nt16(b);
+            if (col >= m.srclen) continue;
+            const bool negr = m.flag & 16;
+            const int j = negr ? m.len - 1 - col : col;
+            uint32_t b = slots[m.slot + m.start + j];
+            const uint32_t q = slots[m.slot + m.cap + m.start + j];
+            if (negr) b = comp_nt16(b);
             const long long v = lr[q];
             D0 += b == kA ? v : 0;
             D1 += b == kC ? v : 0;
@@ -722,135 +1362,75 @@ __device__ void process_family(const KParams &P, const Grp<G> &g, uint8_t *A, co
         if (D1 > Db) { best = 1; Db = D1; }
         if (D2 > Db) { best = 2; Db = D2; }
         if (D3 > Db) { best = 3; Db = D3; }
-        const long long Ds[4] = {D0, D1, D2, D3};
         float S = 0.0f;
-#pragma unroll
-        for (int b = 0; b < 4; b++) {
-            if (b == best) continue;
-            const float x = (float)((double)(Ds[b] - Db) * kLrInvScale);
-            if (x < -80.0f) continue;
-            S += det_expf(x);
-        }
-        // Q = max k with S <= thr[k] (thr non-increasing), binary search over 1..93
-        int lo = 0, hi = 93;
-        while (lo < hi) {
-            const int mid = (lo + hi + 1) >> 1;
-            if (S <= thr[mid])
-                lo = mid;
-            else
-                hi = mid - 1;
-        }
-        const int Q = lo;
-        ssb[s * ssw + c] = Q < 2 ? kN : (uint8_t)(1u << best);
-        ssq[s * ssw + c] = Q < 2 ? (uint8_t)2 : (uint8_t)Q;
+        if (best != 0) S += term(D0 - Db);
+        if (best != 1) S += term(D1 - Db);
+        if (best != 2) S += term(D2 - Db);
+        if (best != 3) S += term(D3 - Db);
+        const int Q = phred_of(S, thr);
+        ssb[s * ssw + col] = Q < 2 ? (uint8_t)kN : (uint8_t)(1u << best);
+        ssq[s * ssw + col] = Q < 2 ? (uint8_t)2 : (uint8_t)Q;
     }
-    g.sync();
+    __syncthreads();
 
-    // ---- phase 7: duplex combine and output (R1 = AB-R1 + BA-R2, R2 = AB-R2 + BA-R1) ----
-    const bool has[4] = {cnt[0] > 0 && lc[0] > 0, cnt[1] > 0 && lc[1] > 0, cnt[2] > 0 && lc[2] > 0, cnt[3] > 0 && lc[3] > 0};
-    int olen[2];
-    int sa_[2] = {0, 1}, sb_[2] = {3, 2};
-    bool ok[2];
-    for (int e = 0; e < 2; e++) {
-        const int sa = sa_[e], sb2 = sb_[e];
-        ok[e] = has[sa] || has[sb2];
-        olen[e] = (has[sa] && has[sb2]) ? ::min(lc[sa], lc[sb2]) : has[sa] ? lc[sa] : has[sb2] ? lc[sb2] : 0;
-    }
-    const bool emit = ok[0] && ok[1];
+    // ---- duplex combine and output ----
+    bool hs[4];
+    for (int s = 0; s < 4; s++) hs[s] = cnt[s] > 0 && lcv[s] > 0;
+    const bool emit = (hs[0] || hs[3]) && (hs[1] || hs[2]);
     const int32_t stride = P.O.stride;
+    int olen[2];
+    for (int e = 0; e < 2; e++) {
+        const int sa = e == 0 ? 0 : 1, sb2 = e == 0 ? 3 : 2;
+        olen[e] = (hs[sa] && hs[sb2]) ? ::min(lcv[sa], lcv[sb2]) : hs[sa] ? lcv[sa] : hs[sb2] ? lcv[sb2] : 0;
+    }
     if (emit) {
         for (int e = 0; e < 2; e++) {
-            const int sa = sa_[e], sb2 = sb_[e];
-            const int64_t slot = (2 * (int64_t)fam + e) * stride;
+            const int sa = e == 0 ? 0 : 1, sb2 = e == 0 ? 3 : 2;
+            const int64_t so = (2 * (int64_t)fam + e) * stride;
             const int npair = (olen[e] + 1) >> 1;
-            for (int k = g.t; k < npair; k += G) {
-                uint8_t ob[2] = {0, 0}, oq[2] = {0, 0};
+            for (int k = tt; k < npair; k += G) {
+                uint32_t ob[2] = {0, 0}, oq[2] = {0, 0};
                 for (int h = 0; h < 2; h++) {
-                    const int c = 2 * k + h;
-                    if (c >= olen[e]) break;
-                    uint8_t b, q;
-                    if (has[sa] && has[sb2]) {
-                        const uint8_t xb = ssb[sa * ssw + c], yb = ssb[sb2 * ssw + c];
-                        const int xq = ssq[sa * ssw + c], yq = ssq[sb2 * ssw + c];
-                        int rq;
-                        uint8_t rb;
-                        if (xb == yb) {
-                            rb = xb;
-                            rq = xq + yq;
-                        } else if (xq > yq) {
-                            rb = xb;
-                            rq = xq - yq;
-                        } else if (yq > xq) {
-                            rb = yb;
-                            rq = yq - xq;
-                        } else {
-                            rb = xb;
-                            rq = 2;
-                        }
-                        if (rq > 93) rq = 93;
-                        if (xb == kN || yb == kN || rq == 2) {
-                            rb = kN;
-                            rq = 2;
-                        }
-                        b = rb;
-                        q = (uint8_t)rq;
+                    const int col = 2 * k + h;
+                    if (col >= olen[e]) break;
+                    if (hs[sa] && hs[sb2]) {
+                        duplex_col(ssb[sa * ssw + col], ssq[sa * ssw + col], ssb[sb2 * ssw + col], ssq[sb2 * ssw + col],
+                                   ob[h], oq[h]);
                     } else {
-                        const int s1 = has[sa] ? sa : sb2;
-                        b = ssb[s1 * ssw + c];
-                        q = ssq[s1 * ssw + c];
+                        const int s1 = hs[sa] ? sa : sb2;
+                        ob[h] = ssb[s1 * ssw + col];
+                        oq[h] = ssq[s1 * ssw + col];
                     }
-                    ob[h] = b;
-                    oq[h] = q;
                 }
-                P.O.seq[slot / 2 + k] = (uint8_t)((ob[0] << 4) | ob[1]);
-                P.O.qual[slot + 2 * k] = oq[0];
-                if (2 * k + 1 < olen[e]) P.O.qual[slot + 2 * k + 1] = oq[1];
+                P.O.seq[so / 2 + k] = (uint8_t)((ob[0] << 4) | ob[1]);
+                P.O.qual[so + 2 * k] = (uint8_t)oq[0];
+                if (2 * k + 1 < olen[e]) P.O.qual[so + 2 * k + 1] = (uint8_t)oq[1];
             }
         }
     }
-    if (g.t == 0) {
+    if (tt == 0) {
         uint8_t st = emit ? 1 : 0;
-        if (has[0] || has[1]) st |= 2;
-        if (has[2] || has[3]) st |= 4;
+        if (hs[0] || hs[1]) st |= 2;
+        if (hs[2] || hs[3]) st |= 4;
         P.O.status[fam] = st;
         P.O.len[2 * fam] = (uint16_t)(emit ? olen[0] : 0);
         P.O.len[2 * fam + 1] = (uint16_t)(emit ? olen[1] : 0);
     }
 }
 
-__device__ __forceinline__ void load_tables(const Tables *tab, long long *lr, float *thr) {
-    for (int i = threadIdx.x; i < 256; i += blockDim.x) lr[i] = tab->lr[i];
-    for (int i = threadIdx.x; i < 96; i += blockDim.x) thr[i] = tab->thr[i];
-    __syncthreads();
-}
-
-// small families: one wavefront per family, arena in LDS
-__global__ __launch_bounds__(kWave *kSmallWaves) void k_small(KParams P) {
-    extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
-    long long *lr = reinterpret_cast<long long *>(smem);
-    float *thr = reinterpret_cast<float *>(smem + 2048);
-    load_tables(P.tab, lr, thr);
-    const int w = threadIdx.x >> 6;
-    const int64_t i = (int64_t)blockIdx.x * kSmallWaves + w;
-    if (i >= P.B.n_small) return;
-    uint8_t *A = smem + 2048 + 384 + (size_t)w * (size_t)P.B.small_arena;
-    Grp<kWave> g{(int)(threadIdx.x & 63), nullptr};
-    process_family<kWave>(P, g, A, lr, thr, P.B.small_fams[i]);
-}
-
-// large families: one workgroup per family; arena in LDS (IN_LDS) or in global scratch
 template <bool IN_LDS>
 __global__ __launch_bounds__(kLargeThreads) void k_large(KParams P) {
     extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
     __shared__ int red[kLargeThreads / kWave];
-    long long *lr = reinterpret_cast<long long *>(smem);
-    float *thr = reinterpret_cast<float *>(smem + 2048);
-    load_tables(P.tab, lr, thr);
+    __shared__ int s_cnt[4], s_lc[4];
+    const Tables *T = reinterpret_cast<const Tables *>(smem);
+    load_tables(P.tab, smem);
+    const int32_t *lr = T->lr;
+    const float *thr = T->thr;
     const int64_t i = blockIdx.x;
     if (i >= P.B.n_large) return;
-    uint8_t *A = IN_LDS ? smem + 2048 + 384 : P.O.scratch + (size_t)i * (size_t)P.B.large_arena;
-    Grp<kLargeThreads> g{(int)threadIdx.x, red};
-    process_family<kLargeThreads>(P, g, A, lr, thr, P.B.large_fams[i]);
+    uint8_t *A = IN_LDS ? smem + kTabBytes : P.O.scratch + (size_t)i * (size_t)P.B.large_arena;
+    process_large(P, A, lr, thr, P.B.large_fams[i], red, s_cnt, s_lc);
 }
 
 }  // namespace
@@ -864,22 +1444,49 @@ struct bsdc_ctx {
     Tables host_tab;
     Tables *dev_tab = nullptr;
     uint8_t *ref_seq = nullptr;
-    int64_t *ref_off = nullptr;
-    int64_t *ref_len = nullptr;
-    int32_t n_contig = 0;
+    int64_t ref_nibbles = 0;
     std::string err;
 };
 
-static void make_tables(const bsdc_params &p, Tables &t) {
+static float det_expf_host(float x) {
+    const float tq = x * 1.44269504088896341f;
+    const float n = rintf(tq);
+    float r = fmaf(n, -6.93145751953125e-1f, x);
+    r = fmaf(n, -1.428606765330187e-6f, r);
+    float p = 1.38888889e-3f;
+    p = fmaf(p, r, 8.33333333e-3f);
+    p = fmaf(p, r, 4.16666667e-2f);
+    p = fmaf(p, r, 1.66666667e-1f);
+    p = fmaf(p, r, 0.5f);
+    p = fmaf(p, r, 1.0f);
+    p = fmaf(p, r, 1.0f);
+    return ldexpf(p, (int)n);
+}
+
+static int phred_agree(int64_t D, const float *thr) {
+    const float x = (float)((double)(-D) * 9.5367431640625e-07);
+    const float e = x < -80.0f ? 0.0f : det_expf_host(x);
+    const float S = ((0.0f + e) + e) + e;
+    int Q = 0;
+    for (int k = 1; k < 94; k++) {
+        if (S <= thr[k])
+            Q = k;
+        else
+            break;
+    }
+    return Q;
+}
+
+static void make_tables(double pre, double post, Tables &t) {
     // keep in step with oracle/bsdc_oracle.c orc_tables
-    const double e_post = pow(10.0, -p.error_rate_post_umi / 10.0);
-    const double e_pre = pow(10.0, -p.error_rate_pre_umi / 10.0);
+    const double e_post = pow(10.0, -post / 10.0);
+    const double e_pre = pow(10.0, -pre / 10.0);
     for (int q = 0; q < 256; q++) {
         const double e = pow(10.0, -(double)q / 10.0);
         const double a = e_post + e - (4.0 / 3.0) * e_post * e;
         const double lnc = log1p(-a);
         const double lne = log(a / 3.0);
-        t.lr[q] = llround((lnc - lne) * kLrScale);
+        t.lr[q] = (int32_t)llround((lnc - lne) * kLrScale);
     }
     t.thr[0] = INFINITY;
     for (int k = 1; k < 94; k++) {
@@ -888,6 +1495,30 @@ static void make_tables(const bsdc_params &p, Tables &t) {
         t.thr[k] = tt < 0.0 ? -1.0f : (float)(tt / (1.0 - tt));
     }
     t.thr[94] = t.thr[95] = -1.0f;
+    // agreement case: every other base has D = 0, S = ((0 + e) + e) + e with e = term(-D); Q(D)
+    // is the oracle's arithmetic on the host (same float ops), tabulated exactly:
+    // Q(D) = qlo[D >> 16] + (D >= dthr[qlo[D >> 16] + 1]).  tests/test_abi.py checks every D.
+    auto qof = [&](int64_t D) { return phred_agree(D, t.thr); };
+    for (int k = 0; k < 2048; k++) t.qlo[k] = (uint8_t)qof((int64_t)k << 16);
+    for (int q = 0; q < 48; q++) {
+        if (q == 0) {
+            t.dthr[q] = 0;
+            continue;
+        }
+        int64_t lo = 0, hi = (int64_t)1 << 27;  // smallest D in [0, 2^27) with Q(D) >= q, else 2^31-1
+        if (qof(hi - 1) < q) {
+            t.dthr[q] = 0x7FFFFFFF;
+            continue;
+        }
+        while (lo < hi) {
+            const int64_t mid = (lo + hi) / 2;
+            if (qof(mid) >= q)
+                hi = mid;
+            else
+                lo = mid + 1;
+        }
+        t.dthr[q] = (int32_t)lo;
+    }
 }
 
 #define HIP_OK(ctx, call)                                                                     \
@@ -903,9 +1534,28 @@ extern "C" {
 
 int32_t bsdc_abi_version(void) { return BSDC_ABI_VERSION; }
 
-int64_t bsdc_family_arena_bytes(int32_t n_rec, int64_t sum_len, int32_t max_len, int64_t complex_ops) {
-    ArenaLayout L(n_rec, sum_len, max_len, complex_ops);
+int64_t bsdc_family_arena_bytes(int32_t n_rec, int64_t slot_bytes, int32_t max_len, int64_t complex_ops) {
+    ArenaLayout L(n_rec, slot_bytes, max_len, complex_ops);
     return (int64_t)L.total;
+}
+
+int64_t bsdc_small_arena_bytes(int32_t n_rec, int64_t img, int32_t n_conv, int64_t complex_ops, int32_t max_len) {
+    SmallLayout L(n_rec, img, n_conv, complex_ops, max_len);
+    return (int64_t)L.total;
+}
+
+void bsdc_model_tables(double pre, double post, int64_t *lr256, float *thr94) {
+    Tables t;
+    make_tables(pre, post, t);
+    for (int i = 0; i < 256; i++) lr256[i] = t.lr[i];
+    for (int i = 0; i < 94; i++) thr94[i] = t.thr[i];
+}
+
+void bsdc_agree_tables(double pre, double post, uint8_t *qlo2048, int32_t *dthr48) {
+    Tables t;
+    make_tables(pre, post, t);
+    memcpy(qlo2048, t.qlo, sizeof t.qlo);
+    memcpy(dthr48, t.dthr, sizeof t.dthr);
 }
 
 int32_t bsdc_ctx_create(int32_t device, const bsdc_params *params, bsdc_ctx **out) {
@@ -917,7 +1567,7 @@ int32_t bsdc_ctx_create(int32_t device, const bsdc_params *params, bsdc_ctx **ou
     bsdc_ctx *c = new bsdc_ctx();
     c->device = device;
     c->params = *params;
-    make_tables(*params, c->host_tab);
+    make_tables(params->error_rate_pre_umi, params->error_rate_post_umi, c->host_tab);
     if (hipSetDevice(device) != hipSuccess || hipMalloc(&c->dev_tab, sizeof(Tables)) != hipSuccess ||
         hipMemcpy(c->dev_tab, &c->host_tab, sizeof(Tables), hipMemcpyHostToDevice) != hipSuccess) {
         delete c;
@@ -932,8 +1582,6 @@ void bsdc_ctx_destroy(bsdc_ctx *c) {
     (void)hipSetDevice(c->device);
     (void)hipFree(c->dev_tab);
     (void)hipFree(c->ref_seq);
-    (void)hipFree(c->ref_off);
-    (void)hipFree(c->ref_len);
     delete c;
 }
 
@@ -946,45 +1594,34 @@ int32_t bsdc_get_tables(const bsdc_ctx *c, int64_t *lr256, float *thr94) {
     return 0;
 }
 
-void bsdc_model_tables(double pre, double post, int64_t *lr256, float *thr94) {
-    bsdc_params p{};
-    p.error_rate_pre_umi = pre;
-    p.error_rate_post_umi = post;
-    Tables t;
-    make_tables(p, t);
-    for (int i = 0; i < 256; i++) lr256[i] = t.lr[i];
-    for (int i = 0; i < 94; i++) thr94[i] = t.thr[i];
-}
-
 int32_t bsdc_load_reference(bsdc_ctx *c, const uint8_t *packed, int64_t n_nib, const int64_t *coff,
                             const int64_t *clen, int32_t n_contig) {
-    if (!c || n_contig < 0 || (n_nib > 0 && !packed)) return BSDC_EINVAL;
+    (void)coff;
+    (void)clen;
+    if (!c || n_contig < 0 || n_nib < 0 || (n_nib > 0 && !packed)) return BSDC_EINVAL;
     HIP_OK(c, hipSetDevice(c->device));
     (void)hipFree(c->ref_seq);
-    (void)hipFree(c->ref_off);
-    (void)hipFree(c->ref_len);
     c->ref_seq = nullptr;
-    c->ref_off = c->ref_len = nullptr;
-    const size_t nb = (size_t)((n_nib + 1) / 2) + 16;
+    // +512 B: window chunks may read past the genome end (their nibbles are masked as N)
+    const size_t nb = (size_t)((n_nib + 1) / 2) + 512;
     HIP_OK(c, hipMalloc(&c->ref_seq, nb));
     HIP_OK(c, hipMemset(c->ref_seq, 0xFF, nb));
     if (n_nib > 0) HIP_OK(c, hipMemcpy(c->ref_seq, packed, (size_t)((n_nib + 1) / 2), hipMemcpyHostToDevice));
-    const size_t nc = sizeof(int64_t) * (size_t)(n_contig > 0 ? n_contig : 1);
-    HIP_OK(c, hipMalloc(&c->ref_off, nc));
-    HIP_OK(c, hipMalloc(&c->ref_len, nc));
-    if (n_contig > 0) {
-        HIP_OK(c, hipMemcpy(c->ref_off, coff, sizeof(int64_t) * n_contig, hipMemcpyHostToDevice));
-        HIP_OK(c, hipMemcpy(c->ref_len, clen, sizeof(int64_t) * n_contig, hipMemcpyHostToDevice));
-    }
-    c->n_contig = n_contig;
+    c->ref_nibbles = n_nib;
     return 0;
 }
 
 int32_t bsdc_run(bsdc_ctx *c, const bsdc_family_batch *b, bsdc_consensus *o, int32_t mode, void *stream) {
     if (!c || !b || !o) return BSDC_EINVAL;
-    if (b->small_arena % 16 || b->large_arena % 16 || o->stride % 16 || o->stride < b->max_len + 2) {
+    if (b->large_arena % 16 || o->stride % 16 || o->stride < b->max_len + 2 || b->max_len > 0xFFFF - 8) {
         c->err = "bad arena/stride sizes";
         return BSDC_EINVAL;
+    }
+    for (int q = 0; q < 4; q++) {
+        if (b->small_arena[q] % 16 || (size_t)kTabBytes + (size_t)kSmallWaves * (size_t)b->small_arena[q] > 160 * 1024) {
+            c->err = "bad small arena size";
+            return BSDC_EINVAL;
+        }
     }
     if ((mode & BSDC_MODE_CONVERT) && !c->ref_seq) {
         c->err = "reference not loaded";
@@ -999,26 +1636,26 @@ int32_t bsdc_run(bsdc_ctx *c, const bsdc_family_batch *b, bsdc_consensus *o, int
     KParams P;
     P.B = *b;
     P.O = *o;
-    P.R.seq = c->ref_seq;
-    P.R.off = c->ref_off;
-    P.R.len = c->ref_len;
-    P.R.n = c->n_contig;
+    P.ref = c->ref_seq;
     P.tab = c->dev_tab;
     P.mode = mode;
     P.overlap = c->params.consensus_call_overlapping_bases;
-    const size_t tab_lds = 2048 + 384;
-    if (b->n_small > 0) {
-        const size_t lds = tab_lds + (size_t)kSmallWaves * (size_t)b->small_arena;
-        if (lds > 160 * 1024) {
-            c->err = "small arena too large";
-            return BSDC_EINVAL;
+    if (!(mode & BSDC_MODE_SKIP_SMALL)) {
+        const uint32_t *f = b->small_fams;
+        for (int q = 0; q < 4; q++) {
+            const int64_t nf = b->n_small[q];
+            if (nf > 0) {
+                const size_t lds = (size_t)kTabBytes + (size_t)kSmallWaves * (size_t)b->small_arena[q];
+                const int64_t blocks = (nf + kSmallWaves - 1) / kSmallWaves;
+                hipLaunchKernelGGL(k_small, dim3((unsigned)blocks), dim3(kWave * kSmallWaves), lds, s, P, f, nf,
+                                   b->small_arena[q]);
+                HIP_OK(c, hipGetLastError());
+            }
+            f += nf;
         }
-        const int64_t blocks = (b->n_small + kSmallWaves - 1) / kSmallWaves;
-        hipLaunchKernelGGL(k_small, dim3((unsigned)blocks), dim3(kWave * kSmallWaves), lds, s, P);
-        HIP_OK(c, hipGetLastError());
     }
-    if (b->n_large > 0) {
-        const size_t lds = tab_lds + (size_t)b->large_arena;
+    if (b->n_large > 0 && !(mode & BSDC_MODE_SKIP_LARGE)) {
+        const size_t lds = (size_t)kTabBytes + (size_t)b->large_arena;
         if (lds <= 64 * 1024) {
             hipLaunchKernelGGL(k_large<true>, dim3((unsigned)b->n_large), dim3(kLargeThreads), lds, s, P);
         } else {
@@ -1026,7 +1663,7 @@ int32_t bsdc_run(bsdc_ctx *c, const bsdc_family_batch *b, bsdc_consensus *o, int
                 c->err = "large families need scratch";
                 return BSDC_EINVAL;
             }
-            hipLaunchKernelGGL(k_large<false>, dim3((unsigned)b->n_large), dim3(kLargeThreads), tab_lds, s, P);
+            hipLaunchKernelGGL(k_large<false>, dim3((unsigned)b->n_large), dim3(kLargeThreads), (size_t)kTabBytes, s, P);
         }
         HIP_OK(c, hipGetLastError());
     }

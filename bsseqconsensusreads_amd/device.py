@@ -54,13 +54,13 @@ class DeviceBatch:
         self.qual = torch.zeros(max(2 * F * self.stride, 16), dtype=torch.uint8, device=device)
         self.dump = dump
         if dump:
-            cap = fb.n_bases + 2 * Rn + 16
+            cap = fb.n_slots + 16
             self.dump_pos = torch.zeros(max(Rn, 1), dtype=torch.int32, device=device)
             self.dump_len = torch.zeros(max(Rn, 1), dtype=torch.int16, device=device)
             self.dump_tags = torch.zeros(max(Rn, 1), dtype=torch.uint8, device=device)
             self.dump_seq = torch.zeros(cap, dtype=torch.uint8, device=device)
             self.dump_qual = torch.zeros(cap, dtype=torch.uint8, device=device)
-        lds_cap = 64 * 1024 - (2048 + 384)
+        lds_cap = 64 * 1024 - (1024 + 384 + 2048 + 192)
         nl = int(fb.large_fams.shape[0])
         self.scratch = None
         if nl and fb.large_arena > lds_cap:
@@ -68,13 +68,14 @@ class DeviceBatch:
         self._b = _lib.FamilyBatchC()
         b = self._b
         b.n_rec, b.n_fam = Rn, F
-        for k in ("fam_off", "rec_off", "rec_pos", "rec_lenflag", "rec_tid", "rec_link", "cig_off",
-                  "cig_info", "cigar", "rt", "seq", "qual", "small_fams", "large_fams"):
+        for k in ("fam_off", "rec", "rec_win", "cig_off", "cig_info", "cigar", "rt", "seq", "qual",
+                  "small_fams", "large_fams"):
             setattr(b, k, _dptr(self.t[k]))
-        b.n_small = int(fb.small_fams.shape[0])
+        for q in range(4):
+            b.n_small[q] = int(fb.small_buckets[q].shape[0])
+            b.small_arena[q] = int(fb.small_arenas[q])
         b.n_large = nl
         b.max_len = fb.max_len
-        b.small_arena = fb.small_arena
         b.large_arena = fb.large_arena
         self._o = _lib.ConsensusC()
         o = self._o

@@ -72,7 +72,7 @@ def _records_from_dump(raw: R.RawRecords, fb: FamilyBatch, out: dict, strip: boo
     seq_off = np.zeros(n, np.int64)
     if n:
         seq_off[1:] = np.cumsum(lens)[:-1]
-    d = fb.rec_off.astype(np.int64) + 2 * np.arange(n, dtype=np.int64)
+    d = fb.rec_off.astype(np.int64)
     idx = np.repeat(d - seq_off, lens) + np.arange(int(lens.sum()), dtype=np.int64)
     seq = out["dump_seq"][idx]
     qual = out["dump_qual"][idx]
@@ -160,7 +160,7 @@ def run_tool1(engine: Engine, raw: R.RawRecords) -> OutRecords:
     """tools/1.convert_AG_to_CT.py:67-186 over a record stream (reference must be loaded)."""
     from .batch import tool1_plan
     pas, conv = tool1_plan(raw)
-    fb = build_family_batch(raw, "convert")
+    fb = build_family_batch(raw, "convert", engine.ref)
     db = engine.upload(fb, dump=True)
     engine.run(db, MODE_CONVERT | MODE_DUMP)
     out = db.fetch()
@@ -190,7 +190,7 @@ def consensus_from_output(fb: FamilyBatch, out: dict) -> Consensus:
 
 def run_step5(engine: Engine, raw: R.RawRecords, dump: bool = False):
     """Rules convert_Bstrain .. callduplex (main.snake.py:121-164) -> (Consensus, tool-2 records or None)."""
-    fb = build_family_batch(raw, "full")
+    fb = build_family_batch(raw, "full", engine.ref)
     db = engine.upload(fb, dump=dump)
     engine.run(db, MODE_CONVERT | MODE_EXTEND | MODE_VOTE | (MODE_DUMP if dump else 0))
     out = db.fetch()

@@ -247,3 +247,16 @@ def messify(raw: R.RawRecords, frac: float = 0.1, seed: int = 1) -> R.RawRecords
         b.add(("t%d" % raw.name_id[k]).encode(), flag, int(raw.tid[k]), pos, 60, cig, seq, qual,
               int(raw.next_tid[k]), int(raw.next_pos[k]), int(raw.tlen[k]), R.encode_aux(tags), tags)
     return b.finish()
+
+
+def subset_families(raw: R.RawRecords, n_fam: int) -> R.RawRecords:
+    """The records of families 0..n_fam-1 of a generate() stream (records are family-major)."""
+    k = int(np.searchsorted(raw.mi_id, n_fam, side="left"))
+    so, co, mo = int(raw.seq_off[k]) if k < raw.n else raw.seq.shape[0], \
+        int(raw.cig_off[k]) if k < raw.n else raw.cigar.shape[0], int(raw.mc_off[k]) if k < raw.n else raw.mc_cigar.shape[0]
+    return R.RawRecords(
+        flag=raw.flag[:k], tid=raw.tid[:k], pos=raw.pos[:k], mapq=raw.mapq[:k], l_seq=raw.l_seq[:k],
+        seq_off=raw.seq_off[:k], seq=raw.seq[:so], qual=raw.qual[:so], cig_off=raw.cig_off[:k], n_cig=raw.n_cig[:k],
+        cigar=raw.cigar[:co], next_tid=raw.next_tid[:k], next_pos=raw.next_pos[:k], tlen=raw.tlen[:k],
+        name_id=raw.name_id[:k], names=raw.names, mi_id=raw.mi_id[:k], mi_strand=raw.mi_strand[:k],
+        mi_names=raw.mi_names, mc_off=raw.mc_off[:k], mc_n=raw.mc_n[:k], mc_cigar=raw.mc_cigar[:mo])

@@ -24,7 +24,7 @@
 extern "C" {
 #endif
 
-#define BSDC_ABI_VERSION 1
+#define BSDC_ABI_VERSION 2
 
 #define BSDC_EINVAL (-22)
 #define BSDC_ENOMEM (-12)
@@ -54,33 +54,32 @@ typedef struct {
 #define BSDC_LINK_USABLE (1u << 26)   /* paired primary record with an /A or /B MI */
 
 /* A batch of MI families in HBM, structure-of-arrays.  Record r of family f is
- * fam_off[f] <= r < fam_off[f+1]; its bases are nibbles rec_off[r] .. rec_off[r]+len-1 of `seq`
- * (nt16 codes "=ACMGRSVTWYHKDBN", two per byte, high nibble first, as in BAM) and its quals the
- * same indices of `qual`.  Soft clips are already stripped by the host (tools 1 and 2 both strip
- * them before anything else).  rec_off must be the running sum of the lengths. */
+ * fam_off[f] <= r < fam_off[f+1].  Records live in "slots": slot r starts at nibble/byte index
+ * S = rec[4r] of `seq` (nt16 codes "=ACMGRSVTWYHKDBN", two per byte, high nibble first, as in
+ * BAM) and of `qual`, is round4(len+2) long, and holds the record's bases/quals at S+1 .. S+len
+ * (S+0 and S+len+1 are the prepend / append room of tools 1 and 2).  A family's slots are
+ * contiguous and its first slot starts at a multiple of 32.  Soft clips are already stripped by
+ * the host (tools 1 and 2 both strip them before anything else). */
 typedef struct {
     int64_t n_rec;
     int64_t n_fam;
     const uint32_t *fam_off;     /* [n_fam+1] */
-    const uint32_t *rec_off;     /* [n_rec]   */
-    const int32_t *rec_pos;      /* [n_rec]   0-based leftmost aligned position */
-    const uint32_t *rec_lenflag; /* [n_rec]   length | flag << 16 */
-    const int32_t *rec_tid;      /* [n_rec]   */
-    const uint32_t *rec_link;    /* [n_rec]   BSDC_LINK_* */
+    const uint32_t *rec;         /* [4*n_rec] slot start, pos (int32, 0-based), len | flag << 16, link */
+    const uint32_t *rec_win;     /* [2*n_rec] converted records: reference window start nibble
+                                    (= contig start + max(pos-1,0)), valid nibbles (<= len+2) */
     const uint32_t *cig_off;     /* [n_rec]   complex records only: first op in `cigar` */
     const uint32_t *cig_info;    /* [n_rec]   complex only: n_ops | reflen << 16 */
     const uint32_t *cigar;       /*           BAM-encoded ops (soft/hard clips removed) */
     const int32_t *rt;           /* [4*n_rec] RT records only: next_pos, tlen, mate unclipped start, end */
     const uint8_t *seq;
     const uint8_t *qual;
-    const uint32_t *small_fams;  /* families processed one wavefront each (LDS arena) */
-    int64_t n_small;
+    const uint32_t *small_fams;  /* families processed one wavefront each, 4 consecutive buckets */
+    int64_t n_small[4];          /* families per bucket */
+    int32_t small_arena[4];      /* LDS bytes per wavefront of each bucket (multiple of 16) */
     const uint32_t *large_fams;  /* families processed one workgroup each */
     int64_t n_large;
-    int32_t max_len;             /* max record length */
-    int32_t small_arena;         /* LDS bytes per wavefront for small families (multiple of 16) */
     int32_t large_arena;         /* bytes per workgroup for large families */
-    int32_t reserved;
+    int32_t max_len;             /* max record length */
 } bsdc_family_batch;
 
 /* Outputs (device pointers).  Consensus slot (f, end) holds `stride` bases. */
@@ -95,7 +94,7 @@ typedef struct {
     int32_t *dump_pos;           /* [n_rec] */
     uint16_t *dump_len;          /* [n_rec] */
     uint8_t *dump_tags;          /* [n_rec] bit0 RD=1, bit1 LA present, bit2 prepended M, bit3 appended M */
-    uint8_t *dump_seq;           /* [rec_off[r] + 2r ...] one nt16 code per byte */
+    uint8_t *dump_seq;           /* [slot start + j] one nt16 code per byte */
     uint8_t *dump_qual;
     uint8_t *scratch;            /* large-family arenas when large_arena exceeds LDS: n_large * large_arena bytes */
 } bsdc_consensus;
@@ -104,6 +103,9 @@ typedef struct {
 #define BSDC_MODE_EXTEND 2
 #define BSDC_MODE_VOTE 4
 #define BSDC_MODE_DUMP 8
+#define BSDC_MODE_SKIP_SMALL 16 /* profiling: do not launch the small-family kernel */
+#define BSDC_MODE_SKIP_LARGE 32 /* profiling: do not launch the large-family kernel */
+#define BSDC_MODE_STOP_SHIFT 8  /* profiling: (mode >> 8) & 15 = k > 0 stops the small kernel after phase k */
 
 typedef struct bsdc_ctx bsdc_ctx;
 
@@ -113,7 +115,8 @@ void bsdc_ctx_destroy(bsdc_ctx *ctx);
 const char *bsdc_last_error(const bsdc_ctx *ctx);
 
 /* Reference genome, host pointers: nt16 codes of the upper-cased FASTA, packed two per byte;
- * contig_off[tid] = first nibble of contig tid (-1 = contig absent from the FASTA). */
+ * contig_off[tid] = first nibble of contig tid (-1 = contig absent from the FASTA).  Batches
+ * address it through rec_win, which the host derives from the same contig table. */
 int32_t bsdc_load_reference(bsdc_ctx *ctx, const uint8_t *packed_nt16, int64_t n_nibbles,
                             const int64_t *contig_off, const int64_t *contig_len, int32_t n_contig);
 
@@ -127,13 +130,18 @@ int32_t bsdc_extend(bsdc_ctx *ctx, const bsdc_family_batch *batch, bsdc_consensu
 int32_t bsdc_duplex_call(bsdc_ctx *ctx, const bsdc_family_batch *batch, bsdc_consensus *out,
                          int32_t with_tools, void *stream);
 
-/* Arena bytes one family needs (host-side helper shared with the batch builder). */
-int64_t bsdc_family_arena_bytes(int32_t n_rec, int64_t sum_len, int32_t max_len, int64_t complex_ops);
+/* Arena bytes one family needs (host-side helpers shared with the batch builder):
+ * workgroup kernel (slot_bytes = 2 x the family's slot span) and wavefront kernel (img = slot
+ * span rounded to 32, n_conv = converted records, max_len = the batch's max record length). */
+int64_t bsdc_family_arena_bytes(int32_t n_rec, int64_t slot_bytes, int32_t max_len, int64_t complex_ops);
+int64_t bsdc_small_arena_bytes(int32_t n_rec, int64_t img, int32_t n_conv, int64_t complex_ops, int32_t max_len);
 
 /* The likelihood tables the vote kernel uses (host copies), for cross-checks. */
 int32_t bsdc_get_tables(const bsdc_ctx *ctx, int64_t *lr256, float *thresh94);
 /* Same tables for given error rates, without a context (no GPU needed). */
 void bsdc_model_tables(double error_rate_pre_umi, double error_rate_post_umi, int64_t *lr256, float *thresh94);
+/* The vote's agreement-case tables: Q(D) = qlo[D >> 16] + (D >= dthr[qlo[D >> 16] + 1]). */
+void bsdc_agree_tables(double error_rate_pre_umi, double error_rate_post_umi, uint8_t *qlo2048, int32_t *dthr48);
 
 #ifdef __cplusplus
 }

@@ -286,8 +286,8 @@ static void ovec_push(orec_vec *v, orec r) {
 /* ------------------------------------------------------------------------------------------ */
 /* the likelihood model (fgbio ConsensusCaller, restated)          */
 /* ------------------------------------------------------------------------------------------ */
-#define LR_SCALE 1099511627776.0 /* 2^40 */
-#define LR_INV_SCALE 9.094947017729282379150390625e-13
+#define LR_SCALE 1048576.0 /* 2^20: likelihoods in exact fixed point, 2^-20 nats */
+#define LR_INV_SCALE 9.5367431640625e-07
 
 void orc_tables(double pre, double post, int64_t *lr, float *thr) {
     const double e_post = pow(10.0, -post / 10.0);
@@ -1016,4 +1016,37 @@ void orc_get_consensus(const orc_result *r, int32_t stride, int32_t *mi_id, int3
             }
         }
     }
+}
+
+/* Exhaustive check of libbsdc's agreement-case tables against this restatement's arithmetic:
+ * for every D in [0, dmax] (the best base's sum, every other base 0) the vote's Q equals
+ * qlo[D >> 16] + (D >= dthr[qlo[D >> 16] + 1]).  Returns the first D that differs, or -1. */
+int64_t orc_check_agree(const uint8_t *qlo, const int32_t *dthr, const float *thr, int64_t dmax) {
+    int64_t bad = -1;
+#pragma omp parallel for schedule(static) reduction(max : bad)
+    for (int64_t blk = 0; blk <= dmax >> 16; blk++) {
+        for (int64_t D = blk << 16; D < ((blk + 1) << 16) && D <= dmax; D++) {
+            float S = 0.0f;
+            for (int b = 0; b < 3; b++) {
+                const float x = (float)((double)(0 - D) * LR_INV_SCALE);
+                if (x < -80.0f) continue;
+                S += orc_det_expf(x);
+            }
+            int Q = 0;
+            for (int k = 1; k < 94; k++) {
+                if (S <= thr[k])
+                    Q = k;
+                else
+                    break;
+            }
+            const int64_t d = D < ((int64_t)1 << 27) ? D : ((int64_t)1 << 27) - 1;
+            const int q0 = qlo[d >> 16];
+            const int qt = q0 + (d >= dthr[q0 + 1] ? 1 : 0);
+            if (qt != Q) {
+                if (bad < 0 || D < bad) bad = D;
+                break;
+            }
+        }
+    }
+    return bad;
 }

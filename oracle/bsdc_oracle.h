@@ -87,6 +87,7 @@ void orc_get_consensus(const orc_result *r, int32_t stride, int32_t *mi_id, int3
 /* Tables of the likelihood model, for a cross-check against libbsdc's own. */
 void orc_tables(double pre, double post, int64_t *lr_fixed256, float *phred_thresh94);
 float orc_det_expf(float x);
+int64_t orc_check_agree(const uint8_t *qlo, const int32_t *dthr, const float *thr, int64_t dmax);
 
 #ifdef __cplusplus
 }

@@ -8,6 +8,7 @@ from __future__ import annotations
 import ctypes as C
 import os
 import subprocess
+import time
 from dataclasses import dataclass
 from typing import Dict, List, Optional
 
@@ -70,6 +71,8 @@ def load():
         lib.orc_tables.argtypes = [C.c_double, C.c_double, C.c_void_p, C.c_void_p]
         lib.orc_det_expf.restype = C.c_float
         lib.orc_det_expf.argtypes = [C.c_float]
+        lib.orc_check_agree.restype = C.c_int64
+        lib.orc_check_agree.argtypes = [C.c_void_p, C.c_void_p, C.c_void_p, C.c_int64]
         _lib = lib
     return _lib
 
@@ -109,6 +112,7 @@ class OracleResult:
     cons_seq: np.ndarray    # [F, 2, stride] nt16 codes
     cons_qual: np.ndarray   # [F, 2, stride]
     n_reads: np.ndarray
+    seconds: float = 0.0    # wall time of orc_run alone
 
 
 def _ptr(a):
@@ -178,7 +182,9 @@ def run(raw, ref, pre=45.0, post=30.0, overlap=True, run_tools=True, threads=0) 
     rf.seq = arr(np.concatenate(parts) if parts else np.zeros(1, np.uint8), np.uint8)
 
     p = _Params(pre, post, 0, int(overlap), int(run_tools), int(threads))
+    t0 = time.perf_counter()
     h = lib.orc_run(C.byref(rr), C.byref(rf), C.byref(p))
+    seconds = time.perf_counter() - t0
     if not h:
         raise OracleError(lib.orc_last_error().decode())
     try:
@@ -217,7 +223,7 @@ def run(raw, ref, pre=45.0, post=30.0, overlap=True, run_tools=True, threads=0) 
         lib.orc_get_consensus(h, stride, _ptr(mi), _ptr(st), _ptr(ln), _ptr(bs), _ptr(qs), _ptr(nr))
         return OracleResult(outs[0], outs[1], mi[:F], st[:F], ln[:2 * F].reshape(F, 2),
                             _ASCII_NT16[bs[:2 * F * stride]].reshape(F, 2, stride) if F else np.zeros((0, 2, stride), np.uint8),
-                            qs[:2 * F * stride].reshape(F, 2, stride), nr[:F])
+                            qs[:2 * F * stride].reshape(F, 2, stride), nr[:F], seconds)
     finally:
         lib.orc_free(h)
 
@@ -232,3 +238,11 @@ def tables(pre=45.0, post=30.0):
 
 def det_expf(x: float) -> float:
     return float(load().orc_det_expf(x))
+
+
+def check_agree_tables(qlo, dthr, thr, dmax) -> int:
+    """First D where libbsdc's agreement tables disagree with this restatement, or -1."""
+    qlo = np.ascontiguousarray(qlo, np.uint8)
+    dthr = np.ascontiguousarray(dthr, np.int32)
+    thr = np.ascontiguousarray(thr, np.float32)
+    return int(load().orc_check_agree(_ptr(qlo), _ptr(dthr), _ptr(thr), int(dmax)))

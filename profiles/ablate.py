@@ -1,0 +1,42 @@
+"""Profiling aid: time the small-family kernel stopped after each phase (BSDC_MODE_STOP_SHIFT).
+Usage on the GPU box: python profiles/ablate.py [--config C2] [--families N]"""
+import argparse
+import json
+import os
+import sys
+
+import torch
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, ROOT)
+from bsseqconsensusreads_amd import batch as B, synth  # noqa: E402
+from bsseqconsensusreads_amd._lib import MODE_CONVERT, MODE_EXTEND, MODE_VOTE, MODE_SKIP_LARGE  # noqa: E402
+from bsseqconsensusreads_amd.device import Engine  # noqa: E402
+
+PHASES = ["staging", "convert", "extend", "overlap", "srcreads+lists", "ss-vote", "full"]
+
+ap = argparse.ArgumentParser()
+ap.add_argument("--config", default="C2")
+ap.add_argument("--families", type=int, default=1_000_000)
+ap.add_argument("--reps", type=int, default=10)
+a = ap.parse_args()
+dev = torch.device("cuda", 0)
+s = synth.generate(a.config, a.families, seed=42, device=dev)
+fb = B.build_family_batch(s.raw, "full", s.ref)
+eng = Engine(0)
+eng.load_reference(s.ref)
+db = eng.upload(fb)
+st = torch.cuda.current_stream()
+out = {}
+for k, name in enumerate(PHASES, start=1):
+    mode = MODE_CONVERT | MODE_EXTEND | MODE_VOTE | MODE_SKIP_LARGE | ((k % 7) << 8)
+    for _ in range(2):
+        eng.run(db, mode, st)
+    e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    e0.record(st)
+    for _ in range(a.reps):
+        eng.run(db, mode, st)
+    e1.record(st)
+    torch.cuda.synchronize()
+    out[name] = round(e0.elapsed_time(e1) / a.reps, 4)
+print(json.dumps({"config": a.config, "small_families": int(fb.small_fams.shape[0]), "ms_after_phase": out}))

@@ -40,9 +40,9 @@ def test_model_tables_follow_fgbio_formula():
     for q in (0, 2, 10, 20, 30, 37, 40, 60, 93):
         e = 10 ** (-q / 10)
         a = ep + e - 4 / 3 * ep * e
-        assert abs(lr[q] / 2.0 ** 40 - (np.log1p(-a) - np.log(a / 3))) < 1e-9
+        assert abs(lr[q] / 2.0 ** 20 - (np.log1p(-a) - np.log(a / 3))) < 1e-6
     # worked value: one Q37 read -> S = 3 e^-lr[37] -> Q29
-    S = 3 * np.exp(-lr[37] / 2.0 ** 40)
+    S = 3 * np.exp(-lr[37] / 2.0 ** 20)
     Q = max(k for k in range(94) if k == 0 or S <= thr[k])
     p = S / (1 + S)
     pp = epre + p - 4 / 3 * epre * p
@@ -55,12 +55,28 @@ def test_det_expf_accuracy():
         assert abs(v / np.exp(np.float64(x)) - 1) < 1e-6, x
 
 
-def test_arena_formula_matches_library():
+def test_arena_formulas_match_library():
     lib = _lib.load()
     rng = np.random.default_rng(0)
     for _ in range(200):
         n = int(rng.integers(1, 600))
-        sl = int(rng.integers(0, 200 * n))
+        sl = int(rng.integers(0, 400 * n))
         ml = int(rng.integers(0, 400))
         co = int(rng.integers(0, 3)) * int(rng.integers(0, 50))
-        assert lib.bsdc_family_arena_bytes(n, sl, ml, co) == int(batch.arena_bytes(n, sl, ml, co))
+        assert lib.bsdc_family_arena_bytes(n, sl, ml, co) == int(batch.large_arena_bytes(n, sl, ml, co))
+        img = 32 * int(rng.integers(1, 200))
+        nc = int(rng.integers(0, min(n, 64) + 1))
+        assert lib.bsdc_small_arena_bytes(min(n, 64), img, nc, co, ml) == int(
+            batch.small_arena_bytes(min(n, 64), img, nc, co, ml))
+
+
+def test_agreement_tables_exhaustive():
+    """The kernel's agreement-case shortcut (integer thresholds on the likelihood sum) gives the
+    same phred as the full float arithmetic of oracle/ for EVERY sum up to past saturation."""
+    lib = _lib.load()
+    for pre, post in ((45.0, 30.0), (40.0, 20.0)):
+        qlo = np.zeros(2048, np.uint8)
+        dthr = np.zeros(48, np.int32)
+        lib.bsdc_agree_tables(pre, post, qlo.ctypes.data, dthr.ctypes.data)
+        _, thr = oracle.tables(pre, post)
+        assert oracle.check_agree_tables(qlo, dthr, thr, (1 << 27) + 1000) == -1

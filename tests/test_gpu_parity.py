@@ -95,7 +95,7 @@ def test_messy_records_vs_oracle(engine):
 def test_read_through_trim_vs_oracle(engine):
     """short inserts: reads run past the (stale) mate end, fgbio trims them."""
     s = synth.generate("C1", 600, seed=6, device="cpu", genome_len=200_000, frag=(140, 40, 60))
-    fb = batch.build_family_batch(s.raw, "full")
+    fb = batch.build_family_batch(s.raw, "full", s.ref)
     assert (fb.rec_link & batch.LINK_RT).any()
     engine.load_reference(s.ref)
     cons, _ = pipeline.run_step5(engine, s.raw)
@@ -109,8 +109,8 @@ def test_large_family_kernel(engine, where, monkeypatch):
     raw = synth.messify(s.raw, frac=0.1, seed=2)
     real = batch.build_family_batch
 
-    def forced(r, mode="full", small_cap=0):
-        fb = real(r, mode, small_cap=0)
+    def forced(r, mode="full", ref=None, small_cap=0):
+        fb = real(r, mode, ref, small_cap=0)
         if where == "global":
             fb.large_arena = max(fb.large_arena, 70000)
         return fb
