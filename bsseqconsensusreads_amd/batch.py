@@ -103,6 +103,7 @@ class FamilyBatch:
     small_buckets: List[np.ndarray]  # 4 lists of family ids (u32), one per LDS arena size
     small_arenas: List[int]
     large_fams: np.ndarray   # u32
+    fam_entry: np.ndarray    # u32 [F, 4] small-kernel list entry of each family
     max_len: int
     large_arena: int
     # ---- host bookkeeping ----
@@ -133,7 +134,8 @@ class FamilyBatch:
              "rec_win": np.ascontiguousarray(self.rec_win, dtype=np.uint32)}
         for k in ("cig_off", "cig_info", "cigar", "rt", "seq", "qual", "large_fams"):
             d[k] = getattr(self, k)
-        d["small_fams"] = self.small_fams
+        d["small_fams"] = np.ascontiguousarray(self.fam_entry[self.small_fams.astype(np.int64)]).reshape(-1) \
+            if self.small_fams.shape[0] else np.zeros(4, np.uint32)
         return d
 
 
@@ -482,7 +484,9 @@ def build_family_batch(raw: R.RawRecords, mode: str = "full", ref: Optional[R.Re
     need_s = small_arena_bytes(fam_sizes, img, nconv, cops, max_len)
     chunks = small_chunks(img, nconv, max_len)
     need_l = large_arena_bytes(fam_sizes, 2 * span, max_len_f, cops)
-    small = (fam_sizes <= 64) & (chunks <= 256) & (need_s <= small_cap)
+    qs_chunks = img // 16 + img // 32
+    ref_c = nconv * ref_chunks(max_len)
+    small = (fam_sizes <= 64) & (qs_chunks <= 256) & (ref_c <= 256) & (need_s <= small_cap) & (img // 32 < (1 << 24))
     buckets, arenas = [], []
     lo = -1
     for cap in SMALL_BUCKETS:
@@ -500,8 +504,14 @@ def build_family_batch(raw: R.RawRecords, mode: str = "full", ref: Optional[R.Re
     large_fams = np.nonzero(~small)[0].astype(np.uint32)
     large_arena = int(round16(need_l[~small].max())) if (~small).any() else 16
 
+    # small-family list entries: family, first record, n | (image / 32) << 8, image base
+    ent = np.zeros((nf, 4), np.int64)
+    ent[:, 0] = np.arange(nf)
+    ent[:, 1] = fam_off[:-1]
+    ent[:, 2] = fam_sizes | ((img // 32) << 8)
+    ent[:, 3] = fam_base[:-1]
     return FamilyBatch(
-        fam_off=fam_off.astype(np.uint32), rec_off=rec_off.astype(np.uint32),
+        fam_off=fam_off.astype(np.uint32), rec_off=rec_off.astype(np.uint32), fam_entry=ent.astype(np.uint32),
         rec_pos=raw.pos[order].astype(np.int32),
         rec_lenflag=(Lb | (fo << 16)).astype(np.uint32), rec_tid=raw.tid[order].astype(np.int32),
         rec_link=link.astype(np.uint32), rec_win=rec_win.astype(np.uint32),

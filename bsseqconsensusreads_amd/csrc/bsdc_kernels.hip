@@ -463,32 +463,47 @@ __global__ __launch_bounds__(kWave *kSmallWaves) void k_small(KParams P, const u
     const int max_len = B.max_len;
     const int stop = (P.mode >> BSDC_MODE_STOP_SHIFT) & 15;  // profiling ablation (0 = full kernel)
 
-    const uint32_t fam = __builtin_amdgcn_readfirstlane(fams[fi]);
-    const uint32_t r0 = __builtin_amdgcn_readfirstlane(B.fam_off[fam]);
-    const int n = (int)(__builtin_amdgcn_readfirstlane(B.fam_off[fam + 1]) - r0);
+    // list entry: family id, first record, record count | image size / 32 << 8, image base
+    const uint4 ent = reinterpret_cast<const uint4 *>(fams)[fi];
+    const uint32_t fam = __builtin_amdgcn_readfirstlane(ent.x);
+    const uint32_t r0 = __builtin_amdgcn_readfirstlane(ent.y);
+    const int n = (int)(__builtin_amdgcn_readfirstlane(ent.z) & 0xFF);
+    const uint32_t img = (__builtin_amdgcn_readfirstlane(ent.z) >> 8) * 32u;
+    const uint32_t base_g = __builtin_amdgcn_readfirstlane(ent.w);
 
-    // ---- record metadata: lane t owns record t ----
+    // ---- one round trip: record metadata, windows and every image chunk ----
     const bool has = t < n;
     uint4 rc = make_uint4(0, 0, 0, 0);
-    if (has) rc = reinterpret_cast<const uint4 *>(B.rec)[r0 + t];
+    uint2 win = make_uint2(0, 0);
+    uint32_t cinfo = 0;
+    const int nqc = (int)(img >> 4), nsc = (int)(img >> 5);  // qual chunks, packed-base chunks
+    uint4 v[4];
+#pragma unroll
+    for (int u = 0; u < 4; u++) {
+        const int k = t + 64 * u;
+        v[u] = make_uint4(0, 0, 0, 0);
+        if (k < nqc)
+            v[u] = *reinterpret_cast<const uint4 *>(B.qual + base_g + 16 * (uint32_t)k);
+        else if (k < nqc + nsc)
+            v[u] = *reinterpret_cast<const uint4 *>(B.seq + (base_g >> 1) + 16 * (uint32_t)(k - nqc));
+    }
+    if (has) {
+        rc = reinterpret_cast<const uint4 *>(B.rec)[r0 + t];
+        win = reinterpret_cast<const uint2 *>(B.rec_win)[r0 + t];
+        cinfo = B.cig_info[r0 + t];
+    }
     const uint32_t gslot = rc.x;
     int32_t pos = (int32_t)rc.y;
     const int32_t L = (int32_t)(rc.z & 0xFFFF);
     const uint32_t flag = rc.z >> 16;
     uint32_t link = rc.w;
     const bool conv = has && do_convert && (link & BSDC_LINK_CONVERT);
-    uint2 win = make_uint2(0, 0);
-    if (conv) win = reinterpret_cast<const uint2 *>(B.rec_win)[r0 + t];
     const bool cplx = has && (link & BSDC_LINK_COMPLEX);
-    const uint32_t cinfo = cplx ? B.cig_info[r0 + t] : 0;
+    if (!cplx) cinfo = 0;
 
     const uint64_t conv_mask = ballot(conv);
     const int nconv = __builtin_popcountll(conv_mask);
     const int ci = mbcnt(conv_mask);
-    const uint32_t base_g = rlu(gslot, 0);
-    const uint32_t cap4 = (uint32_t)((L + 2 + 3) & ~3);
-    const uint32_t end_g = rlu(gslot + cap4, n - 1);
-    const uint32_t img = (end_g - base_g + 31u) & ~31u;
     int cops = (int)(cinfo & 0xFFFF);
 #pragma unroll
     for (int o = 32; o >= 1; o >>= 1) cops += __shfl_xor(cops, o, kWave);
@@ -503,25 +518,25 @@ __global__ __launch_bounds__(kWave *kSmallWaves) void k_small(KParams P, const u
     const uint32_t slot = gslot - base_g;                              // record slot in the image
     if (conv) convwin[ci] = win.x;
     if (t < 4) lc[t] = 0;
+#pragma unroll
+    for (int u = 0; u < 4; u++) {
+        const int k = t + 64 * u;
+        if (k < nqc)
+            *reinterpret_cast<uint4 *>(qimg + 16 * k) = v[u];
+        else if (k < nqc + nsc)
+            unpack32(v[u], bimg + 32 * (k - nqc));
+    }
     wave_sync();
-
-    // ---- stage the family image: every chunk load in flight at once ----
+    // ---- second round trip: the converted records' reference windows ----
     {
         const int rcn = ref_chunks(max_len);
-        const int nq = (int)(img >> 4), ns = (int)(img >> 5);
-        const int total = nq + ns + nconv * rcn;
-        uint4 v[4];
+        const int total = nconv * rcn;
 #pragma unroll
         for (int u = 0; u < 4; u++) {
             const int k = t + 64 * u;
             v[u] = make_uint4(0, 0, 0, 0);
-            if (k < nq) {
-                v[u] = *reinterpret_cast<const uint4 *>(B.qual + base_g + 16 * (uint32_t)k);
-            } else if (k < nq + ns) {
-                v[u] = *reinterpret_cast<const uint4 *>(B.seq + (base_g >> 1) + 16 * (uint32_t)(k - nq));
-            } else if (k < total) {
-                const int kk = k - nq - ns;
-                const int cr = kk / rcn, part = kk - cr * rcn;
+            if (k < total) {
+                const int cr = k / rcn, part = k - cr * rcn;
                 const uint32_t wb = (convwin[cr] >> 1) & ~15u;
                 v[u] = *reinterpret_cast<const uint4 *>(P.ref + wb + 16 * (uint32_t)part);
             }
@@ -529,13 +544,8 @@ __global__ __launch_bounds__(kWave *kSmallWaves) void k_small(KParams P, const u
 #pragma unroll
         for (int u = 0; u < 4; u++) {
             const int k = t + 64 * u;
-            if (k < nq) {
-                *reinterpret_cast<uint4 *>(qimg + 16 * k) = v[u];
-            } else if (k < nq + ns) {
-                unpack32(v[u], bimg + 32 * (k - nq));
-            } else if (k < total) {
-                const int kk = k - nq - ns;
-                const int cr = kk / rcn, part = kk - cr * rcn;
+            if (k < total) {
+                const int cr = k / rcn, part = k - cr * rcn;
                 unpack32(v[u], refw + cr * ws + 32 * part);
             }
         }
@@ -833,64 +843,106 @@ __global__ __launch_bounds__(kWave *kSmallWaves) void k_small(KParams P, const u
         for (int e = 0; e < 2; e++) {
             const int sa = e == 0 ? 0 : 1, sb = e == 0 ? 3 : 2;
             const int ol = olen[e];
-            for (int c = t; c < ((ol + 63) & ~63); c += 64) {
-                const bool col = c < ol;
-                uint32_t vb[2] = {0, 0}, vq[2] = {0, 0};
-                bool slow = false;
+            // the first 4 reads of each strand stay in scalar registers for the whole end
+            const int na = hs[sa] ? cnt[sa] : 0, nb = hs[sb] ? cnt[sb] : 0;
+            uint32_t dA[4], dB[4];
 #pragma unroll
-                for (int side = 0; side < 2; side++) {
-                    const int s = side == 0 ? sa : sb;
-                    if (!hs[s]) continue;
-                    int32_t dsum = 0;
-                    uint32_t bm = 0;
-                    const int ns = cnt[s];
-                    for (int i = 0; i < ns; i += 2) {  // two reads per iteration, loads in flight together
-                        const int ra = (int)__builtin_amdgcn_readfirstlane(lists[s * 64 + i]);
-                        const bool two = i + 1 < ns;
-                        const int rb = two ? (int)__builtin_amdgcn_readfirstlane(lists[s * 64 + i + 1]) : ra;
-                        const uint32_t da = rlu(desc, ra), db = rlu(desc, rb);
-                        const bool va = col && c < (int)((da >> 16) & 0x7FFF);
-                        const bool vbb = two && col && c < (int)((db >> 16) & 0x7FFF);
-                        const uint32_t ia = (da & 0x80000000u) ? (da & 0xFFFF) - c : (da & 0xFFFF) + c;
-                        const uint32_t ib = (db & 0x80000000u) ? (db & 0xFFFF) - c : (db & 0xFFFF) + c;
-                        uint32_t ba = va ? bimg[ia] : kN, qa = va ? qimg[ia] : 0u;
-                        uint32_t bb = vbb ? bimg[ib] : kN, qb = vbb ? qimg[ib] : 0u;
-                        if (da & 0x80000000u) ba = comp_nt16(ba);
-                        if (db & 0x80000000u) bb = comp_nt16(bb);
-                        const bool oka = is_acgt(ba), okb = is_acgt(bb);
-                        const int32_t xa = lr[qa], xb = lr[qb];
-                        bm |= (oka ? ba : 0u) | (okb ? bb : 0u);
-                        dsum += (oka ? xa : 0) + (okb ? xb : 0);
+            for (int i = 0; i < 4; i++) {
+                dA[i] = i < na ? rlu(desc, (int)__builtin_amdgcn_readfirstlane(lists[sa * 64 + i])) : 0u;
+                dB[i] = i < nb ? rlu(desc, (int)__builtin_amdgcn_readfirstlane(lists[sb * 64 + i])) : 0u;
+            }
+            for (int c0 = 0; c0 < ol; c0 += 192) {
+                int cc[3];
+                bool col[3];
+                int32_t dsA[3], dsB[3];
+                uint32_t bmA[3], bmB[3];
+#pragma unroll
+                for (int k = 0; k < 3; k++) {
+                    cc[k] = c0 + t + 64 * k;
+                    col[k] = cc[k] < ol;
+                    dsA[k] = dsB[k] = 0;
+                    bmA[k] = bmB[k] = 0;
+                }
+                // one read at one column: fold its base into the one-hot OR and its likelihood into the sum
+                // (loads are unconditional at a clamped address and predicated by selects, so the
+                // compiler can keep every read of a pass in flight instead of branching per read)
+                auto acc = [&](uint32_t d, int c, bool on, int32_t &ds, uint32_t &bm) {
+                    const bool v = on && c < (int)((d >> 16) & 0x7FFF);
+                    const bool ng = d & 0x80000000u;
+                    const uint32_t idx0 = ng ? (d & 0xFFFF) - (uint32_t)c : (d & 0xFFFF) + (uint32_t)c;
+                    const uint32_t idx = v ? idx0 : 0u;
+                    const uint32_t braw = bimg[idx];
+                    const uint32_t qq = qimg[idx];
+                    const int32_t x = lr[qq];
+                    uint32_t bb = v ? braw : kN;
+                    bb = ng ? comp_nt16(bb) : bb;
+                    const bool ok = is_acgt(bb);
+                    bm |= ok ? bb : 0u;
+                    ds += ok ? x : 0;
+                };
+#pragma unroll
+                for (int i = 0; i < 4; i++) {
+                    if (i < na) {
+#pragma unroll
+                        for (int k = 0; k < 3; k++) acc(dA[i], cc[k], col[k], dsA[k], bmA[k]);
                     }
-                    if (__builtin_popcount(bm) > 1 || dsum < 0) {
-                        slow = true;
-                    } else {
-                        const int32_t d = ::min(dsum, (int32_t)((1 << 27) - 1));
-                        const int q0 = qlo[d >> 16];
-                        const int Q = q0 + (d >= dthr[q0 + 1] ? 1 : 0);
-                        vb[side] = Q < 2 ? kN : bm;
-                        vq[side] = Q < 2 ? 2u : (uint32_t)Q;
+                    if (i < nb) {
+#pragma unroll
+                        for (int k = 0; k < 3; k++) acc(dB[i], cc[k], col[k], dsB[k], bmB[k]);
                     }
                 }
-                if (col && !slow) {
-                    uint32_t ob, oq;
-                    if (hs[sa] && hs[sb]) {
-                        duplex_col(vb[0], vq[0], vb[1], vq[1], ob, oq);
-                    } else {
-                        ob = hs[sa] ? vb[0] : vb[1];
-                        oq = hs[sa] ? vq[0] : vq[1];
-                    }
-                    outb[e * ow + c] = (uint8_t)ob;
-                    outq[e * ow + c] = (uint8_t)oq;
+                for (int i = 4; i < na; i++) {
+                    const uint32_t d = rlu(desc, (int)__builtin_amdgcn_readfirstlane(lists[sa * 64 + i]));
+#pragma unroll
+                    for (int k = 0; k < 3; k++) acc(d, cc[k], col[k], dsA[k], bmA[k]);
                 }
-                const uint64_t ms = ballot(col && slow);
-                if (col && slow) sq[nq + mbcnt(ms)] = (uint16_t)((e << 15) | c);
-                nq += __builtin_popcountll(ms);
+                for (int i = 4; i < nb; i++) {
+                    const uint32_t d = rlu(desc, (int)__builtin_amdgcn_readfirstlane(lists[sb * 64 + i]));
+#pragma unroll
+                    for (int k = 0; k < 3; k++) acc(d, cc[k], col[k], dsB[k], bmB[k]);
+                }
+#pragma unroll
+                for (int k = 0; k < 3; k++) {
+                    uint32_t vb[2] = {0, 0}, vq[2] = {0, 0};
+                    bool slow = false;
+#pragma unroll
+                    for (int side = 0; side < 2; side++) {
+                        const bool present = side == 0 ? hs[sa] : hs[sb];
+                        if (!present) continue;
+                        const int32_t dsum = side == 0 ? dsA[k] : dsB[k];
+                        const uint32_t bm = side == 0 ? bmA[k] : bmB[k];
+                        if (__builtin_popcount(bm) > 1 || dsum < 0) {
+                            slow = true;
+                        } else {
+                            const int32_t d = ::min(dsum, (int32_t)((1 << 27) - 1));
+                            const int q0 = qlo[d >> 16];
+                            const int Q = q0 + (d >= dthr[q0 + 1] ? 1 : 0);
+                            vb[side] = Q < 2 ? kN : bm;
+                            vq[side] = Q < 2 ? 2u : (uint32_t)Q;
+                        }
+                    }
+                    const int c = cc[k];
+                    if (col[k] && !slow) {
+                        uint32_t ob, oq;
+                        if (hs[sa] && hs[sb]) {
+                            duplex_col(vb[0], vq[0], vb[1], vq[1], ob, oq);
+                        } else {
+                            ob = hs[sa] ? vb[0] : vb[1];
+                            oq = hs[sa] ? vq[0] : vq[1];
+                        }
+                        outb[e * ow + c] = (uint8_t)ob;
+                        outq[e * ow + c] = (uint8_t)oq;
+                    }
+                    const uint64_t ms = ballot(col[k] && slow);
+                    if (col[k] && slow) sq[nq + mbcnt(ms)] = (uint16_t)((e << 15) | c);
+                    nq += __builtin_popcountll(ms);
+                }
             }
         }
         // queued columns: the general path (all four likelihoods, up to three exp terms)
         wave_sync();
-        for (int k0 = 0; k0 < nq; k0 += 64) {
+        if (stop == 7) nq = 0;
+        for (int k0 = 0; k0 < nq && stop != 9; k0 += 64) {
             const int k = k0 + t;
             const bool act = k < nq;
             const uint32_t ent = act ? sq[k] : 0u;
@@ -942,7 +994,7 @@ __global__ __launch_bounds__(kWave *kSmallWaves) void k_small(KParams P, const u
         }
         wave_sync();
         // pack and store: lanes 0-31 end 0, lanes 32-63 end 1, 8 columns per lane
-        {
+        if (stop != 7 && stop != 8) {
             const int e = t >> 5;
             const int ol = olen[e];
             for (int c0 = 8 * (t & 31); c0 < ol; c0 += 256) {
@@ -1651,7 +1703,7 @@ int32_t bsdc_run(bsdc_ctx *c, const bsdc_family_batch *b, bsdc_consensus *o, int
                                    b->small_arena[q]);
                 HIP_OK(c, hipGetLastError());
             }
-            f += nf;
+            f += 4 * nf;
         }
     }
     if (b->n_large > 0 && !(mode & BSDC_MODE_SKIP_LARGE)) {

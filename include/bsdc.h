@@ -73,7 +73,9 @@ typedef struct {
     const int32_t *rt;           /* [4*n_rec] RT records only: next_pos, tlen, mate unclipped start, end */
     const uint8_t *seq;
     const uint8_t *qual;
-    const uint32_t *small_fams;  /* families processed one wavefront each, 4 consecutive buckets */
+    const uint32_t *small_fams;  /* families processed one wavefront each, 4 consecutive buckets;
+                                    4 words per family: family, first record,
+                                    n_rec | (image bytes / 32) << 8, image base (first slot) */
     int64_t n_small[4];          /* families per bucket */
     int32_t small_arena[4];      /* LDS bytes per wavefront of each bucket (multiple of 16) */
     const uint32_t *large_fams;  /* families processed one workgroup each */

@@ -13,7 +13,9 @@ from bsseqconsensusreads_amd import batch as B, synth  # noqa: E402
 from bsseqconsensusreads_amd._lib import MODE_CONVERT, MODE_EXTEND, MODE_VOTE, MODE_SKIP_LARGE  # noqa: E402
 from bsseqconsensusreads_amd.device import Engine  # noqa: E402
 
-PHASES = ["staging", "convert", "extend", "overlap", "srcreads+lists", "ss-vote", "full"]
+# (name, stop code): the kernel returns after the named phase
+PHASES = [("staging", 1), ("convert", 2), ("extend", 3), ("overlap", 4), ("srcreads+lists", 5),
+          ("vote-preamble", 6), ("vote-main", 7), ("vote-queue", 8), ("full", 0)]
 
 ap = argparse.ArgumentParser()
 ap.add_argument("--config", default="C2")
@@ -28,8 +30,8 @@ eng.load_reference(s.ref)
 db = eng.upload(fb)
 st = torch.cuda.current_stream()
 out = {}
-for k, name in enumerate(PHASES, start=1):
-    mode = MODE_CONVERT | MODE_EXTEND | MODE_VOTE | MODE_SKIP_LARGE | ((k % 7) << 8)
+for name, code in PHASES:
+    mode = MODE_CONVERT | MODE_EXTEND | MODE_VOTE | MODE_SKIP_LARGE | (code << 8)
     for _ in range(2):
         eng.run(db, mode, st)
     e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
