@@ -152,11 +152,16 @@ def main():
     bytes_small = algorithmic_bytes(fb, out["len"], out["status"], small)
     bytes_all = algorithmic_bytes(fb, out["len"], out["status"], np.arange(fb.n_fam))
     achieved = bytes_small / t_small / 1e9
+    # HBM bytes of one k_small launch set (one dispatch per non-empty LDS bucket), from the PMC
+    # passes of profiles/collect_pmc.sh on this same workload (FETCH_SIZE x2 + WRITE_SIZE,
+    # MI355X_MICROARCH.md HBM section); null when no summary for this config is committed
     traffic = None
     pmc = os.path.join(ROOT, "profiles", "pmc_%s.json" % args.config)
-    if os.path.exists(pmc):
+    if os.path.exists(pmc) and args.families == 1_000_000 and args.seed == 42:
         with open(pmc) as fh:
-            traffic = json.load(fh).get("k_small_hbm_bytes_per_launch")
+            per = json.load(fh).get("k_small", {}).get("hbm_bytes_per_dispatch")
+        if per is not None:
+            traffic = int(per * sum(1 for b in fb.small_buckets if b.shape[0]))
 
     cpu = None
     if rank == 0 and world == 1 and args.cpu_sample > 0:

@@ -9,7 +9,7 @@ d = sys.argv[1]
 PH = ["staging", "convert", "extend", "overlap", "srcreads+lists", "vote-preamble", "vote-main", "vote-queue", "full"]
 RUNS = 12  # 2 warmup + 10 timed per phase
 res = collections.defaultdict(lambda: collections.defaultdict(float))
-for f in sorted(glob.glob(d + "/p*/pmc_counter_collection.csv")):
+for f in sorted(glob.glob(d + "/p*/**/*counter_collection.csv", recursive=True)):
     rows = list(csv.DictReader(open(f)))
     disp = sorted({int(r["Dispatch_Id"]) for r in rows})
     per = collections.defaultdict(lambda: collections.defaultdict(float))
