@@ -7,7 +7,8 @@ import os
 HERE = os.path.dirname(os.path.abspath(__file__))
 LIB_PATH = os.path.join(HERE, "libbsdc.so")
 
-BSDC_ABI_VERSION = 2
+BSDC_ABI_VERSION = 3
+SMALL_BUCKETS = 8  # BSDC_SMALL_BUCKETS
 MODE_CONVERT, MODE_EXTEND, MODE_VOTE, MODE_DUMP = 1, 2, 4, 8
 MODE_SKIP_SMALL, MODE_SKIP_LARGE = 16, 32
 
@@ -23,7 +24,7 @@ class FamilyBatchC(C.Structure):
                 ("fam_off", C.c_void_p), ("rec", C.c_void_p), ("rec_win", C.c_void_p),
                 ("cig_off", C.c_void_p), ("cig_info", C.c_void_p), ("cigar", C.c_void_p),
                 ("rt", C.c_void_p), ("seq", C.c_void_p), ("qual", C.c_void_p),
-                ("small_fams", C.c_void_p), ("n_small", C.c_int64 * 4), ("small_arena", C.c_int32 * 4),
+                ("small_fams", C.c_void_p), ("n_small", C.c_int64 * SMALL_BUCKETS), ("small_arena", C.c_int32 * SMALL_BUCKETS),
                 ("large_fams", C.c_void_p), ("n_large", C.c_int64), ("large_arena", C.c_int32),
                 ("max_len", C.c_int32)]
 

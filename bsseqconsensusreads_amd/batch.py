@@ -38,9 +38,9 @@ LINK_USABLE = 1 << 26
 MODE_CONVERT, MODE_EXTEND, MODE_VOTE, MODE_DUMP = 1, 2, 4, 8
 
 # small families run one per wavefront with their arena in LDS, in buckets of these arena sizes
-SMALL_BUCKETS = (4096, 6144, 8192, 12288)
-SMALL_ARENA_CAP = 12288
-LDS_TABLES = 1024 + 384 + 2048 + 192
+SMALL_BUCKETS = (3072, 4096, 5120, 6144, 8192, 12288, 16384, 24576)  # BSDC_SMALL_BUCKETS classes
+SMALL_ARENA_CAP = 24576
+LDS_TABLES = 1024 + 1024 + 384 + 2048 + 192  # kTabBytes (csrc/bsdc_kernels.hip)
 LARGE_LDS_CAP = 64 * 1024 - LDS_TABLES
 
 
@@ -53,20 +53,19 @@ def ref_chunks(max_len):
     return (15 + (int(max_len) + 4) // 2 + 15) // 16
 
 
-def small_chunks(img, nconv, max_len):
-    img = np.asarray(img, dtype=np.int64)
-    return img // 16 + img // 32 + np.asarray(nconv, dtype=np.int64) * ref_chunks(max_len)
-
-
 def small_arena_bytes(n, img, nconv, complex_ops, max_len):
-    """Mirror of SmallLayout (csrc/bsdc_kernels.hip) / bsdc_small_arena_bytes."""
+    """Mirror of SmallLayout (csrc/bsdc_kernels.hip) / bsdc_small_arena_bytes: the image, the
+    descriptors, lc[4], then the largest of the phase-local regions sharing one span."""
     n = np.asarray(n, dtype=np.int64)
     ws = 32 * ref_chunks(max_len)
     cops = np.asarray(complex_ops, dtype=np.int64)
     ow = int(round16(int(max_len) + 2))
-    total = 2 * np.asarray(img, dtype=np.int64) + np.asarray(nconv, dtype=np.int64) * ws + 256 \
-        + round16(16 * n) + 160 + 8 * ow + 256
-    return total + np.where(cops > 0, round16(4 * (cops + 4 * n)), 0)
+    R = 2 * np.asarray(img, dtype=np.int64) + round16(4 * n) + 16
+    e_ref = R + np.asarray(nconv, dtype=np.int64) * ws
+    simp = R + round16(16 * n) + round16(n) + 2 * round16(2 * n)
+    e_f = simp + np.where(cops > 0, round16(4 * (cops + 4 * n)), 0)
+    e_v = R + 8 * ow
+    return np.maximum(np.maximum(e_ref, e_f), e_v)
 
 
 def large_arena_bytes(n, slot_bytes, max_len, complex_ops):
@@ -482,11 +481,8 @@ def build_family_batch(raw: R.RawRecords, mode: str = "full", ref: Optional[R.Re
     cops = np.bincount(fam_of, weights=cnt_c, minlength=nf)[:nf].astype(np.int64) if nr else np.zeros(nf, np.int64)
     nconv = np.bincount(fam_of, weights=convb.astype(np.int64), minlength=nf)[:nf].astype(np.int64) if nr else np.zeros(nf, np.int64)
     need_s = small_arena_bytes(fam_sizes, img, nconv, cops, max_len)
-    chunks = small_chunks(img, nconv, max_len)
     need_l = large_arena_bytes(fam_sizes, 2 * span, max_len_f, cops)
-    qs_chunks = img // 16 + img // 32
-    ref_c = nconv * ref_chunks(max_len)
-    small = (fam_sizes <= 64) & (qs_chunks <= 256) & (ref_c <= 256) & (need_s <= small_cap) & (img // 32 < (1 << 24))
+    small = (fam_sizes <= 64) & (need_s <= small_cap) & (img // 32 < (1 << 24))
     buckets, arenas = [], []
     lo = -1
     for cap in SMALL_BUCKETS:
@@ -498,7 +494,7 @@ def build_family_batch(raw: R.RawRecords, mode: str = "full", ref: Optional[R.Re
         lo = cap
         if cap == small_cap:
             break
-    while len(buckets) < 4:
+    while len(buckets) < len(SMALL_BUCKETS):
         buckets.append(np.zeros(0, np.uint32))
         arenas.append(16)
     large_fams = np.nonzero(~small)[0].astype(np.uint32)

@@ -23,6 +23,7 @@
 // so any summation order is bit-identical to the CPU restatement (oracle/).
 #include <hip/hip_runtime.h>
 
+#include <algorithm>
 #include <cmath>
 #include <cstdio>
 #include <cstdlib>
@@ -35,15 +36,19 @@ namespace {
 
 constexpr int kWave = 64;
 constexpr int kLargeThreads = 256;
-constexpr int kSmallWaves = 4;                 // wavefronts (families) per small-kernel workgroup
+constexpr int kSmallMaxWaves = 8;              // wavefronts (families) per small-kernel workgroup, at most
+constexpr int kSmallMinWaves = 6;              // occupancy target (waves per SIMD) the register budget is cut for
+constexpr int kLdsBytes = 160 * 1024;           // LDS per CU
 constexpr double kLrScale = 1048576.0;          // 2^20
-constexpr int kTabBytes = 1024 + 384 + 2048 + 192;  // the Tables image in LDS
+constexpr int kTabBytes = 1024 + 1024 + 384 + 2048 + 192;  // the Tables image in LDS
+// k_small base bytes in LDS: nt16 code | 0x10 for A, C, G, T (set at staging, see valid4)
 constexpr uint32_t kLinkRdDev = 1u << 27;       // device-internal: tool 1 trimmed a base (RD=1)
 
 // nt16 codes
 constexpr uint32_t kA = 1, kC = 2, kG = 4, kT = 8, kN = 15;
 
 struct Tables {
+    int32_t zero[256];  // row 0 of the vote's [valid][q] table: a non-ACGT base adds nothing
     int32_t lr[256];    // round((ln(1-a) - ln(a/3)) * 2^20), a = P(error) of a Q base after the post-UMI step
     float thr[96];      // Q >= k  <=>  S <= thr[k]
     uint8_t qlo[2048];  // agreement case (S = 3 e^-D): Q at D = 2^16 k
@@ -329,6 +334,8 @@ struct KParams {
     const Tables *tab;
     int32_t mode;
     int32_t overlap;
+    int32_t ref_chunks;       // 16-B chunks per reference window (ref_chunks(max_len))
+    uint32_t ref_chunks_inv;  // ceil(2^32 / ref_chunks)
 };
 
 __device__ __forceinline__ void load_tables(const Tables *tab, uint8_t *dst) {
@@ -368,8 +375,14 @@ __device__ __forceinline__ void duplex_col(uint32_t xb, uint32_t xq, uint32_t yb
 // ==========================================================================================
 // k_small: one wavefront per family, everything in LDS
 // ==========================================================================================
+// Arena of one small family.  Regions live only as long as their phase and share space:
+//   bimg, qimg  the family image, bases / quals (whole kernel)
+//   lists       reference-window starts (staging) -> read descriptors (vote), 4 B per record
+//   misc        consensus lengths lc[4]
+//   R           reference windows (staging, convert) | alignment-filter scratch (source reads) |
+//               duplex rows + queued columns (vote)
 struct SmallLayout {
-    uint32_t bimg, qimg, ref, lists, meta, misc, outb, outq, squeue, descs, simp, total;
+    uint32_t bimg, qimg, lists, misc, ref, meta, setv, ordv, srcl, simp, outb, outq, squeue, total;
     int32_t ws, ow;
     __host__ __device__ SmallLayout(int n, int64_t img, int nconv, int64_t cops, int max_len) {
         ws = 32 * ref_chunks(max_len);
@@ -379,25 +392,25 @@ struct SmallLayout {
         o += img;
         qimg = (uint32_t)o;
         o += img;
-        ref = (uint32_t)o;
-        o += (int64_t)nconv * ws;
-        lists = (uint32_t)o;  // 4 x 64 record indices (u8)
-        o += 256;
-        meta = (uint32_t)o;   // SMeta per record (serial filter only)
-        o += round16(16 * (int64_t)n);
-        misc = (uint32_t)o;   // lc[4] u32 | srclen[64] u16 (serial filter only)
-        o += 160;
-        outb = (uint32_t)o;   // duplex bases, 2 ends
-        o += 2 * (int64_t)ow;
-        outq = (uint32_t)o;   // duplex quals, 2 ends
-        o += 2 * (int64_t)ow;
-        squeue = (uint32_t)o; // queued (end, column) of disagreeing columns
-        o += 4 * (int64_t)ow;
-        descs = (uint32_t)o;  // per-record source descriptor (queued path)
-        o += 256;
-        simp = (uint32_t)o;   // simplified cigars (serial filter only)
-        if (cops > 0) o += round16(4 * (cops + 4 * (int64_t)n));
-        total = (uint32_t)o;
+        lists = (uint32_t)o;
+        o += round16(4 * (int64_t)n);
+        misc = (uint32_t)o;
+        o += 16;
+        const int64_t R = o;
+        ref = (uint32_t)R;
+        const int64_t e_ref = R + (int64_t)nconv * ws;
+        meta = (uint32_t)R;  // SMeta per record
+        setv = meta + (uint32_t)round16(16 * (int64_t)n);
+        ordv = setv + (uint32_t)round16(n);
+        srcl = ordv + (uint32_t)round16(2 * (int64_t)n);
+        simp = srcl + (uint32_t)round16(2 * (int64_t)n);
+        const int64_t e_f = (int64_t)simp + (cops > 0 ? round16(4 * (cops + 4 * (int64_t)n)) : 0);
+        outb = (uint32_t)R;  // duplex bases, 2 ends
+        outq = (uint32_t)(R + 2 * (int64_t)ow);
+        squeue = (uint32_t)(R + 4 * (int64_t)ow);  // queued (end, column), u16
+        const int64_t e_v = R + 8 * (int64_t)ow;
+        int64_t e = e_ref > e_f ? e_ref : e_f;
+        total = (uint32_t)(e > e_v ? e : e_v);
     }
 };
 
@@ -426,14 +439,45 @@ __device__ __forceinline__ void st32(uint8_t *p, uint32_t v) { *reinterpret_cast
 __device__ __forceinline__ uint32_t alignbyte(uint32_t hi, uint32_t lo, uint32_t s) {
     return __builtin_amdgcn_alignbyte(hi, lo, s);
 }
-// 16 packed bytes (32 nibbles, high first) -> 32 bytes
+// unaligned LDS dword (gfx950 LDS runs in unaligned mode: one ds_read_b32)
+__device__ __forceinline__ uint32_t ldsu32(const uint8_t *p) {
+    uint32_t v;
+    __builtin_memcpy(&v, p, 4);
+    return v;
+}
+// D0..D3 += lr2[v_j][q_j] for the 4 bytes of b (base bytes, kValid flag = v) and q (quals).  The
+// index (v << 8 | q) * 4 is built two columns at a time: v_perm interleaves [q_j, v_j] into 16-bit
+// halves (<= 511, so one 32-bit shift scales both halves).
+__device__ __forceinline__ void lookup4(const int32_t *lr2, uint32_t b, uint32_t q, int32_t &D0, int32_t &D1,
+                                        int32_t &D2, int32_t &D3) {
+    const uint32_t v = (b >> 4) & 0x01010101u;
+    const uint32_t lo = __builtin_amdgcn_perm(v, q, 0x05010400u) << 2;
+    const uint32_t hi = __builtin_amdgcn_perm(v, q, 0x07030602u) << 2;
+    const uint8_t *base = reinterpret_cast<const uint8_t *>(lr2);
+    D0 += *reinterpret_cast<const int32_t *>(base + (lo & 0xFFFFu));
+    D1 += *reinterpret_cast<const int32_t *>(base + (lo >> 16));
+    D2 += *reinterpret_cast<const int32_t *>(base + (hi & 0xFFFFu));
+    D3 += *reinterpret_cast<const int32_t *>(base + (hi >> 16));
+}
+// htsjdk complement of one-hot codes in every byte (nibble bit reversal; 0 stays 0)
+__device__ __forceinline__ uint32_t comp4(uint32_t x) {
+    return (__builtin_bitreverse32(__builtin_bswap32(x)) >> 4) & 0x0F0F0F0Fu;
+}
+// kValid in every byte holding A, C, G or T (a one-hot nt16 code), 0 elsewhere (bytes hold 0..15)
+__device__ __forceinline__ uint32_t valid4(uint32_t x) {
+    const uint32_t z = x & ((x | 0x10101010u) - 0x01010101u);  // per byte x & (x - 1)
+    return (((x + 0x7F7F7F7Fu) & ~(z + 0x7F7F7F7Fu)) & 0x80808080u) >> 3;  // x != 0 and z == 0
+}
+// 16 packed bytes (32 nibbles, high first) -> 32 base bytes, each = code | kValid if A/C/G/T
 __device__ __forceinline__ void unpack32(uint4 v, uint8_t *dst) {
     const uint32_t w[4] = {v.x, v.y, v.z, v.w};
     uint32_t o[8];
 #pragma unroll
     for (int k = 0; k < 4; k++) {
-        const uint32_t lo = w[k] & 0x0F0F0F0Fu;
-        const uint32_t hi = (w[k] >> 4) & 0x0F0F0F0Fu;
+        uint32_t lo = w[k] & 0x0F0F0F0Fu;
+        uint32_t hi = (w[k] >> 4) & 0x0F0F0F0Fu;
+        lo |= valid4(lo);
+        hi |= valid4(hi);
         o[2 * k] = __builtin_amdgcn_perm(lo, hi, 0x05010400u);
         o[2 * k + 1] = __builtin_amdgcn_perm(lo, hi, 0x07030602u);
     }
@@ -442,18 +486,18 @@ __device__ __forceinline__ void unpack32(uint4 v, uint8_t *dst) {
     d[1] = make_uint4(o[4], o[5], o[6], o[7]);
 }
 
-__global__ __launch_bounds__(kWave *kSmallWaves) void k_small(KParams P, const uint32_t *fams, int64_t nfams,
+__global__ __launch_bounds__(kWave *kSmallMaxWaves, kSmallMinWaves) void k_small(KParams P, const uint32_t *fams, int64_t nfams,
                                                               int32_t arena) {
     extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
     const Tables *T = reinterpret_cast<const Tables *>(smem);
-    const int32_t *lr = T->lr;
+    const int32_t *lr2 = T->zero;  // [2][256]: row (base byte >> 4) = 1 for A/C/G/T
     const float *thr = T->thr;
     const uint8_t *qlo = T->qlo;
     const int32_t *dthr = T->dthr;
     load_tables(P.tab, smem);
     const int w = threadIdx.x >> 6;
     const int t = threadIdx.x & 63;
-    const int64_t fi = (int64_t)blockIdx.x * kSmallWaves + w;
+    const int64_t fi = (int64_t)blockIdx.x * (blockDim.x >> 6) + w;
     if (fi >= nfams) return;
     uint8_t *A = smem + kTabBytes + (size_t)w * (size_t)arena;
     const bsdc_family_batch &B = P.B;
@@ -471,26 +515,39 @@ __global__ __launch_bounds__(kWave *kSmallWaves) void k_small(KParams P, const u
     const uint32_t img = (__builtin_amdgcn_readfirstlane(ent.z) >> 8) * 32u;
     const uint32_t base_g = __builtin_amdgcn_readfirstlane(ent.w);
 
-    // ---- one round trip: record metadata, windows and every image chunk ----
+    // ---- staging: record metadata and every 16-byte chunk of the image, then the converted
+    // records' reference windows; up to 4 chunk loads per lane in flight per round ----
     const bool has = t < n;
     uint4 rc = make_uint4(0, 0, 0, 0);
     uint2 win = make_uint2(0, 0);
     uint32_t cinfo = 0;
-    const int nqc = (int)(img >> 4), nsc = (int)(img >> 5);  // qual chunks, packed-base chunks
-    uint4 v[4];
+    const int nqc = (int)(img >> 4), nch = nqc + (int)(img >> 5);  // qual chunks, + packed-base chunks
+    uint8_t *bimg = A;          // SmallLayout: bimg = 0, qimg = img
+    uint8_t *qimg = A + img;
+    for (int k0 = 0; k0 < nch; k0 += 256) {
+        uint4 v[4];
 #pragma unroll
-    for (int u = 0; u < 4; u++) {
-        const int k = t + 64 * u;
-        v[u] = make_uint4(0, 0, 0, 0);
-        if (k < nqc)
-            v[u] = *reinterpret_cast<const uint4 *>(B.qual + base_g + 16 * (uint32_t)k);
-        else if (k < nqc + nsc)
-            v[u] = *reinterpret_cast<const uint4 *>(B.seq + (base_g >> 1) + 16 * (uint32_t)(k - nqc));
-    }
-    if (has) {
-        rc = reinterpret_cast<const uint4 *>(B.rec)[r0 + t];
-        win = reinterpret_cast<const uint2 *>(B.rec_win)[r0 + t];
-        cinfo = B.cig_info[r0 + t];
+        for (int u = 0; u < 4; u++) {
+            const int k = k0 + t + 64 * u;
+            v[u] = make_uint4(0, 0, 0, 0);
+            if (k < nqc)
+                v[u] = *reinterpret_cast<const uint4 *>(B.qual + base_g + 16 * (uint32_t)k);
+            else if (k < nch)
+                v[u] = *reinterpret_cast<const uint4 *>(B.seq + (base_g >> 1) + 16 * (uint32_t)(k - nqc));
+        }
+        if (k0 == 0 && has) {
+            rc = reinterpret_cast<const uint4 *>(B.rec)[r0 + t];
+            win = reinterpret_cast<const uint2 *>(B.rec_win)[r0 + t];
+            cinfo = B.cig_info[r0 + t];
+        }
+#pragma unroll
+        for (int u = 0; u < 4; u++) {
+            const int k = k0 + t + 64 * u;
+            if (k < nqc)
+                *reinterpret_cast<uint4 *>(qimg + 16 * k) = v[u];
+            else if (k < nch)
+                unpack32(v[u], bimg + 32 * (k - nqc));
+        }
     }
     const uint32_t gslot = rc.x;
     int32_t pos = (int32_t)rc.y;
@@ -508,45 +565,38 @@ __global__ __launch_bounds__(kWave *kSmallWaves) void k_small(KParams P, const u
 #pragma unroll
     for (int o = 32; o >= 1; o >>= 1) cops += __shfl_xor(cops, o, kWave);
     const SmallLayout Lo(n, img, nconv, cops, max_len);
-    uint8_t *bimg = A + Lo.bimg;
-    uint8_t *qimg = A + Lo.qimg;
     uint8_t *refw = A + Lo.ref;
     const int ws = Lo.ws;
     uint32_t *lc = reinterpret_cast<uint32_t *>(A + Lo.misc);
-    uint16_t *srcl = reinterpret_cast<uint16_t *>(A + Lo.misc + 16);
-    uint32_t *convwin = reinterpret_cast<uint32_t *>(A + Lo.lists);  // temporary, before the lists exist
+    uint32_t *convwin = reinterpret_cast<uint32_t *>(A + Lo.lists);  // until the descriptors exist
     const uint32_t slot = gslot - base_g;                              // record slot in the image
     if (conv) convwin[ci] = win.x;
     if (t < 4) lc[t] = 0;
-#pragma unroll
-    for (int u = 0; u < 4; u++) {
-        const int k = t + 64 * u;
-        if (k < nqc)
-            *reinterpret_cast<uint4 *>(qimg + 16 * k) = v[u];
-        else if (k < nqc + nsc)
-            unpack32(v[u], bimg + 32 * (k - nqc));
-    }
     wave_sync();
-    // ---- second round trip: the converted records' reference windows ----
     {
-        const int rcn = ref_chunks(max_len);
-        const int total = nconv * rcn;
+        // chunk k -> (converted record k / rcn, part k % rcn); rcn and its 2^32 reciprocal are
+        // launch constants (floor(k * rinv / 2^32) is exact for k, rcn < 2^16)
+        const uint32_t rcn = (uint32_t)P.ref_chunks, rinv = P.ref_chunks_inv;
+        const int total = nconv * (int)rcn;
+        for (int k0 = 0; k0 < total; k0 += 256) {
+            uint4 v[4];
 #pragma unroll
-        for (int u = 0; u < 4; u++) {
-            const int k = t + 64 * u;
-            v[u] = make_uint4(0, 0, 0, 0);
-            if (k < total) {
-                const int cr = k / rcn, part = k - cr * rcn;
-                const uint32_t wb = (convwin[cr] >> 1) & ~15u;
-                v[u] = *reinterpret_cast<const uint4 *>(P.ref + wb + 16 * (uint32_t)part);
+            for (int u = 0; u < 4; u++) {
+                const int k = k0 + t + 64 * u;
+                v[u] = make_uint4(0, 0, 0, 0);
+                if (k < total) {
+                    const uint32_t cr = __umulhi((uint32_t)k, rinv), part = (uint32_t)k - cr * rcn;
+                    const uint32_t wb = (convwin[cr] >> 1) & ~15u;
+                    v[u] = *reinterpret_cast<const uint4 *>(P.ref + wb + 16 * part);
+                }
             }
-        }
 #pragma unroll
-        for (int u = 0; u < 4; u++) {
-            const int k = t + 64 * u;
-            if (k < total) {
-                const int cr = k / rcn, part = k - cr * rcn;
-                unpack32(v[u], refw + cr * ws + 32 * part);
+            for (int u = 0; u < 4; u++) {
+                const int k = k0 + t + 64 * u;
+                if (k < total) {
+                    const uint32_t cr = __umulhi((uint32_t)k, rinv), part = (uint32_t)k - cr * rcn;
+                    unpack32(v[u], refw + cr * ws + 32 * part);
+                }
             }
         }
     }
@@ -589,10 +639,12 @@ __global__ __launch_bounds__(kWave *kSmallWaves) void k_small(KParams P, const u
                 uint32_t nxt = 0x0F0F0F0Fu;
                 const int last = Lm - 1 - j4;  // the record's last position has no next base
                 if (last >= 0 && last < 4) nxt &= ~(0xFFu << (8 * last));
-                const uint32_t out = convert4(m, m1, f0, f1, nxt);
+                // A->G, C->T keep a base A/C/G/T, so the kValid flags of m carry over
+                const uint32_t out = convert4(m & 0x0F0F0F0Fu, m1 & 0x0F0F0F0Fu, f0 & 0x0F0F0F0Fu, f1 & 0x0F0F0F0Fu, nxt) |
+                                     (m & 0x10101010u);
                 st32(bimg + s_slot + j4, out);
                 if (last >= 0 && last < 4) {  // :157-170 a final C before a reference G is trimmed
-                    my_rd = ((out >> (8 * last)) & 0xFF) == kC && ((f1 >> (8 * last)) & 0xFF) == kG;
+                    my_rd = ((out >> (8 * last)) & 0x0F) == kC && ((f1 >> (8 * last)) & 0x0F) == kG;
                 }
             }
             const bool s_rd = ballot(my_rd) != 0;
@@ -661,7 +713,7 @@ __global__ __launch_bounds__(kWave *kSmallWaves) void k_small(KParams P, const u
             const uint32_t s_slot = rlu(slot, r), s_g = rlu(gslot, r);
             const int32_t s_start = rl(start, r), s_len = rl(len, r);
             for (int j = t; j < s_len; j += 64) {
-                P.O.dump_seq[s_g + j] = bimg[s_slot + s_start + j];
+                P.O.dump_seq[s_g + j] = bimg[s_slot + s_start + j] & 0x0F;
                 P.O.dump_qual[s_g + j] = qimg[s_slot + s_start + j];
             }
         }
@@ -754,8 +806,9 @@ __global__ __launch_bounds__(kWave *kSmallWaves) void k_small(KParams P, const u
     // ---- most-common-alignment filter (only families with a non-M-only cigar; serial) ----
     if (ballot(cplx && set != 0xFF)) {
         SMeta *meta = reinterpret_cast<SMeta *>(A + Lo.meta);
-        uint8_t *setv = A + Lo.lists;                                      // 64 B scratch
-        uint16_t *ordv = reinterpret_cast<uint16_t *>(A + Lo.lists + 64);  // 64 x u16 scratch
+        uint8_t *setv = A + Lo.setv;
+        uint16_t *ordv = reinterpret_cast<uint16_t *>(A + Lo.ordv);
+        uint16_t *srcl = reinterpret_cast<uint16_t *>(A + Lo.srcl);
         if (has) {
             meta[t].gidx = r0 + t;
             meta[t].pos = pos;
@@ -797,14 +850,24 @@ __global__ __launch_bounds__(kWave *kSmallWaves) void k_small(KParams P, const u
         wave_sync();
     }
 
-    // ---- per-set read lists (family order) and consensus lengths ----
-    uint8_t *lists = A + Lo.lists;  // 4 x 64 record indices
-    int cnt[4];
+    // ---- read descriptors by set (forward reads first) and consensus lengths ----
+    // R1 = AB-R1 + BA-R2, R2 = AB-R2 + BA-R1.  Descriptor of a source read: its column c is image
+    // byte sbase + c (forward) or sbase - c (reverse); srclen < 2^15.
+    const uint32_t sbase = slot + start + (neg ? (uint32_t)(len - 1) : 0u);
+    const uint32_t desc = sbase | ((uint32_t)srclen << 16) | (neg ? 0x80000000u : 0u);
+    uint32_t *dlist = reinterpret_cast<uint32_t *>(A + Lo.lists);  // <= 64 descriptors, set by set
+    int cnt[4], nfw[4], off[4];
+    {
+        int o = 0;
 #pragma unroll
-    for (int s = 0; s < 4; s++) {
-        const uint64_t ms = ballot(set == (uint32_t)s);
-        cnt[s] = __builtin_popcountll(ms);
-        if (set == (uint32_t)s) lists[s * 64 + mbcnt(ms)] = (uint8_t)t;
+        for (int s = 0; s < 4; s++) {
+            const uint64_t mf = ballot(set == (uint32_t)s && !neg), mr = ballot(set == (uint32_t)s && neg);
+            nfw[s] = __builtin_popcountll(mf);
+            cnt[s] = nfw[s] + __builtin_popcountll(mr);
+            off[s] = o;
+            if (set == (uint32_t)s) dlist[o + (neg ? nfw[s] + mbcnt(mr) : mbcnt(mf))] = desc;
+            o += cnt[s];
+        }
     }
     if (set != 0xFF) atomicMax(&lc[set], (uint32_t)srclen);
     wave_sync();
@@ -813,16 +876,14 @@ __global__ __launch_bounds__(kWave *kSmallWaves) void k_small(KParams P, const u
     for (int s = 0; s < 4; s++) lcs[s] = (int)__builtin_amdgcn_readfirstlane(lc[s]);
     if (stop == 5) return;
 
-    // ---- single-strand vote + duplex combine, per end; lane = consensus column ----
-    // R1 = AB-R1 + BA-R2, R2 = AB-R2 + BA-R1.  A read's source position c is image byte
-    // sbase + c (forward) or sbase - c (reverse).  Fast path: every read that covers the column
-    // shows the same base (OR of one-hot codes has <= 1 bit) -> the vote is a function of the
-    // likelihood sum alone, looked up exactly (Tables::qlo / dthr).  Columns where reads disagree
-    // are queued and run through the general four-likelihood path once per family.
-    const uint32_t sbase = slot + start + (neg ? (uint32_t)(len - 1) : 0u);
-    const uint32_t desc = sbase | ((uint32_t)srclen << 16) | (neg ? 0x80000000u : 0u);  // srclen < 2^15
-    uint32_t *descs = reinterpret_cast<uint32_t *>(A + Lo.descs);
-    descs[t] = desc;  // published for the queued path (ds_bpermute cannot read inactive lanes)
+    // ---- single-strand vote + duplex combine, per end ----
+    // A lane owns 4 consecutive columns of one end.  Per read it loads their 4 bases and 4 quals as
+    // one (unaligned) LDS dword each -- the dword ending at sbase - c for a reverse read, whose
+    // bytes run backwards --, clears the bases of columns past the read's end, ORs the one-hot
+    // bases, and adds Tables::lr2[base][qual] for each column: rows of non-ACGT codes (and the
+    // cleared 0) are zero, so no per-base test is needed.  A column where each side's reads agree
+    // (OR has <= 1 bit set) is resolved from its sum alone (Tables::qlo / dthr); the rest (any
+    // disagreement, any N, a negative sum) are queued for the general four-likelihood path.
     bool hs[4];
 #pragma unroll
     for (int s = 0; s < 4; s++) hs[s] = cnt[s] > 0;
@@ -841,101 +902,79 @@ __global__ __launch_bounds__(kWave *kSmallWaves) void k_small(KParams P, const u
         uint16_t *sq = reinterpret_cast<uint16_t *>(A + Lo.squeue);
         int nq = 0;
         for (int e = 0; e < 2; e++) {
-            const int sa = e == 0 ? 0 : 1, sb = e == 0 ? 3 : 2;
             const int ol = olen[e];
-            // the first 4 reads of each strand stay in scalar registers for the whole end
-            const int na = hs[sa] ? cnt[sa] : 0, nb = hs[sb] ? cnt[sb] : 0;
-            uint32_t dA[4], dB[4];
+            for (int c0 = 0; c0 < ol; c0 += 256) {
+                const int c = c0 + 4 * t;
+                int32_t D[2][4] = {{0, 0, 0, 0}, {0, 0, 0, 0}};
+                uint32_t mf[2] = {0, 0}, mr[2] = {0, 0};  // one-hot ORs of forward / reverse reads
+                if (c < ol) {
 #pragma unroll
-            for (int i = 0; i < 4; i++) {
-                dA[i] = i < na ? rlu(desc, (int)__builtin_amdgcn_readfirstlane(lists[sa * 64 + i])) : 0u;
-                dB[i] = i < nb ? rlu(desc, (int)__builtin_amdgcn_readfirstlane(lists[sb * 64 + i])) : 0u;
-            }
-            for (int c0 = 0; c0 < ol; c0 += 192) {
-                int cc[3];
-                bool col[3];
-                int32_t dsA[3], dsB[3];
-                uint32_t bmA[3], bmB[3];
-#pragma unroll
-                for (int k = 0; k < 3; k++) {
-                    cc[k] = c0 + t + 64 * k;
-                    col[k] = cc[k] < ol;
-                    dsA[k] = dsB[k] = 0;
-                    bmA[k] = bmB[k] = 0;
-                }
-                // one read at one column: fold its base into the one-hot OR and its likelihood into the sum
-                // (loads are unconditional at a clamped address and predicated by selects, so the
-                // compiler can keep every read of a pass in flight instead of branching per read)
-                auto acc = [&](uint32_t d, int c, bool on, int32_t &ds, uint32_t &bm) {
-                    const bool v = on && c < (int)((d >> 16) & 0x7FFF);
-                    const bool ng = d & 0x80000000u;
-                    const uint32_t idx0 = ng ? (d & 0xFFFF) - (uint32_t)c : (d & 0xFFFF) + (uint32_t)c;
-                    const uint32_t idx = v ? idx0 : 0u;
-                    const uint32_t braw = bimg[idx];
-                    const uint32_t qq = qimg[idx];
-                    const int32_t x = lr[qq];
-                    uint32_t bb = v ? braw : kN;
-                    bb = ng ? comp_nt16(bb) : bb;
-                    const bool ok = is_acgt(bb);
-                    bm |= ok ? bb : 0u;
-                    ds += ok ? x : 0;
-                };
-#pragma unroll
-                for (int i = 0; i < 4; i++) {
-                    if (i < na) {
-#pragma unroll
-                        for (int k = 0; k < 3; k++) acc(dA[i], cc[k], col[k], dsA[k], bmA[k]);
-                    }
-                    if (i < nb) {
-#pragma unroll
-                        for (int k = 0; k < 3; k++) acc(dB[i], cc[k], col[k], dsB[k], bmB[k]);
+                    for (int side = 0; side < 2; side++) {
+                        const int s = side == 0 ? (e == 0 ? 0 : 1) : (e == 0 ? 3 : 2);
+                        const uint32_t *dl = dlist + off[s];
+                        for (int i = 0; i < nfw[s]; i++) {
+                            const uint32_t d = __builtin_amdgcn_readfirstlane(dl[i]);
+                            const uint32_t k8 = (uint32_t)::min(::max((int)((d >> 16) & 0x7FFF) - c, 0), 4) * 8u;
+                            const uint32_t m = k8 >= 32u ? 0xFFFFFFFFu : (1u << k8) - 1u;  // columns c.. the read covers
+                            const uint32_t a = (d & 0xFFFFu) + (uint32_t)c;
+                            const uint32_t b = ldsu32(bimg + a) & m, q = ldsu32(qimg + a);
+                            mf[side] |= b;
+                            lookup4(lr2, b, q, D[side][0], D[side][1], D[side][2], D[side][3]);
+                        }
+                        for (int i = nfw[s]; i < cnt[s]; i++) {
+                            const uint32_t d = __builtin_amdgcn_readfirstlane(dl[i]);
+                            const uint32_t k8 = (uint32_t)::min(::max((int)((d >> 16) & 0x7FFF) - c, 0), 4) * 8u;
+                            const uint32_t m = k8 >= 32u ? 0xFFFFFFFFu : ~(0xFFFFFFFFu >> k8);  // high bytes
+                            const uint32_t a = (d & 0xFFFFu) - (uint32_t)c - 3u;
+                            const uint32_t b = ldsu32(bimg + a) & m, q = ldsu32(qimg + a);
+                            mr[side] |= b;
+                            lookup4(lr2, b, q, D[side][3], D[side][2], D[side][1], D[side][0]);
+                        }
                     }
                 }
-                for (int i = 4; i < na; i++) {
-                    const uint32_t d = rlu(desc, (int)__builtin_amdgcn_readfirstlane(lists[sa * 64 + i]));
+                uint32_t bm[2], multi = 0;
 #pragma unroll
-                    for (int k = 0; k < 3; k++) acc(d, cc[k], col[k], dsA[k], bmA[k]);
+                for (int side = 0; side < 2; side++) {
+                    bm[side] = (mf[side] & 0x0F0F0F0Fu) | comp4(__builtin_bswap32(mr[side] & 0x0F0F0F0Fu));
+                    const uint32_t x = bm[side];
+                    multi |= x & ((x | 0x10101010u) - 0x01010101u);  // per byte: more than one base seen
                 }
-                for (int i = 4; i < nb; i++) {
-                    const uint32_t d = rlu(desc, (int)__builtin_amdgcn_readfirstlane(lists[sb * 64 + i]));
+                const int sa = e == 0 ? 0 : 1, sb = e == 0 ? 3 : 2;
+                uint32_t ob4 = 0, oq4 = 0;
 #pragma unroll
-                    for (int k = 0; k < 3; k++) acc(d, cc[k], col[k], dsB[k], bmB[k]);
-                }
-#pragma unroll
-                for (int k = 0; k < 3; k++) {
+                for (int j = 0; j < 4; j++) {
                     uint32_t vb[2] = {0, 0}, vq[2] = {0, 0};
-                    bool slow = false;
+                    bool slow = ((multi >> (8 * j)) & 0xFFu) != 0;
 #pragma unroll
                     for (int side = 0; side < 2; side++) {
                         const bool present = side == 0 ? hs[sa] : hs[sb];
                         if (!present) continue;
-                        const int32_t dsum = side == 0 ? dsA[k] : dsB[k];
-                        const uint32_t bm = side == 0 ? bmA[k] : bmB[k];
-                        if (__builtin_popcount(bm) > 1 || dsum < 0) {
-                            slow = true;
-                        } else {
-                            const int32_t d = ::min(dsum, (int32_t)((1 << 27) - 1));
-                            const int q0 = qlo[d >> 16];
-                            const int Q = q0 + (d >= dthr[q0 + 1] ? 1 : 0);
-                            vb[side] = Q < 2 ? kN : bm;
-                            vq[side] = Q < 2 ? 2u : (uint32_t)Q;
-                        }
+                        const int32_t dsum = D[side][j];
+                        slow |= dsum < 0;
+                        const int32_t d = ::min(::max(dsum, 0), (int32_t)((1 << 27) - 1));
+                        const int q0 = qlo[d >> 16];
+                        const int Q = q0 + (d >= dthr[q0 + 1] ? 1 : 0);
+                        const uint32_t b1 = (bm[side] >> (8 * j)) & 0xFFu;
+                        vb[side] = Q < 2 ? kN : b1;
+                        vq[side] = Q < 2 ? 2u : (uint32_t)Q;
                     }
-                    const int c = cc[k];
-                    if (col[k] && !slow) {
-                        uint32_t ob, oq;
-                        if (hs[sa] && hs[sb]) {
-                            duplex_col(vb[0], vq[0], vb[1], vq[1], ob, oq);
-                        } else {
-                            ob = hs[sa] ? vb[0] : vb[1];
-                            oq = hs[sa] ? vq[0] : vq[1];
-                        }
-                        outb[e * ow + c] = (uint8_t)ob;
-                        outq[e * ow + c] = (uint8_t)oq;
+                    uint32_t ob, oq;
+                    if (hs[sa] && hs[sb]) {
+                        duplex_col(vb[0], vq[0], vb[1], vq[1], ob, oq);
+                    } else {
+                        ob = hs[sa] ? vb[0] : vb[1];
+                        oq = hs[sa] ? vq[0] : vq[1];
                     }
-                    const uint64_t ms = ballot(col[k] && slow);
-                    if (col[k] && slow) sq[nq + mbcnt(ms)] = (uint16_t)((e << 15) | c);
+                    ob4 |= ob << (8 * j);
+                    oq4 |= oq << (8 * j);
+                    const bool qd = slow && c + j < ol;
+                    const uint64_t ms = ballot(qd);
+                    if (qd) sq[nq + mbcnt(ms)] = (uint16_t)((e << 15) | (c + j));
                     nq += __builtin_popcountll(ms);
+                }
+                if (c < ol) {
+                    st32(outb + e * ow + c, ob4);
+                    st32(outq + e * ow + c, oq4);
                 }
             }
         }
@@ -954,13 +993,12 @@ __global__ __launch_bounds__(kWave *kSmallWaves) void k_small(KParams P, const u
                 if (!act || !hs[s]) continue;
                 int32_t D0 = 0, D1 = 0, D2 = 0, D3 = 0;
                 for (int i = 0; i < cnt[s]; i++) {
-                    const int r = lists[s * 64 + i];
-                    const uint32_t d = descs[r];
+                    const uint32_t d = dlist[off[s] + i];
                     if (c >= (int)((d >> 16) & 0x7FFF)) continue;
                     const uint32_t idx = (d & 0x80000000u) ? (d & 0xFFFF) - c : (d & 0xFFFF) + c;
-                    uint32_t bb = bimg[idx];
-                    if (d & 0x80000000u) bb = comp_nt16(bb);
-                    const int32_t v = lr[qimg[idx]];
+                    const uint32_t braw = bimg[idx];
+                    const int32_t v = lr2[(braw >> 4) * 256u + qimg[idx]];
+                    const uint32_t bb = (d & 0x80000000u) ? comp_nt16(braw) : (braw & 0x0F);
                     D0 += bb == kA ? v : 0;
                     D1 += bb == kC ? v : 0;
                     D2 += bb == kG ? v : 0;
@@ -996,7 +1034,7 @@ __global__ __launch_bounds__(kWave *kSmallWaves) void k_small(KParams P, const u
         // pack and store: lanes 0-31 end 0, lanes 32-63 end 1, 8 columns per lane
         if (stop != 7 && stop != 8) {
             const int e = t >> 5;
-            const int ol = olen[e];
+            const int ol = e ? olen[1] : olen[0];
             for (int c0 = 8 * (t & 31); c0 < ol; c0 += 256) {
                 const uint2 bv = *reinterpret_cast<const uint2 *>(outb + e * ow + c0);
                 const uint2 qv = *reinterpret_cast<const uint2 *>(outq + e * ow + c0);
@@ -1540,6 +1578,7 @@ static void make_tables(double pre, double post, Tables &t) {
         const double lne = log(a / 3.0);
         t.lr[q] = (int32_t)llround((lnc - lne) * kLrScale);
     }
+    for (int q = 0; q < 256; q++) t.zero[q] = 0;
     t.thr[0] = INFINITY;
     for (int k = 1; k < 94; k++) {
         const double pk = pow(10.0, -((double)k - 0.001) / 10.0);
@@ -1669,8 +1708,9 @@ int32_t bsdc_run(bsdc_ctx *c, const bsdc_family_batch *b, bsdc_consensus *o, int
         c->err = "bad arena/stride sizes";
         return BSDC_EINVAL;
     }
-    for (int q = 0; q < 4; q++) {
-        if (b->small_arena[q] % 16 || (size_t)kTabBytes + (size_t)kSmallWaves * (size_t)b->small_arena[q] > 160 * 1024) {
+    for (int q = 0; q < BSDC_SMALL_BUCKETS; q++) {
+        if (b->n_small[q] > 0 &&
+            (b->small_arena[q] % 16 || b->small_arena[q] <= 0 || (size_t)kTabBytes + (size_t)b->small_arena[q] > kLdsBytes)) {
             c->err = "bad small arena size";
             return BSDC_EINVAL;
         }
@@ -1692,14 +1732,22 @@ int32_t bsdc_run(bsdc_ctx *c, const bsdc_family_batch *b, bsdc_consensus *o, int
     P.tab = c->dev_tab;
     P.mode = mode;
     P.overlap = c->params.consensus_call_overlapping_bases;
+    P.ref_chunks = ref_chunks(b->max_len);
+    P.ref_chunks_inv = (uint32_t)((((uint64_t)1 << 32) + (uint64_t)P.ref_chunks - 1) / (uint64_t)P.ref_chunks);
     if (!(mode & BSDC_MODE_SKIP_SMALL)) {
         const uint32_t *f = b->small_fams;
-        for (int q = 0; q < 4; q++) {
+        for (int q = 0; q < BSDC_SMALL_BUCKETS; q++) {
             const int64_t nf = b->n_small[q];
             if (nf > 0) {
-                const size_t lds = (size_t)kTabBytes + (size_t)kSmallWaves * (size_t)b->small_arena[q];
-                const int64_t blocks = (nf + kSmallWaves - 1) / kSmallWaves;
-                hipLaunchKernelGGL(k_small, dim3((unsigned)blocks), dim3(kWave * kSmallWaves), lds, s, P, f, nf,
+                // wavefronts per workgroup (they share one copy of the tables): 4 or 8, whichever
+                // keeps more wavefronts resident per CU; the smaller on a tie
+                const int64_t a = b->small_arena[q];
+                const int64_t w4 = 4 * std::min<int64_t>(8, kLdsBytes / (kTabBytes + 4 * a));
+                const int64_t w8 = 8 * std::min<int64_t>(4, kLdsBytes / (kTabBytes + 8 * a));
+                const int nw = w8 > w4 ? 8 : 4;
+                const size_t lds = (size_t)kTabBytes + (size_t)nw * (size_t)b->small_arena[q];
+                const int64_t blocks = (nf + nw - 1) / nw;
+                hipLaunchKernelGGL(k_small, dim3((unsigned)blocks), dim3(kWave * nw), lds, s, P, f, nf,
                                    b->small_arena[q]);
                 HIP_OK(c, hipGetLastError());
             }

@@ -14,7 +14,7 @@ import numpy as np
 import torch
 
 from . import _lib
-from .batch import FamilyBatch
+from .batch import LDS_TABLES, FamilyBatch
 from .records import Reference
 
 
@@ -60,7 +60,7 @@ class DeviceBatch:
             self.dump_tags = torch.zeros(max(Rn, 1), dtype=torch.uint8, device=device)
             self.dump_seq = torch.zeros(cap, dtype=torch.uint8, device=device)
             self.dump_qual = torch.zeros(cap, dtype=torch.uint8, device=device)
-        lds_cap = 64 * 1024 - (1024 + 384 + 2048 + 192)
+        lds_cap = 64 * 1024 - LDS_TABLES
         nl = int(fb.large_fams.shape[0])
         self.scratch = None
         if nl and fb.large_arena > lds_cap:
@@ -71,7 +71,7 @@ class DeviceBatch:
         for k in ("fam_off", "rec", "rec_win", "cig_off", "cig_info", "cigar", "rt", "seq", "qual",
                   "small_fams", "large_fams"):
             setattr(b, k, _dptr(self.t[k]))
-        for q in range(4):
+        for q in range(_lib.SMALL_BUCKETS):
             b.n_small[q] = int(fb.small_buckets[q].shape[0])
             b.small_arena[q] = int(fb.small_arenas[q])
         b.n_large = nl

@@ -24,7 +24,8 @@
 extern "C" {
 #endif
 
-#define BSDC_ABI_VERSION 2
+#define BSDC_ABI_VERSION 3
+#define BSDC_SMALL_BUCKETS 8 /* LDS arena size classes of the wavefront-per-family kernel */
 
 #define BSDC_EINVAL (-22)
 #define BSDC_ENOMEM (-12)
@@ -73,11 +74,11 @@ typedef struct {
     const int32_t *rt;           /* [4*n_rec] RT records only: next_pos, tlen, mate unclipped start, end */
     const uint8_t *seq;
     const uint8_t *qual;
-    const uint32_t *small_fams;  /* families processed one wavefront each, 4 consecutive buckets;
+    const uint32_t *small_fams;  /* families processed one wavefront each, BSDC_SMALL_BUCKETS consecutive buckets;
                                     4 words per family: family, first record,
                                     n_rec | (image bytes / 32) << 8, image base (first slot) */
-    int64_t n_small[4];          /* families per bucket */
-    int32_t small_arena[4];      /* LDS bytes per wavefront of each bucket (multiple of 16) */
+    int64_t n_small[BSDC_SMALL_BUCKETS];      /* families per bucket */
+    int32_t small_arena[BSDC_SMALL_BUCKETS];  /* LDS bytes per wavefront of each bucket (multiple of 16) */
     const uint32_t *large_fams;  /* families processed one workgroup each */
     int64_t n_large;
     int32_t large_arena;         /* bytes per workgroup for large families */
