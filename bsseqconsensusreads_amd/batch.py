@@ -60,7 +60,7 @@ def small_arena_bytes(n, img, nconv, complex_ops, max_len):
     ws = 32 * ref_chunks(max_len)
     cops = np.asarray(complex_ops, dtype=np.int64)
     ow = int(round16(int(max_len) + 2))
-    R = 2 * np.asarray(img, dtype=np.int64) + round16(4 * n) + 16
+    R = 2 * np.asarray(img, dtype=np.int64) + round16(4 * n) + 16 + round16(n)
     e_ref = R + np.asarray(nconv, dtype=np.int64) * ws
     simp = R + round16(16 * n) + round16(n) + 2 * round16(2 * n)
     e_f = simp + np.where(cops > 0, round16(4 * (cops + 4 * n)), 0)

@@ -378,7 +378,7 @@ __device__ __forceinline__ void duplex_col(uint32_t xb, uint32_t xq, uint32_t yb
 // Arena of one small family.  Regions live only as long as their phase and share space:
 //   bimg, qimg  the family image, bases / quals (whole kernel)
 //   lists       reference-window starts (staging) -> read descriptors (vote), 4 B per record
-//   misc        consensus lengths lc[4]
+//   misc        consensus lengths lc[4], converted record -> lane
 //   R           reference windows (staging, convert) | alignment-filter scratch (source reads) |
 //               duplex rows + queued columns (vote)
 struct SmallLayout {
@@ -394,8 +394,8 @@ struct SmallLayout {
         o += img;
         lists = (uint32_t)o;
         o += round16(4 * (int64_t)n);
-        misc = (uint32_t)o;
-        o += 16;
+        misc = (uint32_t)o;  // lc[4] u32, then the lane of each converted record (u8)
+        o += 16 + round16(n);
         const int64_t R = o;
         ref = (uint32_t)R;
         const int64_t e_ref = R + (int64_t)nconv * ws;
@@ -459,6 +459,50 @@ __device__ __forceinline__ void lookup4(const int32_t *lr2, uint32_t b, uint32_t
     D2 += *reinterpret_cast<const int32_t *>(base + (hi & 0xFFFFu));
     D3 += *reinterpret_cast<const int32_t *>(base + (hi >> 16));
 }
+// Mask of the bytes of a lane's dword that lie at or past a read's end, given k8 = 8 x (columns
+// the read still covers from this lane's first column), for a forward read (bytes ascend) or a
+// reverse one (bytes descend).  64-bit shifts give the k8 = 0 and k8 >= 32 ends for free.
+__device__ __forceinline__ uint32_t bytes_past(int k8, bool reverse) {
+    const uint32_t s = (uint32_t)::min(::max(k8, 0), 32);
+    return reverse ? (uint32_t)(0xFFFFFFFFull >> s) : (uint32_t)(~0ull << s);
+}
+// byte-wise helpers; every byte they see is < 128
+__device__ __forceinline__ uint32_t expand80(uint32_t m80) { return m80 | (m80 - (m80 >> 7)); }  // 0x80 -> 0xFF
+__device__ __forceinline__ uint32_t bytes_nonzero(uint32_t x) {  // 0xFF where the byte (< 128) is not 0
+    return expand80((x + 0x7F7F7F7Fu) & 0x80808080u);
+}
+// Single-strand results of 4 columns -> duplex (fgbio DuplexConsensusCaller.duplexConsensus), in
+// bytes.  bmX: one-hot bases seen by side X (0 = none), QX: its phred from the likelihood sum.
+// Q < 2 -> (N, 2); one side absent -> the other side; both -> agree: sum, else the higher
+// quality's base with the difference, equal qualities -> 2; capped at 93; N or 2 -> (N, 2).
+__device__ __forceinline__ void resolve4(bool ha, bool hb, uint32_t bmA, uint32_t QA, uint32_t bmB, uint32_t QB,
+                                         uint32_t &ob, uint32_t &oq) {
+    const uint32_t okA = expand80((QA + 0x7E7E7E7Eu) & 0x80808080u);  // Q >= 2
+    const uint32_t okB = expand80((QB + 0x7E7E7E7Eu) & 0x80808080u);
+    const uint32_t bA = (bmA & okA) | (0x0F0F0F0Fu & ~okA), qA = (QA & okA) | (0x02020202u & ~okA);
+    const uint32_t bB = (bmB & okB) | (0x0F0F0F0Fu & ~okB), qB = (QB & okB) | (0x02020202u & ~okB);
+    if (!(ha && hb)) {
+        ob = ha ? bA : bB;
+        oq = ha ? qA : qB;
+        return;
+    }
+    const uint32_t same = ~bytes_nonzero(bA ^ bB);
+    const uint32_t dAB = (qA | 0x80808080u) - qB;                 // 128 + qA - qB per byte
+    const uint32_t geA = expand80(dAB & 0x80808080u);              // qA >= qB
+    const uint32_t dBA = (qB | 0x80808080u) - qA;
+    const uint32_t ad = ((dAB & geA) | (dBA & ~geA)) & 0x7F7F7F7Fu;  // |qA - qB|
+    const uint32_t sum = qA + qB;
+    const uint32_t over = expand80((sum + 0x22222222u) & 0x80808080u);  // sum >= 94 (sums <= 186)
+    const uint32_t sum93 = (sum & ~over) | (0x5D5D5D5Du & over);
+    const uint32_t ad2 = ad | (0x02020202u & ~bytes_nonzero(ad));  // equal qualities -> 2
+    uint32_t rb = (bA & (same | geA)) | (bB & ~(same | geA));
+    uint32_t rq = (sum93 & same) | (ad2 & ~same);
+    const uint32_t isN = ((bA + 0x01010101u) | (bB + 0x01010101u)) & 0x10101010u;  // a side is N (15)
+    const uint32_t is2 = ~bytes_nonzero(rq ^ 0x02020202u);
+    const uint32_t nm = expand80(isN << 3) | is2;
+    ob = (rb & ~nm) | (0x0F0F0F0Fu & nm);
+    oq = (rq & ~nm) | (0x02020202u & nm);
+}
 // htsjdk complement of one-hot codes in every byte (nibble bit reversal; 0 stays 0)
 __device__ __forceinline__ uint32_t comp4(uint32_t x) {
     return (__builtin_bitreverse32(__builtin_bswap32(x)) >> 4) & 0x0F0F0F0Fu;
@@ -488,18 +532,19 @@ __device__ __forceinline__ void unpack32(uint4 v, uint8_t *dst) {
 
 __global__ __launch_bounds__(kWave *kSmallMaxWaves, kSmallMinWaves) void k_small(KParams P, const uint32_t *fams, int64_t nfams,
                                                               int32_t arena) {
-    extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
-    const Tables *T = reinterpret_cast<const Tables *>(smem);
+    extern __shared__ __attribute__((aligned(16))) uint8_t smem[];  // the wavefronts' arenas
+    __shared__ __attribute__((aligned(16))) Tables s_tab;           // static: its address folds into offsets
+    const Tables *T = &s_tab;
     const int32_t *lr2 = T->zero;  // [2][256]: row (base byte >> 4) = 1 for A/C/G/T
     const float *thr = T->thr;
     const uint8_t *qlo = T->qlo;
     const int32_t *dthr = T->dthr;
-    load_tables(P.tab, smem);
+    load_tables(P.tab, reinterpret_cast<uint8_t *>(&s_tab));
     const int w = threadIdx.x >> 6;
     const int t = threadIdx.x & 63;
     const int64_t fi = (int64_t)blockIdx.x * (blockDim.x >> 6) + w;
     if (fi >= nfams) return;
-    uint8_t *A = smem + kTabBytes + (size_t)w * (size_t)arena;
+    uint8_t *A = smem + (size_t)w * (size_t)arena;
     const bsdc_family_batch &B = P.B;
     const bool do_convert = P.mode & BSDC_MODE_CONVERT;
     const bool do_extend = P.mode & BSDC_MODE_EXTEND;
@@ -515,40 +560,40 @@ __global__ __launch_bounds__(kWave *kSmallMaxWaves, kSmallMinWaves) void k_small
     const uint32_t img = (__builtin_amdgcn_readfirstlane(ent.z) >> 8) * 32u;
     const uint32_t base_g = __builtin_amdgcn_readfirstlane(ent.w);
 
-    // ---- staging: record metadata and every 16-byte chunk of the image, then the converted
-    // records' reference windows; up to 4 chunk loads per lane in flight per round ----
+    // ---- staging: record metadata, every 16-byte chunk of the image and the converted records'
+    // reference windows.  Metadata loads go first so the window loads (whose addresses they hold)
+    // are issued while the image chunks are still in flight; up to 4 chunk loads per lane per
+    // round ----
     const bool has = t < n;
     uint4 rc = make_uint4(0, 0, 0, 0);
     uint2 win = make_uint2(0, 0);
     uint32_t cinfo = 0;
+    if (has) {
+        rc = reinterpret_cast<const uint4 *>(B.rec)[r0 + t];
+        win = reinterpret_cast<const uint2 *>(B.rec_win)[r0 + t];
+        cinfo = B.cig_info[r0 + t];
+    }
     const int nqc = (int)(img >> 4), nch = nqc + (int)(img >> 5);  // qual chunks, + packed-base chunks
     uint8_t *bimg = A;          // SmallLayout: bimg = 0, qimg = img
     uint8_t *qimg = A + img;
-    for (int k0 = 0; k0 < nch; k0 += 256) {
-        uint4 v[4];
+    auto load_img = [&](int k) {
+        uint4 v = make_uint4(0, 0, 0, 0);
+        if (k < nqc)
+            v = *reinterpret_cast<const uint4 *>(B.qual + base_g + 16 * (uint32_t)k);
+        else if (k < nch)
+            v = *reinterpret_cast<const uint4 *>(B.seq + (base_g >> 1) + 16 * (uint32_t)(k - nqc));
+        return v;
+    };
+    auto store_img = [&](int k, uint4 v) {
+        if (k < nqc)
+            *reinterpret_cast<uint4 *>(qimg + 16 * k) = v;
+        else if (k < nch)
+            unpack32(v, bimg + 32 * (k - nqc));
+    };
+    uint4 v[4];
 #pragma unroll
-        for (int u = 0; u < 4; u++) {
-            const int k = k0 + t + 64 * u;
-            v[u] = make_uint4(0, 0, 0, 0);
-            if (k < nqc)
-                v[u] = *reinterpret_cast<const uint4 *>(B.qual + base_g + 16 * (uint32_t)k);
-            else if (k < nch)
-                v[u] = *reinterpret_cast<const uint4 *>(B.seq + (base_g >> 1) + 16 * (uint32_t)(k - nqc));
-        }
-        if (k0 == 0 && has) {
-            rc = reinterpret_cast<const uint4 *>(B.rec)[r0 + t];
-            win = reinterpret_cast<const uint2 *>(B.rec_win)[r0 + t];
-            cinfo = B.cig_info[r0 + t];
-        }
-#pragma unroll
-        for (int u = 0; u < 4; u++) {
-            const int k = k0 + t + 64 * u;
-            if (k < nqc)
-                *reinterpret_cast<uint4 *>(qimg + 16 * k) = v[u];
-            else if (k < nch)
-                unpack32(v[u], bimg + 32 * (k - nqc));
-        }
-    }
+    for (int u = 0; u < 4; u++) v[u] = load_img(t + 64 * u);
+
     const uint32_t gslot = rc.x;
     int32_t pos = (int32_t)rc.y;
     const int32_t L = (int32_t)(rc.z & 0xFFFF);
@@ -557,7 +602,6 @@ __global__ __launch_bounds__(kWave *kSmallMaxWaves, kSmallMinWaves) void k_small
     const bool conv = has && do_convert && (link & BSDC_LINK_CONVERT);
     const bool cplx = has && (link & BSDC_LINK_COMPLEX);
     if (!cplx) cinfo = 0;
-
     const uint64_t conv_mask = ballot(conv);
     const int nconv = __builtin_popcountll(conv_mask);
     const int ci = mbcnt(conv_mask);
@@ -568,61 +612,75 @@ __global__ __launch_bounds__(kWave *kSmallMaxWaves, kSmallMinWaves) void k_small
     uint8_t *refw = A + Lo.ref;
     const int ws = Lo.ws;
     uint32_t *lc = reinterpret_cast<uint32_t *>(A + Lo.misc);
+    uint8_t *convlane = A + Lo.misc + 16;                              // converted record -> its lane
     uint32_t *convwin = reinterpret_cast<uint32_t *>(A + Lo.lists);  // until the descriptors exist
     const uint32_t slot = gslot - base_g;                              // record slot in the image
-    if (conv) convwin[ci] = win.x;
+    if (conv) {
+        convwin[ci] = win.x;
+        convlane[ci] = (uint8_t)t;
+    }
     if (t < 4) lc[t] = 0;
     wave_sync();
-    {
-        // chunk k -> (converted record k / rcn, part k % rcn); rcn and its 2^32 reciprocal are
-        // launch constants (floor(k * rinv / 2^32) is exact for k, rcn < 2^16)
-        const uint32_t rcn = (uint32_t)P.ref_chunks, rinv = P.ref_chunks_inv;
-        const int total = nconv * (int)rcn;
-        for (int k0 = 0; k0 < total; k0 += 256) {
-            uint4 v[4];
-#pragma unroll
-            for (int u = 0; u < 4; u++) {
-                const int k = k0 + t + 64 * u;
-                v[u] = make_uint4(0, 0, 0, 0);
-                if (k < total) {
-                    const uint32_t cr = __umulhi((uint32_t)k, rinv), part = (uint32_t)k - cr * rcn;
-                    const uint32_t wb = (convwin[cr] >> 1) & ~15u;
-                    v[u] = *reinterpret_cast<const uint4 *>(P.ref + wb + 16 * part);
-                }
-            }
-#pragma unroll
-            for (int u = 0; u < 4; u++) {
-                const int k = k0 + t + 64 * u;
-                if (k < total) {
-                    const uint32_t cr = __umulhi((uint32_t)k, rinv), part = (uint32_t)k - cr * rcn;
-                    unpack32(v[u], refw + cr * ws + 32 * part);
-                }
-            }
+    // window chunk k -> (converted record k / rcn, part k % rcn); rcn and its 2^32 reciprocal are
+    // launch constants (floor(k * rinv / 2^32) is exact for k, rcn < 2^16)
+    const uint32_t rcn = (uint32_t)P.ref_chunks, rinv = P.ref_chunks_inv;
+    const int wtot = nconv * (int)rcn;
+    auto load_win = [&](int k) {
+        uint4 x = make_uint4(0, 0, 0, 0);
+        if (k < wtot) {
+            const uint32_t cr = __umulhi((uint32_t)k, rinv), part = (uint32_t)k - cr * rcn;
+            x = *reinterpret_cast<const uint4 *>(P.ref + ((convwin[cr] >> 1) & ~15u) + 16 * part);
         }
+        return x;
+    };
+    auto store_win = [&](int k, uint4 x) {
+        if (k < wtot) {
+            const uint32_t cr = __umulhi((uint32_t)k, rinv), part = (uint32_t)k - cr * rcn;
+            unpack32(x, refw + cr * ws + 32 * part);
+        }
+    };
+    uint4 wv[2];
+#pragma unroll
+    for (int u = 0; u < 2; u++) wv[u] = load_win(t + 64 * u);
+#pragma unroll
+    for (int u = 0; u < 4; u++) store_img(t + 64 * u, v[u]);
+    for (int k0 = 256; k0 < nch; k0 += 256) {  // families with more than 256 image chunks
+#pragma unroll
+        for (int u = 0; u < 4; u++) v[u] = load_img(k0 + t + 64 * u);
+#pragma unroll
+        for (int u = 0; u < 4; u++) store_img(k0 + t + 64 * u, v[u]);
+    }
+#pragma unroll
+    for (int u = 0; u < 2; u++) store_win(t + 64 * u, wv[u]);
+    for (int k0 = 128; k0 < wtot; k0 += 128) {
+#pragma unroll
+        for (int u = 0; u < 2; u++) wv[u] = load_win(k0 + t + 64 * u);
+#pragma unroll
+        for (int u = 0; u < 2; u++) store_win(k0 + t + 64 * u, wv[u]);
     }
     wave_sync();
     if (stop == 1) return;
 
-    // ---- tool 1: convert, one converted record at a time, 4 positions per lane ----
+    // ---- tool 1: every converted record at once -- 16 lanes per record, 4 positions per lane per
+    // step (tools/1.convert_AG_to_CT.py:84-183) ----
     int32_t start = 1, len = L;
     bool rd = false;
-    {
-        uint64_t cm = conv_mask;
-        while (cm) {
-            const int r = __builtin_ctzll(cm);
-            cm &= cm - 1;
-            const uint32_t s_slot = rlu(slot, r);
-            const int32_t s_L = rl(L, r);
-            const int s_ci = rl(ci, r);
-            const uint32_t s_win = rlu(win.x, r);
-            const int32_t s_avail = (int32_t)rlu(win.y, r);
+    for (int cr0 = 0; cr0 < nconv; cr0 += 4) {
+        const int cr = cr0 + (t >> 4);
+        const bool act = cr < nconv;
+        const int src = act ? convlane[cr] : 0;
+        const uint32_t s_slot = (uint32_t)__shfl((int)slot, src, kWave);
+        const int32_t s_L = __shfl(L, src, kWave);
+        const uint32_t s_win = (uint32_t)__shfl((int)win.x, src, kWave);
+        const int32_t s_avail = __shfl((int)win.y, src, kWave);
+        bool my_rd = false;
+        if (act) {
             const int32_t Lm = s_L + 1;
-            const uint32_t ph = s_win & 31u;
-            bool my_rd = false;
-            for (int j4 = 4 * t; j4 < Lm; j4 += 256) {
+            const uint32_t wbase = (uint32_t)(cr * ws) + (s_win & 31u);
+            for (int j4 = 4 * (t & 15); j4 < Lm; j4 += 64) {
                 uint32_t m = lds32(bimg + s_slot + j4);
                 const uint32_t mn = lds32(bimg + s_slot + j4 + 4);
-                const uint32_t a = (uint32_t)(s_ci * ws) + ph + (uint32_t)j4;
+                const uint32_t a = wbase + (uint32_t)j4;
                 const uint32_t d0 = lds32(refw + (a & ~3u)), d1 = lds32(refw + (a & ~3u) + 4);
                 const uint32_t sh = a & 3u;
                 uint32_t f0 = alignbyte(d1, d0, sh);
@@ -639,23 +697,22 @@ __global__ __launch_bounds__(kWave *kSmallMaxWaves, kSmallMinWaves) void k_small
                 uint32_t nxt = 0x0F0F0F0Fu;
                 const int last = Lm - 1 - j4;  // the record's last position has no next base
                 if (last >= 0 && last < 4) nxt &= ~(0xFFu << (8 * last));
-                // A->G, C->T keep a base A/C/G/T, so the kValid flags of m carry over
+                // A->G, C->T keep a base A/C/G/T, so the A/C/G/T flags (0x10) of m carry over
                 const uint32_t out = convert4(m & 0x0F0F0F0Fu, m1 & 0x0F0F0F0Fu, f0 & 0x0F0F0F0Fu, f1 & 0x0F0F0F0Fu, nxt) |
                                      (m & 0x10101010u);
                 st32(bimg + s_slot + j4, out);
-                if (last >= 0 && last < 4) {  // :157-170 a final C before a reference G is trimmed
+                if (last >= 0 && last < 4)  // :157-170 a final C before a reference G is trimmed
                     my_rd = ((out >> (8 * last)) & 0x0F) == kC && ((f1 >> (8 * last)) & 0x0F) == kG;
-                }
             }
-            const bool s_rd = ballot(my_rd) != 0;
-            if (t == 0) qimg[s_slot] = 40;  // :174-177 'I' + quals
-            if (t == r) rd = s_rd;
+            if ((t & 15) == 0) qimg[s_slot] = 40;  // :174-177 'I' + quals
         }
-        if (conv) {
-            start = 0;
-            len = L + 1 - (rd ? 1 : 0);
-            pos = pos - 1 > 0 ? pos - 1 : 0;
-        }
+        const uint64_t bal = ballot(my_rd);
+        if (conv && (ci >> 2) == (cr0 >> 2) && ((bal >> (16 * (ci & 3))) & 0xFFFFu)) rd = true;
+    }
+    if (conv) {
+        start = 0;
+        len = L + 1 - (rd ? 1 : 0);
+        pos = pos - 1 > 0 ? pos - 1 : 0;
     }
     if (!do_convert && has && (link & BSDC_LINK_RD_IN)) rd = true;
     if (rd) link |= kLinkRdDev;
@@ -904,7 +961,7 @@ __global__ __launch_bounds__(kWave *kSmallMaxWaves, kSmallMinWaves) void k_small
         for (int e = 0; e < 2; e++) {
             const int ol = olen[e];
             for (int c0 = 0; c0 < ol; c0 += 256) {
-                const int c = c0 + 4 * t;
+                const int c = c0 + 4 * t, c8 = 8 * c;
                 int32_t D[2][4] = {{0, 0, 0, 0}, {0, 0, 0, 0}};
                 uint32_t mf[2] = {0, 0}, mr[2] = {0, 0};  // one-hot ORs of forward / reverse reads
                 if (c < ol) {
@@ -912,23 +969,36 @@ __global__ __launch_bounds__(kWave *kSmallMaxWaves, kSmallMinWaves) void k_small
                     for (int side = 0; side < 2; side++) {
                         const int s = side == 0 ? (e == 0 ? 0 : 1) : (e == 0 ? 3 : 2);
                         const uint32_t *dl = dlist + off[s];
-                        for (int i = 0; i < nfw[s]; i++) {
-                            const uint32_t d = __builtin_amdgcn_readfirstlane(dl[i]);
-                            const uint32_t k8 = (uint32_t)::min(::max((int)((d >> 16) & 0x7FFF) - c, 0), 4) * 8u;
-                            const uint32_t m = k8 >= 32u ? 0xFFFFFFFFu : (1u << k8) - 1u;  // columns c.. the read covers
+                        // one read: its 4 columns from c (descriptor d is wave-uniform; d = 0 is a
+                        // read of length 0 and adds nothing, which pads the pairs below)
+                        auto fwd = [&](uint32_t d) {
+                            // bytes at or past the read's end: (-1 << 8 * covered) as 64 bits
+                            const uint32_t x = bytes_past(8 * (int)((d >> 16) & 0x7FFF) - c8, false);
                             const uint32_t a = (d & 0xFFFFu) + (uint32_t)c;
-                            const uint32_t b = ldsu32(bimg + a) & m, q = ldsu32(qimg + a);
+                            const uint32_t b = ldsu32(bimg + a) & ~x, q = ldsu32(qimg + a);
                             mf[side] |= b;
                             lookup4(lr2, b, q, D[side][0], D[side][1], D[side][2], D[side][3]);
-                        }
-                        for (int i = nfw[s]; i < cnt[s]; i++) {
-                            const uint32_t d = __builtin_amdgcn_readfirstlane(dl[i]);
-                            const uint32_t k8 = (uint32_t)::min(::max((int)((d >> 16) & 0x7FFF) - c, 0), 4) * 8u;
-                            const uint32_t m = k8 >= 32u ? 0xFFFFFFFFu : ~(0xFFFFFFFFu >> k8);  // high bytes
+                        };
+                        auto rev = [&](uint32_t d) {  // bytes run backwards: byte 3 - j is column c + j
+                            const uint32_t x = bytes_past(8 * (int)((d >> 16) & 0x7FFF) - c8, true);
                             const uint32_t a = (d & 0xFFFFu) - (uint32_t)c - 3u;
-                            const uint32_t b = ldsu32(bimg + a) & m, q = ldsu32(qimg + a);
+                            const uint32_t b = ldsu32(bimg + a) & ~x, q = ldsu32(qimg + a);
                             mr[side] |= b;
                             lookup4(lr2, b, q, D[side][3], D[side][2], D[side][1], D[side][0]);
+                        };
+                        // reads two at a time so both reads' loads are in flight together
+                        const int nf = nfw[s], na = cnt[s];
+                        for (int i = 0; i < nf; i += 2) {
+                            const uint32_t d0 = __builtin_amdgcn_readfirstlane(dl[i]);
+                            const uint32_t d1 = i + 1 < nf ? __builtin_amdgcn_readfirstlane(dl[i + 1]) : 0u;
+                            fwd(d0);
+                            fwd(d1);
+                        }
+                        for (int i = nf; i < na; i += 2) {
+                            const uint32_t d0 = __builtin_amdgcn_readfirstlane(dl[i]);
+                            const uint32_t d1 = i + 1 < na ? __builtin_amdgcn_readfirstlane(dl[i + 1]) : 0u;
+                            rev(d0);
+                            rev(d1);
                         }
                     }
                 }
@@ -940,34 +1010,26 @@ __global__ __launch_bounds__(kWave *kSmallMaxWaves, kSmallMinWaves) void k_small
                     multi |= x & ((x | 0x10101010u) - 0x01010101u);  // per byte: more than one base seen
                 }
                 const int sa = e == 0 ? 0 : 1, sb = e == 0 ? 3 : 2;
-                uint32_t ob4 = 0, oq4 = 0;
+                // per side and column: Q from the sum alone (valid when the column is not slow)
+                uint32_t Qp[2] = {0, 0};
+                bool neg_d[4] = {false, false, false, false};
+#pragma unroll
+                for (int side = 0; side < 2; side++) {
+#pragma unroll
+                    for (int j = 0; j < 4; j++) {
+                        const int32_t dsum = D[side][j];
+                        neg_d[j] |= dsum < 0;
+                        const int32_t d = ::min(::max(dsum, 0), (int32_t)((1 << 27) - 1));
+                        const uint32_t q0 = qlo[d >> 16];
+                        Qp[side] |= (q0 + (d >= dthr[q0 + 1] ? 1u : 0u)) << (8 * j);
+                    }
+                }
+                uint32_t ob4, oq4;
+                resolve4(hs[sa], hs[sb], bm[0], Qp[0], bm[1], Qp[1], ob4, oq4);
+                // slow columns: a side saw more than one base, or a negative sum
 #pragma unroll
                 for (int j = 0; j < 4; j++) {
-                    uint32_t vb[2] = {0, 0}, vq[2] = {0, 0};
-                    bool slow = ((multi >> (8 * j)) & 0xFFu) != 0;
-#pragma unroll
-                    for (int side = 0; side < 2; side++) {
-                        const bool present = side == 0 ? hs[sa] : hs[sb];
-                        if (!present) continue;
-                        const int32_t dsum = D[side][j];
-                        slow |= dsum < 0;
-                        const int32_t d = ::min(::max(dsum, 0), (int32_t)((1 << 27) - 1));
-                        const int q0 = qlo[d >> 16];
-                        const int Q = q0 + (d >= dthr[q0 + 1] ? 1 : 0);
-                        const uint32_t b1 = (bm[side] >> (8 * j)) & 0xFFu;
-                        vb[side] = Q < 2 ? kN : b1;
-                        vq[side] = Q < 2 ? 2u : (uint32_t)Q;
-                    }
-                    uint32_t ob, oq;
-                    if (hs[sa] && hs[sb]) {
-                        duplex_col(vb[0], vq[0], vb[1], vq[1], ob, oq);
-                    } else {
-                        ob = hs[sa] ? vb[0] : vb[1];
-                        oq = hs[sa] ? vq[0] : vq[1];
-                    }
-                    ob4 |= ob << (8 * j);
-                    oq4 |= oq << (8 * j);
-                    const bool qd = slow && c + j < ol;
+                    const bool qd = (((multi >> (8 * j)) & 0xFFu) != 0 || neg_d[j]) && c + j < ol;
                     const uint64_t ms = ballot(qd);
                     if (qd) sq[nq + mbcnt(ms)] = (uint16_t)((e << 15) | (c + j));
                     nq += __builtin_popcountll(ms);
@@ -1510,16 +1572,17 @@ __device__ void process_large(const KParams &P, uint8_t *A, const int32_t *lr, c
 
 template <bool IN_LDS>
 __global__ __launch_bounds__(kLargeThreads) void k_large(KParams P) {
-    extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
+    extern __shared__ __attribute__((aligned(16))) uint8_t smem[];  // the family's arena (IN_LDS)
+    __shared__ __attribute__((aligned(16))) Tables s_tab;
     __shared__ int red[kLargeThreads / kWave];
     __shared__ int s_cnt[4], s_lc[4];
-    const Tables *T = reinterpret_cast<const Tables *>(smem);
-    load_tables(P.tab, smem);
+    const Tables *T = &s_tab;
+    load_tables(P.tab, reinterpret_cast<uint8_t *>(&s_tab));
     const int32_t *lr = T->lr;
     const float *thr = T->thr;
     const int64_t i = blockIdx.x;
     if (i >= P.B.n_large) return;
-    uint8_t *A = IN_LDS ? smem + kTabBytes : P.O.scratch + (size_t)i * (size_t)P.B.large_arena;
+    uint8_t *A = IN_LDS ? smem : P.O.scratch + (size_t)i * (size_t)P.B.large_arena;
     process_large(P, A, lr, thr, P.B.large_fams[i], red, s_cnt, s_lc);
 }
 
@@ -1745,7 +1808,7 @@ int32_t bsdc_run(bsdc_ctx *c, const bsdc_family_batch *b, bsdc_consensus *o, int
                 const int64_t w4 = 4 * std::min<int64_t>(8, kLdsBytes / (kTabBytes + 4 * a));
                 const int64_t w8 = 8 * std::min<int64_t>(4, kLdsBytes / (kTabBytes + 8 * a));
                 const int nw = w8 > w4 ? 8 : 4;
-                const size_t lds = (size_t)kTabBytes + (size_t)nw * (size_t)b->small_arena[q];
+                const size_t lds = (size_t)nw * (size_t)b->small_arena[q];  // + the static tables
                 const int64_t blocks = (nf + nw - 1) / nw;
                 hipLaunchKernelGGL(k_small, dim3((unsigned)blocks), dim3(kWave * nw), lds, s, P, f, nf,
                                    b->small_arena[q]);
@@ -1755,15 +1818,14 @@ int32_t bsdc_run(bsdc_ctx *c, const bsdc_family_batch *b, bsdc_consensus *o, int
         }
     }
     if (b->n_large > 0 && !(mode & BSDC_MODE_SKIP_LARGE)) {
-        const size_t lds = (size_t)kTabBytes + (size_t)b->large_arena;
-        if (lds <= 64 * 1024) {
-            hipLaunchKernelGGL(k_large<true>, dim3((unsigned)b->n_large), dim3(kLargeThreads), lds, s, P);
+        if ((size_t)kTabBytes + (size_t)b->large_arena <= 64 * 1024) {
+            hipLaunchKernelGGL(k_large<true>, dim3((unsigned)b->n_large), dim3(kLargeThreads), (size_t)b->large_arena, s, P);
         } else {
             if (!o->scratch) {
                 c->err = "large families need scratch";
                 return BSDC_EINVAL;
             }
-            hipLaunchKernelGGL(k_large<false>, dim3((unsigned)b->n_large), dim3(kLargeThreads), (size_t)kTabBytes, s, P);
+            hipLaunchKernelGGL(k_large<false>, dim3((unsigned)b->n_large), dim3(kLargeThreads), 0, s, P);
         }
         HIP_OK(c, hipGetLastError());
     }
