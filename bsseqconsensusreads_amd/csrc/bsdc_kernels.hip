@@ -986,20 +986,23 @@ __global__ __launch_bounds__(kWave *kSmallMaxWaves, kSmallMinWaves) void k_small
                             mr[side] |= b;
                             lookup4(lr2, b, q, D[side][3], D[side][2], D[side][1], D[side][0]);
                         };
-                        // reads two at a time so both reads' loads are in flight together
+                        // reads two at a time (both reads' loads in flight together), then an odd one
                         const int nf = nfw[s], na = cnt[s];
-                        for (int i = 0; i < nf; i += 2) {
+                        int i = 0;
+                        for (; i + 1 < nf; i += 2) {
                             const uint32_t d0 = __builtin_amdgcn_readfirstlane(dl[i]);
-                            const uint32_t d1 = i + 1 < nf ? __builtin_amdgcn_readfirstlane(dl[i + 1]) : 0u;
+                            const uint32_t d1 = __builtin_amdgcn_readfirstlane(dl[i + 1]);
                             fwd(d0);
                             fwd(d1);
                         }
-                        for (int i = nf; i < na; i += 2) {
+                        if (i < nf) fwd(__builtin_amdgcn_readfirstlane(dl[i]));
+                        for (i = nf; i + 1 < na; i += 2) {
                             const uint32_t d0 = __builtin_amdgcn_readfirstlane(dl[i]);
-                            const uint32_t d1 = i + 1 < na ? __builtin_amdgcn_readfirstlane(dl[i + 1]) : 0u;
+                            const uint32_t d1 = __builtin_amdgcn_readfirstlane(dl[i + 1]);
                             rev(d0);
                             rev(d1);
                         }
+                        if (i < na) rev(__builtin_amdgcn_readfirstlane(dl[i]));
                     }
                 }
                 uint32_t bm[2], multi = 0;
@@ -1040,7 +1043,8 @@ __global__ __launch_bounds__(kWave *kSmallMaxWaves, kSmallMinWaves) void k_small
                 }
             }
         }
-        // queued columns: the general path (all four likelihoods, up to three exp terms)
+        // queued columns: the general path (all four likelihoods, up to three exp terms); a lane
+        // owns one queued (end, column) and walks the reads of its end's two sides
         wave_sync();
         if (stop == 7) nq = 0;
         for (int k0 = 0; k0 < nq && stop != 9; k0 += 64) {
@@ -1098,21 +1102,16 @@ __global__ __launch_bounds__(kWave *kSmallMaxWaves, kSmallMinWaves) void k_small
             const int e = t >> 5;
             const int ol = e ? olen[1] : olen[0];
             for (int c0 = 8 * (t & 31); c0 < ol; c0 += 256) {
-                const uint2 bv = *reinterpret_cast<const uint2 *>(outb + e * ow + c0);
-                const uint2 qv = *reinterpret_cast<const uint2 *>(outq + e * ow + c0);
-                uint32_t pk = 0, qlo2 = qv.x, qhi2 = qv.y;
-#pragma unroll
-                for (int k = 0; k < 8; k++) {
-                    uint32_t ob = ((k < 4 ? bv.x : bv.y) >> (8 * (k & 3))) & 0xFF;
-                    if (c0 + k >= ol) {
-                        ob = 0;
-                        if (k < 4)
-                            qlo2 &= ~(0xFFu << (8 * k));
-                        else
-                            qhi2 &= ~(0xFFu << (8 * (k - 4)));
-                    }
-                    pk |= ob << (8 * (k >> 1) + ((k & 1) ? 0 : 4));
-                }
+                uint2 bv = *reinterpret_cast<const uint2 *>(outb + e * ow + c0);
+                uint2 qv = *reinterpret_cast<const uint2 *>(outq + e * ow + c0);
+                const int k8 = 8 * (ol - c0);  // columns of the 8 inside the consensus, x 8
+                const uint32_t keep0 = ~bytes_past(k8, false), keep1 = ~bytes_past(k8 - 32, false);
+                bv.x &= keep0;
+                bv.y &= keep1;
+                const uint32_t qlo2 = qv.x & keep0, qhi2 = qv.y & keep1;
+                // bytes b0..b7 -> nibbles b0 b1 | b2 b3 | ... (BAM order, high nibble first)
+                const uint32_t t0 = (bv.x << 4) | (bv.x >> 8), t1 = (bv.y << 4) | (bv.y >> 8);
+                const uint32_t pk = __builtin_amdgcn_perm(t1, t0, 0x06040200u);
                 const int64_t so = (2 * (int64_t)fam + e) * stride;
                 *reinterpret_cast<uint32_t *>(P.O.seq + so / 2 + c0 / 2) = pk;
                 *reinterpret_cast<uint2 *>(P.O.qual + so + c0) = make_uint2(qlo2, qhi2);
