@@ -5,7 +5,8 @@ import ctypes as C
 import os
 
 HERE = os.path.dirname(os.path.abspath(__file__))
-LIB_PATH = os.path.join(HERE, "libbsdc.so")
+# BSDC_LIB_PATH: an alternative build of the same library (profiling A/B runs only)
+LIB_PATH = os.environ.get("BSDC_LIB_PATH") or os.path.join(HERE, "libbsdc.so")
 
 BSDC_ABI_VERSION = 3
 SMALL_BUCKETS = 8  # BSDC_SMALL_BUCKETS

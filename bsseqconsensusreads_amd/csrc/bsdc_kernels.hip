@@ -35,9 +35,13 @@
 namespace {
 
 constexpr int kWave = 64;
+#ifndef SMALL_SGPRS
+#define SMALL_SGPRS 96  // SGPR budget of k_small: <= 96 keeps 7 waves per SIMD (MI355X_MICROARCH.md)
+#endif
 constexpr int kLargeThreads = 256;
 constexpr int kSmallMaxWaves = 8;              // wavefronts (families) per small-kernel workgroup, at most
 constexpr int kSmallMinWaves = 6;              // occupancy target (waves per SIMD) the register budget is cut for
+constexpr int kSmallSimdWaves = 7;             // waves per SIMD its registers allow (<= 64 VGPRs, 82-96 SGPRs)
 constexpr int kLdsBytes = 160 * 1024;           // LDS per CU
 constexpr double kLrScale = 1048576.0;          // 2^20
 constexpr int kTabBytes = 1024 + 1024 + 384 + 2048 + 192;  // the Tables image in LDS
@@ -530,7 +534,7 @@ __device__ __forceinline__ void unpack32(uint4 v, uint8_t *dst) {
     d[1] = make_uint4(o[4], o[5], o[6], o[7]);
 }
 
-__global__ __launch_bounds__(kWave *kSmallMaxWaves, kSmallMinWaves) void k_small(KParams P, const uint32_t *fams, int64_t nfams,
+__global__ __launch_bounds__(kWave *kSmallMaxWaves, kSmallMinWaves) __attribute__((amdgpu_num_sgpr(SMALL_SGPRS))) void k_small(KParams P, const uint32_t *fams, int64_t nfams,
                                                               int32_t arena) {
     extern __shared__ __attribute__((aligned(16))) uint8_t smem[];  // the wavefronts' arenas
     __shared__ __attribute__((aligned(16))) Tables s_tab;           // static: its address folds into offsets
@@ -1803,9 +1807,10 @@ int32_t bsdc_run(bsdc_ctx *c, const bsdc_family_batch *b, bsdc_consensus *o, int
             if (nf > 0) {
                 // wavefronts per workgroup (they share one copy of the tables): 4 or 8, whichever
                 // keeps more wavefronts resident per CU; the smaller on a tie
+                // (a workgroup's wavefronts spread over the 4 SIMDs: at most kSmallSimdWaves each)
                 const int64_t a = b->small_arena[q];
-                const int64_t w4 = 4 * std::min<int64_t>(8, kLdsBytes / (kTabBytes + 4 * a));
-                const int64_t w8 = 8 * std::min<int64_t>(4, kLdsBytes / (kTabBytes + 8 * a));
+                const int64_t w4 = 4 * std::min<int64_t>(kSmallSimdWaves, kLdsBytes / (kTabBytes + 4 * a));
+                const int64_t w8 = 8 * std::min<int64_t>(kSmallSimdWaves / 2, kLdsBytes / (kTabBytes + 8 * a));
                 const int nw = w8 > w4 ? 8 : 4;
                 const size_t lds = (size_t)nw * (size_t)b->small_arena[q];  // + the static tables
                 const int64_t blocks = (nf + nw - 1) / nw;
