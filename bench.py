@@ -149,6 +149,7 @@ def main():
         e1.record(stream)
         torch.cuda.synchronize()
         t_large = e0.elapsed_time(e1) / 1e3 / ks
+    n_disp = sum(1 for b in fb.small_buckets if b.shape[0])  # one k_small dispatch per non-empty LDS bucket
     bytes_small = algorithmic_bytes(fb, out["len"], out["status"], small)
     bytes_all = algorithmic_bytes(fb, out["len"], out["status"], np.arange(fb.n_fam))
     achieved = bytes_small / t_small / 1e9
@@ -194,6 +195,8 @@ def main():
             "roofline": {"bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
                          "frac": round(achieved / HBM_PEAK_GBS, 4), "traffic": traffic,
                          "kernel": "k_small", "kernel_ms": round(t_small * 1e3, 4),
+                         "dispatches_per_launch": n_disp,
+                         "avg_dispatch_ms": round(t_small * 1e3 / max(n_disp, 1), 4),
                          "algorithmic_bytes_per_launch": bytes_small,
                          "large_kernel_ms": round(t_large * 1e3, 4),
                          "step_algorithmic_GBps": round(bytes_all / (elapsed / args.steps) / 1e9, 1)},
