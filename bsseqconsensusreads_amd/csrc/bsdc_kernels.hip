@@ -45,7 +45,7 @@ constexpr int kSmallSimdWaves = 7;             // waves per SIMD its registers a
 constexpr int kLdsBytes = 160 * 1024;           // LDS per CU
 constexpr double kLrScale = 1048576.0;          // 2^20
 constexpr int kTabBytes = 1024 + 1024 + 384 + 2048 + 192;  // the Tables image in LDS
-// k_small base bytes in LDS: nt16 code | 0x10 for A, C, G, T (set at staging, see valid4)
+// k_small base bytes in LDS: nt16 code | 0x10 for A, C, G, T (set at staging, see unpack32)
 constexpr uint32_t kLinkRdDev = 1u << 27;       // device-internal: tool 1 trimmed a base (RD=1)
 
 // nt16 codes
@@ -95,6 +95,12 @@ __device__ __forceinline__ float term(long long d) {
     const float x = (float)((double)d * 9.5367431640625e-07);
     return x < -80.0f ? 0.0f : det_expf(x);
 }
+// the same for |d| < 2^31: scaling by 2^-20 is exact, so rounding d to float first gives the
+// identical float (no i64 -> f64 -> f32 conversions)
+__device__ __forceinline__ float term32(int32_t d) {
+    const float x = (float)d * 9.5367431640625e-07f;
+    return x < -80.0f ? 0.0f : det_expf(x);
+}
 
 // Q = max k with S <= thr[k] (thr is non-increasing), binary search over 1..93
 __device__ __forceinline__ int phred_of(float S, const float *thr) {
@@ -132,15 +138,18 @@ __device__ __forceinline__ uint32_t eq4(uint32_t x, uint32_t code) {
 }
 __device__ __forceinline__ uint32_t sel4(uint32_t m, uint32_t a, uint32_t b) { return (m & a) | (~m & b); }
 
-// the conversion rule on four positions: m = m[j..j+3], m1 = m[j+1..j+4], f0 = ref[j..j+3],
-// f1 = ref[j+1..j+4], nxt = 0x0F where position j+k has a next base
-__device__ __forceinline__ uint32_t convert4(uint32_t m, uint32_t m1, uint32_t f0, uint32_t f1, uint32_t nxt) {
-    const uint32_t mA = eq4(m, kA), mC = eq4(m, kC);
-    const uint32_t cpg = eq4(f0, kC) & eq4(f1, kG);
-    const uint32_t nA = eq4(m1, kA) & nxt;
-    const uint32_t selA = sel4(eq4(f0, kG), 0x04040404u, 0x01010101u);
-    const uint32_t selC = sel4(cpg, sel4(nA, 0x08080808u, 0x02020202u), 0x08080808u);
-    return sel4(mA, selA, sel4(mC, selC, m));
+// The same rule on k_small's base bytes: m, m1 hold code | 0x10 for A/C/G/T, f0, f1 plain codes;
+// nxt80 = 0x80 where position j+k has a next base.  Equality tests are zero tests of the XOR
+// (bytes <= 0x1F), and the two rewrites are XORs: A (0x01) -> G (0x04) is ^ 0x05, C -> T ^ 0x0A,
+// which keep the 0x10 flag.
+__device__ __forceinline__ uint32_t convert4f(uint32_t m, uint32_t m1, uint32_t f0, uint32_t f1, uint32_t nxt80) {
+    auto is = [](uint32_t x, uint32_t code) {  // 0x80 in the bytes of x equal to code
+        return ~((x ^ code) + 0x7F7F7F7Fu) & 0x80808080u;
+    };
+    const uint32_t ag = is(m, 0x11111111u) & is(f0, 0x04040404u);
+    const uint32_t keepc = is(f0, 0x02020202u) & is(f1, 0x04040404u) & ~(is(m1, 0x11111111u) & nxt80);
+    const uint32_t ct = is(m, 0x12121212u) & ~keepc;
+    return m ^ ((ag >> 7) | (ag >> 5)) ^ ((ct >> 6) | (ct >> 4));
 }
 
 // Cigar of the current record for complex records: [npre x M1] + input ops (the last one
@@ -511,12 +520,10 @@ __device__ __forceinline__ void resolve4(bool ha, bool hb, uint32_t bmA, uint32_
 __device__ __forceinline__ uint32_t comp4(uint32_t x) {
     return (__builtin_bitreverse32(__builtin_bswap32(x)) >> 4) & 0x0F0F0F0Fu;
 }
-// kValid in every byte holding A, C, G or T (a one-hot nt16 code), 0 elsewhere (bytes hold 0..15)
-__device__ __forceinline__ uint32_t valid4(uint32_t x) {
-    const uint32_t z = x & ((x | 0x10101010u) - 0x01010101u);  // per byte x & (x - 1)
-    return (((x + 0x7F7F7F7Fu) & ~(z + 0x7F7F7F7Fu)) & 0x80808080u) >> 3;  // x != 0 and z == 0
-}
-// 16 packed bytes (32 nibbles, high first) -> 32 base bytes, each = code | kValid if A/C/G/T
+// 16 packed bytes (32 nibbles, high first) -> 32 base bytes.  With FLAG, each byte also gets
+// 0x10 when its base is A, C, G or T (one bit of 4 set), computed on the packed nibbles:
+// bits a..d of every nibble at once, one-hot = any & !two.
+template <bool FLAG>
 __device__ __forceinline__ void unpack32(uint4 v, uint8_t *dst) {
     const uint32_t w[4] = {v.x, v.y, v.z, v.w};
     uint32_t o[8];
@@ -524,8 +531,14 @@ __device__ __forceinline__ void unpack32(uint4 v, uint8_t *dst) {
     for (int k = 0; k < 4; k++) {
         uint32_t lo = w[k] & 0x0F0F0F0Fu;
         uint32_t hi = (w[k] >> 4) & 0x0F0F0F0Fu;
-        lo |= valid4(lo);
-        hi |= valid4(hi);
+        if (FLAG) {
+            const uint32_t a = w[k], b = w[k] >> 1, c = w[k] >> 2, d = w[k] >> 3;
+            const uint32_t ab = a | b, cd = c | d;
+            const uint32_t two = (a & b) | (c & d) | (ab & cd);
+            const uint32_t vm = (ab | cd) & ~two & 0x11111111u;  // bit 4k: nibble k is one-hot
+            lo |= (vm << 4) & 0x10101010u;
+            hi |= vm & 0x10101010u;
+        }
         o[2 * k] = __builtin_amdgcn_perm(lo, hi, 0x05010400u);
         o[2 * k + 1] = __builtin_amdgcn_perm(lo, hi, 0x07030602u);
     }
@@ -592,7 +605,7 @@ __global__ __launch_bounds__(kWave *kSmallMaxWaves, kSmallMinWaves) __attribute_
         if (k < nqc)
             *reinterpret_cast<uint4 *>(qimg + 16 * k) = v;
         else if (k < nch)
-            unpack32(v, bimg + 32 * (k - nqc));
+            unpack32<true>(v, bimg + 32 * (k - nqc));
     };
     uint4 v[4];
 #pragma unroll
@@ -640,7 +653,7 @@ __global__ __launch_bounds__(kWave *kSmallMaxWaves, kSmallMinWaves) __attribute_
     auto store_win = [&](int k, uint4 x) {
         if (k < wtot) {
             const uint32_t cr = __umulhi((uint32_t)k, rinv), part = (uint32_t)k - cr * rcn;
-            unpack32(x, refw + cr * ws + 32 * part);
+            unpack32<false>(x, refw + cr * ws + 32 * part);
         }
     };
     uint4 wv[2];
@@ -696,14 +709,15 @@ __global__ __launch_bounds__(kWave *kSmallMaxWaves, kSmallMinWaves) __attribute_
                         if (j4 + k + 1 >= s_avail) f1 = (f1 & ~(0xFFu << (8 * k))) | (kN << (8 * k));
                     }
                 }
-                if (j4 == 0) m = (m & ~0xFFu) | (f0 & 0xFFu);  // :121 seed, m[0] = ref[0]
+                if (j4 == 0) {  // :121 seed, m[0] = ref[0] (flagged when A/C/G/T)
+                    const uint32_t r0b = f0 & 0xFFu;
+                    m = (m & ~0xFFu) | r0b | ((r0b != 0 && (r0b & (r0b - 1)) == 0) ? 0x10u : 0u);
+                }
                 const uint32_t m1 = alignbyte(mn, m, 1);
-                uint32_t nxt = 0x0F0F0F0Fu;
+                uint32_t nxt = 0x80808080u;
                 const int last = Lm - 1 - j4;  // the record's last position has no next base
                 if (last >= 0 && last < 4) nxt &= ~(0xFFu << (8 * last));
-                // A->G, C->T keep a base A/C/G/T, so the A/C/G/T flags (0x10) of m carry over
-                const uint32_t out = convert4(m & 0x0F0F0F0Fu, m1 & 0x0F0F0F0Fu, f0 & 0x0F0F0F0Fu, f1 & 0x0F0F0F0Fu, nxt) |
-                                     (m & 0x10101010u);
+                const uint32_t out = convert4f(m, m1, f0, f1, nxt);
                 st32(bimg + s_slot + j4, out);
                 if (last >= 0 && last < 4)  // :157-170 a final C before a reference G is trimmed
                     my_rd = ((out >> (8 * last)) & 0x0F) == kC && ((f1 >> (8 * last)) & 0x0F) == kG;
@@ -1079,11 +1093,11 @@ __global__ __launch_bounds__(kWave *kSmallMaxWaves, kSmallMinWaves) __attribute_
                 if (D1 > Db) { best = 1; Db = D1; }
                 if (D2 > Db) { best = 2; Db = D2; }
                 if (D3 > Db) { best = 3; Db = D3; }
-                float S = 0.0f;
-                if (best != 0) S += term((long long)D0 - Db);
-                if (best != 1) S += term((long long)D1 - Db);
-                if (best != 2) S += term((long long)D2 - Db);
-                if (best != 3) S += term((long long)D3 - Db);
+                float S = 0.0f;  // |D| < 2^30 here (<= 64 reads)
+                if (best != 0) S += term32(D0 - Db);
+                if (best != 1) S += term32(D1 - Db);
+                if (best != 2) S += term32(D2 - Db);
+                if (best != 3) S += term32(D3 - Db);
                 const int Q = phred_of(S, thr);
                 vb[side] = Q < 2 ? kN : (1u << best);
                 vq[side] = Q < 2 ? 2u : (uint32_t)Q;
