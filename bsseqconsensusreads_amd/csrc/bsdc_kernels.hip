@@ -458,6 +458,47 @@ __device__ __forceinline__ uint32_t ldsu32(const uint8_t *p) {
     __builtin_memcpy(&v, p, 4);
     return v;
 }
+__device__ __forceinline__ void stu32(uint8_t *p, uint32_t v) { __builtin_memcpy(p, &v, 4); }
+// 0x80 in every byte of x that is 0 (bytes <= 0x80)
+__device__ __forceinline__ uint32_t zero80(uint32_t x) { return ~(x + 0x7F7F7F7Fu) & 0x80808080u; }
+__device__ __forceinline__ uint32_t expand80(uint32_t m80);
+// Overlapping-bases consensus of 4 consecutive positions of one template: mate a's bytes at ia,
+// mate b's at ib, rem (>= 1) positions of the overlap left.  Same rules as the per-position path
+// (agree: both quals min(qa + qb, 93); disagree: the higher quality's base on both, quals
+// |qa - qb|; equal quals: N / 2; an N on either side: untouched).  Base bytes carry the 0x10
+// A/C/G/T flag (N = 0x0F has none); quals must be < 128 (the caller checks).
+__device__ __forceinline__ void overlap4(uint8_t *bimg, uint8_t *qimg, uint32_t ia, uint32_t ib, int rem) {
+    const uint32_t X = ldsu32(bimg + ia), Y = ldsu32(bimg + ib);
+    const uint32_t QA = ldsu32(qimg + ia), QB = ldsu32(qimg + ib);
+    const uint32_t in = rem >= 4 ? 0xFFFFFFFFu : (1u << (8 * rem)) - 1u;
+    const uint32_t act = expand80(~(zero80(X ^ 0x0F0F0F0Fu) | zero80(Y ^ 0x0F0F0F0Fu)) & 0x80808080u) & in;
+    const uint32_t eq = expand80(zero80(X ^ Y));
+    const uint32_t ge = expand80(((QA | 0x80808080u) - QB) & 0x80808080u);  // qa >= qb
+    const uint32_t qe = expand80(zero80(QA ^ QB));
+    const uint32_t sum = QA + QB;                                           // <= 254
+    const uint32_t over = expand80((sum | ((sum & 0x7F7F7F7Fu) + 0x22222222u)) & 0x80808080u);  // >= 94
+    const uint32_t sum93 = (sum & ~over) | (0x5D5D5D5Du & over);
+    const uint32_t ad = ((((QA | 0x80808080u) - QB) & ge) | (((QB | 0x80808080u) - QA) & ~ge)) & 0x7F7F7F7Fu;
+    const uint32_t nq = (sum93 & eq) | (((ad & ~qe) | (0x02020202u & qe)) & ~eq);
+    const uint32_t w = (X & ge) | (Y & ~ge);              // the higher quality's base
+    const uint32_t v = (w & ~qe) | (0x0F0F0F0Fu & qe);    // equal quals: N
+    const uint32_t nx = (X & eq) | (v & ~eq), ny = (Y & eq) | (v & ~eq);
+    const uint32_t ox = (nx & act) | (X & ~act), oy = (ny & act) | (Y & ~act);
+    const uint32_t oqa = (nq & act) | (QA & ~act), oqb = (nq & act) | (QB & ~act);
+    if (rem >= 4) {
+        stu32(bimg + ia, ox);
+        stu32(bimg + ib, oy);
+        stu32(qimg + ia, oqa);
+        stu32(qimg + ib, oqb);
+    } else {  // the bytes past the overlap may belong to another template's read: byte stores
+        for (int k = 0; k < rem; k++) {
+            bimg[ia + k] = (uint8_t)(ox >> (8 * k));
+            bimg[ib + k] = (uint8_t)(oy >> (8 * k));
+            qimg[ia + k] = (uint8_t)(oqa >> (8 * k));
+            qimg[ib + k] = (uint8_t)(oqb >> (8 * k));
+        }
+    }
+}
 // D0..D3 += lr2[v_j][q_j] for the 4 bytes of b (base bytes, kValid flag = v) and q (quals).  The
 // index (v << 8 | q) * 4 is built two columns at a time: v_perm interleaves [q_j, v_j] into 16-bit
 // halves (<= 511, so one 32-bit shift scales both halves).
@@ -601,10 +642,13 @@ __global__ __launch_bounds__(kWave *kSmallMaxWaves, kSmallMinWaves) __attribute_
             v = *reinterpret_cast<const uint4 *>(B.seq + (base_g >> 1) + 16 * (uint32_t)(k - nqc));
         return v;
     };
+    uint32_t qor = 0;  // OR of every qual byte this lane stages (0x80 set: a qual >= 128)
     auto store_img = [&](int k, uint4 v) {
-        if (k < nqc)
+        if (k < nqc) {
             *reinterpret_cast<uint4 *>(qimg + 16 * k) = v;
-        else if (k < nch)
+            qor |= v.x | v.y | v.z | v.w;
+        } else
+        if (k >= nqc && k < nch)
             unpack32<true>(v, bimg + 32 * (k - nqc));
     };
     uint4 v[4];
@@ -806,30 +850,38 @@ __global__ __launch_bounds__(kWave *kSmallMaxWaves, kSmallMinWaves) __attribute_
     }
     if (!do_vote || stop == 3) return;
 
-    // ---- overlapping-bases consensus, one template at a time ----
+    // ---- overlapping-bases consensus ----
+    // Every R1 lane gets its mate's state by lane shuffles and computes the template's overlap.
+    // Templates with simple cigars then run 4 at a time, 16 lanes each, 4 positions per lane
+    // (overlap4); a complex cigar, or a family with a quality byte >= 128, takes the
+    // per-position path one template at a time.
     const uint32_t mate = link & BSDC_LINK_MATE_MASK;
     const bool usable = has && (link & BSDC_LINK_USABLE);
     if (P.overlap) {
         const bool mate_ok = usable && mate != BSDC_LINK_MATE_MASK && !(flag & 4);
-        uint64_t tm = ballot(mate_ok);
+        const int ml = mate_ok ? (int)mate : t;
+        const uint32_t b_link = (uint32_t)__shfl((int)link, ml, kWave), b_flag = (uint32_t)__shfl((int)flag, ml, kWave);
+        const int32_t b_pos = __shfl(pos, ml, kWave), b_reflen = __shfl(reflen, ml, kWave);
+        const uint32_t b_base = (uint32_t)__shfl((int)(slot + (uint32_t)start), ml, kWave);
+        const int32_t s0 = ::max(pos, b_pos), e0 = ::min(pos + reflen - 1, b_pos + b_reflen - 1);
+        const bool ok = mate_ok && (b_link & BSDC_LINK_USABLE) && !(b_flag & 4) && reflen > 0 && b_reflen > 0 &&
+                        s0 <= e0;
+        const bool wild = ballot((qor & 0x80808080u) != 0) != 0;
+        const bool fast = ok && !((link | b_link) & BSDC_LINK_COMPLEX) && !wild;
+        uint64_t tm = ballot(ok && !fast);
         while (tm) {
             const int a = __builtin_ctzll(tm);
             tm &= tm - 1;
             const int b = (int)rlu(mate, a);
             const uint32_t la_ = rlu(link, a), lb_ = rlu(link, b);
-            if (!(lb_ & BSDC_LINK_USABLE) || (rlu(flag, b) & 4)) continue;
             const int32_t pa = rl(pos, a), pb = rl(pos, b), la = rl(len, a), lb = rl(len, b);
-            const int32_t ra = rl(reflen, a), rbn = rl(reflen, b);
-            if (ra <= 0 || rbn <= 0) continue;
-            const int32_t s0 = ::max(pa, pb);
-            const int32_t e0 = ::min(pa + ra - 1, pb + rbn - 1);
-            if (s0 > e0) continue;
+            const int32_t ps0 = rl(s0, a), pe0 = rl(e0, a);
             const uint32_t sa = rlu(slot, a) + (uint32_t)rl(start, a), sb = rlu(slot, b) + (uint32_t)rl(start, b);
             const bool ca = la_ & BSDC_LINK_COMPLEX, cb = lb_ & BSDC_LINK_COMPLEX;
             CigView va, vb;
             if (ca) va = make_cigview(B, r0 + a, la_, do_convert && (la_ & BSDC_LINK_CONVERT), (la_ & kLinkRdDev) != 0, do_extend);
             if (cb) vb = make_cigview(B, r0 + b, lb_, do_convert && (lb_ & BSDC_LINK_CONVERT), (lb_ & kLinkRdDev) != 0, do_extend);
-            for (int32_t p = s0 + t; p <= e0; p += 64) {
+            for (int32_t p = ps0 + t; p <= pe0; p += 64) {
                 const int ia = ca ? read_at_ref(va, pa, la, p) : (p - pa < la ? p - pa : -1);
                 const int ib = cb ? read_at_ref(vb, pb, lb, p) : (p - pb < lb ? p - pb : -1);
                 if (ia < 0 || ib < 0) continue;
@@ -849,6 +901,26 @@ __global__ __launch_bounds__(kWave *kSmallMaxWaves, kSmallMinWaves) __attribute_
                 } else {
                     bimg[sa + ia] = bimg[sb + ib] = (uint8_t)kN;
                     qimg[sa + ia] = qimg[sb + ib] = 2;
+                }
+            }
+        }
+        const uint64_t fm = ballot(fast);
+        const int nt = __builtin_popcountll(fm);
+        if (nt > 0) {
+            uint32_t *tinfo = reinterpret_cast<uint32_t *>(A + Lo.ref);  // R: the windows are dead
+            if (fast) {
+                const int i = mbcnt(fm);
+                tinfo[3 * i] = slot + (uint32_t)start + (uint32_t)(s0 - pos);
+                tinfo[3 * i + 1] = b_base + (uint32_t)(s0 - b_pos);
+                tinfo[3 * i + 2] = (uint32_t)(e0 - s0 + 1);
+            }
+            wave_sync();
+            for (int g0 = 0; g0 < nt; g0 += 4) {
+                const int g = g0 + (t >> 4);
+                if (g < nt) {
+                    const uint32_t xa = tinfo[3 * g], xb = tinfo[3 * g + 1];
+                    const int ovl = (int)tinfo[3 * g + 2];
+                    for (int j = 4 * (t & 15); j < ovl; j += 64) overlap4(bimg, qimg, xa + (uint32_t)j, xb + (uint32_t)j, ovl - j);
                 }
             }
         }
