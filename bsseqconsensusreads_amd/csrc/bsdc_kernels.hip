@@ -597,7 +597,9 @@ __global__ __launch_bounds__(kWave *kSmallMaxWaves, kSmallMinWaves) __attribute_
     const float *thr = T->thr;
     const uint8_t *qlo = T->qlo;
     const int32_t *dthr = T->dthr;
+    if (((P.mode >> BSDC_MODE_STOP_SHIFT) & 15) == 15) return;  // profiling: launch cost alone
     load_tables(P.tab, reinterpret_cast<uint8_t *>(&s_tab));
+    if (((P.mode >> BSDC_MODE_STOP_SHIFT) & 15) == 14) return;  // profiling: + the table copy
     const int w = threadIdx.x >> 6;
     const int t = threadIdx.x & 63;
     const int64_t fi = (int64_t)blockIdx.x * (blockDim.x >> 6) + w;

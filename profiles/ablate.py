@@ -14,7 +14,7 @@ from bsseqconsensusreads_amd._lib import MODE_CONVERT, MODE_EXTEND, MODE_VOTE, M
 from bsseqconsensusreads_amd.device import Engine  # noqa: E402
 
 # (name, stop code): the kernel returns after the named phase
-PHASES = [("staging", 1), ("convert", 2), ("extend", 3), ("overlap", 4), ("srcreads+lists", 5),
+PHASES = [("launch", 15), ("tables", 14), ("staging", 1), ("convert", 2), ("extend", 3), ("overlap", 4), ("srcreads+lists", 5),
           ("vote-preamble", 6), ("vote-main", 7), ("vote-queue", 8), ("full", 0)]
 
 ap = argparse.ArgumentParser()

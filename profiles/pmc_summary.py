@@ -6,7 +6,7 @@ import json
 import sys
 
 d = sys.argv[1]
-PH = ["staging", "convert", "extend", "overlap", "srcreads+lists", "vote-preamble", "vote-main", "vote-queue", "full"]
+PH = ["launch", "tables", "staging", "convert", "extend", "overlap", "srcreads+lists", "vote-preamble", "vote-main", "vote-queue", "full"]
 RUNS = 12  # 2 warmup + 10 timed per phase
 res = collections.defaultdict(lambda: collections.defaultdict(float))
 for f in sorted(glob.glob(d + "/p*/**/*counter_collection.csv", recursive=True)):
