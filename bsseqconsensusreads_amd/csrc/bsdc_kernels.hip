@@ -530,11 +530,15 @@ __device__ __forceinline__ uint32_t bytes_nonzero(uint32_t x) {  // 0xFF where t
 // Q < 2 -> (N, 2); one side absent -> the other side; both -> agree: sum, else the higher
 // quality's base with the difference, equal qualities -> 2; capped at 93; N or 2 -> (N, 2).
 __device__ __forceinline__ void resolve4(bool ha, bool hb, uint32_t bmA, uint32_t QA, uint32_t bmB, uint32_t QB,
-                                         uint32_t &ob, uint32_t &oq) {
+                                         uint32_t &ob, uint32_t &oq, uint32_t *ss) {
     const uint32_t okA = expand80((QA + 0x7E7E7E7Eu) & 0x80808080u);  // Q >= 2
     const uint32_t okB = expand80((QB + 0x7E7E7E7Eu) & 0x80808080u);
     const uint32_t bA = (bmA & okA) | (0x0F0F0F0Fu & ~okA), qA = (QA & okA) | (0x02020202u & ~okA);
     const uint32_t bB = (bmB & okB) | (0x0F0F0F0Fu & ~okB), qB = (QB & okB) | (0x02020202u & ~okB);
+    ss[0] = bA;  // the single-strand results: side A bases, quals, side B bases, quals
+    ss[1] = qA;
+    ss[2] = bB;
+    ss[3] = qB;
     if (!(ha && hb)) {
         ob = ha ? bA : bB;
         oq = ha ? qA : qB;
@@ -1097,34 +1101,45 @@ __global__ __launch_bounds__(kWave *kSmallMaxWaves, kSmallMinWaves) __attribute_
                         if (i < na) rev(__builtin_amdgcn_readfirstlane(dl[i]));
                     }
                 }
-                uint32_t bm[2], multi = 0;
+                uint32_t bm[2], multi[2];
 #pragma unroll
                 for (int side = 0; side < 2; side++) {
                     bm[side] = (mf[side] & 0x0F0F0F0Fu) | comp4(__builtin_bswap32(mr[side] & 0x0F0F0F0Fu));
                     const uint32_t x = bm[side];
-                    multi |= x & ((x | 0x10101010u) - 0x01010101u);  // per byte: more than one base seen
+                    multi[side] = x & ((x | 0x10101010u) - 0x01010101u);  // per byte: more than one base seen
                 }
                 const int sa = e == 0 ? 0 : 1, sb = e == 0 ? 3 : 2;
                 // per side and column: Q from the sum alone (valid when the column is not slow)
-                uint32_t Qp[2] = {0, 0};
-                bool neg_d[4] = {false, false, false, false};
+                uint32_t Qp[2] = {0, 0}, negm[2] = {0, 0};
 #pragma unroll
                 for (int side = 0; side < 2; side++) {
 #pragma unroll
                     for (int j = 0; j < 4; j++) {
                         const int32_t dsum = D[side][j];
-                        neg_d[j] |= dsum < 0;
+                        negm[side] |= dsum < 0 ? 0xFFu << (8 * j) : 0u;
                         const int32_t d = ::min(::max(dsum, 0), (int32_t)((1 << 27) - 1));
                         const uint32_t q0 = qlo[d >> 16];
                         Qp[side] |= (q0 + (d >= dthr[q0 + 1] ? 1u : 0u)) << (8 * j);
                     }
                 }
-                uint32_t ob4, oq4;
-                resolve4(hs[sa], hs[sb], bm[0], Qp[0], bm[1], Qp[1], ob4, oq4);
-                // slow columns: a side saw more than one base, or a negative sum
+                uint32_t ob4, oq4, ss[4];
+                resolve4(hs[sa], hs[sb], bm[0], Qp[0], bm[1], Qp[1], ob4, oq4, ss);
+                // slow columns: a side saw more than one base, or a negative sum.  The queued
+                // path recomputes only the slow side(s): the other side's single-strand result
+                // rides in the column's output bytes (base | 0x10 if it is side B; qual 0 = none).
+                const uint32_t slowA = hs[sa] ? bytes_nonzero(multi[0] & 0x7F7F7F7Fu) | negm[0] : 0u;
+                const uint32_t slowB = hs[sb] ? bytes_nonzero(multi[1] & 0x7F7F7F7Fu) | negm[1] : 0u;
+                const uint32_t slow4 = slowA | slowB;
+                if (slow4) {
+                    const uint32_t useA = hs[sa] ? ~slowA : 0u, useB = (hs[sb] ? ~slowB : 0u) & ~useA;
+                    const uint32_t fb = (ss[0] & useA) | ((ss[2] | 0x10101010u) & useB);
+                    const uint32_t fq = (ss[1] & useA) | (ss[3] & useB);
+                    ob4 = (ob4 & ~slow4) | (fb & slow4);
+                    oq4 = (oq4 & ~slow4) | (fq & slow4);
+                }
 #pragma unroll
                 for (int j = 0; j < 4; j++) {
-                    const bool qd = (((multi >> (8 * j)) & 0xFFu) != 0 || neg_d[j]) && c + j < ol;
+                    const bool qd = ((slow4 >> (8 * j)) & 0xFFu) != 0 && c + j < ol;
                     const uint64_t ms = ballot(qd);
                     if (qd) sq[nq + mbcnt(ms)] = (uint16_t)((e << 15) | (c + j));
                     nq += __builtin_popcountll(ms);
@@ -1145,10 +1160,16 @@ __global__ __launch_bounds__(kWave *kSmallMaxWaves, kSmallMinWaves) __attribute_
             const uint32_t ent = act ? sq[k] : 0u;
             const int e = (int)(ent >> 15), c = (int)(ent & 0x7FFF);
             const int sa = e == 0 ? 0 : 1, sb = e == 0 ? 3 : 2;
+            const uint32_t kb = act ? outb[e * ow + c] : 0u, kq = act ? outq[e * ow + c] : 0u;  // kept side
             uint32_t vb[2] = {0, 0}, vq[2] = {0, 0};
             for (int side = 0; side < 2; side++) {
                 const int s = side == 0 ? sa : sb;  // per lane: lanes of both ends mix here
                 if (!act || !hs[s]) continue;
+                if (kq != 0 && (int)((kb >> 4) & 1) == side) {
+                    vb[side] = kb & 0x0F;
+                    vq[side] = kq;
+                    continue;
+                }
                 int32_t D0 = 0, D1 = 0, D2 = 0, D3 = 0;
                 for (int i = 0; i < cnt[s]; i++) {
                     const uint32_t d = dlist[off[s] + i];
