@@ -8,7 +8,7 @@ HERE = os.path.dirname(os.path.abspath(__file__))
 # BSDC_LIB_PATH: an alternative build of the same library (profiling A/B runs only)
 LIB_PATH = os.environ.get("BSDC_LIB_PATH") or os.path.join(HERE, "libbsdc.so")
 
-BSDC_ABI_VERSION = 3
+BSDC_ABI_VERSION = 4
 SMALL_BUCKETS = 8  # BSDC_SMALL_BUCKETS
 MODE_CONVERT, MODE_EXTEND, MODE_VOTE, MODE_DUMP = 1, 2, 4, 8
 MODE_SKIP_SMALL, MODE_SKIP_LARGE = 16, 32

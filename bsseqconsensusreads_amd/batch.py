@@ -101,7 +101,7 @@ class FamilyBatch:
     qual: np.ndarray         # u8, slot layout
     small_buckets: List[np.ndarray]  # 4 lists of family ids (u32), one per LDS arena size
     small_arenas: List[int]
-    large_fams: np.ndarray   # u32
+    large_fams: np.ndarray   # u32 [n_large, 4] family, first record, n_rec, image bytes
     fam_entry: np.ndarray    # u32 [F, 4] small-kernel list entry of each family
     max_len: int
     large_arena: int
@@ -481,7 +481,7 @@ def build_family_batch(raw: R.RawRecords, mode: str = "full", ref: Optional[R.Re
     cops = np.bincount(fam_of, weights=cnt_c, minlength=nf)[:nf].astype(np.int64) if nr else np.zeros(nf, np.int64)
     nconv = np.bincount(fam_of, weights=convb.astype(np.int64), minlength=nf)[:nf].astype(np.int64) if nr else np.zeros(nf, np.int64)
     need_s = small_arena_bytes(fam_sizes, img, nconv, cops, max_len)
-    need_l = large_arena_bytes(fam_sizes, 2 * span, max_len_f, cops)
+    need_l = large_arena_bytes(fam_sizes, 2 * img, max_len_f, cops)
     small = (fam_sizes <= 64) & (need_s <= small_cap) & (img // 32 < (1 << 24))
     buckets, arenas = [], []
     lo = -1
@@ -497,7 +497,14 @@ def build_family_batch(raw: R.RawRecords, mode: str = "full", ref: Optional[R.Re
     while len(buckets) < len(SMALL_BUCKETS):
         buckets.append(np.zeros(0, np.uint32))
         arenas.append(16)
-    large_fams = np.nonzero(~small)[0].astype(np.uint32)
+    lf = np.nonzero(~small)[0]
+    # large-family list entries: family, first record, n, image bytes (the image starts at the first slot)
+    large_fams = np.zeros((lf.shape[0], 4), np.int64)
+    large_fams[:, 0] = lf
+    large_fams[:, 1] = fam_off[lf]
+    large_fams[:, 2] = fam_sizes[lf]
+    large_fams[:, 3] = img[lf]
+    large_fams = large_fams.astype(np.uint32)
     large_arena = int(round16(need_l[~small].max())) if (~small).any() else 16
 
     # small-family list entries: family, first record, n | (image / 32) << 8, image base

@@ -142,13 +142,16 @@ __device__ __forceinline__ uint32_t sel4(uint32_t m, uint32_t a, uint32_t b) { r
 // nxt80 = 0x80 where position j+k has a next base.  Equality tests are zero tests of the XOR
 // (bytes <= 0x1F), and the two rewrites are XORs: A (0x01) -> G (0x04) is ^ 0x05, C -> T ^ 0x0A,
 // which keep the 0x10 flag.
+// (FLAG = false: m, m1 hold plain codes too -- k_large)
+template <bool FLAG = true>
 __device__ __forceinline__ uint32_t convert4f(uint32_t m, uint32_t m1, uint32_t f0, uint32_t f1, uint32_t nxt80) {
     auto is = [](uint32_t x, uint32_t code) {  // 0x80 in the bytes of x equal to code
         return ~((x ^ code) + 0x7F7F7F7Fu) & 0x80808080u;
     };
-    const uint32_t ag = is(m, 0x11111111u) & is(f0, 0x04040404u);
-    const uint32_t keepc = is(f0, 0x02020202u) & is(f1, 0x04040404u) & ~(is(m1, 0x11111111u) & nxt80);
-    const uint32_t ct = is(m, 0x12121212u) & ~keepc;
+    constexpr uint32_t kA4 = FLAG ? 0x11111111u : 0x01010101u, kC4 = FLAG ? 0x12121212u : 0x02020202u;
+    const uint32_t ag = is(m, kA4) & is(f0, 0x04040404u);
+    const uint32_t keepc = is(f0, 0x02020202u) & is(f1, 0x04040404u) & ~(is(m1, kA4) & nxt80);
+    const uint32_t ct = is(m, kC4) & ~keepc;
     return m ^ ((ag >> 7) | (ag >> 5)) ^ ((ct >> 6) | (ct >> 4));
 }
 
@@ -1308,13 +1311,13 @@ __device__ __forceinline__ int block_max(int v, int *red) {
     return s;
 }
 
-__device__ void process_large(const KParams &P, uint8_t *A, const int32_t *lr, const float *thr, uint32_t fam, int *red,
+__device__ void process_large(const KParams &P, uint8_t *A, const int32_t *lr, const float *thr, uint4 ent, int *red,
                               int *s_cnt, int *s_lc) {
     constexpr int G = kLargeThreads;
     const int tt = threadIdx.x;
     const bsdc_family_batch &B = P.B;
-    const uint32_t r0 = B.fam_off[fam];
-    const int n = (int)(B.fam_off[fam + 1] - r0);
+    const uint32_t fam = ent.x, r0 = ent.y, img = ent.w;  // list entry: family, first record, n, image bytes
+    const int n = (int)ent.z;
     const bool do_convert = P.mode & BSDC_MODE_CONVERT;
     const bool do_extend = P.mode & BSDC_MODE_EXTEND;
     const bool do_vote = P.mode & BSDC_MODE_VOTE;
@@ -1335,7 +1338,10 @@ __device__ void process_large(const KParams &P, uint8_t *A, const int32_t *lr, c
     uint8_t *ssb = A + Lo.ssb;
     uint8_t *ssq = A + Lo.ssq;
     uint32_t *simp = reinterpret_cast<uint32_t *>(A + Lo.simp);
+    // the family image as in HBM: bases (one byte each) at slots + slot, quals at slots + img + slot
+    // (RecMeta::cap = img, so `base + cap` addresses a base's qual)
     uint8_t *slots = A + Lo.slots;
+    uint8_t *qimg = slots + img;
     const int ssw = Lo.ssw;
 
     // ---- record metadata ----
@@ -1347,8 +1353,8 @@ __device__ void process_large(const KParams &P, uint8_t *A, const int32_t *lr, c
         m.flag = (uint16_t)(rc.z >> 16);
         m.pos = (int32_t)rc.y;
         m.len = m.in_len;
-        m.cap = m.in_len + 2;
-        m.slot = 2u * (rc.x - off0);
+        m.cap = (int32_t)img;
+        m.slot = rc.x - off0;
         m.start = 1;
         m.link = rc.w;
         m.gidx = gi;
@@ -1361,45 +1367,78 @@ __device__ void process_large(const KParams &P, uint8_t *A, const int32_t *lr, c
     }
     __syncthreads();
 
-    // ---- stage bases + tool-1 conversion ----
-    for (int r = 0; r < n; r++) {
-        const RecMeta m = M[r];
-        const int32_t Lin = m.in_len;
-        const int64_t ib = (int64_t)B.rec[4 * (size_t)m.gidx] + 1;  // the record's first base
-        uint8_t *sb = slots + m.slot;
-        uint8_t *sq = sb + m.cap;
-        if (do_convert && (m.link & BSDC_LINK_CONVERT)) {
-            const int32_t Lm = Lin + 1;
-            const int32_t np = m.pos - 1 > 0 ? m.pos - 1 : 0;
-            const int32_t avail = (int32_t)B.rec_win[2 * (size_t)m.gidx + 1];
-            for (int j = tt; j < Lm; j += G) {
-                const uint32_t f0 = j < avail ? nib(P.ref, (int64_t)m.win + j) : kN;
-                const uint32_t f1 = j + 1 < avail ? nib(P.ref, (int64_t)m.win + j + 1) : kN;
-                const uint32_t m0 = j == 0 ? f0 : nib(B.seq, ib + j - 1);
-                const bool has_next = j + 1 < Lm;
-                const uint32_t m1 = has_next ? nib(B.seq, ib + j) : kN;
-                const uint32_t o = convert_rule(m0, m1, has_next, f0, f1);
-                sb[j] = (uint8_t)o;
-                sq[j] = j == 0 ? (uint8_t)40 : B.qual[ib + j - 1];
-                if (j == Lm - 1) {
-                    const uint32_t f2 = Lm < avail ? nib(P.ref, (int64_t)m.win + Lm) : kN;
-                    const uint8_t rdv = (f2 == kG && o == kC) ? 1 : 0;
-                    RecMeta &w = M[r];
-                    w.rd = rdv;
-                    w.len = Lm - rdv;
-                    w.start = 0;
-                    w.pos = np;
-                    w.reflen = m.reflen + 1 - ((rdv && m.reflen > 0) ? 1 : 0);
-                }
-            }
-        } else {
-            for (int j = tt; j < Lin; j += G) {
-                sb[1 + j] = (uint8_t)nib(B.seq, ib + j);
-                sq[1 + j] = B.qual[ib + j];
+    // ---- stage the image: every 16-byte chunk, quals as they are, packed bases unpacked ----
+    {
+        const int nqc = (int)(img >> 4), nch = nqc + (int)(img >> 5);
+        for (int k = tt; k < nch; k += G) {
+            if (k < nqc) {
+                *reinterpret_cast<uint4 *>(qimg + 16 * k) = *reinterpret_cast<const uint4 *>(B.qual + off0 + 16 * (uint32_t)k);
+            } else {
+                const uint4 v = *reinterpret_cast<const uint4 *>(B.seq + (off0 >> 1) + 16 * (uint32_t)(k - nqc));
+                unpack32<false>(v, slots + 32 * (k - nqc));
             }
         }
     }
     __syncthreads();
+
+    // ---- tool 1 (tools/1.convert_AG_to_CT.py:84-183): every converted record at once, 4 positions
+    // per thread, flattened over (converted record, dword).  Each chunk of G dwords reads first and
+    // writes after a barrier: a dword's rule also reads the next dword's original bases ----
+    if (do_convert) {
+        uint16_t *clist = lists;  // the converted records (until the read lists are built)
+        if (tt == 0) s_cnt[0] = 0;
+        __syncthreads();
+        for (int r = tt; r < n; r += G)
+            if (M[r].link & BSDC_LINK_CONVERT) clist[atomicAdd(&s_cnt[0], 1)] = (uint16_t)r;
+        __syncthreads();
+        const int nc = s_cnt[0];
+        const int SD = (maxlen_f + 1 + 3) >> 2;  // dwords per converted record, at most
+        const int total = nc * SD;
+        for (int base = 0; base < total; base += G) {
+            const int k = base + tt;
+            uint32_t out = 0, wa = 0;
+            bool wr = false;
+            if (k < total) {
+                const int ci = k / SD, j4 = 4 * (k - ci * SD);
+                const int r = clist[ci];
+                const RecMeta m = M[r];
+                const int32_t Lm = m.in_len + 1;
+                if (j4 < Lm) {
+                    const int32_t avail = (int32_t)B.rec_win[2 * (size_t)m.gidx + 1];
+                    uint32_t m4 = lds32(slots + m.slot + j4);
+                    const uint32_t mn = lds32(slots + m.slot + j4 + 4);
+                    uint32_t f0 = 0, f1 = 0;
+#pragma unroll
+                    for (int q = 0; q < 5; q++) {
+                        const uint32_t fb = j4 + q < avail ? nib(P.ref, (int64_t)m.win + j4 + q) : kN;
+                        if (q < 4) f0 |= fb << (8 * q);
+                        if (q > 0) f1 |= fb << (8 * (q - 1));
+                    }
+                    if (j4 == 0) m4 = (m4 & ~0xFFu) | (f0 & 0xFFu);  // :121 seed, m[0] = ref[0]
+                    const uint32_t m1 = alignbyte(mn, m4, 1);
+                    uint32_t nxt = 0x80808080u;
+                    const int last = Lm - 1 - j4;  // the record's last position has no next base
+                    if (last < 4) nxt &= ~(0xFFu << (8 * last));
+                    out = convert4f<false>(m4, m1, f0, f1, nxt);
+                    wa = m.slot + (uint32_t)j4;
+                    wr = true;
+                    if (j4 == 0) qimg[m.slot] = 40;  // :174-177 'I' + quals
+                    if (last < 4) {  // :157-170 a final C before a reference G is trimmed
+                        const uint8_t rdv = (((out >> (8 * last)) & 0xFF) == kC && ((f1 >> (8 * last)) & 0xFF) == kG) ? 1 : 0;
+                        RecMeta &w = M[r];
+                        w.rd = rdv;
+                        w.len = Lm - rdv;
+                        w.start = 0;
+                        w.pos = m.pos - 1 > 0 ? m.pos - 1 : 0;
+                        w.reflen = m.reflen + 1 - ((rdv && m.reflen > 0) ? 1 : 0);
+                    }
+                }
+            }
+            __syncthreads();
+            if (wr) st32(slots + wa, out);
+            __syncthreads();
+        }
+    }
     if (!do_convert) {
         for (int r = tt; r < n; r += G)
             if (M[r].link & BSDC_LINK_RD_IN) M[r].rd = 1;
@@ -1695,7 +1734,7 @@ __global__ __launch_bounds__(kLargeThreads) void k_large(KParams P) {
     const int64_t i = blockIdx.x;
     if (i >= P.B.n_large) return;
     uint8_t *A = IN_LDS ? smem : P.O.scratch + (size_t)i * (size_t)P.B.large_arena;
-    process_large(P, A, lr, thr, P.B.large_fams[i], red, s_cnt, s_lc);
+    process_large(P, A, lr, thr, reinterpret_cast<const uint4 *>(P.B.large_fams)[i], red, s_cnt, s_lc);
 }
 
 }  // namespace

@@ -24,7 +24,7 @@
 extern "C" {
 #endif
 
-#define BSDC_ABI_VERSION 3
+#define BSDC_ABI_VERSION 4
 #define BSDC_SMALL_BUCKETS 8 /* LDS arena size classes of the wavefront-per-family kernel */
 
 #define BSDC_EINVAL (-22)
@@ -79,7 +79,8 @@ typedef struct {
                                     n_rec | (image bytes / 32) << 8, image base (first slot) */
     int64_t n_small[BSDC_SMALL_BUCKETS];      /* families per bucket */
     int32_t small_arena[BSDC_SMALL_BUCKETS];  /* LDS bytes per wavefront of each bucket (multiple of 16) */
-    const uint32_t *large_fams;  /* families processed one workgroup each */
+    const uint32_t *large_fams;  /* families processed one workgroup each; 4 words per family:
+                                    family, first record, n_rec, image bytes (from the first slot) */
     int64_t n_large;
     int32_t large_arena;         /* bytes per workgroup for large families */
     int32_t max_len;             /* max record length */
@@ -134,7 +135,7 @@ int32_t bsdc_duplex_call(bsdc_ctx *ctx, const bsdc_family_batch *batch, bsdc_con
                          int32_t with_tools, void *stream);
 
 /* Arena bytes one family needs (host-side helpers shared with the batch builder):
- * workgroup kernel (slot_bytes = 2 x the family's slot span) and wavefront kernel (img = slot
+ * workgroup kernel (slot_bytes = 2 x the family's image bytes) and wavefront kernel (img = slot
  * span rounded to 32, n_conv = converted records, max_len = the batch's max record length). */
 int64_t bsdc_family_arena_bytes(int32_t n_rec, int64_t slot_bytes, int32_t max_len, int64_t complex_ops);
 int64_t bsdc_small_arena_bytes(int32_t n_rec, int64_t img, int32_t n_conv, int64_t complex_ops, int32_t max_len);
