@@ -1312,7 +1312,7 @@ __device__ __forceinline__ int block_max(int v, int *red) {
 }
 
 __device__ void process_large(const KParams &P, uint8_t *A, const int32_t *lr, const float *thr, uint4 ent, int *red,
-                              int *s_cnt, int *s_lc) {
+                              int *s_cnt, int *s_lc, int *s_cur) {
     constexpr int G = kLargeThreads;
     const int tt = threadIdx.x;
     const bsdc_family_batch &B = P.B;
@@ -1323,6 +1323,7 @@ __device__ void process_large(const KParams &P, uint8_t *A, const int32_t *lr, c
     const bool do_vote = P.mode & BSDC_MODE_VOTE;
     const uint4 *REC = reinterpret_cast<const uint4 *>(B.rec);
     const uint32_t off0 = n > 0 ? REC[r0].x : 0u;
+    const int stop = (P.mode >> BSDC_MODE_STOP_SHIFT) & 15;  // profiling ablation (0 = full kernel)
 
     int c = 0, ml = 0;
     for (int r = tt; r < n; r += G) {
@@ -1368,11 +1369,14 @@ __device__ void process_large(const KParams &P, uint8_t *A, const int32_t *lr, c
     __syncthreads();
 
     // ---- stage the image: every 16-byte chunk, quals as they are, packed bases unpacked ----
+    uint32_t qor = 0;  // OR of the family's quals: a byte >= 128 keeps the overlap off the SWAR path
     {
         const int nqc = (int)(img >> 4), nch = nqc + (int)(img >> 5);
         for (int k = tt; k < nch; k += G) {
             if (k < nqc) {
-                *reinterpret_cast<uint4 *>(qimg + 16 * k) = *reinterpret_cast<const uint4 *>(B.qual + off0 + 16 * (uint32_t)k);
+                const uint4 v = *reinterpret_cast<const uint4 *>(B.qual + off0 + 16 * (uint32_t)k);
+                *reinterpret_cast<uint4 *>(qimg + 16 * k) = v;
+                qor |= v.x | v.y | v.z | v.w;
             } else {
                 const uint4 v = *reinterpret_cast<const uint4 *>(B.seq + (off0 >> 1) + 16 * (uint32_t)(k - nqc));
                 unpack32<false>(v, slots + 32 * (k - nqc));
@@ -1380,6 +1384,7 @@ __device__ void process_large(const KParams &P, uint8_t *A, const int32_t *lr, c
         }
     }
     __syncthreads();
+    if (stop == 1) return;
 
     // ---- tool 1 (tools/1.convert_AG_to_CT.py:84-183): every converted record at once, 4 positions
     // per thread, flattened over (converted record, dword).  Each chunk of G dwords reads first and
@@ -1407,10 +1412,18 @@ __device__ void process_large(const KParams &P, uint8_t *A, const int32_t *lr, c
                     const int32_t avail = (int32_t)B.rec_win[2 * (size_t)m.gidx + 1];
                     uint32_t m4 = lds32(slots + m.slot + j4);
                     const uint32_t mn = lds32(slots + m.slot + j4 + 4);
+                    // nibbles win + j4 .. + 4 (high nibble first) from the 8 aligned bytes holding them
+                    const uint64_t x0 = (uint64_t)m.win + (uint64_t)j4;
+                    const uint64_t a4 = (x0 >> 1) & ~3ull;
+                    const uint32_t *rw = reinterpret_cast<const uint32_t *>(P.ref + a4);
+                    const uint64_t W = (uint64_t)rw[0] | ((uint64_t)rw[1] << 32);
+                    const int u0 = (int)(x0 - 2 * a4);
                     uint32_t f0 = 0, f1 = 0;
 #pragma unroll
                     for (int q = 0; q < 5; q++) {
-                        const uint32_t fb = j4 + q < avail ? nib(P.ref, (int64_t)m.win + j4 + q) : kN;
+                        const int u = u0 + q;
+                        const uint32_t nb = (uint32_t)(W >> (8 * (u >> 1) + ((u & 1) ? 0 : 4))) & 0xFu;
+                        const uint32_t fb = j4 + q < avail ? nb : kN;
                         if (q < 4) f0 |= fb << (8 * q);
                         if (q > 0) f1 |= fb << (8 * (q - 1));
                     }
@@ -1444,6 +1457,7 @@ __device__ void process_large(const KParams &P, uint8_t *A, const int32_t *lr, c
             if (M[r].link & BSDC_LINK_RD_IN) M[r].rd = 1;
         __syncthreads();
     }
+    if (stop == 2) return;
 
     // ---- gap extension ----
     if (do_extend) {
@@ -1500,33 +1514,66 @@ __device__ void process_large(const KParams &P, uint8_t *A, const int32_t *lr, c
             }
         }
     }
-    if (!do_vote) return;
+    if (!do_vote || stop == 3) return;
 
     auto cigv = [&](const RecMeta &m) {
         return make_cigview(B, m.gidx, m.link, do_convert && (m.link & BSDC_LINK_CONVERT), m.rd != 0, do_extend);
     };
 
     // ---- overlapping-bases consensus ----
+    // A thread per R1 record finds its template's overlap.  Templates with simple cigars (and a
+    // family without quals >= 128) run flattened over (template, 4 positions) through overlap4;
+    // the rest take the per-position path, one wave per template.  Templates share no bytes.
+    const bool wild = block_max((qor & 0x80808080u) != 0 ? 1 : 0, red) != 0;
     if (P.overlap) {
-        for (int r = 0; r < n; r++) {
+        uint32_t *tl = reinterpret_cast<uint32_t *>(lists);  // fast: 3 words each from the front; slow: 1 from the back
+        if (tt == 0) {
+            s_cnt[0] = 0;
+            s_cnt[1] = 0;
+        }
+        __syncthreads();
+        for (int r = tt; r < n; r += G) {
             const RecMeta a = M[r];
             const uint32_t mate = a.link & BSDC_LINK_MATE_MASK;
             if (mate == BSDC_LINK_MATE_MASK || !(a.link & BSDC_LINK_USABLE)) continue;
             const RecMeta b = M[mate];
             if (!(b.link & BSDC_LINK_USABLE) || (a.flag & 4) || (b.flag & 4)) continue;
             if (a.reflen <= 0 || b.reflen <= 0) continue;
-            const int32_t s = ::max(a.pos, b.pos);
-            const int32_t e = ::min(a.pos + a.reflen - 1, b.pos + b.reflen - 1);
-            if (s > e) continue;
+            const int32_t s0 = ::max(a.pos, b.pos);
+            const int32_t e0 = ::min(a.pos + a.reflen - 1, b.pos + b.reflen - 1);
+            if (s0 > e0) continue;
+            if (!wild && !((a.link | b.link) & BSDC_LINK_COMPLEX)) {
+                const int i = atomicAdd(&s_cnt[0], 1);
+                tl[3 * i] = a.slot + (uint32_t)a.start + (uint32_t)(s0 - a.pos);
+                tl[3 * i + 1] = b.slot + (uint32_t)b.start + (uint32_t)(s0 - b.pos);
+                tl[3 * i + 2] = (uint32_t)(e0 - s0 + 1);
+            } else {
+                tl[2 * n - 1 - atomicAdd(&s_cnt[1], 1)] = (uint32_t)r;
+            }
+        }
+        __syncthreads();
+        const int nfast = s_cnt[0], nslow = s_cnt[1];
+        const int SDo = (maxlen_f + 2 + 3) >> 2;  // dwords of the longest overlap
+        for (int k = tt; k < nfast * SDo; k += G) {
+            const int g = k / SDo, j = 4 * (k - g * SDo);
+            const int ovl = (int)tl[3 * g + 2];
+            if (j < ovl) overlap4(slots, qimg, tl[3 * g] + (uint32_t)j, tl[3 * g + 1] + (uint32_t)j, ovl - j);
+        }
+        for (int i = tt >> 6; i < nslow; i += G / kWave) {
+            const int r = (int)tl[2 * n - 1 - i];
+            const RecMeta a = M[r];
+            const RecMeta b = M[a.link & BSDC_LINK_MATE_MASK];
+            const int32_t s0 = ::max(a.pos, b.pos);
+            const int32_t e0 = ::min(a.pos + a.reflen - 1, b.pos + b.reflen - 1);
             const bool ca = a.link & BSDC_LINK_COMPLEX, cb = b.link & BSDC_LINK_COMPLEX;
             CigView va, vb;
             if (ca) va = cigv(a);
             if (cb) vb = cigv(b);
             uint8_t *ab = slots + a.slot + a.start;
-            uint8_t *aq = slots + a.slot + a.cap + a.start;
+            uint8_t *aq = qimg + a.slot + a.start;
             uint8_t *bb = slots + b.slot + b.start;
-            uint8_t *bq = slots + b.slot + b.cap + b.start;
-            for (int32_t p = s + tt; p <= e; p += G) {
+            uint8_t *bq = qimg + b.slot + b.start;
+            for (int32_t p = s0 + (tt & (kWave - 1)); p <= e0; p += kWave) {
                 const int ia = ca ? read_at_ref(va, a.pos, a.len, p) : (p - a.pos < a.len ? p - a.pos : -1);
                 const int ibb = cb ? read_at_ref(vb, b.pos, b.len, p) : (p - b.pos < b.len ? p - b.pos : -1);
                 if (ia < 0 || ibb < 0) continue;
@@ -1551,6 +1598,7 @@ __device__ void process_large(const KParams &P, uint8_t *A, const int32_t *lr, c
         }
         __syncthreads();
     }
+    if (stop == 4) return;
 
     // ---- source reads ----
     for (int r = tt; r < n; r += G) {
@@ -1576,105 +1624,182 @@ __device__ void process_large(const KParams &P, uint8_t *A, const int32_t *lr, c
         }
     }
     __syncthreads();
+    if (stop == 10) return;
 
     // ---- most-common-alignment filter ----
+    // Simplified cigars in parallel (each record's ops at an offset from a block scan of its op
+    // bound), then the two groups (X = AB-R1 + BA-R2, Y = AB-R2 + BA-R1) by one thread each.
     int hc = 0;
     for (int r = tt; r < n; r += G) hc |= (M[r].link & BSDC_LINK_COMPLEX) && M[r].set != 0xFF;
     if (block_max(hc, red)) {
-        if (tt == 0) {
-            uint32_t *so = simp;
-            uint32_t *sofs = simp + cops + 2 * n;
-            uint16_t *srcl = reinterpret_cast<uint16_t *>(simp + cops + 3 * n);  // n u16 in the last n words
-            uint8_t *setv = reinterpret_cast<uint8_t *>(srcl + n);               // ... and n bytes after them
-            uint32_t fill = 0;
-            for (int r = 0; r < n; r++) {
+        uint32_t *so = simp;
+        uint32_t *sofs = simp + cops + 2 * n;
+        uint16_t *srcl = reinterpret_cast<uint16_t *>(simp + cops + 3 * n);  // n u16 in the last n words
+        uint8_t *setv = reinterpret_cast<uint8_t *>(srcl + n);               // ... and n bytes after them
+        uint32_t run = 0;
+        for (int base = 0; base < n; base += G) {
+            const int r = base + tt;
+            uint32_t v = 0;
+            if (r < n) v = (M[r].link & BSDC_LINK_COMPLEX) ? (B.cig_info[M[r].gidx] & 0xFFFF) + 2u : 1u;  // ops bound
+            uint32_t incl = v;
+#pragma unroll
+            for (int o = 1; o < kWave; o <<= 1) {
+                const uint32_t y = (uint32_t)__shfl_up((int)incl, o, kWave);
+                if ((tt & (kWave - 1)) >= o) incl += y;
+            }
+            if ((tt & (kWave - 1)) == kWave - 1) red[tt >> 6] = (int)incl;
+            __syncthreads();
+            uint32_t woff = 0, ctot = 0;
+            for (int w = 0; w < G / kWave; w++) {
+                woff += w < (tt >> 6) ? (uint32_t)red[w] : 0u;
+                ctot += (uint32_t)red[w];
+            }
+            if (r < n) {
+                const RecMeta m = M[r];
+                const uint32_t off = run + woff + incl - v;
                 sofs[r] = 0;
-                srcl[r] = (uint16_t)M[r].srclen;
-                setv[r] = M[r].set;
-                if (M[r].set == 0xFF) continue;
-                const RecMeta &m = M[r];
-                const bool mc = m.link & BSDC_LINK_COMPLEX;
-                CigView v;
-                if (mc) v = cigv(m);
-                const int c2 = simplified_cigar(&v, mc, m.flag & 16, m.srclen, so + fill);
-                sofs[r] = fill | ((uint32_t)c2 << 16);
-                fill += (uint32_t)c2;
+                srcl[r] = (uint16_t)m.srclen;
+                setv[r] = m.set;
+                if (m.set != 0xFF) {
+                    const bool mc = m.link & BSDC_LINK_COMPLEX;
+                    CigView cv;
+                    if (mc) cv = cigv(m);
+                    const int c2 = simplified_cigar(&cv, mc, m.flag & 16, m.srclen, so + off);
+                    sofs[r] = off | ((uint32_t)c2 << 16);
+                }
             }
-            for (int xy = 0; xy < 2; xy++) {
-                const int s1 = xy == 0 ? 0 : 1, s2 = xy == 0 ? 3 : 2;
-                int cnt = 0;
-                for (int r = 0; r < n; r++)
-                    if (setv[r] == s1) lists[cnt++] = (uint16_t)r;
-                for (int r = 0; r < n; r++)
-                    if (setv[r] == s2) lists[cnt++] = (uint16_t)r;
-                filter_group(lists, cnt, srcl, sofs, so, setv);
-            }
-            for (int r = 0; r < n; r++) M[r].set = setv[r];
+            run += ctot;
+            __syncthreads();
         }
+        if ((tt & (kWave - 1)) == 0 && (tt >> 6) < 2) {
+            const int xy = tt >> 6;
+            const int s1 = xy == 0 ? 0 : 1, s2 = xy == 0 ? 3 : 2;
+            uint16_t *ord = lists + xy * n;
+            int c = 0;
+            for (int r = 0; r < n; r++)
+                if (setv[r] == s1) ord[c++] = (uint16_t)r;
+            for (int r = 0; r < n; r++)
+                if (setv[r] == s2) ord[c++] = (uint16_t)r;
+            filter_group(ord, c, srcl, sofs, so, setv);
+        }
+        __syncthreads();
+        for (int r = tt; r < n; r += G) M[r].set = setv[r];
         __syncthreads();
     }
 
-    // ---- lists and consensus lengths ----
-    if (tt == 0) {
-        int cnt[4] = {0, 0, 0, 0}, lcv[4] = {0, 0, 0, 0};
-        for (int r = 0; r < n; r++) {
-            const int s = M[r].set;
-            if (s == 0xFF) continue;
-            lists[s * n + cnt[s]++] = (uint16_t)r;
-            lcv[s] = ::max(lcv[s], M[r].srclen);
-        }
-        for (int s = 0; s < 4; s++) {
-            s_cnt[s] = cnt[s];
-            s_lc[s] = lcv[s];
-        }
+    // ---- read descriptors by set, consensus lengths ----
+    // desc[soff[s] + i] = {address of column 0, srclen | reverse << 31}; a reverse read's columns
+    // run backwards from its last base.  Order within a set is free: the vote sums are integers.
+    uint2 *desc = reinterpret_cast<uint2 *>(lists);
+    if (tt < 4) {
+        s_cnt[tt] = 0;
+        s_lc[tt] = 0;
+        s_cur[tt] = 0;
     }
     __syncthreads();
-    int cnt[4], lcv[4];
-    for (int s = 0; s < 4; s++) {
+    for (int r = tt; r < n; r += G) {
+        const RecMeta &m = M[r];
+        if (m.set == 0xFF) continue;
+        atomicAdd(&s_cnt[m.set], 1);
+        atomicMax(&s_lc[m.set], m.srclen);
+    }
+    __syncthreads();
+    int cnt[4], lcv[4], soff[4];
+    for (int s = 0, o = 0; s < 4; s++) {
         cnt[s] = s_cnt[s];
         lcv[s] = s_lc[s];
+        soff[s] = o;
+        o += cnt[s];
+    }
+    for (int r = tt; r < n; r += G) {
+        const RecMeta &m = M[r];
+        if (m.set == 0xFF) continue;
+        const bool negr = m.flag & 16;
+        const int i = atomicAdd(&s_cur[m.set], 1);
+        desc[soff[m.set] + i] = make_uint2(m.slot + (uint32_t)m.start + (negr ? (uint32_t)(m.len - 1) : 0u),
+                                           (uint32_t)m.srclen | (negr ? 0x80000000u : 0u));
     }
     __syncthreads();
+    if (stop == 5) return;
 
-    // ---- single-strand vote (int64 sums: sets can exceed 250 reads) ----
-    const int tot = lcv[0] + lcv[1] + lcv[2] + lcv[3];
-    for (int k = tt; k < tot; k += G) {
-        int s = 0, col = k;
-        while (col >= lcv[s]) {
-            col -= lcv[s];
+    // ---- single-strand vote ----
+    // A thread owns 4 consecutive columns of one set and walks its reads: one dword of bases and
+    // one of quals per read (a reverse read's dword is byte-swapped and complemented), columns past
+    // the read's end cleared, lr[q] added to the base's sum.  int32 sums are flushed to int64 every
+    // 128 reads (|lr| < 2^24; sets can exceed 250 reads).
+    int nt4[4];
+    for (int s = 0; s < 4; s++) nt4[s] = (lcv[s] + 3) >> 2;
+    const int ntask = nt4[0] + nt4[1] + nt4[2] + nt4[3];
+    for (int k = tt; k < ntask; k += G) {
+        int s = 0, c = k;
+        while (c >= nt4[s]) {
+            c -= nt4[s];
             s++;
         }
-        long long D0 = 0, D1 = 0, D2 = 0, D3 = 0;
-        const uint16_t *lst = lists + s * n;
-        for (int i = 0; i < cnt[s]; i++) {
-            const RecMeta &m = M[lst[i]];
-            if (col >= m.srclen) continue;
-            const bool negr = m.flag & 16;
-            const int j = negr ? m.len - 1 - col : col;
-            uint32_t b = slots[m.slot + m.start + j];
-            const uint32_t q = slots[m.slot + m.cap + m.start + j];
-            if (negr) b = comp_nt16(b);
-            const long long v = lr[q];
-            D0 += b == kA ? v : 0;
-            D1 += b == kC ? v : 0;
-            D2 += b == kG ? v : 0;
-            D3 += b == kT ? v : 0;
+        c *= 4;
+        long long D[4][4];
+#pragma unroll
+        for (int j = 0; j < 4; j++)
+#pragma unroll
+            for (int x = 0; x < 4; x++) D[j][x] = 0;
+        const uint2 *dl = desc + soff[s];
+        for (int i0 = 0; i0 < cnt[s]; i0 += 128) {
+            int32_t d[4][4];
+#pragma unroll
+            for (int j = 0; j < 4; j++)
+#pragma unroll
+                for (int x = 0; x < 4; x++) d[j][x] = 0;
+            const int i1 = ::min(cnt[s], i0 + 128);
+            for (int i = i0; i < i1; i++) {
+                const uint2 e = dl[i];
+                const int k8 = 8 * ((int)(e.y & 0x7FFFFFFFu) - c);
+                if (k8 <= 0) continue;
+                uint32_t b, q;
+                if (e.y >> 31) {
+                    // may start up to 3 bytes before the image (arena bytes, cleared): signed offset
+                    const int32_t ad = (int32_t)e.x - c - 3;
+                    b = comp4(__builtin_bswap32(ldsu32(slots + ad) & ~bytes_past(k8, true)));
+                    q = __builtin_bswap32(ldsu32(qimg + ad));
+                } else {
+                    b = ldsu32(slots + e.x + (uint32_t)c) & ~bytes_past(k8, false) & 0x0F0F0F0Fu;
+                    q = ldsu32(qimg + e.x + (uint32_t)c);
+                }
+#pragma unroll
+                for (int j = 0; j < 4; j++) {
+                    const uint32_t bj = (b >> (8 * j)) & 0xFu;
+                    const int32_t v = lr[(q >> (8 * j)) & 0xFFu];
+                    d[j][0] += bj == kA ? v : 0;
+                    d[j][1] += bj == kC ? v : 0;
+                    d[j][2] += bj == kG ? v : 0;
+                    d[j][3] += bj == kT ? v : 0;
+                }
+            }
+#pragma unroll
+            for (int j = 0; j < 4; j++)
+#pragma unroll
+                for (int x = 0; x < 4; x++) D[j][x] += d[j][x];
         }
-        int best = 0;
-        long long Db = D0;
-        if (D1 > Db) { best = 1; Db = D1; }
-        if (D2 > Db) { best = 2; Db = D2; }
-        if (D3 > Db) { best = 3; Db = D3; }
-        float S = 0.0f;
-        if (best != 0) S += term(D0 - Db);
-        if (best != 1) S += term(D1 - Db);
-        if (best != 2) S += term(D2 - Db);
-        if (best != 3) S += term(D3 - Db);
-        const int Q = phred_of(S, thr);
-        ssb[s * ssw + col] = Q < 2 ? (uint8_t)kN : (uint8_t)(1u << best);
-        ssq[s * ssw + col] = Q < 2 ? (uint8_t)2 : (uint8_t)Q;
+#pragma unroll
+        for (int j = 0; j < 4; j++) {
+            const int col = c + j;
+            if (col >= lcv[s]) break;
+            int best = 0;
+            long long Db = D[j][0];
+            if (D[j][1] > Db) { best = 1; Db = D[j][1]; }
+            if (D[j][2] > Db) { best = 2; Db = D[j][2]; }
+            if (D[j][3] > Db) { best = 3; Db = D[j][3]; }
+            float S = 0.0f;
+            if (best != 0) S += term(D[j][0] - Db);
+            if (best != 1) S += term(D[j][1] - Db);
+            if (best != 2) S += term(D[j][2] - Db);
+            if (best != 3) S += term(D[j][3] - Db);
+            const int Q = phred_of(S, thr);
+            ssb[s * ssw + col] = Q < 2 ? (uint8_t)kN : (uint8_t)(1u << best);
+            ssq[s * ssw + col] = Q < 2 ? (uint8_t)2 : (uint8_t)Q;
+        }
     }
     __syncthreads();
+    if (stop == 7) return;
 
     // ---- duplex combine and output ----
     bool hs[4];
@@ -1726,15 +1851,17 @@ __global__ __launch_bounds__(kLargeThreads) void k_large(KParams P) {
     extern __shared__ __attribute__((aligned(16))) uint8_t smem[];  // the family's arena (IN_LDS)
     __shared__ __attribute__((aligned(16))) Tables s_tab;
     __shared__ int red[kLargeThreads / kWave];
-    __shared__ int s_cnt[4], s_lc[4];
+    __shared__ int s_cnt[4], s_lc[4], s_cur[4];
     const Tables *T = &s_tab;
+    if (((P.mode >> BSDC_MODE_STOP_SHIFT) & 15) == 15) return;  // profiling: launch cost alone
     load_tables(P.tab, reinterpret_cast<uint8_t *>(&s_tab));
+    if (((P.mode >> BSDC_MODE_STOP_SHIFT) & 15) == 14) return;  // profiling: + the table copy
     const int32_t *lr = T->lr;
     const float *thr = T->thr;
     const int64_t i = blockIdx.x;
     if (i >= P.B.n_large) return;
     uint8_t *A = IN_LDS ? smem : P.O.scratch + (size_t)i * (size_t)P.B.large_arena;
-    process_large(P, A, lr, thr, reinterpret_cast<const uint4 *>(P.B.large_fams)[i], red, s_cnt, s_lc);
+    process_large(P, A, lr, thr, reinterpret_cast<const uint4 *>(P.B.large_fams)[i], red, s_cnt, s_lc, s_cur);
 }
 
 }  // namespace

@@ -64,7 +64,8 @@ class DeviceBatch:
         nl = int(fb.large_fams.shape[0])
         self.scratch = None
         if nl and fb.large_arena > lds_cap:
-            self.scratch = torch.zeros(nl * fb.large_arena, dtype=torch.uint8, device=device)
+            # + slack: dword reads may run a few bytes past the last arena (their bytes are masked)
+            self.scratch = torch.zeros(nl * fb.large_arena + 256, dtype=torch.uint8, device=device)
         self._b = _lib.FamilyBatchC()
         b = self._b
         b.n_rec, b.n_fam = Rn, F

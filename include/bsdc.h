@@ -100,7 +100,7 @@ typedef struct {
     uint8_t *dump_tags;          /* [n_rec] bit0 RD=1, bit1 LA present, bit2 prepended M, bit3 appended M */
     uint8_t *dump_seq;           /* [slot start + j] one nt16 code per byte */
     uint8_t *dump_qual;
-    uint8_t *scratch;            /* large-family arenas when large_arena exceeds LDS: n_large * large_arena bytes */
+    uint8_t *scratch;            /* large-family arenas when large_arena exceeds LDS: n_large * large_arena + 256 bytes */
 } bsdc_consensus;
 
 #define BSDC_MODE_CONVERT 1
