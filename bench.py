@@ -180,7 +180,7 @@ def main():
     if rank == 0:
         line = {
             "metric": METRIC,
-            "value": round(fams_total / elapsed, 1),
+            "value": round(fams_total * args.steps / elapsed, 1),  # every step processes every family
             "unit": "families/s",
             "n_gpus": world,
             "steps": args.steps,

@@ -8,8 +8,9 @@ HERE = os.path.dirname(os.path.abspath(__file__))
 # BSDC_LIB_PATH: an alternative build of the same library (profiling A/B runs only)
 LIB_PATH = os.environ.get("BSDC_LIB_PATH") or os.path.join(HERE, "libbsdc.so")
 
-BSDC_ABI_VERSION = 4
+BSDC_ABI_VERSION = 5
 SMALL_BUCKETS = 8  # BSDC_SMALL_BUCKETS
+LARGE_BUCKETS = 6  # BSDC_LARGE_BUCKETS
 MODE_CONVERT, MODE_EXTEND, MODE_VOTE, MODE_DUMP = 1, 2, 4, 8
 MODE_SKIP_SMALL, MODE_SKIP_LARGE = 16, 32
 
@@ -26,7 +27,7 @@ class FamilyBatchC(C.Structure):
                 ("cig_off", C.c_void_p), ("cig_info", C.c_void_p), ("cigar", C.c_void_p),
                 ("rt", C.c_void_p), ("seq", C.c_void_p), ("qual", C.c_void_p),
                 ("small_fams", C.c_void_p), ("n_small", C.c_int64 * SMALL_BUCKETS), ("small_arena", C.c_int32 * SMALL_BUCKETS),
-                ("large_fams", C.c_void_p), ("n_large", C.c_int64), ("large_arena", C.c_int32),
+                ("large_fams", C.c_void_p), ("n_large", C.c_int64 * LARGE_BUCKETS), ("large_arena", C.c_int32 * LARGE_BUCKETS),
                 ("max_len", C.c_int32)]
 
 

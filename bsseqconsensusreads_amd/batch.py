@@ -41,7 +41,12 @@ MODE_CONVERT, MODE_EXTEND, MODE_VOTE, MODE_DUMP = 1, 2, 4, 8
 SMALL_BUCKETS = (3072, 4096, 5120, 6144, 8192, 12288, 16384, 24576)  # BSDC_SMALL_BUCKETS classes
 SMALL_ARENA_CAP = 24576
 LDS_TABLES = 1024 + 1024 + 384 + 2048 + 192  # kTabBytes (csrc/bsdc_kernels.hip)
-LARGE_LDS_CAP = 64 * 1024 - LDS_TABLES
+# large families run one per 256-thread workgroup, in buckets of these LDS arena sizes; the last
+# bucket (anything larger) keeps its arenas in HBM scratch
+LARGE_LDS_MAX = 158912  # BSDC_LARGE_LDS_MAX: 160 KB - the tables - the kernel's other LDS
+# the largest arena that still fits k = 5, 4, 3, 2, 1 workgroups per CU (5 is the VGPR limit)
+LARGE_BUCKETS = tuple((160 * 1024 // k - LDS_TABLES - 256) // 16 * 16 for k in (5, 4, 3, 2, 1))  # + 1 scratch bucket
+assert LARGE_BUCKETS[-1] == LARGE_LDS_MAX
 
 
 def round16(x):
@@ -101,10 +106,10 @@ class FamilyBatch:
     qual: np.ndarray         # u8, slot layout
     small_buckets: List[np.ndarray]  # 4 lists of family ids (u32), one per LDS arena size
     small_arenas: List[int]
-    large_fams: np.ndarray   # u32 [n_large, 4] family, first record, n_rec, image bytes
+    large_buckets: List[np.ndarray]  # BSDC_LARGE_BUCKETS lists of entries u32 [n, 4]: family, first record, n_rec, image bytes
+    large_arenas: List[int]
     fam_entry: np.ndarray    # u32 [F, 4] small-kernel list entry of each family
     max_len: int
-    large_arena: int
     # ---- host bookkeeping ----
     src: np.ndarray          # i64 [R] input record index
     fam_mi: np.ndarray       # i32 [F] MI id of each family
@@ -126,6 +131,11 @@ class FamilyBatch:
     @property
     def small_fams(self) -> np.ndarray:
         return np.concatenate(self.small_buckets).astype(np.uint32)
+
+    @property
+    def large_fams(self) -> np.ndarray:
+        """u32 [n_large, 4] list entries of every large bucket, in order."""
+        return np.concatenate(self.large_buckets).astype(np.uint32).reshape(-1, 4)
 
     def device_arrays(self):
         rec = np.stack([self.rec_off, self.rec_pos.view(np.uint32), self.rec_lenflag, self.rec_link], axis=1)
@@ -497,15 +507,20 @@ def build_family_batch(raw: R.RawRecords, mode: str = "full", ref: Optional[R.Re
     while len(buckets) < len(SMALL_BUCKETS):
         buckets.append(np.zeros(0, np.uint32))
         arenas.append(16)
-    lf = np.nonzero(~small)[0]
     # large-family list entries: family, first record, n, image bytes (the image starts at the first slot)
-    large_fams = np.zeros((lf.shape[0], 4), np.int64)
-    large_fams[:, 0] = lf
-    large_fams[:, 1] = fam_off[lf]
-    large_fams[:, 2] = fam_sizes[lf]
-    large_fams[:, 3] = img[lf]
-    large_fams = large_fams.astype(np.uint32)
-    large_arena = int(round16(need_l[~small].max())) if (~small).any() else 16
+    lbuckets, larenas = [], []
+    lo = -1
+    for cap in LARGE_BUCKETS + (None,):
+        sel = ~small & (need_l > lo) if cap is None else ~small & (need_l > lo) & (need_l <= cap)
+        lf = np.nonzero(sel)[0]
+        e = np.zeros((lf.shape[0], 4), np.int64)
+        e[:, 0] = lf
+        e[:, 1] = fam_off[lf]
+        e[:, 2] = fam_sizes[lf]
+        e[:, 3] = img[lf]
+        lbuckets.append(e.astype(np.uint32))
+        larenas.append(int(cap) if cap is not None else (int(round16(need_l[lf].max())) if lf.shape[0] else 16))
+        lo = cap if cap is not None else lo
 
     # small-family list entries: family, first record, n | (image / 32) << 8, image base
     ent = np.zeros((nf, 4), np.int64)
@@ -521,6 +536,6 @@ def build_family_batch(raw: R.RawRecords, mode: str = "full", ref: Optional[R.Re
         cig_off=cig_off.astype(np.uint32), cig_info=cig_info,
         cigar=cigar_c if cigar_c.shape[0] else np.zeros(1, np.uint32),
         rt=rt.reshape(-1).astype(np.int32), seq=seq, qual=qual,
-        small_buckets=buckets, small_arenas=arenas, large_fams=large_fams, max_len=max_len,
-        large_arena=large_arena, src=order.astype(np.int64), fam_mi=fam_mi.astype(np.int32),
+        small_buckets=buckets, small_arenas=arenas, large_buckets=lbuckets, large_arenas=larenas,
+        max_len=max_len, src=order.astype(np.int64), fam_mi=fam_mi.astype(np.int32),
         n_bases=total, n_slots=n_slots)

@@ -470,9 +470,14 @@ __device__ __forceinline__ uint32_t expand80(uint32_t m80);
 // (agree: both quals min(qa + qb, 93); disagree: the higher quality's base on both, quals
 // |qa - qb|; equal quals: N / 2; an N on either side: untouched).  Base bytes carry the 0x10
 // A/C/G/T flag (N = 0x0F has none); quals must be < 128 (the caller checks).
-__device__ __forceinline__ void overlap4(uint8_t *bimg, uint8_t *qimg, uint32_t ia, uint32_t ib, int rem) {
-    const uint32_t X = ldsu32(bimg + ia), Y = ldsu32(bimg + ib);
-    const uint32_t QA = ldsu32(qimg + ia), QB = ldsu32(qimg + ib);
+struct Ovl4 {
+    uint32_t x, y, qa, qb;  // mate a's / b's 4 bases, 4 quals
+};
+__device__ __forceinline__ Ovl4 ovl4_load(const uint8_t *bimg, const uint8_t *qimg, uint32_t ia, uint32_t ib) {
+    return Ovl4{ldsu32(bimg + ia), ldsu32(bimg + ib), ldsu32(qimg + ia), ldsu32(qimg + ib)};
+}
+__device__ __forceinline__ Ovl4 ovl4_compute(const Ovl4 &in4, int rem) {
+    const uint32_t X = in4.x, Y = in4.y, QA = in4.qa, QB = in4.qb;
     const uint32_t in = rem >= 4 ? 0xFFFFFFFFu : (1u << (8 * rem)) - 1u;
     const uint32_t act = expand80(~(zero80(X ^ 0x0F0F0F0Fu) | zero80(Y ^ 0x0F0F0F0Fu)) & 0x80808080u) & in;
     const uint32_t eq = expand80(zero80(X ^ Y));
@@ -488,19 +493,25 @@ __device__ __forceinline__ void overlap4(uint8_t *bimg, uint8_t *qimg, uint32_t 
     const uint32_t nx = (X & eq) | (v & ~eq), ny = (Y & eq) | (v & ~eq);
     const uint32_t ox = (nx & act) | (X & ~act), oy = (ny & act) | (Y & ~act);
     const uint32_t oqa = (nq & act) | (QA & ~act), oqb = (nq & act) | (QB & ~act);
+    return Ovl4{ox, oy, oqa, oqb};
+}
+__device__ __forceinline__ void ovl4_store(uint8_t *bimg, uint8_t *qimg, uint32_t ia, uint32_t ib, int rem, const Ovl4 &o) {
     if (rem >= 4) {
-        stu32(bimg + ia, ox);
-        stu32(bimg + ib, oy);
-        stu32(qimg + ia, oqa);
-        stu32(qimg + ib, oqb);
+        stu32(bimg + ia, o.x);
+        stu32(bimg + ib, o.y);
+        stu32(qimg + ia, o.qa);
+        stu32(qimg + ib, o.qb);
     } else {  // the bytes past the overlap may belong to another template's read: byte stores
         for (int k = 0; k < rem; k++) {
-            bimg[ia + k] = (uint8_t)(ox >> (8 * k));
-            bimg[ib + k] = (uint8_t)(oy >> (8 * k));
-            qimg[ia + k] = (uint8_t)(oqa >> (8 * k));
-            qimg[ib + k] = (uint8_t)(oqb >> (8 * k));
+            bimg[ia + k] = (uint8_t)(o.x >> (8 * k));
+            bimg[ib + k] = (uint8_t)(o.y >> (8 * k));
+            qimg[ia + k] = (uint8_t)(o.qa >> (8 * k));
+            qimg[ib + k] = (uint8_t)(o.qb >> (8 * k));
         }
     }
+}
+__device__ __forceinline__ void overlap4(uint8_t *bimg, uint8_t *qimg, uint32_t ia, uint32_t ib, int rem) {
+    ovl4_store(bimg, qimg, ia, ib, rem, ovl4_compute(ovl4_load(bimg, qimg, ia, ib), rem));
 }
 // D0..D3 += lr2[v_j][q_j] for the 4 bytes of b (base bytes, kValid flag = v) and q (quals).  The
 // index (v << 8 | q) * 4 is built two columns at a time: v_perm interleaves [q_j, v_j] into 16-bit
@@ -1371,15 +1382,29 @@ __device__ void process_large(const KParams &P, uint8_t *A, const int32_t *lr, c
     // ---- stage the image: every 16-byte chunk, quals as they are, packed bases unpacked ----
     uint32_t qor = 0;  // OR of the family's quals: a byte >= 128 keeps the overlap off the SWAR path
     {
+        // 16-B chunks: [0, nqc) quals, [nqc, nch) packed bases; kStageU loads per thread in flight
+        constexpr int kStageU = 4;
         const int nqc = (int)(img >> 4), nch = nqc + (int)(img >> 5);
-        for (int k = tt; k < nch; k += G) {
-            if (k < nqc) {
-                const uint4 v = *reinterpret_cast<const uint4 *>(B.qual + off0 + 16 * (uint32_t)k);
-                *reinterpret_cast<uint4 *>(qimg + 16 * k) = v;
-                qor |= v.x | v.y | v.z | v.w;
-            } else {
-                const uint4 v = *reinterpret_cast<const uint4 *>(B.seq + (off0 >> 1) + 16 * (uint32_t)(k - nqc));
-                unpack32<false>(v, slots + 32 * (k - nqc));
+        for (int k0 = tt; k0 < nch; k0 += kStageU * G) {
+            uint4 v[kStageU];
+#pragma unroll
+            for (int u = 0; u < kStageU; u++) {
+                const int k = k0 + u * G;
+                if (k < nch) {
+                    const uint8_t *src = k < nqc ? B.qual + off0 + 16 * (uint32_t)k
+                                                 : B.seq + (off0 >> 1) + 16 * (uint32_t)(k - nqc);
+                    v[u] = *reinterpret_cast<const uint4 *>(src);
+                }
+            }
+#pragma unroll
+            for (int u = 0; u < kStageU; u++) {
+                const int k = k0 + u * G;
+                if (k < nqc) {
+                    *reinterpret_cast<uint4 *>(qimg + 16 * k) = v[u];
+                    qor |= v[u].x | v[u].y | v[u].z | v[u].w;
+                } else if (k < nch) {
+                    unpack32<false>(v[u], slots + 32 * (k - nqc));
+                }
             }
         }
     }
@@ -1399,56 +1424,73 @@ __device__ void process_large(const KParams &P, uint8_t *A, const int32_t *lr, c
         const int nc = s_cnt[0];
         const int SD = (maxlen_f + 1 + 3) >> 2;  // dwords per converted record, at most
         const int total = nc * SD;
-        for (int base = 0; base < total; base += G) {
-            const int k = base + tt;
-            uint32_t out = 0, wa = 0;
-            bool wr = false;
-            if (k < total) {
-                const int ci = k / SD, j4 = 4 * (k - ci * SD);
-                const int r = clist[ci];
-                const RecMeta m = M[r];
-                const int32_t Lm = m.in_len + 1;
-                if (j4 < Lm) {
-                    const int32_t avail = (int32_t)B.rec_win[2 * (size_t)m.gidx + 1];
-                    uint32_t m4 = lds32(slots + m.slot + j4);
-                    const uint32_t mn = lds32(slots + m.slot + j4 + 4);
-                    // nibbles win + j4 .. + 4 (high nibble first) from the 8 aligned bytes holding them
-                    const uint64_t x0 = (uint64_t)m.win + (uint64_t)j4;
-                    const uint64_t a4 = (x0 >> 1) & ~3ull;
-                    const uint32_t *rw = reinterpret_cast<const uint32_t *>(P.ref + a4);
-                    const uint64_t W = (uint64_t)rw[0] | ((uint64_t)rw[1] << 32);
-                    const int u0 = (int)(x0 - 2 * a4);
-                    uint32_t f0 = 0, f1 = 0;
+        constexpr int kConvU = 4;  // tasks per thread per round: their global loads go out together
+        for (int base = 0; base < total; base += kConvU * G) {
+            int rr[kConvU], jj[kConvU], av[kConvU];
+            uint32_t w0[kConvU], w1[kConvU];
 #pragma unroll
-                    for (int q = 0; q < 5; q++) {
-                        const int u = u0 + q;
-                        const uint32_t nb = (uint32_t)(W >> (8 * (u >> 1) + ((u & 1) ? 0 : 4))) & 0xFu;
-                        const uint32_t fb = j4 + q < avail ? nb : kN;
-                        if (q < 4) f0 |= fb << (8 * q);
-                        if (q > 0) f1 |= fb << (8 * (q - 1));
-                    }
-                    if (j4 == 0) m4 = (m4 & ~0xFFu) | (f0 & 0xFFu);  // :121 seed, m[0] = ref[0]
-                    const uint32_t m1 = alignbyte(mn, m4, 1);
-                    uint32_t nxt = 0x80808080u;
-                    const int last = Lm - 1 - j4;  // the record's last position has no next base
-                    if (last < 4) nxt &= ~(0xFFu << (8 * last));
-                    out = convert4f<false>(m4, m1, f0, f1, nxt);
-                    wa = m.slot + (uint32_t)j4;
-                    wr = true;
-                    if (j4 == 0) qimg[m.slot] = 40;  // :174-177 'I' + quals
-                    if (last < 4) {  // :157-170 a final C before a reference G is trimmed
-                        const uint8_t rdv = (((out >> (8 * last)) & 0xFF) == kC && ((f1 >> (8 * last)) & 0xFF) == kG) ? 1 : 0;
-                        RecMeta &w = M[r];
-                        w.rd = rdv;
-                        w.len = Lm - rdv;
-                        w.start = 0;
-                        w.pos = m.pos - 1 > 0 ? m.pos - 1 : 0;
-                        w.reflen = m.reflen + 1 - ((rdv && m.reflen > 0) ? 1 : 0);
+            for (int u = 0; u < kConvU; u++) {
+                const int k = base + u * G + tt;
+                rr[u] = -1;
+                jj[u] = 0;
+                if (k < total) {
+                    const int ci = k / SD, j4 = 4 * (k - ci * SD);
+                    const int r = clist[ci];
+                    if (j4 < M[r].in_len + 1) {
+                        rr[u] = r;
+                        jj[u] = j4;
+                        // nibbles win + j4 .. + 4 (high nibble first) lie in the 8 aligned bytes at a4
+                        const uint64_t x0 = (uint64_t)M[r].win + (uint64_t)j4;
+                        const uint32_t *rw = reinterpret_cast<const uint32_t *>(P.ref + ((x0 >> 1) & ~3ull));
+                        w0[u] = rw[0];
+                        w1[u] = rw[1];
+                        av[u] = (int32_t)B.rec_win[2 * (size_t)M[r].gidx + 1];
                     }
                 }
             }
+            uint32_t out[kConvU], wa[kConvU];
+#pragma unroll
+            for (int u = 0; u < kConvU; u++) {
+                if (rr[u] < 0) continue;
+                const int r = rr[u], j4 = jj[u];
+                const RecMeta m = M[r];
+                const int32_t Lm = m.in_len + 1;
+                uint32_t m4 = lds32(slots + m.slot + j4);
+                const uint32_t mn = lds32(slots + m.slot + j4 + 4);
+                const uint64_t x0 = (uint64_t)m.win + (uint64_t)j4;
+                const uint64_t W = (uint64_t)w0[u] | ((uint64_t)w1[u] << 32);
+                const int u0 = (int)(x0 - 2 * ((x0 >> 1) & ~3ull));
+                uint32_t f0 = 0, f1 = 0;
+#pragma unroll
+                for (int q = 0; q < 5; q++) {
+                    const int x = u0 + q;
+                    const uint32_t nb = (uint32_t)(W >> (8 * (x >> 1) + ((x & 1) ? 0 : 4))) & 0xFu;
+                    const uint32_t fb = j4 + q < av[u] ? nb : kN;
+                    if (q < 4) f0 |= fb << (8 * q);
+                    if (q > 0) f1 |= fb << (8 * (q - 1));
+                }
+                if (j4 == 0) m4 = (m4 & ~0xFFu) | (f0 & 0xFFu);  // :121 seed, m[0] = ref[0]
+                const uint32_t m1 = alignbyte(mn, m4, 1);
+                uint32_t nxt = 0x80808080u;
+                const int last = Lm - 1 - j4;  // the record's last position has no next base
+                if (last < 4) nxt &= ~(0xFFu << (8 * last));
+                out[u] = convert4f<false>(m4, m1, f0, f1, nxt);
+                wa[u] = m.slot + (uint32_t)j4;
+                if (j4 == 0) qimg[m.slot] = 40;  // :174-177 'I' + quals
+                if (last < 4) {  // :157-170 a final C before a reference G is trimmed
+                    const uint8_t rdv = (((out[u] >> (8 * last)) & 0xFF) == kC && ((f1 >> (8 * last)) & 0xFF) == kG) ? 1 : 0;
+                    RecMeta &w = M[r];
+                    w.rd = rdv;
+                    w.len = Lm - rdv;
+                    w.start = 0;
+                    w.pos = m.pos - 1 > 0 ? m.pos - 1 : 0;
+                    w.reflen = m.reflen + 1 - ((rdv && m.reflen > 0) ? 1 : 0);
+                }
+            }
             __syncthreads();
-            if (wr) st32(slots + wa, out);
+#pragma unroll
+            for (int u = 0; u < kConvU; u++)
+                if (rr[u] >= 0) st32(slots + wa[u], out[u]);
             __syncthreads();
         }
     }
@@ -1554,10 +1596,28 @@ __device__ void process_large(const KParams &P, uint8_t *A, const int32_t *lr, c
         __syncthreads();
         const int nfast = s_cnt[0], nslow = s_cnt[1];
         const int SDo = (maxlen_f + 2 + 3) >> 2;  // dwords of the longest overlap
-        for (int k = tt; k < nfast * SDo; k += G) {
-            const int g = k / SDo, j = 4 * (k - g * SDo);
-            const int ovl = (int)tl[3 * g + 2];
-            if (j < ovl) overlap4(slots, qimg, tl[3 * g] + (uint32_t)j, tl[3 * g + 1] + (uint32_t)j, ovl - j);
+        for (int k0 = tt; k0 < nfast * SDo; k0 += 2 * G) {
+            uint32_t ia[2], ib[2];
+            int rem[2];
+#pragma unroll
+            for (int u = 0; u < 2; u++) {
+                const int k = k0 + u * G;
+                rem[u] = 0;
+                ia[u] = ib[u] = 0;
+                if (k < nfast * SDo) {
+                    const int g = k / SDo, j = 4 * (k - g * SDo);
+                    rem[u] = (int)tl[3 * g + 2] - j;
+                    ia[u] = tl[3 * g] + (uint32_t)j;
+                    ib[u] = tl[3 * g + 1] + (uint32_t)j;
+                }
+            }
+            Ovl4 o[2];
+#pragma unroll
+            for (int u = 0; u < 2; u++)
+                if (rem[u] > 0) o[u] = ovl4_load(slots, qimg, ia[u], ib[u]);
+#pragma unroll
+            for (int u = 0; u < 2; u++)
+                if (rem[u] > 0) ovl4_store(slots, qimg, ia[u], ib[u], rem[u], ovl4_compute(o[u], rem[u]));
         }
         for (int i = tt >> 6; i < nslow; i += G / kWave) {
             const int r = (int)tl[2 * n - 1 - i];
@@ -1723,12 +1783,54 @@ __device__ void process_large(const KParams &P, uint8_t *A, const int32_t *lr, c
     if (stop == 5) return;
 
     // ---- single-strand vote ----
-    // A thread owns 4 consecutive columns of one set and walks its reads: one dword of bases and
-    // one of quals per read (a reverse read's dword is byte-swapped and complemented), columns past
-    // the read's end cleared, lr[q] added to the base's sum.  int32 sums are flushed to int64 every
-    // 128 reads (|lr| < 2^24; sets can exceed 250 reads).
-    int nt4[4];
-    for (int s = 0; s < 4; s++) nt4[s] = (lcv[s] + 3) >> 2;
+    // A thread owns consecutive columns of one set and walks its reads: one dword of bases and
+    // one of quals per read (a reverse read's dword byte-swapped and complemented), columns past
+    // the read's end cleared, lr[q] added to the base's sum.  Sets of <= 128 reads: 4 columns per
+    // thread, int32 sums (exact: |lr| < 2^24).  Deeper sets: 2 columns per thread, int32 sums
+    // flushed to int64 every 128 reads.
+    auto resolve = [&](int s, int col, long long D0, long long D1, long long D2, long long D3) {
+        int best = 0;
+        long long Db = D0;
+        if (D1 > Db) { best = 1; Db = D1; }
+        if (D2 > Db) { best = 2; Db = D2; }
+        if (D3 > Db) { best = 3; Db = D3; }
+        float S = 0.0f;
+        if (best != 0) S += term(D0 - Db);
+        if (best != 1) S += term(D1 - Db);
+        if (best != 2) S += term(D2 - Db);
+        if (best != 3) S += term(D3 - Db);
+        const int Q = phred_of(S, thr);
+        ssb[s * ssw + col] = Q < 2 ? (uint8_t)kN : (uint8_t)(1u << best);
+        ssq[s * ssw + col] = Q < 2 ? (uint8_t)2 : (uint8_t)Q;
+    };
+    // one read's dword for columns c..c+3: its address and the mask of the columns it covers.  A
+    // read that ends before column c reads its first dword, all masked; a reverse read's dword may
+    // start up to 3 bytes before the image (arena bytes): signed offsets.
+    auto addr = [&](uint2 e, int c, uint32_t &keep) -> int32_t {
+        const int k8 = 8 * ((int)(e.y & 0x7FFFFFFFu) - c);
+        const bool rv = e.y >> 31;
+        keep = ~bytes_past(k8, rv);
+        const int cc = k8 > 0 ? c : 0;
+        return rv ? (int32_t)e.x - cc - 3 : (int32_t)e.x + cc;
+    };
+    auto fetch = [&](uint2 e, int c, uint32_t &b, uint32_t &q) {  // columns ascend, reverse complemented
+        uint32_t keep;
+        const int32_t a = addr(e, c, keep);
+        b = ldsu32(slots + a) & keep;
+        q = ldsu32(qimg + a);
+        if (e.y >> 31) {
+            b = comp4(__builtin_bswap32(b));
+            q = __builtin_bswap32(q);
+        } else {
+            b &= 0x0F0F0F0Fu;
+        }
+    };
+    constexpr int kSwarReads = 128;
+    int nt4[4], nt2[4];
+    for (int s = 0; s < 4; s++) {
+        nt4[s] = cnt[s] <= kSwarReads ? (lcv[s] + 3) >> 2 : 0;
+        nt2[s] = cnt[s] <= kSwarReads ? 0 : (lcv[s] + 1) >> 1;
+    }
     const int ntask = nt4[0] + nt4[1] + nt4[2] + nt4[3];
     for (int k = tt; k < ntask; k += G) {
         int s = 0, c = k;
@@ -1737,35 +1839,59 @@ __device__ void process_large(const KParams &P, uint8_t *A, const int32_t *lr, c
             s++;
         }
         c *= 4;
-        long long D[4][4];
+        int32_t d[4][4];
 #pragma unroll
         for (int j = 0; j < 4; j++)
 #pragma unroll
-            for (int x = 0; x < 4; x++) D[j][x] = 0;
+            for (int x = 0; x < 4; x++) d[j][x] = 0;
+        auto acc = [&](uint32_t b, uint32_t q) {
+#pragma unroll
+            for (int j = 0; j < 4; j++) {
+                const uint32_t bj = (b >> (8 * j)) & 0xFu;
+                const int32_t v = lr[(q >> (8 * j)) & 0xFFu];
+                d[j][0] += bj == kA ? v : 0;
+                d[j][1] += bj == kC ? v : 0;
+                d[j][2] += bj == kG ? v : 0;
+                d[j][3] += bj == kT ? v : 0;
+            }
+        };
         const uint2 *dl = desc + soff[s];
-        for (int i0 = 0; i0 < cnt[s]; i0 += 128) {
-            int32_t d[4][4];
+        const int na = cnt[s];
+        int i = 0;
+        for (; i + 1 < na; i += 2) {  // two reads' loads in flight together
+            uint32_t b0, q0, b1, q1;
+            fetch(dl[i], c, b0, q0);
+            fetch(dl[i + 1], c, b1, q1);
+            acc(b0, q0);
+            acc(b1, q1);
+        }
+        if (i < na) {
+            uint32_t b0, q0;
+            fetch(dl[i], c, b0, q0);
+            acc(b0, q0);
+        }
 #pragma unroll
-            for (int j = 0; j < 4; j++)
-#pragma unroll
-                for (int x = 0; x < 4; x++) d[j][x] = 0;
-            const int i1 = ::min(cnt[s], i0 + 128);
+        for (int j = 0; j < 4; j++)
+            if (c + j < lcv[s]) resolve(s, c + j, d[j][0], d[j][1], d[j][2], d[j][3]);
+    }
+    const int ntask2 = nt2[0] + nt2[1] + nt2[2] + nt2[3];
+    for (int k = tt; k < ntask2; k += G) {
+        int s = 0, c = k;
+        while (c >= nt2[s]) {
+            c -= nt2[s];
+            s++;
+        }
+        c *= 2;
+        long long D[2][4] = {{0, 0, 0, 0}, {0, 0, 0, 0}};
+        const uint2 *dl = desc + soff[s];
+        for (int i0 = 0; i0 < cnt[s]; i0 += kSwarReads) {
+            int32_t d[2][4] = {{0, 0, 0, 0}, {0, 0, 0, 0}};
+            const int i1 = ::min(cnt[s], i0 + kSwarReads);
             for (int i = i0; i < i1; i++) {
-                const uint2 e = dl[i];
-                const int k8 = 8 * ((int)(e.y & 0x7FFFFFFFu) - c);
-                if (k8 <= 0) continue;
                 uint32_t b, q;
-                if (e.y >> 31) {
-                    // may start up to 3 bytes before the image (arena bytes, cleared): signed offset
-                    const int32_t ad = (int32_t)e.x - c - 3;
-                    b = comp4(__builtin_bswap32(ldsu32(slots + ad) & ~bytes_past(k8, true)));
-                    q = __builtin_bswap32(ldsu32(qimg + ad));
-                } else {
-                    b = ldsu32(slots + e.x + (uint32_t)c) & ~bytes_past(k8, false) & 0x0F0F0F0Fu;
-                    q = ldsu32(qimg + e.x + (uint32_t)c);
-                }
+                fetch(dl[i], c, b, q);
 #pragma unroll
-                for (int j = 0; j < 4; j++) {
+                for (int j = 0; j < 2; j++) {
                     const uint32_t bj = (b >> (8 * j)) & 0xFu;
                     const int32_t v = lr[(q >> (8 * j)) & 0xFFu];
                     d[j][0] += bj == kA ? v : 0;
@@ -1775,28 +1901,13 @@ __device__ void process_large(const KParams &P, uint8_t *A, const int32_t *lr, c
                 }
             }
 #pragma unroll
-            for (int j = 0; j < 4; j++)
+            for (int j = 0; j < 2; j++)
 #pragma unroll
                 for (int x = 0; x < 4; x++) D[j][x] += d[j][x];
         }
 #pragma unroll
-        for (int j = 0; j < 4; j++) {
-            const int col = c + j;
-            if (col >= lcv[s]) break;
-            int best = 0;
-            long long Db = D[j][0];
-            if (D[j][1] > Db) { best = 1; Db = D[j][1]; }
-            if (D[j][2] > Db) { best = 2; Db = D[j][2]; }
-            if (D[j][3] > Db) { best = 3; Db = D[j][3]; }
-            float S = 0.0f;
-            if (best != 0) S += term(D[j][0] - Db);
-            if (best != 1) S += term(D[j][1] - Db);
-            if (best != 2) S += term(D[j][2] - Db);
-            if (best != 3) S += term(D[j][3] - Db);
-            const int Q = phred_of(S, thr);
-            ssb[s * ssw + col] = Q < 2 ? (uint8_t)kN : (uint8_t)(1u << best);
-            ssq[s * ssw + col] = Q < 2 ? (uint8_t)2 : (uint8_t)Q;
-        }
+        for (int j = 0; j < 2; j++)
+            if (c + j < lcv[s]) resolve(s, c + j, D[j][0], D[j][1], D[j][2], D[j][3]);
     }
     __syncthreads();
     if (stop == 7) return;
@@ -1846,8 +1957,9 @@ __device__ void process_large(const KParams &P, uint8_t *A, const int32_t *lr, c
     }
 }
 
+static_assert(BSDC_LARGE_LDS_MAX + kTabBytes + 256 <= kLdsBytes, "large-family LDS budget");
 template <bool IN_LDS>
-__global__ __launch_bounds__(kLargeThreads) void k_large(KParams P) {
+__global__ __launch_bounds__(kLargeThreads, 5) void k_large(KParams P, const uint4 *fams, int64_t nfams, int32_t arena) {
     extern __shared__ __attribute__((aligned(16))) uint8_t smem[];  // the family's arena (IN_LDS)
     __shared__ __attribute__((aligned(16))) Tables s_tab;
     __shared__ int red[kLargeThreads / kWave];
@@ -1859,9 +1971,9 @@ __global__ __launch_bounds__(kLargeThreads) void k_large(KParams P) {
     const int32_t *lr = T->lr;
     const float *thr = T->thr;
     const int64_t i = blockIdx.x;
-    if (i >= P.B.n_large) return;
-    uint8_t *A = IN_LDS ? smem : P.O.scratch + (size_t)i * (size_t)P.B.large_arena;
-    process_large(P, A, lr, thr, reinterpret_cast<const uint4 *>(P.B.large_fams)[i], red, s_cnt, s_lc, s_cur);
+    if (i >= nfams) return;
+    uint8_t *A = IN_LDS ? smem : P.O.scratch + (size_t)i * (size_t)arena;
+    process_large(P, A, lr, thr, fams[i], red, s_cnt, s_lc, s_cur);
 }
 
 }  // namespace
@@ -2045,9 +2157,19 @@ int32_t bsdc_load_reference(bsdc_ctx *c, const uint8_t *packed, int64_t n_nib, c
 
 int32_t bsdc_run(bsdc_ctx *c, const bsdc_family_batch *b, bsdc_consensus *o, int32_t mode, void *stream) {
     if (!c || !b || !o) return BSDC_EINVAL;
-    if (b->large_arena % 16 || o->stride % 16 || o->stride < b->max_len + 2 || b->max_len > 0xFFFF - 8) {
-        c->err = "bad arena/stride sizes";
+    if (o->stride % 16 || o->stride < b->max_len + 2 || b->max_len > 0xFFFF - 8) {
+        c->err = "bad stride";
         return BSDC_EINVAL;
+    }
+    for (int q = 0; q < BSDC_LARGE_BUCKETS; q++) {
+        if (b->n_large[q] > 0 && (b->large_arena[q] % 16 || b->large_arena[q] <= 0)) {
+            c->err = "bad large arena size";
+            return BSDC_EINVAL;
+        }
+        if (b->n_large[q] > 0 && b->large_arena[q] > BSDC_LARGE_LDS_MAX && !o->scratch) {
+            c->err = "large families need scratch";
+            return BSDC_EINVAL;
+        }
     }
     for (int q = 0; q < BSDC_SMALL_BUCKETS; q++) {
         if (b->n_small[q] > 0 &&
@@ -2096,17 +2218,21 @@ int32_t bsdc_run(bsdc_ctx *c, const bsdc_family_batch *b, bsdc_consensus *o, int
             f += 4 * nf;
         }
     }
-    if (b->n_large > 0 && !(mode & BSDC_MODE_SKIP_LARGE)) {
-        if ((size_t)kTabBytes + (size_t)b->large_arena <= 64 * 1024) {
-            hipLaunchKernelGGL(k_large<true>, dim3((unsigned)b->n_large), dim3(kLargeThreads), (size_t)b->large_arena, s, P);
-        } else {
-            if (!o->scratch) {
-                c->err = "large families need scratch";
-                return BSDC_EINVAL;
+    if (!(mode & BSDC_MODE_SKIP_LARGE)) {
+        // one dispatch per non-empty bucket: its LDS arena size sets how many workgroups share a CU
+        const uint4 *f = reinterpret_cast<const uint4 *>(b->large_fams);
+        for (int q = 0; q < BSDC_LARGE_BUCKETS; q++) {
+            const int64_t nf = b->n_large[q];
+            const int32_t a = b->large_arena[q];
+            if (nf > 0) {
+                if (a <= BSDC_LARGE_LDS_MAX)
+                    hipLaunchKernelGGL(k_large<true>, dim3((unsigned)nf), dim3(kLargeThreads), (size_t)a, s, P, f, nf, a);
+                else
+                    hipLaunchKernelGGL(k_large<false>, dim3((unsigned)nf), dim3(kLargeThreads), 0, s, P, f, nf, a);
+                HIP_OK(c, hipGetLastError());
             }
-            hipLaunchKernelGGL(k_large<false>, dim3((unsigned)b->n_large), dim3(kLargeThreads), 0, s, P);
+            f += nf;
         }
-        HIP_OK(c, hipGetLastError());
     }
     return 0;
 }

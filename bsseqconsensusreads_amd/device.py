@@ -14,7 +14,7 @@ import numpy as np
 import torch
 
 from . import _lib
-from .batch import LDS_TABLES, FamilyBatch
+from .batch import LARGE_LDS_MAX, FamilyBatch
 from .records import Reference
 
 
@@ -60,12 +60,12 @@ class DeviceBatch:
             self.dump_tags = torch.zeros(max(Rn, 1), dtype=torch.uint8, device=device)
             self.dump_seq = torch.zeros(cap, dtype=torch.uint8, device=device)
             self.dump_qual = torch.zeros(cap, dtype=torch.uint8, device=device)
-        lds_cap = 64 * 1024 - LDS_TABLES
-        nl = int(fb.large_fams.shape[0])
-        self.scratch = None
-        if nl and fb.large_arena > lds_cap:
-            # + slack: dword reads may run a few bytes past the last arena (their bytes are masked)
-            self.scratch = torch.zeros(nl * fb.large_arena + 256, dtype=torch.uint8, device=device)
+        # HBM arenas of the large buckets beyond the LDS budget (dispatches run one after another
+        # on the stream, so they share one buffer); + slack: dword reads may run a few bytes past
+        # the last arena (their bytes are masked)
+        need = max([int(b.shape[0]) * a for b, a in zip(fb.large_buckets, fb.large_arenas)
+                    if b.shape[0] and a > LARGE_LDS_MAX] + [0])
+        self.scratch = torch.zeros(need + 256, dtype=torch.uint8, device=device) if need else None
         self._b = _lib.FamilyBatchC()
         b = self._b
         b.n_rec, b.n_fam = Rn, F
@@ -75,9 +75,10 @@ class DeviceBatch:
         for q in range(_lib.SMALL_BUCKETS):
             b.n_small[q] = int(fb.small_buckets[q].shape[0])
             b.small_arena[q] = int(fb.small_arenas[q])
-        b.n_large = nl
+        for q in range(_lib.LARGE_BUCKETS):
+            b.n_large[q] = int(fb.large_buckets[q].shape[0])
+            b.large_arena[q] = int(fb.large_arenas[q])
         b.max_len = fb.max_len
-        b.large_arena = fb.large_arena
         self._o = _lib.ConsensusC()
         o = self._o
         o.stride = self.stride

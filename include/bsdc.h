@@ -24,8 +24,10 @@
 extern "C" {
 #endif
 
-#define BSDC_ABI_VERSION 4
-#define BSDC_SMALL_BUCKETS 8 /* LDS arena size classes of the wavefront-per-family kernel */
+#define BSDC_ABI_VERSION 5
+#define BSDC_SMALL_BUCKETS 8
+#define BSDC_LARGE_BUCKETS 6
+#define BSDC_LARGE_LDS_MAX 158912 /* LDS arena bytes one large-family workgroup may use */ /* LDS arena size classes of the wavefront-per-family kernel */
 
 #define BSDC_EINVAL (-22)
 #define BSDC_ENOMEM (-12)
@@ -79,10 +81,12 @@ typedef struct {
                                     n_rec | (image bytes / 32) << 8, image base (first slot) */
     int64_t n_small[BSDC_SMALL_BUCKETS];      /* families per bucket */
     int32_t small_arena[BSDC_SMALL_BUCKETS];  /* LDS bytes per wavefront of each bucket (multiple of 16) */
-    const uint32_t *large_fams;  /* families processed one workgroup each; 4 words per family:
-                                    family, first record, n_rec, image bytes (from the first slot) */
-    int64_t n_large;
-    int32_t large_arena;         /* bytes per workgroup for large families */
+    const uint32_t *large_fams;  /* families processed one workgroup each, BSDC_LARGE_BUCKETS consecutive
+                                    buckets; 4 words per family: family, first record, n_rec,
+                                    image bytes (from the first slot) */
+    int64_t n_large[BSDC_LARGE_BUCKETS];      /* families per bucket */
+    int32_t large_arena[BSDC_LARGE_BUCKETS];  /* bytes per workgroup of each bucket (multiple of 16); a
+                                                 bucket beyond BSDC_LARGE_LDS_MAX keeps its arenas in `scratch` */
     int32_t max_len;             /* max record length */
 } bsdc_family_batch;
 
@@ -100,7 +104,8 @@ typedef struct {
     uint8_t *dump_tags;          /* [n_rec] bit0 RD=1, bit1 LA present, bit2 prepended M, bit3 appended M */
     uint8_t *dump_seq;           /* [slot start + j] one nt16 code per byte */
     uint8_t *dump_qual;
-    uint8_t *scratch;            /* large-family arenas when large_arena exceeds LDS: n_large * large_arena + 256 bytes */
+    uint8_t *scratch;            /* arenas of the large buckets beyond BSDC_LARGE_LDS_MAX: the largest
+                                    n_large[q] * large_arena[q] of them + 256 bytes */
 } bsdc_consensus;
 
 #define BSDC_MODE_CONVERT 1

@@ -71,6 +71,9 @@ def test_missing_mi_raises(engine):
 def test_synthetic_configs_vs_oracle(engine, cfg):
     n = {"C0": 3000, "C1": 1500, "C2": 3000, "C3": 150, "C4": 1200}[cfg]
     s = synth.generate(cfg, n, seed=11, device="cpu", genome_len=400_000)
+    if cfg == "C4":  # the deep-set vote path (a strand/end set of more than 128 reads) is exercised
+        fb = batch.build_family_batch(s.raw, "full", s.ref)
+        assert np.diff(fb.fam_off.astype(np.int64)).max() > 600
     engine.load_reference(s.ref)
     cons, t2 = pipeline.run_step5(engine, s.raw, dump=True)
     ref = oracle.run(s.raw, s.ref)
@@ -111,8 +114,10 @@ def test_large_family_kernel(engine, where, monkeypatch):
 
     def forced(r, mode="full", ref=None, small_cap=0):
         fb = real(r, mode, ref, small_cap=0)
-        if where == "global":
-            fb.large_arena = max(fb.large_arena, 70000)
+        if where == "global":  # every large family in the last (HBM scratch) bucket
+            nb = len(fb.large_buckets)
+            fb.large_buckets = [np.zeros((0, 4), np.uint32)] * (nb - 1) + [fb.large_fams]
+            fb.large_arenas = [16] * (nb - 1) + [max(max(fb.large_arenas), batch.LARGE_LDS_MAX + 16)]
         return fb
 
     monkeypatch.setattr(pipeline, "build_family_batch", forced)
