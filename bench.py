@@ -126,7 +126,10 @@ def main():
     out = db.fetch()
     emitted = int((out["status"] & 1).sum())
     tot = torch.tensor([elapsed, 0.0], dtype=torch.float64, device=dev)
-    cnt = torch.tensor([fb.n_fam, emitted], dtype=torch.int64, device=dev)
+    # the unit is the input family (one MI base = one molecule); TemplateCoordinate order can
+    # split a molecule into several consensus families (config.consensus_families_per_gpu)
+    molecules = int(np.unique(fb.fam_mi).shape[0])
+    cnt = torch.tensor([molecules, emitted], dtype=torch.int64, device=dev)
     if dist is not None:
         dist.all_reduce(tot, op=dist.ReduceOp.MAX)
         dist.all_reduce(cnt, op=dist.ReduceOp.SUM)
@@ -192,7 +195,8 @@ def main():
             "dtype": "u8",
             "data": "synthetic (seeded EM-seq duplex model generated on the GPU, SURVEY.md 8d)",
             "config": {"workload": args.config + " -- " + WORKLOADS[args.config],
-                       "families_per_gpu": int(fb.n_fam), "records_per_gpu": int(fb.n_rec),
+                       "families_per_gpu": molecules, "consensus_families_per_gpu": int(fb.n_fam),
+                       "family_order": "fgbio TemplateCoordinate runs of one MI", "records_per_gpu": int(fb.n_rec),
                        "bases_per_gpu": int(fb.n_bases), "small_families": int(small.size),
                        "large_families": int(large.size), "parallelism": "family-sharded x%d" % world},
             "roofline": {"bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",

@@ -115,6 +115,8 @@ class FamilyBatch:
     fam_mi: np.ndarray       # i32 [F] MI id of each family
     n_bases: int
     n_slots: int
+    t2_rank: np.ndarray      # i64 [R] tool-2 output position of each batch record
+    split_ext: bool          # a tool-2 extension partner sits in another family (see build_family_batch)
 
     @property
     def n_rec(self) -> int:
@@ -196,10 +198,123 @@ def _softclip_strip(raw: R.RawRecords):
     return sL, L, kfirst, kn
 
 
+def _clips_reflen(cig: np.ndarray, off: np.ndarray, cnt: np.ndarray):
+    """Per record of a cigar store (ops at cig[off : off + cnt], cnt <= 0 = none): leading S/H
+    length, trailing S/H length, reference-consuming length."""
+    n = cnt.shape[0]
+    cnt = np.where(cnt > 0, cnt, 0).astype(np.int64)
+    tot = int(cnt.sum())
+    if tot == 0:
+        z = np.zeros(n, np.int64)
+        return z, z.copy(), z.copy()
+    rec = np.repeat(np.arange(n, dtype=np.int64), cnt)
+    start = np.cumsum(cnt) - cnt
+    j = np.arange(tot, dtype=np.int64) - start[rec]
+    c = cig[np.repeat(np.where(cnt > 0, off, 0).astype(np.int64), cnt) + j]
+    op = (c & 0xF).astype(np.int64)
+    ln = (c >> 4).astype(np.int64)
+    clip = np.isin(op, (R.OP_S, R.OP_H))
+    refc = np.isin(op, R.REF_CONSUMING)
+    reflen = np.bincount(rec[refc], weights=ln[refc], minlength=n)[:n].astype(np.int64)
+    nc = np.cumsum(~clip)                       # non-clip ops up to and including this one
+    upto = nc - np.where(start > 0, nc[np.maximum(start - 1, 0)], 0)[rec]
+    before = upto - (~clip)
+    after = np.bincount(rec[~clip], minlength=n)[:n][rec] - upto
+    lm = clip & (before == 0)
+    tm = clip & (after == 0) & ~lm
+    lead = np.bincount(rec[lm], weights=ln[lm], minlength=n)[:n].astype(np.int64)
+    trail = np.bincount(rec[tm], weights=ln[tm], minlength=n)[:n].astype(np.int64)
+    return lead, trail, reflen
+
+
+def mate_unclipped(raw: R.RawRecords):
+    """Mate unclipped (start, end) from PNEXT and the MC tag (stale after tools 1/2); PNEXT alone
+    without MC."""
+    lead, trail, mref = _clips_reflen(raw.mc_cigar, raw.mc_off, np.where(raw.mc_off >= 0, raw.mc_n, 0))
+    np_ = raw.next_pos.astype(np.int64)
+    has = raw.mc_off >= 0
+    return np.where(has, np_ - lead, np_), np.where(has, np_ + mref - 1 + trail, np_)
+
+
+def predict_rd(raw: R.RawRecords, ref: R.Reference, sel: np.ndarray, sL: np.ndarray, L: np.ndarray) -> np.ndarray:
+    """Tool 1's RD (tools/1.convert_AG_to_CT.py:157-170) of converted records `sel`, from the input
+    bases and the reference alone: the last output base is C iff the last input base (the seed
+    ref[0] for an empty read) is C with ref = C G at (L', L'+1) -- the rule at :134-150 with no next
+    base -- and RD = that C before a reference G."""
+    sel = np.asarray(sel, np.int64)
+    if sel.shape[0] == 0:
+        return np.zeros(0, bool)
+    tid = raw.tid[sel].astype(np.int64)
+    np0 = np.maximum(raw.pos[sel].astype(np.int64) - 1, 0)
+    nt = len(ref.names)
+    okt = (tid >= 0) & (tid < nt)
+    ti = np.clip(tid, 0, max(nt - 1, 0))
+    coff = np.where(okt, ref.contig_off[ti], -1) if nt else np.full(sel.shape[0], -1)
+    clen = np.where(okt, ref.contig_len[ti], 0) if nt else np.zeros(sel.shape[0], np.int64)
+    Ls = L[sel].astype(np.int64)
+    Lp = Ls + 1
+    avail = np.where(coff >= 0, np.clip(clen - np0, 0, Lp + 1), 0)
+
+    def refnib(i):
+        ok = i < avail
+        idx = np.where(ok, coff + np0 + i, 0)
+        b = ref.packed[np.minimum(idx >> 1, max(ref.packed.shape[0] - 1, 0))] if ref.packed.shape[0] else np.zeros_like(idx)
+        nib = np.where(idx & 1, b & 0xF, b >> 4)
+        return np.where(ok, nib, 15)
+
+    lastpos = raw.seq_off[sel] + sL[sel] + Ls - 1
+    last = np.where(Ls > 0, raw.seq[np.clip(lastpos, 0, max(raw.seq.shape[0] - 1, 0))], refnib(np.zeros_like(Ls)))
+    return (last == 2) & (refnib(Lp - 1) == 2) & (refnib(Lp) == 4)
+
+
+def lex_rank(strings, ids: np.ndarray) -> np.ndarray:
+    """A key per element of ids that orders them as strings[id] sort in byte order."""
+    ids = np.asarray(ids, np.int64)
+    if hasattr(strings, "lex_key"):  # synthetic names: computed, not materialised
+        return strings.lex_key(ids)
+    if ids.shape[0] == 0:
+        return np.zeros(0, np.int64)
+    u, inv = np.unique(ids, return_inverse=True)
+    a = np.array([strings[int(i)] if isinstance(strings[int(i)], bytes) else strings[int(i)].encode() for i in u],
+                 dtype=object).astype(bytes)
+    _, rk = np.unique(a, return_inverse=True)
+    return rk.astype(np.int64)[inv]
+
+
+def template_coordinate_order(raw: R.RawRecords, recs: np.ndarray, us: np.ndarray, ue: np.ndarray,
+                              mate_us: np.ndarray, mate_ue: np.ndarray) -> np.ndarray:
+    """fgbio SortBam -s TemplateCoordinate (main.snake.py:152; SURVEY.md 8a row 7, parity
+    unpinned) of records `recs` (raw indices) whose current unclipped ends are us / ue: the
+    stable permutation by (tid, mate tid, unclipped 5' pos, mate unclipped 5' pos, strands,
+    library, MI base, name, upper-of-pair), the template's lower end first.  Mate fields are the
+    input's (stale), one library."""
+    fl = raw.flag[recs].astype(np.int64)
+    neg = (fl & 16) != 0
+    t1 = raw.tid[recs].astype(np.int64)
+    p1 = np.where(neg, ue, us)
+    paired = ((fl & 1) != 0) & ((fl & 8) == 0)
+    big = np.int64(np.iinfo(np.int32).max)
+    n2 = paired & ((fl & 32) != 0)
+    t2 = np.where(paired, raw.next_tid[recs].astype(np.int64), big)
+    p2 = np.where(paired, np.where(n2, mate_ue[recs], mate_us[recs]), big)
+    lower = (t1 < t2) | ((t1 == t2) & ((p1 < p2) | ((p1 == p2) & (neg <= n2))))
+    T1, T2 = np.where(lower, t1, t2), np.where(lower, t2, t1)
+    P1, P2 = np.where(lower, p1, p2), np.where(lower, p2, p1)
+    N1, N2 = np.where(lower, neg, n2), np.where(lower, n2, neg)
+    mi = lex_rank(raw.mi_names, raw.mi_id[recs])
+    nm = lex_rank(raw.names, raw.name_id[recs])
+    return np.lexsort((np.arange(recs.shape[0]), ~lower, nm, mi, N2, N1, P2, P1, T2, T1))
+
+
 def build_family_batch(raw: R.RawRecords, mode: str = "full", ref: Optional[R.Reference] = None,
-                       small_cap: int = SMALL_ARENA_CAP) -> FamilyBatch:
+                       small_cap: int = SMALL_ARENA_CAP, family_order: str = "template-coordinate") -> FamilyBatch:
     """mode: 'full' (raw step-5 input: tools 1+2 then the vote), 'convert' (tool 1 alone: one
-    family per converted record), 'extend' (tool-1 output: tool 2 alone), 'vote' (tool-2 output)."""
+    family per converted record), 'extend' (tool-1 output: tool 2 alone), 'vote' (tool-2 output).
+    family_order ('full' / 'vote'): 'template-coordinate' -- the vote's families are the runs of one
+    MI base in fgbio TemplateCoordinate order of the tool-2 records (SortBam, main.snake.py:152,
+    then the duplex caller's grouping), records in that order; 'mi-group' -- tool 2's MI groups."""
+    if family_order not in ("template-coordinate", "mi-group"):
+        raise ValueError(family_order)
     n = raw.n
     f = raw.flag.astype(np.int64)
     rec, ops, lens, jop = _per_record_ops(raw)
@@ -234,7 +349,7 @@ def build_family_batch(raw: R.RawRecords, mode: str = "full", ref: Optional[R.Re
     idx2 = np.nonzero(keep2)[0].astype(np.int64)
     ext_right = np.zeros(n, bool)
     ext_left = np.zeros(n, bool)
-    partner_local = np.zeros(n, np.int64)
+    partner_raw = np.full(n, -1, np.int64)  # tool-2 extension partner (input record index)
     rd_in = np.zeros(n, bool)
 
     if mode == "convert":
@@ -313,26 +428,64 @@ def build_family_batch(raw: R.RawRecords, mode: str = "full", ref: Optional[R.Re
                 # roles; local indices are positions within the group's output list
                 q = p1 & la_b
                 ext_right[a_rec[q]] = True
-                partner_local[a_rec[q]] = a_pos[q]
+                partner_raw[a_rec[q]] = b_rec[q]
                 ext_left[b_rec[p1]] = True
-                partner_local[b_rec[p1]] = b_pos[p1]
+                partner_raw[b_rec[p1]] = a_rec[p1]
                 q = p2 & la_c
                 ext_right[d_rec[q]] = True
-                partner_local[d_rec[q]] = c_pos[q]
+                partner_raw[d_rec[q]] = c_rec[q]
                 ext_left[c_rec[p2]] = True
-                partner_local[c_rec[p2]] = d_pos[p2]
+                partner_raw[c_rec[p2]] = d_rec[p2]
                 # write back the new order; dropped flags go to the tail and are masked out
                 out_members[base[:, None] + np.arange(4)[None, :]] = outm
                 kr = np.arange(4)[None, :] < nkeep[:, None]
                 keep_rec[base[:, None] + np.arange(4)[None, :]] = kr
                 fam_sizes[g4] = nkeep
         order = out_members[keep_rec]
+    t2_rank = np.arange(order.shape[0], dtype=np.int64)  # tool-2 output position of each batch record
+    if mode in ("full", "vote") and family_order == "template-coordinate" and order.shape[0]:
+        # the tool-2 records' current unclipped ends: tools 1/2 move pos and grow the cigar by the
+        # prepended / appended base (clips are stripped); tool 1's RD is predicted from the input
+        lead, trail, rref = _clips_reflen(raw.cigar, raw.cig_off, raw.n_cig)
+        pos0 = raw.pos[order].astype(np.int64)
+        if mode == "full":
+            cv = conv[order]
+            rdp = np.zeros(order.shape[0], bool)
+            if cv.any():
+                if ref is None:
+                    raise ValueError("converting records needs the reference")
+                rdp[cv] = predict_rd(raw, ref, order[cv], sL, L)
+            er, el = ext_right[order], ext_left[order]
+            pos1 = np.where(cv, np.maximum(pos0 - 1, 0), np.where(er, pos0 - 1, pos0))
+            rl1 = rref[order] + cv.astype(np.int64) - (cv & rdp) + er.astype(np.int64) + (el & rdp)
+            us, ue = pos1, pos1 + rl1 - 1
+        else:
+            us, ue = pos0 - lead[order], pos0 + rref[order] - 1 + trail[order]
+        mus, mue = mate_unclipped(raw)
+        perm = template_coordinate_order(raw, order, us, ue, mus, mue)
+        order = order[perm]
+        t2_rank = perm
+        mi = raw.mi_id[order]
+        brk = np.ones(order.shape[0], bool)
+        brk[1:] = mi[1:] != mi[:-1]
+        starts = np.nonzero(brk)[0]
+        fam_sizes = np.diff(np.append(starts, order.shape[0])).astype(np.int64)
+        fam_mi = mi[starts].astype(np.int32)
     nr = int(order.shape[0])
     nf = int(fam_sizes.shape[0])
     fam_off = np.zeros(nf + 1, np.int64)
     fam_off[1:] = np.cumsum(fam_sizes)
     fam_of = np.repeat(np.arange(nf, dtype=np.int64), fam_sizes)
     local = np.arange(nr, dtype=np.int64) - fam_off[fam_of]
+    # extension partners as family-local indices; a partner in another family (a TemplateCoordinate
+    # run that splits a tool-2 4-group between the two pairs' reads) makes the fused launch invalid
+    inv = np.full(n, -1, np.int64)
+    inv[order] = np.arange(nr, dtype=np.int64)
+    has_p = (ext_right | ext_left)[order]
+    pb = inv[np.where(has_p, partner_raw[order], 0)]
+    pl = np.where(has_p, pb - fam_off[fam_of], 0)
+    split_ext = bool((has_p & ((pb < 0) | (pl < 0) | (pl >= fam_sizes[fam_of]) | (pl > 3))).any()) if nr else False
+    pl = np.where(has_p & (pl >= 0) & (pl <= 3), pl, 0)
 
     # ---- per batch record ----
     Lb = L[order]
@@ -422,7 +575,7 @@ def build_family_batch(raw: R.RawRecords, mode: str = "full", ref: Optional[R.Re
     link |= np.where(conv[order], LINK_CONVERT, 0)
     link |= np.where(ext_right[order], LINK_EXT_RIGHT, 0)
     link |= np.where(ext_left[order], LINK_EXT_LEFT, 0)
-    link |= np.where(ext_right[order] | ext_left[order], partner_local[order] << LINK_PARTNER_SHIFT, 0)
+    link |= np.where(has_p, pl << LINK_PARTNER_SHIFT, 0)
     link |= np.where(rd_in[order], LINK_RD_IN, 0)
     link |= np.where(usable, LINK_USABLE, 0)
 
@@ -538,4 +691,4 @@ def build_family_batch(raw: R.RawRecords, mode: str = "full", ref: Optional[R.Re
         rt=rt.reshape(-1).astype(np.int32), seq=seq, qual=qual,
         small_buckets=buckets, small_arenas=arenas, large_buckets=lbuckets, large_arenas=larenas,
         max_len=max_len, src=order.astype(np.int64), fam_mi=fam_mi.astype(np.int32),
-        n_bases=total, n_slots=n_slots)
+        n_bases=total, n_slots=n_slots, t2_rank=t2_rank, split_ext=split_ext)

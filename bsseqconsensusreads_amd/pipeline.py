@@ -67,21 +67,25 @@ def _stripped_cigar(raw: R.RawRecords, k: int, strip: bool) -> List[int]:
 
 
 def _records_from_dump(raw: R.RawRecords, fb: FamilyBatch, out: dict, strip: bool) -> OutRecords:
+    """The stage dump as tool-2 output records, in tool-2 output order (the batch may hold them in
+    TemplateCoordinate order)."""
     n = fb.n_rec
-    lens = out["dump_len"][:n].astype(np.int64)
+    bo = np.argsort(fb.t2_rank, kind="stable")  # batch record of each tool-2 output position
+    lens = out["dump_len"][:n].astype(np.int64)[bo]
     seq_off = np.zeros(n, np.int64)
     if n:
         seq_off[1:] = np.cumsum(lens)[:-1]
-    d = fb.rec_off.astype(np.int64)
+    d = fb.rec_off.astype(np.int64)[bo]
     idx = np.repeat(d - seq_off, lens) + np.arange(int(lens.sum()), dtype=np.int64)
     seq = out["dump_seq"][idx]
     qual = out["dump_qual"][idx]
-    tags = out["dump_tags"][:n]
+    tags = out["dump_tags"][:n][bo]
+    src = fb.src[bo]
     cig, ncig = [], []
     rd = np.full(n, -1, np.int32)
     la = np.full(n, -1, np.int32)
     for b in range(n):
-        k = int(fb.src[b])
+        k = int(src[b])
         ops = _stripped_cigar(raw, k, strip)
         t = int(tags[b])
         if t & 2:  # converted in this launch: [(M,1)] + cigar, RD trims the last op
@@ -104,8 +108,27 @@ def _records_from_dump(raw: R.RawRecords, fb: FamilyBatch, out: dict, strip: boo
     cig_off = np.zeros(n, np.int64)
     if n:
         cig_off[1:] = np.cumsum(n_cig)[:-1]
-    return OutRecords(fb.src.copy(), out["dump_pos"][:n].astype(np.int32), lens.astype(np.int32), seq_off, seq, qual,
+    return OutRecords(src.copy(), out["dump_pos"][:n].astype(np.int32)[bo], lens.astype(np.int32), seq_off, seq, qual,
                       n_cig, cig_off, np.asarray(cig, np.uint32), rd, la)
+
+
+def raw_from_records(raw: R.RawRecords, t: OutRecords) -> R.RawRecords:
+    """Tool-2 output records as a RawRecords stream (mate fields, MI, name and MC from the input
+    record: the tools leave them stale), for callduplex alone."""
+    src = t.src.astype(np.int64)
+    mcn = np.where(raw.mc_off[src] >= 0, raw.mc_n[src], 0).astype(np.int64)
+    mc_off = np.where(mcn > 0, np.cumsum(mcn) - mcn, -1)
+    mcj = np.repeat(np.where(mcn > 0, raw.mc_off[src], 0), mcn) + \
+        (np.arange(int(mcn.sum())) - np.repeat(np.cumsum(mcn) - mcn, mcn))
+    return R.RawRecords(
+        flag=raw.flag[src], tid=raw.tid[src], pos=t.pos.astype(np.int32), mapq=raw.mapq[src],
+        l_seq=t.l_seq.astype(np.int32), seq_off=t.seq_off.astype(np.int64), seq=t.seq, qual=t.qual,
+        cig_off=t.cig_off.astype(np.int64), n_cig=t.n_cig.astype(np.int32), cigar=t.cigar,
+        next_tid=raw.next_tid[src], next_pos=raw.next_pos[src], tlen=raw.tlen[src],
+        name_id=raw.name_id[src], names=raw.names, mi_id=raw.mi_id[src], mi_strand=raw.mi_strand[src],
+        mi_names=raw.mi_names, mc_off=np.where(raw.mc_off[src] >= 0, mc_off, -1).astype(np.int64),
+        mc_n=raw.mc_n[src], mc_cigar=raw.mc_cigar[mcj] if mcj.shape[0] else np.zeros(0, np.uint32),
+        la_tag=t.la.astype(np.int32), rd_tag=t.rd.astype(np.int32))
 
 
 def _concat_records(parts: List[OutRecords], order: np.ndarray) -> OutRecords:
@@ -191,6 +214,14 @@ def consensus_from_output(fb: FamilyBatch, out: dict) -> Consensus:
 def run_step5(engine: Engine, raw: R.RawRecords, dump: bool = False):
     """Rules convert_Bstrain .. callduplex (main.snake.py:121-164) -> (Consensus, tool-2 records or None)."""
     fb = build_family_batch(raw, "full", engine.ref)
+    if fb.split_ext:
+        # a TemplateCoordinate family lacks a record's tool-2 extension partner: run the tools as
+        # their own launch (tool-2 MI groups), then callduplex on their records
+        fb2 = build_family_batch(raw, "full", engine.ref, family_order="mi-group")
+        db = engine.upload(fb2, dump=True)
+        engine.run(db, MODE_CONVERT | MODE_EXTEND | MODE_DUMP)
+        t2 = _records_from_dump(raw, fb2, db.fetch(), strip=True)
+        return run_duplex(engine, raw_from_records(raw, t2)), (t2 if dump else None)
     db = engine.upload(fb, dump=dump)
     engine.run(db, MODE_CONVERT | MODE_EXTEND | MODE_VOTE | (MODE_DUMP if dump else 0))
     out = db.fetch()

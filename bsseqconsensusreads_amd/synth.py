@@ -204,6 +204,15 @@ class _LazyNames:
     def __len__(self):
         return 1 << 62
 
+    def lex_key(self, ids: np.ndarray) -> np.ndarray:
+        """int64 keys that order ids as their strings sort in byte order (one prefix, decimal
+        digits): the digits left-aligned to 10 places, then the digit count (a prefix first)."""
+        x = np.asarray(ids, np.int64)
+        d = np.ones_like(x)
+        for k in range(1, 11):
+            d += x >= 10 ** k
+        return (x * 10 ** (10 - d)) * 16 + d
+
 
 def messify(raw: R.RawRecords, frac: float = 0.1, seed: int = 1) -> R.RawRecords:
     """Sprinkle the edge cases the tools handle differently: soft clips, I/D/N ops, hard clips,

@@ -679,6 +679,8 @@ struct orc_result {
     int32_t *fam_nreads;
     char **fam_b;       /* [2*f + end] */
     uint8_t **fam_q;
+    int64_t *fam_rec_off; /* [nfam + 1] into fam_src */
+    int64_t *fam_src;     /* input record index of each family record, family order */
 };
 
 static void family_call(orec *recs, int n, const orc_records *in, const orc_params *p, const int64_t *lr,
@@ -799,6 +801,78 @@ static void family_call(orec *recs, int n, const orc_records *in, const orc_para
     free(ky);
 }
 
+/* ------------------------------------------------------------------------------------------ */
+/* family formation: fgbio SortBam -s TemplateCoordinate (main.snake.py:152) + the duplex       */
+/* caller's grouping of consecutive records with one MI base (fgbio is not  */
+/* vendored: PARITY UNPINNED).  Key: (tid, mate tid, unclipped 5' pos, mate unclipped 5' pos,    */
+/* strands, library, MI base, name, upper-of-pair), the lower end of the template first; the     */
+/* mate fields are the stale ones the tools leave (PNEXT, MC).                                    */
+/* ------------------------------------------------------------------------------------------ */
+typedef struct {
+    int32_t tid1, tid2, pos1, pos2;
+    int32_t neg1, neg2, lib, mi, name, upper;
+    int64_t ord; /* tool-2 output position: ties keep it (a stable sort) */
+} tc_key;
+
+static void unclipped_ends(const uint32_t *c, int32_t n, int32_t pos, int32_t *us, int32_t *ue) {
+    int32_t lead = 0, trail = 0, i = 0, j = n - 1;
+    for (; i < n && (cig_op(c[i]) == OP_S || cig_op(c[i]) == OP_H); i++) lead += cig_len(c[i]);
+    for (; j >= i && (cig_op(c[j]) == OP_S || cig_op(c[j]) == OP_H); j--) trail += cig_len(c[j]);
+    *us = pos - lead;
+    *ue = pos + ref_len_ops(c, n) - 1 + trail;
+}
+
+static tc_key tc_key_of(const orec *r, const orc_records *in, int64_t ord) {
+    tc_key k;
+    int32_t us, ue, mus, mue;
+    unclipped_ends(r->cig, r->ncig, r->pos, &us, &ue);
+    const int32_t neg = (r->flag & 16) != 0;
+    const int32_t t1 = r->tid, p1 = neg ? ue : us;
+    int32_t t2 = INT32_MAX, p2 = INT32_MAX, n2 = 0;
+    if ((r->flag & 1) && !(r->flag & 8)) {
+        const int64_t s = r->src;
+        t2 = in->next_tid[s];
+        n2 = (r->flag & 32) != 0;
+        if (in->mc_off[s] >= 0) {
+            unclipped_ends(in->mc_cigar + in->mc_off[s], in->mc_n[s], in->next_pos[s], &mus, &mue);
+        } else {
+            mus = mue = in->next_pos[s];
+        }
+        p2 = n2 ? mue : mus;
+    }
+    const int lower = t1 < t2 || (t1 == t2 && (p1 < p2 || (p1 == p2 && neg <= n2)));
+    k.tid1 = lower ? t1 : t2;
+    k.pos1 = lower ? p1 : p2;
+    k.neg1 = lower ? neg : n2;
+    k.tid2 = lower ? t2 : t1;
+    k.pos2 = lower ? p2 : p1;
+    k.neg2 = lower ? n2 : neg;
+    k.upper = !lower;
+    k.lib = in->lib_id ? in->lib_id[r->src] : 0;
+    k.mi = in->mi_lex[in->mi_id[r->src]];
+    k.name = in->name_lex[in->name_id[r->src]];
+    k.ord = ord;
+    return k;
+}
+
+static int tc_cmp(const void *pa, const void *pb) {
+    const tc_key *a = (const tc_key *)pa, *b = (const tc_key *)pb;
+#define TC_CMP(f) if (a->f != b->f) return a->f < b->f ? -1 : 1
+    TC_CMP(tid1);
+    TC_CMP(tid2);
+    TC_CMP(pos1);
+    TC_CMP(pos2);
+    TC_CMP(neg1);
+    TC_CMP(neg2);
+    TC_CMP(lib);
+    TC_CMP(mi);
+    TC_CMP(name);
+    TC_CMP(upper);
+    TC_CMP(ord);
+#undef TC_CMP
+    return 0;
+}
+
 orc_result *orc_run(const orc_records *in, const orc_reference *ref, const orc_params *p) {
     g_err[0] = 0;
 #ifdef _OPENMP
@@ -911,6 +985,29 @@ orc_result *orc_run(const orc_records *in, const orc_reference *ref, const orc_p
             if (!used[i]) orec_free(&v[i]);
     }
     fam_off[ng] = res->t2.n;
+    /* family records: the tool-2 groups as they are, or runs of one MI in TemplateCoordinate order */
+    orec *frecs = (orec *)malloc(sizeof(orec) * (size_t)(res->t2.n + 1)); /* shallow copies */
+    if (p->family_order == 1) {
+        tc_key *keys = (tc_key *)malloc(sizeof(tc_key) * (size_t)(res->t2.n + 1));
+        for (int64_t k = 0; k < res->t2.n; k++) keys[k] = tc_key_of(&res->t2.v[k], in, k);
+        qsort(keys, (size_t)res->t2.n, sizeof(tc_key), tc_cmp);
+        fam_off = (int64_t *)realloc(fam_off, sizeof(int64_t) * (size_t)(res->t2.n + 2)); /* runs >= groups */
+        int64_t nf = 0;
+        for (int64_t k = 0; k < res->t2.n; k++) {
+            frecs[k] = res->t2.v[keys[k].ord];
+            const int32_t mi = in->mi_id[frecs[k].src];
+            if (k == 0 || mi != in->mi_id[frecs[k - 1].src]) {
+                fam_off[nf] = k;
+                gorder_mi[nf] = mi;
+                nf++;
+            }
+        }
+        fam_off[nf] = res->t2.n;
+        ng = nf;
+        free(keys);
+    } else {
+        for (int64_t k = 0; k < res->t2.n; k++) frecs[k] = res->t2.v[k];
+    }
     free(grouped);
     free(goff);
     free(gfill);
@@ -922,6 +1019,10 @@ orc_result *orc_run(const orc_records *in, const orc_reference *ref, const orc_p
     float thr[94];
     orc_tables(p->error_rate_pre_umi, p->error_rate_post_umi, lr, thr);
     res->nfam = ng;
+    res->fam_rec_off = (int64_t *)malloc(sizeof(int64_t) * (size_t)(ng + 1));
+    res->fam_src = (int64_t *)malloc(sizeof(int64_t) * (size_t)(res->t2.n + 1));
+    for (int64_t g = 0; g <= ng; g++) res->fam_rec_off[g] = fam_off[g];
+    for (int64_t k = 0; k < res->t2.n; k++) res->fam_src[k] = frecs[k].src;
     int32_t maxlen = 0;
     for (int64_t k = 0; k < res->t2.n; k++)
         if (res->t2.v[k].len > maxlen) maxlen = res->t2.v[k].len;
@@ -935,7 +1036,8 @@ orc_result *orc_run(const orc_records *in, const orc_reference *ref, const orc_p
     for (int64_t g = 0; g < ng; g++) res->fam_mi[g] = gorder_mi[g];
 #pragma omp parallel for schedule(dynamic, 64)
     for (int64_t g = 0; g < ng; g++)
-        family_call(res->t2.v + fam_off[g], (int)(fam_off[g + 1] - fam_off[g]), in, p, lr, thr, res, g);
+        family_call(frecs + fam_off[g], (int)(fam_off[g + 1] - fam_off[g]), in, p, lr, thr, res, g);
+    free(frecs);
     free(gorder_mi);
     free(fam_off);
     return res;
@@ -945,6 +1047,8 @@ void orc_free(orc_result *r) {
     if (!r) return;
     for (int64_t k = 0; k < r->t1.n; k++) orec_free(&r->t1.v[k]);
     for (int64_t k = 0; k < r->t2.n; k++) orec_free(&r->t2.v[k]);
+    free(r->fam_rec_off);
+    free(r->fam_src);
     free(r->t1.v);
     free(r->t2.v);
     for (int64_t i = 0; i < 2 * r->nfam; i++) {
@@ -996,6 +1100,10 @@ void orc_get_records(const orc_result *r, int which, int64_t *src, int32_t *pos,
 }
 
 int64_t orc_n_families(const orc_result *r) { return r->nfam; }
+void orc_get_families(const orc_result *r, int64_t *rec_off, int64_t *src) {
+    for (int64_t g = 0; g <= r->nfam; g++) rec_off[g] = r->fam_rec_off[g];
+    for (int64_t k = 0; k < r->fam_rec_off[r->nfam]; k++) src[k] = r->fam_src[k];
+}
 int32_t orc_max_cons_len(const orc_result *r) { return r->maxlen; }
 void orc_get_consensus(const orc_result *r, int32_t stride, int32_t *mi_id, int32_t *status, int32_t *len,
                        uint8_t *bases, uint8_t *quals, int32_t *n_reads) {

@@ -43,6 +43,11 @@ typedef struct {
     const int64_t *mc_off;    /* MC tag cigar, -1 = no MC tag */
     const int32_t *mc_n;
     const uint32_t *mc_cigar;
+    /* TemplateCoordinate order (family_order = 1): byte-order rank of each MI base string (per mi
+     * id) and of each QNAME (per name id); library id per record (NULL = one library) */
+    const int32_t *mi_lex;
+    const int32_t *name_lex;
+    const int32_t *lib_id;
 } orc_records;
 
 typedef struct {
@@ -59,6 +64,8 @@ typedef struct {
     int32_t consensus_call_overlapping_bases; /* 1 */
     int32_t run_tools;           /* 1: raw input -> tool1 -> tool2 -> vote; 0: input is already tool-2 output */
     int32_t n_threads;           /* OpenMP threads, <= 0 = default */
+    int32_t family_order;        /* 1: families = runs of one MI base in fgbio TemplateCoordinate order of the
+                                    tool-2 records (SortBam at main.snake.py:152); 0: tool-2 MI groups */
 } orc_params;
 
 typedef struct orc_result orc_result;
@@ -77,8 +84,10 @@ void orc_get_records(const orc_result *r, int which, int64_t *src, int32_t *pos,
                      uint8_t *seq, uint8_t *qual, int32_t *n_cig, uint32_t *cigar, int32_t *rd,
                      int32_t *la);
 
-/* Consensus per family (families = tool-2 MI groups, in tool-2 order). */
+/* Consensus per family, in family order (TemplateCoordinate runs, or tool-2 MI groups). */
 int64_t orc_n_families(const orc_result *r);
+/* Family membership: rec_off[nfam + 1], src[rec_off[nfam]] = input record index per family record. */
+void orc_get_families(const orc_result *r, int64_t *rec_off, int64_t *src);
 int32_t orc_max_cons_len(const orc_result *r);
 /* stride = bases per (family, end) slot; bases ASCII (A,C,G,T,N); status 1 = pair emitted. */
 void orc_get_consensus(const orc_result *r, int32_t stride, int32_t *mi_id, int32_t *status,

@@ -29,7 +29,8 @@ _ASCII_NT16[ord("U")] = _ASCII_NT16[ord("u")] = 8
 class _Records(C.Structure):
     _fields_ = [("n", C.c_int64)] + [(k, C.c_void_p) for k in (
         "flag", "tid", "pos", "l_seq", "seq_off", "seq", "qual", "cig_off", "n_cig", "cigar", "mi_id",
-        "mi_strand", "name_id", "next_tid", "next_pos", "tlen", "mc_off", "mc_n", "mc_cigar")]
+        "mi_strand", "name_id", "next_tid", "next_pos", "tlen", "mc_off", "mc_n", "mc_cigar", "mi_lex", "name_lex",
+        "lib_id")]
 
 
 class _Reference(C.Structure):
@@ -39,7 +40,7 @@ class _Reference(C.Structure):
 class _Params(C.Structure):
     _fields_ = [("error_rate_pre_umi", C.c_double), ("error_rate_post_umi", C.c_double),
                 ("min_input_base_quality", C.c_int32), ("consensus_call_overlapping_bases", C.c_int32),
-                ("run_tools", C.c_int32), ("n_threads", C.c_int32)]
+                ("run_tools", C.c_int32), ("n_threads", C.c_int32), ("family_order", C.c_int32)]
 
 
 _lib = None
@@ -65,6 +66,7 @@ def load():
         lib.orc_get_records.argtypes = [C.c_void_p, C.c_int] + [C.c_void_p] * 9
         lib.orc_n_families.restype = C.c_int64
         lib.orc_n_families.argtypes = [C.c_void_p]
+        lib.orc_get_families.argtypes = [C.c_void_p, C.c_void_p, C.c_void_p]
         lib.orc_max_cons_len.restype = C.c_int32
         lib.orc_max_cons_len.argtypes = [C.c_void_p]
         lib.orc_get_consensus.argtypes = [C.c_void_p, C.c_int32] + [C.c_void_p] * 6
@@ -113,14 +115,34 @@ class OracleResult:
     cons_qual: np.ndarray   # [F, 2, stride]
     n_reads: np.ndarray
     seconds: float = 0.0    # wall time of orc_run alone
+    fam_rec_off: np.ndarray = None  # [F + 1] family membership: fam_src[fam_rec_off[f]:fam_rec_off[f+1]]
+    fam_src: np.ndarray = None      # input record index of each family record (family order)
 
 
 def _ptr(a):
     return a.ctypes.data
 
 
-def run(raw, ref, pre=45.0, post=30.0, overlap=True, run_tools=True, threads=0) -> OracleResult:
-    """raw: bsseqconsensusreads_amd.records.RawRecords; ref: records.Reference."""
+def lex_ranks(strings, ids) -> np.ndarray:
+    """rank[id] = byte-order rank of strings[id] over the ids in use (equal strings share a rank)."""
+    ids = np.asarray(ids, np.int64)
+    used = sorted(set(int(i) for i in np.unique(ids[ids >= 0])))
+    rank = np.zeros(max(used[-1] + 1 if used else 1, 1), np.int32)
+    b = {i: (strings[i] if isinstance(strings[i], bytes) else strings[i].encode()) for i in used}
+    r, prev = -1, None
+    for i in sorted(used, key=lambda i: b[i]):
+        if prev is None or b[i] != prev:
+            r += 1
+            prev = b[i]
+        rank[i] = r
+    return rank
+
+
+def run(raw, ref, pre=45.0, post=30.0, overlap=True, run_tools=True, threads=0,
+        family_order="template-coordinate") -> OracleResult:
+    """raw: bsseqconsensusreads_amd.records.RawRecords; ref: records.Reference.
+    family_order: "template-coordinate" (fgbio SortBam + consecutive-MI grouping) or "mi-group"
+    (tool 2's first-seen MI groups)."""
     lib = load()
     keep = []
 
@@ -152,6 +174,9 @@ def run(raw, ref, pre=45.0, post=30.0, overlap=True, run_tools=True, threads=0) 
     rr.mc_off = arr(raw.mc_off, np.int64)
     rr.mc_n = arr(raw.mc_n, np.int32)
     rr.mc_cigar = arr(raw.mc_cigar, np.uint32)
+    rr.mi_lex = arr(lex_ranks(raw.mi_names, raw.mi_id), np.int32)
+    rr.name_lex = arr(lex_ranks(raw.names, raw.name_id), np.int32)
+    rr.lib_id = None
 
     # reference letters: the FASTA's own when kept, else the nt16 letters
     offs, lens, parts, o = [], [], [], 0
@@ -181,7 +206,9 @@ def run(raw, ref, pre=45.0, post=30.0, overlap=True, run_tools=True, threads=0) 
     rf.len = arr(np.asarray(lens, np.int64), np.int64)
     rf.seq = arr(np.concatenate(parts) if parts else np.zeros(1, np.uint8), np.uint8)
 
-    p = _Params(pre, post, 0, int(overlap), int(run_tools), int(threads))
+    if family_order not in ("template-coordinate", "mi-group"):
+        raise ValueError(family_order)
+    p = _Params(pre, post, 0, int(overlap), int(run_tools), int(threads), int(family_order == "template-coordinate"))
     t0 = time.perf_counter()
     h = lib.orc_run(C.byref(rr), C.byref(rf), C.byref(p))
     seconds = time.perf_counter() - t0
@@ -221,9 +248,12 @@ def run(raw, ref, pre=45.0, post=30.0, overlap=True, run_tools=True, threads=0) 
         qs = np.zeros(max(2 * F * stride, 1), np.uint8)
         nr = np.zeros(max(F, 1), np.int32)
         lib.orc_get_consensus(h, stride, _ptr(mi), _ptr(st), _ptr(ln), _ptr(bs), _ptr(qs), _ptr(nr))
+        fro = np.zeros(F + 1, np.int64)
+        fsrc = np.zeros(max(lib.orc_n_records(h, 2), 1), np.int64)
+        lib.orc_get_families(h, _ptr(fro), _ptr(fsrc))
         return OracleResult(outs[0], outs[1], mi[:F], st[:F], ln[:2 * F].reshape(F, 2),
                             _ASCII_NT16[bs[:2 * F * stride]].reshape(F, 2, stride) if F else np.zeros((0, 2, stride), np.uint8),
-                            qs[:2 * F * stride].reshape(F, 2, stride), nr[:F], seconds)
+                            qs[:2 * F * stride].reshape(F, 2, stride), nr[:F], seconds, fro, fsrc[:int(fro[-1])])
     finally:
         lib.orc_free(h)
 

@@ -112,8 +112,8 @@ def test_large_family_kernel(engine, where, monkeypatch):
     raw = synth.messify(s.raw, frac=0.1, seed=2)
     real = batch.build_family_batch
 
-    def forced(r, mode="full", ref=None, small_cap=0):
-        fb = real(r, mode, ref, small_cap=0)
+    def forced(r, mode="full", ref=None, small_cap=0, **kw):
+        fb = real(r, mode, ref, small_cap=0, **kw)
         if where == "global":  # every large family in the last (HBM scratch) bucket
             nb = len(fb.large_buckets)
             fb.large_buckets = [np.zeros((0, 4), np.uint32)] * (nb - 1) + [fb.large_fams]
@@ -143,6 +143,23 @@ def test_vote_only_on_tool2_output(engine):
     cons = pipeline.run_duplex(engine, raw2)
     ref2 = oracle.run(raw2, s.ref, run_tools=False)
     assert_consensus_equal(cons, ref2, "vote-only")
+
+
+def test_split_extension_partner_falls_back(engine):
+    """A tool-2 4-group whose extension partners land in different TemplateCoordinate families
+    (here: one 163 record's stale mate contig changed) runs the tools and callduplex as two
+    launches; the result still equals the restatement's."""
+    s = synth.generate("C0", 400, seed=15, device="cpu", genome_len=100_000)
+    raw = s.raw
+    k = int(np.nonzero(raw.flag == 163)[0][7])
+    raw.next_tid[k] = 1
+    fb = batch.build_family_batch(raw, "full", s.ref)
+    assert fb.split_ext
+    engine.load_reference(s.ref)
+    cons, t2 = pipeline.run_step5(engine, raw, dump=True)
+    ref = oracle.run(raw, s.ref)
+    assert_consensus_equal(cons, ref, "split-fallback")
+    assert np.array_equal(t2.src, ref.tool2.src) and np.array_equal(t2.seq, ref.tool2.seq)
 
 
 def test_empty_and_repeatable(engine):
