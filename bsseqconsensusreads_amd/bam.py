@@ -1,0 +1,379 @@
+"""The file-level step-5 drop-in: BAM in -> duplex consensus BAM out.
+
+The reference's step 5 is four Snakemake rules over files (main.snake.py:121-164): tool 1 and
+tool 2 read and write BAM through pysam, fgbio SortBam writes the TemplateCoordinate-sorted BAM,
+and CallDuplexConsensusReads writes the unmapped consensus pairs.  Here one call reads the input
+BAM (libbsdc_io: BGZF inflated and records parsed in parallel, include/bsdc_io.h), runs the fused
+device path (pipeline.run_step5: tools 1+2, TemplateCoordinate families, vote, duplex), builds
+fgbio's output records and writes them (libbsdc_io: BGZF deflated in
+parallel).
+
+Output records (fgbio DuplexConsensusCaller as restated; PARITY UNPINNED -- fgbio is not
+vendored): an unmapped pair per emitted family, R1 flag 77 and R2 flag 141, name
+``<prefix>:<MI base>``, tags RG:Z:A, MI:Z:<MI base>, RX:Z:<consensus UMI> (when the inputs carry
+RX).  The per-base statistics tags (aD/bD/cD, aM/bM/cM, aE/bE/cE, ad/bd, ae/be, ac/bc, aq/bq) are
+not emitted: the consumer of this file (SamToFastq, main.snake.py:167-177) reads name, flag, SEQ
+and QUAL only.
+"""
+from __future__ import annotations
+
+import ctypes as C
+import os
+from dataclasses import dataclass
+from typing import List, Optional
+
+import numpy as np
+
+from . import records as R
+
+IO_LIB_PATH = os.environ.get("BSDC_IO_LIB_PATH") or os.path.join(os.path.dirname(os.path.abspath(__file__)),
+                                                                 "libbsdc_io.so")
+BSDC_IO_ABI_VERSION = 1
+_P = C.c_void_p
+
+
+class _Sizes(C.Structure):
+    _fields_ = [(k, C.c_int64) for k in ("n_rec", "n_bases", "n_cigar", "n_mc", "aux_bytes", "n_names", "name_bytes",
+                                         "n_mi", "mi_bytes", "header_bytes")] + \
+               [("n_ref", C.c_int32), ("ref_name_bytes", C.c_int64)]
+
+
+class _Arrays(C.Structure):
+    _fields_ = [(k, _P) for k in (
+        "flag", "tid", "pos", "mapq", "l_seq", "seq_off", "seq", "qual", "cig_off", "n_cig", "cigar", "next_tid",
+        "next_pos", "tlen", "name_id", "name_off", "name_buf", "mi_id", "mi_strand", "mi_off", "mi_buf", "mc_off",
+        "mc_n", "mc_cigar", "la", "rd", "aux_off", "aux", "header", "ref_len", "ref_name_off", "ref_name_buf")]
+
+
+class _Records(C.Structure):
+    _fields_ = [("n_rec", C.c_int64)] + [(k, _P) for k in (
+        "flag", "tid", "pos", "mapq", "next_tid", "next_pos", "tlen", "name_off", "name_buf", "cig_off", "cigar",
+        "seq_off", "seq", "qual", "aux_off", "aux")]
+
+
+_lib = None
+
+
+def _load():
+    global _lib
+    if _lib is not None:
+        return _lib
+    if not os.path.exists(IO_LIB_PATH):
+        raise RuntimeError("%s is missing: run __graft_entry__.build()" % IO_LIB_PATH)
+    lib = C.CDLL(IO_LIB_PATH)
+    lib.bsdc_io_abi_version.restype = C.c_int32
+    lib.bsdc_io_last_error.restype = C.c_char_p
+    lib.bsdc_bam_read.argtypes = [C.c_char_p, C.c_int32, C.POINTER(_P)]
+    lib.bsdc_bam_read.restype = C.c_int32
+    lib.bsdc_bam_sizes_of.argtypes = [_P, C.POINTER(_Sizes)]
+    lib.bsdc_bam_copy.argtypes = [_P, C.POINTER(_Arrays)]
+    lib.bsdc_bam_copy.restype = C.c_int32
+    lib.bsdc_bam_free.argtypes = [_P]
+    lib.bsdc_bam_write.argtypes = [C.c_char_p, C.c_char_p, C.c_int64, C.c_int32, _P, _P, _P, C.POINTER(_Records),
+                                   C.c_int32, C.c_int32]
+    lib.bsdc_bam_write.restype = C.c_int32
+    lib.bsdc_rx_consensus.argtypes = [C.c_int64, _P, _P, _P, _P, _P, _P, _P, C.c_int32]
+    lib.bsdc_rx_consensus.restype = C.c_int64
+    if lib.bsdc_io_abi_version() != BSDC_IO_ABI_VERSION:
+        raise RuntimeError("libbsdc_io ABI %d != %d" % (lib.bsdc_io_abi_version(), BSDC_IO_ABI_VERSION))
+    _lib = lib
+    return lib
+
+
+def _ptr(a: np.ndarray):
+    return a.ctypes.data_as(_P)
+
+
+class StringTable:
+    """Strings packed in one buffer (``buf[off[i]:off[i+1]]``); indexing gives bytes (or str)."""
+
+    def __init__(self, buf: np.ndarray, off: np.ndarray, as_str: bool = False):
+        self.buf = np.ascontiguousarray(buf, np.uint8)
+        self.off = np.ascontiguousarray(off, np.int64)
+        self.as_str = as_str
+
+    def __len__(self):
+        return int(self.off.shape[0]) - 1
+
+    def __getitem__(self, i):
+        b = self.buf[int(self.off[i]):int(self.off[i + 1])].tobytes()
+        return b.decode() if self.as_str else b
+
+    @staticmethod
+    def from_list(items) -> "StringTable":
+        bs = [x if isinstance(x, bytes) else str(x).encode() for x in items]
+        off = np.zeros(len(bs) + 1, np.int64)
+        if bs:
+            off[1:] = np.cumsum([len(x) for x in bs])
+        return StringTable(np.frombuffer(b"".join(bs), np.uint8) if bs else np.zeros(0, np.uint8), off,
+                           as_str=bool(items) and isinstance(items[0], str))
+
+    def lex_key(self, ids: np.ndarray) -> np.ndarray:
+        """A key per id ordering the ids as their strings sort in byte order (vectorised)."""
+        ids = np.asarray(ids, np.int64)
+        if ids.shape[0] == 0:
+            return np.zeros(0, np.int64)
+        u, inv = np.unique(ids, return_inverse=True)
+        lens = self.off[u + 1] - self.off[u]
+        w = max(int(lens.max()), 1)
+        j = np.arange(w)[None, :]
+        idx = self.off[u][:, None] + j
+        m = np.where(j < lens[:, None], self.buf[np.minimum(idx, max(self.buf.shape[0] - 1, 0))], 0).astype(np.uint8)
+        fixed = np.ascontiguousarray(m).view("S%d" % w).reshape(-1)
+        _, rk = np.unique(fixed, return_inverse=True)
+        return rk.astype(np.int64)[inv]
+
+
+@dataclass
+class BamHeader:
+    text: str
+    ref_names: List[str]
+    ref_lens: np.ndarray
+
+    def read_groups(self) -> List[dict]:
+        out = []
+        for line in self.text.splitlines():
+            if line.startswith("@RG"):
+                out.append(dict(f.split(":", 1) for f in line.split("\t")[1:] if ":" in f))
+        return out
+
+
+def read_bam(path: str, threads: int = 0):
+    """BAM file -> (BamHeader, records.RawRecords) with MI / MC / LA / RD decoded and the other
+    aux bytes kept (``raw.aux`` is a StringTable of per-record aux blocks)."""
+    lib = _load()
+    h = _P()
+    rc = lib.bsdc_bam_read(path.encode(), int(threads), C.byref(h))
+    if rc != 0:
+        raise OSError("%s: %s" % (path, lib.bsdc_io_last_error().decode()))
+    try:
+        s = _Sizes()
+        lib.bsdc_bam_sizes_of(h, C.byref(s))
+        n = s.n_rec
+
+        def z(k, dt):
+            return np.zeros(max(int(k), 1), dt)
+        A = dict(flag=z(n, np.uint16), tid=z(n, np.int32), pos=z(n, np.int32), mapq=z(n, np.uint8),
+                 l_seq=z(n, np.int32), seq_off=z(n, np.int64), seq=z(s.n_bases, np.uint8), qual=z(s.n_bases, np.uint8),
+                 cig_off=z(n, np.int64), n_cig=z(n, np.int32), cigar=z(s.n_cigar, np.uint32),
+                 next_tid=z(n, np.int32), next_pos=z(n, np.int32), tlen=z(n, np.int32), name_id=z(n, np.int32),
+                 name_off=z(s.n_names + 1, np.int64), name_buf=z(s.name_bytes, np.uint8), mi_id=z(n, np.int32),
+                 mi_strand=z(n, np.int8), mi_off=z(s.n_mi + 1, np.int64), mi_buf=z(s.mi_bytes, np.uint8),
+                 mc_off=z(n, np.int64), mc_n=z(n, np.int32), mc_cigar=z(s.n_mc, np.uint32), la=z(n, np.int32),
+                 rd=z(n, np.int32), aux_off=z(n + 1, np.int64), aux=z(s.aux_bytes, np.uint8),
+                 header=z(s.header_bytes, np.uint8), ref_len=z(s.n_ref, np.int64),
+                 ref_name_off=z(s.n_ref + 1, np.int64), ref_name_buf=z(s.ref_name_bytes, np.uint8))
+        a = _Arrays(**{k: _ptr(v) for k, v in A.items()})
+        if lib.bsdc_bam_copy(h, C.byref(a)) != 0:
+            raise OSError("%s: %s" % (path, lib.bsdc_io_last_error().decode()))
+    finally:
+        lib.bsdc_bam_free(h)
+    names_tab = StringTable(A["ref_name_buf"][:s.ref_name_bytes], A["ref_name_off"][:s.n_ref + 1], as_str=True)
+    header = BamHeader(A["header"][:s.header_bytes].tobytes().decode(errors="replace"),
+                       [names_tab[i] for i in range(s.n_ref)], A["ref_len"][:s.n_ref].copy())
+    raw = R.RawRecords(
+        flag=A["flag"][:n], tid=A["tid"][:n], pos=A["pos"][:n], mapq=A["mapq"][:n], l_seq=A["l_seq"][:n],
+        seq_off=A["seq_off"][:n], seq=A["seq"][:s.n_bases], qual=A["qual"][:s.n_bases], cig_off=A["cig_off"][:n],
+        n_cig=A["n_cig"][:n], cigar=A["cigar"][:s.n_cigar], next_tid=A["next_tid"][:n], next_pos=A["next_pos"][:n],
+        tlen=A["tlen"][:n], name_id=A["name_id"][:n],
+        names=StringTable(A["name_buf"][:s.name_bytes], A["name_off"][:s.n_names + 1]),
+        mi_id=A["mi_id"][:n], mi_strand=A["mi_strand"][:n],
+        mi_names=StringTable(A["mi_buf"][:s.mi_bytes], A["mi_off"][:s.n_mi + 1], as_str=True),
+        mc_off=A["mc_off"][:n], mc_n=A["mc_n"][:n], mc_cigar=A["mc_cigar"][:s.n_mc],
+        aux=StringTable(A["aux"][:s.aux_bytes], A["aux_off"][:n + 1]), la_tag=A["la"][:n], rd_tag=A["rd"][:n])
+    return header, raw
+
+
+def _aux_table(raw: R.RawRecords) -> StringTable:
+    if isinstance(raw.aux, StringTable):
+        return raw.aux
+    if raw.aux is None:
+        return StringTable(np.zeros(0, np.uint8), np.zeros(raw.n + 1, np.int64))
+    return StringTable.from_list(list(raw.aux))
+
+
+@dataclass
+class OutRecordsBam:
+    """Records to write, structure-of-arrays (the bsdc_bam_records layout)."""
+
+    flag: np.ndarray
+    tid: np.ndarray
+    pos: np.ndarray
+    mapq: np.ndarray
+    next_tid: np.ndarray
+    next_pos: np.ndarray
+    tlen: np.ndarray
+    names: StringTable
+    cig_off: np.ndarray     # [n + 1]
+    cigar: np.ndarray
+    seq_off: np.ndarray     # [n + 1]
+    seq: np.ndarray         # nt16 codes
+    qual: np.ndarray
+    aux: StringTable
+
+    @property
+    def n(self) -> int:
+        return int(self.flag.shape[0])
+
+
+def records_to_bam(raw: R.RawRecords) -> OutRecordsBam:
+    """A RawRecords stream as records to write: its own aux bytes, or for synthetic streams
+    (no aux) the MI (with the /A|/B strand) and MC tags rebuilt from the decoded fields."""
+    n = raw.n
+    if raw.aux is not None:
+        aux = _aux_table(raw)
+    else:
+        parts = []
+        for k in range(n):
+            t = []
+            if raw.mi_id[k] >= 0:
+                sfx = {0: "/A", 1: "/B"}.get(int(raw.mi_strand[k]), "")
+                t.append(("MI", "Z", "%s%s" % (raw.mi_names[int(raw.mi_id[k])], sfx)))
+            if raw.mc_off[k] >= 0:
+                mc = raw.mc_cigar[raw.mc_off[k]:raw.mc_off[k] + raw.mc_n[k]]
+                t.append(("MC", "Z", R.cigar_string([int(x) for x in mc])))
+            parts.append(R.encode_aux(t))
+        aux = StringTable.from_list(parts)
+    cig_off = np.zeros(n + 1, np.int64)
+    cig_off[:n] = raw.cig_off
+    cig_off[n] = int(raw.cig_off[-1] + raw.n_cig[-1]) if n else 0
+    seq_off = np.zeros(n + 1, np.int64)
+    seq_off[:n] = raw.seq_off
+    seq_off[n] = int(raw.seq_off[-1] + raw.l_seq[-1]) if n else 0
+    nid = raw.name_id.astype(np.int64)
+    names = raw.names
+    tab = StringTable.from_list([names[int(i)] for i in nid])
+    return OutRecordsBam(raw.flag, raw.tid, raw.pos, raw.mapq, raw.next_tid, raw.next_pos, raw.tlen, tab, cig_off,
+                         raw.cigar, seq_off, raw.seq, raw.qual, aux)
+
+
+def write_bam(path: str, header: BamHeader, recs: OutRecordsBam, level: int = 6, threads: int = 0):
+    lib = _load()
+    rn = StringTable.from_list([x.encode() for x in header.ref_names])
+    keep = []
+
+    def c(x, dt):
+        a = np.ascontiguousarray(x, dtype=dt)
+        if a.size == 0:
+            a = np.zeros(1, dt)
+        keep.append(a)
+        return _ptr(a)
+    r = _Records(recs.n, c(recs.flag, np.uint16), c(recs.tid, np.int32), c(recs.pos, np.int32), c(recs.mapq, np.uint8),
+                 c(recs.next_tid, np.int32), c(recs.next_pos, np.int32), c(recs.tlen, np.int32),
+                 c(recs.names.off, np.int64), c(recs.names.buf, np.uint8), c(recs.cig_off, np.int64),
+                 c(recs.cigar, np.uint32), c(recs.seq_off, np.int64), c(recs.seq, np.uint8), c(recs.qual, np.uint8),
+                 c(recs.aux.off, np.int64), c(recs.aux.buf, np.uint8))
+    text = header.text.encode()
+    rc = lib.bsdc_bam_write(path.encode(), text, len(text), len(header.ref_names), c(rn.off, np.int64),
+                            c(rn.buf, np.uint8), c(np.asarray(header.ref_lens, np.int64), np.int64), C.byref(r),
+                            int(level), int(threads))
+    if rc != 0:
+        raise OSError("%s: %s" % (path, lib.bsdc_io_last_error().decode()))
+
+
+def read_fasta(path: str, header: BamHeader) -> R.Reference:
+    """FASTA -> the packed reference in the BAM header's tid order (contigs the FASTA lacks are
+    absent: tool 1 then converts against N, tools/1.convert_AG_to_CT.py:103-117)."""
+    data = np.fromfile(path, dtype=np.uint8)
+    starts = np.nonzero(data == ord(">"))[0]
+    starts = starts[(starts == 0) | (data[np.maximum(starts - 1, 0)] == ord("\n"))]
+    contigs = {}
+    for i, s0 in enumerate(starts):
+        e = int(starts[i + 1]) if i + 1 < len(starts) else data.shape[0]
+        nl = s0 + int(np.argmax(data[s0:e] == ord("\n"))) if (data[s0:e] == ord("\n")).any() else e
+        name = data[s0 + 1:nl].tobytes().decode().split()[0]
+        body = data[nl:e]
+        body = body[(body != ord("\n")) & (body != ord("\r"))]
+        contigs[name] = body.tobytes()
+    return R.Reference.from_contigs(header.ref_names, {k: v for k, v in contigs.items()}, keep_letters=False,
+                                    header_lengths=list(header.ref_lens))
+
+
+def read_name_prefix(header: BamHeader) -> str:
+    """fgbio's default consensus read-name prefix (restated, parity unpinned): the input read
+    groups' libraries (or IDs), distinct, sorted, joined by '|'."""
+    ids = sorted({rg.get("LB", rg.get("ID", "")) for rg in header.read_groups()})
+    return "|".join(ids)
+
+
+def output_header(header: BamHeader) -> BamHeader:
+    """fgbio's consensus header (restated): unsorted/query-grouped, the input's @SQ lines, one
+    read group A carrying the input's sample and library when they are unique."""
+    rgs = header.read_groups()
+    rg = ["@RG", "ID:A"]
+    for key in ("SM", "LB"):
+        vals = sorted({g[key] for g in rgs if key in g})
+        if len(vals) == 1:
+            rg.append("%s:%s" % (key, vals[0]))
+    lines = ["@HD\tVN:1.6\tSO:unsorted\tGO:query"]
+    lines += [ln for ln in header.text.splitlines() if ln.startswith("@SQ")]
+    lines += ["\t".join(rg), "@PG\tID:bsseqconsensusreads_amd\tPN:bsseqconsensusreads_amd\tCL:step5"]
+    return BamHeader("\n".join(lines) + "\n", list(header.ref_names), np.asarray(header.ref_lens, np.int64))
+
+
+def duplex_records(cons, raw: R.RawRecords, prefix: str, threads: int = 0) -> OutRecordsBam:
+    """fgbio duplex output records for the emitted families of `cons`
+    (pipeline.Consensus, family order): R1 then R2 per family."""
+    lib = _load()
+    em = np.nonzero((cons.status & 1) != 0)[0]
+    F = em.shape[0]
+    n = 2 * F
+    # consensus UMI per family from its records' RX (libbsdc_io)
+    aux = _aux_table(raw)
+    fro = np.ascontiguousarray(cons.fam_rec_off, np.int64)
+    fsrc = np.ascontiguousarray(cons.fam_src, np.int64)
+    strand = np.ascontiguousarray(raw.mi_strand, np.int8)
+    nf_all = int(fro.shape[0]) - 1
+    width = lib.bsdc_rx_consensus(nf_all, _ptr(fro), _ptr(fsrc), _ptr(strand), _ptr(aux.off),
+                                  _ptr(aux.buf if aux.buf.size else np.zeros(1, np.uint8)), None, None, int(threads))
+    rx = np.zeros(max(nf_all * max(width, 1), 1), np.uint8)
+    rx_len = np.zeros(max(nf_all, 1), np.int32)
+    if width > 0:
+        lib.bsdc_rx_consensus(nf_all, _ptr(fro), _ptr(fsrc), _ptr(strand), _ptr(aux.off), _ptr(aux.buf), _ptr(rx),
+                              _ptr(rx_len), int(threads))
+    mi_names = raw.mi_names
+    pre = (prefix + ":").encode()
+    names, auxs = [], []
+    for f in em:
+        mi = mi_names[int(cons.fam_mi[f])]
+        mi = mi if isinstance(mi, bytes) else mi.encode()
+        nm = pre + mi
+        a = b"RGZA\0MIZ" + mi + b"\0"
+        if width > 0 and rx_len[f] > 0:
+            a += b"RXZ" + rx[f * width:f * width + rx_len[f]].tobytes() + b"\0"
+        names += [nm, nm]
+        auxs += [a, a]
+    L = cons.length[em].astype(np.int64).reshape(-1)            # R1, R2, R1, R2 ...
+    seq_off = np.zeros(n + 1, np.int64)
+    seq_off[1:] = np.cumsum(L)
+    stride = cons.seq.shape[2]
+    flat = (np.repeat(em, 2) * 2 + np.tile([0, 1], F)) * stride  # row of (family, end)
+    idx = np.repeat(flat - seq_off[:-1], L) + np.arange(int(L.sum()), dtype=np.int64)
+    seq = cons.seq.reshape(-1)[idx]
+    qual = cons.qual.reshape(-1)[idx]
+    return OutRecordsBam(
+        flag=np.tile(np.asarray([77, 141], np.uint16), F), tid=np.full(n, -1, np.int32), pos=np.full(n, -1, np.int32),
+        mapq=np.zeros(n, np.uint8), next_tid=np.full(n, -1, np.int32), next_pos=np.full(n, -1, np.int32),
+        tlen=np.zeros(n, np.int32), names=StringTable.from_list(names), cig_off=np.zeros(n + 1, np.int64),
+        cigar=np.zeros(0, np.uint32), seq_off=seq_off, seq=seq, qual=qual, aux=StringTable.from_list(auxs))
+
+
+def step5(in_bam: str, fasta: str, out_bam: str, engine=None, prefix: Optional[str] = None, threads: int = 0,
+          level: int = 6) -> dict:
+    """Rules convert_Bstrain .. callduplex (main.snake.py:121-164) as one call on files."""
+    from . import pipeline
+    from .device import Engine
+    header, raw = read_bam(in_bam, threads)
+    ref = read_fasta(fasta, header)
+    own = engine is None
+    eng = Engine(0) if own else engine
+    try:
+        eng.load_reference(ref)
+        cons, _ = pipeline.run_step5(eng, raw)
+    finally:
+        if own:
+            eng.close()
+    recs = duplex_records(cons, raw, read_name_prefix(header) if prefix is None else prefix, threads)
+    write_bam(out_bam, output_header(header), recs, level, threads)
+    return {"records_in": raw.n, "families": int(cons.status.shape[0]),
+            "families_emitted": int(((cons.status & 1) != 0).sum()), "records_out": recs.n}

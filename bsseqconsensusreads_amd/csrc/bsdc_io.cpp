@@ -1,0 +1,659 @@
+// bsdc_io.cpp -- BAM/BGZF codec for the step-5 drop-in (include/bsdc_io.h).
+//
+// Reader: the file is read whole, its BGZF blocks are located by one scan of the block headers
+// (BSIZE in the BC extra field), inflated in parallel straight into one buffer at their
+// uncompressed offsets (raw deflate, CRC32 checked), then the records are found by one scan of
+// block_size words and parsed in parallel into structure-of-arrays.  QNAMEs and MI bases are
+// interned sequentially (hash maps over views into the buffer).
+// Writer: record sizes -> prefix sums -> parallel encode into one buffer -> 0xff00-byte BGZF
+// blocks deflated in parallel -> one write, then the 28-byte EOF block.
+#include "../../include/bsdc_io.h"
+
+#include <zlib.h>
+
+#include <algorithm>
+#include <cstdio>
+#include <cstdlib>
+#include <cstring>
+#include <string>
+#include <string_view>
+#include <unordered_map>
+#include <vector>
+#ifdef _OPENMP
+#include <omp.h>
+#endif
+
+namespace {
+
+thread_local std::string g_err;
+
+int fail(int code, const std::string &msg) {
+    g_err = msg;
+    return code;
+}
+
+inline uint16_t rd16(const uint8_t *p) { return (uint16_t)(p[0] | (p[1] << 8)); }
+inline uint32_t rd32(const uint8_t *p) { return (uint32_t)p[0] | ((uint32_t)p[1] << 8) | ((uint32_t)p[2] << 16) | ((uint32_t)p[3] << 24); }
+inline int32_t rdi32(const uint8_t *p) { return (int32_t)rd32(p); }
+inline void wr16(uint8_t *p, uint16_t v) {
+    p[0] = (uint8_t)v;
+    p[1] = (uint8_t)(v >> 8);
+}
+inline void wr32(uint8_t *p, uint32_t v) {
+    for (int i = 0; i < 4; i++) p[i] = (uint8_t)(v >> (8 * i));
+}
+
+void set_threads(int n) {
+#ifdef _OPENMP
+    if (n > 0) omp_set_num_threads(n);
+#else
+    (void)n;
+#endif
+}
+
+const char kCigarOps[] = "MIDNSHP=X";
+
+// aux field size past the 3-byte tag+type header, or -1 if malformed
+int64_t aux_value_size(const uint8_t *p, const uint8_t *end) {
+    const char t = (char)p[2];
+    const uint8_t *v = p + 3;
+    switch (t) {
+    case 'A': case 'c': case 'C': return 1;
+    case 's': case 'S': return 2;
+    case 'i': case 'I': case 'f': return 4;
+    case 'Z': case 'H': {
+        const uint8_t *z = (const uint8_t *)memchr(v, 0, (size_t)(end - v));
+        return z ? (int64_t)(z - v) + 1 : -1;
+    }
+    case 'B': {
+        if (end - v < 5) return -1;
+        const char sub = (char)v[0];
+        const int64_t cnt = rd32(v + 1);
+        const int w = (sub == 'c' || sub == 'C') ? 1 : (sub == 's' || sub == 'S') ? 2 : 4;
+        return 5 + cnt * w;
+    }
+    default: return -1;
+    }
+}
+
+int64_t aux_int(const uint8_t *p) {
+    const uint8_t *v = p + 3;
+    switch ((char)p[2]) {
+    case 'c': return (int8_t)v[0];
+    case 'C': return v[0];
+    case 's': return (int16_t)rd16(v);
+    case 'S': return rd16(v);
+    case 'i': return rdi32(v);
+    case 'I': return rd32(v);
+    default: return -1;
+    }
+}
+
+}  // namespace
+
+struct bsdc_bam {
+    std::vector<uint8_t> data;  // the uncompressed stream
+    std::string header;
+    std::vector<std::string> ref_names;
+    std::vector<int64_t> ref_len;
+    std::vector<int64_t> rec_start;  // offset of each record's block_size word
+    // parsed
+    std::vector<int32_t> name_id, mi_id;
+    std::vector<int8_t> mi_strand;
+    std::vector<std::string_view> names, mis;
+    std::vector<int32_t> la, rd;
+    std::vector<int64_t> mc_tag_off;  // offset of the MC string in data, -1 = none
+    std::vector<int32_t> mc_n;
+    int64_t n_bases = 0, n_cigar = 0, n_mc = 0, aux_bytes = 0;
+};
+
+extern "C" {
+
+int32_t bsdc_io_abi_version(void) { return BSDC_IO_ABI_VERSION; }
+const char *bsdc_io_last_error(void) { return g_err.c_str(); }
+
+int32_t bsdc_bam_read(const char *path, int32_t n_threads, bsdc_bam **out) {
+    *out = nullptr;
+    set_threads(n_threads);
+    FILE *f = fopen(path, "rb");
+    if (!f) return fail(BSDC_IO_EIO, std::string("cannot open ") + path);
+    std::vector<uint8_t> comp;
+    {
+        fseek(f, 0, SEEK_END);
+        const long sz = ftell(f);
+        fseek(f, 0, SEEK_SET);
+        comp.resize(sz > 0 ? (size_t)sz : 0);
+        if (sz > 0 && fread(comp.data(), 1, comp.size(), f) != comp.size()) {
+            fclose(f);
+            return fail(BSDC_IO_EIO, std::string("short read on ") + path);
+        }
+        fclose(f);
+    }
+    // ---- BGZF blocks ----
+    std::vector<int64_t> boff, bsz, uoff;
+    int64_t o = 0, u = 0;
+    const int64_t n = (int64_t)comp.size();
+    while (o < n) {
+        const uint8_t *h = comp.data() + o;
+        if (n - o < 18 || h[0] != 31 || h[1] != 139 || h[2] != 8 || !(h[3] & 4))
+            return fail(BSDC_IO_EFORMAT, "not a BGZF file (bad block header)");
+        const int xlen = rd16(h + 10);
+        int64_t bsize = -1;
+        for (int x = 0; x + 4 <= xlen;) {
+            const uint8_t *sf = h + 12 + x;
+            const int slen = rd16(sf + 2);
+            if (sf[0] == 'B' && sf[1] == 'C' && slen == 2) bsize = rd16(sf + 4) + 1;
+            x += 4 + slen;
+        }
+        if (bsize < 0 || o + bsize > n) return fail(BSDC_IO_EFORMAT, "truncated BGZF block");
+        boff.push_back(o);
+        bsz.push_back(bsize);
+        uoff.push_back(u);
+        u += rd32(h + bsize - 4);
+        o += bsize;
+    }
+    auto *b = new bsdc_bam();
+    b->data.resize((size_t)u + 8);
+    const int64_t nb = (int64_t)boff.size();
+    int bad = 0;
+#pragma omp parallel for schedule(dynamic, 16) reduction(| : bad)
+    for (int64_t i = 0; i < nb; i++) {
+        const uint8_t *h = comp.data() + boff[i];
+        const int xlen = rd16(h + 10);
+        const uint8_t *cdata = h + 12 + xlen;
+        const int64_t clen = bsz[i] - 12 - xlen - 8;
+        const uint32_t isize = rd32(h + bsz[i] - 4), crc = rd32(h + bsz[i] - 8);
+        if (isize == 0) continue;
+        z_stream zs;
+        memset(&zs, 0, sizeof zs);
+        if (inflateInit2(&zs, -15) != Z_OK) {
+            bad |= 1;
+            continue;
+        }
+        zs.next_in = const_cast<uint8_t *>(cdata);
+        zs.avail_in = (uInt)clen;
+        zs.next_out = b->data.data() + uoff[i];
+        zs.avail_out = isize;
+        const int rc = inflate(&zs, Z_FINISH);
+        inflateEnd(&zs);
+        if (rc != Z_STREAM_END || zs.total_out != isize ||
+            crc32(0L, b->data.data() + uoff[i], isize) != crc)
+            bad |= 1;
+    }
+    if (bad) {
+        delete b;
+        return fail(BSDC_IO_EFORMAT, "corrupt BGZF block (inflate or CRC32)");
+    }
+    // ---- header ----
+    const uint8_t *d = b->data.data();
+    const int64_t dn = u;
+    if (dn < 12 || memcmp(d, "BAM\1", 4) != 0) {
+        delete b;
+        return fail(BSDC_IO_EFORMAT, "missing BAM magic");
+    }
+    int64_t p = 4;
+    const int64_t l_text = rd32(d + p);
+    p += 4;
+    if (p + l_text + 4 > dn) {
+        delete b;
+        return fail(BSDC_IO_EFORMAT, "truncated BAM header");
+    }
+    b->header.assign((const char *)d + p, (size_t)l_text);
+    b->header.resize(strnlen(b->header.c_str(), b->header.size()));
+    p += l_text;
+    const int32_t n_ref = rdi32(d + p);
+    p += 4;
+    for (int32_t i = 0; i < n_ref; i++) {
+        if (p + 4 > dn) break;
+        const int32_t ln = rdi32(d + p);
+        p += 4;
+        if (ln < 1 || p + ln + 4 > dn) {
+            delete b;
+            return fail(BSDC_IO_EFORMAT, "truncated reference list");
+        }
+        b->ref_names.emplace_back((const char *)d + p, (size_t)ln - 1);
+        p += ln;
+        b->ref_len.push_back(rd32(d + p));
+        p += 4;
+    }
+    // ---- record boundaries ----
+    while (p + 4 <= dn) {
+        const int64_t bs = rd32(d + p);
+        if (bs < 32 || p + 4 + bs > dn) {
+            delete b;
+            return fail(BSDC_IO_EFORMAT, "truncated BAM record");
+        }
+        b->rec_start.push_back(p);
+        p += 4 + bs;
+    }
+    const int64_t nr = (int64_t)b->rec_start.size();
+    // ---- per record: tags, sizes ----
+    b->la.assign(nr, -1);
+    b->rd.assign(nr, -1);
+    b->mc_tag_off.assign(nr, -1);
+    b->mc_n.assign(nr, 0);
+    std::vector<std::string_view> mi_full(nr);
+    int64_t nbases = 0, ncig = 0, nmc = 0, naux = 0;
+    int badrec = 0;
+#pragma omp parallel for schedule(static) reduction(+ : nbases, ncig, nmc, naux) reduction(| : badrec)
+    for (int64_t k = 0; k < nr; k++) {
+        const uint8_t *r = d + b->rec_start[k];
+        const int64_t bs = rd32(r);
+        const uint8_t *end = r + 4 + bs;
+        const int l_name = r[12];
+        const int n_cig = rd16(r + 16);
+        const int32_t l_seq = rdi32(r + 20);
+        const uint8_t *aux = r + 36 + l_name + 4 * n_cig + (l_seq + 1) / 2 + l_seq;
+        if (l_seq < 0 || aux > end) {
+            badrec |= 1;
+            continue;
+        }
+        nbases += l_seq;
+        ncig += n_cig;
+        naux += end - aux;
+        for (const uint8_t *a = aux; a + 3 <= end;) {
+            const int64_t vs = aux_value_size(a, end);
+            if (vs < 0 || a + 3 + vs > end) {
+                badrec |= 1;
+                break;
+            }
+            if (a[0] == 'M' && a[1] == 'I' && a[2] == 'Z') {
+                mi_full[k] = std::string_view((const char *)a + 3, (size_t)vs - 1);
+            } else if (a[0] == 'M' && a[1] == 'C' && a[2] == 'Z') {
+                const char *s = (const char *)a + 3;
+                if (!(vs == 2 && s[0] == '*')) {
+                    int cnt = 0;
+                    for (int64_t i = 0; i < vs - 1; i++) cnt += strchr(kCigarOps, s[i]) != nullptr && !(s[i] >= '0' && s[i] <= '9');
+                    b->mc_tag_off[k] = (int64_t)((const uint8_t *)s - d);
+                    b->mc_n[k] = cnt;
+                    nmc += cnt;
+                }
+            } else if (a[0] == 'L' && a[1] == 'A') {
+                b->la[k] = (int32_t)aux_int(a);
+            } else if (a[0] == 'R' && a[1] == 'D') {
+                b->rd[k] = (int32_t)aux_int(a);
+            }
+            a += 3 + vs;
+        }
+    }
+    if (badrec) {
+        delete b;
+        return fail(BSDC_IO_EFORMAT, "malformed BAM record (lengths or aux)");
+    }
+    b->n_bases = nbases;
+    b->n_cigar = ncig;
+    b->n_mc = nmc;
+    b->aux_bytes = naux;
+    // ---- interning (sequential): QNAME, MI base = MI up to the first '/' ----
+    b->name_id.resize(nr);
+    b->mi_id.resize(nr);
+    b->mi_strand.resize(nr);
+    std::unordered_map<std::string_view, int32_t> nmap, mmap;
+    nmap.reserve((size_t)nr);
+    mmap.reserve((size_t)nr / 2 + 1);
+    for (int64_t k = 0; k < nr; k++) {
+        const uint8_t *r = d + b->rec_start[k];
+        const int l_name = r[12];
+        std::string_view nm((const char *)r + 36, l_name > 0 ? (size_t)l_name - 1 : 0);
+        auto it = nmap.emplace(nm, (int32_t)b->names.size());
+        if (it.second) b->names.push_back(nm);
+        b->name_id[k] = it.first->second;
+        const std::string_view mi = mi_full[k];
+        if (mi.empty()) {
+            b->mi_id[k] = -1;
+            b->mi_strand[k] = -1;
+            continue;
+        }
+        const size_t slash = mi.find('/');
+        const std::string_view key = slash == std::string_view::npos ? mi : mi.substr(0, slash);
+        auto jt = mmap.emplace(key, (int32_t)b->mis.size());
+        if (jt.second) b->mis.push_back(key);
+        b->mi_id[k] = jt.first->second;
+        const size_t L = mi.size();
+        b->mi_strand[k] = (L >= 2 && mi[L - 2] == '/' && mi[L - 1] == 'A') ? 0
+                          : (L >= 2 && mi[L - 2] == '/' && mi[L - 1] == 'B') ? 1 : -1;
+    }
+    *out = b;
+    return 0;
+}
+
+void bsdc_bam_sizes_of(const bsdc_bam *b, bsdc_bam_sizes *s) {
+    memset(s, 0, sizeof *s);
+    s->n_rec = (int64_t)b->rec_start.size();
+    s->n_bases = b->n_bases;
+    s->n_cigar = b->n_cigar;
+    s->n_mc = b->n_mc;
+    s->aux_bytes = b->aux_bytes;
+    s->n_names = (int64_t)b->names.size();
+    for (auto &x : b->names) s->name_bytes += (int64_t)x.size();
+    s->n_mi = (int64_t)b->mis.size();
+    for (auto &x : b->mis) s->mi_bytes += (int64_t)x.size();
+    s->header_bytes = (int64_t)b->header.size();
+    s->n_ref = (int32_t)b->ref_names.size();
+    for (auto &x : b->ref_names) s->ref_name_bytes += (int64_t)x.size();
+}
+
+int32_t bsdc_bam_copy(const bsdc_bam *b, const bsdc_bam_arrays *a) {
+    const int64_t nr = (int64_t)b->rec_start.size();
+    const uint8_t *d = b->data.data();
+    // running offsets (sequential prefix sums)
+    std::vector<int64_t> so(nr + 1), co(nr + 1), ao(nr + 1), mo(nr + 1);
+    for (int64_t k = 0; k < nr; k++) {
+        const uint8_t *r = d + b->rec_start[k];
+        const int64_t bs = rd32(r);
+        const int l_name = r[12];
+        const int n_cig = rd16(r + 16);
+        const int32_t l_seq = rdi32(r + 20);
+        const int64_t auxlen = 4 + bs - (36 + l_name + 4 * n_cig + (l_seq + 1) / 2 + l_seq);
+        so[k + 1] = so[k] + l_seq;
+        co[k + 1] = co[k] + n_cig;
+        ao[k + 1] = ao[k] + auxlen;
+        mo[k + 1] = mo[k] + b->mc_n[k];
+    }
+#pragma omp parallel for schedule(static)
+    for (int64_t k = 0; k < nr; k++) {
+        const uint8_t *r = d + b->rec_start[k];
+        const int64_t bs = rd32(r);
+        const int l_name = r[12];
+        const int n_cig = rd16(r + 16);
+        const int32_t l_seq = rdi32(r + 20);
+        a->tid[k] = rdi32(r + 4);
+        a->pos[k] = rdi32(r + 8);
+        a->mapq[k] = r[13];
+        a->flag[k] = rd16(r + 18);
+        a->l_seq[k] = l_seq;
+        a->next_tid[k] = rdi32(r + 24);
+        a->next_pos[k] = rdi32(r + 28);
+        a->tlen[k] = rdi32(r + 32);
+        a->seq_off[k] = so[k];
+        a->cig_off[k] = co[k];
+        a->n_cig[k] = n_cig;
+        const uint8_t *c = r + 36 + l_name;
+        for (int i = 0; i < n_cig; i++) a->cigar[co[k] + i] = rd32(c + 4 * i);
+        const uint8_t *sq = c + 4 * n_cig;
+        uint8_t *dst = a->seq + so[k];
+        for (int32_t i = 0; i < l_seq; i++) dst[i] = (i & 1) ? (sq[i >> 1] & 0xF) : (sq[i >> 1] >> 4);
+        memcpy(a->qual + so[k], sq + (l_seq + 1) / 2, (size_t)l_seq);
+        const uint8_t *aux = sq + (l_seq + 1) / 2 + l_seq;
+        memcpy(a->aux + ao[k], aux, (size_t)(ao[k + 1] - ao[k]));
+        a->aux_off[k] = ao[k];
+        a->name_id[k] = b->name_id[k];
+        a->mi_id[k] = b->mi_id[k];
+        a->mi_strand[k] = b->mi_strand[k];
+        a->la[k] = b->la[k];
+        a->rd[k] = b->rd[k];
+        a->mc_n[k] = b->mc_n[k];
+        a->mc_off[k] = b->mc_tag_off[k] >= 0 ? mo[k] : -1;
+        if (b->mc_tag_off[k] >= 0) {
+            const char *s = (const char *)d + b->mc_tag_off[k];
+            int64_t w = mo[k];
+            uint32_t num = 0;
+            for (; *s; s++) {
+                if (*s >= '0' && *s <= '9') {
+                    num = num * 10 + (uint32_t)(*s - '0');
+                } else {
+                    const char *q = strchr(kCigarOps, *s);
+                    if (q) a->mc_cigar[w++] = (num << 4) | (uint32_t)(q - kCigarOps);
+                    num = 0;
+                }
+            }
+        }
+        (void)bs;
+    }
+    a->aux_off[nr] = ao[nr];
+    int64_t o = 0;
+    for (size_t i = 0; i < b->names.size(); i++) {
+        a->name_off[i] = o;
+        memcpy(a->name_buf + o, b->names[i].data(), b->names[i].size());
+        o += (int64_t)b->names[i].size();
+    }
+    a->name_off[b->names.size()] = o;
+    o = 0;
+    for (size_t i = 0; i < b->mis.size(); i++) {
+        a->mi_off[i] = o;
+        memcpy(a->mi_buf + o, b->mis[i].data(), b->mis[i].size());
+        o += (int64_t)b->mis[i].size();
+    }
+    a->mi_off[b->mis.size()] = o;
+    memcpy(a->header, b->header.data(), b->header.size());
+    o = 0;
+    for (size_t i = 0; i < b->ref_names.size(); i++) {
+        a->ref_len[i] = b->ref_len[i];
+        a->ref_name_off[i] = o;
+        memcpy(a->ref_name_buf + o, b->ref_names[i].data(), b->ref_names[i].size());
+        o += (int64_t)b->ref_names[i].size();
+    }
+    a->ref_name_off[b->ref_names.size()] = o;
+    return 0;
+}
+
+void bsdc_bam_free(bsdc_bam *b) { delete b; }
+
+}  // extern "C"
+
+namespace {
+// SAM spec reg2bin (0-based, end exclusive)
+int reg2bin(int64_t beg, int64_t end) {
+    --end;
+    if (beg >> 14 == end >> 14) return (int)(((1 << 15) - 1) / 7 + (beg >> 14));
+    if (beg >> 17 == end >> 17) return (int)(((1 << 12) - 1) / 7 + (beg >> 17));
+    if (beg >> 20 == end >> 20) return (int)(((1 << 9) - 1) / 7 + (beg >> 20));
+    if (beg >> 23 == end >> 23) return (int)(((1 << 6) - 1) / 7 + (beg >> 23));
+    if (beg >> 26 == end >> 26) return (int)(((1 << 3) - 1) / 7 + (beg >> 26));
+    return 0;
+}
+constexpr int64_t kBlock = 0xff00;  // uncompressed bytes per BGZF block (htslib's size)
+}  // namespace
+
+extern "C" int32_t bsdc_bam_write(const char *path, const char *header_text, int64_t header_len, int32_t n_ref,
+                                  const int64_t *ref_name_off, const char *ref_name_buf, const int64_t *ref_len,
+                                  const bsdc_bam_records *r, int32_t level, int32_t n_threads) {
+    set_threads(n_threads);
+    const int64_t nr = r->n_rec;
+    // ---- header bytes ----
+    std::vector<uint8_t> head;
+    auto put32 = [&](uint32_t v) {
+        uint8_t t[4];
+        wr32(t, v);
+        head.insert(head.end(), t, t + 4);
+    };
+    head.insert(head.end(), {'B', 'A', 'M', 1});
+    put32((uint32_t)header_len);
+    head.insert(head.end(), header_text, header_text + header_len);
+    put32((uint32_t)n_ref);
+    for (int32_t i = 0; i < n_ref; i++) {
+        const int64_t l = ref_name_off[i + 1] - ref_name_off[i];
+        put32((uint32_t)(l + 1));
+        head.insert(head.end(), ref_name_buf + ref_name_off[i], ref_name_buf + ref_name_off[i] + l);
+        head.push_back(0);
+        put32((uint32_t)ref_len[i]);
+    }
+    // ---- record sizes, offsets ----
+    std::vector<int64_t> off(nr + 1);
+    off[0] = (int64_t)head.size();
+    for (int64_t k = 0; k < nr; k++) {
+        const int64_t l_name = r->name_off[k + 1] - r->name_off[k] + 1;
+        const int64_t n_cig = r->cig_off[k + 1] - r->cig_off[k];
+        const int64_t l_seq = r->seq_off[k + 1] - r->seq_off[k];
+        const int64_t l_aux = r->aux_off[k + 1] - r->aux_off[k];
+        if (l_name > 254 || n_cig > 0xFFFF) return fail(BSDC_IO_EFORMAT, "record name or cigar too long for BAM");
+        off[k + 1] = off[k] + 4 + 32 + l_name + 4 * n_cig + (l_seq + 1) / 2 + l_seq + l_aux;
+    }
+    std::vector<uint8_t> buf((size_t)off[nr]);
+    memcpy(buf.data(), head.data(), head.size());
+#pragma omp parallel for schedule(static)
+    for (int64_t k = 0; k < nr; k++) {
+        uint8_t *p = buf.data() + off[k];
+        const int64_t l_name = r->name_off[k + 1] - r->name_off[k] + 1;
+        const int64_t n_cig = r->cig_off[k + 1] - r->cig_off[k];
+        const int64_t l_seq = r->seq_off[k + 1] - r->seq_off[k];
+        const int64_t l_aux = r->aux_off[k + 1] - r->aux_off[k];
+        const uint32_t *cg = r->cigar + r->cig_off[k];
+        int64_t reflen = 0;
+        for (int64_t i = 0; i < n_cig; i++) {
+            const uint32_t op = cg[i] & 0xF;
+            if (op == 0 || op == 2 || op == 3 || op == 7 || op == 8) reflen += cg[i] >> 4;
+        }
+        const int64_t pos = r->pos[k];
+        const int bin = pos < 0 ? 4680 : reg2bin(pos, pos + (reflen > 0 ? reflen : 1));
+        wr32(p, (uint32_t)(off[k + 1] - off[k] - 4));
+        wr32(p + 4, (uint32_t)r->tid[k]);
+        wr32(p + 8, (uint32_t)pos);
+        p[12] = (uint8_t)l_name;
+        p[13] = r->mapq[k];
+        wr16(p + 14, (uint16_t)bin);
+        wr16(p + 16, (uint16_t)n_cig);
+        wr16(p + 18, r->flag[k]);
+        wr32(p + 20, (uint32_t)l_seq);
+        wr32(p + 24, (uint32_t)r->next_tid[k]);
+        wr32(p + 28, (uint32_t)r->next_pos[k]);
+        wr32(p + 32, (uint32_t)r->tlen[k]);
+        uint8_t *q = p + 36;
+        memcpy(q, r->name_buf + r->name_off[k], (size_t)(l_name - 1));
+        q[l_name - 1] = 0;
+        q += l_name;
+        for (int64_t i = 0; i < n_cig; i++) wr32(q + 4 * i, cg[i]);
+        q += 4 * n_cig;
+        const uint8_t *s = r->seq + r->seq_off[k];
+        for (int64_t i = 0; i < l_seq; i += 2) q[i >> 1] = (uint8_t)((s[i] << 4) | (i + 1 < l_seq ? s[i + 1] : 0));
+        q += (l_seq + 1) / 2;
+        memcpy(q, r->qual + r->seq_off[k], (size_t)l_seq);
+        q += l_seq;
+        memcpy(q, r->aux + r->aux_off[k], (size_t)l_aux);
+    }
+    // ---- BGZF ----
+    const int64_t total = (int64_t)buf.size();
+    const int64_t nb = (total + kBlock - 1) / kBlock;
+    std::vector<std::vector<uint8_t>> blocks((size_t)nb);
+    int bad = 0;
+#pragma omp parallel for schedule(dynamic, 4) reduction(| : bad)
+    for (int64_t i = 0; i < nb; i++) {
+        const uint8_t *src = buf.data() + i * kBlock;
+        const int64_t len = std::min(kBlock, total - i * kBlock);
+        std::vector<uint8_t> &o = blocks[(size_t)i];
+        o.resize(18 + (size_t)compressBound((uLong)len) + 8 + 64);
+        z_stream zs;
+        memset(&zs, 0, sizeof zs);
+        int lv = level;
+        for (int attempt = 0; attempt < 2; attempt++) {
+            if (deflateInit2(&zs, lv, Z_DEFLATED, -15, 8, Z_DEFAULT_STRATEGY) != Z_OK) {
+                bad |= 1;
+                break;
+            }
+            zs.next_in = const_cast<uint8_t *>(src);
+            zs.avail_in = (uInt)len;
+            zs.next_out = o.data() + 18;
+            zs.avail_out = (uInt)(o.size() - 26);
+            const int rc = deflate(&zs, Z_FINISH);
+            deflateEnd(&zs);
+            if (rc != Z_STREAM_END) {
+                bad |= 1;
+                break;
+            }
+            if (18 + zs.total_out + 8 <= 65536) break;
+            lv = 0;  // incompressible: store
+            memset(&zs, 0, sizeof zs);
+        }
+        const int64_t bsize = 18 + (int64_t)zs.total_out + 8;
+        uint8_t *h = o.data();
+        const uint8_t hdr[16] = {31, 139, 8, 4, 0, 0, 0, 0, 0, 255, 6, 0, 'B', 'C', 2, 0};
+        memcpy(h, hdr, 16);
+        wr16(h + 16, (uint16_t)(bsize - 1));
+        wr32(h + 18 + zs.total_out, (uint32_t)crc32(0L, src, (uInt)len));
+        wr32(h + 18 + zs.total_out + 4, (uint32_t)len);
+        o.resize((size_t)bsize);
+    }
+    if (bad) return fail(BSDC_IO_EFORMAT, "deflate failed");
+    FILE *f = fopen(path, "wb");
+    if (!f) return fail(BSDC_IO_EIO, std::string("cannot create ") + path);
+    for (auto &bk : blocks)
+        if (fwrite(bk.data(), 1, bk.size(), f) != bk.size()) {
+            fclose(f);
+            return fail(BSDC_IO_EIO, std::string("write failed on ") + path);
+        }
+    static const uint8_t eof[28] = {31, 139, 8, 4, 0, 0, 0, 0, 0, 255, 6, 0, 66, 67, 2, 0, 27, 0, 3, 0, 0, 0, 0, 0, 0, 0, 0, 0};
+    if (fwrite(eof, 1, 28, f) != 28 || fclose(f) != 0) return fail(BSDC_IO_EIO, std::string("write failed on ") + path);
+    return 0;
+}
+
+namespace {
+// the RX value of one record's aux block (empty view if absent)
+std::string_view find_rx(const uint8_t *a, const uint8_t *end) {
+    while (a + 3 <= end) {
+        const int64_t vs = aux_value_size(a, end);
+        if (vs < 0 || a + 3 + vs > end) break;
+        if (a[0] == 'R' && a[1] == 'X' && a[2] == 'Z') return std::string_view((const char *)a + 3, (size_t)vs - 1);
+        a += 3 + vs;
+    }
+    return {};
+}
+}  // namespace
+
+extern "C" int64_t bsdc_rx_consensus(int64_t n_fam, const int64_t *fam_rec_off, const int64_t *rec, const int8_t *strand,
+                                     const int64_t *aux_off, const uint8_t *aux, char *out, int32_t *out_len,
+                                     int32_t n_threads) {
+    set_threads(n_threads);
+    const int64_t nrec = fam_rec_off[n_fam];
+    if (!out) {
+        int64_t w = 0;
+#pragma omp parallel for schedule(static) reduction(max : w)
+        for (int64_t i = 0; i < nrec; i++) {
+            const int64_t k = rec[i];
+            w = std::max<int64_t>(w, (int64_t)find_rx(aux + aux_off[k], aux + aux_off[k + 1]).size());
+        }
+        return w;
+    }
+    int64_t width = 0;
+    for (int64_t i = 0; i < nrec; i++) {
+        const int64_t k = rec[i];
+        width = std::max<int64_t>(width, (int64_t)find_rx(aux + aux_off[k], aux + aux_off[k + 1]).size());
+    }
+#pragma omp parallel for schedule(dynamic, 256)
+    for (int64_t f = 0; f < n_fam; f++) {
+        std::vector<std::string> v;
+        for (int64_t i = fam_rec_off[f]; i < fam_rec_off[f + 1]; i++) {
+            const int64_t k = rec[i];
+            const std::string_view rx = find_rx(aux + aux_off[k], aux + aux_off[k + 1]);
+            if (rx.empty()) continue;
+            std::string s(rx);
+            const size_t dash = s.find('-');
+            if (strand[k] == 1 && dash != std::string::npos)  // B strand: U2-U1 -> U1-U2
+                s = s.substr(dash + 1) + "-" + s.substr(0, dash);
+            v.push_back(std::move(s));
+        }
+        char *o = out + f * width;
+        if (v.empty()) {
+            out_len[f] = 0;
+            continue;
+        }
+        // the most common length (the first seen on a tie)
+        size_t L = v[0].size();
+        int best = 0;
+        for (auto &a : v) {
+            int c = 0;
+            for (auto &b2 : v) c += b2.size() == a.size();
+            if (c > best) {
+                best = c;
+                L = a.size();
+            }
+        }
+        for (size_t j = 0; j < L; j++) {
+            int cnt[256] = {0};
+            for (auto &a : v)
+                if (a.size() == L) cnt[(uint8_t)a[j]]++;
+            int top = 0, ties = 0, ch = 'N';
+            for (int c = 0; c < 256; c++) {
+                if (cnt[c] > top) {
+                    top = cnt[c];
+                    ch = c;
+                    ties = 0;
+                } else if (cnt[c] == top && top > 0) {
+                    ties++;
+                }
+            }
+            o[j] = (char)(ties ? 'N' : ch);
+        }
+        out_len[f] = (int32_t)L;
+    }
+    return width;
+}

@@ -54,6 +54,8 @@ class Consensus:
     length: np.ndarray     # [F, 2]
     seq: np.ndarray        # [F, 2, stride] nt16 codes
     qual: np.ndarray       # [F, 2, stride]
+    fam_rec_off: np.ndarray = None  # [F + 1] family membership: fam_src[fam_rec_off[f]:fam_rec_off[f+1]]
+    fam_src: np.ndarray = None      # input record index of each family record (family order)
 
 
 def _stripped_cigar(raw: R.RawRecords, k: int, strip: bool) -> List[int]:
@@ -208,7 +210,8 @@ def consensus_from_output(fb: FamilyBatch, out: dict) -> Consensus:
     seq = np.empty((F, 2, stride), np.uint8)
     seq[:, :, 0::2] = packed >> 4
     seq[:, :, 1::2] = packed & 0xF
-    return Consensus(fb.fam_mi.copy(), out["status"], out["len"], seq, out["qual"])
+    return Consensus(fb.fam_mi.copy(), out["status"], out["len"], seq, out["qual"], fb.fam_off.astype(np.int64),
+                     fb.src.astype(np.int64))
 
 
 def run_step5(engine: Engine, raw: R.RawRecords, dump: bool = False):
@@ -221,7 +224,9 @@ def run_step5(engine: Engine, raw: R.RawRecords, dump: bool = False):
         db = engine.upload(fb2, dump=True)
         engine.run(db, MODE_CONVERT | MODE_EXTEND | MODE_DUMP)
         t2 = _records_from_dump(raw, fb2, db.fetch(), strip=True)
-        return run_duplex(engine, raw_from_records(raw, t2)), (t2 if dump else None)
+        cons = run_duplex(engine, raw_from_records(raw, t2))
+        cons.fam_src = t2.src[cons.fam_src]  # raw2 record k is tool-2 record k
+        return cons, (t2 if dump else None)
     db = engine.upload(fb, dump=dump)
     engine.run(db, MODE_CONVERT | MODE_EXTEND | MODE_VOTE | (MODE_DUMP if dump else 0))
     out = db.fetch()

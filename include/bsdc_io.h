@@ -1,0 +1,114 @@
+/* bsdc_io.h -- host-side BAM/BGZF codec for the step-5 drop-in (libbsdc_io.so, C++/zlib/OpenMP).
+ *
+ * Replaces the file I/O around the step: the reference's tools read and write BAM
+ * through pysam (tools/1.convert_AG_to_CT.py:86-99, tools/2.extend_gap.py:147-190) and fgbio
+ * through htsjdk (main.snake.py:152,163).  The reader hands the step the structure-of-arrays
+ * record stream the family builder consumes (bsseqconsensusreads_amd.records.RawRecords): MI tags
+ * interned to MI-base ids with the /A|/B strand, QNAMEs interned, MC parsed to cigar ops, LA/RD
+ * pulled out, everything else kept as raw aux bytes.  The writer encodes records and BGZF-deflates
+ * blocks in parallel.
+ *
+ * Conventions: 0 on success, a negative code on failure (message in bsdc_io_last_error(), per
+ * thread); caller-owned output arrays, sized from bsdc_bam_sizes. */
+#ifndef BSDC_IO_H
+#define BSDC_IO_H
+#include <stdint.h>
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define BSDC_IO_ABI_VERSION 1
+#define BSDC_IO_EFORMAT (-10) /* not BGZF/BAM, truncated, bad CRC */
+#define BSDC_IO_EIO (-11)     /* open/read/write failed */
+
+typedef struct bsdc_bam bsdc_bam; /* a decoded BAM held in host memory */
+
+typedef struct {
+    int64_t n_rec;
+    int64_t n_bases;      /* sum of l_seq */
+    int64_t n_cigar;      /* cigar ops */
+    int64_t n_mc;         /* MC-tag cigar ops */
+    int64_t aux_bytes;
+    int64_t n_names, name_bytes; /* distinct QNAMEs */
+    int64_t n_mi, mi_bytes;      /* distinct MI bases (MI up to the first '/') */
+    int64_t header_bytes;        /* SAM header text */
+    int32_t n_ref;
+    int64_t ref_name_bytes;
+} bsdc_bam_sizes;
+
+/* Output arrays (caller-allocated; n = n_rec).  seq is one nt16 code per byte. */
+typedef struct {
+    uint16_t *flag;
+    int32_t *tid, *pos;
+    uint8_t *mapq;
+    int32_t *l_seq;
+    int64_t *seq_off;
+    uint8_t *seq, *qual;
+    int64_t *cig_off;
+    int32_t *n_cig;
+    uint32_t *cigar;
+    int32_t *next_tid, *next_pos, *tlen;
+    int32_t *name_id;
+    int64_t *name_off; /* [n_names + 1] */
+    char *name_buf;
+    int32_t *mi_id;     /* -1: no (or empty) MI tag */
+    int8_t *mi_strand;  /* 0 "/A", 1 "/B", -1 neither */
+    int64_t *mi_off;    /* [n_mi + 1] */
+    char *mi_buf;
+    int64_t *mc_off;    /* -1: no MC tag */
+    int32_t *mc_n;
+    uint32_t *mc_cigar;
+    int32_t *la, *rd;   /* -1: tag absent */
+    int64_t *aux_off;   /* [n + 1] */
+    uint8_t *aux;
+    char *header;
+    int64_t *ref_len;       /* [n_ref] */
+    int64_t *ref_name_off;  /* [n_ref + 1] */
+    char *ref_name_buf;
+} bsdc_bam_arrays;
+
+int32_t bsdc_io_abi_version(void);
+const char *bsdc_io_last_error(void);
+
+/* Reads and decodes a whole BAM (BGZF blocks inflated in parallel, records parsed in parallel). */
+int32_t bsdc_bam_read(const char *path, int32_t n_threads, bsdc_bam **out);
+void bsdc_bam_sizes_of(const bsdc_bam *b, bsdc_bam_sizes *s);
+int32_t bsdc_bam_copy(const bsdc_bam *b, const bsdc_bam_arrays *a);
+void bsdc_bam_free(bsdc_bam *b);
+
+/* Records to write (n_rec entries; every *_off array has n_rec + 1 entries). */
+typedef struct {
+    int64_t n_rec;
+    const uint16_t *flag;
+    const int32_t *tid, *pos;
+    const uint8_t *mapq;
+    const int32_t *next_tid, *next_pos, *tlen;
+    const int64_t *name_off;
+    const char *name_buf;
+    const int64_t *cig_off;
+    const uint32_t *cigar;
+    const int64_t *seq_off;  /* l_seq = seq_off[k+1] - seq_off[k] */
+    const uint8_t *seq;      /* nt16 codes, one per byte */
+    const uint8_t *qual;
+    const int64_t *aux_off;
+    const uint8_t *aux;
+} bsdc_bam_records;
+
+/* Writes header + records as BGZF (blocks deflated in parallel at `level`), with the EOF block. */
+int32_t bsdc_bam_write(const char *path, const char *header_text, int64_t header_len, int32_t n_ref,
+                       const int64_t *ref_name_off, const char *ref_name_buf, const int64_t *ref_len,
+                       const bsdc_bam_records *r, int32_t level, int32_t n_threads);
+
+/* Consensus RX per family for the duplex output records (fgbio's consensus
+ * UMI, parity unpinned): every family record's RX, a /B-strand record's two '-'-separated halves
+ * swapped, then per position the most common character over the RX values of the most common
+ * length (a tie -> 'N').  Families with no RX get an empty string.  Output: width = longest RX
+ * (call with out = NULL to get it), out[f * width ...] and out_len[f]. */
+int64_t bsdc_rx_consensus(int64_t n_fam, const int64_t *fam_rec_off, const int64_t *rec, const int8_t *strand,
+                          const int64_t *aux_off, const uint8_t *aux, char *out, int32_t *out_len,
+                          int32_t n_threads);
+
+#ifdef __cplusplus
+}
+#endif
+#endif

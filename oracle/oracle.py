@@ -126,6 +126,13 @@ def _ptr(a):
 def lex_ranks(strings, ids) -> np.ndarray:
     """rank[id] = byte-order rank of strings[id] over the ids in use (equal strings share a rank)."""
     ids = np.asarray(ids, np.int64)
+    if hasattr(strings, "lex_key"):  # synthetic / decoded name tables order their own ids
+        u = np.unique(ids[ids >= 0])
+        rank = np.zeros(max(int(u[-1]) + 1 if u.shape[0] else 1, 1), np.int32)
+        if u.shape[0]:
+            _, rk = np.unique(strings.lex_key(u), return_inverse=True)
+            rank[u] = rk
+        return rank
     used = sorted(set(int(i) for i in np.unique(ids[ids >= 0])))
     rank = np.zeros(max(used[-1] + 1 if used else 1, 1), np.int32)
     b = {i: (strings[i] if isinstance(strings[i], bytes) else strings[i].encode()) for i in used}

@@ -1,0 +1,219 @@
+"""Host BAM/BGZF codec (libbsdc_io, include/bsdc_io.h) and the duplex output records
+(SURVEY.md 8a row 8, 8f ranks 1-2).  CPU only: round trips, an independent BGZF reader/writer
+written here with zlib, the RX consensus against a Python restatement, and the output records of
+the oracle's consensus."""
+import gzip
+import struct
+import zlib
+
+import numpy as np
+import pytest
+
+from bsseqconsensusreads_amd import bam, batch, synth
+from bsseqconsensusreads_amd import records as R
+from oracle import oracle
+
+
+def _header(ref):
+    text = "@HD\tVN:1.6\tSO:coordinate\n" + "".join("@SQ\tSN:%s\tLN:%d\n" % (n, l) for n, l in
+                                                    zip(ref.names, ref.lengths)) + "@RG\tID:rg1\tSM:s1\tLB:libA\n"
+    return bam.BamHeader(text, list(ref.names), np.asarray(ref.lengths, np.int64))
+
+
+def _messy(n_fam=400, seed=3):
+    s = synth.generate("C2", n_fam, seed=seed, device="cpu", genome_len=100_000)
+    return s, synth.messify(s.raw, frac=0.3, seed=seed)
+
+
+def _same_records(a: R.RawRecords, b: R.RawRecords):
+    assert a.n == b.n
+    for k in ("flag", "tid", "pos", "mapq", "l_seq", "next_tid", "next_pos", "tlen", "mi_strand", "n_cig"):
+        assert np.array_equal(getattr(a, k), getattr(b, k)), k
+    assert np.array_equal(a.seq, b.seq) and np.array_equal(a.qual, b.qual)
+    assert np.array_equal(a.cigar, b.cigar)
+    for k in range(a.n):
+        assert a.names[int(a.name_id[k])] == b.names[int(b.name_id[k])]
+        if a.mi_id[k] < 0:
+            assert b.mi_id[k] < 0
+        else:
+            assert a.mi_names[int(a.mi_id[k])] == b.mi_names[int(b.mi_id[k])]
+        ma = a.mc_cigar[a.mc_off[k]:a.mc_off[k] + a.mc_n[k]] if a.mc_off[k] >= 0 else None
+        mb = b.mc_cigar[b.mc_off[k]:b.mc_off[k] + b.mc_n[k]] if b.mc_off[k] >= 0 else None
+        assert (ma is None) == (mb is None) and (ma is None or np.array_equal(ma, mb))
+
+
+def test_round_trip(tmp_path):
+    s, raw = _messy()
+    hdr = _header(s.ref)
+    p = str(tmp_path / "a.bam")
+    bam.write_bam(p, hdr, bam.records_to_bam(raw), level=6, threads=4)
+    h2, raw2 = bam.read_bam(p, threads=4)
+    assert h2.text == hdr.text and h2.ref_names == hdr.ref_names
+    assert np.array_equal(h2.ref_lens, hdr.ref_lens)
+    _same_records(raw, raw2)
+    # aux bytes survive untouched, and the family builder sees the same families
+    for k in range(0, raw.n, 97):
+        assert raw2.aux[k] == raw.aux[k]
+    f1 = batch.build_family_batch(raw, "full", s.ref)
+    f2 = batch.build_family_batch(raw2, "full", s.ref)
+    assert np.array_equal(f1.src, f2.src) and np.array_equal(f1.fam_off, f2.fam_off)
+
+
+def _py_bgzf_read(path):
+    """Independent reader: BGZF is multi-member gzip."""
+    with gzip.open(path, "rb") as f:
+        return f.read()
+
+
+def _py_bgzf_write(path, data: bytes, block=40000):
+    out = bytearray()
+    for i in range(0, len(data), block):
+        chunk = data[i:i + block]
+        c = zlib.compressobj(6, zlib.DEFLATED, -15)
+        cd = c.compress(chunk) + c.flush()
+        out += struct.pack("<BBBBIBBHBBHH", 31, 139, 8, 4, 0, 0, 255, 6, 66, 67, 2, len(cd) + 25)
+        out += cd + struct.pack("<II", zlib.crc32(chunk) & 0xFFFFFFFF, len(chunk))
+    out += bytes([31, 139, 8, 4, 0, 0, 0, 0, 0, 255, 6, 0, 66, 67, 2, 0, 27, 0, 3, 0, 0, 0, 0, 0, 0, 0, 0, 0])
+    open(path, "wb").write(bytes(out))
+
+
+def test_bgzf_interoperates_with_zlib(tmp_path):
+    s, raw = _messy(200, seed=4)
+    hdr = _header(s.ref)
+    p = str(tmp_path / "b.bam")
+    bam.write_bam(p, hdr, bam.records_to_bam(raw), level=1, threads=2)
+    data = _py_bgzf_read(p)
+    assert data[:4] == b"BAM\1"
+    l_text = struct.unpack("<i", data[4:8])[0]
+    assert data[8:8 + l_text].decode() == hdr.text
+    # rewrite the same stream with other block boundaries (records split across blocks)
+    q = str(tmp_path / "c.bam")
+    _py_bgzf_write(q, data, block=777)
+    _, raw3 = bam.read_bam(q, threads=3)
+    _same_records(raw, raw3)
+
+
+def test_corrupt_input_fails_loudly(tmp_path):
+    p = tmp_path / "bad.bam"
+    p.write_bytes(b"not a bam at all")
+    with pytest.raises(OSError, match="BGZF"):
+        bam.read_bam(str(p))
+    s, raw = _messy(50, seed=5)
+    good = tmp_path / "g.bam"
+    bam.write_bam(str(good), _header(s.ref), bam.records_to_bam(raw))
+    b = bytearray(good.read_bytes())
+    b[40] ^= 0xFF  # inside the first block's deflate data
+    (tmp_path / "x.bam").write_bytes(bytes(b))
+    with pytest.raises(OSError):
+        bam.read_bam(str(tmp_path / "x.bam"))
+
+
+def _py_rx(rxs, strands):
+    vals = []
+    for rx, st in zip(rxs, strands):
+        if rx is None:
+            continue
+        if st == 1 and "-" in rx:
+            a, b2 = rx.split("-", 1)
+            rx = b2 + "-" + a
+        vals.append(rx)
+    if not vals:
+        return ""
+    lens = [len(v) for v in vals]
+    L = max(set(lens), key=lambda l: (lens.count(l), -lens.index(l)))
+    out = []
+    for j in range(L):
+        col = [v[j] for v in vals if len(v) == L]
+        cnt = {c: col.count(c) for c in set(col)}
+        top = max(cnt.values())
+        best = [c for c in cnt if cnt[c] == top]
+        out.append(best[0] if len(best) == 1 else "N")
+    return "".join(out)
+
+
+def test_rx_consensus_matches_restatement():
+    rng = np.random.default_rng(9)
+    b = R._Builder()
+    fams, rxs, strands = [], [], []
+    k = 0
+    for f in range(300):
+        recs = []
+        u1 = "".join(rng.choice(list("ACGT"), 6))
+        u2 = "".join(rng.choice(list("ACGT"), 6))
+        for j in range(int(rng.integers(1, 6))):
+            st = int(rng.integers(0, 2))
+            rx = (u1 + "-" + u2) if st == 0 else (u2 + "-" + u1)
+            rx = "".join(c if rng.random() > 0.1 else "T" for c in rx)
+            if rng.random() < 0.05:
+                rx = rx[:-1]
+            has = rng.random() > 0.05
+            tags = [("MI", "Z", "%d/%s" % (f, "AB"[st]))] + ([("RX", "Z", rx)] if has else [])
+            b.add(b"r%d" % k, 99, 0, 10, 60, [(4 << 4)], np.ones(4, np.uint8), np.full(4, 30, np.uint8), 0, 10, 0,
+                  R.encode_aux(tags), tags)
+            recs.append(k)
+            rxs.append(rx if has else None)
+            strands.append(st)
+            k += 1
+        fams.append(recs)
+    raw = b.finish()
+    off = np.zeros(len(fams) + 1, np.int64)
+    off[1:] = np.cumsum([len(x) for x in fams])
+    cons = type("C", (), {})()
+    cons.fam_rec_off = off
+    cons.fam_src = np.concatenate([np.asarray(x, np.int64) for x in fams])
+    cons.status = np.ones(len(fams), np.uint8)
+    cons.fam_mi = np.asarray([raw.mi_id[x[0]] for x in fams], np.int32)
+    cons.length = np.ones((len(fams), 2), np.int32)
+    cons.seq = np.ones((len(fams), 2, 16), np.uint8)
+    cons.qual = np.full((len(fams), 2, 16), 30, np.uint8)
+    recs = bam.duplex_records(cons, raw, "pfx", threads=3)
+    for f, members in enumerate(fams):
+        want = _py_rx([rxs[i] for i in members], [strands[i] for i in members])
+        got = R.aux_get(recs.aux[2 * f], "RX") or ""
+        assert got == want, (f, got, want)
+
+
+def test_duplex_records_of_the_oracle_consensus(tmp_path):
+    s, raw = _messy(300, seed=6)
+    res = oracle.run(raw, s.ref)
+    stride = res.cons_seq.shape[2]
+    cons = type("C", (), {})()
+    cons.fam_rec_off, cons.fam_src = res.fam_rec_off, res.fam_src
+    cons.status, cons.fam_mi, cons.length = res.status.astype(np.uint8), res.fam_mi, res.cons_len
+    cons.seq, cons.qual = res.cons_seq, res.cons_qual
+    hdr = _header(s.ref)
+    recs = bam.duplex_records(cons, raw, bam.read_name_prefix(hdr))
+    p = str(tmp_path / "out.bam")
+    bam.write_bam(p, bam.output_header(hdr), recs)
+    h2, out = bam.read_bam(p)
+    em = np.nonzero(res.status == 1)[0]
+    assert out.n == 2 * em.shape[0]
+    assert np.array_equal(out.flag, np.tile([77, 141], em.shape[0]))
+    assert (out.tid == -1).all() and (out.pos == -1).all() and (out.n_cig == 0).all()
+    assert "@RG\tID:A\tSM:s1\tLB:libA" in h2.text and h2.text.startswith("@HD\tVN:1.6\tSO:unsorted")
+    for i, f in enumerate(em):
+        mi = raw.mi_names[int(res.fam_mi[f])]
+        for e in range(2):
+            k = 2 * i + e
+            assert out.names[int(out.name_id[k])] == ("libA:%s" % mi).encode()
+            assert out.mi_names[int(out.mi_id[k])] == mi and R.aux_get(out.aux[k], "RG") == "A"
+            L = int(res.cons_len[f, e])
+            o = int(out.seq_off[k])
+            assert int(out.l_seq[k]) == L
+            assert np.array_equal(out.seq[o:o + L], res.cons_seq[f, e, :L])
+            assert np.array_equal(out.qual[o:o + L], res.cons_qual[f, e, :L])
+    assert stride > 0
+
+
+def test_fasta_reader(tmp_path):
+    s = synth.generate("C2", 10, seed=8, device="cpu", genome_len=5_000)
+    codes = R.unpack_nibbles(s.ref.packed, s.ref.n_nibbles)
+    letters = R.NT16_TO_ASCII[codes].tobytes().decode()
+    fa = tmp_path / "g.fa"
+    fa.write_text(">chrX other words\nACGTNNNN\nacgt\n>%s\n%s\n" % (
+        s.ref.names[0], "\n".join(letters[i:i + 60] for i in range(0, len(letters), 60))))
+    hdr = bam.BamHeader("", [s.ref.names[0], "chrMissing"], np.asarray([len(letters), 5], np.int64))
+    ref = bam.read_fasta(str(fa), hdr)
+    assert ref.contig_off[1] == -1
+    got = R.unpack_nibbles(ref.packed, ref.n_nibbles)[ref.contig_off[0]:ref.contig_off[0] + ref.contig_len[0]]
+    assert np.array_equal(got, codes)
