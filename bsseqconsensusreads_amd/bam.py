@@ -216,12 +216,74 @@ class OutRecordsBam:
         return int(self.flag.shape[0])
 
 
+def _ascii_int(x: np.ndarray):
+    """Non-negative ints -> their decimal ASCII, packed: (buf, off)."""
+    x = np.asarray(x, np.int64)
+    d = np.ones_like(x)
+    for k in range(1, 19):
+        d += x >= 10 ** k
+    off = np.zeros(x.shape[0] + 1, np.int64)
+    off[1:] = np.cumsum(d)
+    pos = np.arange(int(off[-1]), dtype=np.int64)
+    rec = np.repeat(np.arange(x.shape[0]), d)
+    p = pos - off[rec]                       # digit index from the left
+    buf = (48 + (x[rec] // (10 ** (d[rec] - 1 - p))) % 10).astype(np.uint8)
+    return buf, off
+
+
+def _concat_fields(parts, n):
+    """Per-record byte fields (each (buf, off) or a constant bytes) -> one packed StringTable."""
+    lens = np.zeros(n, np.int64)
+    for p in parts:
+        lens += len(p) if isinstance(p, bytes) else (p[1][1:] - p[1][:-1])
+    off = np.zeros(n + 1, np.int64)
+    off[1:] = np.cumsum(lens)
+    buf = np.zeros(int(off[-1]), np.uint8)
+    cur = off[:-1].copy()
+    for p in parts:
+        if isinstance(p, bytes):
+            if p:
+                b = np.frombuffer(p, np.uint8)
+                buf[(cur[:, None] + np.arange(len(p))[None, :]).reshape(-1)] = np.tile(b, n)
+                cur += len(p)
+        else:
+            pb, po = p
+            ln = po[1:] - po[:-1]
+            dst = np.repeat(cur - po[:-1], ln) + np.arange(int(ln.sum()), dtype=np.int64)
+            buf[dst] = pb
+            cur += ln
+    return StringTable(buf, off)
+
+
+def _synthetic_fields(raw: R.RawRecords):
+    """Vectorised MI / MC aux and QNAMEs of a synthetic stream (decimal lazy names, one-op MC)."""
+    n = raw.n
+    mi_pre = getattr(raw.mi_names, "prefix", None)
+    nm_pre = getattr(raw.names, "prefix", None)
+    if mi_pre is None or nm_pre is None or (raw.mc_n > 1).any() or (raw.mi_id < 0).any() or (raw.mi_strand < 0).any():
+        return None
+    mi = _ascii_int(raw.mi_id)
+    sfx = (np.frombuffer(b"AB", np.uint8)[raw.mi_strand.astype(np.int64)], np.arange(n + 1, dtype=np.int64))
+    has_mc = raw.mc_off >= 0
+    mcv = raw.mc_cigar[np.where(has_mc, raw.mc_off, 0)] if raw.mc_cigar.shape[0] else np.zeros(n, np.uint32)
+    if not has_mc.all():
+        return None
+    mcl = _ascii_int(mcv >> 4)
+    mco = (np.frombuffer(R.CIGAR_OPS.encode(), np.uint8)[(mcv & 0xF).astype(np.int64)], np.arange(n + 1, dtype=np.int64))
+    aux = _concat_fields([b"MIZ" + mi_pre.encode(), mi, b"/", sfx, b"\0MCZ", mcl, mco, b"\0"], n)
+    names = _concat_fields([nm_pre.encode(), _ascii_int(raw.name_id)], n)
+    return aux, names
+
+
 def records_to_bam(raw: R.RawRecords) -> OutRecordsBam:
     """A RawRecords stream as records to write: its own aux bytes, or for synthetic streams
     (no aux) the MI (with the /A|/B strand) and MC tags rebuilt from the decoded fields."""
     n = raw.n
+    syn = _synthetic_fields(raw) if raw.aux is None and n else None
     if raw.aux is not None:
         aux = _aux_table(raw)
+    elif syn is not None:
+        aux = syn[0]
     else:
         parts = []
         for k in range(n):
@@ -240,9 +302,11 @@ def records_to_bam(raw: R.RawRecords) -> OutRecordsBam:
     seq_off = np.zeros(n + 1, np.int64)
     seq_off[:n] = raw.seq_off
     seq_off[n] = int(raw.seq_off[-1] + raw.l_seq[-1]) if n else 0
-    nid = raw.name_id.astype(np.int64)
-    names = raw.names
-    tab = StringTable.from_list([names[int(i)] for i in nid])
+    if syn is not None:
+        tab = syn[1]
+    else:
+        names = raw.names
+        tab = StringTable.from_list([names[int(i)] for i in raw.name_id.astype(np.int64)])
     return OutRecordsBam(raw.flag, raw.tid, raw.pos, raw.mapq, raw.next_tid, raw.next_pos, raw.tlen, tab, cig_off,
                          raw.cigar, seq_off, raw.seq, raw.qual, aux)
 
