@@ -20,7 +20,7 @@ from __future__ import annotations
 import ctypes as C
 import os
 from dataclasses import dataclass
-from typing import List, Optional
+from typing import List, Optional, Tuple
 
 import numpy as np
 
@@ -28,7 +28,7 @@ from . import records as R
 
 IO_LIB_PATH = os.environ.get("BSDC_IO_LIB_PATH") or os.path.join(os.path.dirname(os.path.abspath(__file__)),
                                                                  "libbsdc_io.so")
-BSDC_IO_ABI_VERSION = 1
+BSDC_IO_ABI_VERSION = 2
 _P = C.c_void_p
 
 
@@ -74,6 +74,8 @@ def _load():
     lib.bsdc_bam_write.restype = C.c_int32
     lib.bsdc_rx_consensus.argtypes = [C.c_int64, _P, _P, _P, _P, _P, _P, _P, C.c_int32]
     lib.bsdc_rx_consensus.restype = C.c_int64
+    lib.bsdc_fastq_write.argtypes = [C.c_char_p, C.c_char_p, C.POINTER(_Records), C.c_int32, C.c_int32]
+    lib.bsdc_fastq_write.restype = C.c_int32
     if lib.bsdc_io_abi_version() != BSDC_IO_ABI_VERSION:
         raise RuntimeError("libbsdc_io ABI %d != %d" % (lib.bsdc_io_abi_version(), BSDC_IO_ABI_VERSION))
     _lib = lib
@@ -311,6 +313,32 @@ def records_to_bam(raw: R.RawRecords) -> OutRecordsBam:
                          raw.cigar, seq_off, raw.seq, raw.qual, aux)
 
 
+def _records_struct(recs: OutRecordsBam, keep: list) -> _Records:
+    def c(x, dt):
+        a = np.ascontiguousarray(x, dtype=dt)
+        if a.size == 0:
+            a = np.zeros(1, dt)
+        keep.append(a)
+        return _ptr(a)
+    return _Records(recs.n, c(recs.flag, np.uint16), c(recs.tid, np.int32), c(recs.pos, np.int32),
+                    c(recs.mapq, np.uint8), c(recs.next_tid, np.int32), c(recs.next_pos, np.int32),
+                    c(recs.tlen, np.int32), c(recs.names.off, np.int64), c(recs.names.buf, np.uint8),
+                    c(recs.cig_off, np.int64), c(recs.cigar, np.uint32), c(recs.seq_off, np.int64),
+                    c(recs.seq, np.uint8), c(recs.qual, np.uint8), c(recs.aux.off, np.int64),
+                    c(recs.aux.buf, np.uint8))
+
+
+def write_fastq(path1: str, path2: str, recs: OutRecordsBam, level: int = 6, threads: int = 0):
+    """Paired gzip FASTQ of `recs` as picard SamToFastq F=path1 F2=path2 writes it (the rule after
+    step 5, main.snake.py:167-177): '@name/1' / '@name/2', SEQ, '+', QUAL+33 (libbsdc_io)."""
+    lib = _load()
+    keep = []
+    r = _records_struct(recs, keep)
+    rc = lib.bsdc_fastq_write(path1.encode(), path2.encode(), C.byref(r), int(level), int(threads))
+    if rc != 0:
+        raise ValueError("%s, %s: %s" % (path1, path2, lib.bsdc_io_last_error().decode()))
+
+
 def write_bam(path: str, header: BamHeader, recs: OutRecordsBam, level: int = 6, threads: int = 0):
     lib = _load()
     rn = StringTable.from_list([x.encode() for x in header.ref_names])
@@ -322,11 +350,7 @@ def write_bam(path: str, header: BamHeader, recs: OutRecordsBam, level: int = 6,
             a = np.zeros(1, dt)
         keep.append(a)
         return _ptr(a)
-    r = _Records(recs.n, c(recs.flag, np.uint16), c(recs.tid, np.int32), c(recs.pos, np.int32), c(recs.mapq, np.uint8),
-                 c(recs.next_tid, np.int32), c(recs.next_pos, np.int32), c(recs.tlen, np.int32),
-                 c(recs.names.off, np.int64), c(recs.names.buf, np.uint8), c(recs.cig_off, np.int64),
-                 c(recs.cigar, np.uint32), c(recs.seq_off, np.int64), c(recs.seq, np.uint8), c(recs.qual, np.uint8),
-                 c(recs.aux.off, np.int64), c(recs.aux.buf, np.uint8))
+    r = _records_struct(recs, keep)
     text = header.text.encode()
     rc = lib.bsdc_bam_write(path.encode(), text, len(text), len(header.ref_names), c(rn.off, np.int64),
                             c(rn.buf, np.uint8), c(np.asarray(header.ref_lens, np.int64), np.int64), C.byref(r),
@@ -422,9 +446,11 @@ def duplex_records(cons, raw: R.RawRecords, prefix: str, threads: int = 0) -> Ou
         cigar=np.zeros(0, np.uint32), seq_off=seq_off, seq=seq, qual=qual, aux=StringTable.from_list(auxs))
 
 
-def step5(in_bam: str, fasta: str, out_bam: str, engine=None, prefix: Optional[str] = None, threads: int = 0,
-          level: int = 6) -> dict:
-    """Rules convert_Bstrain .. callduplex (main.snake.py:121-164) as one call on files."""
+def step5(in_bam: str, fasta: str, out_bam: Optional[str], engine=None, prefix: Optional[str] = None, threads: int = 0,
+          level: int = 6, fastq: Optional[Tuple[str, str]] = None) -> dict:
+    """Rules convert_Bstrain .. callduplex (main.snake.py:121-164) as one call on files; with
+    `fastq`, also the following consensusduplex_to_fq rule (main.snake.py:167-177) straight from
+    the consensus records (out_bam may then be None: no BAM round trip)."""
     from . import pipeline
     from .device import Engine
     header, raw = read_bam(in_bam, threads)
@@ -438,6 +464,9 @@ def step5(in_bam: str, fasta: str, out_bam: str, engine=None, prefix: Optional[s
         if own:
             eng.close()
     recs = duplex_records(cons, raw, read_name_prefix(header) if prefix is None else prefix, threads)
-    write_bam(out_bam, output_header(header), recs, level, threads)
+    if out_bam is not None:
+        write_bam(out_bam, output_header(header), recs, level, threads)
+    if fastq is not None:
+        write_fastq(fastq[0], fastq[1], recs, level, threads)
     return {"records_in": raw.n, "families": int(cons.status.shape[0]),
             "families_emitted": int(((cons.status & 1) != 0).sum()), "records_out": recs.n}

@@ -443,6 +443,62 @@ int reg2bin(int64_t beg, int64_t end) {
     return 0;
 }
 constexpr int64_t kBlock = 0xff00;  // uncompressed bytes per BGZF block (htslib's size)
+// BGZF framing of an uncompressed buffer: 0xff00-byte blocks deflated in parallel (each a gzip
+// member, so the file is also plain multi-member gzip), one write, then the 28-byte EOF block.
+int32_t write_bgzf(const char *path, const std::vector<uint8_t> &buf, int32_t level) {
+    const int64_t total = (int64_t)buf.size();
+    const int64_t nb = (total + kBlock - 1) / kBlock;
+    std::vector<std::vector<uint8_t>> blocks((size_t)nb);
+    int bad = 0;
+#pragma omp parallel for schedule(dynamic, 4) reduction(| : bad)
+    for (int64_t i = 0; i < nb; i++) {
+        const uint8_t *src = buf.data() + i * kBlock;
+        const int64_t len = std::min(kBlock, total - i * kBlock);
+        std::vector<uint8_t> &o = blocks[(size_t)i];
+        o.resize(18 + (size_t)compressBound((uLong)len) + 8 + 64);
+        z_stream zs;
+        memset(&zs, 0, sizeof zs);
+        int lv = level;
+        for (int attempt = 0; attempt < 2; attempt++) {
+            if (deflateInit2(&zs, lv, Z_DEFLATED, -15, 8, Z_DEFAULT_STRATEGY) != Z_OK) {
+                bad |= 1;
+                break;
+            }
+            zs.next_in = const_cast<uint8_t *>(src);
+            zs.avail_in = (uInt)len;
+            zs.next_out = o.data() + 18;
+            zs.avail_out = (uInt)(o.size() - 26);
+            const int rc = deflate(&zs, Z_FINISH);
+            deflateEnd(&zs);
+            if (rc != Z_STREAM_END) {
+                bad |= 1;
+                break;
+            }
+            if (18 + zs.total_out + 8 <= 65536) break;
+            lv = 0;  // incompressible: store
+            memset(&zs, 0, sizeof zs);
+        }
+        const int64_t bsize = 18 + (int64_t)zs.total_out + 8;
+        uint8_t *h = o.data();
+        const uint8_t hdr[16] = {31, 139, 8, 4, 0, 0, 0, 0, 0, 255, 6, 0, 'B', 'C', 2, 0};
+        memcpy(h, hdr, 16);
+        wr16(h + 16, (uint16_t)(bsize - 1));
+        wr32(h + 18 + zs.total_out, (uint32_t)crc32(0L, src, (uInt)len));
+        wr32(h + 18 + zs.total_out + 4, (uint32_t)len);
+        o.resize((size_t)bsize);
+    }
+    if (bad) return fail(BSDC_IO_EFORMAT, "deflate failed");
+    FILE *f = fopen(path, "wb");
+    if (!f) return fail(BSDC_IO_EIO, std::string("cannot create ") + path);
+    for (auto &bk : blocks)
+        if (fwrite(bk.data(), 1, bk.size(), f) != bk.size()) {
+            fclose(f);
+            return fail(BSDC_IO_EIO, std::string("write failed on ") + path);
+        }
+    static const uint8_t eof[28] = {31, 139, 8, 4, 0, 0, 0, 0, 0, 255, 6, 0, 66, 67, 2, 0, 27, 0, 3, 0, 0, 0, 0, 0, 0, 0, 0, 0};
+    if (fwrite(eof, 1, 28, f) != 28 || fclose(f) != 0) return fail(BSDC_IO_EIO, std::string("write failed on ") + path);
+    return 0;
+}
 }  // namespace
 
 extern "C" int32_t bsdc_bam_write(const char *path, const char *header_text, int64_t header_len, int32_t n_ref,
@@ -521,59 +577,7 @@ extern "C" int32_t bsdc_bam_write(const char *path, const char *header_text, int
         q += l_seq;
         memcpy(q, r->aux + r->aux_off[k], (size_t)l_aux);
     }
-    // ---- BGZF ----
-    const int64_t total = (int64_t)buf.size();
-    const int64_t nb = (total + kBlock - 1) / kBlock;
-    std::vector<std::vector<uint8_t>> blocks((size_t)nb);
-    int bad = 0;
-#pragma omp parallel for schedule(dynamic, 4) reduction(| : bad)
-    for (int64_t i = 0; i < nb; i++) {
-        const uint8_t *src = buf.data() + i * kBlock;
-        const int64_t len = std::min(kBlock, total - i * kBlock);
-        std::vector<uint8_t> &o = blocks[(size_t)i];
-        o.resize(18 + (size_t)compressBound((uLong)len) + 8 + 64);
-        z_stream zs;
-        memset(&zs, 0, sizeof zs);
-        int lv = level;
-        for (int attempt = 0; attempt < 2; attempt++) {
-            if (deflateInit2(&zs, lv, Z_DEFLATED, -15, 8, Z_DEFAULT_STRATEGY) != Z_OK) {
-                bad |= 1;
-                break;
-            }
-            zs.next_in = const_cast<uint8_t *>(src);
-            zs.avail_in = (uInt)len;
-            zs.next_out = o.data() + 18;
-            zs.avail_out = (uInt)(o.size() - 26);
-            const int rc = deflate(&zs, Z_FINISH);
-            deflateEnd(&zs);
-            if (rc != Z_STREAM_END) {
-                bad |= 1;
-                break;
-            }
-            if (18 + zs.total_out + 8 <= 65536) break;
-            lv = 0;  // incompressible: store
-            memset(&zs, 0, sizeof zs);
-        }
-        const int64_t bsize = 18 + (int64_t)zs.total_out + 8;
-        uint8_t *h = o.data();
-        const uint8_t hdr[16] = {31, 139, 8, 4, 0, 0, 0, 0, 0, 255, 6, 0, 'B', 'C', 2, 0};
-        memcpy(h, hdr, 16);
-        wr16(h + 16, (uint16_t)(bsize - 1));
-        wr32(h + 18 + zs.total_out, (uint32_t)crc32(0L, src, (uInt)len));
-        wr32(h + 18 + zs.total_out + 4, (uint32_t)len);
-        o.resize((size_t)bsize);
-    }
-    if (bad) return fail(BSDC_IO_EFORMAT, "deflate failed");
-    FILE *f = fopen(path, "wb");
-    if (!f) return fail(BSDC_IO_EIO, std::string("cannot create ") + path);
-    for (auto &bk : blocks)
-        if (fwrite(bk.data(), 1, bk.size(), f) != bk.size()) {
-            fclose(f);
-            return fail(BSDC_IO_EIO, std::string("write failed on ") + path);
-        }
-    static const uint8_t eof[28] = {31, 139, 8, 4, 0, 0, 0, 0, 0, 255, 6, 0, 66, 67, 2, 0, 27, 0, 3, 0, 0, 0, 0, 0, 0, 0, 0, 0};
-    if (fwrite(eof, 1, 28, f) != 28 || fclose(f) != 0) return fail(BSDC_IO_EIO, std::string("write failed on ") + path);
-    return 0;
+    return write_bgzf(path, buf, level);
 }
 
 namespace {
@@ -656,4 +660,75 @@ extern "C" int64_t bsdc_rx_consensus(int64_t n_fam, const int64_t *fam_rec_off, 
         out_len[f] = (int32_t)L;
     }
     return width;
+}
+
+namespace {
+const char kNt16[] = "=ACMGRSVTWYHKDBN";
+const char kNt16Comp[] = "=TGKCYSBAWRDMHVN";
+}  // namespace
+
+extern "C" int32_t bsdc_fastq_write(const char *path1, const char *path2, const bsdc_bam_records *r, int32_t level,
+                                    int32_t n_threads) {
+    set_threads(n_threads);
+    const int64_t nr = r->n_rec;
+    // record k -> its file (0: first of pair, 1: second) or -1 (not written); pairs must be adjacent
+    std::vector<int8_t> dst((size_t)nr, -1);
+    for (int64_t k = 0; k < nr; k++) {
+        const uint16_t fl = r->flag[k];
+        if (fl & (0x100 | 0x800 | 0x200)) continue;  // secondary, supplementary, QC-fail
+        if (!(fl & 1)) return fail(BSDC_IO_EFORMAT, "unpaired record in a paired FASTQ write");
+        dst[(size_t)k] = (fl & 0x40) ? 0 : 1;
+    }
+    int64_t want = 0, first = -1;
+    for (int64_t k = 0; k < nr; k++) {
+        if (dst[(size_t)k] < 0) continue;
+        if (dst[(size_t)k] != want) return fail(BSDC_IO_EFORMAT, "records are not in first/second-of-pair order");
+        if (want == 0) {
+            first = k;
+        } else {
+            const int64_t l0 = r->name_off[first + 1] - r->name_off[first], l1 = r->name_off[k + 1] - r->name_off[k];
+            if (l0 != l1 || memcmp(r->name_buf + r->name_off[first], r->name_buf + r->name_off[k], (size_t)l0) != 0)
+                return fail(BSDC_IO_EFORMAT, "mates of a pair have different names");
+        }
+        want ^= 1;
+    }
+    if (want) return fail(BSDC_IO_EFORMAT, "a first-of-pair record has no mate");
+    // "@name/N\nSEQ\n+\nQUAL\n" per record, sizes -> offsets per file -> parallel format
+    std::vector<int64_t> off[2] = {std::vector<int64_t>((size_t)nr + 1), std::vector<int64_t>((size_t)nr + 1)};
+    int64_t tot[2] = {0, 0};
+    for (int64_t k = 0; k < nr; k++) {
+        off[0][(size_t)k] = tot[0];
+        off[1][(size_t)k] = tot[1];
+        const int d = dst[(size_t)k];
+        if (d < 0) continue;
+        const int64_t ln = r->name_off[k + 1] - r->name_off[k], ls = r->seq_off[k + 1] - r->seq_off[k];
+        tot[d] += 1 + ln + 2 + 1 + ls + 1 + 2 + ls + 1;
+    }
+    std::vector<uint8_t> buf[2] = {std::vector<uint8_t>((size_t)tot[0]), std::vector<uint8_t>((size_t)tot[1])};
+#pragma omp parallel for schedule(static)
+    for (int64_t k = 0; k < nr; k++) {
+        const int d = dst[(size_t)k];
+        if (d < 0) continue;
+        uint8_t *p = buf[d].data() + off[d][(size_t)k];
+        const int64_t ln = r->name_off[k + 1] - r->name_off[k], ls = r->seq_off[k + 1] - r->seq_off[k];
+        const bool rev = r->flag[k] & 0x10;  // SamToFastq writes reads in sequencing orientation
+        const uint8_t *s = r->seq + r->seq_off[k], *q = r->qual + r->seq_off[k];
+        *p++ = '@';
+        memcpy(p, r->name_buf + r->name_off[k], (size_t)ln);
+        p += ln;
+        *p++ = '/';
+        *p++ = d == 0 ? '1' : '2';
+        *p++ = '\n';
+        for (int64_t i = 0; i < ls; i++) *p++ = rev ? kNt16Comp[s[ls - 1 - i] & 15] : kNt16[s[i] & 15];
+        *p++ = '\n';
+        *p++ = '+';
+        *p++ = '\n';
+        for (int64_t i = 0; i < ls; i++) *p++ = (uint8_t)(33 + (rev ? q[ls - 1 - i] : q[i]));
+        *p++ = '\n';
+    }
+    for (int d = 0; d < 2; d++) {
+        const int32_t rc = write_bgzf(d == 0 ? path1 : path2, buf[d], level);
+        if (rc != 0) return rc;
+    }
+    return 0;
 }

@@ -35,13 +35,16 @@
 namespace {
 
 constexpr int kWave = 64;
+#ifndef SMALL_WAVES
+#define SMALL_WAVES 7  // k_small waves per SIMD the register budget is cut for (7: <= 64 VGPRs, <= 96 SGPRs)
+#endif
 #ifndef SMALL_SGPRS
-#define SMALL_SGPRS 96  // SGPR budget of k_small: <= 96 keeps 7 waves per SIMD (MI355X_MICROARCH.md)
+#define SMALL_SGPRS (SMALL_WAVES >= 8 ? 80 : 96)  // SGPR budget: <= 80 -> 8, <= 96 -> 7 waves per SIMD (MI355X_MICROARCH.md)
 #endif
 constexpr int kLargeThreads = 256;
 constexpr int kSmallMaxWaves = 8;              // wavefronts (families) per small-kernel workgroup, at most
-constexpr int kSmallMinWaves = 6;              // occupancy target (waves per SIMD) the register budget is cut for
-constexpr int kSmallSimdWaves = 7;             // waves per SIMD its registers allow (<= 64 VGPRs, 82-96 SGPRs)
+constexpr int kSmallMinWaves = SMALL_WAVES >= 8 ? 8 : 6;  // occupancy target the register budget is cut for
+constexpr int kSmallSimdWaves = SMALL_WAVES;   // waves per SIMD its registers allow
 constexpr int kLdsBytes = 160 * 1024;           // LDS per CU
 constexpr double kLrScale = 1048576.0;          // 2^20
 constexpr int kTabBytes = 1024 + 1024 + 384 + 2048 + 192;  // the Tables image in LDS
@@ -262,7 +265,7 @@ __device__ int32_t readthrough_keep(const bsdc_family_batch &B, uint32_t gidx, u
     return keep;
 }
 
-// Simplified cigar of a source read (sequencing orientation, M/=/X -> M, merged, truncated to
+// Simplified cigar of a source read (sequencing orientation, M/=/X/S -> M, merged, truncated to
 // srclen query bases) into `so`; returns the op count.
 __device__ int simplified_cigar(const CigView *cv, bool complex_, bool neg, int32_t srclen, uint32_t *so) {
     if (!complex_) {
@@ -278,8 +281,8 @@ __device__ int simplified_cigar(const CigView *cv, bool complex_, bool neg, int3
         int32_t l;
         cv->at(k, op, l);
         if (l <= 0) continue;
-        if (op == 7 || op == 8) op = 0;
-        if (op == 4 || op == 5) continue;
+        if (op == 7 || op == 8 || op == 4) op = 0;  // fgbio simplifyCigar: S, =, X -> M
+        if (op == 5) continue;
         if (op == 0 || op == 1) {
             if (q + l > srclen) l = srclen - q;
             q += l;
@@ -1038,6 +1041,8 @@ __global__ __launch_bounds__(kWave *kSmallMaxWaves, kSmallMinWaves) __attribute_
     }
     if (set != 0xFF) atomicMax(&lc[set], (uint32_t)srclen);
     wave_sync();
+    // lane j holds descriptor j: the vote reads them with v_readlane (no LDS round trip per read)
+    const uint32_t dreg = t < off[3] + cnt[3] ? dlist[t] : 0u;
     int lcs[4];
 #pragma unroll
     for (int s = 0; s < 4; s++) lcs[s] = (int)__builtin_amdgcn_readfirstlane(lc[s]);
@@ -1078,7 +1083,7 @@ __global__ __launch_bounds__(kWave *kSmallMaxWaves, kSmallMinWaves) __attribute_
 #pragma unroll
                     for (int side = 0; side < 2; side++) {
                         const int s = side == 0 ? (e == 0 ? 0 : 1) : (e == 0 ? 3 : 2);
-                        const uint32_t *dl = dlist + off[s];
+                        const int o = off[s];
                         // one read: its 4 columns from c (descriptor d is wave-uniform; d = 0 is a
                         // read of length 0 and adds nothing, which pads the pairs below)
                         auto fwd = [&](uint32_t d) {
@@ -1100,19 +1105,17 @@ __global__ __launch_bounds__(kWave *kSmallMaxWaves, kSmallMinWaves) __attribute_
                         const int nf = nfw[s], na = cnt[s];
                         int i = 0;
                         for (; i + 1 < nf; i += 2) {
-                            const uint32_t d0 = __builtin_amdgcn_readfirstlane(dl[i]);
-                            const uint32_t d1 = __builtin_amdgcn_readfirstlane(dl[i + 1]);
+                            const uint32_t d0 = rlu(dreg, o + i), d1 = rlu(dreg, o + i + 1);
                             fwd(d0);
                             fwd(d1);
                         }
-                        if (i < nf) fwd(__builtin_amdgcn_readfirstlane(dl[i]));
+                        if (i < nf) fwd(rlu(dreg, o + i));
                         for (i = nf; i + 1 < na; i += 2) {
-                            const uint32_t d0 = __builtin_amdgcn_readfirstlane(dl[i]);
-                            const uint32_t d1 = __builtin_amdgcn_readfirstlane(dl[i + 1]);
+                            const uint32_t d0 = rlu(dreg, o + i), d1 = rlu(dreg, o + i + 1);
                             rev(d0);
                             rev(d1);
                         }
-                        if (i < na) rev(__builtin_amdgcn_readfirstlane(dl[i]));
+                        if (i < na) rev(rlu(dreg, o + i));
                     }
                 }
                 uint32_t bm[2], multi[2];
@@ -1164,29 +1167,32 @@ __global__ __launch_bounds__(kWave *kSmallMaxWaves, kSmallMinWaves) __attribute_
                 }
             }
         }
-        // queued columns: the general path (all four likelihoods, up to three exp terms); a lane
-        // owns one queued (end, column) and walks the reads of its end's two sides
+        // queued columns: the general path (all four likelihoods, up to three exp terms).  Two lanes
+        // per queued (end, column): lane 2k the end's side A, lane 2k+1 its side B, each walking its
+        // own side's reads; the side-A lane then combines the pair (partner value by lane shuffle).
         wave_sync();
         if (stop == 7) nq = 0;
-        for (int k0 = 0; k0 < nq && stop != 9; k0 += 64) {
-            const int k = k0 + t;
+        const uint32_t hsm = (hs[0] ? 1u : 0u) | (hs[1] ? 2u : 0u) | (hs[2] ? 4u : 0u) | (hs[3] ? 8u : 0u);
+        const int side = t & 1;
+        for (int k0 = 0; k0 < 2 * nq && stop != 9; k0 += 64) {
+            const int k = (k0 + t) >> 1;
             const bool act = k < nq;
             const uint32_t ent = act ? sq[k] : 0u;
             const int e = (int)(ent >> 15), c = (int)(ent & 0x7FFF);
-            const int sa = e == 0 ? 0 : 1, sb = e == 0 ? 3 : 2;
+            // this lane's set: side A of end 0 / 1 is set 0 / 1, side B is set 3 / 2
+            const int s = side == 0 ? e : 3 - e;
+            const int ns = s == 0 ? cnt[0] : s == 1 ? cnt[1] : s == 2 ? cnt[2] : cnt[3];
+            const int os = s == 0 ? off[0] : s == 1 ? off[1] : s == 2 ? off[2] : off[3];
+            const bool have = act && ((hsm >> s) & 1u);
             const uint32_t kb = act ? outb[e * ow + c] : 0u, kq = act ? outq[e * ow + c] : 0u;  // kept side
-            uint32_t vb[2] = {0, 0}, vq[2] = {0, 0};
-            for (int side = 0; side < 2; side++) {
-                const int s = side == 0 ? sa : sb;  // per lane: lanes of both ends mix here
-                if (!act || !hs[s]) continue;
-                if (kq != 0 && (int)((kb >> 4) & 1) == side) {
-                    vb[side] = kb & 0x0F;
-                    vq[side] = kq;
-                    continue;
-                }
+            uint32_t vb = 0, vq = 0;
+            if (have && kq != 0 && (int)((kb >> 4) & 1) == side) {
+                vb = kb & 0x0F;
+                vq = kq;
+            } else if (have) {
                 int32_t D0 = 0, D1 = 0, D2 = 0, D3 = 0;
-                for (int i = 0; i < cnt[s]; i++) {
-                    const uint32_t d = dlist[off[s] + i];
+                for (int i = 0; i < ns; i++) {
+                    const uint32_t d = dlist[os + i];
                     if (c >= (int)((d >> 16) & 0x7FFF)) continue;
                     const uint32_t idx = (d & 0x80000000u) ? (d & 0xFFFF) - c : (d & 0xFFFF) + c;
                     const uint32_t braw = bimg[idx];
@@ -1208,16 +1214,18 @@ __global__ __launch_bounds__(kWave *kSmallMaxWaves, kSmallMinWaves) __attribute_
                 if (best != 2) S += term32(D2 - Db);
                 if (best != 3) S += term32(D3 - Db);
                 const int Q = phred_of(S, thr);
-                vb[side] = Q < 2 ? kN : (1u << best);
-                vq[side] = Q < 2 ? 2u : (uint32_t)Q;
+                vb = Q < 2 ? kN : (1u << best);
+                vq = Q < 2 ? 2u : (uint32_t)Q;
             }
-            if (act) {
+            const uint32_t pb = (uint32_t)__shfl_xor((int)vb, 1, kWave), pq = (uint32_t)__shfl_xor((int)vq, 1, kWave);
+            if (act && side == 0) {
+                const bool ha = (hsm >> e) & 1u, hb = (hsm >> (3 - e)) & 1u;
                 uint32_t ob, oq;
-                if (hs[sa] && hs[sb]) {
-                    duplex_col(vb[0], vq[0], vb[1], vq[1], ob, oq);
+                if (ha && hb) {
+                    duplex_col(vb, vq, pb, pq, ob, oq);
                 } else {
-                    ob = hs[sa] ? vb[0] : vb[1];
-                    oq = hs[sa] ? vq[0] : vq[1];
+                    ob = ha ? vb : pb;
+                    oq = ha ? vq : pq;
                 }
                 outb[e * ow + c] = (uint8_t)ob;
                 outq[e * ow + c] = (uint8_t)oq;

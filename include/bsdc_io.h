@@ -17,7 +17,7 @@
 extern "C" {
 #endif
 
-#define BSDC_IO_ABI_VERSION 1
+#define BSDC_IO_ABI_VERSION 2
 #define BSDC_IO_EFORMAT (-10) /* not BGZF/BAM, truncated, bad CRC */
 #define BSDC_IO_EIO (-11)     /* open/read/write failed */
 
@@ -98,6 +98,14 @@ typedef struct {
 int32_t bsdc_bam_write(const char *path, const char *header_text, int64_t header_len, int32_t n_ref,
                        const int64_t *ref_name_off, const char *ref_name_buf, const int64_t *ref_len,
                        const bsdc_bam_records *r, int32_t level, int32_t n_threads);
+
+/* Paired FASTQ of records, as picard SamToFastq F=path1 F2=path2 writes them (the step after the
+ * duplex call, main.snake.py:167-177; parity unpinned): "@name/1" or "/2", SEQ, "+", QUAL+33,
+ * reverse-strand records reverse-complemented; secondary, supplementary and QC-fail records
+ * skipped.  The written records must come as adjacent first/second-of-pair mates of one name
+ * (an error otherwise, as picard raises on an unpaired mate).  Each file is BGZF-framed gzip. */
+int32_t bsdc_fastq_write(const char *path1, const char *path2, const bsdc_bam_records *r, int32_t level,
+                         int32_t n_threads);
 
 /* Consensus RX per family for the duplex output records (fgbio's consensus
  * UMI, parity unpinned): every family record's RX, a /B-strand record's two '-'-separated halves

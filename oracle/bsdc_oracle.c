@@ -496,7 +496,7 @@ static int to_source_read(const orec *r, const orc_records *in, srcread *s) {
     }
     while (keep > 0 && s->b[keep - 1] == 'N') keep--;
     s->len = keep;
-    /* simplified cigar: sequencing orientation, M/=/X -> M, merged, truncated to `keep` query bases */
+    /* simplified cigar: sequencing orientation, M/=/X/S -> M, merged, truncated to `keep` query bases */
     s->cig = (uint32_t *)malloc(sizeof(uint32_t) * ((size_t)r->ncig + 1));
     s->ncig = 0;
     int32_t q = 0;
@@ -504,8 +504,8 @@ static int to_source_read(const orec *r, const orc_records *in, srcread *s) {
         uint32_t c = neg ? r->cig[r->ncig - 1 - j] : r->cig[j];
         int op = cig_op(c);
         int32_t l = cig_len(c);
-        if (op == OP_EQ || op == OP_X) op = OP_M;
-        if (op == OP_H || op == OP_S) continue;
+        if (op == OP_EQ || op == OP_X || op == OP_S) op = OP_M; /* soft-clipped bases stay in the source read */
+        if (op == OP_H) continue;
         if (op == OP_M || op == OP_I) {
             if (q + l > keep) l = keep - q;
             q += l;

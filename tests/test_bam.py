@@ -217,3 +217,56 @@ def test_fasta_reader(tmp_path):
     assert ref.contig_off[1] == -1
     got = R.unpack_nibbles(ref.packed, ref.n_nibbles)[ref.contig_off[0]:ref.contig_off[0] + ref.contig_len[0]]
     assert np.array_equal(got, codes)
+
+
+def _py_fastq(recs, mate):
+    """Python restatement of picard SamToFastq's record text for first (mate 1) / second (2) of pair."""
+    out = []
+    for k in range(recs.n):
+        fl = int(recs.flag[k])
+        if fl & 0xB00 or not fl & 1 or bool(fl & 0x40) != (mate == 1):
+            continue
+        s = recs.seq[recs.seq_off[k]:recs.seq_off[k + 1]]
+        q = recs.qual[recs.seq_off[k]:recs.seq_off[k + 1]]
+        seq = R.NT16_TO_ASCII[s].tobytes().decode()
+        if fl & 16:
+            seq = seq[::-1].translate(str.maketrans("ACGTMRWSYKVHDBN=", "TGCAKYWSRMBDHVN="))
+            q = q[::-1]
+        out.append("@%s/%d\n%s\n+\n%s\n" % (recs.names[k].decode(), mate, seq, (q + 33).tobytes().decode()))
+    return "".join(out)
+
+
+def test_fastq_of_the_oracle_consensus(tmp_path):
+    s, raw = _messy(300, seed=9)
+    res = oracle.run(raw, s.ref)
+    cons = type("C", (), {})()
+    cons.fam_rec_off, cons.fam_src = res.fam_rec_off, res.fam_src
+    cons.status, cons.fam_mi, cons.length = res.status.astype(np.uint8), res.fam_mi, res.cons_len
+    cons.seq, cons.qual = res.cons_seq, res.cons_qual
+    recs = bam.duplex_records(cons, raw, "libA")
+    p1, p2 = str(tmp_path / "r_1.fq.gz"), str(tmp_path / "r_2.fq.gz")
+    bam.write_fastq(p1, p2, recs, level=5, threads=3)
+    for p, mate in ((p1, 1), (p2, 2)):
+        with gzip.open(p, "rt") as fh:
+            assert fh.read() == _py_fastq(recs, mate)
+
+
+def test_fastq_orientation_and_errors(tmp_path):
+    b = R._Builder()
+    seq = np.asarray([1, 2, 4, 8, 15], np.uint8)
+    for nm, fl in ((b"a", 77), (b"a", 141), (b"b", 83), (b"b", 163), (b"c", 77 | 0x100), (b"d", 77 | 0x200),
+                   (b"d", 141 | 0x200)):
+        b.add(nm, fl, -1, -1, 0, [], seq, np.asarray([30, 31, 32, 33, 2], np.uint8), -1, -1, 0, b"", [("MI", "Z", "1/A")])
+    recs = bam.records_to_bam(b.finish())
+    p1, p2 = str(tmp_path / "x_1.fq.gz"), str(tmp_path / "x_2.fq.gz")
+    bam.write_fastq(p1, p2, recs)
+    with gzip.open(p1, "rt") as fh:
+        assert fh.read() == "@a/1\nACGTN\n+\n?@AB#\n@b/1\nNACGT\n+\n#BA@?\n"
+    with gzip.open(p2, "rt") as fh:
+        assert fh.read() == "@a/2\nACGTN\n+\n?@AB#\n@b/2\nACGTN\n+\n?@AB#\n"
+    for bad in (((b"a", 77),), ((b"a", 77), (b"z", 141)), ((b"a", 141), (b"a", 77)), ((b"a", 4),)):
+        b = R._Builder()
+        for nm, fl in bad:
+            b.add(nm, fl, -1, -1, 0, [], seq, np.full(5, 30, np.uint8), -1, -1, 0, b"", [("MI", "Z", "1/A")])
+        with pytest.raises(ValueError):
+            bam.write_fastq(p1, p2, bam.records_to_bam(b.finish()))
