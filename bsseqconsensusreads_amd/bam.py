@@ -470,3 +470,26 @@ def step5(in_bam: str, fasta: str, out_bam: Optional[str], engine=None, prefix: 
         write_fastq(fastq[0], fastq[1], recs, level, threads)
     return {"records_in": raw.n, "families": int(cons.status.shape[0]),
             "families_emitted": int(((cons.status & 1) != 0).sum()), "records_out": recs.n}
+
+
+def molecular(in_bam: str, out_bam: Optional[str], engine=None, prefix: Optional[str] = None, threads: int = 0,
+              level: int = 6, fastq: Optional[Tuple[str, str]] = None) -> dict:
+    """Rule call_consensus_reads_molecular (main.snake.py:46-55, fgbio CallMolecularConsensusReads)
+    on files; with `fastq`, also consensus_to_fq_unfiltered (main.snake.py:58-67)."""
+    from . import pipeline
+    from .device import Engine
+    header, raw = read_bam(in_bam, threads)
+    own = engine is None
+    eng = Engine(0) if own else engine
+    try:
+        cons, rm = pipeline.run_molecular(eng, raw)
+    finally:
+        if own:
+            eng.close()
+    recs = duplex_records(cons, rm, read_name_prefix(header) if prefix is None else prefix, threads)
+    if out_bam is not None:
+        write_bam(out_bam, output_header(header), recs, level, threads)
+    if fastq is not None:
+        write_fastq(fastq[0], fastq[1], recs, level, threads)
+    return {"records_in": raw.n, "families": int(cons.status.shape[0]),
+            "families_emitted": int(((cons.status & 1) != 0).sum()), "records_out": recs.n}

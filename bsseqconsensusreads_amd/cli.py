@@ -1,0 +1,66 @@
+"""Command lines for the Snakemake rules this package replaces.
+
+    python -m bsseqconsensusreads_amd.cli step5 --reference FA IN.bam OUT.bam [--fastq1 F1 --fastq2 F2]
+        rules convert_Bstrain, extend, groupsort_convert, callduplex (main.snake.py:121-164), and
+        with --fastq1/--fastq2 also consensusduplex_to_fq (main.snake.py:167-177)
+    python -m bsseqconsensusreads_amd.cli molecular IN.bam OUT.bam [--fastq1 F1 --fastq2 F2]
+        rule call_consensus_reads_molecular (main.snake.py:46-55) [+ consensus_to_fq_unfiltered]
+
+OUT.bam may be '-' to skip the BAM when only the FASTQ pair is wanted.  Errors exit non-zero with
+the message on stderr, so Snakemake aborts the rule and removes partial outputs, as it does for
+the reference tools (tools/2.extend_gap.py:179-180 raises on a record without MI).
+"""
+from __future__ import annotations
+
+import argparse
+import json
+import sys
+
+
+def parse(argv):
+    ap = argparse.ArgumentParser(prog="bsseqconsensusreads_amd.cli")
+    sub = ap.add_subparsers(dest="cmd", required=True)
+    for name in ("step5", "molecular"):
+        p = sub.add_parser(name)
+        if name == "step5":
+            p.add_argument("--reference", "-r", required=True, help="FASTA of the alignment (tools/1 --reference)")
+        p.add_argument("input")
+        p.add_argument("output", help="consensus BAM, or '-' for none")
+        p.add_argument("--fastq1")
+        p.add_argument("--fastq2")
+        p.add_argument("--read-name-prefix", default=None)
+        p.add_argument("--threads", type=int, default=8)
+        p.add_argument("--compression", type=int, default=6)
+        p.add_argument("--device", type=int, default=0)
+    a = ap.parse_args(argv)
+    if (a.fastq1 is None) != (a.fastq2 is None):
+        ap.error("--fastq1 and --fastq2 go together")
+    if a.output == "-" and a.fastq1 is None:
+        ap.error("nothing to write: give OUT.bam or --fastq1/--fastq2")
+    return a
+
+
+def main(argv=None) -> int:
+    a = parse(sys.argv[1:] if argv is None else argv)
+    from . import bam
+    from .device import Engine
+    out = None if a.output == "-" else a.output
+    fq = (a.fastq1, a.fastq2) if a.fastq1 else None
+    try:
+        eng = Engine(a.device)
+        try:
+            if a.cmd == "step5":
+                info = bam.step5(a.input, a.reference, out, eng, a.read_name_prefix, a.threads, a.compression, fq)
+            else:
+                info = bam.molecular(a.input, out, eng, a.read_name_prefix, a.threads, a.compression, fq)
+        finally:
+            eng.close()
+    except Exception as e:  # noqa: BLE001 -- the rule fails with the message, like the tools do
+        print("%s: %s" % (type(e).__name__, e), file=sys.stderr)
+        return 1
+    print(json.dumps(info), file=sys.stderr)
+    return 0
+
+
+if __name__ == "__main__":
+    sys.exit(main())

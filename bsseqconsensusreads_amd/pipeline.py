@@ -6,9 +6,12 @@
 * ``run_step5``  -- convert_Bstrain -> extend -> groupsort_convert -> callduplex in one device pass;
   returns the consensus pair per family and, on request, the tool-2 records (parity dump).
 * ``run_duplex`` -- callduplex alone on already converted + extended records.
+* ``run_molecular`` -- pipeline step 1, fgbio CallMolecularConsensusReads (main.snake.py:46-55):
+  the same single-strand vote over raw MI groups, one consensus pair (R1, R2) per MI.
 """
 from __future__ import annotations
 
+import dataclasses
 from dataclasses import dataclass
 from typing import List, Optional
 
@@ -240,3 +243,35 @@ def run_duplex(engine: Engine, raw: R.RawRecords) -> Consensus:
     db = engine.upload(fb)
     engine.run(db, MODE_VOTE)
     return consensus_from_output(fb, db.fetch())
+
+
+def molecular_records(raw: R.RawRecords) -> R.RawRecords:
+    """The input of CallMolecularConsensusReads (main.snake.py:46-55) as records the vote reads:
+    fgbio groups consecutive records of one MI tag (GroupReadsByUmi output order), the /A and /B
+    molecules of a duplex apart.  Each run becomes its own MI id with the full tag as its name, and
+    every record is marked strand A, so the kernel's X set is the run's R1s and Y its R2s with no
+    BA side: the duplex combine passes the two single-strand consensus reads through unchanged."""
+    n = raw.n
+    key = raw.mi_id.astype(np.int64) * 4 + (raw.mi_strand.astype(np.int64) + 1)
+    brk = np.ones(n, bool)
+    if n:
+        brk[1:] = key[1:] != key[:-1]
+    run = np.cumsum(brk) - 1
+    starts = np.nonzero(brk)[0]
+    suffix = {0: "/A", 1: "/B", -1: ""}
+    names = [raw.mi_names[int(raw.mi_id[k])] + suffix[int(raw.mi_strand[k])] if raw.mi_id[k] >= 0 else ""
+             for k in starts]
+    mi_id = np.where(raw.mi_id >= 0, run, -1).astype(np.int32)
+    mi_strand = np.where(raw.mi_id >= 0, 0, -1).astype(np.int8)
+    return dataclasses.replace(raw, mi_id=mi_id, mi_strand=mi_strand, mi_names=names)
+
+
+def run_molecular(engine: Engine, raw: R.RawRecords):
+    """fgbio CallMolecularConsensusReads with the step-1 flags (main.snake.py:54: pre 45, post 30,
+    min-reads 1, overlapping bases on) -> (Consensus over the runs, the run records).  Consensus
+    family f is MI run f; its R1 / R2 are the single-strand consensus of the run's R1s / R2s."""
+    rm = molecular_records(raw)
+    fb = build_family_batch(rm, "vote", family_order="mi-group")
+    db = engine.upload(fb)
+    engine.run(db, MODE_VOTE)
+    return consensus_from_output(fb, db.fetch()), rm

@@ -268,6 +268,34 @@ class _Builder:
             la_tag=np.asarray(c["la"], dtype=np.int32), rd_tag=np.asarray(c["rd"], dtype=np.int32))
 
 
+def _gather_ranges(off: np.ndarray, ln: np.ndarray):
+    """Concatenated index ranges [off[k], off[k] + ln[k]) and the new per-record offsets."""
+    ln = ln.astype(np.int64)
+    new_off = np.zeros(ln.shape[0], np.int64)
+    if ln.shape[0]:
+        new_off[1:] = np.cumsum(ln)[:-1]
+    idx = np.repeat(off.astype(np.int64) - new_off, ln) + np.arange(int(ln.sum()), dtype=np.int64)
+    return idx, new_off
+
+
+def take(raw: RawRecords, idx: np.ndarray) -> RawRecords:
+    """Records idx[0], idx[1], ... of `raw` as a new stream (name / MI tables shared)."""
+    idx = np.asarray(idx, np.int64)
+    si, so = _gather_ranges(raw.seq_off[idx], raw.l_seq[idx])
+    ci, co = _gather_ranges(raw.cig_off[idx], raw.n_cig[idx])
+    has_mc = raw.mc_off[idx] >= 0
+    mi_, mo = _gather_ranges(np.where(has_mc, raw.mc_off[idx], 0), np.where(has_mc, raw.mc_n[idx], 0))
+    sub = lambda a: None if a is None else a[idx]  # noqa: E731
+    return RawRecords(
+        flag=raw.flag[idx], tid=raw.tid[idx], pos=raw.pos[idx], mapq=raw.mapq[idx], l_seq=raw.l_seq[idx],
+        seq_off=so, seq=raw.seq[si], qual=raw.qual[si], cig_off=co, n_cig=raw.n_cig[idx], cigar=raw.cigar[ci],
+        next_tid=raw.next_tid[idx], next_pos=raw.next_pos[idx], tlen=raw.tlen[idx], name_id=raw.name_id[idx],
+        names=raw.names, mi_id=raw.mi_id[idx], mi_strand=raw.mi_strand[idx], mi_names=raw.mi_names,
+        mc_off=np.where(has_mc, mo, -1), mc_n=raw.mc_n[idx], mc_cigar=raw.mc_cigar[mi_],
+        aux=None if raw.aux is None else [raw.aux[int(k)] for k in idx], la_tag=sub(raw.la_tag),
+        rd_tag=sub(raw.rd_tag))
+
+
 def records_from_dicts(recs: Sequence[dict]) -> RawRecords:
     """Fixture records ({name, flag, tid, pos, cigar, seq, qual, tags, ...}) -> RawRecords."""
     b = _Builder()

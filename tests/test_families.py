@@ -131,3 +131,42 @@ def test_rd_prediction_matches_tool1():
     got = batch.predict_rd(raw, s.ref, sel, sL, L)
     assert sel.shape[0] > 100 and want.any()
     assert np.array_equal(got, want)
+
+
+def test_molecular_runs():
+    """Step 1's families (CallMolecularConsensusReads): consecutive records of one full MI tag,
+    /A and /B apart, in input order; every record on the A side."""
+    from bsseqconsensusreads_amd import pipeline
+
+    s = synth.generate("C2", 60, seed=4, device="cpu", genome_len=50_000)
+    raw = R.take(s.raw, np.lexsort((s.raw.mi_strand, s.raw.mi_id)))
+    rm = pipeline.molecular_records(raw)
+    assert (rm.mi_strand == 0).all()
+    full = [raw.mi_names[int(raw.mi_id[k])] + "/" + "AB"[int(raw.mi_strand[k])] for k in range(raw.n)]
+    runs = [full[0]] + [full[k] for k in range(1, raw.n) if full[k] != full[k - 1]]
+    assert rm.mi_names == runs and len(set(runs)) == len(runs)
+    assert all(rm.mi_names[int(rm.mi_id[k])] == full[k] for k in range(raw.n))
+    fb = batch.build_family_batch(rm, "vote", family_order="mi-group")
+    assert fb.n_fam == len(runs) and np.array_equal(fb.fam_mi, np.arange(len(runs)))
+
+
+def test_take_round_trip():
+    s = synth.generate("C4", 40, seed=5, device="cpu", genome_len=50_000)
+    raw = synth.messify(s.raw, frac=0.3, seed=5)
+    idx = np.random.default_rng(0).permutation(raw.n)
+    t = R.take(raw, idx)
+    back = R.take(t, np.argsort(idx))
+    for k in ("flag", "pos", "l_seq", "seq", "qual", "cigar", "n_cig", "mc_n", "mc_cigar", "mi_id", "name_id"):
+        assert np.array_equal(getattr(back, k), getattr(raw, k)), k
+
+
+def test_cli_arguments():
+    from bsseqconsensusreads_amd import cli
+
+    a = cli.parse(["step5", "--reference", "g.fa", "in.bam", "out.bam", "--threads", "3"])
+    assert (a.cmd, a.reference, a.input, a.output, a.threads, a.fastq1) == ("step5", "g.fa", "in.bam", "out.bam", 3, None)
+    a = cli.parse(["molecular", "in.bam", "-", "--fastq1", "a", "--fastq2", "b"])
+    assert a.output == "-" and (a.fastq1, a.fastq2) == ("a", "b")
+    for bad in (["step5", "in.bam", "out.bam"], ["molecular", "in.bam", "-"], ["molecular", "i", "o", "--fastq1", "a"]):
+        with pytest.raises(SystemExit):
+            cli.parse(bad)

@@ -199,3 +199,66 @@ def test_step5_bam_end_to_end(engine, tmp_path):
             assert out.names[int(out.name_id[k])] == ("L1:%s" % raw.mi_names[int(ref.fam_mi[f])]).encode()
             assert np.array_equal(out.seq[o:o + L], ref.cons_seq[f, e, :L])
             assert np.array_equal(out.qual[o:o + L], ref.cons_qual[f, e, :L])
+
+
+def _grouped(cfg, n_fam, seed, messy=0.0):
+    """A GroupReadsByUmi-like stream: every MI's /A and /B molecules contiguous."""
+    s = synth.generate(cfg, n_fam, seed=seed, device="cpu", genome_len=200_000)
+    raw = synth.messify(s.raw, frac=messy, seed=seed) if messy else s.raw
+    return s, R.take(raw, np.lexsort((raw.mi_strand, raw.mi_id)))
+
+
+@pytest.mark.parametrize("cfg,n_fam,messy", [("C1", 300, 0.0), ("C2", 800, 0.2), ("C3", 40, 0.0), ("C4", 150, 0.1)])
+def test_molecular_vs_oracle(engine, cfg, n_fam, messy):
+    """Step 1 (CallMolecularConsensusReads, main.snake.py:46-55): the same vote kernel over MI runs
+    (no BA side); equal to the restatement run as callduplex on the run records."""
+    s, raw = _grouped(cfg, n_fam, seed=21, messy=messy)
+    cons, rm = pipeline.run_molecular(engine, raw)
+    ref = oracle.run(rm, s.ref, run_tools=False, family_order="mi-group")
+    assert_consensus_equal(cons, ref, "molecular " + cfg)
+    assert ((cons.status & 4) == 0).all()  # no BA side anywhere
+    assert (cons.status & 1).sum() > 0.5 * len(rm.mi_names)
+
+
+def test_cli_step5_and_molecular_files(engine, tmp_path):
+    """The command lines the Snakemake rules call (bsseqconsensusreads_amd/cli.py): BAM + FASTQ
+    outputs of both steps agree with each other and with the restatement."""
+    import gzip
+
+    from bsseqconsensusreads_amd import bam, cli
+
+    s, raw = _grouped("C2", 300, seed=22)
+    codes = R.unpack_nibbles(s.ref.packed, s.ref.n_nibbles)
+    fa = tmp_path / "g.fa"
+    fa.write_text(">%s\n%s\n" % (s.ref.names[0], R.NT16_TO_ASCII[codes].tobytes().decode()))
+    hdr = bam.BamHeader("@HD\tVN:1.6\tSO:unsorted\n@SQ\tSN:%s\tLN:%d\n@RG\tID:x\tLB:L1\n" % (
+        s.ref.names[0], len(codes)), [s.ref.names[0]], np.asarray([len(codes)], np.int64))
+    inp = str(tmp_path / "in.bam")
+    bam.write_bam(inp, hdr, bam.records_to_bam(raw))
+    p = lambda n: str(tmp_path / n)  # noqa: E731
+    assert cli.main(["step5", "--reference", str(fa), inp, p("d.bam"), "--fastq1", p("d1.fq.gz"),
+                     "--fastq2", p("d2.fq.gz"), "--threads", "4"]) == 0
+    assert cli.main(["molecular", inp, "-", "--fastq1", p("m1.fq.gz"), "--fastq2", p("m2.fq.gz")]) == 0
+    assert cli.main(["molecular", p("missing.bam"), p("x.bam")]) == 1
+    _, d = bam.read_bam(p("d.bam"))
+    ref = oracle.run(raw, s.ref)
+    em = np.nonzero(ref.status == 1)[0]
+    assert d.n == 2 * em.shape[0]
+    with gzip.open(p("d1.fq.gz"), "rt") as fh:
+        lines = fh.read().split("\n")
+    assert len(lines) == 4 * em.shape[0] + 1
+    for i, f in enumerate(em[:50]):
+        L = int(ref.cons_len[f, 0])
+        assert lines[4 * i] == "@L1:%s/1" % raw.mi_names[int(ref.fam_mi[f])]
+        assert lines[4 * i + 1] == R.NT16_TO_ASCII[ref.cons_seq[f, 0, :L]].tobytes().decode()
+        assert lines[4 * i + 3] == (ref.cons_qual[f, 0, :L] + 33).tobytes().decode()
+    rm = pipeline.molecular_records(raw)
+    mref = oracle.run(rm, s.ref, run_tools=False, family_order="mi-group")
+    mem = np.nonzero(mref.status == 1)[0]
+    with gzip.open(p("m2.fq.gz"), "rt") as fh:
+        lines = fh.read().split("\n")
+    assert len(lines) == 4 * mem.shape[0] + 1
+    for i, f in enumerate(mem[:50]):
+        L = int(mref.cons_len[f, 1])
+        assert lines[4 * i] == "@L1:%s/2" % rm.mi_names[int(mref.fam_mi[f])]
+        assert lines[4 * i + 1] == R.NT16_TO_ASCII[mref.cons_seq[f, 1, :L]].tobytes().decode()
