@@ -76,6 +76,8 @@ def _load():
     lib.bsdc_rx_consensus.restype = C.c_int64
     lib.bsdc_fastq_write.argtypes = [C.c_char_p, C.c_char_p, C.POINTER(_Records), C.c_int32, C.c_int32]
     lib.bsdc_fastq_write.restype = C.c_int32
+    lib.bsdc_family_image.argtypes = [C.c_int64, _P, _P, _P, _P, _P, C.c_int64, _P, _P, C.c_int32]
+    lib.bsdc_family_image.restype = C.c_int32
     if lib.bsdc_io_abi_version() != BSDC_IO_ABI_VERSION:
         raise RuntimeError("libbsdc_io ABI %d != %d" % (lib.bsdc_io_abi_version(), BSDC_IO_ABI_VERSION))
     _lib = lib
@@ -326,6 +328,27 @@ def _records_struct(recs: OutRecordsBam, keep: list) -> _Records:
                     c(recs.cig_off, np.int64), c(recs.cigar, np.uint32), c(recs.seq_off, np.int64),
                     c(recs.seq, np.uint8), c(recs.qual, np.uint8), c(recs.aux.off, np.int64),
                     c(recs.aux.buf, np.uint8))
+
+
+def family_image(src_off, length, dst_off, seq, qual, n_slots: int, packed: np.ndarray, qual_out: np.ndarray,
+                 threads: int = 0):
+    """batch.build_family_batch's image: record r's bases / quals at src_off[r] -> nibble / byte
+    dst_off[r] + 1 of `packed` / `qual_out` (zeroed by the caller; libbsdc_io)."""
+    lib = _load()
+    so = np.ascontiguousarray(src_off, np.int64)
+    ln = np.ascontiguousarray(length, np.int64)
+    do = np.ascontiguousarray(dst_off, np.int64)
+    sq = np.ascontiguousarray(seq, np.uint8)
+    ql = np.ascontiguousarray(qual, np.uint8)
+    if packed.shape[0] * 2 < n_slots or qual_out.shape[0] < n_slots or not (packed.flags.c_contiguous and
+                                                                           qual_out.flags.c_contiguous):
+        raise ValueError("family image outputs too small")
+    if so.shape[0] and (int((so + ln).max()) > sq.shape[0] or int((so + ln).max()) > ql.shape[0]):
+        raise ValueError("family image: record past the end of seq / qual")
+    rc = lib.bsdc_family_image(so.shape[0], _ptr(so), _ptr(ln), _ptr(do), _ptr(sq), _ptr(ql), int(n_slots),
+                               _ptr(packed), _ptr(qual_out), int(threads))
+    if rc != 0:
+        raise ValueError(lib.bsdc_io_last_error().decode())
 
 
 def write_fastq(path1: str, path2: str, recs: OutRecordsBam, level: int = 6, threads: int = 0):

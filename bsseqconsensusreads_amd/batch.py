@@ -507,20 +507,12 @@ def build_family_batch(raw: R.RawRecords, mode: str = "full", ref: Optional[R.Re
     if n_slots >= 1 << 32:
         raise ValueError("batch too large for 32-bit offsets; split it")
     total = int(Lb.sum()) if nr else 0
-    codes = np.zeros(n_slots, np.uint8)
+    seq = np.zeros(n_slots // 2, np.uint8)
     qual = np.zeros(n_slots, np.uint8)
     shift = raw.seq_off[order] + sL[order]
-    step = 1 << 18
-    for c0 in range(0, nr, step):
-        c1 = min(nr, c0 + step)
-        ln = Lb[c0:c1]
-        m = int(ln.sum())
-        rel = np.arange(m, dtype=np.int64) - np.repeat(np.cumsum(ln) - ln, ln)
-        srcpos = np.repeat(shift[c0:c1], ln) + rel
-        dst = np.repeat(rec_off[c0:c1] + 1, ln) + rel
-        codes[dst] = raw.seq[srcpos]
-        qual[dst] = raw.qual[srcpos]
-    seq = R.pack_nibbles(codes)
+    if nr:
+        from .bam import family_image  # libbsdc_io: per-record copies, OpenMP over records
+        family_image(shift, Lb, rec_off, raw.seq, raw.qual, n_slots, seq, qual)
 
     # stripped cigars, complex records
     nops = kn[order]

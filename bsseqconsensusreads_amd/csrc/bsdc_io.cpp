@@ -732,3 +732,32 @@ extern "C" int32_t bsdc_fastq_write(const char *path1, const char *path2, const 
     }
     return 0;
 }
+
+extern "C" int32_t bsdc_family_image(int64_t n_rec, const int64_t *src_off, const int64_t *len, const int64_t *dst_off,
+                                     const uint8_t *seq, const uint8_t *qual, int64_t n_slots, uint8_t *packed,
+                                     uint8_t *qual_out, int32_t n_threads) {
+    set_threads(n_threads);
+    int bad = 0;
+#pragma omp parallel for schedule(dynamic, 1024) reduction(| : bad)
+    for (int64_t r = 0; r < n_rec; r++) {
+        const int64_t d = dst_off[r] + 1, l = len[r];
+        if (dst_off[r] < 0 || (dst_off[r] & 1) || d + l > n_slots) {
+            bad |= 1;
+            continue;
+        }
+        const uint8_t *s = seq + src_off[r];
+        memcpy(qual_out + d, qual + src_off[r], (size_t)l);
+        // nibble d (odd) is the low half of byte d / 2; then whole bytes, then a last high nibble
+        uint8_t *p = packed + (d >> 1);
+        int64_t j = 0;
+        if (l > 0) {
+            *p = (uint8_t)((*p & 0xF0) | (s[0] & 15));
+            p++;
+            j = 1;
+        }
+        for (; j + 1 < l; j += 2) *p++ = (uint8_t)(((s[j] & 15) << 4) | (s[j + 1] & 15));
+        if (j < l) *p = (uint8_t)(((s[j] & 15) << 4) | (*p & 0x0F));
+    }
+    if (bad) return fail(BSDC_IO_EFORMAT, "family image: record slot out of range or misaligned");
+    return 0;
+}

@@ -107,6 +107,14 @@ int32_t bsdc_bam_write(const char *path, const char *header_text, int64_t header
 int32_t bsdc_fastq_write(const char *path1, const char *path2, const bsdc_bam_records *r, int32_t level,
                          int32_t n_threads);
 
+/* Host side of the family batch (bsseqconsensusreads_amd/batch.py, include/bsdc.h layout): record r's
+ * len[r] bases and quals, from seq/qual (nt16 codes and phred, one per byte) at src_off[r], go to
+ * nibble / byte dst_off[r] + 1 of the image (dst_off even; the caller zeroes both outputs):
+ * packed holds n_slots nibbles, two per byte, high nibble first; qual_out n_slots bytes. */
+int32_t bsdc_family_image(int64_t n_rec, const int64_t *src_off, const int64_t *len, const int64_t *dst_off,
+                          const uint8_t *seq, const uint8_t *qual, int64_t n_slots, uint8_t *packed,
+                          uint8_t *qual_out, int32_t n_threads);
+
 /* Consensus RX per family for the duplex output records (fgbio's consensus
  * UMI, parity unpinned): every family record's RX, a /B-strand record's two '-'-separated halves
  * swapped, then per position the most common character over the RX values of the most common

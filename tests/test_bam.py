@@ -270,3 +270,28 @@ def test_fastq_orientation_and_errors(tmp_path):
             b.add(nm, fl, -1, -1, 0, [], seq, np.full(5, 30, np.uint8), -1, -1, 0, b"", [("MI", "Z", "1/A")])
         with pytest.raises(ValueError):
             bam.write_fastq(p1, p2, bam.records_to_bam(b.finish()))
+
+
+def test_family_image_matches_numpy():
+    """libbsdc_io's family image (batch.build_family_batch) against a numpy restatement of the
+    per-base scatter and the BAM nibble packing."""
+    s, raw = _messy(300, seed=11)
+    rng = np.random.default_rng(1)
+    n = raw.n
+    L = raw.l_seq.astype(np.int64)
+    cap4 = (L + 2 + 3) & ~np.int64(3)
+    dst = np.zeros(n, np.int64)
+    dst[1:] = np.cumsum(cap4 + 4 * rng.integers(0, 3, n))[:-1]
+    n_slots = int(dst[-1] + cap4[-1]) + 64
+    src = raw.seq_off.astype(np.int64)
+    packed = np.zeros(n_slots // 2, np.uint8)
+    qual = np.zeros(n_slots, np.uint8)
+    bam.family_image(src, L, dst, raw.seq, raw.qual, n_slots, packed, qual, threads=4)
+    codes = np.zeros(n_slots, np.uint8)
+    q2 = np.zeros(n_slots, np.uint8)
+    for k in range(n):
+        codes[dst[k] + 1:dst[k] + 1 + L[k]] = raw.seq[src[k]:src[k] + L[k]]
+        q2[dst[k] + 1:dst[k] + 1 + L[k]] = raw.qual[src[k]:src[k] + L[k]]
+    assert np.array_equal(packed, R.pack_nibbles(codes)) and np.array_equal(qual, q2)
+    with pytest.raises(ValueError):
+        bam.family_image(src, L, dst + 1, raw.seq, raw.qual, n_slots, packed, qual)
