@@ -259,6 +259,15 @@ def _concat_fields(parts, n):
     return StringTable(buf, off)
 
 
+def _take_table(t: StringTable, idx: np.ndarray) -> StringTable:
+    """Entries idx[0], idx[1], ... of a packed table."""
+    ln = (t.off[1:] - t.off[:-1])[idx]
+    off = np.zeros(idx.shape[0] + 1, np.int64)
+    off[1:] = np.cumsum(ln)
+    src = np.repeat(t.off[:-1][idx] - off[:-1], ln) + np.arange(int(off[-1]), dtype=np.int64)
+    return StringTable(t.buf[src], off)
+
+
 def _synthetic_fields(raw: R.RawRecords):
     """Vectorised MI / MC aux and QNAMEs of a synthetic stream (decimal lazy names, one-op MC)."""
     n = raw.n
@@ -442,18 +451,30 @@ def duplex_records(cons, raw: R.RawRecords, prefix: str, threads: int = 0) -> Ou
     if width > 0:
         lib.bsdc_rx_consensus(nf_all, _ptr(fro), _ptr(fsrc), _ptr(strand), _ptr(aux.off), _ptr(aux.buf), _ptr(rx),
                               _ptr(rx_len), int(threads))
-    mi_names = raw.mi_names
-    pre = (prefix + ":").encode()
-    names, auxs = [], []
-    for f in em:
-        mi = mi_names[int(cons.fam_mi[f])]
-        mi = mi if isinstance(mi, bytes) else mi.encode()
-        nm = pre + mi
-        a = b"RGZA\0MIZ" + mi + b"\0"
-        if width > 0 and rx_len[f] > 0:
-            a += b"RXZ" + rx[f * width:f * width + rx_len[f]].tobytes() + b"\0"
-        names += [nm, nm]
-        auxs += [a, a]
+    # names "prefix:MI" and aux RG/MI/RX, both mates of a family alike (packed tables, no per-family
+    # Python objects for the byte work)
+    mi_ids = cons.fam_mi[em].astype(np.int64)
+    uniq, inv = np.unique(mi_ids, return_inverse=True)
+    mt = StringTable.from_list([(lambda m: m if isinstance(m, bytes) else m.encode())(raw.mi_names[int(i)])
+                                for i in uniq])
+    mlen = mt.off[1:] - mt.off[:-1]
+    mi = (mt.buf[np.repeat(mt.off[:-1][inv] - np.concatenate([[0], np.cumsum(mlen[inv])[:-1]]), mlen[inv])
+                 + np.arange(int(mlen[inv].sum()), dtype=np.int64)] if F else np.zeros(0, np.uint8),
+          np.concatenate([[0], np.cumsum(mlen[inv])]).astype(np.int64))
+    if width > 0:
+        rl = rx_len[em].astype(np.int64)
+        has = rl > 0
+        rxb = rx.reshape(-1, width)[em] if F else np.zeros((0, max(width, 1)), np.uint8)
+        rxv = (rxb[np.arange(width)[None, :] < rl[:, None]], np.concatenate([[0], np.cumsum(rl)]).astype(np.int64))
+        tag = (np.repeat(np.frombuffer(b"RXZ", np.uint8)[None, :], F, 0)[has].reshape(-1),
+               np.concatenate([[0], np.cumsum(np.where(has, 3, 0))]).astype(np.int64))
+        nul = (np.zeros(int(has.sum()), np.uint8), np.concatenate([[0], np.cumsum(has)]).astype(np.int64))
+        fam_aux = _concat_fields([b"RGZA\0MIZ", mi, b"\0", tag, rxv, nul], F)
+    else:
+        fam_aux = _concat_fields([b"RGZA\0MIZ", mi, b"\0"], F)
+    fam_names = _concat_fields([prefix.encode() + b":", mi], F)
+    two = np.repeat(np.arange(F, dtype=np.int64), 2)
+    names_t, auxs_t = _take_table(fam_names, two), _take_table(fam_aux, two)
     L = cons.length[em].astype(np.int64).reshape(-1)            # R1, R2, R1, R2 ...
     seq_off = np.zeros(n + 1, np.int64)
     seq_off[1:] = np.cumsum(L)
@@ -465,8 +486,8 @@ def duplex_records(cons, raw: R.RawRecords, prefix: str, threads: int = 0) -> Ou
     return OutRecordsBam(
         flag=np.tile(np.asarray([77, 141], np.uint16), F), tid=np.full(n, -1, np.int32), pos=np.full(n, -1, np.int32),
         mapq=np.zeros(n, np.uint8), next_tid=np.full(n, -1, np.int32), next_pos=np.full(n, -1, np.int32),
-        tlen=np.zeros(n, np.int32), names=StringTable.from_list(names), cig_off=np.zeros(n + 1, np.int64),
-        cigar=np.zeros(0, np.uint32), seq_off=seq_off, seq=seq, qual=qual, aux=StringTable.from_list(auxs))
+        tlen=np.zeros(n, np.int32), names=names_t, cig_off=np.zeros(n + 1, np.int64),
+        cigar=np.zeros(0, np.uint32), seq_off=seq_off, seq=seq, qual=qual, aux=auxs_t)
 
 
 def step5(in_bam: str, fasta: str, out_bam: Optional[str], engine=None, prefix: Optional[str] = None, threads: int = 0,

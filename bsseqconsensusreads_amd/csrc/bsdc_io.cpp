@@ -91,6 +91,54 @@ int64_t aux_int(const uint8_t *p) {
 
 }  // namespace
 
+// ids[k] = index of keys[k] among the distinct keys in first-seen order, appended to `uniq`; with
+// `present`, a record whose present[k] is empty gets -1.  Hash-sharded: the hashes and the shard
+// maps run in parallel, then the shards' first occurrences are merged by record index.
+static void intern(const std::vector<std::string_view> &keys, const std::vector<std::string_view> *present,
+            std::vector<int32_t> &ids, std::vector<std::string_view> &uniq) {
+    const int64_t n = (int64_t)keys.size();
+    constexpr int S = 256;
+    std::vector<uint32_t> shard((size_t)n);
+#pragma omp parallel for schedule(static)
+    for (int64_t k = 0; k < n; k++) {
+        const bool ok = present == nullptr || !(*present)[(size_t)k].empty();
+        shard[(size_t)k] = ok ? (uint32_t)(std::hash<std::string_view>{}(keys[(size_t)k]) % S) : (uint32_t)S;
+    }
+    std::vector<int64_t> start(S + 2, 0);
+    for (int64_t k = 0; k < n; k++) start[shard[(size_t)k] + 1]++;
+    for (int s = 0; s <= S; s++) start[s + 1] += start[s];
+    std::vector<int64_t> order((size_t)n), fill(start.begin(), start.end() - 1);
+    for (int64_t k = 0; k < n; k++) order[(size_t)fill[shard[(size_t)k]]++] = k;  // ascending k per shard
+    std::vector<int32_t> local((size_t)n, -1);
+    std::vector<std::vector<int64_t>> first(S);
+#pragma omp parallel for schedule(dynamic, 4)
+    for (int s = 0; s < S; s++) {
+        std::unordered_map<std::string_view, int32_t> m;
+        m.reserve((size_t)(start[s + 1] - start[s]));
+        for (int64_t i = start[s]; i < start[s + 1]; i++) {
+            const int64_t k = order[(size_t)i];
+            auto it = m.emplace(keys[(size_t)k], (int32_t)first[s].size());
+            if (it.second) first[s].push_back(k);
+            local[(size_t)k] = it.first->second;
+        }
+    }
+    std::vector<int64_t> firsts;
+    for (int s = 0; s < S; s++) firsts.insert(firsts.end(), first[s].begin(), first[s].end());
+    std::sort(firsts.begin(), firsts.end());
+    std::vector<int32_t> gid((size_t)n, -1);  // global id, stored at each key's first record
+    const int32_t base = (int32_t)uniq.size();
+    for (size_t i = 0; i < firsts.size(); i++) {
+        gid[(size_t)firsts[i]] = base + (int32_t)i;
+        uniq.push_back(keys[(size_t)firsts[i]]);
+    }
+    ids.resize((size_t)n);
+#pragma omp parallel for schedule(static)
+    for (int64_t k = 0; k < n; k++) {
+        const uint32_t s = shard[(size_t)k];
+        ids[(size_t)k] = s == (uint32_t)S ? -1 : gid[(size_t)first[s][(size_t)local[(size_t)k]]];
+    }
+}
+
 struct bsdc_bam {
     std::vector<uint8_t> data;  // the uncompressed stream
     std::string header;
@@ -284,35 +332,27 @@ int32_t bsdc_bam_read(const char *path, int32_t n_threads, bsdc_bam **out) {
     b->n_cigar = ncig;
     b->n_mc = nmc;
     b->aux_bytes = naux;
-    // ---- interning (sequential): QNAME, MI base = MI up to the first '/' ----
+    // ---- interning: QNAME, MI base = MI up to the first '/'; ids in first-seen order ----
     b->name_id.resize(nr);
     b->mi_id.resize(nr);
     b->mi_strand.resize(nr);
-    std::unordered_map<std::string_view, int32_t> nmap, mmap;
-    nmap.reserve((size_t)nr);
-    mmap.reserve((size_t)nr / 2 + 1);
+    std::vector<std::string_view> nm(nr), mk(nr);
+#pragma omp parallel for schedule(static)
     for (int64_t k = 0; k < nr; k++) {
         const uint8_t *r = d + b->rec_start[k];
         const int l_name = r[12];
-        std::string_view nm((const char *)r + 36, l_name > 0 ? (size_t)l_name - 1 : 0);
-        auto it = nmap.emplace(nm, (int32_t)b->names.size());
-        if (it.second) b->names.push_back(nm);
-        b->name_id[k] = it.first->second;
+        nm[k] = std::string_view((const char *)r + 36, l_name > 0 ? (size_t)l_name - 1 : 0);
         const std::string_view mi = mi_full[k];
-        if (mi.empty()) {
-            b->mi_id[k] = -1;
-            b->mi_strand[k] = -1;
-            continue;
-        }
-        const size_t slash = mi.find('/');
-        const std::string_view key = slash == std::string_view::npos ? mi : mi.substr(0, slash);
-        auto jt = mmap.emplace(key, (int32_t)b->mis.size());
-        if (jt.second) b->mis.push_back(key);
-        b->mi_id[k] = jt.first->second;
         const size_t L = mi.size();
+        if (L) {
+            const size_t slash = mi.find('/');
+            mk[k] = slash == std::string_view::npos ? mi : mi.substr(0, slash);
+        }
         b->mi_strand[k] = (L >= 2 && mi[L - 2] == '/' && mi[L - 1] == 'A') ? 0
                           : (L >= 2 && mi[L - 2] == '/' && mi[L - 1] == 'B') ? 1 : -1;
     }
+    intern(nm, nullptr, b->name_id, b->names);
+    intern(mk, &mi_full, b->mi_id, b->mis);
     *out = b;
     return 0;
 }
