@@ -8,11 +8,12 @@ HERE = os.path.dirname(os.path.abspath(__file__))
 # BSDC_LIB_PATH: an alternative build of the same library (profiling A/B runs only)
 LIB_PATH = os.environ.get("BSDC_LIB_PATH") or os.path.join(HERE, "libbsdc.so")
 
-BSDC_ABI_VERSION = 5
+BSDC_ABI_VERSION = 6
 SMALL_BUCKETS = 8  # BSDC_SMALL_BUCKETS
 LARGE_BUCKETS = 6  # BSDC_LARGE_BUCKETS
 MODE_CONVERT, MODE_EXTEND, MODE_VOTE, MODE_DUMP = 1, 2, 4, 8
 MODE_SKIP_SMALL, MODE_SKIP_LARGE = 16, 32
+MODE_TAGS = 64  # single-strand reads + column statistics for the consensus tags
 
 
 class Params(C.Structure):
@@ -35,7 +36,9 @@ class ConsensusC(C.Structure):
     _fields_ = [("stride", C.c_int32), ("reserved", C.c_int32),
                 ("status", C.c_void_p), ("len", C.c_void_p), ("seq", C.c_void_p), ("qual", C.c_void_p),
                 ("dump_pos", C.c_void_p), ("dump_len", C.c_void_p), ("dump_tags", C.c_void_p),
-                ("dump_seq", C.c_void_p), ("dump_qual", C.c_void_p), ("scratch", C.c_void_p)]
+                ("dump_seq", C.c_void_p), ("dump_qual", C.c_void_p), ("scratch", C.c_void_p),
+                ("ss_len", C.c_void_p), ("ss_base", C.c_void_p), ("ss_qual", C.c_void_p), ("ss_depth", C.c_void_p),
+                ("ss_err", C.c_void_p)]
 
 
 EXPORTS = ("bsdc_abi_version", "bsdc_ctx_create", "bsdc_ctx_destroy", "bsdc_last_error",

@@ -11,9 +11,11 @@ parallel).
 Output records (fgbio DuplexConsensusCaller as restated; PARITY UNPINNED -- fgbio is not
 vendored): an unmapped pair per emitted family, R1 flag 77 and R2 flag 141, name
 ``<prefix>:<MI base>``, tags RG:Z:A, MI:Z:<MI base>, RX:Z:<consensus UMI> (when the inputs carry
-RX).  The per-base statistics tags (aD/bD/cD, aM/bM/cM, aE/bE/cE, ad/bd, ae/be, ac/bc, aq/bq) are
-not emitted: the consumer of this file (SamToFastq, main.snake.py:167-177) reads name, flag, SEQ
-and QUAL only.
+RX), then fgbio's consensus tags when the consensus was called with tags=True (the default of
+the file-level calls, as fgbio's --output-per-base-tags defaults to true): per read cD cM cE,
+aD aM aE, bD bM bE; per base ad ae ac aq, bd be bc bq (molecular: cD cM cE, cd ce), encoded by
+libbsdc_io (bsdc_consensus_tags) from the single-strand reads the kernels write.  The consumer of
+this file (SamToFastq, main.snake.py:167-177) reads name, flag, SEQ and QUAL only.
 """
 from __future__ import annotations
 
@@ -28,7 +30,7 @@ from . import records as R
 
 IO_LIB_PATH = os.environ.get("BSDC_IO_LIB_PATH") or os.path.join(os.path.dirname(os.path.abspath(__file__)),
                                                                  "libbsdc_io.so")
-BSDC_IO_ABI_VERSION = 2
+BSDC_IO_ABI_VERSION = 3
 _P = C.c_void_p
 
 
@@ -78,6 +80,9 @@ def _load():
     lib.bsdc_fastq_write.restype = C.c_int32
     lib.bsdc_family_image.argtypes = [C.c_int64, _P, _P, _P, _P, _P, C.c_int64, _P, _P, C.c_int32]
     lib.bsdc_family_image.restype = C.c_int32
+    lib.bsdc_consensus_tags.argtypes = [C.c_int64, _P, _P, _P, C.c_int32, C.c_int32, _P, _P, _P, _P, _P, _P,
+                                        C.c_int32]
+    lib.bsdc_consensus_tags.restype = C.c_int64
     if lib.bsdc_io_abi_version() != BSDC_IO_ABI_VERSION:
         raise RuntimeError("libbsdc_io ABI %d != %d" % (lib.bsdc_io_abi_version(), BSDC_IO_ABI_VERSION))
     _lib = lib
@@ -431,9 +436,45 @@ def output_header(header: BamHeader) -> BamHeader:
     return BamHeader("\n".join(lines) + "\n", list(header.ref_names), np.asarray(header.ref_lens, np.int64))
 
 
-def duplex_records(cons, raw: R.RawRecords, prefix: str, threads: int = 0) -> OutRecordsBam:
+def consensus_tags(cons, em: np.ndarray, molecular: bool = False, threads: int = 0) -> StringTable:
+    """fgbio's consensus tags (aux bytes) of the output records R1, R2 of families `em`, from the
+    single-strand reads in cons.ss (libbsdc_io bsdc_consensus_tags).  Duplex: a record's 'a'
+    strand is its AB read (AB-R1 for R1, AB-R2 for R2), or the only strand present; 'b' its BA read
+    when both are present.  Molecular: set 0 for R1, set 1 for R2."""
+    lib = _load()
+    ss = cons.ss
+    F = em.shape[0]
+    n = 2 * F
+    em2 = np.repeat(em.astype(np.int64), 2)
+    end = np.tile(np.asarray([0, 1], np.int64), F)
+    if molecular:
+        row_a = 4 * em2 + end
+        row_b = np.full(n, -1, np.int64)
+    else:
+        sa, sb = end, 3 - end                      # R1: sets 0 / 3, R2: sets 1 / 2
+        la = ss["len"][em2, sa] > 0
+        lb = ss["len"][em2, sb] > 0
+        row_a = 4 * em2 + np.where(la, sa, sb)
+        row_b = np.where(la & lb, 4 * em2 + sb, -1)
+    out_len = np.ascontiguousarray(cons.length[em].reshape(-1), np.int32)
+    stride = int(ss["base"].shape[2])
+    c = lambda a, dt: np.ascontiguousarray(a, dt).reshape(-1)
+    base, qual = c(ss["base"], np.uint8), c(ss["qual"], np.uint8)
+    depth, err = c(ss["depth"], np.uint16), c(ss["err"], np.uint16)
+    row_a, row_b = np.ascontiguousarray(row_a), np.ascontiguousarray(row_b)
+    off = np.zeros(n + 1, np.int64)
+    args = (n, _ptr(row_a), _ptr(row_b), _ptr(out_len), 1 if molecular else 0, stride, _ptr(base), _ptr(qual),
+            _ptr(depth), _ptr(err), _ptr(off))
+    total = lib.bsdc_consensus_tags(*args, None, int(threads))
+    buf = np.zeros(max(int(total), 1), np.uint8)
+    lib.bsdc_consensus_tags(*args, _ptr(buf), int(threads))
+    return StringTable(buf[:int(total)], off)
+
+
+def duplex_records(cons, raw: R.RawRecords, prefix: str, threads: int = 0, molecular: bool = False) -> OutRecordsBam:
     """fgbio duplex output records for the emitted families of `cons`
-    (pipeline.Consensus, family order): R1 then R2 per family."""
+    (pipeline.Consensus, family order): R1 then R2 per family; fgbio's consensus tags appended
+    when cons.ss holds the single-strand reads (``molecular``: CallMolecularConsensusReads' set)."""
     lib = _load()
     em = np.nonzero((cons.status & 1) != 0)[0]
     F = em.shape[0]
@@ -475,6 +516,9 @@ def duplex_records(cons, raw: R.RawRecords, prefix: str, threads: int = 0) -> Ou
     fam_names = _concat_fields([prefix.encode() + b":", mi], F)
     two = np.repeat(np.arange(F, dtype=np.int64), 2)
     names_t, auxs_t = _take_table(fam_names, two), _take_table(fam_aux, two)
+    if getattr(cons, "ss", None) is not None:
+        tg = consensus_tags(cons, em, molecular, threads)
+        auxs_t = _concat_fields([(auxs_t.buf, auxs_t.off), (tg.buf, tg.off)], n)
     L = cons.length[em].astype(np.int64).reshape(-1)            # R1, R2, R1, R2 ...
     seq_off = np.zeros(n + 1, np.int64)
     seq_off[1:] = np.cumsum(L)
@@ -491,7 +535,7 @@ def duplex_records(cons, raw: R.RawRecords, prefix: str, threads: int = 0) -> Ou
 
 
 def step5(in_bam: str, fasta: str, out_bam: Optional[str], engine=None, prefix: Optional[str] = None, threads: int = 0,
-          level: int = 6, fastq: Optional[Tuple[str, str]] = None) -> dict:
+          level: int = 6, fastq: Optional[Tuple[str, str]] = None, tags: bool = True) -> dict:
     """Rules convert_Bstrain .. callduplex (main.snake.py:121-164) as one call on files; with
     `fastq`, also the following consensusduplex_to_fq rule (main.snake.py:167-177) straight from
     the consensus records (out_bam may then be None: no BAM round trip)."""
@@ -503,7 +547,7 @@ def step5(in_bam: str, fasta: str, out_bam: Optional[str], engine=None, prefix: 
     eng = Engine(0) if own else engine
     try:
         eng.load_reference(ref)
-        cons, _ = pipeline.run_step5(eng, raw)
+        cons, _ = pipeline.run_step5(eng, raw, tags=tags and out_bam is not None)
     finally:
         if own:
             eng.close()
@@ -517,7 +561,7 @@ def step5(in_bam: str, fasta: str, out_bam: Optional[str], engine=None, prefix: 
 
 
 def molecular(in_bam: str, out_bam: Optional[str], engine=None, prefix: Optional[str] = None, threads: int = 0,
-              level: int = 6, fastq: Optional[Tuple[str, str]] = None) -> dict:
+              level: int = 6, fastq: Optional[Tuple[str, str]] = None, tags: bool = True) -> dict:
     """Rule call_consensus_reads_molecular (main.snake.py:46-55, fgbio CallMolecularConsensusReads)
     on files; with `fastq`, also consensus_to_fq_unfiltered (main.snake.py:58-67)."""
     from . import pipeline
@@ -526,11 +570,11 @@ def molecular(in_bam: str, out_bam: Optional[str], engine=None, prefix: Optional
     own = engine is None
     eng = Engine(0) if own else engine
     try:
-        cons, rm = pipeline.run_molecular(eng, raw)
+        cons, rm = pipeline.run_molecular(eng, raw, tags=tags and out_bam is not None)
     finally:
         if own:
             eng.close()
-    recs = duplex_records(cons, rm, read_name_prefix(header) if prefix is None else prefix, threads)
+    recs = duplex_records(cons, rm, read_name_prefix(header) if prefix is None else prefix, threads, molecular=True)
     if out_bam is not None:
         write_bam(out_bam, output_header(header), recs, level, threads)
     if fastq is not None:

@@ -32,6 +32,8 @@ def parse(argv):
         p.add_argument("--threads", type=int, default=8)
         p.add_argument("--compression", type=int, default=6)
         p.add_argument("--device", type=int, default=0)
+        p.add_argument("--output-per-base-tags", default="true", choices=["true", "false"],
+                       help="fgbio's consensus tags (per-read and per-base statistics); off = name/SEQ/QUAL/RG/MI/RX")
     a = ap.parse_args(argv)
     if (a.fastq1 is None) != (a.fastq2 is None):
         ap.error("--fastq1 and --fastq2 go together")
@@ -50,9 +52,11 @@ def main(argv=None) -> int:
         eng = Engine(a.device)
         try:
             if a.cmd == "step5":
-                info = bam.step5(a.input, a.reference, out, eng, a.read_name_prefix, a.threads, a.compression, fq)
+                info = bam.step5(a.input, a.reference, out, eng, a.read_name_prefix, a.threads, a.compression, fq,
+                                 tags=a.output_per_base_tags == "true")
             else:
-                info = bam.molecular(a.input, out, eng, a.read_name_prefix, a.threads, a.compression, fq)
+                info = bam.molecular(a.input, out, eng, a.read_name_prefix, a.threads, a.compression, fq,
+                                     tags=a.output_per_base_tags == "true")
         finally:
             eng.close()
     except Exception as e:  # noqa: BLE001 -- the rule fails with the message, like the tools do

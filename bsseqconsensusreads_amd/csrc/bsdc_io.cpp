@@ -705,7 +705,167 @@ extern "C" int64_t bsdc_rx_consensus(int64_t n_fam, const int64_t *fam_rec_off, 
 namespace {
 const char kNt16[] = "=ACMGRSVTWYHKDBN";
 const char kNt16Comp[] = "=TGKCYSBAWRDMHVN";
+
+// BAM aux writer: sizes only when p == nullptr.  Integers take the smallest BAM type that holds
+// them (htsjdk's encoding of an Int attribute).
+struct AuxOut {
+    uint8_t *p;
+    int64_t n = 0;
+    void bytes(const void *src, int64_t k) {
+        if (p) memcpy(p + n, src, (size_t)k);
+        n += k;
+    }
+    void head(const char *tag, char type) {
+        const uint8_t h[3] = {(uint8_t)tag[0], (uint8_t)tag[1], (uint8_t)type};
+        bytes(h, 3);
+    }
+    void integer(const char *tag, int64_t v) {
+        uint8_t b[4];
+        if (v >= 0 && v <= 255) {
+            head(tag, 'C');
+            b[0] = (uint8_t)v;
+            bytes(b, 1);
+        } else if (v >= 0 && v <= 65535) {
+            head(tag, 'S');
+            wr16(b, (uint16_t)v);
+            bytes(b, 2);
+        } else if (v >= -128 && v < 0) {
+            head(tag, 'c');
+            b[0] = (uint8_t)(int8_t)v;
+            bytes(b, 1);
+        } else if (v >= -32768 && v < 0) {
+            head(tag, 's');
+            wr16(b, (uint16_t)(int16_t)v);
+            bytes(b, 2);
+        } else {
+            head(tag, v < 0 ? 'i' : 'I');
+            wr32(b, (uint32_t)v);
+            bytes(b, 4);
+        }
+    }
+    void real(const char *tag, float v) {
+        head(tag, 'f');
+        uint32_t u;
+        memcpy(&u, &v, 4);
+        uint8_t b[4];
+        wr32(b, u);
+        bytes(b, 4);
+    }
+    void shorts(const char *tag, const int32_t *v, int32_t len) {
+        head(tag, 'B');
+        uint8_t b[5] = {'s'};
+        wr32(b + 1, (uint32_t)len);
+        bytes(b, 5);
+        if (p)
+            for (int32_t i = 0; i < len; i++) wr16(p + n + 2 * i, (uint16_t)(int16_t)v[i]);
+        n += 2 * (int64_t)len;
+    }
+    void text(const char *tag, const uint8_t *v, int32_t len, const char *map, int add) {
+        head(tag, 'Z');
+        if (p)
+            for (int32_t i = 0; i < len; i++) p[n + i] = map ? (uint8_t)map[v[i] & 15] : (uint8_t)(v[i] + add);
+        n += len;
+        const uint8_t z = 0;
+        bytes(&z, 1);
+    }
+};
+
+struct SsView {  // one single-strand consensus read, truncated to `len`
+    const uint8_t *b, *q;
+    const uint16_t *d, *e;
+    int32_t len;
+};
+
+void per_read(AuxOut &o, const char *tD, const char *tM, const char *tE, const int32_t *depth, const int32_t *err,
+              int32_t len) {
+    int64_t mx = 0, mn = len ? INT64_MAX : 0, sd = 0, se = 0;
+    for (int32_t i = 0; i < len; i++) {
+        mx = std::max<int64_t>(mx, depth[i]);
+        mn = std::min<int64_t>(mn, depth[i]);
+        sd += depth[i];
+        se += err[i];
+    }
+    o.integer(tD, mx);
+    o.integer(tM, mn);
+    o.real(tE, (float)se / (float)sd);
+}
 }  // namespace
+
+// fgbio's consensus tags of one output record (DuplexConsensusCaller / VanillaUmiConsensusCaller
+// createSamRecord, restated: PARITY UNPINNED), from the single-strand reads the kernels wrote with
+// BSDC_MODE_TAGS.  See include/bsdc_io.h.
+extern "C" int64_t bsdc_consensus_tags(int64_t n, const int64_t *row_a, const int64_t *row_b, const int32_t *out_len,
+                                       int32_t kind, int32_t stride, const uint8_t *ss_base, const uint8_t *ss_qual,
+                                       const uint16_t *ss_depth, const uint16_t *ss_err, int64_t *off, uint8_t *buf,
+                                       int32_t n_threads) {
+    set_threads(n_threads);
+    auto one = [&](int64_t k, uint8_t *p) -> int64_t {
+        AuxOut o{p};
+        const int32_t L = out_len[k];
+        auto view = [&](int64_t row) {
+            const size_t at = (size_t)row * (size_t)stride;
+            return SsView{ss_base + at, ss_qual + at, ss_depth + at, ss_err + at, L};
+        };
+        std::vector<int32_t> td(L), te(L), ad(L), ae(L), bd(L), be(L);
+        const SsView a = view(row_a[k]);
+        for (int32_t i = 0; i < L; i++) {
+            ad[i] = a.d[i];
+            ae[i] = a.e[i];
+        }
+        if (kind == 1) {  // molecular: cD cM cE, cd ce
+            per_read(o, "cD", "cM", "cE", ad.data(), ae.data(), L);
+            o.shorts("cd", ad.data(), L);
+            o.shorts("ce", ae.data(), L);
+            return o.n;
+        }
+        const bool two = row_b[k] >= 0;
+        SsView b{};
+        if (two) {
+            b = view(row_b[k]);
+            for (int32_t i = 0; i < L; i++) {
+                bd[i] = b.d[i];
+                be[i] = b.e[i];
+            }
+        }
+        for (int32_t i = 0; i < L; i++) {
+            if (!two) {
+                td[i] = ad[i];
+                te[i] = ae[i];
+                continue;
+            }
+            // the duplex call before its N mask; errors counted against it: a strand whose call
+            // agrees contributes its errors, one that disagrees all of its reads
+            const uint8_t ab = a.b[i] & 15, bb = b.b[i] & 15;
+            const uint8_t raw = ab == bb ? ab : a.q[i] > b.q[i] ? ab : b.q[i] > a.q[i] ? bb : ab;
+            td[i] = ad[i] + bd[i];
+            te[i] = (ab == raw ? ae[i] : ad[i]) + (bb == raw ? be[i] : bd[i]);
+        }
+        per_read(o, "cD", "cM", "cE", td.data(), te.data(), L);
+        per_read(o, "aD", "aM", "aE", ad.data(), ae.data(), L);
+        if (two) per_read(o, "bD", "bM", "bE", bd.data(), be.data(), L);
+        o.shorts("ad", ad.data(), L);
+        o.shorts("ae", ae.data(), L);
+        o.text("ac", a.b, L, kNt16, 0);
+        o.text("aq", a.q, L, nullptr, 33);
+        if (two) {
+            o.shorts("bd", bd.data(), L);
+            o.shorts("be", be.data(), L);
+            o.text("bc", b.b, L, kNt16, 0);
+            o.text("bq", b.q, L, nullptr, 33);
+        }
+        return o.n;
+    };
+    if (!buf) {
+#pragma omp parallel for schedule(dynamic, 256)
+        for (int64_t k = 0; k < n; k++) off[k + 1] = one(k, nullptr);
+        off[0] = 0;
+        for (int64_t k = 0; k < n; k++) off[k + 1] += off[k];
+        return off[n];
+    }
+#pragma omp parallel for schedule(dynamic, 256)
+    for (int64_t k = 0; k < n; k++) one(k, buf + off[k]);
+    return off[n];
+}
 
 extern "C" int32_t bsdc_fastq_write(const char *path1, const char *path2, const bsdc_bam_records *r, int32_t level,
                                     int32_t n_threads) {

@@ -121,6 +121,53 @@ __device__ __forceinline__ int phred_of(float S, const float *thr) {
     return lo;
 }
 
+// Per-column statistics of a single-strand consensus read (BSDC_MODE_TAGS), as fgbio
+// VanillaUmiConsensusCaller keeps them for the consensus tags: the call itself (N / 2 below Q2),
+// depth = reads with an A/C/G/T at the column, errors = depth - reads showing the RAW best base
+// (before the Q2 mask; a column without reads has depth 0 and errors 0).  Both counts saturate at
+// 32767 (fgbio stores Shorts).  D: likelihood sums (2^-20 nats), n: reads per base.
+struct SsAcc {
+    long long D[4];
+    uint32_t n[4];
+    __device__ __forceinline__ void clear() {
+#pragma unroll
+        for (int x = 0; x < 4; x++) {
+            D[x] = 0;
+            n[x] = 0;
+        }
+    }
+    // one read's base (plain nt16 code, sequencing orientation) and its lr value
+    __device__ __forceinline__ void add(uint32_t code, int32_t v) {
+#pragma unroll
+        for (int x = 0; x < 4; x++) {
+            const bool hit = code == (1u << x);
+            D[x] += hit ? v : 0;
+            n[x] += hit ? 1u : 0u;
+        }
+    }
+};
+__device__ __forceinline__ void ss_store(const SsAcc &a, const float *thr, uint8_t *b, uint8_t *q, uint16_t *dp,
+                                         uint16_t *er) {
+    int best = 0;
+    long long Db = a.D[0];
+#pragma unroll
+    for (int x = 1; x < 4; x++)
+        if (a.D[x] > Db) {
+            best = x;
+            Db = a.D[x];
+        }
+    float S = 0.0f;
+#pragma unroll
+    for (int x = 0; x < 4; x++)
+        if (x != best) S += term(a.D[x] - Db);
+    const int Q = phred_of(S, thr);
+    const uint32_t depth = a.n[0] + a.n[1] + a.n[2] + a.n[3];
+    *b = Q < 2 ? (uint8_t)kN : (uint8_t)(1u << best);
+    *q = Q < 2 ? (uint8_t)2 : (uint8_t)Q;
+    *dp = (uint16_t)::min(depth, 32767u);
+    *er = (uint16_t)::min(depth - a.n[best], 32767u);
+}
+
 // tool 1 per-base rule (tools/1.convert_AG_to_CT.py:123-150), in its local form: the value at i
 // depends on m[i], m[i+1], ref[i], ref[i+1] only (the skip at :140 writes what the A rule would)
 __device__ __forceinline__ uint32_t convert_rule(uint32_t m0, uint32_t m1, bool has_next, uint32_t f0, uint32_t f1) {
@@ -609,6 +656,9 @@ __device__ __forceinline__ void unpack32(uint4 v, uint8_t *dst) {
     d[1] = make_uint4(o[4], o[5], o[6], o[7]);
 }
 
+// TAGS: also the single-strand reads + column statistics (BSDC_MODE_TAGS; its own instance, so the
+// hot instance carries none of that code)
+template <bool TAGS>
 __global__ __launch_bounds__(kWave *kSmallMaxWaves, kSmallMinWaves) __attribute__((amdgpu_num_sgpr(SMALL_SGPRS))) void k_small(KParams P, const uint32_t *fams, int64_t nfams,
                                                               int32_t arena) {
     extern __shared__ __attribute__((aligned(16))) uint8_t smem[];  // the wavefronts' arenas
@@ -1251,6 +1301,30 @@ __global__ __launch_bounds__(kWave *kSmallMaxWaves, kSmallMinWaves) __attribute_
                 *reinterpret_cast<uint32_t *>(P.O.seq + so / 2 + c0 / 2) = pk;
                 *reinterpret_cast<uint2 *>(P.O.qual + so + c0) = make_uint2(qlo2, qhi2);
             }
+        }
+    }
+    // single-strand reads and column statistics for the consensus tags: a lane per (set, column),
+    // walking the set's reads like the queued path (only with BSDC_MODE_TAGS)
+    if (TAGS && stop == 0) {
+#pragma unroll 1
+        for (int s = 0; s < 4; s++) {
+            const int ls = hs[s] ? lcs[s] : 0;
+            const int64_t row = (4 * (int64_t)fam + s) * stride;
+            for (int c = t; c < ls; c += kWave) {
+                SsAcc acc;
+                acc.clear();
+                for (int i = 0; i < cnt[s]; i++) {
+                    const uint32_t d = dlist[off[s] + i];
+                    if (c >= (int)((d >> 16) & 0x7FFF)) continue;
+                    const uint32_t idx = (d & 0x80000000u) ? (d & 0xFFFF) - c : (d & 0xFFFF) + c;
+                    const uint32_t braw = bimg[idx];
+                    const uint32_t bb = (d & 0x80000000u) ? comp_nt16(braw) : (braw & 0x0F);
+                    acc.add(bb, lr2[256 + qimg[idx]]);  // only one-hot codes count
+                }
+                ss_store(acc, thr, P.O.ss_base + row + c, P.O.ss_qual + row + c, P.O.ss_depth + row + c,
+                         P.O.ss_err + row + c);
+            }
+            if (t == 0) P.O.ss_len[4 * fam + s] = (uint16_t)ls;
         }
     }
     if (t == 0) {
@@ -1955,6 +2029,30 @@ __device__ void process_large(const KParams &P, uint8_t *A, const int32_t *lr, c
             }
         }
     }
+    if ((P.mode & BSDC_MODE_TAGS) && stop == 0) {  // consensus-tag statistics, a thread per (set, column)
+        const int ntag = (hs[0] ? lcv[0] : 0) + (hs[1] ? lcv[1] : 0) + (hs[2] ? lcv[2] : 0) + (hs[3] ? lcv[3] : 0);
+        for (int k = tt; k < ntag; k += G) {
+            int s = 0, c = k;
+            while (c >= (hs[s] ? lcv[s] : 0)) {
+                c -= hs[s] ? lcv[s] : 0;
+                s++;
+            }
+            SsAcc acc;
+            acc.clear();
+            const uint2 *dl = desc + soff[s];
+            for (int i = 0; i < cnt[s]; i++) {
+                const uint2 e = dl[i];
+                if (c >= (int)(e.y & 0x7FFFFFFFu)) continue;
+                const bool rv = e.y >> 31;
+                const int32_t a = rv ? (int32_t)e.x - c : (int32_t)e.x + c;
+                const uint32_t braw = slots[a] & 0x0Fu;
+                acc.add(rv ? comp_nt16(braw) : braw, lr[qimg[a]]);
+            }
+            const int64_t at = (4 * (int64_t)fam + s) * stride + c;
+            ss_store(acc, thr, P.O.ss_base + at, P.O.ss_qual + at, P.O.ss_depth + at, P.O.ss_err + at);
+        }
+        if (tt < 4) P.O.ss_len[4 * fam + tt] = (uint16_t)(hs[tt] ? lcv[tt] : 0);
+    }
     if (tt == 0) {
         uint8_t st = emit ? 1 : 0;
         if (hs[0] || hs[1]) st |= 2;
@@ -2190,6 +2288,11 @@ int32_t bsdc_run(bsdc_ctx *c, const bsdc_family_batch *b, bsdc_consensus *o, int
         c->err = "reference not loaded";
         return BSDC_EINVAL;
     }
+    if ((mode & BSDC_MODE_TAGS) && (!(mode & BSDC_MODE_VOTE) || !o->ss_len || !o->ss_base || !o->ss_qual ||
+                                    !o->ss_depth || !o->ss_err)) {
+        c->err = "BSDC_MODE_TAGS needs BSDC_MODE_VOTE and the ss_* outputs";
+        return BSDC_EINVAL;
+    }
     if ((mode & BSDC_MODE_DUMP) && (!o->dump_pos || !o->dump_len || !o->dump_tags || !o->dump_seq || !o->dump_qual)) {
         c->err = "dump buffers missing";
         return BSDC_EINVAL;
@@ -2219,8 +2322,12 @@ int32_t bsdc_run(bsdc_ctx *c, const bsdc_family_batch *b, bsdc_consensus *o, int
                 const int nw = w8 > w4 ? 8 : 4;
                 const size_t lds = (size_t)nw * (size_t)b->small_arena[q];  // + the static tables
                 const int64_t blocks = (nf + nw - 1) / nw;
-                hipLaunchKernelGGL(k_small, dim3((unsigned)blocks), dim3(kWave * nw), lds, s, P, f, nf,
-                                   b->small_arena[q]);
+                if (mode & BSDC_MODE_TAGS)
+                    hipLaunchKernelGGL(k_small<true>, dim3((unsigned)blocks), dim3(kWave * nw), lds, s, P, f, nf,
+                                       b->small_arena[q]);
+                else
+                    hipLaunchKernelGGL(k_small<false>, dim3((unsigned)blocks), dim3(kWave * nw), lds, s, P, f, nf,
+                                       b->small_arena[q]);
                 HIP_OK(c, hipGetLastError());
             }
             f += 4 * nf;

@@ -36,7 +36,7 @@ def _dptr(t: torch.Tensor) -> int:
 class DeviceBatch:
     """A FamilyBatch resident in HBM plus its output buffers."""
 
-    def __init__(self, fb: FamilyBatch, device: torch.device, dump: bool = False):
+    def __init__(self, fb: FamilyBatch, device: torch.device, dump: bool = False, tags: bool = False):
         self.fb = fb
         self.device = device
         self.t: Dict[str, torch.Tensor] = {}
@@ -60,6 +60,14 @@ class DeviceBatch:
             self.dump_tags = torch.zeros(max(Rn, 1), dtype=torch.uint8, device=device)
             self.dump_seq = torch.zeros(cap, dtype=torch.uint8, device=device)
             self.dump_qual = torch.zeros(cap, dtype=torch.uint8, device=device)
+        self.tags = tags
+        if tags:  # single-strand reads + column statistics (BSDC_MODE_TAGS), rows (family, set)
+            nss = max(4 * F * self.stride, 16)
+            self.ss_len = torch.zeros(max(4 * F, 1), dtype=torch.int16, device=device)
+            self.ss_base = torch.zeros(nss, dtype=torch.uint8, device=device)
+            self.ss_qual = torch.zeros(nss, dtype=torch.uint8, device=device)
+            self.ss_depth = torch.zeros(nss, dtype=torch.int16, device=device)
+            self.ss_err = torch.zeros(nss, dtype=torch.int16, device=device)
         # HBM arenas of the large buckets beyond the LDS budget (dispatches run one after another
         # on the stream, so they share one buffer); + slack: dword reads may run a few bytes past
         # the last arena (their bytes are masked)
@@ -87,6 +95,9 @@ class DeviceBatch:
             o.dump_pos, o.dump_len, o.dump_tags = _dptr(self.dump_pos), _dptr(self.dump_len), _dptr(self.dump_tags)
             o.dump_seq, o.dump_qual = _dptr(self.dump_seq), _dptr(self.dump_qual)
         o.scratch = _dptr(self.scratch) if self.scratch is not None else None
+        if tags:
+            o.ss_len, o.ss_base, o.ss_qual = _dptr(self.ss_len), _dptr(self.ss_base), _dptr(self.ss_qual)
+            o.ss_depth, o.ss_err = _dptr(self.ss_depth), _dptr(self.ss_err)
 
     def fetch(self):
         """-> dict of numpy arrays (consensus and, if dumped, the post-tool records)."""
@@ -98,6 +109,14 @@ class DeviceBatch:
             "qual": self.qual[:2 * F * self.stride].cpu().numpy().reshape(F, 2, self.stride),
             "stride": self.stride,
         }
+        if self.tags:
+            n = 4 * F * self.stride
+            u16 = lambda t: t.cpu().numpy().view(np.uint16)
+            out["ss_len"] = u16(self.ss_len[:4 * F]).astype(np.int32).reshape(F, 4)
+            out["ss_base"] = self.ss_base[:n].cpu().numpy().reshape(F, 4, self.stride)
+            out["ss_qual"] = self.ss_qual[:n].cpu().numpy().reshape(F, 4, self.stride)
+            out["ss_depth"] = u16(self.ss_depth[:n]).reshape(F, 4, self.stride)
+            out["ss_err"] = u16(self.ss_err[:n]).reshape(F, 4, self.stride)
         if self.dump:
             Rn = self.fb.n_rec
             out["dump_pos"] = self.dump_pos[:Rn].cpu().numpy()
@@ -152,9 +171,9 @@ class Engine:
         self._check(rc, "bsdc_load_reference")
         self.ref = ref
 
-    def upload(self, fb: FamilyBatch, dump: bool = False) -> DeviceBatch:
+    def upload(self, fb: FamilyBatch, dump: bool = False, tags: bool = False) -> DeviceBatch:
         with torch.cuda.device(self.device):
-            return DeviceBatch(fb, self.device, dump)
+            return DeviceBatch(fb, self.device, dump, tags)
 
     def run(self, db: DeviceBatch, mode: int, stream: Optional[torch.cuda.Stream] = None):
         s = stream if stream is not None else torch.cuda.current_stream(self.device)

@@ -20,7 +20,7 @@ import numpy as np
 from . import records as R
 from .batch import FamilyBatch, build_family_batch
 from .device import Engine
-from ._lib import MODE_CONVERT, MODE_DUMP, MODE_EXTEND, MODE_VOTE
+from ._lib import MODE_CONVERT, MODE_DUMP, MODE_EXTEND, MODE_TAGS, MODE_VOTE
 
 
 @dataclass
@@ -59,6 +59,10 @@ class Consensus:
     qual: np.ndarray       # [F, 2, stride]
     fam_rec_off: np.ndarray = None  # [F + 1] family membership: fam_src[fam_rec_off[f]:fam_rec_off[f+1]]
     fam_src: np.ndarray = None      # input record index of each family record (family order)
+    # with tags=True: the four single-strand consensus reads per family and their column
+    # statistics (BSDC_MODE_TAGS), sets s = 0 AB-R1, 1 AB-R2, 2 BA-R1, 3 BA-R2: "len" [F, 4],
+    # "base" (nt16) / "qual" / "depth" / "err" [F, 4, stride]
+    ss: Optional[dict] = None
 
 
 def _stripped_cigar(raw: R.RawRecords, k: int, strip: bool) -> List[int]:
@@ -213,12 +217,17 @@ def consensus_from_output(fb: FamilyBatch, out: dict) -> Consensus:
     seq = np.empty((F, 2, stride), np.uint8)
     seq[:, :, 0::2] = packed >> 4
     seq[:, :, 1::2] = packed & 0xF
+    ss = None
+    if "ss_len" in out:
+        ss = {"len": out["ss_len"], "base": out["ss_base"], "qual": out["ss_qual"], "depth": out["ss_depth"],
+              "err": out["ss_err"]}
     return Consensus(fb.fam_mi.copy(), out["status"], out["len"], seq, out["qual"], fb.fam_off.astype(np.int64),
-                     fb.src.astype(np.int64))
+                     fb.src.astype(np.int64), ss)
 
 
-def run_step5(engine: Engine, raw: R.RawRecords, dump: bool = False):
-    """Rules convert_Bstrain .. callduplex (main.snake.py:121-164) -> (Consensus, tool-2 records or None)."""
+def run_step5(engine: Engine, raw: R.RawRecords, dump: bool = False, tags: bool = False):
+    """Rules convert_Bstrain .. callduplex (main.snake.py:121-164) -> (Consensus, tool-2 records or None).
+    tags: also the single-strand reads and column statistics of fgbio's consensus tags (Consensus.ss)."""
     fb = build_family_batch(raw, "full", engine.ref)
     if fb.split_ext:
         # a TemplateCoordinate family lacks a record's tool-2 extension partner: run the tools as
@@ -227,21 +236,21 @@ def run_step5(engine: Engine, raw: R.RawRecords, dump: bool = False):
         db = engine.upload(fb2, dump=True)
         engine.run(db, MODE_CONVERT | MODE_EXTEND | MODE_DUMP)
         t2 = _records_from_dump(raw, fb2, db.fetch(), strip=True)
-        cons = run_duplex(engine, raw_from_records(raw, t2))
+        cons = run_duplex(engine, raw_from_records(raw, t2), tags)
         cons.fam_src = t2.src[cons.fam_src]  # raw2 record k is tool-2 record k
         return cons, (t2 if dump else None)
-    db = engine.upload(fb, dump=dump)
-    engine.run(db, MODE_CONVERT | MODE_EXTEND | MODE_VOTE | (MODE_DUMP if dump else 0))
+    db = engine.upload(fb, dump=dump, tags=tags)
+    engine.run(db, MODE_CONVERT | MODE_EXTEND | MODE_VOTE | (MODE_DUMP if dump else 0) | (MODE_TAGS if tags else 0))
     out = db.fetch()
     t2 = _records_from_dump(raw, fb, out, strip=True) if dump else None
     return consensus_from_output(fb, out), t2
 
 
-def run_duplex(engine: Engine, raw: R.RawRecords) -> Consensus:
+def run_duplex(engine: Engine, raw: R.RawRecords, tags: bool = False) -> Consensus:
     """callduplex alone (main.snake.py:155-164) on converted + extended records."""
     fb = build_family_batch(raw, "vote")
-    db = engine.upload(fb)
-    engine.run(db, MODE_VOTE)
+    db = engine.upload(fb, tags=tags)
+    engine.run(db, MODE_VOTE | (MODE_TAGS if tags else 0))
     return consensus_from_output(fb, db.fetch())
 
 
@@ -266,12 +275,12 @@ def molecular_records(raw: R.RawRecords) -> R.RawRecords:
     return dataclasses.replace(raw, mi_id=mi_id, mi_strand=mi_strand, mi_names=names)
 
 
-def run_molecular(engine: Engine, raw: R.RawRecords):
+def run_molecular(engine: Engine, raw: R.RawRecords, tags: bool = False):
     """fgbio CallMolecularConsensusReads with the step-1 flags (main.snake.py:54: pre 45, post 30,
     min-reads 1, overlapping bases on) -> (Consensus over the runs, the run records).  Consensus
     family f is MI run f; its R1 / R2 are the single-strand consensus of the run's R1s / R2s."""
     rm = molecular_records(raw)
     fb = build_family_batch(rm, "vote", family_order="mi-group")
-    db = engine.upload(fb)
-    engine.run(db, MODE_VOTE)
+    db = engine.upload(fb, tags=tags)
+    engine.run(db, MODE_VOTE | (MODE_TAGS if tags else 0))
     return consensus_from_output(fb, db.fetch()), rm

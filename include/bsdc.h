@@ -24,7 +24,7 @@
 extern "C" {
 #endif
 
-#define BSDC_ABI_VERSION 5
+#define BSDC_ABI_VERSION 6
 #define BSDC_SMALL_BUCKETS 8
 #define BSDC_LARGE_BUCKETS 6
 #define BSDC_LARGE_LDS_MAX 158912 /* LDS arena bytes one large-family workgroup may use */ /* LDS arena size classes of the wavefront-per-family kernel */
@@ -106,12 +106,22 @@ typedef struct {
     uint8_t *dump_qual;
     uint8_t *scratch;            /* arenas of the large buckets beyond BSDC_LARGE_LDS_MAX: the largest
                                     n_large[q] * large_arena[q] of them + 256 bytes */
+    /* optional single-strand consensus reads and their per-column statistics (BSDC_MODE_TAGS),
+     * the inputs of fgbio's per-read / per-base consensus tags (aD/aM/aE, ad/ae/ac/aq, ...;
+     * cD/cM/cE, cd/ce for the molecular caller).  Row (f, s), s = 0 AB-R1, 1 AB-R2, 2 BA-R1,
+     * 3 BA-R2, holds `stride` columns of family f's set s (sequencing orientation). */
+    uint16_t *ss_len;            /* [4*n_fam] single-strand consensus length (0 = set empty) */
+    uint8_t *ss_base;            /* [4*n_fam*stride] nt16 code per byte (N when Q < 2) */
+    uint8_t *ss_qual;            /* [4*n_fam*stride] */
+    uint16_t *ss_depth;          /* [4*n_fam*stride] reads with an A/C/G/T at the column */
+    uint16_t *ss_err;            /* [4*n_fam*stride] depth - reads showing the raw (pre-mask) best base */
 } bsdc_consensus;
 
 #define BSDC_MODE_CONVERT 1
 #define BSDC_MODE_EXTEND 2
 #define BSDC_MODE_VOTE 4
 #define BSDC_MODE_DUMP 8
+#define BSDC_MODE_TAGS 64       /* also write the ss_* outputs (with BSDC_MODE_VOTE) */
 #define BSDC_MODE_SKIP_SMALL 16 /* profiling: do not launch the small-family kernel */
 #define BSDC_MODE_SKIP_LARGE 32 /* profiling: do not launch the large-family kernel */
 #define BSDC_MODE_STOP_SHIFT 8  /* profiling: (mode >> 8) & 15 = k > 0 stops the small kernel after phase k */

@@ -17,7 +17,7 @@
 extern "C" {
 #endif
 
-#define BSDC_IO_ABI_VERSION 2
+#define BSDC_IO_ABI_VERSION 3
 #define BSDC_IO_EFORMAT (-10) /* not BGZF/BAM, truncated, bad CRC */
 #define BSDC_IO_EIO (-11)     /* open/read/write failed */
 
@@ -123,6 +123,20 @@ int32_t bsdc_family_image(int64_t n_rec, const int64_t *src_off, const int64_t *
 int64_t bsdc_rx_consensus(int64_t n_fam, const int64_t *fam_rec_off, const int64_t *rec, const int8_t *strand,
                           const int64_t *aux_off, const uint8_t *aux, char *out, int32_t *out_len,
                           int32_t n_threads);
+
+/* fgbio consensus tags of n output records, BAM aux bytes (replaces the tag block of fgbio
+ * DuplexConsensusCaller.createSamRecord (kind 0) / VanillaUmiConsensusCaller.createSamRecord
+ * (kind 1), main.snake.py:54,163; fgbio unvendored: PARITY UNPINNED).  Record k's consensus has
+ * out_len[k] columns; row_a[k] / row_b[k] are its single-strand reads' rows of the ss_* arrays
+ * libbsdc writes with BSDC_MODE_TAGS (row_b = -1: one strand; kind 1 uses row_a only).
+ *   kind 0: cD cM cE, aD aM aE, [bD bM bE], ad ae ac aq, [bd be bc bq]
+ *   kind 1: cD cM cE, cd ce
+ * Call with buf = NULL to fill off[0..n] (prefix sums of the sizes), then with buf. Returns the
+ * total bytes. */
+int64_t bsdc_consensus_tags(int64_t n, const int64_t *row_a, const int64_t *row_b, const int32_t *out_len,
+                            int32_t kind, int32_t stride, const uint8_t *ss_base, const uint8_t *ss_qual,
+                            const uint16_t *ss_depth, const uint16_t *ss_err, int64_t *off, uint8_t *buf,
+                            int32_t n_threads);
 
 #ifdef __cplusplus
 }

@@ -580,9 +580,14 @@ typedef struct {
     int32_t len;
     char *b;
     uint8_t *q;
+    int32_t *depth; /* reads with an A/C/G/T at the column */
+    int32_t *err;   /* depth - reads showing the raw (pre-mask) best base */
 } ssread;
 
-/* single-strand consensus (fgbio VanillaUmiConsensusCaller, min-reads 1), restated */
+/* single-strand consensus (fgbio VanillaUmiConsensusCaller, min-reads 1), restated; with the
+ * per-column depth and errors fgbio keeps for its consensus tags:
+ *   errors = if (rawBase == NoCall) depth else depth - builder.observations(rawBase)
+ * where rawBase is the likelihood call before the minimum-quality mask (PARITY UNPINNED). */
 static int ss_consensus(srcread **v, int n, const int64_t *lr, const float *thr, ssread *out) {
     int32_t lc = 0;
     for (int i = 0; i < n; i++)
@@ -591,13 +596,17 @@ static int ss_consensus(srcread **v, int n, const int64_t *lr, const float *thr,
     out->len = lc;
     out->b = (char *)malloc((size_t)lc);
     out->q = (uint8_t *)malloc((size_t)lc);
+    out->depth = (int32_t *)malloc(sizeof(int32_t) * (size_t)lc);
+    out->err = (int32_t *)malloc(sizeof(int32_t) * (size_t)lc);
     for (int32_t c = 0; c < lc; c++) {
         int64_t D[4] = {0, 0, 0, 0};
+        int32_t obs[4] = {0, 0, 0, 0};
         for (int i = 0; i < n; i++) {
             if (v[i]->len <= c) continue;
             int bi = base_index(v[i]->b[c]);
             if (bi < 0) continue;
             D[bi] += lr[v[i]->q[c]];
+            obs[bi]++;
         }
         int best = 0;
         for (int b = 1; b < 4; b++)
@@ -623,6 +632,9 @@ static int ss_consensus(srcread **v, int n, const int64_t *lr, const float *thr,
             out->b[c] = "ACGT"[best];
             out->q[c] = (uint8_t)Q;
         }
+        const int32_t depth = obs[0] + obs[1] + obs[2] + obs[3];
+        out->depth[c] = depth > 32767 ? 32767 : depth;
+        out->err[c] = depth - obs[best] > 32767 ? 32767 : depth - obs[best];
     }
     return 1;
 }
@@ -679,6 +691,7 @@ struct orc_result {
     int32_t *fam_nreads;
     char **fam_b;       /* [2*f + end] */
     uint8_t **fam_q;
+    ssread *fam_ss;       /* [4*f + set] single-strand reads (len 0 = set empty) */
     int64_t *fam_rec_off; /* [nfam + 1] into fam_src */
     int64_t *fam_src;     /* input record index of each family record, family order */
 };
@@ -779,10 +792,10 @@ static void family_call(orec *recs, int n, const orc_records *in, const orc_para
         free(q2);
     }
     for (int s = 0; s < 4; s++) {
-        if (has[s]) {
-            free(ss[s].b);
-            free(ss[s].q);
-        }
+        if (has[s])
+            res->fam_ss[4 * f + s] = ss[s];  /* owned by the result */
+        else
+            memset(&res->fam_ss[4 * f + s], 0, sizeof(ssread));
         free(sets[s]);
     }
     for (int i = 0; i < n; i++) {
@@ -1033,6 +1046,7 @@ orc_result *orc_run(const orc_records *in, const orc_reference *ref, const orc_p
     res->fam_len = (int32_t *)calloc((size_t)(2 * ng + 2), sizeof(int32_t));
     res->fam_b = (char **)calloc((size_t)(2 * ng + 2), sizeof(char *));
     res->fam_q = (uint8_t **)calloc((size_t)(2 * ng + 2), sizeof(uint8_t *));
+    res->fam_ss = (ssread *)calloc((size_t)(4 * ng + 4), sizeof(ssread));
     for (int64_t g = 0; g < ng; g++) res->fam_mi[g] = gorder_mi[g];
 #pragma omp parallel for schedule(dynamic, 64)
     for (int64_t g = 0; g < ng; g++)
@@ -1055,6 +1069,13 @@ void orc_free(orc_result *r) {
         if (r->fam_b) free(r->fam_b[i]);
         if (r->fam_q) free(r->fam_q[i]);
     }
+    for (int64_t i = 0; r->fam_ss && i < 4 * r->nfam; i++) {
+        free(r->fam_ss[i].b);
+        free(r->fam_ss[i].q);
+        free(r->fam_ss[i].depth);
+        free(r->fam_ss[i].err);
+    }
+    free(r->fam_ss);
     free(r->fam_b);
     free(r->fam_q);
     free(r->fam_mi);
@@ -1122,6 +1143,25 @@ void orc_get_consensus(const orc_result *r, int32_t stride, int32_t *mi_id, int3
                 memcpy(ob, r->fam_b[2 * f + e], (size_t)l);
                 memcpy(oq, r->fam_q[2 * f + e], (size_t)l);
             }
+        }
+    }
+}
+
+void orc_get_ss(const orc_result *r, int32_t stride, int32_t *len, uint8_t *bases, uint8_t *quals, int32_t *depth,
+                int32_t *err) {
+    for (int64_t i = 0; i < 4 * r->nfam; i++) {
+        const ssread *x = &r->fam_ss[i];
+        len[i] = x->len;
+        const size_t o = (size_t)i * (size_t)stride;
+        memset(bases + o, 0, (size_t)stride);
+        memset(quals + o, 0, (size_t)stride);
+        memset(depth + o, 0, sizeof(int32_t) * (size_t)stride);
+        memset(err + o, 0, sizeof(int32_t) * (size_t)stride);
+        if (x->len > 0) {
+            memcpy(bases + o, x->b, (size_t)x->len);
+            memcpy(quals + o, x->q, (size_t)x->len);
+            memcpy(depth + o, x->depth, sizeof(int32_t) * (size_t)x->len);
+            memcpy(err + o, x->err, sizeof(int32_t) * (size_t)x->len);
         }
     }
 }

@@ -93,6 +93,12 @@ int32_t orc_max_cons_len(const orc_result *r);
 void orc_get_consensus(const orc_result *r, int32_t stride, int32_t *mi_id, int32_t *status,
                        int32_t *len, uint8_t *bases, uint8_t *quals, int32_t *n_reads);
 
+/* The four single-strand consensus reads per family (sets 0 AB-R1, 1 AB-R2, 2 BA-R1, 3 BA-R2, row
+ * 4*f + s, `stride` columns, len 0 = empty set) with the per-column depth and errors of fgbio's
+ * consensus tags (PARITY UNPINNED). */
+void orc_get_ss(const orc_result *r, int32_t stride, int32_t *len, uint8_t *bases, uint8_t *quals, int32_t *depth,
+                int32_t *err);
+
 /* Tables of the likelihood model, for a cross-check against libbsdc's own. */
 void orc_tables(double pre, double post, int64_t *lr_fixed256, float *phred_thresh94);
 float orc_det_expf(float x);

@@ -70,6 +70,7 @@ def load():
         lib.orc_max_cons_len.restype = C.c_int32
         lib.orc_max_cons_len.argtypes = [C.c_void_p]
         lib.orc_get_consensus.argtypes = [C.c_void_p, C.c_int32] + [C.c_void_p] * 6
+        lib.orc_get_ss.argtypes = [C.c_void_p, C.c_int32] + [C.c_void_p] * 5
         lib.orc_tables.argtypes = [C.c_double, C.c_double, C.c_void_p, C.c_void_p]
         lib.orc_det_expf.restype = C.c_float
         lib.orc_det_expf.argtypes = [C.c_float]
@@ -117,6 +118,9 @@ class OracleResult:
     seconds: float = 0.0    # wall time of orc_run alone
     fam_rec_off: np.ndarray = None  # [F + 1] family membership: fam_src[fam_rec_off[f]:fam_rec_off[f+1]]
     fam_src: np.ndarray = None      # input record index of each family record (family order)
+    # single-strand reads per family and set (0 AB-R1, 1 AB-R2, 2 BA-R1, 3 BA-R2) with the
+    # consensus-tag column statistics: "len" [F, 4], "base" (nt16) / "qual" / "depth" / "err" [F, 4, stride]
+    ss: dict = None
 
 
 def _ptr(a):
@@ -258,9 +262,19 @@ def run(raw, ref, pre=45.0, post=30.0, overlap=True, run_tools=True, threads=0,
         fro = np.zeros(F + 1, np.int64)
         fsrc = np.zeros(max(lib.orc_n_records(h, 2), 1), np.int64)
         lib.orc_get_families(h, _ptr(fro), _ptr(fsrc))
+        sl = np.zeros(max(4 * F, 1), np.int32)
+        sb = np.zeros(max(4 * F * stride, 1), np.uint8)
+        sq = np.zeros(max(4 * F * stride, 1), np.uint8)
+        sd = np.zeros(max(4 * F * stride, 1), np.int32)
+        se = np.zeros(max(4 * F * stride, 1), np.int32)
+        lib.orc_get_ss(h, stride, _ptr(sl), _ptr(sb), _ptr(sq), _ptr(sd), _ptr(se))
+        n4 = 4 * F * stride
+        ss = {"len": sl[:4 * F].reshape(F, 4), "base": _ASCII_NT16[sb[:n4]].reshape(F, 4, stride),
+              "qual": sq[:n4].reshape(F, 4, stride), "depth": sd[:n4].reshape(F, 4, stride),
+              "err": se[:n4].reshape(F, 4, stride)}
         return OracleResult(outs[0], outs[1], mi[:F], st[:F], ln[:2 * F].reshape(F, 2),
                             _ASCII_NT16[bs[:2 * F * stride]].reshape(F, 2, stride) if F else np.zeros((0, 2, stride), np.uint8),
-                            qs[:2 * F * stride].reshape(F, 2, stride), nr[:F], seconds, fro, fsrc[:int(fro[-1])])
+                            qs[:2 * F * stride].reshape(F, 2, stride), nr[:F], seconds, fro, fsrc[:int(fro[-1])], ss)
     finally:
         lib.orc_free(h)
 

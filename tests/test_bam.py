@@ -295,3 +295,94 @@ def test_family_image_matches_numpy():
     assert np.array_equal(packed, R.pack_nibbles(codes)) and np.array_equal(qual, q2)
     with pytest.raises(ValueError):
         bam.family_image(src, L, dst + 1, raw.seq, raw.qual, n_slots, packed, qual)
+
+
+def _expected_tags(ss, f, e, L, molecular):
+    """fgbio createSamRecord's consensus tags of record (f, e), restated in Python (the C++
+    encoder bsdc_consensus_tags is checked against this; fgbio itself: PARITY UNPINNED)."""
+    def per_read(d, er, names):
+        return [(names[0], int(d.max())), (names[1], int(d.min())), (names[2], np.float32(er.sum()) / np.float32(d.sum()))]
+    if molecular:
+        d, er = ss["depth"][f, e, :L].astype(np.int64), ss["err"][f, e, :L].astype(np.int64)
+        return per_read(d, er, "cD cM cE".split()) + [("cd", list(d)), ("ce", list(er))]
+    sa, sb = (0, 3) if e == 0 else (1, 2)
+    la, lb = ss["len"][f, sa] > 0, ss["len"][f, sb] > 0
+    a = sa if la else sb
+    col = lambda s, k: ss[k][f, s, :L].astype(np.int64)  # noqa: E731
+    ad, ae = col(a, "depth"), col(a, "err")
+    tags = []
+    if la and lb:
+        bd, be = col(sb, "depth"), col(sb, "err")
+        ab, bb, aq, bq = col(sa, "base"), col(sb, "base"), col(sa, "qual"), col(sb, "qual")
+        raw = np.where(ab == bb, ab, np.where(aq > bq, ab, np.where(bq > aq, bb, ab)))
+        td = ad + bd
+        te = np.where(ab == raw, ae, ad) + np.where(bb == raw, be, bd)
+        tags += per_read(td, te, "cD cM cE".split()) + per_read(ad, ae, "aD aM aE".split())
+        tags += per_read(bd, be, "bD bM bE".split())
+    else:
+        tags += per_read(ad, ae, "cD cM cE".split()) + per_read(ad, ae, "aD aM aE".split())
+    tags += [("ad", list(ad)), ("ae", list(ae)), ("ac", R.NT16_TO_ASCII[col(a, "base")].tobytes().decode()),
+             ("aq", (col(a, "qual") + 33).astype(np.uint8).tobytes().decode())]
+    if la and lb:
+        tags += [("bd", list(bd)), ("be", list(be)), ("bc", R.NT16_TO_ASCII[col(sb, "base")].tobytes().decode()),
+                 ("bq", (col(sb, "qual") + 33).astype(np.uint8).tobytes().decode())]
+    return tags
+
+
+def _check_tags(out, res, em, molecular):
+    n_two = 0
+    for i, f in enumerate(em):
+        for e in range(2):
+            k = 2 * i + e
+            got = [(t, v) for t, _, v in R.parse_aux(bytes(out.aux[k])) if t not in ("RG", "MI", "RX")]
+            exp = _expected_tags(res.ss, f, e, int(res.cons_len[f, e]), molecular)
+            assert [t for t, _ in got] == [t for t, _ in exp], (f, e)
+            for (t, g), (_, x) in zip(got, exp):
+                if t.endswith("E"):
+                    assert np.float32(g) == x or (np.isnan(g) and np.isnan(x)), (f, e, t, g, x)
+                else:
+                    assert g == x, (f, e, t)
+            n_two += any(t == "bd" for t, _ in got)
+    return n_two
+
+
+def _cons_of(res, with_ss=True):
+    cons = type("C", (), {})()
+    cons.fam_rec_off, cons.fam_src = res.fam_rec_off, res.fam_src
+    cons.status, cons.fam_mi, cons.length = res.status.astype(np.uint8), res.fam_mi, res.cons_len
+    cons.seq, cons.qual = res.cons_seq, res.cons_qual
+    cons.ss = res.ss if with_ss else None
+    return cons
+
+
+def test_consensus_tags_of_the_oracle_consensus(tmp_path):
+    """fgbio's per-read / per-base consensus tags (SURVEY.md 8a row 8) from the restatement's
+    single-strand reads, through the native encoder, the BAM writer and the reader."""
+    s, raw = _messy(300, seed=8)
+    res = oracle.run(raw, s.ref)
+    ss = res.ss
+    assert (ss["err"] <= ss["depth"]).all() and (ss["depth"] >= 0).all()
+    hdr = _header(s.ref)
+    p = str(tmp_path / "t.bam")
+    bam.write_bam(p, bam.output_header(hdr), bam.duplex_records(_cons_of(res), raw, "x"))
+    _, out = bam.read_bam(p)
+    em = np.nonzero(res.status == 1)[0]
+    assert out.n == 2 * em.shape[0]
+    assert _check_tags(out, res, em, False) > 0  # both-strand records are covered
+    # one-strand families (AB-only / BA-only ends) are covered too
+    one = [(f, e) for f in em for e in range(2) if (res.ss["len"][f, [0, 1][e]] > 0) != (res.ss["len"][f, [3, 2][e]] > 0)]
+    assert one
+
+
+def test_molecular_tags_of_the_oracle_consensus(tmp_path):
+    from bsseqconsensusreads_amd import pipeline
+    s, raw = _messy(200, seed=9)
+    raw = R.take(raw, np.lexsort((raw.mi_strand, raw.mi_id)))
+    rm = pipeline.molecular_records(raw)
+    res = oracle.run(rm, s.ref, run_tools=False, family_order="mi-group")
+    p = str(tmp_path / "m.bam")
+    bam.write_bam(p, bam.output_header(_header(s.ref)), bam.duplex_records(_cons_of(res), rm, "x", molecular=True))
+    _, out = bam.read_bam(p)
+    em = np.nonzero(res.status == 1)[0]
+    assert out.n == 2 * em.shape[0]
+    assert _check_tags(out, res, em, True) == 0

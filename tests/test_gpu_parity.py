@@ -35,6 +35,23 @@ def assert_consensus_equal(cons, ref, what=""):
                     what, f, e, d[:8], cons.qual[f, e, d[:8]], ref.cons_qual[f, e, d[:8]]))
 
 
+def assert_ss_equal(cons, ref, what=""):
+    """The single-strand reads and consensus-tag column statistics (BSDC_MODE_TAGS) of every
+    family and set equal the restatement's."""
+    assert cons.ss is not None, what + ": no tag outputs"
+    assert np.array_equal(cons.ss["len"], ref.ss["len"]), what + ": single-strand lengths"
+    F = len(ref.status)
+    for f in range(F):
+        for s in range(4):
+            n = int(ref.ss["len"][f, s])
+            for k in ("base", "qual", "depth", "err"):
+                g, r = cons.ss[k][f, s, :n].astype(np.int64), ref.ss[k][f, s, :n].astype(np.int64)
+                if not np.array_equal(g, r):
+                    d = np.nonzero(g != r)[0]
+                    raise AssertionError("%s: family %d set %d %s differs at %s: gpu %s oracle %s" % (
+                        what, f, s, k, d[:8], g[d[:8]], r[d[:8]]))
+
+
 def test_tool1_fuzz_matches_reference(engine):
     g = load_golden("tool1_fuzz.json.gz")
     raw, ref = golden_inputs(g)
@@ -75,9 +92,10 @@ def test_synthetic_configs_vs_oracle(engine, cfg):
         fb = batch.build_family_batch(s.raw, "full", s.ref)
         assert np.diff(fb.fam_off.astype(np.int64)).max() > 600
     engine.load_reference(s.ref)
-    cons, t2 = pipeline.run_step5(engine, s.raw, dump=True)
+    cons, t2 = pipeline.run_step5(engine, s.raw, dump=True, tags=True)
     ref = oracle.run(s.raw, s.ref)
     assert_consensus_equal(cons, ref, cfg)
+    assert_ss_equal(cons, ref, cfg)
     # the fused kernel's tool-2 state equals the restatement's tool-2 records
     assert np.array_equal(t2.src, ref.tool2.src)
     assert np.array_equal(t2.pos, ref.tool2.pos)
@@ -91,8 +109,10 @@ def test_messy_records_vs_oracle(engine):
     s = synth.generate("C2", 800, seed=5, device="cpu", genome_len=200_000)
     raw = synth.messify(s.raw, frac=0.25, seed=9)
     engine.load_reference(s.ref)
-    cons, _ = pipeline.run_step5(engine, raw)
-    assert_consensus_equal(cons, oracle.run(raw, s.ref), "messy")
+    cons, _ = pipeline.run_step5(engine, raw, tags=True)
+    ref = oracle.run(raw, s.ref)
+    assert_consensus_equal(cons, ref, "messy")
+    assert_ss_equal(cons, ref, "messy")
 
 
 def test_read_through_trim_vs_oracle(engine):
@@ -122,8 +142,10 @@ def test_large_family_kernel(engine, where, monkeypatch):
 
     monkeypatch.setattr(pipeline, "build_family_batch", forced)
     engine.load_reference(s.ref)
-    cons, _ = pipeline.run_step5(engine, raw)
-    assert_consensus_equal(cons, oracle.run(raw, s.ref), "large-" + where)
+    cons, _ = pipeline.run_step5(engine, raw, tags=True)
+    ref = oracle.run(raw, s.ref)
+    assert_consensus_equal(cons, ref, "large-" + where)
+    assert_ss_equal(cons, ref, "large-" + where)
 
 
 def test_vote_only_on_tool2_output(engine):
@@ -199,6 +221,10 @@ def test_step5_bam_end_to_end(engine, tmp_path):
             assert out.names[int(out.name_id[k])] == ("L1:%s" % raw.mi_names[int(ref.fam_mi[f])]).encode()
             assert np.array_equal(out.seq[o:o + L], ref.cons_seq[f, e, :L])
             assert np.array_equal(out.qual[o:o + L], ref.cons_qual[f, e, :L])
+    # fgbio's consensus tags, from the kernels' single-strand reads, equal the ones the encoder
+    # makes from the restatement's (tests/test_bam.py checks the encoder itself)
+    from test_bam import _check_tags
+    assert _check_tags(out, ref, em, False) > 0
 
 
 def _grouped(cfg, n_fam, seed, messy=0.0):
@@ -213,9 +239,10 @@ def test_molecular_vs_oracle(engine, cfg, n_fam, messy):
     """Step 1 (CallMolecularConsensusReads, main.snake.py:46-55): the same vote kernel over MI runs
     (no BA side); equal to the restatement run as callduplex on the run records."""
     s, raw = _grouped(cfg, n_fam, seed=21, messy=messy)
-    cons, rm = pipeline.run_molecular(engine, raw)
+    cons, rm = pipeline.run_molecular(engine, raw, tags=True)
     ref = oracle.run(rm, s.ref, run_tools=False, family_order="mi-group")
     assert_consensus_equal(cons, ref, "molecular " + cfg)
+    assert_ss_equal(cons, ref, "molecular " + cfg)
     assert ((cons.status & 4) == 0).all()  # no BA side anywhere
     assert (cons.status & 1).sum() > 0.5 * len(rm.mi_names)
 
