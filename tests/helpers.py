@@ -49,3 +49,27 @@ def compare_records(golden_out, produced, raw, inputs, what=""):
             assert exp == got, ctx + ": tag %s %r vs %r" % (t, got, exp)
         # every other tag passes through
         assert {k: v for k, v in gt.items() if k not in ("RD", "LA")} == {k: v for k, v in st.items() if k not in ("RD", "LA")}, ctx
+
+
+def trim_tails(raw, frac=0.3, seed=1, min_len=30):
+    """Adapter-trimmed reads: a fraction of records lose a random number of 3' bases (sequencing
+    orientation: the end of a forward read, the start of a reverse one), cigar and position
+    adjusted.  Simple-cigar records only; others pass unchanged."""
+    rng = np.random.default_rng(seed)
+    b = R._Builder()
+    for k in range(raw.n):
+        seq, qual = raw.record_seq(k).copy(), raw.record_qual(k).copy()
+        cig = [int(x) for x in raw.record_cigar(k)]
+        flag, pos, L = int(raw.flag[k]), int(raw.pos[k]), len(seq)
+        if len(cig) == 1 and (cig[0] & 0xF) == R.OP_M and L > min_len and rng.random() < frac:
+            cut = int(rng.integers(1, L - min_len))
+            if flag & 16:  # reverse read: its 3' end is the leftmost bases
+                seq, qual, pos = seq[cut:], qual[cut:], pos + cut
+            else:
+                seq, qual = seq[:L - cut], qual[:L - cut]
+            cig = [((L - cut) << 4) | R.OP_M]
+        tags = [("MI", "Z", "%s/%s" % (raw.mi_id[k], "A" if raw.mi_strand[k] == 0 else "B")),
+                ("MC", "Z", "%dM" % L)]
+        b.add(("t%d" % raw.name_id[k]).encode(), flag, int(raw.tid[k]), pos, 60, cig, seq, qual,
+              int(raw.next_tid[k]), int(raw.next_pos[k]), int(raw.tlen[k]), R.encode_aux(tags), tags)
+    return b.finish()

@@ -9,7 +9,7 @@ import pytest
 
 from bsseqconsensusreads_amd import batch, pipeline, synth
 from bsseqconsensusreads_amd import records as R
-from helpers import compare_records, golden_inputs, load_golden
+from helpers import compare_records, golden_inputs, load_golden, trim_tails
 from oracle import oracle
 
 pytestmark = pytest.mark.gpu
@@ -113,6 +113,22 @@ def test_messy_records_vs_oracle(engine):
     ref = oracle.run(raw, s.ref)
     assert_consensus_equal(cons, ref, "messy")
     assert_ss_equal(cons, ref, "messy")
+
+
+@pytest.mark.parametrize("read_len,trim", [(100, 0.0), (250, 0.0), (150, 0.4), (300, 0.2)])
+def test_read_lengths_vs_oracle(engine, read_len, trim):
+    """2x100 / 2x250 / 2x300 runs and adapter-trimmed reads of mixed lengths (columns past a read's
+    end, consensus lengths set by the longest read, wider arenas and output strides)."""
+    s = synth.generate("C2", 600, seed=31, device="cpu", genome_len=200_000, read_len=read_len)
+    raw = trim_tails(s.raw, trim, seed=4) if trim else s.raw
+    engine.load_reference(s.ref)
+    cons, t2 = pipeline.run_step5(engine, raw, dump=True, tags=True)
+    ref = oracle.run(raw, s.ref)
+    assert_consensus_equal(cons, ref, "L%d trim %.1f" % (read_len, trim))
+    assert_ss_equal(cons, ref, "L%d" % read_len)
+    assert np.array_equal(t2.seq, ref.tool2.seq) and np.array_equal(t2.pos, ref.tool2.pos)
+    if trim:
+        assert len(set(ref.cons_len[ref.status == 1].reshape(-1).tolist())) > 10
 
 
 def test_read_through_trim_vs_oracle(engine):
