@@ -41,6 +41,10 @@ constexpr int kWave = 64;
 #ifndef SMALL_SGPRS
 #define SMALL_SGPRS (SMALL_WAVES >= 8 ? 80 : 96)  // SGPR budget: <= 80 -> 8, <= 96 -> 7 waves per SIMD (MI355X_MICROARCH.md)
 #endif
+#ifndef SMALL_STAGE_U
+#define SMALL_STAGE_U 4  // k_small staging: image chunk loads in flight per lane
+#endif
+constexpr int kStageU = SMALL_STAGE_U;
 constexpr int kLargeThreads = 256;
 constexpr int kSmallMaxWaves = 8;              // wavefronts (families) per small-kernel workgroup, at most
 constexpr int kSmallMinWaves = SMALL_WAVES >= 8 ? 8 : 6;  // occupancy target the register budget is cut for
@@ -724,9 +728,9 @@ __global__ __launch_bounds__(kWave *kSmallMaxWaves, kSmallMinWaves) __attribute_
         if (k >= nqc && k < nch)
             unpack32<true>(v, bimg + 32 * (k - nqc));
     };
-    uint4 v[4];
+    uint4 v[kStageU];
 #pragma unroll
-    for (int u = 0; u < 4; u++) v[u] = load_img(t + 64 * u);
+    for (int u = 0; u < kStageU; u++) v[u] = load_img(t + 64 * u);
 
     const uint32_t gslot = rc.x;
     int32_t pos = (int32_t)rc.y;
@@ -777,12 +781,12 @@ __global__ __launch_bounds__(kWave *kSmallMaxWaves, kSmallMinWaves) __attribute_
 #pragma unroll
     for (int u = 0; u < 2; u++) wv[u] = load_win(t + 64 * u);
 #pragma unroll
-    for (int u = 0; u < 4; u++) store_img(t + 64 * u, v[u]);
-    for (int k0 = 256; k0 < nch; k0 += 256) {  // families with more than 256 image chunks
+    for (int u = 0; u < kStageU; u++) store_img(t + 64 * u, v[u]);
+    for (int k0 = 64 * kStageU; k0 < nch; k0 += 64 * kStageU) {  // families with more image chunks
 #pragma unroll
-        for (int u = 0; u < 4; u++) v[u] = load_img(k0 + t + 64 * u);
+        for (int u = 0; u < kStageU; u++) v[u] = load_img(k0 + t + 64 * u);
 #pragma unroll
-        for (int u = 0; u < 4; u++) store_img(k0 + t + 64 * u, v[u]);
+        for (int u = 0; u < kStageU; u++) store_img(k0 + t + 64 * u, v[u]);
     }
 #pragma unroll
     for (int u = 0; u < 2; u++) store_win(t + 64 * u, wv[u]);
