@@ -44,7 +44,7 @@ class ConsensusC(C.Structure):
 EXPORTS = ("bsdc_abi_version", "bsdc_ctx_create", "bsdc_ctx_destroy", "bsdc_last_error",
            "bsdc_load_reference", "bsdc_run", "bsdc_convert", "bsdc_extend", "bsdc_duplex_call",
            "bsdc_family_arena_bytes", "bsdc_small_arena_bytes", "bsdc_get_tables", "bsdc_model_tables",
-           "bsdc_agree_tables")
+           "bsdc_agree_tables", "bsdc_phred_buckets")
 
 _lib = None
 
@@ -83,6 +83,8 @@ def load(path: str = LIB_PATH):
     lib.bsdc_model_tables.restype = None
     lib.bsdc_agree_tables.argtypes = [C.c_double, C.c_double, C.c_void_p, C.c_void_p]
     lib.bsdc_agree_tables.restype = None
+    lib.bsdc_phred_buckets.argtypes = [C.c_double, C.c_double, C.c_void_p]
+    lib.bsdc_phred_buckets.restype = None
     if lib.bsdc_abi_version() != BSDC_ABI_VERSION:
         raise RuntimeError("libbsdc ABI %d != %d" % (lib.bsdc_abi_version(), BSDC_ABI_VERSION))
     if path == LIB_PATH:

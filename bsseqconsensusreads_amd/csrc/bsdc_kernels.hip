@@ -51,7 +51,10 @@ constexpr int kSmallMinWaves = SMALL_WAVES >= 8 ? 8 : 6;  // occupancy target th
 constexpr int kSmallSimdWaves = SMALL_WAVES;   // waves per SIMD its registers allow
 constexpr int kLdsBytes = 160 * 1024;           // LDS per CU
 constexpr double kLrScale = 1048576.0;          // 2^20
-constexpr int kTabBytes = 1024 + 1024 + 384 + 2048 + 192;  // the Tables image in LDS
+constexpr int kSqBuckets = 136;                 // phred buckets of S: 4 per octave over [2^-32, 4)
+constexpr int kSqBase = (127 - 32) << 2;         // (float bits >> 21) of 2^-32
+constexpr int kTabBytesL = 1024 + 1024 + 384 + 144;  // the prefix k_large uses (zero, lr, thr, sq)
+constexpr int kTabBytes = kTabBytesL + 2048 + 192;  // the Tables image in LDS
 // k_small base bytes in LDS: nt16 code | 0x10 for A, C, G, T (set at staging, see unpack32)
 constexpr uint32_t kLinkRdDev = 1u << 27;       // device-internal: tool 1 trimmed a base (RD=1)
 
@@ -62,6 +65,7 @@ struct Tables {
     int32_t zero[256];  // row 0 of the vote's [valid][q] table: a non-ACGT base adds nothing
     int32_t lr[256];    // round((ln(1-a) - ln(a/3)) * 2^20), a = P(error) of a Q base after the post-UMI step
     float thr[96];      // Q >= k  <=>  S <= thr[k]
+    uint8_t sq[144];    // Q at the top of S bucket j (S bits >> 21 = kSqBase + j; bucket 0 also below)
     uint8_t qlo[2048];  // agreement case (S = 3 e^-D): Q at D = 2^16 k
     int32_t dthr[48];   // agreement case: smallest D with Q >= q (INT32_MAX: never)
 };
@@ -109,20 +113,16 @@ __device__ __forceinline__ float term32(int32_t d) {
     return x < -80.0f ? 0.0f : det_expf(x);
 }
 
-// Q = max k with S <= thr[k] (thr is non-increasing), binary search over 1..93
+// Q = max k with S <= thr[k] (thr is non-increasing, S >= 0).  Tables::sq[j] is Q at the top of
+// S's bucket (4 buckets per octave, so at most one threshold inside for the usual parameters), a
+// lower bound on Q(S); step up while the next threshold still holds -- exact for any thr.
+// `thr` points into a Tables image: sq follows it.
 __device__ __forceinline__ int phred_of(float S, const float *thr) {
-    int lo = 0, hi = 93;
-#pragma unroll
-    for (int it = 0; it < 7; it++) {
-        const int mid = (lo + hi + 1) >> 1;
-        if (lo < hi) {
-            if (S <= thr[mid])
-                lo = mid;
-            else
-                hi = mid - 1;
-        }
-    }
-    return lo;
+    const uint8_t *sq = reinterpret_cast<const uint8_t *>(thr + 96);
+    const int j = ::min(::max((int)(__float_as_uint(S) >> 21) - kSqBase, 0), kSqBuckets - 1);
+    int q = sq[j];
+    while (q < 93 && S <= thr[q + 1]) q++;
+    return q;
 }
 
 // Per-column statistics of a single-strand consensus read (BSDC_MODE_TAGS), as fgbio
@@ -408,11 +408,15 @@ struct KParams {
     uint32_t ref_chunks_inv;  // ceil(2^32 / ref_chunks)
 };
 
+// the first `bytes` of the Tables image (k_small: all of it; k_large: the kTabBytesL prefix)
+template <int BYTES>
 __device__ __forceinline__ void load_tables(const Tables *tab, uint8_t *dst) {
     static_assert(sizeof(Tables) == kTabBytes, "Tables image");
+    static_assert(offsetof(Tables, sq) == offsetof(Tables, thr) + sizeof(float) * 96, "sq follows thr");
+    static_assert(offsetof(Tables, qlo) == kTabBytesL, "k_large's prefix");
     const uint4 *src = reinterpret_cast<const uint4 *>(tab);
     uint4 *d = reinterpret_cast<uint4 *>(dst);
-    for (int i = threadIdx.x; i < kTabBytes / 16; i += blockDim.x) d[i] = src[i];
+    for (int i = threadIdx.x; i < BYTES / 16; i += blockDim.x) d[i] = src[i];
     __syncthreads();
 }
 
@@ -673,7 +677,7 @@ __global__ __launch_bounds__(kWave *kSmallMaxWaves, kSmallMinWaves) __attribute_
     const uint8_t *qlo = T->qlo;
     const int32_t *dthr = T->dthr;
     if (((P.mode >> BSDC_MODE_STOP_SHIFT) & 15) == 15) return;  // profiling: launch cost alone
-    load_tables(P.tab, reinterpret_cast<uint8_t *>(&s_tab));
+    load_tables<kTabBytes>(P.tab, reinterpret_cast<uint8_t *>(&s_tab));
     if (((P.mode >> BSDC_MODE_STOP_SHIFT) & 15) == 14) return;  // profiling: + the table copy
     const int w = threadIdx.x >> 6;
     const int t = threadIdx.x & 63;
@@ -2067,16 +2071,23 @@ __device__ void process_large(const KParams &P, uint8_t *A, const int32_t *lr, c
     }
 }
 
-static_assert(BSDC_LARGE_LDS_MAX + kTabBytes + 256 <= kLdsBytes, "large-family LDS budget");
+static_assert(BSDC_LARGE_LDS_MAX + kTabBytesL + 256 <= kLdsBytes, "large-family LDS budget");
+struct TablesL {  // k_large's LDS copy: the prefix of Tables it reads
+    int32_t zero[256];
+    int32_t lr[256];
+    float thr[96];
+    uint8_t sq[144];
+};
+static_assert(sizeof(TablesL) == kTabBytesL, "TablesL image");
 template <bool IN_LDS>
 __global__ __launch_bounds__(kLargeThreads, 5) void k_large(KParams P, const uint4 *fams, int64_t nfams, int32_t arena) {
     extern __shared__ __attribute__((aligned(16))) uint8_t smem[];  // the family's arena (IN_LDS)
-    __shared__ __attribute__((aligned(16))) Tables s_tab;
+    __shared__ __attribute__((aligned(16))) TablesL s_tab;
     __shared__ int red[kLargeThreads / kWave];
     __shared__ int s_cnt[4], s_lc[4], s_cur[4];
-    const Tables *T = &s_tab;
+    const TablesL *T = &s_tab;
     if (((P.mode >> BSDC_MODE_STOP_SHIFT) & 15) == 15) return;  // profiling: launch cost alone
-    load_tables(P.tab, reinterpret_cast<uint8_t *>(&s_tab));
+    load_tables<kTabBytesL>(P.tab, reinterpret_cast<uint8_t *>(&s_tab));
     if (((P.mode >> BSDC_MODE_STOP_SHIFT) & 15) == 14) return;  // profiling: + the table copy
     const int32_t *lr = T->lr;
     const float *thr = T->thr;
@@ -2149,6 +2160,18 @@ static void make_tables(double pre, double post, Tables &t) {
         t.thr[k] = tt < 0.0 ? -1.0f : (float)(tt / (1.0 - tt));
     }
     t.thr[94] = t.thr[95] = -1.0f;
+    // sq[j] = Q at the largest S of bucket j (bits (kSqBase + j + 1) << 21, minus one ulp): Q is
+    // non-increasing in S, so it is a lower bound on Q over the bucket (and below it, for j = 0)
+    for (int j = 0; j < 144; j++) {
+        const int jj = j < kSqBuckets ? j : kSqBuckets - 1;
+        const uint32_t bits = ((uint32_t)(kSqBase + jj + 1) << 21) - 1u;
+        float S;
+        memcpy(&S, &bits, 4);
+        int q = 0;
+        for (int k = 1; k < 94; k++)
+            if (S <= t.thr[k]) q = k;
+        t.sq[j] = (uint8_t)q;
+    }
     // agreement case: every other base has D = 0, S = ((0 + e) + e) + e with e = term(-D); Q(D)
     // is the oracle's arithmetic on the host (same float ops), tabulated exactly:
     // Q(D) = qlo[D >> 16] + (D >= dthr[qlo[D >> 16] + 1]).  tests/test_abi.py checks every D.
@@ -2210,6 +2233,12 @@ void bsdc_agree_tables(double pre, double post, uint8_t *qlo2048, int32_t *dthr4
     make_tables(pre, post, t);
     memcpy(qlo2048, t.qlo, sizeof t.qlo);
     memcpy(dthr48, t.dthr, sizeof t.dthr);
+}
+
+void bsdc_phred_buckets(double pre, double post, uint8_t *sq144) {
+    Tables t;
+    make_tables(pre, post, t);
+    memcpy(sq144, t.sq, sizeof t.sq);
 }
 
 int32_t bsdc_ctx_create(int32_t device, const bsdc_params *params, bsdc_ctx **out) {

@@ -161,6 +161,9 @@ int32_t bsdc_get_tables(const bsdc_ctx *ctx, int64_t *lr256, float *thresh94);
 void bsdc_model_tables(double error_rate_pre_umi, double error_rate_post_umi, int64_t *lr256, float *thresh94);
 /* The vote's agreement-case tables: Q(D) = qlo[D >> 16] + (D >= dthr[qlo[D >> 16] + 1]). */
 void bsdc_agree_tables(double error_rate_pre_umi, double error_rate_post_umi, uint8_t *qlo2048, int32_t *dthr48);
+/* The general case's phred buckets: Q(S) = the largest k >= sq[j] with S <= thresh[k], j = the
+   bucket of S ((float bits >> 21) - ((127 - 32) << 2), clamped to [0, 135]). */
+void bsdc_phred_buckets(double error_rate_pre_umi, double error_rate_post_umi, uint8_t *sq144);
 
 #ifdef __cplusplus
 }

@@ -80,3 +80,31 @@ def test_agreement_tables_exhaustive():
         lib.bsdc_agree_tables(pre, post, qlo.ctypes.data, dthr.ctypes.data)
         _, thr = oracle.tables(pre, post)
         assert oracle.check_agree_tables(qlo, dthr, thr, (1 << 27) + 1000) == -1
+
+
+def test_phred_buckets_match_threshold_scan():
+    """The kernels' phred of the general (disagreement) case -- bucket lower bound Tables::sq, then
+    step up while S <= thr[q + 1] -- equals oracle/'s rule (the largest k with S <= thr[k]) on
+    every 2^7-th float in [0, 4) (S = the sum of three exp terms <= 1) and on every threshold and
+    its float neighbours."""
+    lib = _lib.load()
+    for pre, post in ((45.0, 30.0), (40.0, 20.0), (93.0, 93.0), (10.0, 5.0)):
+        sq = np.zeros(144, np.uint8)
+        lib.bsdc_phred_buckets(pre, post, sq.ctypes.data)
+        _, thr = oracle.tables(pre, post)
+        thr = np.concatenate([np.asarray(thr, np.float32)[:94], np.float32([-1.0, -1.0])])
+        bits = np.arange(0, 0x40800000, 1 << 7, dtype=np.uint32)
+        t = thr[1:94][thr[1:94] > 0]
+        bits = np.concatenate([bits, t.view(np.uint32) - 1, t.view(np.uint32), t.view(np.uint32) + 1])
+        bits = bits[bits < 0x40800000]
+        S = bits.view(np.float32)
+        want = np.searchsorted(-thr[1:94], -S, side="right")  # thr is non-increasing
+        j = np.clip((bits >> 21).astype(np.int64) - ((127 - 32) << 2), 0, 135)
+        q = sq[j].astype(np.int64)
+        for _ in range(94):
+            up = (q < 93) & (S <= thr[np.minimum(q + 1, 95)])
+            if not up.any():
+                break
+            q = q + up
+        bad = np.nonzero(q != want)[0]
+        assert bad.size == 0, (pre, post, S[bad[:5]], q[bad[:5]], want[bad[:5]])
