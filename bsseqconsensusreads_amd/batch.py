@@ -203,6 +203,18 @@ def _clips_reflen(cig: np.ndarray, off: np.ndarray, cnt: np.ndarray):
     length, trailing S/H length, reference-consuming length."""
     n = cnt.shape[0]
     cnt = np.where(cnt > 0, cnt, 0).astype(np.int64)
+    one = cnt == 1
+    if one.any():  # one-op cigars (the common 150M) without the per-op expansion
+        lead, trail, reflen = np.zeros(n, np.int64), np.zeros(n, np.int64), np.zeros(n, np.int64)
+        c1 = cig[np.where(one, off, 0).astype(np.int64)]
+        op1, ln1 = (c1 & 0xF).astype(np.int64), (c1 >> 4).astype(np.int64)
+        reflen[one] = np.where(np.isin(op1, R.REF_CONSUMING), ln1, 0)[one]
+        lead[one] = np.where(np.isin(op1, (R.OP_S, R.OP_H)), ln1, 0)[one]  # a lone clip leads
+        many = np.nonzero(cnt > 1)[0]
+        if many.shape[0]:
+            lm_, tm_, rm_ = _clips_reflen(cig, np.asarray(off)[many], cnt[many])
+            lead[many], trail[many], reflen[many] = lm_, tm_, rm_
+        return lead, trail, reflen
     tot = int(cnt.sum())
     if tot == 0:
         z = np.zeros(n, np.int64)

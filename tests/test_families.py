@@ -170,3 +170,32 @@ def test_cli_arguments():
     for bad in (["step5", "in.bam", "out.bam"], ["molecular", "in.bam", "-"], ["molecular", "i", "o", "--fastq1", "a"]):
         with pytest.raises(SystemExit):
             cli.parse(bad)
+
+
+def test_clips_reflen_vs_loop():
+    """_clips_reflen (one-op fast path + the per-op expansion) against a loop over the cigar ops:
+    leading / trailing S+H and the reference-consuming length, absent and all-clip cigars included."""
+    rng = np.random.default_rng(3)
+    n = 4000
+    cnt = rng.integers(-1, 6, n)
+    cnt[rng.random(n) < 0.5] = 1
+    c = np.maximum(cnt, 0)
+    off = np.zeros(n, np.int64)
+    off[1:] = np.cumsum(c)[:-1]
+    off[cnt <= 0] = -1
+    cig = (rng.integers(1, 200, c.sum()) << 4 | rng.choice([0, 1, 2, 3, 4, 5, 7, 8], c.sum())).astype(np.uint32)
+    want = ([], [], [])
+    for o, k in zip(off, cnt):
+        ops = [(int(x) & 15, int(x) >> 4) for x in cig[o:o + k]] if k > 0 else []
+        i, lead = 0, 0
+        while i < len(ops) and ops[i][0] in (R.OP_S, R.OP_H):
+            lead += ops[i][1]
+            i += 1
+        j, trail = len(ops) - 1, 0
+        while j >= i and ops[j][0] in (R.OP_S, R.OP_H):
+            trail += ops[j][1]
+            j -= 1
+        for lst, v in zip(want, (lead, trail, sum(ln for op, ln in ops if op in R.REF_CONSUMING))):
+            lst.append(v)
+    for g, w in zip(batch._clips_reflen(cig, off, cnt), want):
+        assert np.array_equal(g, np.asarray(w))
