@@ -45,7 +45,10 @@ constexpr int kWave = 64;
 #define SMALL_STAGE_U 4  // k_small staging: image chunk loads in flight per lane
 #endif
 constexpr int kStageU = SMALL_STAGE_U;
-constexpr int kLargeThreads = 256;
+#ifndef LARGE_THREADS
+#define LARGE_THREADS 256  // k_large workgroup size (a multiple of 64)
+#endif
+constexpr int kLargeThreads = LARGE_THREADS;
 constexpr int kSmallMaxWaves = 8;              // wavefronts (families) per small-kernel workgroup, at most
 constexpr int kSmallMinWaves = SMALL_WAVES >= 8 ? 8 : 6;  // occupancy target the register budget is cut for
 constexpr int kSmallSimdWaves = SMALL_WAVES;   // waves per SIMD its registers allow
