@@ -1660,6 +1660,7 @@ __device__ void process_large(const KParams &P, uint8_t *A, const int32_t *lr, c
     // family without quals >= 128) run flattened over (template, 4 positions) through overlap4;
     // the rest take the per-position path, one wave per template.  Templates share no bytes.
     const bool wild = block_max((qor & 0x80808080u) != 0 ? 1 : 0, red) != 0;
+    if (stop == 11) return;
     if (P.overlap) {
         uint32_t *tl = reinterpret_cast<uint32_t *>(lists);  // fast: 3 words each from the front; slow: 1 from the back
         if (tt == 0) {
@@ -1687,6 +1688,7 @@ __device__ void process_large(const KParams &P, uint8_t *A, const int32_t *lr, c
             }
         }
         __syncthreads();
+        if (stop == 12) return;
         const int nfast = s_cnt[0], nslow = s_cnt[1];
         const int SDo = (maxlen_f + 2 + 3) >> 2;  // dwords of the longest overlap
         for (int k0 = tt; k0 < nfast * SDo; k0 += 2 * G) {
