@@ -49,6 +49,10 @@ constexpr int kStageU = SMALL_STAGE_U;
 #define LARGE_THREADS 256  // k_large workgroup size (a multiple of 64)
 #endif
 constexpr int kLargeThreads = LARGE_THREADS;
+#ifndef LARGE_OVL_CHUNKS
+#define LARGE_OVL_CHUNKS 2  // k_large overlap: SWAR dwords (4 positions each) per task
+#endif
+constexpr int kOvlChunks = LARGE_OVL_CHUNKS;
 constexpr int kSmallMaxWaves = 8;              // wavefronts (families) per small-kernel workgroup, at most
 constexpr int kSmallMinWaves = SMALL_WAVES >= 8 ? 8 : 6;  // occupancy target the register budget is cut for
 constexpr int kSmallSimdWaves = SMALL_WAVES;   // waves per SIMD its registers allow
@@ -1690,29 +1694,20 @@ __device__ void process_large(const KParams &P, uint8_t *A, const int32_t *lr, c
         __syncthreads();
         if (stop == 12) return;
         const int nfast = s_cnt[0], nslow = s_cnt[1];
-        const int SDo = (maxlen_f + 2 + 3) >> 2;  // dwords of the longest overlap
-        for (int k0 = tt; k0 < nfast * SDo; k0 += 2 * G) {
-            uint32_t ia[2], ib[2];
-            int rem[2];
+        // a task is 4 * kOvlChunks positions of one template (kOvlChunks SWAR dwords): the task ->
+        // template map, the entry loads and the address math are paid once per task
+        const int SDo = (maxlen_f + 2 + 4 * kOvlChunks - 1) / (4 * kOvlChunks);  // tasks of the longest overlap
+        for (int k = tt; k < nfast * SDo; k += G) {
+            const int g = k / SDo, j = 4 * kOvlChunks * (k - g * SDo);
+            const int rem = (int)tl[3 * g + 2] - j;
+            const uint32_t ia = tl[3 * g] + (uint32_t)j, ib = tl[3 * g + 1] + (uint32_t)j;
+            Ovl4 o[kOvlChunks];
 #pragma unroll
-            for (int u = 0; u < 2; u++) {
-                const int k = k0 + u * G;
-                rem[u] = 0;
-                ia[u] = ib[u] = 0;
-                if (k < nfast * SDo) {
-                    const int g = k / SDo, j = 4 * (k - g * SDo);
-                    rem[u] = (int)tl[3 * g + 2] - j;
-                    ia[u] = tl[3 * g] + (uint32_t)j;
-                    ib[u] = tl[3 * g + 1] + (uint32_t)j;
-                }
-            }
-            Ovl4 o[2];
+            for (int c = 0; c < kOvlChunks; c++)
+                if (rem > 4 * c) o[c] = ovl4_load(slots, qimg, ia + 4 * c, ib + 4 * c);
 #pragma unroll
-            for (int u = 0; u < 2; u++)
-                if (rem[u] > 0) o[u] = ovl4_load(slots, qimg, ia[u], ib[u]);
-#pragma unroll
-            for (int u = 0; u < 2; u++)
-                if (rem[u] > 0) ovl4_store(slots, qimg, ia[u], ib[u], rem[u], ovl4_compute(o[u], rem[u]));
+            for (int c = 0; c < kOvlChunks; c++)
+                if (rem > 4 * c) ovl4_store(slots, qimg, ia + 4 * c, ib + 4 * c, rem - 4 * c, ovl4_compute(o[c], rem - 4 * c));
         }
         for (int i = tt >> 6; i < nslow; i += G / kWave) {
             const int r = (int)tl[2 * n - 1 - i];
