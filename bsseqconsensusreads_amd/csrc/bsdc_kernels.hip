@@ -53,6 +53,11 @@ constexpr int kLargeThreads = LARGE_THREADS;
 #define LARGE_OVL_CHUNKS 2  // k_large overlap: SWAR dwords (4 positions each) per task
 #endif
 constexpr int kOvlChunks = LARGE_OVL_CHUNKS;
+#ifndef LARGE_CONV_H
+#define LARGE_CONV_H 2  // k_large convert: SWAR dwords (4 positions each) per task, 1 or 2
+#endif
+constexpr int kConvH = LARGE_CONV_H;
+static_assert(kConvH == 1 || kConvH == 2, "16 reference nibbles cover at most 9 positions");
 constexpr int kSmallMaxWaves = 8;              // wavefronts (families) per small-kernel workgroup, at most
 constexpr int kSmallMinWaves = SMALL_WAVES >= 8 ? 8 : 6;  // occupancy target the register budget is cut for
 constexpr int kSmallSimdWaves = SMALL_WAVES;   // waves per SIMD its registers allow
@@ -1519,9 +1524,12 @@ __device__ void process_large(const KParams &P, uint8_t *A, const int32_t *lr, c
             if (M[r].link & BSDC_LINK_CONVERT) clist[atomicAdd(&s_cnt[0], 1)] = (uint16_t)r;
         __syncthreads();
         const int nc = s_cnt[0];
-        const int SD = (maxlen_f + 1 + 3) >> 2;  // dwords per converted record, at most
+        // a task is kConvH dwords (4 positions each) of one converted record; the 16 reference
+        // nibbles at the task's aligned 8 bytes cover 4 * kConvH + 1 positions for kConvH <= 2
+        constexpr int H = kConvH, TP = 4 * kConvH;
+        const int SD = (maxlen_f + 1 + TP - 1) / TP;  // tasks per converted record, at most
         const int total = nc * SD;
-        constexpr int kConvU = 4;  // tasks per thread per round: their global loads go out together
+        constexpr int kConvU = 4 / kConvH;  // tasks per thread per round: their global loads go out together
         for (int base = 0; base < total; base += kConvU * G) {
             int rr[kConvU], jj[kConvU], av[kConvU];
             uint32_t w0[kConvU], w1[kConvU];
@@ -1531,12 +1539,12 @@ __device__ void process_large(const KParams &P, uint8_t *A, const int32_t *lr, c
                 rr[u] = -1;
                 jj[u] = 0;
                 if (k < total) {
-                    const int ci = k / SD, j4 = 4 * (k - ci * SD);
+                    const int ci = k / SD, j4 = TP * (k - ci * SD);
                     const int r = clist[ci];
                     if (j4 < M[r].in_len + 1) {
                         rr[u] = r;
                         jj[u] = j4;
-                        // nibbles win + j4 .. + 4 (high nibble first) lie in the 8 aligned bytes at a4
+                        // nibbles win + j4 .. + TP (high nibble first) lie in the 8 aligned bytes at a4
                         const uint64_t x0 = (uint64_t)M[r].win + (uint64_t)j4;
                         const uint32_t *rw = reinterpret_cast<const uint32_t *>(P.ref + ((x0 >> 1) & ~3ull));
                         w0[u] = rw[0];
@@ -1545,49 +1553,61 @@ __device__ void process_large(const KParams &P, uint8_t *A, const int32_t *lr, c
                     }
                 }
             }
-            uint32_t out[kConvU], wa[kConvU];
+            uint32_t out[kConvU][H], wa[kConvU][H];
+            bool ok[kConvU][H];
 #pragma unroll
             for (int u = 0; u < kConvU; u++) {
+#pragma unroll
+                for (int h = 0; h < H; h++) ok[u][h] = false;
                 if (rr[u] < 0) continue;
-                const int r = rr[u], j4 = jj[u];
+                const int r = rr[u];
                 const RecMeta m = M[r];
                 const int32_t Lm = m.in_len + 1;
-                uint32_t m4 = lds32(slots + m.slot + j4);
-                const uint32_t mn = lds32(slots + m.slot + j4 + 4);
-                const uint64_t x0 = (uint64_t)m.win + (uint64_t)j4;
+                const uint64_t x00 = (uint64_t)m.win + (uint64_t)jj[u];
                 const uint64_t W = (uint64_t)w0[u] | ((uint64_t)w1[u] << 32);
-                const int u0 = (int)(x0 - 2 * ((x0 >> 1) & ~3ull));
-                uint32_t f0 = 0, f1 = 0;
+                const int u00 = (int)(x00 - 2 * ((x00 >> 1) & ~3ull));
 #pragma unroll
-                for (int q = 0; q < 5; q++) {
-                    const int x = u0 + q;
-                    const uint32_t nb = (uint32_t)(W >> (8 * (x >> 1) + ((x & 1) ? 0 : 4))) & 0xFu;
-                    const uint32_t fb = j4 + q < av[u] ? nb : kN;
-                    if (q < 4) f0 |= fb << (8 * q);
-                    if (q > 0) f1 |= fb << (8 * (q - 1));
-                }
-                if (j4 == 0) m4 = (m4 & ~0xFFu) | (f0 & 0xFFu);  // :121 seed, m[0] = ref[0]
-                const uint32_t m1 = alignbyte(mn, m4, 1);
-                uint32_t nxt = 0x80808080u;
-                const int last = Lm - 1 - j4;  // the record's last position has no next base
-                if (last < 4) nxt &= ~(0xFFu << (8 * last));
-                out[u] = convert4f<false>(m4, m1, f0, f1, nxt);
-                wa[u] = m.slot + (uint32_t)j4;
-                if (j4 == 0) qimg[m.slot] = 40;  // :174-177 'I' + quals
-                if (last < 4) {  // :157-170 a final C before a reference G is trimmed
-                    const uint8_t rdv = (((out[u] >> (8 * last)) & 0xFF) == kC && ((f1 >> (8 * last)) & 0xFF) == kG) ? 1 : 0;
-                    RecMeta &w = M[r];
-                    w.rd = rdv;
-                    w.len = Lm - rdv;
-                    w.start = 0;
-                    w.pos = m.pos - 1 > 0 ? m.pos - 1 : 0;
-                    w.reflen = m.reflen + 1 - ((rdv && m.reflen > 0) ? 1 : 0);
+                for (int h = 0; h < H; h++) {
+                    const int j4 = jj[u] + 4 * h;
+                    if (j4 >= Lm) continue;
+                    ok[u][h] = true;
+                    uint32_t m4 = lds32(slots + m.slot + j4);
+                    const uint32_t mn = lds32(slots + m.slot + j4 + 4);
+                    const int u0 = u00 + 4 * h;
+                    uint32_t f0 = 0, f1 = 0;
+#pragma unroll
+                    for (int q = 0; q < 5; q++) {
+                        const int x = u0 + q;
+                        const uint32_t nb = (uint32_t)(W >> (8 * (x >> 1) + ((x & 1) ? 0 : 4))) & 0xFu;
+                        const uint32_t fb = j4 + q < av[u] ? nb : kN;
+                        if (q < 4) f0 |= fb << (8 * q);
+                        if (q > 0) f1 |= fb << (8 * (q - 1));
+                    }
+                    if (j4 == 0) m4 = (m4 & ~0xFFu) | (f0 & 0xFFu);  // :121 seed, m[0] = ref[0]
+                    const uint32_t m1 = alignbyte(mn, m4, 1);
+                    uint32_t nxt = 0x80808080u;
+                    const int last = Lm - 1 - j4;  // the record's last position has no next base
+                    if (last < 4) nxt &= ~(0xFFu << (8 * last));
+                    out[u][h] = convert4f<false>(m4, m1, f0, f1, nxt);
+                    wa[u][h] = m.slot + (uint32_t)j4;
+                    if (j4 == 0) qimg[m.slot] = 40;  // :174-177 'I' + quals
+                    if (last < 4) {  // :157-170 a final C before a reference G is trimmed
+                        const uint8_t rdv = (((out[u][h] >> (8 * last)) & 0xFF) == kC && ((f1 >> (8 * last)) & 0xFF) == kG) ? 1 : 0;
+                        RecMeta &w = M[r];
+                        w.rd = rdv;
+                        w.len = Lm - rdv;
+                        w.start = 0;
+                        w.pos = m.pos - 1 > 0 ? m.pos - 1 : 0;
+                        w.reflen = m.reflen + 1 - ((rdv && m.reflen > 0) ? 1 : 0);
+                    }
                 }
             }
             __syncthreads();
 #pragma unroll
             for (int u = 0; u < kConvU; u++)
-                if (rr[u] >= 0) st32(slots + wa[u], out[u]);
+#pragma unroll
+                for (int h = 0; h < H; h++)
+                    if (ok[u][h]) st32(slots + wa[u][h], out[u][h]);
             __syncthreads();
         }
     }
