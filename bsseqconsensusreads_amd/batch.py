@@ -239,6 +239,38 @@ def _clips_reflen(cig: np.ndarray, off: np.ndarray, cnt: np.ndarray):
     return lead, trail, reflen
 
 
+def _mc_clips_reflen(raw: R.RawRecords, idx: np.ndarray):
+    """MC cigars of records `idx`: (leading S/H length, trailing S/H length, reference length); a
+    clip op counts as leading when no non-clip op precedes it and as trailing when none follows
+    (an all-clip MC counts as both -- fgbio's mate-end arithmetic on an unusable mate)."""
+    idx = np.asarray(idx, np.int64)
+    m = idx.shape[0]
+    cnt = np.where(raw.mc_off[idx] >= 0, raw.mc_n[idx], 0).astype(np.int64)
+    tot = int(cnt.sum())
+    z = np.zeros(m, np.int64)
+    if tot == 0:
+        return z, z.copy(), z.copy()
+    rec = np.repeat(np.arange(m, dtype=np.int64), cnt)
+    first = np.cumsum(cnt) - cnt
+    j = np.arange(tot, dtype=np.int64) - first[rec]
+    c = raw.mc_cigar[np.repeat(np.where(cnt > 0, raw.mc_off[idx], 0), cnt) + j]
+    op = (c & 0xF).astype(np.int64)
+    ln = (c >> 4).astype(np.int64)
+    refm = np.isin(op, R.REF_CONSUMING)
+    mref = np.bincount(rec[refm], weights=ln[refm], minlength=m)[:m].astype(np.int64)
+    clip = np.isin(op, (R.OP_S, R.OP_H))
+    ncum = np.cumsum(~clip)
+    base = np.where(first > 0, ncum[np.maximum(first - 1, 0)], 0)
+    upto = ncum - base[rec]                       # non-clip ops up to and including this one
+    before = upto - (~clip)
+    after = np.bincount(rec[~clip], minlength=m)[:m][rec] - upto
+    lm = clip & (before == 0)
+    tm = clip & (after == 0)
+    lead = np.bincount(rec[lm], weights=ln[lm], minlength=m)[:m].astype(np.int64)
+    trail = np.bincount(rec[tm], weights=ln[tm], minlength=m)[:m].astype(np.int64)
+    return lead, trail, mref
+
+
 def mate_unclipped(raw: R.RawRecords):
     """Mate unclipped (start, end) from PNEXT and the MC tag (stale after tools 1/2); PNEXT alone
     without MC."""
@@ -318,13 +350,63 @@ def template_coordinate_order(raw: R.RawRecords, recs: np.ndarray, us: np.ndarra
     return np.lexsort((np.arange(recs.shape[0]), ~lower, nm, mi, N2, N1, P2, P1, T2, T1))
 
 
+@dataclass
+class FamilyPlan:
+    """Family formation over a whole record stream, before any per-record device array exists:
+    which records reach the kernels, in which order, grouped into which families, and the tool-1 /
+    tool-2 roles.  ``materialize`` turns any contiguous family range of it into a device batch, so a
+    stream larger than one batch (32-bit slot offsets, HBM budget) runs as a sequence of batches
+    whose concatenated output equals the one-batch output."""
+
+    raw: R.RawRecords
+    mode: str
+    ref: Optional[R.Reference]
+    order: np.ndarray        # i64 [R] input record of each plan record, family order
+    fam_off: np.ndarray      # i64 [F + 1]
+    fam_mi: np.ndarray       # i32 [F]
+    t2_rank: np.ndarray      # i64 [R] tool-2 output position of each plan record
+    conv: np.ndarray         # bool [n] per input record: tool 1 converts it (this launch)
+    ext_right: np.ndarray    # bool [n] tool 2 prepends its partner's first base
+    ext_left: np.ndarray     # bool [n] tool 2 appends its partner's last base (if RD)
+    partner_raw: np.ndarray  # i64 [n] tool-2 extension partner, -1 = none
+    rd_in: np.ndarray        # bool [n] RD of an already converted input
+    sL: np.ndarray           # i64 [n] leading soft clip stripped
+    L: np.ndarray            # i64 [n] length after the strip
+    kfirst: np.ndarray       # i64 [n] first kept cigar op
+    kn: np.ndarray           # i64 [n] kept cigar ops
+    fam_split: np.ndarray    # bool [F] a record's tool-2 extension partner is outside its family
+
+    @property
+    def n_fam(self) -> int:
+        return int(self.fam_off.shape[0]) - 1
+
+    @property
+    def split_ext(self) -> bool:
+        return bool(self.fam_split.any())
+
+    def fam_bases(self) -> np.ndarray:
+        """Bases per family (the size measure shard.plan_batches balances)."""
+        if self.order.shape[0] == 0:
+            return np.zeros(self.n_fam, np.int64)
+        cs = np.concatenate([[0], np.cumsum(self.L[self.order] + 2)])
+        return cs[self.fam_off[1:]] - cs[self.fam_off[:-1]]
+
+
 def build_family_batch(raw: R.RawRecords, mode: str = "full", ref: Optional[R.Reference] = None,
                        small_cap: int = SMALL_ARENA_CAP, family_order: str = "template-coordinate") -> FamilyBatch:
     """mode: 'full' (raw step-5 input: tools 1+2 then the vote), 'convert' (tool 1 alone: one
     family per converted record), 'extend' (tool-1 output: tool 2 alone), 'vote' (tool-2 output).
     family_order ('full' / 'vote'): 'template-coordinate' -- the vote's families are the runs of one
     MI base in fgbio TemplateCoordinate order of the tool-2 records (SortBam, main.snake.py:152,
-    then the duplex caller's grouping), records in that order; 'mi-group' -- tool 2's MI groups."""
+    then the duplex caller's grouping), records in that order; 'mi-group' -- tool 2's MI groups.
+    The whole stream as one batch: materialize(plan_families(...))."""
+    plan = plan_families(raw, mode, ref, family_order)
+    return materialize(plan, 0, plan.n_fam, small_cap)
+
+
+def plan_families(raw: R.RawRecords, mode: str = "full", ref: Optional[R.Reference] = None,
+                  family_order: str = "template-coordinate") -> FamilyPlan:
+    """Family formation of build_family_batch (see there), without the device arrays."""
     if family_order not in ("template-coordinate", "mi-group"):
         raise ValueError(family_order)
     n = raw.n
@@ -487,17 +569,57 @@ def build_family_batch(raw: R.RawRecords, mode: str = "full", ref: Optional[R.Re
     nf = int(fam_sizes.shape[0])
     fam_off = np.zeros(nf + 1, np.int64)
     fam_off[1:] = np.cumsum(fam_sizes)
+    # extension partners must share the record's family for the fused launch; a partner in another
+    # family (a TemplateCoordinate run that splits a tool-2 4-group between the two pairs' reads)
+    # marks both families
+    fam_split = np.zeros(nf, bool)
+    if nr:
+        fam_of = np.repeat(np.arange(nf, dtype=np.int64), fam_sizes)
+        inv = np.full(n, -1, np.int64)
+        inv[order] = np.arange(nr, dtype=np.int64)
+        has_p = (ext_right | ext_left)[order]
+        pb = inv[np.where(has_p, partner_raw[order], 0)]
+        pfam = np.where(pb >= 0, fam_of[np.maximum(pb, 0)], -1)
+        pl = pb - fam_off[fam_of]
+        bad = has_p & ((pb < 0) | (pfam != fam_of) | (pl > 3))
+        fam_split[fam_of[bad]] = True
+    return FamilyPlan(raw=raw, mode=mode, ref=ref, order=order.astype(np.int64), fam_off=fam_off,
+                      fam_mi=np.asarray(fam_mi, np.int32), t2_rank=np.asarray(t2_rank, np.int64), conv=conv,
+                      ext_right=ext_right, ext_left=ext_left, partner_raw=partner_raw, rd_in=rd_in, sL=sL, L=L,
+                      kfirst=kfirst, kn=kn, fam_split=fam_split)
+
+
+def materialize(plan: FamilyPlan, f0: int, f1: int, small_cap: int = SMALL_ARENA_CAP) -> FamilyBatch:
+    """The device batch of plan families [f0, f1) (family ids renumbered from 0)."""
+    raw, mode, ref = plan.raw, plan.mode, plan.ref
+    n = raw.n
+    f = raw.flag.astype(np.int64)
+    conv, ext_right, ext_left, partner_raw, rd_in = plan.conv, plan.ext_right, plan.ext_left, plan.partner_raw, plan.rd_in
+    sL, L, kfirst, kn = plan.sL, plan.L, plan.kfirst, plan.kn
+    r0, r1 = int(plan.fam_off[f0]), int(plan.fam_off[f1])
+    order = plan.order[r0:r1]
+    fam_sizes = np.diff(plan.fam_off[f0:f1 + 1])
+    fam_mi = plan.fam_mi[f0:f1]
+    t2_rank = plan.t2_rank[r0:r1]
+    nr = int(order.shape[0])
+    nf = int(fam_sizes.shape[0])
+    fam_off = np.zeros(nf + 1, np.int64)
+    fam_off[1:] = np.cumsum(fam_sizes)
     fam_of = np.repeat(np.arange(nf, dtype=np.int64), fam_sizes)
     local = np.arange(nr, dtype=np.int64) - fam_off[fam_of]
-    # extension partners as family-local indices; a partner in another family (a TemplateCoordinate
-    # run that splits a tool-2 4-group between the two pairs' reads) makes the fused launch invalid
-    inv = np.full(n, -1, np.int64)
-    inv[order] = np.arange(nr, dtype=np.int64)
+    # extension partners as family-local indices (a partner outside the family -- plan.fam_split --
+    # makes the fused launch invalid; the caller then runs the tools and the vote apart)
     has_p = (ext_right | ext_left)[order]
-    pb = inv[np.where(has_p, partner_raw[order], 0)]
-    pl = np.where(has_p, pb - fam_off[fam_of], 0)
-    split_ext = bool((has_p & ((pb < 0) | (pl < 0) | (pl >= fam_sizes[fam_of]) | (pl > 3))).any()) if nr else False
-    pl = np.where(has_p & (pl >= 0) & (pl <= 3), pl, 0)
+    pl = np.zeros(nr, np.int64)
+    if has_p.any():
+        srt = np.argsort(order, kind="stable")
+        so = order[srt]
+        want = partner_raw[order[has_p]]
+        k = np.minimum(np.searchsorted(so, want), nr - 1)
+        found = so[k] == want
+        plh = np.where(found, srt[k], -1) - fam_off[fam_of[has_p]]
+        pl[has_p] = np.where(found & (plh >= 0) & (plh <= 3), plh, 0)
+    split_ext = bool(plan.fam_split[f0:f1].any())
 
     # ---- per batch record ----
     Lb = L[order]
@@ -605,30 +727,10 @@ def build_family_batch(raw: R.RawRecords, mode: str = "full", ref: Optional[R.Re
     has_mc = raw.mc_off[order] >= 0
     base_rt = usable & ((fo & 0xC) == 0) & (raw.next_tid[order] == raw.tid[order]) & has_mc
     if base_rt.any():
-        # MC cigars are stored contiguously in record order (records.py / synth.py invariant)
-        mcn = np.where(raw.mc_off >= 0, raw.mc_n, 0).astype(np.int64)
-        mrec = np.repeat(np.arange(raw.n, dtype=np.int64), mcn)
-        mo = raw.mc_cigar[:mrec.shape[0]]
-        mop = (mo & 0xF).astype(np.int64)
-        mln = (mo >> 4).astype(np.int64)
-        refm = np.isin(mop, R.REF_CONSUMING)
-        mref = np.bincount(mrec[refm], weights=mln[refm], minlength=raw.n)[:raw.n].astype(np.int64)
-        clip = np.isin(mop, (R.OP_S, R.OP_H))
-        ncum = np.cumsum(~clip)
-        mstart = np.zeros(raw.n, np.int64)
-        mstart[1:] = np.cumsum(mcn)[:-1]
-        base = np.where(mstart > 0, ncum[np.maximum(mstart - 1, 0)], 0) if ncum.shape[0] else np.zeros(raw.n, np.int64)
-        upto = ncum - base[mrec]                       # non-clip ops up to and including this one
-        before = upto - (~clip)
-        rtot = np.bincount(mrec[~clip], minlength=raw.n)[:raw.n]
-        after = rtot[mrec] - upto
-        lm = clip & (before == 0)
-        tm = clip & (after == 0)
-        lead = np.bincount(mrec[lm], weights=mln[lm], minlength=raw.n)[:raw.n].astype(np.int64)
-        trail = np.bincount(mrec[tm], weights=mln[tm], minlength=raw.n)[:raw.n].astype(np.int64)
+        lead, trail, mref = _mc_clips_reflen(raw, order)
         np_ = raw.next_pos[order].astype(np.int64)
-        mate_us = np_ - lead[order]
-        mate_ue = np_ + mref[order] - 1 + trail[order]
+        mate_us = np_ - lead
+        mate_ue = np_ + mref - 1 + trail
         pos = raw.pos[order].astype(np.int64)
         rl = np.where(complex_, reflen, Lb)
         neg = (fo & 16) != 0

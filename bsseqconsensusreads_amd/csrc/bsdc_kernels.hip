@@ -81,6 +81,13 @@ struct Tables {
     uint8_t qlo[2048];  // agreement case (S = 3 e^-D): Q at D = 2^16 k
     int32_t dthr[48];   // agreement case: smallest D with Q >= q (INT32_MAX: never)
 };
+// The device copy: the LDS image above plus the near-tie residuals, read from HBM on the rare
+// near-tie path only.  r40[q] = round(x 2^40) - lr[q] 2^20 (|r40| <= 2^19 + 1), x the same
+// log-likelihood ratio: a 2^-40 sum is D 2^20 + sum r40.
+struct DevTables {
+    Tables t;
+    int32_t r40[256];
+};
 
 __host__ __device__ inline int64_t round16(int64_t x) { return (x + 15) & ~int64_t(15); }
 __host__ __device__ inline int ref_chunks(int max_len) { return (15 + (max_len + 4) / 2 + 15) / 16; }
@@ -144,34 +151,55 @@ __device__ __forceinline__ int phred_of(float S, const float *thr) {
 // 32767 (fgbio stores Shorts).  D: likelihood sums (2^-20 nats), n: reads per base.
 struct SsAcc {
     long long D[4];
+    long long R[4];  // sums of DevTables::r40 (the near-tie refinement)
     uint32_t n[4];
     __device__ __forceinline__ void clear() {
 #pragma unroll
         for (int x = 0; x < 4; x++) {
             D[x] = 0;
+            R[x] = 0;
             n[x] = 0;
         }
     }
-    // one read's base (plain nt16 code, sequencing orientation) and its lr value
-    __device__ __forceinline__ void add(uint32_t code, int32_t v) {
+    // one read's base (plain nt16 code, sequencing orientation), its lr and r40 values
+    __device__ __forceinline__ void add(uint32_t code, int32_t v, int32_t r) {
 #pragma unroll
         for (int x = 0; x < 4; x++) {
             const bool hit = code == (1u << x);
             D[x] += hit ? v : 0;
+            R[x] += hit ? r : 0;
             n[x] += hit ? 1u : 0u;
         }
     }
 };
-__device__ __forceinline__ void ss_store(const SsAcc &a, const float *thr, uint8_t *b, uint8_t *q, uint16_t *dp,
-                                         uint16_t *er) {
+// Near tie: each read's 2^-20 term is rounded by up to half a unit, so a
+// gap between the best and the second sum of at most one unit per read of the set (nset) can hide
+// the true order.  Then the 2^-40 sums D 2^20 + R decide (first maximum).  Returns the best base.
+template <typename T>
+__device__ __forceinline__ int first_max4(T d0, T d1, T d2, T d3) {
     int best = 0;
-    long long Db = a.D[0];
-#pragma unroll
-    for (int x = 1; x < 4; x++)
-        if (a.D[x] > Db) {
-            best = x;
-            Db = a.D[x];
-        }
+    T m = d0;
+    if (d1 > m) { best = 1; m = d1; }
+    if (d2 > m) { best = 2; m = d2; }
+    if (d3 > m) { best = 3; }
+    return best;
+}
+template <typename T>
+__device__ __forceinline__ bool near_tie(T d0, T d1, T d2, T d3, int best, int nset) {
+    const T m = best == 0 ? d0 : best == 1 ? d1 : best == 2 ? d2 : d3;
+    T sec = best == 0 ? d1 : d0;
+    if (best != 1 && d1 > sec) sec = d1;
+    if (best != 2 && d2 > sec) sec = d2;
+    if (best != 3 && d3 > sec) sec = d3;
+    return nset > 1 && (long long)m - (long long)sec <= (long long)nset;
+}
+__device__ __forceinline__ void ss_store(const SsAcc &a, const float *thr, int nset, uint8_t *b, uint8_t *q,
+                                         uint16_t *dp, uint16_t *er) {
+    int best = first_max4(a.D[0], a.D[1], a.D[2], a.D[3]);
+    if (near_tie(a.D[0], a.D[1], a.D[2], a.D[3], best, nset))
+        best = first_max4((a.D[0] << 20) + a.R[0], (a.D[1] << 20) + a.R[1], (a.D[2] << 20) + a.R[2],
+                          (a.D[3] << 20) + a.R[3]);
+    const long long Db = a.D[best];
     float S = 0.0f;
 #pragma unroll
     for (int x = 0; x < 4; x++)
@@ -413,7 +441,7 @@ struct KParams {
     bsdc_family_batch B;
     bsdc_consensus O;
     const uint8_t *ref;  // packed nt16 genome
-    const Tables *tab;
+    const DevTables *tab;
     int32_t mode;
     int32_t overlap;
     int32_t ref_chunks;       // 16-B chunks per reference window (ref_chunks(max_len))
@@ -688,8 +716,9 @@ __global__ __launch_bounds__(kWave *kSmallMaxWaves, kSmallMinWaves) __attribute_
     const float *thr = T->thr;
     const uint8_t *qlo = T->qlo;
     const int32_t *dthr = T->dthr;
+    const int32_t *r40g = P.tab->r40;  // HBM: the near-tie path only
     if (((P.mode >> BSDC_MODE_STOP_SHIFT) & 15) == 15) return;  // profiling: launch cost alone
-    load_tables<kTabBytes>(P.tab, reinterpret_cast<uint8_t *>(&s_tab));
+    load_tables<kTabBytes>(&P.tab->t, reinterpret_cast<uint8_t *>(&s_tab));
     if (((P.mode >> BSDC_MODE_STOP_SHIFT) & 15) == 14) return;  // profiling: + the table copy
     const int w = threadIdx.x >> 6;
     const int t = threadIdx.x & 63;
@@ -1145,6 +1174,7 @@ __global__ __launch_bounds__(kWave *kSmallMaxWaves, kSmallMinWaves) __attribute_
         int nq = 0;
         for (int e = 0; e < 2; e++) {
             const int ol = olen[e];
+            const int sa = e == 0 ? 0 : 1, sb = e == 0 ? 3 : 2;
             for (int c0 = 0; c0 < ol; c0 += 256) {
                 const int c = c0 + 4 * t, c8 = 8 * c;
                 int32_t D[2][4] = {{0, 0, 0, 0}, {0, 0, 0, 0}};
@@ -1195,15 +1225,17 @@ __global__ __launch_bounds__(kWave *kSmallMaxWaves, kSmallMinWaves) __attribute_
                     const uint32_t x = bm[side];
                     multi[side] = x & ((x | 0x10101010u) - 0x01010101u);  // per byte: more than one base seen
                 }
-                const int sa = e == 0 ? 0 : 1, sb = e == 0 ? 3 : 2;
                 // per side and column: Q from the sum alone (valid when the column is not slow)
+                // (a sum of at most one unit per read of the set is a potential near tie with the
+                // unseen bases' 0: it takes the general path too)
                 uint32_t Qp[2] = {0, 0}, negm[2] = {0, 0};
 #pragma unroll
                 for (int side = 0; side < 2; side++) {
+                    const int32_t nset = side == 0 ? cnt[sa] : cnt[sb];
 #pragma unroll
                     for (int j = 0; j < 4; j++) {
                         const int32_t dsum = D[side][j];
-                        negm[side] |= dsum < 0 ? 0xFFu << (8 * j) : 0u;
+                        negm[side] |= dsum <= nset ? 0xFFu << (8 * j) : 0u;
                         const int32_t d = ::min(::max(dsum, 0), (int32_t)((1 << 27) - 1));
                         const uint32_t q0 = qlo[d >> 16];
                         Qp[side] |= (q0 + (d >= dthr[q0 + 1] ? 1u : 0u)) << (8 * j);
@@ -1273,11 +1305,25 @@ __global__ __launch_bounds__(kWave *kSmallMaxWaves, kSmallMinWaves) __attribute_
                     D2 += bb == kG ? v : 0;
                     D3 += bb == kT ? v : 0;
                 }
-                int best = 0;
-                int32_t Db = D0;
-                if (D1 > Db) { best = 1; Db = D1; }
-                if (D2 > Db) { best = 2; Db = D2; }
-                if (D3 > Db) { best = 3; Db = D3; }
+                int best = first_max4(D0, D1, D2, D3);
+                if (near_tie(D0, D1, D2, D3, best, ns)) {  // rare: the 2^-40 sums decide
+                    int32_t E0 = 0, E1 = 0, E2 = 0, E3 = 0;
+                    for (int i = 0; i < ns; i++) {
+                        const uint32_t d = dlist[os + i];
+                        if (c >= (int)((d >> 16) & 0x7FFF)) continue;
+                        const uint32_t idx = (d & 0x80000000u) ? (d & 0xFFFF) - c : (d & 0xFFFF) + c;
+                        const uint32_t braw = bimg[idx];
+                        const int32_t v = ((braw >> 4) & 1u) ? r40g[qimg[idx]] : 0;
+                        const uint32_t bb = (d & 0x80000000u) ? comp_nt16(braw) : (braw & 0x0F);
+                        E0 += bb == kA ? v : 0;
+                        E1 += bb == kC ? v : 0;
+                        E2 += bb == kG ? v : 0;
+                        E3 += bb == kT ? v : 0;
+                    }
+                    best = first_max4(((long long)D0 << 20) + E0, ((long long)D1 << 20) + E1,
+                                      ((long long)D2 << 20) + E2, ((long long)D3 << 20) + E3);
+                }
+                const int32_t Db = best == 0 ? D0 : best == 1 ? D1 : best == 2 ? D2 : D3;
                 float S = 0.0f;  // |D| < 2^30 here (<= 64 reads)
                 if (best != 0) S += term32(D0 - Db);
                 if (best != 1) S += term32(D1 - Db);
@@ -1339,9 +1385,9 @@ __global__ __launch_bounds__(kWave *kSmallMaxWaves, kSmallMinWaves) __attribute_
                     const uint32_t idx = (d & 0x80000000u) ? (d & 0xFFFF) - c : (d & 0xFFFF) + c;
                     const uint32_t braw = bimg[idx];
                     const uint32_t bb = (d & 0x80000000u) ? comp_nt16(braw) : (braw & 0x0F);
-                    acc.add(bb, lr2[256 + qimg[idx]]);  // only one-hot codes count
+                    acc.add(bb, lr2[256 + qimg[idx]], r40g[qimg[idx]]);  // only one-hot codes count
                 }
-                ss_store(acc, thr, P.O.ss_base + row + c, P.O.ss_qual + row + c, P.O.ss_depth + row + c,
+                ss_store(acc, thr, cnt[s], P.O.ss_base + row + c, P.O.ss_qual + row + c, P.O.ss_depth + row + c,
                          P.O.ss_err + row + c);
             }
             if (t == 0) P.O.ss_len[4 * fam + s] = (uint16_t)ls;
@@ -1898,12 +1944,23 @@ __device__ void process_large(const KParams &P, uint8_t *A, const int32_t *lr, c
     // the read's end cleared, lr[q] added to the base's sum.  Sets of <= 128 reads: 4 columns per
     // thread, int32 sums (exact: |lr| < 2^24).  Deeper sets: 2 columns per thread, int32 sums
     // flushed to int64 every 128 reads.
+    const int32_t *r40g = P.tab->r40;  // HBM: the near-tie path only
     auto resolve = [&](int s, int col, long long D0, long long D1, long long D2, long long D3) {
-        int best = 0;
-        long long Db = D0;
-        if (D1 > Db) { best = 1; Db = D1; }
-        if (D2 > Db) { best = 2; Db = D2; }
-        if (D3 > Db) { best = 3; Db = D3; }
+        int best = first_max4(D0, D1, D2, D3);
+        if (near_tie(D0, D1, D2, D3, best, cnt[s])) {  // rare: the 2^-40 sums decide
+            long long E[4] = {0, 0, 0, 0};
+            const uint2 *dl = desc + soff[s];
+            for (int i = 0; i < cnt[s]; i++) {
+                const uint2 e = dl[i];
+                if (col >= (int)(e.y & 0x7FFFFFFFu)) continue;
+                const bool rv = e.y >> 31;
+                const int32_t a = rv ? (int32_t)e.x - col : (int32_t)e.x + col;
+                const uint32_t braw = slots[a] & 0x0Fu, bb = rv ? comp_nt16(braw) : braw;
+                if (is_acgt(bb)) E[acgt_idx(bb)] += r40g[qimg[a]];
+            }
+            best = first_max4((D0 << 20) + E[0], (D1 << 20) + E[1], (D2 << 20) + E[2], (D3 << 20) + E[3]);
+        }
+        const long long Db = best == 0 ? D0 : best == 1 ? D1 : best == 2 ? D2 : D3;
         float S = 0.0f;
         if (best != 0) S += term(D0 - Db);
         if (best != 1) S += term(D1 - Db);
@@ -2074,10 +2131,10 @@ __device__ void process_large(const KParams &P, uint8_t *A, const int32_t *lr, c
                 const bool rv = e.y >> 31;
                 const int32_t a = rv ? (int32_t)e.x - c : (int32_t)e.x + c;
                 const uint32_t braw = slots[a] & 0x0Fu;
-                acc.add(rv ? comp_nt16(braw) : braw, lr[qimg[a]]);
+                acc.add(rv ? comp_nt16(braw) : braw, lr[qimg[a]], r40g[qimg[a]]);
             }
             const int64_t at = (4 * (int64_t)fam + s) * stride + c;
-            ss_store(acc, thr, P.O.ss_base + at, P.O.ss_qual + at, P.O.ss_depth + at, P.O.ss_err + at);
+            ss_store(acc, thr, cnt[s], P.O.ss_base + at, P.O.ss_qual + at, P.O.ss_depth + at, P.O.ss_err + at);
         }
         if (tt < 4) P.O.ss_len[4 * fam + tt] = (uint16_t)(hs[tt] ? lcv[tt] : 0);
     }
@@ -2107,7 +2164,7 @@ __global__ __launch_bounds__(kLargeThreads, 5) void k_large(KParams P, const uin
     __shared__ int s_cnt[4], s_lc[4], s_cur[4];
     const TablesL *T = &s_tab;
     if (((P.mode >> BSDC_MODE_STOP_SHIFT) & 15) == 15) return;  // profiling: launch cost alone
-    load_tables<kTabBytesL>(P.tab, reinterpret_cast<uint8_t *>(&s_tab));
+    load_tables<kTabBytesL>(&P.tab->t, reinterpret_cast<uint8_t *>(&s_tab));
     if (((P.mode >> BSDC_MODE_STOP_SHIFT) & 15) == 14) return;  // profiling: + the table copy
     const int32_t *lr = T->lr;
     const float *thr = T->thr;
@@ -2125,8 +2182,8 @@ __global__ __launch_bounds__(kLargeThreads, 5) void k_large(KParams P, const uin
 struct bsdc_ctx {
     int device;
     bsdc_params params;
-    Tables host_tab;
-    Tables *dev_tab = nullptr;
+    DevTables host_tab;
+    DevTables *dev_tab = nullptr;
     uint8_t *ref_seq = nullptr;
     int64_t ref_nibbles = 0;
     std::string err;
@@ -2218,6 +2275,18 @@ static void make_tables(double pre, double post, Tables &t) {
     }
 }
 
+// near-tie residuals: r40[q] = round(x 2^40) - lr[q] 2^20, x = ln(1 - a) - ln(a / 3) as in
+// make_tables (keep in step with oracle/bsdc_oracle.c orc_tables40)
+static void make_r40(double post, const Tables &t, int32_t *r40) {
+    const double e_post = pow(10.0, -post / 10.0);
+    for (int q = 0; q < 256; q++) {
+        const double e = pow(10.0, -(double)q / 10.0);
+        const double a = e_post + e - (4.0 / 3.0) * e_post * e;
+        const long long x40 = llround((log1p(-a) - log(a / 3.0)) * 1099511627776.0);
+        r40[q] = (int32_t)(x40 - ((long long)t.lr[q] << 20));
+    }
+}
+
 #define HIP_OK(ctx, call)                                                                     \
     do {                                                                                      \
         hipError_t e_ = (call);                                                               \
@@ -2255,6 +2324,14 @@ void bsdc_agree_tables(double pre, double post, uint8_t *qlo2048, int32_t *dthr4
     memcpy(dthr48, t.dthr, sizeof t.dthr);
 }
 
+void bsdc_model_tables40(double pre, double post, int64_t *lr40_256) {
+    Tables t;
+    make_tables(pre, post, t);
+    int32_t r40[256];
+    make_r40(post, t, r40);
+    for (int i = 0; i < 256; i++) lr40_256[i] = ((int64_t)t.lr[i] << 20) + r40[i];
+}
+
 void bsdc_phred_buckets(double pre, double post, uint8_t *sq144) {
     Tables t;
     make_tables(pre, post, t);
@@ -2270,9 +2347,10 @@ int32_t bsdc_ctx_create(int32_t device, const bsdc_params *params, bsdc_ctx **ou
     bsdc_ctx *c = new bsdc_ctx();
     c->device = device;
     c->params = *params;
-    make_tables(params->error_rate_pre_umi, params->error_rate_post_umi, c->host_tab);
-    if (hipSetDevice(device) != hipSuccess || hipMalloc(&c->dev_tab, sizeof(Tables)) != hipSuccess ||
-        hipMemcpy(c->dev_tab, &c->host_tab, sizeof(Tables), hipMemcpyHostToDevice) != hipSuccess) {
+    make_tables(params->error_rate_pre_umi, params->error_rate_post_umi, c->host_tab.t);
+    make_r40(params->error_rate_post_umi, c->host_tab.t, c->host_tab.r40);
+    if (hipSetDevice(device) != hipSuccess || hipMalloc(&c->dev_tab, sizeof(DevTables)) != hipSuccess ||
+        hipMemcpy(c->dev_tab, &c->host_tab, sizeof(DevTables), hipMemcpyHostToDevice) != hipSuccess) {
         delete c;
         return BSDC_EDEVICE;
     }
@@ -2292,8 +2370,8 @@ const char *bsdc_last_error(const bsdc_ctx *c) { return c ? c->err.c_str() : "nu
 
 int32_t bsdc_get_tables(const bsdc_ctx *c, int64_t *lr256, float *thr94) {
     if (!c) return BSDC_EINVAL;
-    for (int i = 0; i < 256; i++) lr256[i] = c->host_tab.lr[i];
-    for (int i = 0; i < 94; i++) thr94[i] = c->host_tab.thr[i];
+    for (int i = 0; i < 256; i++) lr256[i] = c->host_tab.t.lr[i];
+    for (int i = 0; i < 94; i++) thr94[i] = c->host_tab.t.thr[i];
     return 0;
 }
 

@@ -8,6 +8,12 @@
 * ``run_duplex`` -- callduplex alone on already converted + extended records.
 * ``run_molecular`` -- pipeline step 1, fgbio CallMolecularConsensusReads (main.snake.py:46-55):
   the same single-strand vote over raw MI groups, one consensus pair (R1, R2) per MI.
+
+A record stream of any size runs as a sequence of device batches: the host forms every family
+once (batch.plan_families), cuts the family list into contiguous ranges of about `batch_bases`
+bases (shard.plan_batches; never inside a family), and each range goes through one launch.  The
+concatenated output equals the one-batch output (tests/test_gpu_batches.py).  With several GPUs
+the ranges are dealt round-robin to ranks and gathered back in order (shard.deal / gather_in_order).
 """
 from __future__ import annotations
 
@@ -18,7 +24,8 @@ from typing import List, Optional
 import numpy as np
 
 from . import records as R
-from .batch import FamilyBatch, build_family_batch
+from . import shard
+from .batch import FamilyBatch, FamilyPlan, build_family_batch, materialize, plan_families
 from .device import Engine
 from ._lib import MODE_CONVERT, MODE_DUMP, MODE_EXTEND, MODE_TAGS, MODE_VOTE
 
@@ -225,33 +232,123 @@ def consensus_from_output(fb: FamilyBatch, out: dict) -> Consensus:
                      fb.src.astype(np.int64), ss)
 
 
-def run_step5(engine: Engine, raw: R.RawRecords, dump: bool = False, tags: bool = False):
-    """Rules convert_Bstrain .. callduplex (main.snake.py:121-164) -> (Consensus, tool-2 records or None).
-    tags: also the single-strand reads and column statistics of fgbio's consensus tags (Consensus.ss)."""
-    fb = build_family_batch(raw, "full", engine.ref)
-    if fb.split_ext:
-        # a TemplateCoordinate family lacks a record's tool-2 extension partner: run the tools as
-        # their own launch (tool-2 MI groups), then callduplex on their records
-        fb2 = build_family_batch(raw, "full", engine.ref, family_order="mi-group")
-        db = engine.upload(fb2, dump=True)
+# Device batch budget: bases (+2 per record, the tools' prepend / append room) per launch.  2^31
+# keeps a batch's slot offsets inside 32 bits (include/bsdc.h) with room for the 32-entry family
+# alignment; a C2 batch of that size is ~1.7M families, ~5 GB of HBM with its outputs.
+DEFAULT_BATCH_BASES = 1 << 31
+
+
+def plan_ranges(plan: FamilyPlan, batch_bases: Optional[int] = None):
+    """Contiguous family ranges [a, b) of about batch_bases bases each (shard.plan_batches)."""
+    return shard.plan_batches(plan.fam_bases(), DEFAULT_BATCH_BASES if batch_bases is None else batch_bases)
+
+
+def run_ranges(engine: Engine, plan: FamilyPlan, ranges, mode: int, tags: bool = False) -> List[Consensus]:
+    """Plan family ranges through the kernels, one launch each, output per range in range order.
+    The host builds range i + 1 while the kernels of range i run."""
+    parts: List[Consensus] = []
+    prev = None
+    for a, b in ranges:
+        fb = materialize(plan, a, b)
+        db = engine.upload(fb, tags=tags)
+        engine.run(db, mode | (MODE_TAGS if tags else 0))
+        if prev is not None:
+            parts.append(consensus_from_output(prev[0], prev[1].fetch()))
+        prev = (fb, db)
+    if prev is not None:
+        parts.append(consensus_from_output(prev[0], prev[1].fetch()))
+    return parts
+
+
+def concat_consensus(parts: List[Consensus]) -> Consensus:
+    """Consensus of consecutive family ranges -> one Consensus in range order (strides padded to
+    the widest)."""
+    if len(parts) == 1:
+        return parts[0]
+    if not parts:
+        z = np.zeros(0, np.int32)
+        return Consensus(z, np.zeros(0, np.uint8), np.zeros((0, 2), np.int32), np.zeros((0, 2, 16), np.uint8),
+                         np.zeros((0, 2, 16), np.uint8), np.zeros(1, np.int64), np.zeros(0, np.int64))
+    stride = max(int(p.seq.shape[2]) for p in parts)
+
+    def pad(a):
+        return np.pad(a, [(0, 0)] * (a.ndim - 1) + [(0, stride - a.shape[-1])])
+    offs = [0]
+    for p in parts:
+        offs.append(offs[-1] + int(p.fam_rec_off[-1]))
+    fro = np.concatenate([np.asarray(p.fam_rec_off[:-1], np.int64) + o for p, o in zip(parts, offs)] + [[offs[-1]]])
+    ss = None
+    if all(p.ss is not None for p in parts):
+        ss = {"len": np.concatenate([p.ss["len"] for p in parts])}
+        for k in ("base", "qual", "depth", "err"):
+            ss[k] = np.concatenate([pad(p.ss[k]) for p in parts])
+    return Consensus(np.concatenate([p.fam_mi for p in parts]), np.concatenate([p.status for p in parts]),
+                     np.concatenate([p.length for p in parts]), np.concatenate([pad(p.seq) for p in parts]),
+                     np.concatenate([pad(p.qual) for p in parts]), fro.astype(np.int64),
+                     np.concatenate([np.asarray(p.fam_src, np.int64) for p in parts]), ss)
+
+
+def _tools_batched(engine: Engine, raw: R.RawRecords, batch_bases: Optional[int]) -> OutRecords:
+    """Tools 1 + 2 over tool-2 MI groups, batch by batch, as tool-2 output records in order."""
+    plan = plan_families(raw, "full", engine.ref, family_order="mi-group")
+    parts = []
+    for a, b in plan_ranges(plan, batch_bases):
+        fb = materialize(plan, a, b)
+        db = engine.upload(fb, dump=True)
         engine.run(db, MODE_CONVERT | MODE_EXTEND | MODE_DUMP)
-        t2 = _records_from_dump(raw, fb2, db.fetch(), strip=True)
-        cons = run_duplex(engine, raw_from_records(raw, t2), tags)
+        parts.append(_records_from_dump(raw, fb, db.fetch(), strip=True))
+    return _cat_records(parts)
+
+
+def _cat_records(parts: List[OutRecords]) -> OutRecords:
+    if len(parts) == 1:
+        return parts[0]
+    if not parts:
+        e = np.zeros(0, np.int64)
+        return OutRecords(e, e.astype(np.int32), e.astype(np.int32), e, np.zeros(0, np.uint8), np.zeros(0, np.uint8),
+                          e.astype(np.int32), e, np.zeros(0, np.uint32), e.astype(np.int32), e.astype(np.int32))
+    so, co = [], []
+    bs, cs = 0, 0
+    for p in parts:
+        so.append(p.seq_off + bs)
+        co.append(p.cig_off + cs)
+        bs += int(p.seq.shape[0])
+        cs += int(p.cigar.shape[0])
+    cat = np.concatenate
+    return OutRecords(cat([p.src for p in parts]), cat([p.pos for p in parts]), cat([p.l_seq for p in parts]),
+                      cat(so), cat([p.seq for p in parts]), cat([p.qual for p in parts]),
+                      cat([p.n_cig for p in parts]), cat(co), cat([p.cigar for p in parts]),
+                      cat([p.rd for p in parts]), cat([p.la for p in parts]))
+
+
+def run_step5(engine: Engine, raw: R.RawRecords, dump: bool = False, tags: bool = False,
+              batch_bases: Optional[int] = None):
+    """Rules convert_Bstrain .. callduplex (main.snake.py:121-164) -> (Consensus, tool-2 records or None).
+    tags: also the single-strand reads and column statistics of fgbio's consensus tags (Consensus.ss).
+    batch_bases: device batch budget (DEFAULT_BATCH_BASES); dump (the tool-2 records, parity
+    tests) needs the stream in one batch."""
+    plan = plan_families(raw, "full", engine.ref)
+    if plan.split_ext:
+        # a TemplateCoordinate family lacks a record's tool-2 extension partner: run the tools as
+        # their own launches (tool-2 MI groups), then callduplex on their records
+        t2 = _tools_batched(engine, raw, batch_bases)
+        cons = run_duplex(engine, raw_from_records(raw, t2), tags, batch_bases)
         cons.fam_src = t2.src[cons.fam_src]  # raw2 record k is tool-2 record k
         return cons, (t2 if dump else None)
-    db = engine.upload(fb, dump=dump, tags=tags)
-    engine.run(db, MODE_CONVERT | MODE_EXTEND | MODE_VOTE | (MODE_DUMP if dump else 0) | (MODE_TAGS if tags else 0))
-    out = db.fetch()
-    t2 = _records_from_dump(raw, fb, out, strip=True) if dump else None
-    return consensus_from_output(fb, out), t2
+    mode = MODE_CONVERT | MODE_EXTEND | MODE_VOTE
+    if dump:
+        fb = materialize(plan, 0, plan.n_fam)
+        db = engine.upload(fb, dump=True, tags=tags)
+        engine.run(db, mode | MODE_DUMP | (MODE_TAGS if tags else 0))
+        out = db.fetch()
+        return consensus_from_output(fb, out), _records_from_dump(raw, fb, out, strip=True)
+    return concat_consensus(run_ranges(engine, plan, plan_ranges(plan, batch_bases), mode, tags)), None
 
 
-def run_duplex(engine: Engine, raw: R.RawRecords, tags: bool = False) -> Consensus:
+def run_duplex(engine: Engine, raw: R.RawRecords, tags: bool = False, batch_bases: Optional[int] = None) -> Consensus:
     """callduplex alone (main.snake.py:155-164) on converted + extended records."""
-    fb = build_family_batch(raw, "vote")
-    db = engine.upload(fb, tags=tags)
-    engine.run(db, MODE_VOTE | (MODE_TAGS if tags else 0))
-    return consensus_from_output(fb, db.fetch())
+    plan = plan_families(raw, "vote")
+    return concat_consensus(run_ranges(engine, plan, plan_ranges(plan, batch_bases), MODE_VOTE, tags))
 
 
 def molecular_records(raw: R.RawRecords) -> R.RawRecords:
@@ -280,7 +377,5 @@ def run_molecular(engine: Engine, raw: R.RawRecords, tags: bool = False):
     min-reads 1, overlapping bases on) -> (Consensus over the runs, the run records).  Consensus
     family f is MI run f; its R1 / R2 are the single-strand consensus of the run's R1s / R2s."""
     rm = molecular_records(raw)
-    fb = build_family_batch(rm, "vote", family_order="mi-group")
-    db = engine.upload(fb, tags=tags)
-    engine.run(db, MODE_VOTE | (MODE_TAGS if tags else 0))
-    return consensus_from_output(fb, db.fetch()), rm
+    plan = plan_families(rm, "vote", family_order="mi-group")
+    return concat_consensus(run_ranges(engine, plan, plan_ranges(plan), MODE_VOTE, tags)), rm

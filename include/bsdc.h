@@ -24,7 +24,7 @@
 extern "C" {
 #endif
 
-#define BSDC_ABI_VERSION 6
+#define BSDC_ABI_VERSION 7
 #define BSDC_SMALL_BUCKETS 8
 #define BSDC_LARGE_BUCKETS 6
 #define BSDC_LARGE_LDS_MAX 158912 /* LDS arena bytes one large-family workgroup may use */ /* LDS arena size classes of the wavefront-per-family kernel */
@@ -159,6 +159,8 @@ int64_t bsdc_small_arena_bytes(int32_t n_rec, int64_t img, int32_t n_conv, int64
 int32_t bsdc_get_tables(const bsdc_ctx *ctx, int64_t *lr256, float *thresh94);
 /* Same tables for given error rates, without a context (no GPU needed). */
 void bsdc_model_tables(double error_rate_pre_umi, double error_rate_post_umi, int64_t *lr256, float *thresh94);
+/* The near-tie tables: the same log-likelihood ratios in 2^-40 nats. */
+void bsdc_model_tables40(double error_rate_pre_umi, double error_rate_post_umi, int64_t *lr40_256);
 /* The vote's agreement-case tables: Q(D) = qlo[D >> 16] + (D >= dthr[qlo[D >> 16] + 1]). */
 void bsdc_agree_tables(double error_rate_pre_umi, double error_rate_post_umi, uint8_t *qlo2048, int32_t *dthr48);
 /* The general case's phred buckets: Q(S) = the largest k >= sq[j] with S <= thresh[k], j = the

@@ -309,6 +309,17 @@ void orc_tables(double pre, double post, int64_t *lr, float *thr) {
     }
 }
 
+/* the same log-likelihood ratios in 2^-40 nats (the near-tie decision of ss_consensus) */
+void orc_tables40(double pre, double post, int64_t *lr40) {
+    (void)pre;
+    const double e_post = pow(10.0, -post / 10.0);
+    for (int q = 0; q < 256; q++) {
+        const double e = pow(10.0, -(double)q / 10.0);
+        const double a = e_post + e - (4.0 / 3.0) * e_post * e;
+        lr40[q] = llround((log1p(-a) - log(a / 3.0)) * 1099511627776.0);
+    }
+}
+
 float orc_det_expf(float x) {
     /* exp for x in [-80, 0]: Cody-Waite reduction, degree-6 Taylor, explicit fma everywhere */
     const float t = x * 1.44269504088896341f;
@@ -588,7 +599,7 @@ typedef struct {
  * per-column depth and errors fgbio keeps for its consensus tags:
  *   errors = if (rawBase == NoCall) depth else depth - builder.observations(rawBase)
  * where rawBase is the likelihood call before the minimum-quality mask (PARITY UNPINNED). */
-static int ss_consensus(srcread **v, int n, const int64_t *lr, const float *thr, ssread *out) {
+static int ss_consensus(srcread **v, int n, const int64_t *lr, const int64_t *lr40, const float *thr, ssread *out) {
     int32_t lc = 0;
     for (int i = 0; i < n; i++)
         if (v[i]->len > lc) lc = v[i]->len;
@@ -611,6 +622,24 @@ static int ss_consensus(srcread **v, int n, const int64_t *lr, const float *thr,
         int best = 0;
         for (int b = 1; b < 4; b++)
             if (D[b] > D[best]) best = b;
+        /* near tie: the 2^-20 sums carry up to half a unit of rounding per read, so a gap of at most
+         * one unit per read of the set can hide the true order -- decide it on the 2^-40 sums
+         * (fgbio sums in double precision; 2^-40 resolves every gap that is not an exact tie of the
+         * same qualities) */
+        int64_t second = INT64_MIN;
+        for (int b = 0; b < 4; b++)
+            if (b != best && D[b] > second) second = D[b];
+        if (n > 1 && D[best] - second <= n) {
+            int64_t E[4] = {0, 0, 0, 0};
+            for (int i = 0; i < n; i++) {
+                if (v[i]->len <= c) continue;
+                int bi = base_index(v[i]->b[c]);
+                if (bi >= 0) E[bi] += lr40[v[i]->q[c]];
+            }
+            best = 0;
+            for (int b = 1; b < 4; b++)
+                if (E[b] > E[best]) best = b;
+        }
         float S = 0.0f;
         for (int b = 0; b < 4; b++) {
             if (b == best) continue;
@@ -694,10 +723,15 @@ struct orc_result {
     ssread *fam_ss;       /* [4*f + set] single-strand reads (len 0 = set empty) */
     int64_t *fam_rec_off; /* [nfam + 1] into fam_src */
     int64_t *fam_src;     /* input record index of each family record, family order */
+    /* keep_sources: per family the vote's source reads, set by set */
+    int32_t *src_count;   /* [4*f + set] */
+    int32_t **src_len;    /* [f] -> lengths of the family's source reads */
+    char **src_b;         /* [f] -> their bases, concatenated */
+    uint8_t **src_q;
 };
 
 static void family_call(orec *recs, int n, const orc_records *in, const orc_params *p, const int64_t *lr,
-                        const float *thr, struct orc_result *res, int64_t f) {
+                        const int64_t *lr40, const float *thr, struct orc_result *res, int64_t f) {
     res->fam_status[f] = 0;
     res->fam_len[2 * f] = res->fam_len[2 * f + 1] = 0;
     res->fam_b[2 * f] = res->fam_b[2 * f + 1] = NULL;
@@ -766,9 +800,29 @@ static void family_call(orec *recs, int n, const orc_records *in, const orc_para
             int s = Y[i]->strand == 0 ? 1 : 2;
             sets[s][ns[s]++] = Y[i];
         }
+    if (p->keep_sources) {
+        int64_t nr = 0, nb = 0;
+        for (int s = 0; s < 4; s++) {
+            res->src_count[4 * f + s] = ns[s];
+            nr += ns[s];
+            for (int i = 0; i < ns[s]; i++) nb += sets[s][i]->len;
+        }
+        res->src_len[f] = (int32_t *)malloc(sizeof(int32_t) * (size_t)(nr + 1));
+        res->src_b[f] = (char *)malloc((size_t)nb + 1);
+        res->src_q[f] = (uint8_t *)malloc((size_t)nb + 1);
+        int64_t ri = 0, bi = 0;
+        for (int s = 0; s < 4; s++)
+            for (int i = 0; i < ns[s]; i++) {
+                const srcread *x = sets[s][i];
+                res->src_len[f][ri++] = x->len;
+                memcpy(res->src_b[f] + bi, x->b, (size_t)x->len);
+                memcpy(res->src_q[f] + bi, x->q, (size_t)x->len);
+                bi += x->len;
+            }
+    }
     ssread ss[4];
     int has[4];
-    for (int s = 0; s < 4; s++) has[s] = ss_consensus(sets[s], ns[s], lr, thr, &ss[s]);
+    for (int s = 0; s < 4; s++) has[s] = ss_consensus(sets[s], ns[s], lr, lr40, thr, &ss[s]);
     int32_t nreads = 0;
     for (int s = 0; s < 4; s++) nreads += ns[s];
     res->fam_nreads[f] = nreads;
@@ -1028,9 +1082,10 @@ orc_result *orc_run(const orc_records *in, const orc_reference *ref, const orc_p
     free(rec_group);
     free(gfirst);
     /* ---- vote, per family ---- */
-    int64_t lr[256];
+    int64_t lr[256], lr40[256];
     float thr[94];
     orc_tables(p->error_rate_pre_umi, p->error_rate_post_umi, lr, thr);
+    orc_tables40(p->error_rate_pre_umi, p->error_rate_post_umi, lr40);
     res->nfam = ng;
     res->fam_rec_off = (int64_t *)malloc(sizeof(int64_t) * (size_t)(ng + 1));
     res->fam_src = (int64_t *)malloc(sizeof(int64_t) * (size_t)(res->t2.n + 1));
@@ -1048,9 +1103,15 @@ orc_result *orc_run(const orc_records *in, const orc_reference *ref, const orc_p
     res->fam_q = (uint8_t **)calloc((size_t)(2 * ng + 2), sizeof(uint8_t *));
     res->fam_ss = (ssread *)calloc((size_t)(4 * ng + 4), sizeof(ssread));
     for (int64_t g = 0; g < ng; g++) res->fam_mi[g] = gorder_mi[g];
+    if (p->keep_sources) {
+        res->src_count = (int32_t *)calloc((size_t)(4 * ng + 4), sizeof(int32_t));
+        res->src_len = (int32_t **)calloc((size_t)(ng + 1), sizeof(int32_t *));
+        res->src_b = (char **)calloc((size_t)(ng + 1), sizeof(char *));
+        res->src_q = (uint8_t **)calloc((size_t)(ng + 1), sizeof(uint8_t *));
+    }
 #pragma omp parallel for schedule(dynamic, 64)
     for (int64_t g = 0; g < ng; g++)
-        family_call(frecs + fam_off[g], (int)(fam_off[g + 1] - fam_off[g]), in, p, lr, thr, res, g);
+        family_call(frecs + fam_off[g], (int)(fam_off[g + 1] - fam_off[g]), in, p, lr, lr40, thr, res, g);
     free(frecs);
     free(gorder_mi);
     free(fam_off);
@@ -1076,6 +1137,15 @@ void orc_free(orc_result *r) {
         free(r->fam_ss[i].err);
     }
     free(r->fam_ss);
+    for (int64_t i = 0; r->src_len && i < r->nfam; i++) {
+        free(r->src_len[i]);
+        free(r->src_b[i]);
+        free(r->src_q[i]);
+    }
+    free(r->src_count);
+    free(r->src_len);
+    free(r->src_b);
+    free(r->src_q);
     free(r->fam_b);
     free(r->fam_q);
     free(r->fam_mi);
@@ -1163,6 +1233,36 @@ void orc_get_ss(const orc_result *r, int32_t stride, int32_t *len, uint8_t *base
             memcpy(depth + o, x->depth, sizeof(int32_t) * (size_t)x->len);
             memcpy(err + o, x->err, sizeof(int32_t) * (size_t)x->len);
         }
+    }
+}
+
+void orc_sources_size(const orc_result *r, int64_t *n_reads, int64_t *n_bases) {
+    int64_t nr = 0, nb = 0;
+    for (int64_t f = 0; r->src_count && f < r->nfam; f++) {
+        int32_t c = r->src_count[4 * f] + r->src_count[4 * f + 1] + r->src_count[4 * f + 2] + r->src_count[4 * f + 3];
+        for (int32_t i = 0; i < c; i++) nb += r->src_len[f][i];
+        nr += c;
+    }
+    *n_reads = nr;
+    *n_bases = nb;
+}
+
+void orc_get_sources(const orc_result *r, int32_t *set_count, int32_t *len, uint8_t *bases, uint8_t *quals) {
+    int64_t ri = 0, bi = 0;
+    for (int64_t f = 0; r->src_count && f < r->nfam; f++) {
+        int32_t c = 0;
+        for (int s = 0; s < 4; s++) {
+            set_count[4 * f + s] = r->src_count[4 * f + s];
+            c += r->src_count[4 * f + s];
+        }
+        int64_t fb = 0;
+        for (int32_t i = 0; i < c; i++) {
+            len[ri++] = r->src_len[f][i];
+            fb += r->src_len[f][i];
+        }
+        memcpy(bases + bi, r->src_b[f], (size_t)fb);
+        memcpy(quals + bi, r->src_q[f], (size_t)fb);
+        bi += fb;
     }
 }
 

@@ -66,6 +66,7 @@ typedef struct {
     int32_t n_threads;           /* OpenMP threads, <= 0 = default */
     int32_t family_order;        /* 1: families = runs of one MI base in fgbio TemplateCoordinate order of the
                                     tool-2 records (SortBam at main.snake.py:152); 0: tool-2 MI groups */
+    int32_t keep_sources;        /* 1: keep every family's source reads per set (orc_get_sources) */
 } orc_params;
 
 typedef struct orc_result orc_result;
@@ -99,8 +100,16 @@ void orc_get_consensus(const orc_result *r, int32_t stride, int32_t *mi_id, int3
 void orc_get_ss(const orc_result *r, int32_t stride, int32_t *len, uint8_t *bases, uint8_t *quals, int32_t *depth,
                 int32_t *err);
 
+/* The source reads the vote saw (keep_sources = 1): per family and set (row 4*f + s) the count of
+ * reads, then every read in set order -- its length, its bases (ASCII, sequencing orientation, after
+ * the overlapping-bases consensus, read-through and trailing-N trims) and quals.  For restating the
+ * vote independently (tests/fgbio_vote.py). */
+void orc_sources_size(const orc_result *r, int64_t *n_reads, int64_t *n_bases);
+void orc_get_sources(const orc_result *r, int32_t *set_count, int32_t *len, uint8_t *bases, uint8_t *quals);
+
 /* Tables of the likelihood model, for a cross-check against libbsdc's own. */
 void orc_tables(double pre, double post, int64_t *lr_fixed256, float *phred_thresh94);
+void orc_tables40(double pre, double post, int64_t *lr40_fixed256);
 float orc_det_expf(float x);
 int64_t orc_check_agree(const uint8_t *qlo, const int32_t *dthr, const float *thr, int64_t dmax);
 

@@ -40,7 +40,8 @@ class _Reference(C.Structure):
 class _Params(C.Structure):
     _fields_ = [("error_rate_pre_umi", C.c_double), ("error_rate_post_umi", C.c_double),
                 ("min_input_base_quality", C.c_int32), ("consensus_call_overlapping_bases", C.c_int32),
-                ("run_tools", C.c_int32), ("n_threads", C.c_int32), ("family_order", C.c_int32)]
+                ("run_tools", C.c_int32), ("n_threads", C.c_int32), ("family_order", C.c_int32),
+                ("keep_sources", C.c_int32)]
 
 
 _lib = None
@@ -72,8 +73,11 @@ def load():
         lib.orc_get_consensus.argtypes = [C.c_void_p, C.c_int32] + [C.c_void_p] * 6
         lib.orc_get_ss.argtypes = [C.c_void_p, C.c_int32] + [C.c_void_p] * 5
         lib.orc_tables.argtypes = [C.c_double, C.c_double, C.c_void_p, C.c_void_p]
+        lib.orc_tables40.argtypes = [C.c_double, C.c_double, C.c_void_p]
         lib.orc_det_expf.restype = C.c_float
         lib.orc_det_expf.argtypes = [C.c_float]
+        lib.orc_sources_size.argtypes = [C.c_void_p, C.c_void_p, C.c_void_p]
+        lib.orc_get_sources.argtypes = [C.c_void_p] + [C.c_void_p] * 4
         lib.orc_check_agree.restype = C.c_int64
         lib.orc_check_agree.argtypes = [C.c_void_p, C.c_void_p, C.c_void_p, C.c_int64]
         _lib = lib
@@ -121,6 +125,9 @@ class OracleResult:
     # single-strand reads per family and set (0 AB-R1, 1 AB-R2, 2 BA-R1, 3 BA-R2) with the
     # consensus-tag column statistics: "len" [F, 4], "base" (nt16) / "qual" / "depth" / "err" [F, 4, stride]
     ss: dict = None
+    # keep_sources=True: the source reads each set's vote saw -- "count" [F, 4] reads per (family,
+    # set), then per read in family / set order "len", and flat "base" (nt16) / "qual" arrays
+    sources: dict = None
 
 
 def _ptr(a):
@@ -150,7 +157,7 @@ def lex_ranks(strings, ids) -> np.ndarray:
 
 
 def run(raw, ref, pre=45.0, post=30.0, overlap=True, run_tools=True, threads=0,
-        family_order="template-coordinate") -> OracleResult:
+        family_order="template-coordinate", keep_sources=False) -> OracleResult:
     """raw: bsseqconsensusreads_amd.records.RawRecords; ref: records.Reference.
     family_order: "template-coordinate" (fgbio SortBam + consecutive-MI grouping) or "mi-group"
     (tool 2's first-seen MI groups)."""
@@ -219,7 +226,8 @@ def run(raw, ref, pre=45.0, post=30.0, overlap=True, run_tools=True, threads=0,
 
     if family_order not in ("template-coordinate", "mi-group"):
         raise ValueError(family_order)
-    p = _Params(pre, post, 0, int(overlap), int(run_tools), int(threads), int(family_order == "template-coordinate"))
+    p = _Params(pre, post, 0, int(overlap), int(run_tools), int(threads), int(family_order == "template-coordinate"),
+                int(keep_sources))
     t0 = time.perf_counter()
     h = lib.orc_run(C.byref(rr), C.byref(rf), C.byref(p))
     seconds = time.perf_counter() - t0
@@ -268,13 +276,25 @@ def run(raw, ref, pre=45.0, post=30.0, overlap=True, run_tools=True, threads=0,
         sd = np.zeros(max(4 * F * stride, 1), np.int32)
         se = np.zeros(max(4 * F * stride, 1), np.int32)
         lib.orc_get_ss(h, stride, _ptr(sl), _ptr(sb), _ptr(sq), _ptr(sd), _ptr(se))
+        sources = None
+        if keep_sources:
+            nrd, nbs = C.c_int64(0), C.c_int64(0)
+            lib.orc_sources_size(h, C.byref(nrd), C.byref(nbs))
+            cnt = np.zeros(max(4 * F, 1), np.int32)
+            sln = np.zeros(max(nrd.value, 1), np.int32)
+            sbs = np.zeros(max(nbs.value, 1), np.uint8)
+            sqs = np.zeros(max(nbs.value, 1), np.uint8)
+            lib.orc_get_sources(h, _ptr(cnt), _ptr(sln), _ptr(sbs), _ptr(sqs))
+            sources = {"count": cnt[:4 * F].reshape(F, 4), "len": sln[:nrd.value],
+                       "base": _ASCII_NT16[sbs[:nbs.value]], "qual": sqs[:nbs.value]}
         n4 = 4 * F * stride
         ss = {"len": sl[:4 * F].reshape(F, 4), "base": _ASCII_NT16[sb[:n4]].reshape(F, 4, stride),
               "qual": sq[:n4].reshape(F, 4, stride), "depth": sd[:n4].reshape(F, 4, stride),
               "err": se[:n4].reshape(F, 4, stride)}
         return OracleResult(outs[0], outs[1], mi[:F], st[:F], ln[:2 * F].reshape(F, 2),
                             _ASCII_NT16[bs[:2 * F * stride]].reshape(F, 2, stride) if F else np.zeros((0, 2, stride), np.uint8),
-                            qs[:2 * F * stride].reshape(F, 2, stride), nr[:F], seconds, fro, fsrc[:int(fro[-1])], ss)
+                            qs[:2 * F * stride].reshape(F, 2, stride), nr[:F], seconds, fro, fsrc[:int(fro[-1])], ss,
+                            sources)
     finally:
         lib.orc_free(h)
 
@@ -285,6 +305,12 @@ def tables(pre=45.0, post=30.0):
     thr = np.zeros(94, np.float32)
     lib.orc_tables(pre, post, _ptr(lr), _ptr(thr))
     return lr, thr
+
+
+def tables40(pre=45.0, post=30.0):
+    lr40 = np.zeros(256, np.int64)
+    load().orc_tables40(pre, post, _ptr(lr40))
+    return lr40
 
 
 def det_expf(x: float) -> float:

@@ -1,0 +1,69 @@
+"""The HIP vote against the independent fp64 restatement of fgbio (tests/fgbio_vote.py), through
+the C-ABI: single-strand reads (BSDC_MODE_TAGS) and duplex consensus on C0-C4 and on adversarial
+near-tie columns, in both kernels (k_small, and k_large with every family forced into it).
+
+Bar (north_star): consensus bases bit-exact and quals within +-1 of fgbio's double-precision
+log-space arithmetic.  Exact ties (the same multiset of qualities on two bases) are reported
+separately: fgbio's pick there is the rounding of its own summation order; the kernel must pick one
+of the tied bases.  Counts are printed (run with -s) and asserted.
+"""
+import numpy as np
+import pytest
+
+import fgbio_vote as fv
+from bsseqconsensusreads_amd import batch, pipeline, synth
+from helpers import near_tie_votes
+from oracle import oracle
+from test_fgbio_vote import CASES, assert_fp64_bar
+from test_gpu_parity import assert_consensus_equal, assert_ss_equal
+
+pytestmark = pytest.mark.gpu
+
+
+def _gpu_vs_fp64(engine, raw, ref, run_tools, what):
+    engine.load_reference(ref)
+    if run_tools:
+        cons, _ = pipeline.run_step5(engine, raw, tags=True)
+    else:
+        cons = pipeline.run_duplex(engine, raw, tags=True)
+    r = oracle.run(raw, ref, keep_sources=True, run_tools=run_tools)
+    assert_consensus_equal(cons, r, what)      # GPU == fixed-point restatement, bit for bit
+    assert_ss_equal(cons, r, what)
+    src = r.sources
+    stride = cons.ss["base"].shape[2]
+    ss = fv.ss_vote(src["count"], src["len"], src["base"], src["qual"], stride)
+    c = fv.compare_ss({"len": cons.ss["len"], "base": cons.ss["base"], "qual": cons.ss["qual"]}, ss)
+    assert_fp64_bar(c, what)
+    # duplex consensus vs fgbio fp64 duplex of the fp64 single-strand reads
+    st, ln, b, q = fv.duplex(ss)
+    assert np.array_equal(st, (cons.status & 1).astype(np.int32)) and np.array_equal(ln, cons.length)
+    w = min(b.shape[2], cons.seq.shape[2])
+    live = np.arange(w)[None, None, :] < ln[:, :, None]
+    db = live & (cons.seq[:, :, :w] != b[:, :, :w])
+    dq = np.abs(cons.qual[:, :, :w].astype(np.int64) - q[:, :, :w].astype(np.int64))
+    print(what, "duplex columns %d, base diffs %d, qual +-1 %d, qual >1 %d" % (
+        int(live.sum()), int(db.sum()), int((live & (dq == 1)).sum()), int((live & (dq > 1)).sum())))
+    # every duplex difference traces back to an exact single-strand tie
+    tie = (ss["gap"] < 1e-9) & (np.bitwise_count(ss["tied"].astype(np.uint64)) > 1)
+    tie_e = np.zeros(b.shape, bool)
+    for e, (sa, sb) in enumerate(((0, 3), (1, 2))):
+        tie_e[:, e, :w] = tie[:, sa, :w] | tie[:, sb, :w]
+    assert not (db & ~tie_e[:, :, :w]).any(), what + ": duplex base differs outside exact ties"
+    assert not (live & (dq > 0) & ~tie_e[:, :, :w]).any(), what + ": duplex qual differs outside exact ties"
+
+
+@pytest.mark.parametrize("cfg,n,qlo", CASES)
+def test_gpu_vote_vs_fgbio_fp64(engine, cfg, n, qlo):
+    s = synth.generate(cfg, n, seed=11, device="cpu", genome_len=400_000)
+    raw = s.raw if qlo is None else near_tie_votes(s.raw, qlo=qlo, seed=5)
+    _gpu_vs_fp64(engine, raw, s.ref, qlo is None, "%s n=%d q>=%s" % (cfg, n, qlo))
+
+
+@pytest.mark.parametrize("qlo", [84, 88])
+def test_gpu_large_kernel_near_ties_vs_fgbio_fp64(engine, qlo, monkeypatch):
+    """Every family through k_large (its near-tie path in `resolve` and the tag pass)."""
+    s = synth.generate("C1", 800, seed=13, device="cpu", genome_len=200_000)
+    raw = near_tie_votes(s.raw, qlo=qlo, seed=7)
+    real = batch.materialize
+    monkeypatch.setattr(pipeline, "materialize", lambda plan, f0, f1, small_cap=0: real(plan, f0, f1, small_cap=0))
+    _gpu_vs_fp64(engine, raw, s.ref, False, "k_large q>=%d" % qlo)

@@ -1,25 +1,29 @@
-"""Parity at BASELINE.json's full size: the bench workload itself (C2, configs[1]: 1M duplex
-families, 2x150 bp, Poisson(4) templates, seed 42 -- the batch `bench.py` times), every family
-against oracle/ bit-exact, plus size-independent properties of the resident-batch step:
+"""Parity at BASELINE.json's full sizes, every family against oracle/ bit-exact:
 
-- idempotence: a second step over the same resident batch writes the same bytes (the kernels
-  read only their inputs; `bench.py` times K such steps);
-- output invariants on every family: bases are A/C/G/T/N codes, quals in [1, 93], every
-  emitted end has a non-zero length no longer than the batch's longest record + 1.
-
-C3 (configs[2], 200K deep families) and C4 (configs[3], skewed) run at a 20K-family sample of
-their full-size model: the oracle restatement needs minutes for the whole C3 batch.
+- C2 (configs[1]): 1M duplex families, 2x150 bp, Poisson(4) templates, seed 42 -- the batch
+  `bench.py` times -- plus size-independent properties of the resident-batch step: idempotence (a
+  second step over the same resident batch writes the same bytes) and output invariants (bases
+  A/C/G/T/N, quals in [1, 93], lengths bounded by the longest record + 1);
+- C3 (configs[2]): all 200K deep families (20-100 templates), same checks;
+- C4 (configs[3]): a 20K-family sample of the skewed model;
+- C5 (configs[4], per-GPU shape): a C2-shaped stream larger than one batch's 32-bit slot range,
+  cut into bounded batches that run back to back on one GPU and are gathered in order -- what each
+  rank of a 2/4/8-GPU run does with its share of the 100M families.
 """
 import numpy as np
 import pytest
 import torch
 
-from bsseqconsensusreads_amd import batch, synth
+import os
+
+from bsseqconsensusreads_amd import batch, pipeline, synth
 from bsseqconsensusreads_amd._lib import MODE_CONVERT, MODE_EXTEND, MODE_VOTE
 from bsseqconsensusreads_amd.pipeline import consensus_from_output
 from oracle import oracle
 
 pytestmark = pytest.mark.gpu
+# the box's CPU share (OMP_NUM_THREADS = 16 there); os.cpu_count() shows the whole machine
+THREADS = int(os.environ.get("OMP_NUM_THREADS", "0") or 0) or min(os.cpu_count() or 1, 16)
 FULL = MODE_CONVERT | MODE_EXTEND | MODE_VOTE
 ACGTN = np.array([1, 2, 4, 8, 15])
 
@@ -62,28 +66,66 @@ def test_bench_workload_c2_full_size(engine):
     for k in ("status", "len", "seq", "qual"):
         assert np.array_equal(a[k], b[k]), "second step over the resident batch differs in " + k
     cons = consensus_from_output(fb, a)
-    ref = oracle.run(s.raw, s.ref, threads=16)
+    ref = oracle.run(s.raw, s.ref, threads=THREADS)
     live = _compare_all(cons, ref, "C2 1M")
+    # (a duplex disagreement keeps |qa - qb|, which can be 1: fgbio duplexConsensus)
+    _invariants(cons, live, int((fb.rec_lenflag & 0xFFFF).max()))
+    assert ((cons.status & 1) != 0).sum() > 0.8 * fb.n_fam
+
+
+def _invariants(cons, live, fb_max_len):
     w = live.shape[2]
     seq, qual = cons.seq[:, :, :w], cons.qual[:, :, :w]
     assert np.isin(seq[live], ACGTN).all()
-    q = qual[live]  # a duplex disagreement keeps |qa - qb|, which can be 1 (fgbio duplexConsensus)
+    q = qual[live]
     assert q.min() >= 1 and q.max() <= 93
     emitted = (cons.status & 1) != 0
     assert (cons.length[emitted] > 0).all()
-    assert cons.length.max() <= int((fb.rec_lenflag & 0xFFFF).max()) + 1
-    assert emitted.sum() > 0.8 * fb.n_fam
+    assert cons.length.max() <= fb_max_len + 1
 
 
-@pytest.mark.parametrize("cfg", ["C3", "C4"])
-def test_deep_and_skewed_configs_sample(engine, cfg):
-    s = synth.generate(cfg, 20_000, seed=42, device="cuda")
+@pytest.mark.timeout(900)
+def test_c3_full_size_every_family(engine):
+    s = synth.generate("C3", 200_000, seed=42, device="cuda")  # bench.py --config C3
+    fb = batch.build_family_batch(s.raw, "full", s.ref)
+    assert fb.n_fam >= 200_000 and not fb.split_ext and fb.large_fams.shape[0] > 100_000
+    engine.load_reference(s.ref)
+    a, b = _run_resident(engine, fb)
+    for k in ("status", "len", "seq", "qual"):
+        assert np.array_equal(a[k], b[k]), "C3: second step differs in " + k
+    cons = consensus_from_output(fb, a)
+    del fb, a, b
+    ref = oracle.run(s.raw, s.ref, threads=THREADS)
+    live = _compare_all(cons, ref, "C3 200K")
+    _invariants(cons, live, int(s.raw.l_seq.max()) + 1)
+
+
+def test_c4_skewed_sample(engine):
+    s = synth.generate("C4", 20_000, seed=42, device="cuda")
     fb = batch.build_family_batch(s.raw, "full", s.ref)
     engine.load_reference(s.ref)
     a, b = _run_resident(engine, fb)
     for k in ("status", "len", "seq", "qual"):
-        assert np.array_equal(a[k], b[k]), "%s: second step differs in %s" % (cfg, k)
+        assert np.array_equal(a[k], b[k]), "C4: second step differs in " + k
     if fb.split_ext:
         pytest.skip("split extension partner: covered by test_split_extension_partner_falls_back")
-    ref = oracle.run(s.raw, s.ref, threads=16)
-    _compare_all(consensus_from_output(fb, a), ref, cfg + " 20K")
+    ref = oracle.run(s.raw, s.ref, threads=THREADS)
+    _compare_all(consensus_from_output(fb, a), ref, "C4 20K")
+
+
+@pytest.mark.timeout(900)
+def test_c5_stream_beyond_one_batch(engine):
+    """One GPU's share of C5: 3.7M C2-shaped families, more slots than 32-bit batch offsets hold,
+    as >= 3 bounded batches run back to back (pipeline.run_step5 -> plan_families / plan_ranges
+    / run_ranges / concat_consensus), gathered in order, every family bit-exact."""
+    s = synth.generate("C2", 3_700_000, seed=5, device="cuda")
+    engine.load_reference(s.ref)
+    plan = batch.plan_families(s.raw, "full", s.ref)
+    ranges = pipeline.plan_ranges(plan, 1 << 30)
+    slots = int(plan.fam_bases().sum())
+    assert len(ranges) >= 3 and slots > (1 << 32), (len(ranges), slots)
+    cons, _ = pipeline.run_step5(engine, s.raw, batch_bases=1 << 30)
+    assert cons.status.shape[0] == plan.n_fam
+    ref = oracle.run(s.raw, s.ref, threads=THREADS)
+    live = _compare_all(cons, ref, "C5 stream %d batches" % len(ranges))
+    _invariants(cons, live, int(s.raw.l_seq.max()) + 1)

@@ -146,17 +146,17 @@ def test_large_family_kernel(engine, where, monkeypatch):
     """every family through the workgroup-per-family kernel (arena in LDS, or in HBM scratch)."""
     s = synth.generate("C2", 700, seed=12, device="cpu", genome_len=200_000)
     raw = synth.messify(s.raw, frac=0.1, seed=2)
-    real = batch.build_family_batch
+    real = batch.materialize
 
-    def forced(r, mode="full", ref=None, small_cap=0, **kw):
-        fb = real(r, mode, ref, small_cap=0, **kw)
+    def forced(plan, f0, f1, small_cap=0):
+        fb = real(plan, f0, f1, small_cap=0)
         if where == "global":  # every large family in the last (HBM scratch) bucket
             nb = len(fb.large_buckets)
             fb.large_buckets = [np.zeros((0, 4), np.uint32)] * (nb - 1) + [fb.large_fams]
             fb.large_arenas = [16] * (nb - 1) + [max(max(fb.large_arenas), batch.LARGE_LDS_MAX + 16)]
         return fb
 
-    monkeypatch.setattr(pipeline, "build_family_batch", forced)
+    monkeypatch.setattr(pipeline, "materialize", forced)
     engine.load_reference(s.ref)
     cons, _ = pipeline.run_step5(engine, raw, tags=True)
     ref = oracle.run(raw, s.ref)
