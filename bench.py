@@ -4,13 +4,19 @@ Workload (BASELINE.json configs[1], SURVEY.md 8d "C2"): 1M synthetic WGBS/EM-seq
 GPU, 2x150 bp, Poisson(4) templates per family split between the strands, generated on the GPU
 from a seeded model (no network, no real data).  A "step" is one pass of the fused hot path --
 B-strand conversion, gap extension, overlapping-bases consensus, source reads, alignment filter,
-single-strand vote, duplex combine -- over the whole resident batch (bsdc_run, both family
-kernels).  Inputs are in HBM before the timed region; outputs stay in HBM.
+single-strand vote, duplex combine -- over every resident batch of the rank (bsdc_run, both
+family kernels).  Inputs are in HBM before the timed region; outputs stay in HBM.
 
-Multi-GPU: one process per GPU (torch.distributed.run), every rank owns its own 1M families
-(weak scaling, no data-path collective); barrier + synchronize around the timed steps, max time
-over ranks, value = families on all ranks / that time.  One all_reduce of a counter pair rides
-along (the optional RCCL counter reduction of SURVEY.md 8e).
+Multi-GPU: one process per GPU.  `--gpus N` without a launcher spawns the N ranks itself
+(shard.launch, before anything touches the GPU); under torch.distributed.run the environment's
+WORLD_SIZE must equal N.  Every rank owns its own families (weak scaling, no data-path
+collective); barrier + synchronize around the timed steps; shard.reduce_step takes the MAX time
+over ranks and SUMs the family counters (the optional RCCL counter reduction of SURVEY.md 8e);
+value = families on all ranks / that time.
+
+C5 (configs[4], 100M families over 2/4/8 GPUs): C2-shaped families, each rank's share (default
+12.5M = 100M / 8) generated and uploaded as a stream of bounded batches (--batch-families) that
+stay resident; a step runs every batch once.
 """
 from __future__ import annotations
 
@@ -27,10 +33,9 @@ ROOT = os.path.dirname(os.path.abspath(__file__))
 sys.path.insert(0, ROOT)
 
 from bsseqconsensusreads_amd import batch as B  # noqa: E402
-from bsseqconsensusreads_amd import synth  # noqa: E402
+from bsseqconsensusreads_amd import shard, synth  # noqa: E402
 from bsseqconsensusreads_amd._lib import (MODE_CONVERT, MODE_EXTEND, MODE_SKIP_LARGE, MODE_SKIP_SMALL,  # noqa: E402
                                           MODE_VOTE)
-from bsseqconsensusreads_amd.device import Engine  # noqa: E402
 
 METRIC = "duplex families/sec (node) at 1/2/4/8 MI355X; % HBM roofline; speedup vs CPU"
 HBM_PEAK_GBS = 8000.0  # MI355X_MICROARCH.md: HBM3E 8.0 TB/s spec
@@ -40,71 +45,94 @@ WORKLOADS = {
     "C1": "configs[0] shape: 3 reads/strand EM-seq families, 2x150bp",
     "C3": "configs[2]: high-depth panel, 20-100 templates/family, short overlapping inserts",
     "C4": "configs[3]: skewed 1-500 family sizes, 30% AB-only",
+    "C5": "configs[4]: 100M-family C2-shaped EM-seq set sharded by family batch; per-GPU share as a "
+          "stream of resident batches",
 }
+DEFAULT_FAMILIES = {"C3": 200_000, "C5": 12_500_000}
 FULL_MODE = MODE_CONVERT | MODE_EXTEND | MODE_VOTE
 
 
-def algorithmic_bytes(fb: B.FamilyBatch, cons_len: np.ndarray, status: np.ndarray, fams: np.ndarray) -> int:
-    """B_fam = sum_records(ceil(L/2) + L + 16) + sum_converted ceil((L+2)/2)
-    + sum_{2 ends}(ceil(Lc/2) + Lc), summed over `fams`."""
+def family_input_bytes(fb: B.FamilyBatch) -> np.ndarray:
+    """SURVEY.md 8d, input side per family: sum_records(ceil(L/2) + L + 16) + sum_converted ceil((L+2)/2)."""
     L = (fb.rec_lenflag & 0xFFFF).astype(np.int64)
     conv = (fb.rec_link & B.LINK_CONVERT) != 0
     per_rec = (L + 1) // 2 + L + 16 + np.where(conv, (L + 3) // 2, 0)
     sizes = np.diff(fb.fam_off.astype(np.int64))
     fam_of = np.repeat(np.arange(fb.n_fam), sizes)
-    per_fam = np.bincount(fam_of, weights=per_rec, minlength=fb.n_fam)
+    return np.bincount(fam_of, weights=per_rec, minlength=fb.n_fam).astype(np.int64)
+
+
+def family_output_bytes(cons_len: np.ndarray, status: np.ndarray) -> np.ndarray:
+    """SURVEY.md 8d, output side per family: sum_{2 ends}(ceil(Lc/2) + Lc)."""
     lc = np.where((status & 1)[:, None] != 0, cons_len, 0).astype(np.int64)
-    per_fam = per_fam + ((lc + 1) // 2 + lc).sum(1)
-    return int(per_fam[fams].sum())
+    return ((lc + 1) // 2 + lc).sum(1)
 
 
 def cpu_baseline(raw, ref, n_fam_sample: int, threads: int):
-    """oracle/ (C restatement, OpenMP over families) on the first n_fam_sample families."""
+    """oracle/ (C restatement, OpenMP over families) on the first n_fam_sample families -> families/s."""
     from oracle import oracle
     sub = synth.subset_families(raw, n_fam_sample)
     res = oracle.run(sub, ref, threads=threads)
     return n_fam_sample / res.seconds, res.seconds
 
 
-def main():
-    ap = argparse.ArgumentParser()
-    ap.add_argument("--gpus", type=int, default=1)
-    ap.add_argument("--steps", type=int, default=20)
-    ap.add_argument("--warmup", type=int, default=3)
-    ap.add_argument("--config", default="C2", choices=sorted(WORKLOADS))
-    ap.add_argument("--families", type=int, default=None,
-                    help="families per GPU (default 1M; C3 200K, whose deep families fill 32-bit image offsets)")
-    ap.add_argument("--cpu-sample", type=int, default=1_000_000, help="families for the CPU baseline (0 = skip)")
-    ap.add_argument("--seed", type=int, default=42)
-    args = ap.parse_args()
+class Resident:
+    """One device batch kept in HBM for the timed steps, with its host-side accounting."""
 
-    world = int(os.environ.get("WORLD_SIZE", "1"))
-    rank = int(os.environ.get("RANK", "0"))
-    local = int(os.environ.get("LOCAL_RANK", "0"))
-    dist = None
-    if world > 1:
-        import torch.distributed as dist
-        os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
-        torch.cuda.set_device(local)
-        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
-    else:
-        torch.cuda.set_device(local)
+    def __init__(self, eng, fb: B.FamilyBatch):
+        self.db = eng.upload(fb)
+        self.in_bytes = family_input_bytes(fb)
+        self.small = fb.small_fams.astype(np.int64)
+        self.n_large = int(fb.large_fams.shape[0])
+        self.n_disp = sum(1 for b in fb.small_buckets if b.shape[0])  # one k_small dispatch per LDS bucket
+        self.molecules = int(np.unique(fb.fam_mi).shape[0])
+        self.n_fam, self.n_rec, self.n_bases = fb.n_fam, fb.n_rec, fb.n_bases
+        self.db.release_host()
+
+
+def build(args, rank: int, dev, eng):
+    """-> (resident batches, the first batch's raw records + reference for the CPU baseline)."""
+    if args.config != "C5":
+        s = synth.generate(args.config, args.families, seed=args.seed + rank, device=dev)
+        eng.load_reference(s.ref)
+        return [Resident(eng, B.build_family_batch(s.raw, "full", s.ref))], s
+    # C5: the rank's share as a stream of batches, each its own seeded chunk of families (the
+    # chunk index is part of the seed) on the rank's one genome
+    out, first = [], None
+    left, i = args.families, 0
+    while left > 0:
+        n = min(args.batch_families, left)
+        s = synth.generate("C2", n, seed=args.seed + 1000 * rank + i, device=dev, reuse=first)
+        if first is None:
+            eng.load_reference(s.ref)
+            first = s
+        out.append(Resident(eng, B.build_family_batch(s.raw, "full", s.ref)))
+        left -= n
+        i += 1
+    return out, first
+
+
+def run(args):
+    rank, world, local = shard.env_rank()
+    torch.cuda.set_device(local)
     dev = torch.device("cuda", local)
+    dist = shard.init("nccl", dev)
+    from bsseqconsensusreads_amd.device import Engine
 
     t0 = time.time()
-    if args.families is None:
-        args.families = 200_000 if args.config == "C3" else 1_000_000
-    s = synth.generate(args.config, args.families, seed=args.seed + rank, device=dev)
-    fb = B.build_family_batch(s.raw, "full", s.ref)
     eng = Engine(local)
-    eng.load_reference(s.ref)
-    db = eng.upload(fb)
+    res, s0 = build(args, rank, dev, eng)
     torch.cuda.synchronize()
     setup_s = time.time() - t0
 
     stream = torch.cuda.current_stream(dev)
+
+    def step(mode=FULL_MODE):
+        for r in res:
+            eng.run(r.db, mode, stream)
+
     for _ in range(args.warmup):
-        eng.run(db, FULL_MODE, stream)
+        step()
     torch.cuda.synchronize()
 
     # ---- timed region: K full steps ----
@@ -115,7 +143,7 @@ def main():
     w0 = time.perf_counter()
     ev0.record(stream)
     for _ in range(args.steps):
-        eng.run(db, FULL_MODE, stream)
+        step()
     ev1.record(stream)
     torch.cuda.synchronize()
     if dist is not None:
@@ -123,41 +151,36 @@ def main():
     wall = time.perf_counter() - w0
     elapsed = max(wall, ev0.elapsed_time(ev1) / 1e3)
 
-    out = db.fetch()
-    emitted = int((out["status"] & 1).sum())
-    tot = torch.tensor([elapsed, 0.0], dtype=torch.float64, device=dev)
+    outs = [r.db.fetch_lengths() for r in res]
+    emitted = sum(int((st & 1).sum()) for st, _ in outs)
     # the unit is the input family (one MI base = one molecule); TemplateCoordinate order can
     # split a molecule into several consensus families (config.consensus_families_per_gpu)
-    molecules = int(np.unique(fb.fam_mi).shape[0])
-    cnt = torch.tensor([molecules, emitted], dtype=torch.int64, device=dev)
-    if dist is not None:
-        dist.all_reduce(tot, op=dist.ReduceOp.MAX)
-        dist.all_reduce(cnt, op=dist.ReduceOp.SUM)
-    elapsed = float(tot[0])
-    fams_total = int(cnt[0])
+    molecules = sum(r.molecules for r in res)
+    elapsed, (fams_total, emitted_total) = shard.reduce_step(dist, elapsed, [molecules, emitted], dev)
 
     # ---- roofline of the dominant kernel (small-family kernel), HIP events on its stream ----
-    small = fb.small_fams.astype(np.int64)
-    large = fb.large_fams[:, 0].astype(np.int64)
     ks = max(5, args.steps)
     e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
     e0.record(stream)
     for _ in range(ks):
-        eng.run(db, FULL_MODE | MODE_SKIP_LARGE, stream)
+        step(FULL_MODE | MODE_SKIP_LARGE)
     e1.record(stream)
     torch.cuda.synchronize()
     t_small = e0.elapsed_time(e1) / 1e3 / ks
     t_large = 0.0
-    if large.size:
+    if any(r.n_large for r in res):
         e0.record(stream)
         for _ in range(ks):
-            eng.run(db, FULL_MODE | MODE_SKIP_SMALL, stream)
+            step(FULL_MODE | MODE_SKIP_SMALL)
         e1.record(stream)
         torch.cuda.synchronize()
         t_large = e0.elapsed_time(e1) / 1e3 / ks
-    n_disp = sum(1 for b in fb.small_buckets if b.shape[0])  # one k_small dispatch per non-empty LDS bucket
-    bytes_small = algorithmic_bytes(fb, out["len"], out["status"], small)
-    bytes_all = algorithmic_bytes(fb, out["len"], out["status"], np.arange(fb.n_fam))
+    n_disp = sum(r.n_disp for r in res)
+    bytes_small, bytes_all = 0, 0
+    for r, (st, ln) in zip(res, outs):
+        per = r.in_bytes + family_output_bytes(ln, st)
+        bytes_small += int(per[r.small].sum())
+        bytes_all += int(per.sum())
     achieved = bytes_small / t_small / 1e9
     # HBM bytes of one k_small launch set (one dispatch per non-empty LDS bucket), from the PMC
     # passes of profiles/collect_pmc.sh on this same workload (FETCH_SIZE x2 + WRITE_SIZE,
@@ -167,29 +190,37 @@ def main():
     pmc = os.path.join(ROOT, "profiles", "pmc_%s.json" % args.config)
     if os.path.exists(pmc) and args.families == 1_000_000 and args.seed == 42:
         with open(pmc) as fh:
-            ks = json.load(fh).get("k_small", {})
-        per = ks.get("hbm_bytes_per_dispatch")
+            kd = json.load(fh).get("k_small", {})
+        per = kd.get("hbm_bytes_per_dispatch")
         if per is not None:
             traffic = int(per * n_disp)
         # the bound that actually binds: VALU issue.  A wave64 VALU instruction takes 2 cycles of
         # its SIMD (MI355X_MICROARCH.md), 1024 SIMDs at 2.4 GHz; instructions per launch from the
         # same PMC passes (SQ_INSTS_VALU is per wave-instruction)
-        valu = ks.get("mean_per_dispatch", {}).get("SQ_INSTS_VALU")
+        valu = kd.get("mean_per_dispatch", {}).get("SQ_INSTS_VALU")
         if valu is not None:
             v_launch = valu * n_disp
-            issue = {"valu_insts_per_family": round(v_launch / max(int(small.size), 1), 1),
+            n_small = sum(int(r.small.size) for r in res)
+            issue = {"valu_insts_per_family": round(v_launch / max(n_small, 1), 1),
                      "valu_issue_floor_ms": round(v_launch * 2 / (1024 * 2.4e9) * 1e3, 4),
-                     "valu_issue_frac": round(v_launch * 2 / (1024 * 2.4e9) / t_small, 4)}
+                     "valu_issue_frac": round(v_launch * 2 / (1024 * 2.4e9) / t_small, 4),
+                     "pmc_source": os.path.relpath(pmc, ROOT)}
 
     cpu = None
     if rank == 0 and world == 1 and args.cpu_sample > 0:
+        # the host's CPU share: OMP_NUM_THREADS / nproc (16 on the GPU box, whose os.cpu_count()
+        # shows the whole machine); no further cap
         threads = int(os.environ.get("OMP_NUM_THREADS", "0") or 0) or (os.cpu_count() or 1)
-        threads = min(threads, 16)
-        n_s = min(args.cpu_sample, args.families)
-        v, secs = cpu_baseline(s.raw, s.ref, n_s, threads)
+        n_s = min(args.cpu_sample, int(s0.n_fam))
+        v, secs = cpu_baseline(s0.raw, s0.ref, n_s, threads)
+        n_1 = min(args.cpu_sample_1core, n_s)
+        v1, secs1 = cpu_baseline(s0.raw, s0.ref, n_1, 1) if n_1 > 0 else (None, 0.0)
         cpu = {"value": round(v, 1), "unit": "families/s", "cores": threads, "kind": "port",
-               "sample": "first %d families of the same %s workload through oracle/ (C restatement of tools 1+2 and "
-                         "the duplex vote, OpenMP over families), %.1f s" % (n_s, args.config, secs)}
+               "cores_all": threads, "value_all": round(v, 1),
+               "value_1core": round(v1, 1) if v1 is not None else None,
+               "sample": "first %d families of the same %s workload through oracle/ (C restatement of tools 1+2 "
+                         "and the duplex vote, OpenMP over families) on %d threads, %.1f s; 1 core: first %d "
+                         "families, %.1f s" % (n_s, args.config, threads, secs, n_1, secs1)}
 
     if rank == 0:
         line = {
@@ -206,10 +237,12 @@ def main():
             "dtype": "u8",
             "data": "synthetic (seeded EM-seq duplex model generated on the GPU, SURVEY.md 8d)",
             "config": {"workload": args.config + " -- " + WORKLOADS[args.config],
-                       "families_per_gpu": molecules, "consensus_families_per_gpu": int(fb.n_fam),
-                       "family_order": "fgbio TemplateCoordinate runs of one MI", "records_per_gpu": int(fb.n_rec),
-                       "bases_per_gpu": int(fb.n_bases), "small_families": int(small.size),
-                       "large_families": int(large.size), "parallelism": "family-sharded x%d" % world},
+                       "families_per_gpu": molecules, "consensus_families_per_gpu": sum(r.n_fam for r in res),
+                       "batches_per_gpu": len(res),
+                       "family_order": "fgbio TemplateCoordinate runs of one MI",
+                       "records_per_gpu": sum(r.n_rec for r in res), "bases_per_gpu": sum(r.n_bases for r in res),
+                       "small_families": sum(int(r.small.size) for r in res),
+                       "large_families": sum(r.n_large for r in res), "parallelism": "family-sharded x%d" % world},
             "roofline": {"bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
                          "frac": round(achieved / HBM_PEAK_GBS, 4), "traffic": traffic,
                          "kernel": "k_small", "kernel_ms": round(t_small * 1e3, 4),
@@ -220,7 +253,7 @@ def main():
                          "step_algorithmic_GBps": round(bytes_all / (elapsed / args.steps) / 1e9, 1),
                          "issue": issue},
             "cpu_baseline": cpu,
-            "families_emitted": int(cnt[1]),
+            "families_emitted": int(emitted_total),
             "setup_s": round(setup_s, 1),
         }
         print(json.dumps(line), flush=True)
@@ -229,5 +262,38 @@ def main():
         dist.destroy_process_group()
 
 
+def parse(argv=None):
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=20)
+    ap.add_argument("--warmup", type=int, default=3)
+    ap.add_argument("--config", default="C2", choices=sorted(WORKLOADS))
+    ap.add_argument("--families", type=int, default=None,
+                    help="families per GPU (default 1M; C3 200K, whose deep families fill 32-bit image offsets; "
+                         "C5 12.5M = 100M / 8)")
+    ap.add_argument("--batch-families", type=int, default=1_500_000, help="C5: families per resident batch")
+    ap.add_argument("--cpu-sample", type=int, default=1_000_000,
+                    help="families for the all-cores CPU baseline (0 = skip)")
+    ap.add_argument("--cpu-sample-1core", type=int, default=100_000, help="families for the 1-core CPU baseline")
+    ap.add_argument("--seed", type=int, default=42)
+    a = ap.parse_args(argv)
+    if a.families is None:
+        a.families = DEFAULT_FAMILIES.get(a.config, 1_000_000)
+    return a
+
+
+def main(argv=None) -> int:
+    args = parse(argv)
+    if "WORLD_SIZE" not in os.environ and args.gpus > 1:
+        # no launcher: one spawned process per GPU (this process never touches the GPU)
+        return shard.launch(args.gpus, run, (args,))
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    if world != args.gpus:
+        print("bench.py: --gpus %d but WORLD_SIZE=%d" % (args.gpus, world), file=sys.stderr)
+        return 2
+    run(args)
+    return 0
+
+
 if __name__ == "__main__":
-    main()
+    sys.exit(main())

@@ -534,12 +534,35 @@ def duplex_records(cons, raw: R.RawRecords, prefix: str, threads: int = 0, molec
         cigar=np.zeros(0, np.uint32), seq_off=seq_off, seq=seq, qual=qual, aux=auxs_t)
 
 
+def consensus_sharded(eng, raw: R.RawRecords, tags: bool, batch_bases: Optional[int] = None, dist=None):
+    """pipeline.run_step5 over the ranks of `dist` (None = this process alone): every rank forms
+    the same family plan, runs the batches shard.deal gives it on its own GPU, and rank 0 gets the
+    consensus of all batches in plan order (shard.gather_in_order; other ranks get None).  A plan
+    whose tool-2 extension partners straddle families runs on rank 0 alone (pipeline.run_step5's
+    two-launch fallback)."""
+    from . import pipeline, shard
+    if dist is None or dist.get_world_size() == 1:
+        return pipeline.run_step5(eng, raw, tags=tags, batch_bases=batch_bases)[0]
+    rank, world = dist.get_rank(), dist.get_world_size()
+    plan = pipeline.plan_families(raw, "full", eng.ref)
+    if plan.split_ext:
+        return pipeline.run_step5(eng, raw, tags=tags, batch_bases=batch_bases)[0] if rank == 0 else None
+    ranges = pipeline.plan_ranges(plan, batch_bases)
+    mine_idx = shard.deal(ranges, world, rank)
+    parts = pipeline.run_ranges(eng, plan, [ranges[i] for i in mine_idx],
+                                pipeline.MODE_CONVERT | pipeline.MODE_EXTEND | pipeline.MODE_VOTE, tags)
+    got = shard.gather_in_order(dist, dict(zip(mine_idx, parts)), len(ranges))
+    return pipeline.concat_consensus(got) if rank == 0 else None
+
+
 def step5(in_bam: str, fasta: str, out_bam: Optional[str], engine=None, prefix: Optional[str] = None, threads: int = 0,
-          level: int = 6, fastq: Optional[Tuple[str, str]] = None, tags: bool = True) -> dict:
+          level: int = 6, fastq: Optional[Tuple[str, str]] = None, tags: bool = True, batch_bases: Optional[int] = None,
+          dist=None) -> dict:
     """Rules convert_Bstrain .. callduplex (main.snake.py:121-164) as one call on files; with
     `fastq`, also the following consensusduplex_to_fq rule (main.snake.py:167-177) straight from
-    the consensus records (out_bam may then be None: no BAM round trip)."""
-    from . import pipeline
+    the consensus records (out_bam may then be None: no BAM round trip).  The stream runs as
+    bounded device batches (batch_bases, pipeline.DEFAULT_BATCH_BASES); with `dist` the batches
+    are shared by the ranks (one GPU each) and rank 0 writes the files."""
     from .device import Engine
     header, raw = read_bam(in_bam, threads)
     ref = read_fasta(fasta, header)
@@ -547,10 +570,12 @@ def step5(in_bam: str, fasta: str, out_bam: Optional[str], engine=None, prefix: 
     eng = Engine(0) if own else engine
     try:
         eng.load_reference(ref)
-        cons, _ = pipeline.run_step5(eng, raw, tags=tags and out_bam is not None)
+        cons = consensus_sharded(eng, raw, tags and out_bam is not None, batch_bases, dist)
     finally:
         if own:
             eng.close()
+    if cons is None:  # not rank 0
+        return {"records_in": raw.n}
     recs = duplex_records(cons, raw, read_name_prefix(header) if prefix is None else prefix, threads)
     if out_bam is not None:
         write_bam(out_bam, output_header(header), recs, level, threads)

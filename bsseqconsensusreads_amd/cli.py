@@ -9,11 +9,16 @@
 OUT.bam may be '-' to skip the BAM when only the FASTQ pair is wanted.  Errors exit non-zero with
 the message on stderr, so Snakemake aborts the rule and removes partial outputs, as it does for
 the reference tools (tools/2.extend_gap.py:179-180 raises on a record without MI).
+
+step5 --gpus N: one process per GPU (spawned here, or under torch.distributed.run); the family
+batches are dealt to the ranks and rank 0 writes the outputs, identical to --gpus 1
+(bam.consensus_sharded).  --devices maps ranks to device ids (default rank r -> GPU r).
 """
 from __future__ import annotations
 
 import argparse
 import json
+import os
 import sys
 
 
@@ -32,6 +37,10 @@ def parse(argv):
         p.add_argument("--threads", type=int, default=8)
         p.add_argument("--compression", type=int, default=6)
         p.add_argument("--device", type=int, default=0)
+        if name == "step5":
+            p.add_argument("--gpus", type=int, default=1, help="one process per GPU, family batches dealt to them")
+            p.add_argument("--devices", default=None, help="comma-separated device id per rank (default 0..gpus-1)")
+            p.add_argument("--batch-bases", type=int, default=None, help="device batch budget in bases")
         p.add_argument("--output-per-base-tags", default="true", choices=["true", "false"],
                        help="fgbio's consensus tags (per-read and per-base statistics); off = name/SEQ/QUAL/RG/MI/RX")
     a = ap.parse_args(argv)
@@ -43,17 +52,34 @@ def parse(argv):
 
 
 def main(argv=None) -> int:
-    a = parse(sys.argv[1:] if argv is None else argv)
-    from . import bam
+    argv = sys.argv[1:] if argv is None else list(argv)
+    a = parse(argv)
+    from . import bam, shard
+    gpus = getattr(a, "gpus", 1)
+    if gpus > 1 and "WORLD_SIZE" not in os.environ:
+        return shard.launch(gpus, main, (argv,))  # this process never touches the GPU
+    rank, world, local = shard.env_rank()
+    if world != gpus:
+        print("--gpus %d but WORLD_SIZE=%d" % (gpus, world), file=sys.stderr)
+        return 2
+    device = a.device
+    if world > 1:
+        devs = [int(x) for x in a.devices.split(",")] if a.devices else list(range(world))
+        if len(devs) != world:
+            print("--devices needs %d ids" % world, file=sys.stderr)
+            return 2
+        device = devs[local]
     from .device import Engine
     out = None if a.output == "-" else a.output
     fq = (a.fastq1, a.fastq2) if a.fastq1 else None
+    dist = None
     try:
-        eng = Engine(a.device)
+        dist = shard.init("gloo") if world > 1 else None  # host gather of the batch outputs only
+        eng = Engine(device)
         try:
             if a.cmd == "step5":
                 info = bam.step5(a.input, a.reference, out, eng, a.read_name_prefix, a.threads, a.compression, fq,
-                                 tags=a.output_per_base_tags == "true")
+                                 tags=a.output_per_base_tags == "true", batch_bases=a.batch_bases, dist=dist)
             else:
                 info = bam.molecular(a.input, out, eng, a.read_name_prefix, a.threads, a.compression, fq,
                                      tags=a.output_per_base_tags == "true")
@@ -62,7 +88,11 @@ def main(argv=None) -> int:
     except Exception as e:  # noqa: BLE001 -- the rule fails with the message, like the tools do
         print("%s: %s" % (type(e).__name__, e), file=sys.stderr)
         return 1
-    print(json.dumps(info), file=sys.stderr)
+    finally:
+        if dist is not None:
+            dist.destroy_process_group()
+    if rank == 0:
+        print(json.dumps(info), file=sys.stderr)
     return 0
 
 

@@ -38,6 +38,7 @@ class DeviceBatch:
 
     def __init__(self, fb: FamilyBatch, device: torch.device, dump: bool = False, tags: bool = False):
         self.fb = fb
+        self.n_fam, self.n_rec = fb.n_fam, fb.n_rec
         self.device = device
         self.t: Dict[str, torch.Tensor] = {}
         for k, v in fb.device_arrays().items():
@@ -99,9 +100,19 @@ class DeviceBatch:
             o.ss_len, o.ss_base, o.ss_qual = _dptr(self.ss_len), _dptr(self.ss_base), _dptr(self.ss_qual)
             o.ss_depth, o.ss_err = _dptr(self.ss_depth), _dptr(self.ss_err)
 
+    def release_host(self):
+        """Drop the host copy of the batch (the device copy stays resident)."""
+        self.fb = None
+
+    def fetch_lengths(self):
+        """-> (status [F], len [F, 2]): the small outputs only (bench bookkeeping)."""
+        F = self.n_fam
+        return (self.status[:F].cpu().numpy(),
+                self.len[:2 * F].cpu().numpy().view(np.uint16).astype(np.int32).reshape(F, 2))
+
     def fetch(self):
         """-> dict of numpy arrays (consensus and, if dumped, the post-tool records)."""
-        F = self.fb.n_fam
+        F = self.n_fam
         out = {
             "status": self.status[:F].cpu().numpy(),
             "len": self.len[:2 * F].cpu().numpy().view(np.uint16).astype(np.int32).reshape(F, 2),
@@ -118,7 +129,7 @@ class DeviceBatch:
             out["ss_depth"] = u16(self.ss_depth[:n]).reshape(F, 4, self.stride)
             out["ss_err"] = u16(self.ss_err[:n]).reshape(F, 4, self.stride)
         if self.dump:
-            Rn = self.fb.n_rec
+            Rn = self.n_rec
             out["dump_pos"] = self.dump_pos[:Rn].cpu().numpy()
             out["dump_len"] = self.dump_len[:Rn].cpu().numpy().view(np.uint16).astype(np.int32)
             out["dump_tags"] = self.dump_tags[:Rn].cpu().numpy()

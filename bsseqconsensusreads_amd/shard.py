@@ -5,10 +5,16 @@ family stream into contiguous batches balanced by bases (not by family count -- 
 them round-robin to the ranks (one process per GPU, torch.distributed), and gathers the per-batch
 outputs back in input order.  The only collectives are the step-time MAX and the counter SUM of
 the bench line (8 + 16 bytes) and the host-side object gather of the outputs.
+
+``launch`` starts the ranks itself (spawn) when no external launcher did, so `bench.py --gpus N`
+and `cli step5 --gpus N` run one process per GPU either way.
 """
 from __future__ import annotations
 
-from typing import Dict, List, Sequence, Tuple
+import os
+import socket
+import sys
+from typing import Callable, Dict, List, Optional, Sequence, Tuple
 
 import numpy as np
 import torch
@@ -74,3 +80,63 @@ def gather_in_order(dist, mine: Dict[int, object], n_batches: int, dst: int = 0)
     if missing:
         raise RuntimeError("batches %s produced by no rank" % missing[:8])
     return [merged[i] for i in range(n_batches)]
+
+
+def free_port() -> int:
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    port = s.getsockname()[1]
+    s.close()
+    return port
+
+
+def _rank_main(rank: int, world: int, port: int, fn: Callable, args: tuple):
+    # runs in a fresh (spawned) interpreter: nothing has touched the GPU yet
+    os.environ.update({"RANK": str(rank), "LOCAL_RANK": str(rank), "WORLD_SIZE": str(world),
+                       "LOCAL_WORLD_SIZE": str(world), "MASTER_ADDR": "127.0.0.1", "MASTER_PORT": str(port)})
+    try:
+        rc = fn(*args)
+    except Exception as e:  # noqa: BLE001 -- one line per failing rank, non-zero exit
+        print("rank %d/%d: %s: %s" % (rank, world, type(e).__name__, e), file=sys.stderr, flush=True)
+        sys.exit(1)
+    if rc:
+        sys.exit(int(rc))
+
+
+def launch(world: int, fn: Callable, args: tuple = ()) -> int:
+    """One process per GPU without an external launcher: `world` spawned ranks run fn(*args) with
+    RANK / LOCAL_RANK / WORLD_SIZE / MASTER_* set as torch.distributed.run sets them.  The caller
+    must not have touched the GPU (spawn, never fork or exec from a GPU process).  Returns the
+    first non-zero exit code of the ranks (0 when all succeed)."""
+    import torch.multiprocessing as mp
+    ctx = mp.get_context("spawn")
+    port = free_port()
+    procs = [ctx.Process(target=_rank_main, args=(r, world, port, fn, args)) for r in range(world)]
+    for p in procs:
+        p.start()
+    code = 0
+    for p in procs:
+        p.join()
+        if p.exitcode and not code:
+            code = p.exitcode if p.exitcode > 0 else 128 - p.exitcode
+    return code
+
+
+def env_rank() -> Tuple[int, int, int]:
+    """(rank, world, local rank) from the torch.distributed.run environment (1 rank without it)."""
+    return (int(os.environ.get("RANK", "0")), int(os.environ.get("WORLD_SIZE", "1")),
+            int(os.environ.get("LOCAL_RANK", "0")))
+
+
+def init(backend: str, device: Optional[torch.device] = None):
+    """torch.distributed over the environment's rendezvous (127.0.0.1); None for one rank."""
+    rank, world, _ = env_rank()
+    if world <= 1:
+        return None
+    import torch.distributed as dist
+    os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
+    if backend == "nccl" and device is not None:
+        dist.init_process_group(backend, device_id=device)
+    else:
+        dist.init_process_group(backend)
+    return dist

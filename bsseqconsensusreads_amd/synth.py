@@ -81,19 +81,26 @@ class SynthSet:
     ref: R.Reference
     cfg: str
     n_fam: int
+    genome: Optional[torch.Tensor] = None  # nt16 codes on the generating device (reusable by later chunks)
 
 
 def generate(cfg: str = "C2", n_fam: int = 1000, seed: int = 42, device=None, genome_len: int = 10_000_000,
-             read_len: int = 150, chunk: int = 1 << 22, frag: Optional[Tuple[float, float, int]] = None) -> SynthSet:
+             read_len: int = 150, chunk: int = 1 << 22, frag: Optional[Tuple[float, float, int]] = None,
+             reuse: Optional["SynthSet"] = None) -> SynthSet:
     """frag = (mean, sd, min) overrides the fragment-length model (tests use short inserts to
-    exercise read-through trimming; the configs keep the survey's model)."""
+    exercise read-through trimming; the configs keep the survey's model).  reuse: draw the
+    families on that set's genome (one reference for a stream of chunks)."""
     if device is None:
         device = "cuda" if torch.cuda.is_available() else "cpu"
     device = torch.device(device)
     gen = torch.Generator(device=device)
     gen.manual_seed(seed)
     L = read_len
-    genome = make_genome(genome_len, gen, device)
+    if reuse is not None and reuse.genome is not None:
+        genome = reuse.genome.to(device)
+        genome_len = int(genome.shape[0])
+    else:
+        genome = make_genome(genome_len, gen, device)
     na, nb = family_sizes(cfg, n_fam, gen, device)
     fam_ab_top = torch.rand(n_fam, generator=gen, device=device) < 0.5
     if frag is not None:
@@ -187,8 +194,8 @@ def generate(cfg: str = "C2", n_fam: int = 1000, seed: int = 42, device=None, ge
         names=_LazyNames("t"), mi_id=to(fam, np.int32), mi_strand=to(strand, np.int8),
         mi_names=_LazyNames(""), mc_off=np.arange(n, dtype=np.int64), mc_n=np.ones(n, np.int32),
         mc_cigar=np.full(n, (L << 4) | 0, np.uint32), aux=None, la_tag=None, rd_tag=None)
-    ref = R.Reference.from_codes(["chrS"], [genome.to("cpu").numpy()])
-    return SynthSet(raw, ref, cfg, n_fam)
+    ref = reuse.ref if reuse is not None else R.Reference.from_codes(["chrS"], [genome.to("cpu").numpy()])
+    return SynthSet(raw, ref, cfg, n_fam, genome)
 
 
 class _LazyNames:
