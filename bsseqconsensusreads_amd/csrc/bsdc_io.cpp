@@ -69,7 +69,13 @@ int64_t aux_value_size(const uint8_t *p, const uint8_t *end) {
         if (end - v < 5) return -1;
         const char sub = (char)v[0];
         const int64_t cnt = rd32(v + 1);
-        const int w = (sub == 'c' || sub == 'C') ? 1 : (sub == 's' || sub == 'S') ? 2 : 4;
+        int w;
+        switch (sub) {
+        case 'c': case 'C': w = 1; break;
+        case 's': case 'S': w = 2; break;
+        case 'i': case 'I': case 'f': w = 4; break;
+        default: return -1;
+        }
         return 5 + cnt * w;
     }
     default: return -1;
@@ -291,17 +297,19 @@ int32_t bsdc_bam_read(const char *path, int32_t n_threads, bsdc_bam **out) {
         const int l_name = r[12];
         const int n_cig = rd16(r + 16);
         const int32_t l_seq = rdi32(r + 20);
-        const uint8_t *aux = r + 36 + l_name + 4 * n_cig + (l_seq + 1) / 2 + l_seq;
-        if (l_seq < 0 || aux > end) {
+        // fixed part + name + cigar + seq + qual, in 64 bits (untrusted lengths)
+        const int64_t body = 36 + (int64_t)l_name + 4 * (int64_t)n_cig + ((int64_t)l_seq + 1) / 2 + (int64_t)l_seq;
+        if (l_seq < 0 || l_name < 1 || body > 4 + bs) {
             badrec |= 1;
             continue;
         }
+        const uint8_t *aux = r + body;
         nbases += l_seq;
         ncig += n_cig;
         naux += end - aux;
         for (const uint8_t *a = aux; a + 3 <= end;) {
             const int64_t vs = aux_value_size(a, end);
-            if (vs < 0 || a + 3 + vs > end) {
+            if (vs < 0 || vs > (end - a) - 3) {
                 badrec |= 1;
                 break;
             }
@@ -625,7 +633,7 @@ namespace {
 std::string_view find_rx(const uint8_t *a, const uint8_t *end) {
     while (a + 3 <= end) {
         const int64_t vs = aux_value_size(a, end);
-        if (vs < 0 || a + 3 + vs > end) break;
+        if (vs < 0 || vs > (end - a) - 3) break;
         if (a[0] == 'R' && a[1] == 'X' && a[2] == 'Z') return std::string_view((const char *)a + 3, (size_t)vs - 1);
         a += 3 + vs;
     }

@@ -15,7 +15,8 @@ from typing import Dict, List, Optional
 import numpy as np
 
 HERE = os.path.dirname(os.path.abspath(__file__))
-LIB = os.path.join(HERE, "build", "liboracle.so")
+# BSDC_ORACLE_LIB: an alternative build of the same restatement (the sanitizer run, tests/sanitize/)
+LIB = os.environ.get("BSDC_ORACLE_LIB") or os.path.join(HERE, "build", "liboracle.so")
 
 NT16 = "=ACMGRSVTWYHKDBN"
 _NT16_ASCII = np.frombuffer(NT16.encode(), dtype=np.uint8)

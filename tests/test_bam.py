@@ -386,3 +386,92 @@ def test_molecular_tags_of_the_oracle_consensus(tmp_path):
     em = np.nonzero(res.status == 1)[0]
     assert out.n == 2 * em.shape[0]
     assert _check_tags(out, res, em, True) == 0
+
+
+def _raw_stream(tmp_path, n_fam=20, seed=6):
+    """(uncompressed BAM bytes, offset of the first record) of a small valid file."""
+    s, raw = _messy(n_fam, seed=seed)
+    p = str(tmp_path / "ok.bam")
+    bam.write_bam(p, _header(s.ref), bam.records_to_bam(raw))
+    data = bytearray(_py_bgzf_read(p))
+    l_text = struct.unpack("<i", data[4:8])[0]
+    o = 8 + l_text
+    n_ref = struct.unpack("<i", data[o:o + 4])[0]
+    o += 4
+    for _ in range(n_ref):
+        ln = struct.unpack("<i", data[o:o + 4])[0]
+        o += 4 + ln + 4
+    return data, o
+
+
+def test_truncated_files_fail_loudly(tmp_path):
+    """A BAM cut anywhere -- inside the magic, the header, a record, a block, or just before the
+    EOF block -- is refused or read to its last whole block, never read past."""
+    s, raw = _messy(60, seed=7)
+    good = tmp_path / "g.bam"
+    bam.write_bam(str(good), _header(s.ref), bam.records_to_bam(raw), level=1)
+    b = good.read_bytes()
+    for cut in (1, 10, 17, 18, 30, len(b) // 3, len(b) // 2, len(b) - 29, len(b) - 28, len(b) - 1):
+        t = tmp_path / ("t%d.bam" % cut)
+        t.write_bytes(b[:cut])
+        try:
+            _, r2 = bam.read_bam(str(t))
+        except OSError:
+            continue
+        assert r2.n <= raw.n  # a cut at a block boundary: the records of the whole blocks
+    # the same stream re-blocked so that records straddle blocks, then cut mid-record
+    data, _ = _raw_stream(tmp_path)
+    q = tmp_path / "q.bam"
+    _py_bgzf_write(str(q), bytes(data[:len(data) - 100]), block=333)
+    with pytest.raises(OSError, match="truncated"):
+        bam.read_bam(str(q))
+
+
+@pytest.mark.parametrize("what", ["block_size_small", "block_size_past_end", "l_read_name_zero", "n_cigar_huge",
+                                  "l_seq_huge", "l_seq_negative", "aux_bad_type", "aux_Z_unterminated",
+                                  "aux_B_huge_count", "aux_B_bad_subtype", "l_text_huge", "ref_name_len_huge"])
+def test_malformed_bam_fields_fail_loudly(tmp_path, what):
+    """Hand-damaged fields of valid BGZF content: every length the parser trusts is checked (the
+    sanitizer run, tests/sanitize/run.sh, runs these under ASan/UBSan)."""
+    data, o = _raw_stream(tmp_path)
+    bs = struct.unpack("<i", data[o:o + 4])[0]
+    r = o + 4  # first record's body
+    l_name = data[r + 8]
+    n_cig = struct.unpack("<H", data[r + 12:r + 14])[0]
+    l_seq = struct.unpack("<i", data[r + 16:r + 20])[0]
+    aux = r + 32 + l_name + 4 * n_cig + (l_seq + 1) // 2 + l_seq
+    end = r + bs
+    if what == "block_size_small":
+        data[o:o + 4] = struct.pack("<i", 20)
+    elif what == "block_size_past_end":
+        data[o:o + 4] = struct.pack("<i", len(data))
+    elif what == "l_read_name_zero":
+        data[r + 8] = 0
+    elif what == "n_cigar_huge":
+        data[r + 12:r + 14] = struct.pack("<H", 0xFFFF)
+    elif what == "l_seq_huge":
+        data[r + 16:r + 20] = struct.pack("<i", 0x7FFFFFFF)
+    elif what == "l_seq_negative":
+        data[r + 16:r + 20] = struct.pack("<i", -5)
+    elif what == "aux_bad_type":
+        data[aux + 2] = ord("q")
+    elif what == "aux_Z_unterminated":
+        # the record's last aux byte is the final NUL of a Z field: make it a letter
+        assert data[end - 1] == 0
+        data[end - 1] = ord("x")
+    elif what in ("aux_B_huge_count", "aux_B_bad_subtype"):
+        # replace the record's aux block by one B array of the same size
+        n = end - aux
+        assert n >= 8
+        sub, cnt = (b"C", 0x7FFFFFF0) if what == "aux_B_huge_count" else (b"k", 1)
+        data[aux:end] = b"XBB" + sub + struct.pack("<I", cnt) + bytes(n - 8)
+    elif what == "l_text_huge":
+        data[4:8] = struct.pack("<I", 0xFFFFFFF0)
+    elif what == "ref_name_len_huge":
+        l_text = struct.unpack("<i", data[4:8])[0]
+        p = 8 + l_text + 4
+        data[p:p + 4] = struct.pack("<i", 0x7FFFFFF0)
+    q = tmp_path / "m.bam"
+    _py_bgzf_write(str(q), bytes(data), block=5000)
+    with pytest.raises(OSError):
+        bam.read_bam(str(q))
