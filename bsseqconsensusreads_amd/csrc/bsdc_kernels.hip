@@ -49,6 +49,11 @@ constexpr int kStageU = SMALL_STAGE_U;
 #define LARGE_THREADS 256  // k_large workgroup size (a multiple of 64)
 #endif
 constexpr int kLargeThreads = LARGE_THREADS;
+#ifndef LARGE_THREADS_BIG
+#define LARGE_THREADS_BIG 512  // k_large workgroup size of the LDS-heavy buckets
+#endif
+constexpr int kLargeThreadsBig = LARGE_THREADS_BIG;
+constexpr int kLargeBigBucket = 3;  // large buckets q >= this (2, 1 workgroups per CU, scratch) use kLargeThreadsBig
 #ifndef LARGE_OVL_CHUNKS
 #define LARGE_OVL_CHUNKS 2  // k_large overlap: SWAR dwords (4 positions each) per task
 #endif
@@ -560,6 +565,14 @@ __device__ __forceinline__ uint32_t ldsu32(const uint8_t *p) {
     return v;
 }
 __device__ __forceinline__ void stu32(uint8_t *p, uint32_t v) { __builtin_memcpy(p, &v, 4); }
+// The LDS dword at any byte offset p of `base` (16-aligned) from two aligned loads and a byte
+// align: gfx950 LDS stalls an unaligned dword access (SQ_LDS_UNALIGNED_STALL)
+__device__ __forceinline__ uint32_t lds_any32(const uint8_t *base, int32_t p) {
+    const int32_t a = p & ~3;
+    const uint32_t lo = *reinterpret_cast<const uint32_t *>(base + a);
+    const uint32_t hi = *reinterpret_cast<const uint32_t *>(base + a + 4);
+    return __builtin_amdgcn_alignbyte(hi, lo, (uint32_t)p & 3u);
+}
 // 0x80 in every byte of x that is 0 (bytes <= 0x80)
 __device__ __forceinline__ uint32_t zero80(uint32_t x) { return ~(x + 0x7F7F7F7Fu) & 0x80808080u; }
 __device__ __forceinline__ uint32_t expand80(uint32_t m80);
@@ -572,7 +585,8 @@ struct Ovl4 {
     uint32_t x, y, qa, qb;  // mate a's / b's 4 bases, 4 quals
 };
 __device__ __forceinline__ Ovl4 ovl4_load(const uint8_t *bimg, const uint8_t *qimg, uint32_t ia, uint32_t ib) {
-    return Ovl4{ldsu32(bimg + ia), ldsu32(bimg + ib), ldsu32(qimg + ia), ldsu32(qimg + ib)};
+    return Ovl4{lds_any32(bimg, (int32_t)ia), lds_any32(bimg, (int32_t)ib), lds_any32(qimg, (int32_t)ia),
+                lds_any32(qimg, (int32_t)ib)};
 }
 __device__ __forceinline__ Ovl4 ovl4_compute(const Ovl4 &in4, int rem) {
     const uint32_t X = in4.x, Y = in4.y, QA = in4.qa, QB = in4.qb;
@@ -624,6 +638,22 @@ __device__ __forceinline__ void lookup4(const int32_t *lr2, uint32_t b, uint32_t
     D1 += *reinterpret_cast<const int32_t *>(base + (lo >> 16));
     D2 += *reinterpret_cast<const int32_t *>(base + (hi & 0xFFFFu));
     D3 += *reinterpret_cast<const int32_t *>(base + (hi >> 16));
+}
+// The same with the valid flags given as 0 / 1 per byte (v)
+__device__ __forceinline__ void lookup4v(const int32_t *lr2, uint32_t v, uint32_t q, int32_t &D0, int32_t &D1,
+                                         int32_t &D2, int32_t &D3) {
+    const uint32_t lo = __builtin_amdgcn_perm(v, q, 0x05010400u) << 2;
+    const uint32_t hi = __builtin_amdgcn_perm(v, q, 0x07030602u) << 2;
+    const uint8_t *base = reinterpret_cast<const uint8_t *>(lr2);
+    D0 += *reinterpret_cast<const int32_t *>(base + (lo & 0xFFFFu));
+    D1 += *reinterpret_cast<const int32_t *>(base + (lo >> 16));
+    D2 += *reinterpret_cast<const int32_t *>(base + (hi & 0xFFFFu));
+    D3 += *reinterpret_cast<const int32_t *>(base + (hi >> 16));
+}
+// 0x01 in every byte of x (plain nt16 codes, <= 15) that is one-hot (A, C, G or T), 0 elsewhere
+__device__ __forceinline__ uint32_t onehot01(uint32_t x) {
+    const uint32_t t = x & ((x | 0x80808080u) - 0x01010101u);  // x & (x - 1) per byte, 0 for x = 0
+    return (~(t + 0x7F7F7F7Fu) & (x + 0x7F7F7F7Fu) & 0x80808080u) >> 7;  // t == 0 && x != 0
 }
 // Mask of the bytes of a lane's dword that lie at or past a read's end, given k8 = 8 x (columns
 // the read still covers from this lane's first column), for a forward read (bytes ascend) or a
@@ -1189,15 +1219,15 @@ __global__ __launch_bounds__(kWave *kSmallMaxWaves, kSmallMinWaves) __attribute_
                         auto fwd = [&](uint32_t d) {
                             // bytes at or past the read's end: (-1 << 8 * covered) as 64 bits
                             const uint32_t x = bytes_past(8 * (int)((d >> 16) & 0x7FFF) - c8, false);
-                            const uint32_t a = (d & 0xFFFFu) + (uint32_t)c;
-                            const uint32_t b = ldsu32(bimg + a) & ~x, q = ldsu32(qimg + a);
+                            const int32_t a = (int32_t)(d & 0xFFFFu) + c;
+                            const uint32_t b = lds_any32(bimg, a) & ~x, q = lds_any32(qimg, a);
                             mf[side] |= b;
                             lookup4(lr2, b, q, D[side][0], D[side][1], D[side][2], D[side][3]);
                         };
                         auto rev = [&](uint32_t d) {  // bytes run backwards: byte 3 - j is column c + j
                             const uint32_t x = bytes_past(8 * (int)((d >> 16) & 0x7FFF) - c8, true);
-                            const uint32_t a = (d & 0xFFFFu) - (uint32_t)c - 3u;
-                            const uint32_t b = ldsu32(bimg + a) & ~x, q = ldsu32(qimg + a);
+                            const int32_t a = (int32_t)(d & 0xFFFFu) - c - 3;
+                            const uint32_t b = lds_any32(bimg, a) & ~x, q = lds_any32(qimg, a);
                             mr[side] |= b;
                             lookup4(lr2, b, q, D[side][3], D[side][2], D[side][1], D[side][0]);
                         };
@@ -1431,8 +1461,9 @@ struct ArenaLayout {
     __host__ __device__ ArenaLayout(int n, int64_t slot_bytes, int max_len, int64_t complex_ops) {
         ssw = (int32_t)round16(max_len + 2);
         int64_t o = 0;
-        meta = (uint32_t)o;
-        o += round16((int64_t)n * (int64_t)sizeof(RecMeta));
+        meta = (uint32_t)o;  // RecMeta per record; in the vote (RecMeta dead) the second wave part's sums
+        const int64_t mb = round16((int64_t)n * (int64_t)sizeof(RecMeta)), vb = 36 * (int64_t)ssw;
+        o += mb > vb ? mb : vb;
         lists = (uint32_t)o;
         o += round16((int64_t)n * 8);
         ssb = (uint32_t)o;
@@ -1447,6 +1478,7 @@ struct ArenaLayout {
     }
 };
 
+template <int G>
 __device__ __forceinline__ int block_sum(int v, int *red) {
 #pragma unroll
     for (int o = 32; o >= 1; o >>= 1) v += __shfl_xor(v, o, kWave);
@@ -1454,10 +1486,11 @@ __device__ __forceinline__ int block_sum(int v, int *red) {
     if ((threadIdx.x & 63) == 0) red[threadIdx.x >> 6] = v;
     __syncthreads();
     int s = 0;
-    for (int w = 0; w < kLargeThreads / kWave; w++) s += red[w];
+    for (int w = 0; w < G / kWave; w++) s += red[w];
     __syncthreads();
     return s;
 }
+template <int G>
 __device__ __forceinline__ int block_max(int v, int *red) {
 #pragma unroll
     for (int o = 32; o >= 1; o >>= 1) v = ::max(v, __shfl_xor(v, o, kWave));
@@ -1465,14 +1498,14 @@ __device__ __forceinline__ int block_max(int v, int *red) {
     if ((threadIdx.x & 63) == 0) red[threadIdx.x >> 6] = v;
     __syncthreads();
     int s = red[0];
-    for (int w = 1; w < kLargeThreads / kWave; w++) s = ::max(s, red[w]);
+    for (int w = 1; w < G / kWave; w++) s = ::max(s, red[w]);
     __syncthreads();
     return s;
 }
 
+template <int G>
 __device__ void process_large(const KParams &P, uint8_t *A, const int32_t *lr, const float *thr, uint4 ent, int *red,
                               int *s_cnt, int *s_lc, int *s_cur) {
-    constexpr int G = kLargeThreads;
     const int tt = threadIdx.x;
     const bsdc_family_batch &B = P.B;
     const uint32_t fam = ent.x, r0 = ent.y, img = ent.w;  // list entry: family, first record, n, image bytes
@@ -1490,8 +1523,8 @@ __device__ void process_large(const KParams &P, uint8_t *A, const int32_t *lr, c
         if (rc.w & BSDC_LINK_COMPLEX) c += (int)(B.cig_info[r0 + r] & 0xFFFF);
         ml = ::max(ml, (int)(rc.z & 0xFFFF));
     }
-    const int cops = block_sum(c, red);
-    const int maxlen_f = block_max(ml, red);
+    const int cops = block_sum<G>(c, red);
+    const int maxlen_f = block_max<G>(ml, red);
     const ArenaLayout Lo(n, 0, maxlen_f, cops);
     RecMeta *M = reinterpret_cast<RecMeta *>(A + Lo.meta);
     uint16_t *lists = reinterpret_cast<uint16_t *>(A + Lo.lists);
@@ -1729,7 +1762,7 @@ __device__ void process_large(const KParams &P, uint8_t *A, const int32_t *lr, c
     // A thread per R1 record finds its template's overlap.  Templates with simple cigars (and a
     // family without quals >= 128) run flattened over (template, 4 positions) through overlap4;
     // the rest take the per-position path, one wave per template.  Templates share no bytes.
-    const bool wild = block_max((qor & 0x80808080u) != 0 ? 1 : 0, red) != 0;
+    const bool wild = block_max<G>((qor & 0x80808080u) != 0 ? 1 : 0, red) != 0;
     if (stop == 11) return;
     if (P.overlap) {
         uint32_t *tl = reinterpret_cast<uint32_t *>(lists);  // fast: 3 words each from the front; slow: 1 from the back
@@ -1847,7 +1880,7 @@ __device__ void process_large(const KParams &P, uint8_t *A, const int32_t *lr, c
     // bound), then the two groups (X = AB-R1 + BA-R2, Y = AB-R2 + BA-R1) by one thread each.
     int hc = 0;
     for (int r = tt; r < n; r += G) hc |= (M[r].link & BSDC_LINK_COMPLEX) && M[r].set != 0xFF;
-    if (block_max(hc, red)) {
+    if (block_max<G>(hc, red)) {
         uint32_t *so = simp;
         uint32_t *sofs = simp + cops + 2 * n;
         uint16_t *srcl = reinterpret_cast<uint16_t *>(simp + cops + 3 * n);  // n u16 in the last n words
@@ -1911,6 +1944,7 @@ __device__ void process_large(const KParams &P, uint8_t *A, const int32_t *lr, c
         s_cnt[tt] = 0;
         s_lc[tt] = 0;
         s_cur[tt] = 0;
+        s_cur[4 + tt] = 0;
     }
     __syncthreads();
     for (int r = tt; r < n; r += G) {
@@ -1927,15 +1961,17 @@ __device__ void process_large(const KParams &P, uint8_t *A, const int32_t *lr, c
         soff[s] = o;
         o += cnt[s];
     }
-    for (int r = tt; r < n; r += G) {
+    for (int r = tt; r < n; r += G) {  // forward reads from the front of the set, reverse from the back
         const RecMeta &m = M[r];
         if (m.set == 0xFF) continue;
         const bool negr = m.flag & 16;
-        const int i = atomicAdd(&s_cur[m.set], 1);
+        const int i = negr ? cnt[m.set] - 1 - atomicAdd(&s_cur[4 + m.set], 1) : atomicAdd(&s_cur[m.set], 1);
         desc[soff[m.set] + i] = make_uint2(m.slot + (uint32_t)m.start + (negr ? (uint32_t)(m.len - 1) : 0u),
                                            (uint32_t)m.srclen | (negr ? 0x80000000u : 0u));
     }
     __syncthreads();
+    int nfw[4];
+    for (int s = 0; s < 4; s++) nfw[s] = s_cur[s];
     if (stop == 5) return;
 
     // ---- single-strand vote ----
@@ -1970,111 +2006,186 @@ __device__ void process_large(const KParams &P, uint8_t *A, const int32_t *lr, c
         ssb[s * ssw + col] = Q < 2 ? (uint8_t)kN : (uint8_t)(1u << best);
         ssq[s * ssw + col] = Q < 2 ? (uint8_t)2 : (uint8_t)Q;
     };
-    // one read's dword for columns c..c+3: its address and the mask of the columns it covers.  A
-    // read that ends before column c reads its first dword, all masked; a reverse read's dword may
-    // start up to 3 bytes before the image (arena bytes): signed offsets.
-    auto addr = [&](uint2 e, int c, uint32_t &keep) -> int32_t {
-        const int k8 = 8 * ((int)(e.y & 0x7FFFFFFFu) - c);
-        const bool rv = e.y >> 31;
-        keep = ~bytes_past(k8, rv);
-        const int cc = k8 > 0 ? c : 0;
-        return rv ? (int32_t)e.x - cc - 3 : (int32_t)e.x + cc;
-    };
-    auto fetch = [&](uint2 e, int c, uint32_t &b, uint32_t &q) {  // columns ascend, reverse complemented
-        uint32_t keep;
-        const int32_t a = addr(e, c, keep);
-        b = ldsu32(slots + a) & keep;
-        q = ldsu32(qimg + a);
-        if (e.y >> 31) {
-            b = comp4(__builtin_bswap32(b));
-            q = __builtin_bswap32(q);
-        } else {
-            b &= 0x0F0F0F0Fu;
-        }
-    };
-    constexpr int kSwarReads = 128;
-    int nt4[4], nt2[4];
-    for (int s = 0; s < 4; s++) {
-        nt4[s] = cnt[s] <= kSwarReads ? (lcv[s] + 3) >> 2 : 0;
-        nt2[s] = cnt[s] <= kSwarReads ? 0 : (lcv[s] + 1) >> 1;
-    }
-    const int ntask = nt4[0] + nt4[1] + nt4[2] + nt4[3];
-    for (int k = tt; k < ntask; k += G) {
-        int s = 0, c = k;
-        while (c >= nt4[s]) {
-            c -= nt4[s];
-            s++;
-        }
-        c *= 4;
-        int32_t d[4][4];
-#pragma unroll
-        for (int j = 0; j < 4; j++)
-#pragma unroll
-            for (int x = 0; x < 4; x++) d[j][x] = 0;
-        auto acc = [&](uint32_t b, uint32_t q) {
-#pragma unroll
-            for (int j = 0; j < 4; j++) {
-                const uint32_t bj = (b >> (8 * j)) & 0xFu;
-                const int32_t v = lr[(q >> (8 * j)) & 0xFFu];
-                d[j][0] += bj == kA ? v : 0;
-                d[j][1] += bj == kC ? v : 0;
-                d[j][2] += bj == kG ? v : 0;
-                d[j][3] += bj == kT ? v : 0;
-            }
-        };
-        const uint2 *dl = desc + soff[s];
-        const int na = cnt[s];
-        int i = 0;
-        for (; i + 1 < na; i += 2) {  // two reads' loads in flight together
-            uint32_t b0, q0, b1, q1;
-            fetch(dl[i], c, b0, q0);
-            fetch(dl[i + 1], c, b1, q1);
-            acc(b0, q0);
-            acc(b1, q1);
-        }
-        if (i < na) {
-            uint32_t b0, q0;
-            fetch(dl[i], c, b0, q0);
-            acc(b0, q0);
-        }
-#pragma unroll
-        for (int j = 0; j < 4; j++)
-            if (c + j < lcv[s]) resolve(s, c + j, d[j][0], d[j][1], d[j][2], d[j][3]);
-    }
-    const int ntask2 = nt2[0] + nt2[1] + nt2[2] + nt2[3];
-    for (int k = tt; k < ntask2; k += G) {
-        int s = 0, c = k;
-        while (c >= nt2[s]) {
-            c -= nt2[s];
-            s++;
-        }
-        c *= 2;
-        long long D[2][4] = {{0, 0, 0, 0}, {0, 0, 0, 0}};
-        const uint2 *dl = desc + soff[s];
-        for (int i0 = 0; i0 < cnt[s]; i0 += kSwarReads) {
-            int32_t d[2][4] = {{0, 0, 0, 0}, {0, 0, 0, 0}};
-            const int i1 = ::min(cnt[s], i0 + kSwarReads);
-            for (int i = i0; i < i1; i++) {
-                uint32_t b, q;
-                fetch(dl[i], c, b, q);
-#pragma unroll
-                for (int j = 0; j < 2; j++) {
-                    const uint32_t bj = (b >> (8 * j)) & 0xFu;
-                    const int32_t v = lr[(q >> (8 * j)) & 0xFFu];
-                    d[j][0] += bj == kA ? v : 0;
-                    d[j][1] += bj == kC ? v : 0;
-                    d[j][2] += bj == kG ? v : 0;
-                    d[j][3] += bj == kT ? v : 0;
+    // Wavefronts by set: wave w works on set w % 4; with 8 waves (512 threads) the two waves of a
+    // set split its reads (PARTS = 2).
+    // Pass A: a lane owns 4 columns and walks the wave's reads, forward ones then reverse ones,
+    // 4 in flight; descriptors are read 64 at a time, one per lane, and broadcast with v_readlane.
+    // Per column: one likelihood sum over the reads showing an A/C/G/T there (Tables zero / lr
+    // rows: a non-ACGT code adds 0) and the OR of the codes.  A column whose OR is one A/C/G/T
+    // code, with a sum above one unit per read (no near tie with the unseen bases' 0), is resolved
+    // from the sum alone: S = 3 e^-T, as the four-sum path computes it.  Every other column (a
+    // disagreement, an N or IUPAC code, a small or negative sum) is marked (ssq = 0).
+    // Pass B: the marked columns, 8 lanes each: the lanes split the reads, sum per base, reduce
+    // by lane shuffles, and the first lane makes the general call (resolve).
+    constexpr int NW = G / kWave, PARTS = NW >= 8 ? 2 : 1;
+    static_assert(NW == 4 * PARTS, "k_large: 4 or 8 wavefronts");
+    const int32_t *lr2 = lr - 256;  // TablesL: zero[256] then lr[256]
+    const int lane = tt & (kWave - 1), wv = tt >> 6, ws = wv & 3, wpart = wv >> 2;
+    int64_t *psum = reinterpret_cast<int64_t *>(A + Lo.meta);        // [4][ssw] part-1 sums (RecMeta is dead)
+    uint8_t *por = reinterpret_cast<uint8_t *>(psum + 4 * ssw);     // [4][ssw] part-1 ORs
+    {
+        const int na = cnt[ws], lc = lcv[ws], nf = nfw[ws];
+        const uint2 *dl = desc + soff[ws];
+        const int rb = wpart == 0 ? 0 : na / 2, re = PARTS == 1 || wpart == 1 ? na : na / 2;
+        const int lmax = ::max(::max(lcv[0], lcv[1]), ::max(lcv[2], lcv[3]));
+        for (int cb = 0; cb < lmax; cb += 4 * kWave) {  // the same trip count in every wave (barriers inside)
+            const int c = cb + 4 * lane, c8 = 8 * c;
+            long long T0 = 0, T1 = 0, T2 = 0, T3 = 0;
+            uint32_t orm = 0;
+            if (cb < lc) {
+                int32_t t0 = 0, t1 = 0, t2 = 0, t3 = 0;
+                auto fwd = [&](uint32_t ex, uint32_t ey) {
+                    const int sl = (int)ey;
+                    const uint32_t keep = ~bytes_past(8 * sl - c8, false);
+                    const int32_t a = (int32_t)ex + (sl > c ? c : 0);
+                    const uint32_t b = lds_any32(slots, a) & keep, q = lds_any32(qimg, a);
+                    orm |= b;
+                    lookup4v(lr2, onehot01(b), q, t0, t1, t2, t3);
+                };
+                auto rev = [&](uint32_t ex, uint32_t ey) {  // bytes run backwards from the read's last base
+                    const int sl = (int)(ey & 0x7FFFFFFFu);
+                    const uint32_t keep = ~bytes_past(8 * sl - c8, true);
+                    const int32_t a = (int32_t)ex - (sl > c ? c : 0) - 3;
+                    const uint32_t b = comp4(__builtin_bswap32(lds_any32(slots, a) & keep));
+                    const uint32_t q = __builtin_bswap32(lds_any32(qimg, a));
+                    orm |= b;
+                    lookup4v(lr2, onehot01(b), q, t0, t1, t2, t3);
+                };
+                auto flush = [&]() {  // int32 partials over <= 64 reads: exact
+                    T0 += t0;
+                    T1 += t1;
+                    T2 += t2;
+                    T3 += t3;
+                    t0 = t1 = t2 = t3 = 0;
+                };
+                const int fe = ::min(re, nf);
+                for (int r0 = rb; r0 < fe; r0 += kWave) {
+                    const uint2 dr = r0 + lane < fe ? dl[r0 + lane] : make_uint2(0u, 0u);
+                    const int nr = ::min(kWave, fe - r0);
+                    int i = 0;
+                    for (; i + 3 < nr; i += 4) {
+                        const uint32_t x0 = rlu(dr.x, i), y0 = rlu(dr.y, i), x1 = rlu(dr.x, i + 1), y1 = rlu(dr.y, i + 1);
+                        const uint32_t x2 = rlu(dr.x, i + 2), y2 = rlu(dr.y, i + 2), x3 = rlu(dr.x, i + 3), y3 = rlu(dr.y, i + 3);
+                        fwd(x0, y0);
+                        fwd(x1, y1);
+                        fwd(x2, y2);
+                        fwd(x3, y3);
+                    }
+                    for (; i < nr; i++) fwd(rlu(dr.x, i), rlu(dr.y, i));
+                    flush();
+                }
+                for (int r0 = ::max(rb, nf); r0 < re; r0 += kWave) {
+                    const uint2 dr = r0 + lane < re ? dl[r0 + lane] : make_uint2(0u, 0u);
+                    const int nr = ::min(kWave, re - r0);
+                    int i = 0;
+                    for (; i + 3 < nr; i += 4) {
+                        const uint32_t x0 = rlu(dr.x, i), y0 = rlu(dr.y, i), x1 = rlu(dr.x, i + 1), y1 = rlu(dr.y, i + 1);
+                        const uint32_t x2 = rlu(dr.x, i + 2), y2 = rlu(dr.y, i + 2), x3 = rlu(dr.x, i + 3), y3 = rlu(dr.y, i + 3);
+                        rev(x0, y0);
+                        rev(x1, y1);
+                        rev(x2, y2);
+                        rev(x3, y3);
+                    }
+                    for (; i < nr; i++) rev(rlu(dr.x, i), rlu(dr.y, i));
+                    flush();
                 }
             }
+            if (PARTS == 2) {
+                if (wpart == 1 && cb < lc) {
 #pragma unroll
-            for (int j = 0; j < 2; j++)
+                    for (int j = 0; j < 4; j++)
+                        if (c + j < lc) {
+                            psum[ws * ssw + c + j] = j == 0 ? T0 : j == 1 ? T1 : j == 2 ? T2 : T3;
+                            por[ws * ssw + c + j] = (uint8_t)(orm >> (8 * j));
+                        }
+                }
+                __syncthreads();
+            }
+            if (wpart == 0 && cb < lc) {
 #pragma unroll
-                for (int x = 0; x < 4; x++) D[j][x] += d[j][x];
+                for (int j = 0; j < 4; j++) {
+                    const int col = c + j;
+                    if (col >= lc) break;
+                    uint32_t ob = (orm >> (8 * j)) & 0xFFu;
+                    long long Tj = j == 0 ? T0 : j == 1 ? T1 : j == 2 ? T2 : T3;
+                    if (PARTS == 2) {
+                        Tj += psum[ws * ssw + col];
+                        ob |= por[ws * ssw + col];
+                    }
+                    if (ob != 0 && (ob & (ob - 1)) == 0 && Tj > na) {
+                        const float e = term(-Tj);
+                        const float S = ((0.0f + e) + e) + e;
+                        const int Q = phred_of(S, thr);
+                        ssb[ws * ssw + col] = Q < 2 ? (uint8_t)kN : (uint8_t)ob;
+                        ssq[ws * ssw + col] = Q < 2 ? (uint8_t)2 : (uint8_t)Q;
+                    } else {
+                        ssq[ws * ssw + col] = 0;
+                    }
+                }
+            }
+            if (PARTS == 2) __syncthreads();
         }
-#pragma unroll
-        for (int j = 0; j < 2; j++)
-            if (c + j < lcv[s]) resolve(s, c + j, D[j][0], D[j][1], D[j][2], D[j][3]);
+    }
+    __syncthreads();
+    if (stop == 6) return;
+    // Pass B.  The marked columns of each set are listed (ballot compaction; the list lives in the
+    // part-sum region, dead now), then lane j of a wave owns the set's j-th marked column (the two
+    // waves of a set take alternate blocks of 64) and walks all the set's reads, 4 in flight, with
+    // the descriptors broadcast as in pass A: four per-base sums, then the general call (resolve).
+    uint16_t *mlist = reinterpret_cast<uint16_t *>(psum);  // [4][ssw]
+    if (wpart == 0) {
+        const int lc = lcv[ws];
+        int nm = 0;
+        for (int cb = 0; cb < lc; cb += kWave) {
+            const int col = cb + lane;
+            const bool mk = col < lc && ssq[ws * ssw + col] == 0;
+            const uint64_t bal = ballot(mk);
+            if (mk) mlist[ws * ssw + nm + mbcnt(bal)] = (uint16_t)col;
+            nm += __builtin_popcountll(bal);
+        }
+        if (lane == 0) s_lc[ws] = nm;
+    }
+    __syncthreads();
+    {
+        const int s = ws, na = cnt[s], nm = s_lc[s];
+        const uint2 *dl = desc + soff[s];
+        for (int k0 = kWave * wpart; k0 < nm; k0 += kWave * PARTS) {
+            const bool act = k0 + lane < nm;
+            const int col = act ? mlist[s * ssw + k0 + lane] : 0;
+            long long D0 = 0, D1 = 0, D2 = 0, D3 = 0;
+            int32_t d0 = 0, d1 = 0, d2 = 0, d3 = 0;
+            auto one = [&](uint32_t ex, uint32_t ey) {
+                const int sl = (int)(ey & 0x7FFFFFFFu);
+                const bool rv = ey >> 31, in = col < sl;
+                const int32_t a = !in ? (int32_t)ex : rv ? (int32_t)ex - col : (int32_t)ex + col;
+                const uint32_t braw = slots[a] & 0x0Fu, bb = rv ? comp_nt16(braw) : braw;
+                const int32_t v = in ? lr[qimg[a]] : 0;
+                d0 += bb == kA ? v : 0;
+                d1 += bb == kC ? v : 0;
+                d2 += bb == kG ? v : 0;
+                d3 += bb == kT ? v : 0;
+            };
+            for (int r0 = 0; r0 < na; r0 += kWave) {
+                const uint2 dr = r0 + lane < na ? dl[r0 + lane] : make_uint2(0u, 0u);
+                const int nr = ::min(kWave, na - r0);
+                int i = 0;
+                for (; i + 3 < nr; i += 4) {
+                    const uint32_t x0 = rlu(dr.x, i), y0 = rlu(dr.y, i), x1 = rlu(dr.x, i + 1), y1 = rlu(dr.y, i + 1);
+                    const uint32_t x2 = rlu(dr.x, i + 2), y2 = rlu(dr.y, i + 2), x3 = rlu(dr.x, i + 3), y3 = rlu(dr.y, i + 3);
+                    one(x0, y0);
+                    one(x1, y1);
+                    one(x2, y2);
+                    one(x3, y3);
+                }
+                for (; i < nr; i++) one(rlu(dr.x, i), rlu(dr.y, i));
+                D0 += d0;  // int32 partials over <= 64 reads: exact
+                D1 += d1;
+                D2 += d2;
+                D3 += d3;
+                d0 = d1 = d2 = d3 = 0;
+            }
+            if (act) resolve(s, col, D0, D1, D2, D3);
+        }
     }
     __syncthreads();
     if (stop == 7) return;
@@ -2156,12 +2267,14 @@ struct TablesL {  // k_large's LDS copy: the prefix of Tables it reads
     uint8_t sq[144];
 };
 static_assert(sizeof(TablesL) == kTabBytesL, "TablesL image");
-template <bool IN_LDS>
-__global__ __launch_bounds__(kLargeThreads, 5) void k_large(KParams P, const uint4 *fams, int64_t nfams, int32_t arena) {
+// G = 256 threads for the buckets that fit 3 or more workgroups per CU, 512 for the LDS-heavy ones
+// (2 or 1 per CU, HBM scratch): twice the wavefronts in flight for the same LDS.
+template <bool IN_LDS, int G>
+__global__ __launch_bounds__(G, G == 256 ? 5 : 2) void k_large(KParams P, const uint4 *fams, int64_t nfams, int32_t arena) {
     extern __shared__ __attribute__((aligned(16))) uint8_t smem[];  // the family's arena (IN_LDS)
     __shared__ __attribute__((aligned(16))) TablesL s_tab;
-    __shared__ int red[kLargeThreads / kWave];
-    __shared__ int s_cnt[4], s_lc[4], s_cur[4];
+    __shared__ int red[G / kWave];
+    __shared__ int s_cnt[4], s_lc[4], s_cur[8];
     const TablesL *T = &s_tab;
     if (((P.mode >> BSDC_MODE_STOP_SHIFT) & 15) == 15) return;  // profiling: launch cost alone
     load_tables<kTabBytesL>(&P.tab->t, reinterpret_cast<uint8_t *>(&s_tab));
@@ -2171,7 +2284,7 @@ __global__ __launch_bounds__(kLargeThreads, 5) void k_large(KParams P, const uin
     const int64_t i = blockIdx.x;
     if (i >= nfams) return;
     uint8_t *A = IN_LDS ? smem : P.O.scratch + (size_t)i * (size_t)arena;
-    process_large(P, A, lr, thr, fams[i], red, s_cnt, s_lc, s_cur);
+    process_large<G>(P, A, lr, thr, fams[i], red, s_cnt, s_lc, s_cur);
 }
 
 }  // namespace
@@ -2471,10 +2584,13 @@ int32_t bsdc_run(bsdc_ctx *c, const bsdc_family_batch *b, bsdc_consensus *o, int
             const int64_t nf = b->n_large[q];
             const int32_t a = b->large_arena[q];
             if (nf > 0) {
-                if (a <= BSDC_LARGE_LDS_MAX)
-                    hipLaunchKernelGGL(k_large<true>, dim3((unsigned)nf), dim3(kLargeThreads), (size_t)a, s, P, f, nf, a);
+                const bool big = q >= kLargeBigBucket;  // 2 or 1 workgroups per CU, or HBM scratch
+                if (a <= BSDC_LARGE_LDS_MAX && !big)
+                    hipLaunchKernelGGL((k_large<true, kLargeThreads>), dim3((unsigned)nf), dim3(kLargeThreads), (size_t)a, s, P, f, nf, a);
+                else if (a <= BSDC_LARGE_LDS_MAX)
+                    hipLaunchKernelGGL((k_large<true, kLargeThreadsBig>), dim3((unsigned)nf), dim3(kLargeThreadsBig), (size_t)a, s, P, f, nf, a);
                 else
-                    hipLaunchKernelGGL(k_large<false>, dim3((unsigned)nf), dim3(kLargeThreads), 0, s, P, f, nf, a);
+                    hipLaunchKernelGGL((k_large<false, kLargeThreadsBig>), dim3((unsigned)nf), dim3(kLargeThreadsBig), 0, s, P, f, nf, a);
                 HIP_OK(c, hipGetLastError());
             }
             f += nf;

@@ -17,7 +17,8 @@ from bsseqconsensusreads_amd.device import Engine  # noqa: E402
 PHASES = [("launch", 15), ("tables", 14), ("staging", 1), ("convert", 2), ("extend", 3), ("overlap", 4), ("srcreads+lists", 5),
           ("vote-preamble", 6), ("vote-main", 7), ("vote-queue", 8), ("full", 0)]
 LARGE_PHASES = [("launch", 15), ("tables", 14), ("staging", 1), ("convert", 2), ("extend", 3), ("overlap-wild", 11),
-                ("overlap-templates", 12), ("overlap", 4), ("srcreads", 10), ("filter+lists", 5), ("vote", 7), ("full", 0)]
+                ("overlap-templates", 12), ("overlap", 4), ("srcreads", 10), ("filter+lists", 5), ("vote-sums", 6), ("vote", 7),
+                ("full", 0)]
 
 ap = argparse.ArgumentParser()
 ap.add_argument("--config", default="C2")
