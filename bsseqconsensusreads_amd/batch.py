@@ -407,7 +407,18 @@ def build_family_batch(raw: R.RawRecords, mode: str = "full", ref: Optional[R.Re
 
 def plan_families(raw: R.RawRecords, mode: str = "full", ref: Optional[R.Reference] = None,
                   family_order: str = "template-coordinate") -> FamilyPlan:
-    """Family formation of build_family_batch (see there), without the device arrays."""
+    """Family formation of build_family_batch (see there), without the device arrays: the C++
+    statement (hostplan, csrc/bsdc_host.cpp) for the step-5 modes, this module's numpy statement
+    (plan_families_py) for the tool-only modes or with BSDC_HOST_PLAN=numpy."""
+    from . import hostplan
+    if mode in ("full", "vote") and hostplan.enabled():
+        return hostplan.plan_families(raw, mode, ref, family_order)
+    return plan_families_py(raw, mode, ref, family_order)
+
+
+def plan_families_py(raw: R.RawRecords, mode: str = "full", ref: Optional[R.Reference] = None,
+                     family_order: str = "template-coordinate") -> FamilyPlan:
+    """The numpy statement of plan_families (every mode)."""
     if family_order not in ("template-coordinate", "mi-group"):
         raise ValueError(family_order)
     n = raw.n
@@ -591,7 +602,16 @@ def plan_families(raw: R.RawRecords, mode: str = "full", ref: Optional[R.Referen
 
 
 def materialize(plan: FamilyPlan, f0: int, f1: int, small_cap: int = SMALL_ARENA_CAP) -> FamilyBatch:
-    """The device batch of plan families [f0, f1) (family ids renumbered from 0)."""
+    """The device batch of plan families [f0, f1) (family ids renumbered from 0): C++ (hostplan)
+    for the step-5 modes, materialize_py otherwise."""
+    from . import hostplan
+    if plan.mode in ("full", "vote") and hostplan.enabled():
+        return hostplan.materialize(plan, f0, f1, small_cap)
+    return materialize_py(plan, f0, f1, small_cap)
+
+
+def materialize_py(plan: FamilyPlan, f0: int, f1: int, small_cap: int = SMALL_ARENA_CAP) -> FamilyBatch:
+    """The numpy statement of materialize (every mode)."""
     raw, mode, ref = plan.raw, plan.mode, plan.ref
     n = raw.n
     f = raw.flag.astype(np.int64)

@@ -31,6 +31,7 @@
 #include <string>
 
 #include "../../include/bsdc.h"
+#include "../../include/bsdc_layout.h"
 
 namespace {
 
@@ -53,7 +54,11 @@ constexpr int kLargeThreads = LARGE_THREADS;
 #define LARGE_THREADS_BIG 512  // k_large workgroup size of the LDS-heavy buckets
 #endif
 constexpr int kLargeThreadsBig = LARGE_THREADS_BIG;
-constexpr int kLargeBigBucket = 3;  // large buckets q >= this (2, 1 workgroups per CU, scratch) use kLargeThreadsBig
+constexpr int kLargeBigBucket = 3;
+#ifndef LARGE_VOTE_U
+#define LARGE_VOTE_U 4  // k_large vote pass A: reads in flight per lane
+#endif
+constexpr int kVoteU = LARGE_VOTE_U;  // large buckets q >= this (2, 1 workgroups per CU, scratch) use kLargeThreadsBig
 #ifndef LARGE_OVL_CHUNKS
 #define LARGE_OVL_CHUNKS 2  // k_large overlap: SWAR dwords (4 positions each) per task
 #endif
@@ -72,6 +77,7 @@ constexpr int kSqBuckets = 136;                 // phred buckets of S: 4 per oct
 constexpr int kSqBase = (127 - 32) << 2;         // (float bits >> 21) of 2^-32
 constexpr int kTabBytesL = 1024 + 1024 + 384 + 144;  // the prefix k_large uses (zero, lr, thr, sq)
 constexpr int kTabBytes = kTabBytesL + 2048 + 192;  // the Tables image in LDS
+constexpr int kArenaGuard = 16;  // k_small: LDS bytes before the first and after the last arena
 // k_small base bytes in LDS: nt16 code | 0x10 for A, C, G, T (set at staging, see unpack32)
 constexpr uint32_t kLinkRdDev = 1u << 27;       // device-internal: tool 1 trimmed a base (RD=1)
 
@@ -94,8 +100,10 @@ struct DevTables {
     int32_t r40[256];
 };
 
-__host__ __device__ inline int64_t round16(int64_t x) { return (x + 15) & ~int64_t(15); }
-__host__ __device__ inline int ref_chunks(int max_len) { return (15 + (max_len + 4) / 2 + 15) / 16; }
+using bsdc_layout::ArenaLayout;
+using bsdc_layout::ref_chunks;
+using bsdc_layout::round16;
+using bsdc_layout::SmallLayout;
 
 // ------------------------------------------------------------------------------------------
 // shared device helpers
@@ -494,45 +502,6 @@ __device__ __forceinline__ void duplex_col(uint32_t xb, uint32_t xq, uint32_t yb
 // ==========================================================================================
 // k_small: one wavefront per family, everything in LDS
 // ==========================================================================================
-// Arena of one small family.  Regions live only as long as their phase and share space:
-//   bimg, qimg  the family image, bases / quals (whole kernel)
-//   lists       reference-window starts (staging) -> read descriptors (vote), 4 B per record
-//   misc        consensus lengths lc[4], converted record -> lane
-//   R           reference windows (staging, convert) | alignment-filter scratch (source reads) |
-//               duplex rows + queued columns (vote)
-struct SmallLayout {
-    uint32_t bimg, qimg, lists, misc, ref, meta, setv, ordv, srcl, simp, outb, outq, squeue, total;
-    int32_t ws, ow;
-    __host__ __device__ SmallLayout(int n, int64_t img, int nconv, int64_t cops, int max_len) {
-        ws = 32 * ref_chunks(max_len);
-        ow = (int32_t)round16(max_len + 2);
-        int64_t o = 0;
-        bimg = (uint32_t)o;
-        o += img;
-        qimg = (uint32_t)o;
-        o += img;
-        lists = (uint32_t)o;
-        o += round16(4 * (int64_t)n);
-        misc = (uint32_t)o;  // lc[4] u32, then the lane of each converted record (u8)
-        o += 16 + round16(n);
-        const int64_t R = o;
-        ref = (uint32_t)R;
-        const int64_t e_ref = R + (int64_t)nconv * ws;
-        meta = (uint32_t)R;  // SMeta per record
-        setv = meta + (uint32_t)round16(16 * (int64_t)n);
-        ordv = setv + (uint32_t)round16(n);
-        srcl = ordv + (uint32_t)round16(2 * (int64_t)n);
-        simp = srcl + (uint32_t)round16(2 * (int64_t)n);
-        const int64_t e_f = (int64_t)simp + (cops > 0 ? round16(4 * (cops + 4 * (int64_t)n)) : 0);
-        outb = (uint32_t)R;  // duplex bases, 2 ends
-        outq = (uint32_t)(R + 2 * (int64_t)ow);
-        squeue = (uint32_t)(R + 4 * (int64_t)ow);  // queued (end, column), u16
-        const int64_t e_v = R + 8 * (int64_t)ow;
-        int64_t e = e_ref > e_f ? e_ref : e_f;
-        total = (uint32_t)(e > e_v ? e : e_v);
-    }
-};
-
 struct SMeta {  // 16 B, LDS copy of a record's registers (only for the rare serial path)
     uint32_t gidx;
     int32_t pos;
@@ -588,9 +557,9 @@ __device__ __forceinline__ Ovl4 ovl4_load(const uint8_t *bimg, const uint8_t *qi
     return Ovl4{lds_any32(bimg, (int32_t)ia), lds_any32(bimg, (int32_t)ib), lds_any32(qimg, (int32_t)ia),
                 lds_any32(qimg, (int32_t)ib)};
 }
-__device__ __forceinline__ Ovl4 ovl4_compute(const Ovl4 &in4, int rem) {
+// (`in`: 0xFF in the bytes inside the overlap)
+__device__ __forceinline__ Ovl4 ovl4_compute_m(const Ovl4 &in4, uint32_t in) {
     const uint32_t X = in4.x, Y = in4.y, QA = in4.qa, QB = in4.qb;
-    const uint32_t in = rem >= 4 ? 0xFFFFFFFFu : (1u << (8 * rem)) - 1u;
     const uint32_t act = expand80(~(zero80(X ^ 0x0F0F0F0Fu) | zero80(Y ^ 0x0F0F0F0Fu)) & 0x80808080u) & in;
     const uint32_t eq = expand80(zero80(X ^ Y));
     const uint32_t ge = expand80(((QA | 0x80808080u) - QB) & 0x80808080u);  // qa >= qb
@@ -606,6 +575,50 @@ __device__ __forceinline__ Ovl4 ovl4_compute(const Ovl4 &in4, int rem) {
     const uint32_t ox = (nx & act) | (X & ~act), oy = (ny & act) | (Y & ~act);
     const uint32_t oqa = (nq & act) | (QA & ~act), oqb = (nq & act) | (QB & ~act);
     return Ovl4{ox, oy, oqa, oqb};
+}
+__device__ __forceinline__ Ovl4 ovl4_compute(const Ovl4 &in4, int rem) {
+    return ovl4_compute_m(in4, rem >= 4 ? 0xFFFFFFFFu : (1u << (8 * rem)) - 1u);
+}
+// One dword of a template's overlap, aligned to mate a: dword d of a's bytes from (xa & ~3)
+// holds overlap positions 4d - (xa & 3) .. + 3 (the overlap is ovl positions from xa in a and xb
+// in b).  a's bases and quals are loaded as aligned dwords (and stored so when the dword lies
+// inside the overlap); b's come from two aligned loads each and go back byte by byte, only inside
+// the overlap (a dword store when b is aligned too and the dword is whole): gfx950 stalls unaligned LDS accesses.
+__device__ __forceinline__ void overlap_dw(uint8_t *bimg, uint8_t *qimg, uint32_t xa, uint32_t xb, int ovl, int d) {
+    const int p0 = 4 * d - (int)(xa & 3u);
+    const uint32_t A0 = (xa & ~3u) + 4u * (uint32_t)d;
+    const int32_t B0 = (int32_t)xb + p0;
+    const int lo = ::max(-p0, 0), hi = ::min(ovl - p0, 4);
+    if (hi <= lo) return;
+    const uint32_t inm = (0xFFFFFFFFu >> (32 - 8 * (hi - lo))) << (8 * lo);
+    // b's bytes from its first overlap byte B0 + lo, moved up to byte lo with zeros below: B0 itself
+    // may lie before the image, and a byte from there (>= 128: not a qual) would borrow into the
+    // next byte in the SWAR qual compare
+    const int32_t Bl = B0 + lo;
+    const uint32_t sh = 8u * (uint32_t)lo;
+    const Ovl4 o = ovl4_compute_m(
+        Ovl4{lds32(bimg + A0), lds_any32(bimg, Bl) << sh, lds32(qimg + A0), lds_any32(qimg, Bl) << sh}, inm);
+    // a partial dword of a goes back byte by byte too: its other bytes may belong to the record
+    // before a (an extended record starts one byte before its slot), which another template's
+    // lanes may be writing in the same instruction
+    const bool whole = inm == 0xFFFFFFFFu;
+    if (whole) {
+        st32(bimg + A0, o.x);
+        st32(qimg + A0, o.qa);
+    }
+    if (whole && (B0 & 3) == 0) {
+        st32(bimg + B0, o.y);
+        st32(qimg + B0, o.qb);
+    } else {
+        for (int k = lo; k < hi; k++) {
+            if (!whole) {
+                bimg[A0 + k] = (uint8_t)(o.x >> (8 * k));
+                qimg[A0 + k] = (uint8_t)(o.qa >> (8 * k));
+            }
+            bimg[B0 + k] = (uint8_t)(o.y >> (8 * k));
+            qimg[B0 + k] = (uint8_t)(o.qb >> (8 * k));
+        }
+    }
 }
 __device__ __forceinline__ void ovl4_store(uint8_t *bimg, uint8_t *qimg, uint32_t ia, uint32_t ib, int rem, const Ovl4 &o) {
     if (rem >= 4) {
@@ -754,7 +767,9 @@ __global__ __launch_bounds__(kWave *kSmallMaxWaves, kSmallMinWaves) __attribute_
     const int t = threadIdx.x & 63;
     const int64_t fi = (int64_t)blockIdx.x * (blockDim.x >> 6) + w;
     if (fi >= nfams) return;
-    uint8_t *A = smem + (size_t)w * (size_t)arena;
+    // (the arenas start kArenaGuard bytes into smem: a dword load that straddles the start of a
+    // family image -- its bytes before the image masked -- stays inside the allocation)
+    uint8_t *A = smem + kArenaGuard + (size_t)w * (size_t)arena;
     const bsdc_family_batch &B = P.B;
     const bool do_convert = P.mode & BSDC_MODE_CONVERT;
     const bool do_extend = P.mode & BSDC_MODE_EXTEND;
@@ -803,9 +818,18 @@ __global__ __launch_bounds__(kWave *kSmallMaxWaves, kSmallMinWaves) __attribute_
         if (k >= nqc && k < nch)
             unpack32<true>(v, bimg + 32 * (k - nqc));
     };
+    // lanes take qual chunks and packed-base chunks in separate rounds (the unpack runs once per
+    // round of base chunks instead of in every round where some lane has one): chunk k of round u
+    // is qual chunk t + 64 u for u < uq, packed-base chunk t + 64 (u - uq) after
+    const int uq = (nqc + 63) >> 6;
+    auto kmap = [&](int u) {
+        if (u < uq) return t + 64 * u < nqc ? t + 64 * u : nch;
+        const int kb = t + 64 * (u - uq);
+        return kb < nch - nqc ? nqc + kb : nch;
+    };
     uint4 v[kStageU];
 #pragma unroll
-    for (int u = 0; u < kStageU; u++) v[u] = load_img(t + 64 * u);
+    for (int u = 0; u < kStageU; u++) v[u] = load_img(kmap(u));
 
     const uint32_t gslot = rc.x;
     int32_t pos = (int32_t)rc.y;
@@ -856,12 +880,13 @@ __global__ __launch_bounds__(kWave *kSmallMaxWaves, kSmallMinWaves) __attribute_
 #pragma unroll
     for (int u = 0; u < 2; u++) wv[u] = load_win(t + 64 * u);
 #pragma unroll
-    for (int u = 0; u < kStageU; u++) store_img(t + 64 * u, v[u]);
-    for (int k0 = 64 * kStageU; k0 < nch; k0 += 64 * kStageU) {  // families with more image chunks
+    for (int u = 0; u < kStageU; u++) store_img(kmap(u), v[u]);
+    const int ub = (nch - nqc + 63) >> 6;  // rounds of base chunks
+    for (int u0 = kStageU; u0 < uq + ub; u0 += kStageU) {  // families with more image chunks
 #pragma unroll
-        for (int u = 0; u < kStageU; u++) v[u] = load_img(k0 + t + 64 * u);
+        for (int u = 0; u < kStageU; u++) v[u] = load_img(kmap(u0 + u));
 #pragma unroll
-        for (int u = 0; u < kStageU; u++) store_img(k0 + t + 64 * u, v[u]);
+        for (int u = 0; u < kStageU; u++) store_img(kmap(u0 + u), v[u]);
     }
 #pragma unroll
     for (int u = 0; u < 2; u++) store_win(t + 64 * u, wv[u]);
@@ -1072,7 +1097,8 @@ __global__ __launch_bounds__(kWave *kSmallMaxWaves, kSmallMinWaves) __attribute_
                 if (g < nt) {
                     const uint32_t xa = tinfo[3 * g], xb = tinfo[3 * g + 1];
                     const int ovl = (int)tinfo[3 * g + 2];
-                    for (int j = 4 * (t & 15); j < ovl; j += 64) overlap4(bimg, qimg, xa + (uint32_t)j, xb + (uint32_t)j, ovl - j);
+                    const int nd = ((int)(xa & 3u) + ovl + 3) >> 2;
+                    for (int d = t & 15; d < nd; d += 16) overlap_dw(bimg, qimg, xa, xb, ovl, d);
                 }
             }
         }
@@ -1452,31 +1478,8 @@ struct RecMeta {  // 48 B, one per record of the family, in the arena
     uint8_t set;     // 0 AB-R1, 1 AB-R2, 2 BA-R1, 3 BA-R2, 0xFF none
     int32_t in_len;
 };
-static_assert(sizeof(RecMeta) == 48, "RecMeta layout");
+static_assert(sizeof(RecMeta) == bsdc_layout::kRecMetaBytes, "RecMeta layout");
 
-// Arena layout of one large family (offsets from the arena base).
-struct ArenaLayout {
-    uint32_t meta, lists, ssb, ssq, simp, slots, total;
-    int32_t ssw;
-    __host__ __device__ ArenaLayout(int n, int64_t slot_bytes, int max_len, int64_t complex_ops) {
-        ssw = (int32_t)round16(max_len + 2);
-        int64_t o = 0;
-        meta = (uint32_t)o;  // RecMeta per record; in the vote (RecMeta dead) the second wave part's sums
-        const int64_t mb = round16((int64_t)n * (int64_t)sizeof(RecMeta)), vb = 36 * (int64_t)ssw;
-        o += mb > vb ? mb : vb;
-        lists = (uint32_t)o;
-        o += round16((int64_t)n * 8);
-        ssb = (uint32_t)o;
-        o += 4 * (int64_t)ssw;
-        ssq = (uint32_t)o;
-        o += 4 * (int64_t)ssw;
-        simp = (uint32_t)o;
-        if (complex_ops > 0) o += round16(4 * (complex_ops + 4 * (int64_t)n));
-        slots = (uint32_t)o;
-        o += round16(slot_bytes);
-        total = (uint32_t)o;
-    }
-};
 
 template <int G>
 __device__ __forceinline__ int block_sum(int v, int *red) {
@@ -1795,18 +1798,14 @@ __device__ void process_large(const KParams &P, uint8_t *A, const int32_t *lr, c
         const int nfast = s_cnt[0], nslow = s_cnt[1];
         // a task is 4 * kOvlChunks positions of one template (kOvlChunks SWAR dwords): the task ->
         // template map, the entry loads and the address math are paid once per task
-        const int SDo = (maxlen_f + 2 + 4 * kOvlChunks - 1) / (4 * kOvlChunks);  // tasks of the longest overlap
+        // aligned on mate a: the longest overlap spans (maxlen + 2 + 3) / 4 + 1 dwords of a
+        const int SDo = ((maxlen_f + 2 + 3) / 4 + 1 + kOvlChunks - 1) / kOvlChunks;  // tasks of the longest overlap
         for (int k = tt; k < nfast * SDo; k += G) {
-            const int g = k / SDo, j = 4 * kOvlChunks * (k - g * SDo);
-            const int rem = (int)tl[3 * g + 2] - j;
-            const uint32_t ia = tl[3 * g] + (uint32_t)j, ib = tl[3 * g + 1] + (uint32_t)j;
-            Ovl4 o[kOvlChunks];
+            const int g = k / SDo, d0 = kOvlChunks * (k - g * SDo);
+            const uint32_t xa = tl[3 * g], xb = tl[3 * g + 1];
+            const int ovl = (int)tl[3 * g + 2];
 #pragma unroll
-            for (int c = 0; c < kOvlChunks; c++)
-                if (rem > 4 * c) o[c] = ovl4_load(slots, qimg, ia + 4 * c, ib + 4 * c);
-#pragma unroll
-            for (int c = 0; c < kOvlChunks; c++)
-                if (rem > 4 * c) ovl4_store(slots, qimg, ia + 4 * c, ib + 4 * c, rem - 4 * c, ovl4_compute(o[c], rem - 4 * c));
+            for (int c = 0; c < kOvlChunks; c++) overlap_dw(slots, qimg, xa, xb, ovl, d0 + c);
         }
         for (int i = tt >> 6; i < nslow; i += G / kWave) {
             const int r = (int)tl[2 * n - 1 - i];
@@ -2063,13 +2062,9 @@ __device__ void process_large(const KParams &P, uint8_t *A, const int32_t *lr, c
                     const uint2 dr = r0 + lane < fe ? dl[r0 + lane] : make_uint2(0u, 0u);
                     const int nr = ::min(kWave, fe - r0);
                     int i = 0;
-                    for (; i + 3 < nr; i += 4) {
-                        const uint32_t x0 = rlu(dr.x, i), y0 = rlu(dr.y, i), x1 = rlu(dr.x, i + 1), y1 = rlu(dr.y, i + 1);
-                        const uint32_t x2 = rlu(dr.x, i + 2), y2 = rlu(dr.y, i + 2), x3 = rlu(dr.x, i + 3), y3 = rlu(dr.y, i + 3);
-                        fwd(x0, y0);
-                        fwd(x1, y1);
-                        fwd(x2, y2);
-                        fwd(x3, y3);
+                    for (; i + kVoteU - 1 < nr; i += kVoteU) {  // kVoteU reads' loads in flight
+#pragma unroll
+                        for (int u = 0; u < kVoteU; u++) fwd(rlu(dr.x, i + u), rlu(dr.y, i + u));
                     }
                     for (; i < nr; i++) fwd(rlu(dr.x, i), rlu(dr.y, i));
                     flush();
@@ -2078,13 +2073,9 @@ __device__ void process_large(const KParams &P, uint8_t *A, const int32_t *lr, c
                     const uint2 dr = r0 + lane < re ? dl[r0 + lane] : make_uint2(0u, 0u);
                     const int nr = ::min(kWave, re - r0);
                     int i = 0;
-                    for (; i + 3 < nr; i += 4) {
-                        const uint32_t x0 = rlu(dr.x, i), y0 = rlu(dr.y, i), x1 = rlu(dr.x, i + 1), y1 = rlu(dr.y, i + 1);
-                        const uint32_t x2 = rlu(dr.x, i + 2), y2 = rlu(dr.y, i + 2), x3 = rlu(dr.x, i + 3), y3 = rlu(dr.y, i + 3);
-                        rev(x0, y0);
-                        rev(x1, y1);
-                        rev(x2, y2);
-                        rev(x3, y3);
+                    for (; i + kVoteU - 1 < nr; i += kVoteU) {  // kVoteU reads' loads in flight
+#pragma unroll
+                        for (int u = 0; u < kVoteU; u++) rev(rlu(dr.x, i + u), rlu(dr.y, i + u));
                     }
                     for (; i < nr; i++) rev(rlu(dr.x, i), rlu(dr.y, i));
                     flush();
@@ -2169,13 +2160,9 @@ __device__ void process_large(const KParams &P, uint8_t *A, const int32_t *lr, c
                 const uint2 dr = r0 + lane < na ? dl[r0 + lane] : make_uint2(0u, 0u);
                 const int nr = ::min(kWave, na - r0);
                 int i = 0;
-                for (; i + 3 < nr; i += 4) {
-                    const uint32_t x0 = rlu(dr.x, i), y0 = rlu(dr.y, i), x1 = rlu(dr.x, i + 1), y1 = rlu(dr.y, i + 1);
-                    const uint32_t x2 = rlu(dr.x, i + 2), y2 = rlu(dr.y, i + 2), x3 = rlu(dr.x, i + 3), y3 = rlu(dr.y, i + 3);
-                    one(x0, y0);
-                    one(x1, y1);
-                    one(x2, y2);
-                    one(x3, y3);
+                for (; i + 7 < nr; i += 8) {  // 8 reads' loads in flight
+#pragma unroll
+                    for (int u = 0; u < 8; u++) one(rlu(dr.x, i + u), rlu(dr.y, i + u));
                 }
                 for (; i < nr; i++) one(rlu(dr.x, i), rlu(dr.y, i));
                 D0 += d0;  // int32 partials over <= 64 reads: exact
@@ -2523,7 +2510,7 @@ int32_t bsdc_run(bsdc_ctx *c, const bsdc_family_batch *b, bsdc_consensus *o, int
     }
     for (int q = 0; q < BSDC_SMALL_BUCKETS; q++) {
         if (b->n_small[q] > 0 &&
-            (b->small_arena[q] % 16 || b->small_arena[q] <= 0 || (size_t)kTabBytes + (size_t)b->small_arena[q] > kLdsBytes)) {
+            (b->small_arena[q] % 16 || b->small_arena[q] <= 0 || (size_t)kTabBytes + 2 * (size_t)kArenaGuard + (size_t)b->small_arena[q] > kLdsBytes)) {
             c->err = "bad small arena size";
             return BSDC_EINVAL;
         }
@@ -2561,10 +2548,11 @@ int32_t bsdc_run(bsdc_ctx *c, const bsdc_family_batch *b, bsdc_consensus *o, int
                 // keeps more wavefronts resident per CU; the smaller on a tie
                 // (a workgroup's wavefronts spread over the 4 SIMDs: at most kSmallSimdWaves each)
                 const int64_t a = b->small_arena[q];
-                const int64_t w4 = 4 * std::min<int64_t>(kSmallSimdWaves, kLdsBytes / (kTabBytes + 4 * a));
-                const int64_t w8 = 8 * std::min<int64_t>(kSmallSimdWaves / 2, kLdsBytes / (kTabBytes + 8 * a));
+                const int64_t g2 = 2 * kArenaGuard;
+                const int64_t w4 = 4 * std::min<int64_t>(kSmallSimdWaves, kLdsBytes / (kTabBytes + g2 + 4 * a));
+                const int64_t w8 = 8 * std::min<int64_t>(kSmallSimdWaves / 2, kLdsBytes / (kTabBytes + g2 + 8 * a));
                 const int nw = w8 > w4 ? 8 : 4;
-                const size_t lds = (size_t)nw * (size_t)b->small_arena[q];  // + the static tables
+                const size_t lds = (size_t)nw * (size_t)b->small_arena[q] + (size_t)g2;  // + the static tables
                 const int64_t blocks = (nf + nw - 1) / nw;
                 if (mode & BSDC_MODE_TAGS)
                     hipLaunchKernelGGL(k_small<true>, dim3((unsigned)blocks), dim3(kWave * nw), lds, s, P, f, nf,

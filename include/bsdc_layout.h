@@ -1,0 +1,85 @@
+/* bsdc_layout.h -- LDS arena layouts of the two family kernels, shared by the HIP kernels
+ * (csrc/bsdc_kernels.hip) and the host batch builder (csrc/bsdc_host.cpp), so that the arena a
+ * bucket reserves and the arena a kernel carves are one formula.  Not part of the C-ABI. */
+#ifndef BSDC_LAYOUT_H
+#define BSDC_LAYOUT_H
+#include <stdint.h>
+
+#if defined(__HIPCC__)
+#define BSDC_HD __host__ __device__
+#else
+#define BSDC_HD
+#endif
+
+namespace bsdc_layout {
+
+BSDC_HD inline int64_t round16(int64_t x) { return (x + 15) & ~int64_t(15); }
+// 16-B chunks that cover one converted record's packed reference window
+BSDC_HD inline int ref_chunks(int max_len) { return (15 + (max_len + 4) / 2 + 15) / 16; }
+constexpr int kRecMetaBytes = 48;  // k_large's per-record metadata (RecMeta)
+
+// Arena of one small family.  Regions live only as long as their phase and share space:
+//   bimg, qimg  the family image, bases / quals (whole kernel)
+//   lists       reference-window starts (staging) -> read descriptors (vote), 4 B per record
+//   misc        consensus lengths lc[4], converted record -> lane
+//   R           reference windows (staging, convert) | alignment-filter scratch (source reads) |
+//               duplex rows + queued columns (vote)
+struct SmallLayout {
+    uint32_t bimg, qimg, lists, misc, ref, meta, setv, ordv, srcl, simp, outb, outq, squeue, total;
+    int32_t ws, ow;
+    BSDC_HD SmallLayout(int n, int64_t img, int nconv, int64_t cops, int max_len) {
+        ws = 32 * ref_chunks(max_len);
+        ow = (int32_t)round16(max_len + 2);
+        int64_t o = 0;
+        bimg = (uint32_t)o;
+        o += img;
+        qimg = (uint32_t)o;
+        o += img;
+        lists = (uint32_t)o;
+        o += round16(4 * (int64_t)n);
+        misc = (uint32_t)o;  // lc[4] u32, then the lane of each converted record (u8)
+        o += 16 + round16(n);
+        const int64_t R = o;
+        ref = (uint32_t)R;
+        const int64_t e_ref = R + (int64_t)nconv * ws;
+        meta = (uint32_t)R;  // SMeta per record
+        setv = meta + (uint32_t)round16(16 * (int64_t)n);
+        ordv = setv + (uint32_t)round16(n);
+        srcl = ordv + (uint32_t)round16(2 * (int64_t)n);
+        simp = srcl + (uint32_t)round16(2 * (int64_t)n);
+        const int64_t e_f = (int64_t)simp + (cops > 0 ? round16(4 * (cops + 4 * (int64_t)n)) : 0);
+        outb = (uint32_t)R;  // duplex bases, 2 ends
+        outq = (uint32_t)(R + 2 * (int64_t)ow);
+        squeue = (uint32_t)(R + 4 * (int64_t)ow);  // queued (end, column), u16
+        const int64_t e_v = R + 8 * (int64_t)ow;
+        int64_t e = e_ref > e_f ? e_ref : e_f;
+        total = (uint32_t)(e > e_v ? e : e_v);
+    }
+};
+
+// Arena layout of one large family (offsets from the arena base).
+struct ArenaLayout {
+    uint32_t meta, lists, ssb, ssq, simp, slots, total;
+    int32_t ssw;
+    BSDC_HD ArenaLayout(int n, int64_t slot_bytes, int max_len, int64_t complex_ops) {
+        ssw = (int32_t)round16(max_len + 2);
+        int64_t o = 0;
+        meta = (uint32_t)o;  // RecMeta per record; in the vote (RecMeta dead) the second wave part's sums
+        const int64_t mb = round16((int64_t)n * (int64_t)kRecMetaBytes), vb = 36 * (int64_t)ssw;
+        o += mb > vb ? mb : vb;
+        lists = (uint32_t)o;
+        o += round16((int64_t)n * 8);
+        ssb = (uint32_t)o;
+        o += 4 * (int64_t)ssw;
+        ssq = (uint32_t)o;
+        o += 4 * (int64_t)ssw;
+        simp = (uint32_t)o;
+        if (complex_ops > 0) o += round16(4 * (complex_ops + 4 * (int64_t)n));
+        slots = (uint32_t)o;
+        o += round16(slot_bytes);
+        total = (uint32_t)o;
+    }
+};
+
+}  // namespace bsdc_layout
+#endif

@@ -2,7 +2,8 @@
 # Host sanitizer run ("ASan/UBSan on host C++"): the host codec libbsdc_io
 # (BGZF/BAM parsing of untrusted bytes, include/bsdc_io.h) and the oracle/ restatement rebuilt
 # with -fsanitize=address,undefined, then the CPU tests that drive them -- round trips, corrupt,
-# truncated and malformed BAMs (tests/test_bam.py), family formation (tests/test_families.py),
+# truncated and malformed BAMs (tests/test_bam.py), family formation (tests/test_families.py, and
+# the C++ family formation bsdc_host.cpp against its numpy statement, tests/test_host_plan.py),
 # the golden fixtures (tests/test_oracle_golden.py) -- loaded against the instrumented builds.
 # CPU only (GPU sanitizers are not available on the MI355X pool).  Usage: tests/sanitize/run.sh
 set -euo pipefail
@@ -11,7 +12,7 @@ OUT="$ROOT/build/sanitize"
 mkdir -p "$OUT"
 SAN="-fsanitize=address,undefined -fno-sanitize-recover=undefined -fno-omit-frame-pointer -g -O1"
 g++ -std=c++17 -fopenmp -fPIC -shared -Wall $SAN -o "$OUT/libbsdc_io.so" \
-    "$ROOT/bsseqconsensusreads_amd/csrc/bsdc_io.cpp" -lz
+    "$ROOT/bsseqconsensusreads_amd/csrc/bsdc_io.cpp" "$ROOT/bsseqconsensusreads_amd/csrc/bsdc_host.cpp" -lz
 gcc -fopenmp -fPIC -shared -ffp-contract=off -Wall $SAN -o "$OUT/liboracle.so" "$ROOT/oracle/bsdc_oracle.c" -lm
 # python itself is not instrumented: the runtimes go in first; leak checking is off (the
 # interpreter keeps its arenas to exit)
@@ -29,4 +30,5 @@ maps = open('/proc/self/maps').read()
 assert '$OUT/libbsdc_io.so' in maps and '$OUT/liboracle.so' in maps, 'instrumented libraries not loaded'
 print('sanitizer builds loaded:', '$OUT')
 "
-python -m pytest -q -p no:cacheprovider tests/test_bam.py tests/test_families.py tests/test_oracle_golden.py "$@"
+python -m pytest -q -p no:cacheprovider tests/test_bam.py tests/test_families.py tests/test_oracle_golden.py \
+    tests/test_host_plan.py "$@"
