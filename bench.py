@@ -85,6 +85,7 @@ class Resident:
         self.small = fb.small_fams.astype(np.int64)
         self.n_large = int(fb.large_fams.shape[0])
         self.n_disp = sum(1 for b in fb.small_buckets if b.shape[0])  # one k_small dispatch per LDS bucket
+        self.n_disp_large = sum(1 for b in fb.large_buckets if b.shape[0])  # one k_large dispatch per bucket
         self.molecules = int(np.unique(fb.fam_mi).shape[0])
         self.n_fam, self.n_rec, self.n_bases = fb.n_fam, fb.n_rec, fb.n_bases
         self.db.release_host()
@@ -181,29 +182,35 @@ def run(args):
         per = r.in_bytes + family_output_bytes(ln, st)
         bytes_small += int(per[r.small].sum())
         bytes_all += int(per.sum())
-    achieved = bytes_small / t_small / 1e9
-    # HBM bytes of one k_small launch set (one dispatch per non-empty LDS bucket), from the PMC
+    # the dominant kernel: the one that takes longer per step (k_small on C0-C2, k_large on C3)
+    bytes_large = bytes_all - bytes_small
+    dom_large = t_large > t_small
+    kname = "k_large" if dom_large else "k_small"
+    t_dom, b_dom = (t_large, bytes_large) if dom_large else (t_small, bytes_small)
+    n_disp_dom = sum(r.n_disp_large for r in res) if dom_large else n_disp
+    achieved = b_dom / t_dom / 1e9
+    # HBM bytes of one launch set of that kernel (one dispatch per non-empty bucket), from the PMC
     # passes of profiles/collect_pmc.sh on this same workload (FETCH_SIZE x2 + WRITE_SIZE,
     # MI355X_MICROARCH.md HBM section); null when no summary for this config is committed
     traffic = None
     issue = None
     pmc = os.path.join(ROOT, "profiles", "pmc_%s.json" % args.config)
-    if os.path.exists(pmc) and args.families == 1_000_000 and args.seed == 42:
+    if os.path.exists(pmc) and args.families == DEFAULT_FAMILIES.get(args.config, 1_000_000) and args.seed == 42:
         with open(pmc) as fh:
-            kd = json.load(fh).get("k_small", {})
+            kd = json.load(fh).get(kname, {})
         per = kd.get("hbm_bytes_per_dispatch")
         if per is not None:
-            traffic = int(per * n_disp)
+            traffic = int(per * n_disp_dom)
         # the bound that actually binds: VALU issue.  A wave64 VALU instruction takes 2 cycles of
         # its SIMD (MI355X_MICROARCH.md), 1024 SIMDs at 2.4 GHz; instructions per launch from the
         # same PMC passes (SQ_INSTS_VALU is per wave-instruction)
         valu = kd.get("mean_per_dispatch", {}).get("SQ_INSTS_VALU")
         if valu is not None:
-            v_launch = valu * n_disp
-            n_small = sum(int(r.small.size) for r in res)
-            issue = {"valu_insts_per_family": round(v_launch / max(n_small, 1), 1),
+            v_launch = valu * n_disp_dom
+            n_k = sum(r.n_large if dom_large else int(r.small.size) for r in res)
+            issue = {"valu_insts_per_family": round(v_launch / max(n_k, 1), 1),
                      "valu_issue_floor_ms": round(v_launch * 2 / (1024 * 2.4e9) * 1e3, 4),
-                     "valu_issue_frac": round(v_launch * 2 / (1024 * 2.4e9) / t_small, 4),
+                     "valu_issue_frac": round(v_launch * 2 / (1024 * 2.4e9) / t_dom, 4),
                      "pmc_source": os.path.relpath(pmc, ROOT)}
 
     cpu = None
@@ -245,11 +252,14 @@ def run(args):
                        "large_families": sum(r.n_large for r in res), "parallelism": "family-sharded x%d" % world},
             "roofline": {"bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
                          "frac": round(achieved / HBM_PEAK_GBS, 4), "traffic": traffic,
-                         "kernel": "k_small", "kernel_ms": round(t_small * 1e3, 4),
-                         "dispatches_per_launch": n_disp,
-                         "avg_dispatch_ms": round(t_small * 1e3 / max(n_disp, 1), 4),
-                         "algorithmic_bytes_per_launch": bytes_small,
+                         "kernel": kname, "kernel_ms": round(t_dom * 1e3, 4),
+                         "dispatches_per_launch": n_disp_dom,
+                         "avg_dispatch_ms": round(t_dom * 1e3 / max(n_disp_dom, 1), 4),
+                         "algorithmic_bytes_per_launch": b_dom,
+                         "small_kernel_ms": round(t_small * 1e3, 4),
+                         "small_frac": round(bytes_small / t_small / 1e9 / HBM_PEAK_GBS, 4) if t_small > 0 else None,
                          "large_kernel_ms": round(t_large * 1e3, 4),
+                         "large_frac": round(bytes_large / t_large / 1e9 / HBM_PEAK_GBS, 4) if t_large > 0 else None,
                          "step_algorithmic_GBps": round(bytes_all / (elapsed / args.steps) / 1e9, 1),
                          "issue": issue},
             "cpu_baseline": cpu,

@@ -30,7 +30,7 @@ from . import records as R
 
 IO_LIB_PATH = os.environ.get("BSDC_IO_LIB_PATH") or os.path.join(os.path.dirname(os.path.abspath(__file__)),
                                                                  "libbsdc_io.so")
-BSDC_IO_ABI_VERSION = 3
+BSDC_IO_ABI_VERSION = 4
 _P = C.c_void_p
 
 
@@ -71,6 +71,20 @@ def _load():
     lib.bsdc_bam_copy.argtypes = [_P, C.POINTER(_Arrays)]
     lib.bsdc_bam_copy.restype = C.c_int32
     lib.bsdc_bam_free.argtypes = [_P]
+    lib.bsdc_bam_stream_open.argtypes = [C.c_char_p, C.c_int32, C.c_int64, C.POINTER(_P)]
+    lib.bsdc_bam_stream_open.restype = C.c_int32
+    lib.bsdc_bam_stream_next.argtypes = [_P, C.c_int64, C.c_int64, C.POINTER(_P)]
+    lib.bsdc_bam_stream_next.restype = C.c_int32
+    lib.bsdc_bam_stream_close.argtypes = [_P]
+    lib.bsdc_bam_stream_header.argtypes = [_P, C.POINTER(_P)]
+    lib.bsdc_bam_stream_header.restype = C.c_int32
+    lib.bsdc_bam_writer_open.argtypes = [C.c_char_p, C.c_char_p, C.c_int64, C.c_int32, _P, _P, _P, C.c_int32,
+                                         C.POINTER(_P)]
+    lib.bsdc_bam_writer_open.restype = C.c_int32
+    lib.bsdc_bam_writer_add.argtypes = [_P, C.POINTER(_Records), C.c_int32]
+    lib.bsdc_bam_writer_add.restype = C.c_int32
+    lib.bsdc_bam_writer_close.argtypes = [_P, C.c_int32]
+    lib.bsdc_bam_writer_close.restype = C.c_int32
     lib.bsdc_bam_write.argtypes = [C.c_char_p, C.c_char_p, C.c_int64, C.c_int32, _P, _P, _P, C.POINTER(_Records),
                                    C.c_int32, C.c_int32]
     lib.bsdc_bam_write.restype = C.c_int32
@@ -147,36 +161,27 @@ class BamHeader:
         return out
 
 
-def read_bam(path: str, threads: int = 0):
-    """BAM file -> (BamHeader, records.RawRecords) with MI / MC / LA / RD decoded and the other
-    aux bytes kept (``raw.aux`` is a StringTable of per-record aux blocks)."""
-    lib = _load()
-    h = _P()
-    rc = lib.bsdc_bam_read(path.encode(), int(threads), C.byref(h))
-    if rc != 0:
-        raise OSError("%s: %s" % (path, lib.bsdc_io_last_error().decode()))
-    try:
-        s = _Sizes()
-        lib.bsdc_bam_sizes_of(h, C.byref(s))
-        n = s.n_rec
+def _decode(lib, h, what: str):
+    """A bsdc_bam handle (whole file or stream chunk) -> (BamHeader, RawRecords); frees nothing."""
+    s = _Sizes()
+    lib.bsdc_bam_sizes_of(h, C.byref(s))
+    n = s.n_rec
 
-        def z(k, dt):
-            return np.zeros(max(int(k), 1), dt)
-        A = dict(flag=z(n, np.uint16), tid=z(n, np.int32), pos=z(n, np.int32), mapq=z(n, np.uint8),
-                 l_seq=z(n, np.int32), seq_off=z(n, np.int64), seq=z(s.n_bases, np.uint8), qual=z(s.n_bases, np.uint8),
-                 cig_off=z(n, np.int64), n_cig=z(n, np.int32), cigar=z(s.n_cigar, np.uint32),
-                 next_tid=z(n, np.int32), next_pos=z(n, np.int32), tlen=z(n, np.int32), name_id=z(n, np.int32),
-                 name_off=z(s.n_names + 1, np.int64), name_buf=z(s.name_bytes, np.uint8), mi_id=z(n, np.int32),
-                 mi_strand=z(n, np.int8), mi_off=z(s.n_mi + 1, np.int64), mi_buf=z(s.mi_bytes, np.uint8),
-                 mc_off=z(n, np.int64), mc_n=z(n, np.int32), mc_cigar=z(s.n_mc, np.uint32), la=z(n, np.int32),
-                 rd=z(n, np.int32), aux_off=z(n + 1, np.int64), aux=z(s.aux_bytes, np.uint8),
-                 header=z(s.header_bytes, np.uint8), ref_len=z(s.n_ref, np.int64),
-                 ref_name_off=z(s.n_ref + 1, np.int64), ref_name_buf=z(s.ref_name_bytes, np.uint8))
-        a = _Arrays(**{k: _ptr(v) for k, v in A.items()})
-        if lib.bsdc_bam_copy(h, C.byref(a)) != 0:
-            raise OSError("%s: %s" % (path, lib.bsdc_io_last_error().decode()))
-    finally:
-        lib.bsdc_bam_free(h)
+    def z(k, dt):
+        return np.zeros(max(int(k), 1), dt)
+    A = dict(flag=z(n, np.uint16), tid=z(n, np.int32), pos=z(n, np.int32), mapq=z(n, np.uint8),
+             l_seq=z(n, np.int32), seq_off=z(n, np.int64), seq=z(s.n_bases, np.uint8), qual=z(s.n_bases, np.uint8),
+             cig_off=z(n, np.int64), n_cig=z(n, np.int32), cigar=z(s.n_cigar, np.uint32),
+             next_tid=z(n, np.int32), next_pos=z(n, np.int32), tlen=z(n, np.int32), name_id=z(n, np.int32),
+             name_off=z(s.n_names + 1, np.int64), name_buf=z(s.name_bytes, np.uint8), mi_id=z(n, np.int32),
+             mi_strand=z(n, np.int8), mi_off=z(s.n_mi + 1, np.int64), mi_buf=z(s.mi_bytes, np.uint8),
+             mc_off=z(n, np.int64), mc_n=z(n, np.int32), mc_cigar=z(s.n_mc, np.uint32), la=z(n, np.int32),
+             rd=z(n, np.int32), aux_off=z(n + 1, np.int64), aux=z(s.aux_bytes, np.uint8),
+             header=z(s.header_bytes, np.uint8), ref_len=z(s.n_ref, np.int64),
+             ref_name_off=z(s.n_ref + 1, np.int64), ref_name_buf=z(s.ref_name_bytes, np.uint8))
+    a = _Arrays(**{k: _ptr(v) for k, v in A.items()})
+    if lib.bsdc_bam_copy(h, C.byref(a)) != 0:
+        raise OSError("%s: %s" % (what, lib.bsdc_io_last_error().decode()))
     names_tab = StringTable(A["ref_name_buf"][:s.ref_name_bytes], A["ref_name_off"][:s.n_ref + 1], as_str=True)
     header = BamHeader(A["header"][:s.header_bytes].tobytes().decode(errors="replace"),
                        [names_tab[i] for i in range(s.n_ref)], A["ref_len"][:s.n_ref].copy())
@@ -191,6 +196,68 @@ def read_bam(path: str, threads: int = 0):
         mc_off=A["mc_off"][:n], mc_n=A["mc_n"][:n], mc_cigar=A["mc_cigar"][:s.n_mc],
         aux=StringTable(A["aux"][:s.aux_bytes], A["aux_off"][:n + 1]), la_tag=A["la"][:n], rd_tag=A["rd"][:n])
     return header, raw
+
+
+def read_bam(path: str, threads: int = 0):
+    """BAM file -> (BamHeader, records.RawRecords) with MI / MC / LA / RD decoded and the other
+    aux bytes kept (``raw.aux`` is a StringTable of per-record aux blocks)."""
+    lib = _load()
+    h = _P()
+    rc = lib.bsdc_bam_read(path.encode(), int(threads), C.byref(h))
+    if rc != 0:
+        raise OSError("%s: %s" % (path, lib.bsdc_io_last_error().decode()))
+    try:
+        return _decode(lib, h, path)
+    finally:
+        lib.bsdc_bam_free(h)
+
+
+DEFAULT_CHUNK_BYTES = 256 << 20  # uncompressed record bytes per stream chunk (about 0.8M records)
+DEFAULT_SLACK = 10_000           # positions: > any template's span (fragment + clips)
+
+
+def read_bam_header(path: str) -> BamHeader:
+    """The header of a BAM (its first BGZF blocks only)."""
+    lib = _load()
+    st = _P()
+    if lib.bsdc_bam_stream_open(path.encode(), 1, 1 << 20, C.byref(st)) != 0:
+        raise OSError("%s: %s" % (path, lib.bsdc_io_last_error().decode()))
+    try:
+        h = _P()
+        lib.bsdc_bam_stream_header(st, C.byref(h))
+        try:
+            return _decode(lib, h, path)[0]
+        finally:
+            lib.bsdc_bam_free(h)
+    finally:
+        lib.bsdc_bam_stream_close(st)
+
+
+def stream_bam(path: str, threads: int = 0, chunk_bytes: int = DEFAULT_CHUNK_BYTES, slack: int = DEFAULT_SLACK,
+               read_size: int = 64 << 20):
+    """Chunks of a coordinate-sorted BAM in bounded memory: yields (BamHeader, RawRecords) per chunk,
+    cut where no template or MI family straddles two chunks (include/bsdc_io.h,
+    bsdc_bam_stream_next); names and MI ids are chunk-local."""
+    lib = _load()
+    st = _P()
+    rc = lib.bsdc_bam_stream_open(path.encode(), int(threads), int(read_size), C.byref(st))
+    if rc != 0:
+        raise OSError("%s: %s" % (path, lib.bsdc_io_last_error().decode()))
+    try:
+        while True:
+            h = _P()
+            rc = lib.bsdc_bam_stream_next(st, int(chunk_bytes), int(slack), C.byref(h))
+            if rc != 0:
+                raise OSError("%s: %s" % (path, lib.bsdc_io_last_error().decode()))
+            if not h:
+                return
+            try:
+                hdr, raw = _decode(lib, h, path)
+            finally:
+                lib.bsdc_bam_free(h)
+            yield hdr, raw
+    finally:
+        lib.bsdc_bam_stream_close(st)
 
 
 def _aux_table(raw: R.RawRecords) -> StringTable:
@@ -271,6 +338,25 @@ def _take_table(t: StringTable, idx: np.ndarray) -> StringTable:
     off[1:] = np.cumsum(ln)
     src = np.repeat(t.off[:-1][idx] - off[:-1], ln) + np.arange(int(off[-1]), dtype=np.int64)
     return StringTable(t.buf[src], off)
+
+
+def take_records(recs: "OutRecordsBam", idx: np.ndarray) -> "OutRecordsBam":
+    """Records idx[0], idx[1], ... of an OutRecordsBam (a contiguous range for the streaming writer)."""
+    idx = np.asarray(idx, np.int64)
+
+    def ragged(off, vals):
+        ln = (off[1:] - off[:-1])[idx]
+        o = np.zeros(idx.shape[0] + 1, np.int64)
+        o[1:] = np.cumsum(ln)
+        src = np.repeat(off[:-1][idx] - o[:-1], ln) + np.arange(int(o[-1]), dtype=np.int64)
+        return o, vals[src]
+    co, cig = ragged(recs.cig_off, recs.cigar)
+    so, seq = ragged(recs.seq_off, recs.seq)
+    _, qual = ragged(recs.seq_off, recs.qual)
+    return OutRecordsBam(flag=recs.flag[idx], tid=recs.tid[idx], pos=recs.pos[idx], mapq=recs.mapq[idx],
+                         next_tid=recs.next_tid[idx], next_pos=recs.next_pos[idx], tlen=recs.tlen[idx],
+                         names=_take_table(recs.names, idx), cig_off=co, cigar=cig, seq_off=so, seq=seq, qual=qual,
+                         aux=_take_table(recs.aux, idx))
 
 
 def _synthetic_fields(raw: R.RawRecords):
@@ -394,6 +480,43 @@ def write_bam(path: str, header: BamHeader, recs: OutRecordsBam, level: int = 6,
                             int(level), int(threads))
     if rc != 0:
         raise OSError("%s: %s" % (path, lib.bsdc_io_last_error().decode()))
+
+
+class BamWriter:
+    """Streaming BAM writer (bsdc_bam_writer): header at open, records added in order, the same
+    bytes as write_bam of all the records at once."""
+
+    def __init__(self, path: str, header: BamHeader, level: int = 6):
+        self.lib = _load()
+        self.path = path
+        rn = StringTable.from_list([x.encode() for x in header.ref_names])
+        keep = []
+
+        def c(x, dt):
+            a = np.ascontiguousarray(x, dtype=dt)
+            if a.size == 0:
+                a = np.zeros(1, dt)
+            keep.append(a)
+            return _ptr(a)
+        text = header.text.encode()
+        self.h = _P()
+        rc = self.lib.bsdc_bam_writer_open(path.encode(), text, len(text), len(header.ref_names), c(rn.off, np.int64),
+                                           c(rn.buf, np.uint8), c(np.asarray(header.ref_lens, np.int64), np.int64),
+                                           int(level), C.byref(self.h))
+        if rc != 0:
+            raise OSError("%s: %s" % (path, self.lib.bsdc_io_last_error().decode()))
+
+    def add(self, recs: OutRecordsBam, threads: int = 0):
+        keep = []
+        r = _records_struct(recs, keep)
+        if self.lib.bsdc_bam_writer_add(self.h, C.byref(r), int(threads)) != 0:
+            raise OSError("%s: %s" % (self.path, self.lib.bsdc_io_last_error().decode()))
+
+    def close(self, threads: int = 0):
+        if self.h:
+            h, self.h = self.h, _P()
+            if self.lib.bsdc_bam_writer_close(h, int(threads)) != 0:
+                raise OSError("%s: %s" % (self.path, self.lib.bsdc_io_last_error().decode()))
 
 
 def read_fasta(path: str, header: BamHeader) -> R.Reference:
@@ -583,6 +706,115 @@ def step5(in_bam: str, fasta: str, out_bam: Optional[str], engine=None, prefix: 
         write_fastq(fastq[0], fastq[1], recs, level, threads)
     return {"records_in": raw.n, "families": int(cons.status.shape[0]),
             "families_emitted": int(((cons.status & 1) != 0).sum()), "records_out": recs.n}
+
+
+def step5_stream(in_bam: str, fasta: str, out_bam: str, engine=None, prefix: Optional[str] = None, threads: int = 0,
+                 level: int = 6, tags: bool = True, chunk_bytes: int = DEFAULT_CHUNK_BYTES, slack: int = DEFAULT_SLACK,
+                 batch_bases: Optional[int] = None, stats: Optional[dict] = None) -> dict:
+    """step5 in bounded memory, pipelined: a reader thread decodes the next chunk of the
+    coordinate-sorted input (stream_bam: cut where no template or MI family straddles) and forms
+    its families (C++ plan); this thread runs the chunk's family batches on the GPU; a writer
+    thread builds the output records of the previous chunk and appends them to the BAM
+    (BamWriter).  Peak host memory is about three chunks, whatever the file size.  The output is
+    byte-identical to step5's (tests/test_stream.py): every chunk's TemplateCoordinate keys sort
+    before the next chunk's, so the chunks' families in order are the whole file's."""
+    import queue
+    import threading
+    import time
+
+    from . import pipeline
+    from .device import Engine
+    own = engine is None
+    eng = Engine(0) if own else engine
+    chunks: "queue.Queue" = queue.Queue(maxsize=1)
+    outs: "queue.Queue" = queue.Queue(maxsize=1)
+    err: list = []
+    info = {"records_in": 0, "families": 0, "families_emitted": 0, "records_out": 0, "chunks": 0}
+    T = {"decode+plan": 0.0, "gpu": 0.0, "records+encode": 0.0}
+    first = {}
+
+    def reader():
+        try:
+            for hdr, raw in stream_bam(in_bam, threads, chunk_bytes, slack):
+                t0 = time.perf_counter()
+                plan = pipeline.plan_families(raw, "full", first["ref"])
+                T["decode+plan"] += time.perf_counter() - t0
+                chunks.put((raw, plan))
+        except BaseException as e:  # noqa: BLE001 -- handed to the main thread
+            err.append(e)
+        finally:
+            chunks.put(None)
+
+    def writer():
+        w = None
+        try:
+            while True:
+                item = outs.get()
+                if item is None:
+                    break
+                cons, raw = item
+                t0 = time.perf_counter()
+                if w is None:
+                    w = BamWriter(out_bam, output_header(first["header"]), level)
+                recs = duplex_records(cons, raw, first["prefix"], threads)
+                w.add(recs, threads)
+                info["records_out"] += recs.n
+                T["records+encode"] += time.perf_counter() - t0
+            if w is None:
+                w = BamWriter(out_bam, output_header(first["header"]), level)
+            w.close(threads)
+        except BaseException as e:  # noqa: BLE001
+            err.append(e)
+            while outs.get() is not None:  # drain so the main thread never blocks
+                pass
+
+    # the header and the reference come first: the plan of a chunk needs the reference
+    hdr0 = read_bam_header(in_bam)
+    first["header"] = hdr0
+    ref = read_fasta(fasta, hdr0)
+    first["ref"] = ref
+    first["prefix"] = read_name_prefix(hdr0) if prefix is None else prefix
+    try:
+        eng.load_reference(ref)
+        tr = threading.Thread(target=reader, daemon=True)
+        tw = threading.Thread(target=writer, daemon=True)
+        tr.start()
+        tw.start()
+        mode = pipeline.MODE_CONVERT | pipeline.MODE_EXTEND | pipeline.MODE_VOTE
+        try:
+            while True:
+                item = chunks.get()
+                if item is None:
+                    break
+                raw, plan = item
+                t0 = time.perf_counter()
+                if plan.split_ext:
+                    cons = pipeline.run_step5(eng, raw, tags=tags, batch_bases=batch_bases)[0]
+                else:
+                    cons = pipeline.concat_consensus(
+                        pipeline.run_ranges(eng, plan, pipeline.plan_ranges(plan, batch_bases), mode, tags))
+                T["gpu"] += time.perf_counter() - t0
+                info["records_in"] += raw.n
+                info["families"] += int(cons.status.shape[0])
+                info["families_emitted"] += int(((cons.status & 1) != 0).sum())
+                info["chunks"] += 1
+                outs.put((cons, raw))
+        except BaseException:
+            while chunks.get() is not None:  # let the reader finish
+                pass
+            raise
+        finally:
+            outs.put(None)
+            tw.join()
+            tr.join()
+    finally:
+        if own:
+            eng.close()
+    if err:
+        raise err[0]
+    if stats is not None:
+        stats.update({k: round(v, 4) for k, v in T.items()})
+    return info
 
 
 def molecular(in_bam: str, out_bam: Optional[str], engine=None, prefix: Optional[str] = None, threads: int = 0,

@@ -166,32 +166,30 @@ extern "C" {
 int32_t bsdc_io_abi_version(void) { return BSDC_IO_ABI_VERSION; }
 const char *bsdc_io_last_error(void) { return g_err.c_str(); }
 
-int32_t bsdc_bam_read(const char *path, int32_t n_threads, bsdc_bam **out) {
-    *out = nullptr;
-    set_threads(n_threads);
-    FILE *f = fopen(path, "rb");
-    if (!f) return fail(BSDC_IO_EIO, std::string("cannot open ") + path);
-    std::vector<uint8_t> comp;
-    {
-        fseek(f, 0, SEEK_END);
-        const long sz = ftell(f);
-        fseek(f, 0, SEEK_SET);
-        comp.resize(sz > 0 ? (size_t)sz : 0);
-        if (sz > 0 && fread(comp.data(), 1, comp.size(), f) != comp.size()) {
-            fclose(f);
-            return fail(BSDC_IO_EIO, std::string("short read on ") + path);
-        }
-        fclose(f);
-    }
-    // ---- BGZF blocks ----
+}  // extern "C"
+
+namespace {
+
+// Whole BGZF blocks of comp[0, n) inflated (in parallel) and appended to `out`; *used = the bytes
+// of the whole blocks (a trailing partial block is left for the caller unless `final`, where it
+// is an error).  Every block is CRC-checked.
+int32_t inflate_blocks(const uint8_t *comp, int64_t n, bool final, std::vector<uint8_t> &out, int64_t *used) {
     std::vector<int64_t> boff, bsz, uoff;
-    int64_t o = 0, u = 0;
-    const int64_t n = (int64_t)comp.size();
+    int64_t o = 0, u = (int64_t)out.size();
+    *used = 0;
     while (o < n) {
-        const uint8_t *h = comp.data() + o;
-        if (n - o < 18 || h[0] != 31 || h[1] != 139 || h[2] != 8 || !(h[3] & 4))
+        const uint8_t *h = comp + o;
+        if (n - o < 18) {
+            if (!final) break;
+            return fail(BSDC_IO_EFORMAT, "truncated BGZF block");
+        }
+        if (h[0] != 31 || h[1] != 139 || h[2] != 8 || !(h[3] & 4))
             return fail(BSDC_IO_EFORMAT, "not a BGZF file (bad block header)");
         const int xlen = rd16(h + 10);
+        if (n - o < 12 + xlen) {
+            if (!final) break;
+            return fail(BSDC_IO_EFORMAT, "truncated BGZF block");
+        }
         int64_t bsize = -1;
         for (int x = 0; x + 4 <= xlen;) {
             const uint8_t *sf = h + 12 + x;
@@ -199,25 +197,32 @@ int32_t bsdc_bam_read(const char *path, int32_t n_threads, bsdc_bam **out) {
             if (sf[0] == 'B' && sf[1] == 'C' && slen == 2) bsize = rd16(sf + 4) + 1;
             x += 4 + slen;
         }
-        if (bsize < 0 || o + bsize > n) return fail(BSDC_IO_EFORMAT, "truncated BGZF block");
+        if (bsize < 0) return fail(BSDC_IO_EFORMAT, "truncated BGZF block");
+        if (o + bsize > n) {
+            if (!final) break;
+            return fail(BSDC_IO_EFORMAT, "truncated BGZF block");
+        }
         boff.push_back(o);
         bsz.push_back(bsize);
         uoff.push_back(u);
         u += rd32(h + bsize - 4);
         o += bsize;
     }
-    auto *b = new bsdc_bam();
-    b->data.resize((size_t)u + 8);
+    out.resize((size_t)u);
     const int64_t nb = (int64_t)boff.size();
     int bad = 0;
 #pragma omp parallel for schedule(dynamic, 16) reduction(| : bad)
     for (int64_t i = 0; i < nb; i++) {
-        const uint8_t *h = comp.data() + boff[i];
+        const uint8_t *h = comp + boff[i];
         const int xlen = rd16(h + 10);
         const uint8_t *cdata = h + 12 + xlen;
         const int64_t clen = bsz[i] - 12 - xlen - 8;
         const uint32_t isize = rd32(h + bsz[i] - 4), crc = rd32(h + bsz[i] - 8);
         if (isize == 0) continue;
+        if (clen < 0) {
+            bad |= 1;
+            continue;
+        }
         z_stream zs;
         memset(&zs, 0, sizeof zs);
         if (inflateInit2(&zs, -15) != Z_OK) {
@@ -226,32 +231,24 @@ int32_t bsdc_bam_read(const char *path, int32_t n_threads, bsdc_bam **out) {
         }
         zs.next_in = const_cast<uint8_t *>(cdata);
         zs.avail_in = (uInt)clen;
-        zs.next_out = b->data.data() + uoff[i];
+        zs.next_out = out.data() + uoff[i];
         zs.avail_out = isize;
         const int rc = inflate(&zs, Z_FINISH);
         inflateEnd(&zs);
-        if (rc != Z_STREAM_END || zs.total_out != isize ||
-            crc32(0L, b->data.data() + uoff[i], isize) != crc)
-            bad |= 1;
+        if (rc != Z_STREAM_END || zs.total_out != isize || crc32(0L, out.data() + uoff[i], isize) != crc) bad |= 1;
     }
-    if (bad) {
-        delete b;
-        return fail(BSDC_IO_EFORMAT, "corrupt BGZF block (inflate or CRC32)");
-    }
-    // ---- header ----
-    const uint8_t *d = b->data.data();
-    const int64_t dn = u;
-    if (dn < 12 || memcmp(d, "BAM\1", 4) != 0) {
-        delete b;
-        return fail(BSDC_IO_EFORMAT, "missing BAM magic");
-    }
+    if (bad) return fail(BSDC_IO_EFORMAT, "corrupt BGZF block (inflate or CRC32)");
+    *used = o;
+    return 0;
+}
+
+// The BAM header at the start of d[0, dn): text, references; *p = the first record's offset.
+int32_t parse_header(const uint8_t *d, int64_t dn, bsdc_bam *b, int64_t *p_out) {
+    if (dn < 12 || memcmp(d, "BAM\1", 4) != 0) return fail(BSDC_IO_EFORMAT, "missing BAM magic");
     int64_t p = 4;
     const int64_t l_text = rd32(d + p);
     p += 4;
-    if (p + l_text + 4 > dn) {
-        delete b;
-        return fail(BSDC_IO_EFORMAT, "truncated BAM header");
-    }
+    if (p + l_text + 4 > dn) return fail(BSDC_IO_EFORMAT, "truncated BAM header");
     b->header.assign((const char *)d + p, (size_t)l_text);
     b->header.resize(strnlen(b->header.c_str(), b->header.size()));
     p += l_text;
@@ -261,25 +258,26 @@ int32_t bsdc_bam_read(const char *path, int32_t n_threads, bsdc_bam **out) {
         if (p + 4 > dn) break;
         const int32_t ln = rdi32(d + p);
         p += 4;
-        if (ln < 1 || p + ln + 4 > dn) {
-            delete b;
-            return fail(BSDC_IO_EFORMAT, "truncated reference list");
-        }
+        if (ln < 1 || p + ln + 4 > dn) return fail(BSDC_IO_EFORMAT, "truncated reference list");
         b->ref_names.emplace_back((const char *)d + p, (size_t)ln - 1);
         p += ln;
         b->ref_len.push_back(rd32(d + p));
         p += 4;
     }
-    // ---- record boundaries ----
+    *p_out = p;
+    return 0;
+}
+
+// The records of b->data from offset p to dn (whole records only): boundaries, tags, interning.
+int32_t parse_records(bsdc_bam *b, int64_t p, int64_t dn) {
+    const uint8_t *d = b->data.data();
     while (p + 4 <= dn) {
         const int64_t bs = rd32(d + p);
-        if (bs < 32 || p + 4 + bs > dn) {
-            delete b;
-            return fail(BSDC_IO_EFORMAT, "truncated BAM record");
-        }
+        if (bs < 32 || p + 4 + bs > dn) return fail(BSDC_IO_EFORMAT, "truncated BAM record");
         b->rec_start.push_back(p);
         p += 4 + bs;
     }
+    if (p != dn) return fail(BSDC_IO_EFORMAT, "truncated BAM record");
     const int64_t nr = (int64_t)b->rec_start.size();
     // ---- per record: tags, sizes ----
     b->la.assign(nr, -1);
@@ -332,10 +330,7 @@ int32_t bsdc_bam_read(const char *path, int32_t n_threads, bsdc_bam **out) {
             a += 3 + vs;
         }
     }
-    if (badrec) {
-        delete b;
-        return fail(BSDC_IO_EFORMAT, "malformed BAM record (lengths or aux)");
-    }
+    if (badrec) return fail(BSDC_IO_EFORMAT, "malformed BAM record (lengths or aux)");
     b->n_bases = nbases;
     b->n_cigar = ncig;
     b->n_mc = nmc;
@@ -361,8 +356,375 @@ int32_t bsdc_bam_read(const char *path, int32_t n_threads, bsdc_bam **out) {
     }
     intern(nm, nullptr, b->name_id, b->names);
     intern(mk, &mi_full, b->mi_id, b->mis);
+    return 0;
+}
+
+}  // namespace
+
+extern "C" {
+
+int32_t bsdc_bam_read(const char *path, int32_t n_threads, bsdc_bam **out) {
+    *out = nullptr;
+    set_threads(n_threads);
+    FILE *f = fopen(path, "rb");
+    if (!f) return fail(BSDC_IO_EIO, std::string("cannot open ") + path);
+    std::vector<uint8_t> comp;
+    {
+        fseek(f, 0, SEEK_END);
+        const long sz = ftell(f);
+        fseek(f, 0, SEEK_SET);
+        comp.resize(sz > 0 ? (size_t)sz : 0);
+        if (sz > 0 && fread(comp.data(), 1, comp.size(), f) != comp.size()) {
+            fclose(f);
+            return fail(BSDC_IO_EIO, std::string("short read on ") + path);
+        }
+        fclose(f);
+    }
+    auto *b = new bsdc_bam();
+    int64_t used = 0, p = 0;
+    int32_t rc = inflate_blocks(comp.data(), (int64_t)comp.size(), true, b->data, &used);
+    const int64_t dn = (int64_t)b->data.size();
+    if (rc == 0) rc = parse_header(b->data.data(), dn, b, &p);
+    b->data.resize((size_t)dn + 8);
+    if (rc == 0) rc = parse_records(b, p, dn);
+    if (rc != 0) {
+        delete b;
+        return rc;
+    }
     *out = b;
     return 0;
+}
+
+// ------------------------------------------------------------------------------------------
+// streaming reader: family-complete chunks of a coordinate-sorted BAM, in bounded memory
+// ------------------------------------------------------------------------------------------
+namespace {
+// (contig, position) as one ordered coordinate; unmapped (tid -1) sorts last
+inline int64_t coord(int32_t tid, int32_t pos) {
+    return tid < 0 ? INT64_MAX / 4 : ((int64_t)tid << 32) + (int64_t)pos;
+}
+struct StreamRec {
+    int64_t off, len;  // the record's bytes in bsdc_bam_stream::buf
+    int32_t fam;       // its MI family (stream-wide index)
+};
+// a TemplateCoordinate key, coarsely: (lower end's contig << 32 | other end's contig, lower end's
+// position); BIG (0x7FFFFFFF) for an unmapped or absent mate, as the key's mate contig
+using TcKey = std::pair<int64_t, int64_t>;
+constexpr int64_t kBigTid = 0x7FFFFFFF;
+constexpr int64_t kKeyDelta = 4;  // |key position before tools 1 + 2 - after| <= 2, twice
+struct StreamFam {
+    int64_t lo = INT64_MAX, hi = INT64_MIN;  // min own position, max own or mate position (coord)
+    TcKey klo{INT64_MAX, INT64_MAX}, khi{INT64_MIN, INT64_MIN};  // bounds of its records' keys
+    int64_t n = 0;                           // buffered records
+};
+}  // namespace
+
+struct bsdc_bam_stream {
+    FILE *f = nullptr;
+    bsdc_bam hdr;                 // header text and references only
+    std::vector<uint8_t> comp;    // compressed bytes read but not yet inflated (a partial block)
+    std::vector<uint8_t> pend;    // inflated bytes not yet split into records (starts at a record)
+    bool eof = false;
+    int64_t read_size = 0;
+    // buffered records (file order) and their families
+    std::vector<uint8_t> buf;
+    std::vector<StreamRec> recs;
+    std::unordered_map<std::string, int32_t> fam_of;  // MI base -> family
+    std::vector<StreamFam> fams;
+    std::vector<int32_t> free_fams;
+    int64_t cursor = INT64_MIN;  // the last record's position
+};
+
+int32_t bsdc_bam_stream_open(const char *path, int32_t n_threads, int64_t read_size, bsdc_bam_stream **out) {
+    *out = nullptr;
+    set_threads(n_threads);
+    FILE *f = fopen(path, "rb");
+    if (!f) return fail(BSDC_IO_EIO, std::string("cannot open ") + path);
+    auto *s = new bsdc_bam_stream();
+    s->f = f;
+    s->read_size = read_size > 0 ? read_size : ((int64_t)64 << 20);
+    // inflate until the header is whole
+    for (;;) {
+        int64_t p = 0;
+        bsdc_bam probe;
+        const bool have = s->pend.size() >= 12 &&
+                          parse_header(s->pend.data(), (int64_t)s->pend.size(), &probe, &p) == 0;
+        if (have) {
+            s->hdr.header = probe.header;
+            s->hdr.ref_names = probe.ref_names;
+            s->hdr.ref_len = probe.ref_len;
+            s->pend.erase(s->pend.begin(), s->pend.begin() + p);
+            break;
+        }
+        if (s->eof) {
+            const int64_t dn = (int64_t)s->pend.size();
+            const int32_t rc = parse_header(s->pend.data(), dn, &probe, &p);
+            bsdc_bam_stream_close(s);
+            return rc != 0 ? rc : fail(BSDC_IO_EFORMAT, "missing BAM header");
+        }
+        const int32_t rc = bsdc_bam_stream_fill(s);
+        if (rc != 0) {
+            bsdc_bam_stream_close(s);
+            return rc;
+        }
+    }
+    *out = s;
+    return 0;
+}
+
+// Reads read_size more compressed bytes and inflates the whole blocks into pend.
+int32_t bsdc_bam_stream_fill(bsdc_bam_stream *s) {
+    if (s->eof) return 0;
+    const size_t have = s->comp.size();
+    s->comp.resize(have + (size_t)s->read_size);
+    const size_t got = fread(s->comp.data() + have, 1, (size_t)s->read_size, s->f);
+    s->comp.resize(have + got);
+    if (got < (size_t)s->read_size) {
+        if (ferror(s->f)) return fail(BSDC_IO_EIO, "read error");
+        s->eof = true;
+    }
+    int64_t used = 0;
+    const int32_t rc = inflate_blocks(s->comp.data(), (int64_t)s->comp.size(), s->eof, s->pend, &used);
+    if (rc != 0) return rc;
+    s->comp.erase(s->comp.begin(), s->comp.begin() + used);
+    return 0;
+}
+
+namespace {
+// The whole records of s->pend moved into the buffer, each with its MI family.  A record's family
+// is its MI base (the MI up to the first '/', as the reader interns it); a record without MI is a
+// family of its own.
+int32_t stream_split(bsdc_bam_stream *s) {
+    const uint8_t *d = s->pend.data();
+    const int64_t dn = (int64_t)s->pend.size();
+    int64_t p = 0;
+    while (p + 4 <= dn) {
+        const int64_t bs = rd32(d + p);
+        if (bs < 32) return fail(BSDC_IO_EFORMAT, "truncated BAM record");
+        if (p + 4 + bs > dn) break;
+        const uint8_t *r = d + p;
+        const uint8_t *end = r + 4 + bs;
+        const int l_name = r[12];
+        const int n_cig = rd16(r + 16);
+        const int32_t l_seq = rdi32(r + 20);
+        const int64_t body = 36 + (int64_t)l_name + 4 * (int64_t)n_cig + ((int64_t)l_seq + 1) / 2 + (int64_t)l_seq;
+        if (l_seq < 0 || l_name < 1 || body > 4 + bs) return fail(BSDC_IO_EFORMAT, "malformed BAM record (lengths or aux)");
+        std::string_view mi, mc;
+        for (const uint8_t *a = r + body; a + 3 <= end;) {
+            const int64_t vs = aux_value_size(a, end);
+            if (vs < 0 || vs > (end - a) - 3) return fail(BSDC_IO_EFORMAT, "malformed BAM record (lengths or aux)");
+            if (a[0] == 'M' && a[1] == 'I' && a[2] == 'Z') mi = std::string_view((const char *)a + 3, (size_t)vs - 1);
+            if (a[0] == 'M' && a[1] == 'C' && a[2] == 'Z') mc = std::string_view((const char *)a + 3, (size_t)vs - 1);
+            a += 3 + vs;
+        }
+        const size_t slash = mi.find('/');
+        if (slash != std::string_view::npos) mi = mi.substr(0, slash);
+        int32_t fam;
+        if (!mi.empty()) {
+            auto it = s->fam_of.find(std::string(mi));
+            if (it == s->fam_of.end() || s->fams[(size_t)it->second].n == 0) {
+                if (!s->free_fams.empty()) {
+                    fam = s->free_fams.back();
+                    s->free_fams.pop_back();
+                    s->fams[(size_t)fam] = StreamFam();
+                } else {
+                    fam = (int32_t)s->fams.size();
+                    s->fams.emplace_back();
+                }
+                s->fam_of[std::string(mi)] = fam;
+            } else {
+                fam = it->second;
+            }
+        } else {
+            if (!s->free_fams.empty()) {
+                fam = s->free_fams.back();
+                s->free_fams.pop_back();
+                s->fams[(size_t)fam] = StreamFam();
+            } else {
+                fam = (int32_t)s->fams.size();
+                s->fams.emplace_back();
+            }
+        }
+        const int32_t tid = rdi32(r + 4), pos = rdi32(r + 8), ntid = rdi32(r + 24), npos = rdi32(r + 28);
+        const int flag = rd16(r + 18);
+        const int64_t c = coord(tid, pos);
+        const int64_t e = ntid >= 0 ? std::max(c, coord(ntid, npos)) : c;
+        // the template's key (batch.template_coordinate_order): the lower end's contig, then the
+        // other end's (BIG for an unpaired record or unmapped mate), then the lower end's unclipped
+        // 5' position -- from the input's cigar and MC, so within kKeyDelta of the key of the
+        // records tools 1 and 2 make (a prepended base, an appended one, the RD trim)
+        const uint8_t *cg = r + 36 + l_name;
+        int64_t lead = 0, trail = 0, reflen = 0;
+        {
+            int first_nc = -1, last_nc = -1;
+            for (int i = 0; i < n_cig; i++) {
+                const uint32_t op = rd32(cg + 4 * i) & 15;
+                if (op == 0 || op == 2 || op == 3 || op == 7 || op == 8) reflen += rd32(cg + 4 * i) >> 4;
+                if (op != 4 && op != 5) {
+                    if (first_nc < 0) first_nc = i;
+                    last_nc = i;
+                }
+            }
+            for (int i = 0; i < n_cig; i++) {
+                const uint32_t op = rd32(cg + 4 * i) & 15;
+                if (op != 4 && op != 5) continue;
+                if (first_nc < 0 || i < first_nc) lead += rd32(cg + 4 * i) >> 4;
+                else if (i > last_nc) trail += rd32(cg + 4 * i) >> 4;
+            }
+        }
+        const int64_t p_own = (flag & 16) ? pos + reflen - 1 + trail : pos - lead;
+        int64_t p_mate = npos;
+        if (!mc.empty() && !(mc.size() == 1 && mc[0] == '*')) {
+            int64_t mlead = 0, mref = 0, num = 0, clip_run = 0;  // clip_run: clips since the last non-clip op
+            bool seen_nc = false;
+            for (char ch : mc) {
+                if (ch >= '0' && ch <= '9') {
+                    num = num * 10 + (ch - '0');
+                    continue;
+                }
+                if (ch == 'M' || ch == 'D' || ch == 'N' || ch == '=' || ch == 'X') mref += num;
+                if (ch == 'S' || ch == 'H') {
+                    if (!seen_nc) mlead += num;
+                    else clip_run += num;
+                } else {
+                    seen_nc = true;
+                    clip_run = 0;
+                }
+                num = 0;
+            }
+            p_mate = (flag & 32) ? npos + mref - 1 + clip_run : npos - mlead;
+        }
+        const bool paired = (flag & 1) && !(flag & 8) && ntid >= 0;
+        const int64_t t1 = tid < 0 ? kBigTid : tid;
+        TcKey key;
+        if (!paired) key = {(t1 << 32) | kBigTid, p_own};
+        else if (tid == ntid) key = {(t1 << 32) | t1, std::min(p_own, p_mate)};
+        else if (tid >= 0 && tid < ntid) key = {(t1 << 32) | (int64_t)ntid, p_own};
+        else key = {((int64_t)ntid << 32) | t1, p_mate};
+        StreamFam &F = s->fams[(size_t)fam];
+        F.lo = std::min(F.lo, c);
+        F.hi = std::max(F.hi, e);
+        F.klo = std::min(F.klo, key);
+        F.khi = std::max(F.khi, key);
+        F.n++;
+        s->cursor = std::max(s->cursor, c);
+        s->recs.push_back(StreamRec{(int64_t)s->buf.size(), 4 + bs, fam});
+        s->buf.insert(s->buf.end(), r, end);
+        p += 4 + bs;
+    }
+    s->pend.erase(s->pend.begin(), s->pend.begin() + p);
+    return 0;
+}
+}  // namespace
+
+// The next chunk (see include/bsdc_io.h): the buffered records of every family that is complete
+// and whose TemplateCoordinate keys all sort before any key still to come, once they reach
+// min_bytes (everything left at the end of the file).  Per family m: hi_m = its highest record
+// or mate position; m is complete once the stream has passed hi_m + slack (a family's templates
+// share their coordinates; slack > any read's reference span plus clips).  Its records' keys lie
+// within [klo_m, khi_m] up to kKeyDelta in the position.  T = the least key a record not yet
+// emitted can have: (cursor contig, cursor contig, cursor - slack) for the records still unread,
+// klo_m - kKeyDelta of the incomplete families and of the complete ones kept back; a complete
+// family goes out when khi_m + kKeyDelta < T.  (Templates whose mate is on another contig or unmapped sort after every
+// template of their contig with both ends on it, so they wait for the contig's end.)
+int32_t bsdc_bam_stream_next(bsdc_bam_stream *s, int64_t min_bytes, int64_t slack, bsdc_bam **out) {
+    *out = nullptr;
+    std::vector<uint8_t> take;  // per buffered family: goes out now
+    for (;;) {
+        int32_t rc = stream_split(s);
+        if (rc != 0) return rc;
+        const bool end = s->eof && s->comp.empty();
+        if (end && !s->pend.empty()) return fail(BSDC_IO_EFORMAT, "truncated BAM record");
+        take.assign(s->fams.size(), 0);
+        int64_t bytes = 0;
+        if (end) {
+            for (auto &r : s->recs) take[(size_t)r.fam] = 1;
+            bytes = (int64_t)s->buf.size();
+        } else if (s->cursor != INT64_MIN) {
+            const int64_t ct = s->cursor >> 32, cp = s->cursor & 0xFFFFFFFFll;
+            const int64_t ctid = s->cursor >= INT64_MAX / 4 ? kBigTid : ct;
+            // records still unread start at or after the cursor: their keys' positions are at
+            // least cursor - slack (a leading clip, a mate's reverse 5' end)
+            TcKey T{(ctid << 32) | ctid, (s->cursor >= INT64_MAX / 4 ? 0 : cp) - slack};
+            auto lo_of = [&](const StreamFam &F) { return TcKey{F.klo.first, F.klo.second - kKeyDelta}; };
+            auto hi_of = [&](const StreamFam &F) { return TcKey{F.khi.first, F.khi.second + kKeyDelta}; };
+            for (size_t m = 0; m < s->fams.size(); m++) {
+                const StreamFam &F = s->fams[m];
+                if (F.n > 0 && F.hi + slack >= s->cursor) T = std::min(T, lo_of(F));  // incomplete
+            }
+            for (bool moved = true; moved;) {  // complete ones kept back lower T in turn
+                moved = false;
+                for (size_t m = 0; m < s->fams.size(); m++) {
+                    const StreamFam &F = s->fams[m];
+                    if (F.n > 0 && F.hi + slack < s->cursor && !(hi_of(F) < T) && lo_of(F) < T) {
+                        T = lo_of(F);
+                        moved = true;
+                    }
+                }
+            }
+            for (size_t m = 0; m < s->fams.size(); m++) {
+                const StreamFam &F = s->fams[m];
+                take[m] = F.n > 0 && F.hi + slack < s->cursor && hi_of(F) < T;
+            }
+            for (auto &r : s->recs) bytes += take[(size_t)r.fam] ? r.len : 0;
+        }
+        if (end || (bytes > 0 && bytes >= min_bytes)) {
+            if (bytes == 0) return 0;  // the end of the stream
+            auto *b = new bsdc_bam();
+            b->header = s->hdr.header;
+            b->ref_names = s->hdr.ref_names;
+            b->ref_len = s->hdr.ref_len;
+            b->data.reserve((size_t)bytes + 8);
+            std::vector<uint8_t> keep;
+            std::vector<StreamRec> krecs;
+            keep.reserve(s->buf.size() - (size_t)bytes);
+            for (auto &r : s->recs) {
+                const uint8_t *src = s->buf.data() + r.off;
+                if (take[(size_t)r.fam]) {
+                    b->data.insert(b->data.end(), src, src + r.len);
+                } else {
+                    krecs.push_back(StreamRec{(int64_t)keep.size(), r.len, r.fam});
+                    keep.insert(keep.end(), src, src + r.len);
+                }
+            }
+            for (size_t m = 0; m < s->fams.size(); m++)
+                if (take[m]) {
+                    s->fams[m].n = 0;
+                    s->free_fams.push_back((int32_t)m);
+                }
+            for (auto it = s->fam_of.begin(); it != s->fam_of.end();)  // forget the emitted MI bases
+                it = s->fams[(size_t)it->second].n == 0 ? s->fam_of.erase(it) : std::next(it);
+            s->buf.swap(keep);
+            s->recs.swap(krecs);
+            b->data.resize((size_t)bytes + 8);
+            rc = parse_records(b, 0, bytes);
+            if (rc != 0) {
+                delete b;
+                return rc;
+            }
+            *out = b;
+            return 0;
+        }
+        rc = bsdc_bam_stream_fill(s);
+        if (rc != 0) return rc;
+    }
+}
+
+// The stream's header and references as a record-less bsdc_bam.
+int32_t bsdc_bam_stream_header(const bsdc_bam_stream *s, bsdc_bam **out) {
+    auto *b = new bsdc_bam();
+    b->header = s->hdr.header;
+    b->ref_names = s->hdr.ref_names;
+    b->ref_len = s->hdr.ref_len;
+    b->data.resize(8);
+    *out = b;
+    return 0;
+}
+
+void bsdc_bam_stream_close(bsdc_bam_stream *s) {
+    if (!s) return;
+    if (s->f) fclose(s->f);
+    delete s;
 }
 
 void bsdc_bam_sizes_of(const bsdc_bam *b, bsdc_bam_sizes *s) {
@@ -493,14 +855,15 @@ int reg2bin(int64_t beg, int64_t end) {
 constexpr int64_t kBlock = 0xff00;  // uncompressed bytes per BGZF block (htslib's size)
 // BGZF framing of an uncompressed buffer: 0xff00-byte blocks deflated in parallel (each a gzip
 // member, so the file is also plain multi-member gzip), one write, then the 28-byte EOF block.
-int32_t write_bgzf(const char *path, const std::vector<uint8_t> &buf, int32_t level) {
-    const int64_t total = (int64_t)buf.size();
+// BGZF blocks of src[0, total) (kBlock uncompressed bytes each, the last one shorter), deflated
+// in parallel and written to f.
+int32_t deflate_write(FILE *f, const uint8_t *src0, int64_t total, int32_t level) {
     const int64_t nb = (total + kBlock - 1) / kBlock;
     std::vector<std::vector<uint8_t>> blocks((size_t)nb);
     int bad = 0;
 #pragma omp parallel for schedule(dynamic, 4) reduction(| : bad)
     for (int64_t i = 0; i < nb; i++) {
-        const uint8_t *src = buf.data() + i * kBlock;
+        const uint8_t *src = src0 + i * kBlock;
         const int64_t len = std::min(kBlock, total - i * kBlock);
         std::vector<uint8_t> &o = blocks[(size_t)i];
         o.resize(18 + (size_t)compressBound((uLong)len) + 8 + 64);
@@ -536,26 +899,25 @@ int32_t write_bgzf(const char *path, const std::vector<uint8_t> &buf, int32_t le
         o.resize((size_t)bsize);
     }
     if (bad) return fail(BSDC_IO_EFORMAT, "deflate failed");
-    FILE *f = fopen(path, "wb");
-    if (!f) return fail(BSDC_IO_EIO, std::string("cannot create ") + path);
     for (auto &bk : blocks)
-        if (fwrite(bk.data(), 1, bk.size(), f) != bk.size()) {
-            fclose(f);
-            return fail(BSDC_IO_EIO, std::string("write failed on ") + path);
-        }
-    static const uint8_t eof[28] = {31, 139, 8, 4, 0, 0, 0, 0, 0, 255, 6, 0, 66, 67, 2, 0, 27, 0, 3, 0, 0, 0, 0, 0, 0, 0, 0, 0};
-    if (fwrite(eof, 1, 28, f) != 28 || fclose(f) != 0) return fail(BSDC_IO_EIO, std::string("write failed on ") + path);
+        if (fwrite(bk.data(), 1, bk.size(), f) != bk.size()) return fail(BSDC_IO_EIO, "BGZF write failed");
     return 0;
 }
-}  // namespace
 
-extern "C" int32_t bsdc_bam_write(const char *path, const char *header_text, int64_t header_len, int32_t n_ref,
-                                  const int64_t *ref_name_off, const char *ref_name_buf, const int64_t *ref_len,
-                                  const bsdc_bam_records *r, int32_t level, int32_t n_threads) {
-    set_threads(n_threads);
-    const int64_t nr = r->n_rec;
-    // ---- header bytes ----
-    std::vector<uint8_t> head;
+const uint8_t kBgzfEof[28] = {31, 139, 8, 4, 0, 0, 0, 0, 0, 255, 6, 0, 66, 67, 2, 0, 27, 0, 3, 0, 0, 0, 0, 0, 0, 0, 0, 0};
+
+int32_t write_bgzf(const char *path, const std::vector<uint8_t> &buf, int32_t level) {
+    FILE *f = fopen(path, "wb");
+    if (!f) return fail(BSDC_IO_EIO, std::string("cannot create ") + path);
+    int32_t rc = deflate_write(f, buf.data(), (int64_t)buf.size(), level);
+    if (rc == 0 && fwrite(kBgzfEof, 1, 28, f) != 28) rc = fail(BSDC_IO_EIO, std::string("write failed on ") + path);
+    if (fclose(f) != 0 && rc == 0) rc = fail(BSDC_IO_EIO, std::string("write failed on ") + path);
+    return rc;
+}
+
+// BAM header bytes (magic, text, references)
+void encode_header(std::vector<uint8_t> &head, const char *header_text, int64_t header_len, int32_t n_ref,
+                   const int64_t *ref_name_off, const char *ref_name_buf, const int64_t *ref_len) {
     auto put32 = [&](uint32_t v) {
         uint8_t t[4];
         wr32(t, v);
@@ -572,9 +934,13 @@ extern "C" int32_t bsdc_bam_write(const char *path, const char *header_text, int
         head.push_back(0);
         put32((uint32_t)ref_len[i]);
     }
-    // ---- record sizes, offsets ----
+}
+
+// The records' BAM bytes appended to buf (encoded in parallel)
+int32_t encode_records(const bsdc_bam_records *r, std::vector<uint8_t> &buf) {
+    const int64_t nr = r->n_rec;
     std::vector<int64_t> off(nr + 1);
-    off[0] = (int64_t)head.size();
+    off[0] = (int64_t)buf.size();
     for (int64_t k = 0; k < nr; k++) {
         const int64_t l_name = r->name_off[k + 1] - r->name_off[k] + 1;
         const int64_t n_cig = r->cig_off[k + 1] - r->cig_off[k];
@@ -583,8 +949,7 @@ extern "C" int32_t bsdc_bam_write(const char *path, const char *header_text, int
         if (l_name > 254 || n_cig > 0xFFFF) return fail(BSDC_IO_EFORMAT, "record name or cigar too long for BAM");
         off[k + 1] = off[k] + 4 + 32 + l_name + 4 * n_cig + (l_seq + 1) / 2 + l_seq + l_aux;
     }
-    std::vector<uint8_t> buf((size_t)off[nr]);
-    memcpy(buf.data(), head.data(), head.size());
+    buf.resize((size_t)off[nr]);
 #pragma omp parallel for schedule(static)
     for (int64_t k = 0; k < nr; k++) {
         uint8_t *p = buf.data() + off[k];
@@ -625,7 +990,66 @@ extern "C" int32_t bsdc_bam_write(const char *path, const char *header_text, int
         q += l_seq;
         memcpy(q, r->aux + r->aux_off[k], (size_t)l_aux);
     }
+    return 0;
+}
+}  // namespace
+
+extern "C" int32_t bsdc_bam_write(const char *path, const char *header_text, int64_t header_len, int32_t n_ref,
+                                  const int64_t *ref_name_off, const char *ref_name_buf, const int64_t *ref_len,
+                                  const bsdc_bam_records *r, int32_t level, int32_t n_threads) {
+    set_threads(n_threads);
+    std::vector<uint8_t> buf;
+    encode_header(buf, header_text, header_len, n_ref, ref_name_off, ref_name_buf, ref_len);
+    const int32_t rc = encode_records(r, buf);
+    if (rc != 0) return rc;
     return write_bgzf(path, buf, level);
+}
+
+// ------------------------------------------------------------------------------------------
+// streaming writer: the same bytes as bsdc_bam_write of all the records at once (whole kBlock
+// blocks are deflated as they fill; the rest waits for the next records or the close)
+// ------------------------------------------------------------------------------------------
+struct bsdc_bam_writer {
+    FILE *f = nullptr;
+    int32_t level = 6;
+    std::vector<uint8_t> tail;
+};
+
+extern "C" int32_t bsdc_bam_writer_open(const char *path, const char *header_text, int64_t header_len, int32_t n_ref,
+                                        const int64_t *ref_name_off, const char *ref_name_buf, const int64_t *ref_len,
+                                        int32_t level, bsdc_bam_writer **out) {
+    *out = nullptr;
+    FILE *f = fopen(path, "wb");
+    if (!f) return fail(BSDC_IO_EIO, std::string("cannot create ") + path);
+    auto *w = new bsdc_bam_writer();
+    w->f = f;
+    w->level = level;
+    encode_header(w->tail, header_text, header_len, n_ref, ref_name_off, ref_name_buf, ref_len);
+    *out = w;
+    return 0;
+}
+
+extern "C" int32_t bsdc_bam_writer_add(bsdc_bam_writer *w, const bsdc_bam_records *r, int32_t n_threads) {
+    set_threads(n_threads);
+    int32_t rc = encode_records(r, w->tail);
+    if (rc != 0) return rc;
+    const int64_t whole = ((int64_t)w->tail.size() / kBlock) * kBlock;
+    if (whole > 0) {
+        rc = deflate_write(w->f, w->tail.data(), whole, w->level);
+        if (rc != 0) return rc;
+        w->tail.erase(w->tail.begin(), w->tail.begin() + whole);
+    }
+    return 0;
+}
+
+extern "C" int32_t bsdc_bam_writer_close(bsdc_bam_writer *w, int32_t n_threads) {
+    if (!w) return 0;
+    set_threads(n_threads);
+    int32_t rc = deflate_write(w->f, w->tail.data(), (int64_t)w->tail.size(), w->level);
+    if (rc == 0 && fwrite(kBgzfEof, 1, 28, w->f) != 28) rc = fail(BSDC_IO_EIO, "BGZF write failed");
+    if (fclose(w->f) != 0 && rc == 0) rc = fail(BSDC_IO_EIO, "BGZF close failed");
+    delete w;
+    return rc;
 }
 
 namespace {

@@ -17,7 +17,7 @@
 extern "C" {
 #endif
 
-#define BSDC_IO_ABI_VERSION 3
+#define BSDC_IO_ABI_VERSION 4
 #define BSDC_IO_EFORMAT (-10) /* not BGZF/BAM, truncated, bad CRC */
 #define BSDC_IO_EIO (-11)     /* open/read/write failed */
 
@@ -76,6 +76,22 @@ void bsdc_bam_sizes_of(const bsdc_bam *b, bsdc_bam_sizes *s);
 int32_t bsdc_bam_copy(const bsdc_bam *b, const bsdc_bam_arrays *a);
 void bsdc_bam_free(bsdc_bam *b);
 
+/* Streaming reader (bounded memory): the file's records as a sequence of decoded chunks
+ * (bsdc_bam objects, read with bsdc_bam_sizes_of / bsdc_bam_copy, freed with bsdc_bam_free; names
+ * and MI ids are chunk-local).  A chunk holds at least min_bytes of record bytes (the rest of the
+ * file at its end) and ends where a cut is safe for a coordinate-sorted file: every record before
+ * the cut, and its mate, lies more than `slack` positions before the next record on that record's
+ * contig, or on an earlier contig.  Templates and MI families (which share their template's
+ * coordinates) then never straddle chunks, and each chunk's TemplateCoordinate keys sort before
+ * the next chunk's, so the chunks' family plans concatenate to the whole file's (tests/test_stream.py).
+ * read_size: compressed bytes read (and inflated in parallel) per refill.  *out = NULL at the end. */
+typedef struct bsdc_bam_stream bsdc_bam_stream;
+int32_t bsdc_bam_stream_open(const char *path, int32_t n_threads, int64_t read_size, bsdc_bam_stream **out);
+int32_t bsdc_bam_stream_fill(bsdc_bam_stream *s);
+int32_t bsdc_bam_stream_next(bsdc_bam_stream *s, int64_t min_bytes, int64_t slack, bsdc_bam **out);
+int32_t bsdc_bam_stream_header(const bsdc_bam_stream *s, bsdc_bam **out); /* header only, no records */
+void bsdc_bam_stream_close(bsdc_bam_stream *s);
+
 /* Records to write (n_rec entries; every *_off array has n_rec + 1 entries). */
 typedef struct {
     int64_t n_rec;
@@ -98,6 +114,15 @@ typedef struct {
 int32_t bsdc_bam_write(const char *path, const char *header_text, int64_t header_len, int32_t n_ref,
                        const int64_t *ref_name_off, const char *ref_name_buf, const int64_t *ref_len,
                        const bsdc_bam_records *r, int32_t level, int32_t n_threads);
+
+/* Streaming writer: the bytes bsdc_bam_write writes for all the records at once, written as
+ * records are added (whole BGZF blocks deflated in parallel as they fill). */
+typedef struct bsdc_bam_writer bsdc_bam_writer;
+int32_t bsdc_bam_writer_open(const char *path, const char *header_text, int64_t header_len, int32_t n_ref,
+                             const int64_t *ref_name_off, const char *ref_name_buf, const int64_t *ref_len,
+                             int32_t level, bsdc_bam_writer **out);
+int32_t bsdc_bam_writer_add(bsdc_bam_writer *w, const bsdc_bam_records *r, int32_t n_threads);
+int32_t bsdc_bam_writer_close(bsdc_bam_writer *w, int32_t n_threads);
 
 /* Paired FASTQ of records, as picard SamToFastq F=path1 F2=path2 writes them (the step after the
  * duplex call, main.snake.py:167-177; parity unpinned): "@name/1" or "/2", SEQ, "+", QUAL+33,

@@ -1,0 +1,107 @@
+"""End-to-end families/s of the file-level step 5 on the GPU box (not the bench metric): a
+synthetic coordinate-sorted C2 BAM + FASTA on local disk, then, each in a fresh child process
+(so that its peak RSS is its own):
+  whole   bam.step5: read the whole BAM, form every family, GPU batches, write the BAM
+  stream  bam.step5_stream: bounded chunks, reader / GPU / writer threads overlapped
+Both outputs are compared byte for byte.  Usage:
+  python profiles/e2e_stream.py [--families N] [--threads T] [--chunk-mb M] [--level L]"""
+import argparse
+import json
+import os
+import resource
+import subprocess
+import sys
+import tempfile
+import time
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, ROOT)
+
+
+def prep(args):
+    """The input files (synthetic data generated on the GPU, in this child only)."""
+    import numpy as np
+
+    from bsseqconsensusreads_amd import bam, synth
+    from bsseqconsensusreads_amd import records as R
+    s = synth.generate("C2", args.families, seed=42, device="cuda", genome_len=50_000_000)
+    raw = R.take(s.raw, np.lexsort((s.raw.pos, s.raw.tid)))
+    codes = R.unpack_nibbles(s.ref.packed, s.ref.n_nibbles)
+    with open(args.fa, "wb") as fh:
+        fh.write((">%s\n" % s.ref.names[0]).encode() + R.NT16_TO_ASCII[codes].tobytes() + b"\n")
+    hdr = bam.BamHeader("@HD\tVN:1.6\tSO:coordinate\n@SQ\tSN:%s\tLN:%d\n@RG\tID:x\tSM:s\tLB:L1\n" % (
+        s.ref.names[0], len(codes)), [s.ref.names[0]], np.asarray([len(codes)], np.int64))
+    bam.write_bam(args.inp, hdr, bam.records_to_bam(raw), level=args.level, threads=args.threads)
+    print(json.dumps({"records": int(raw.n)}))
+
+
+def child(args):
+    if args.mode == "prep":
+        return prep(args)
+    import torch  # noqa: F401  (the GPU runtime, as the CLI loads it)
+
+    from bsseqconsensusreads_amd import bam
+    from bsseqconsensusreads_amd.device import Engine
+    eng = Engine(0)
+    stats = {}
+    t0 = time.perf_counter()
+    if args.mode == "whole":
+        info = bam.step5(args.inp, args.fa, args.out, engine=eng, threads=args.threads, level=args.level)
+    else:
+        info = bam.step5_stream(args.inp, args.fa, args.out, engine=eng, threads=args.threads, level=args.level,
+                                chunk_bytes=args.chunk_mb << 20, stats=stats)
+    dt = time.perf_counter() - t0
+    eng.close()
+    rss = resource.getrusage(resource.RUSAGE_SELF).ru_maxrss / 1024  # MiB
+    print(json.dumps({"mode": args.mode, "seconds": round(dt, 3), "peak_rss_MiB": round(rss, 1),
+                      "stage_busy_s": stats, **info}))
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--families", type=int, default=1_000_000)
+    ap.add_argument("--threads", type=int, default=16)
+    ap.add_argument("--chunk-mb", type=int, default=256)
+    ap.add_argument("--level", type=int, default=5)
+    ap.add_argument("--mode", default=None)
+    ap.add_argument("--inp")
+    ap.add_argument("--fa")
+    ap.add_argument("--out")
+    a = ap.parse_args()
+    if a.mode:
+        return child(a)
+    # this process never touches the GPU: every GPU step runs in a child process
+    d = tempfile.mkdtemp(prefix="bsdc_e2es_")
+    t0 = time.perf_counter()
+    fa, inp = os.path.join(d, "g.fa"), os.path.join(d, "in.bam")
+    p = subprocess.run([sys.executable, os.path.abspath(__file__), "--mode", "prep", "--inp", inp, "--fa", fa,
+                        "--families", str(a.families), "--threads", str(a.threads), "--level", str(a.level)],
+                       stdout=subprocess.PIPE, text=True, timeout=900)
+    if p.returncode != 0:
+        print(p.stdout[-2000:], file=sys.stderr)
+        return p.returncode
+    n_rec = json.loads(p.stdout.strip().splitlines()[-1])["records"]
+    prep = time.perf_counter() - t0
+    res = {"families": a.families, "records": n_rec, "input_MB": round(os.path.getsize(inp) / 1e6, 1),
+           "host_threads": a.threads, "level": a.level, "chunk_MiB": a.chunk_mb, "prep_s": round(prep, 1)}
+    print("prepared", json.dumps(res), flush=True)
+    outs = {}
+    for mode in ("stream", "whole"):
+        out = os.path.join(d, mode + ".bam")
+        p = subprocess.run([sys.executable, os.path.abspath(__file__), "--mode", mode, "--inp", inp, "--fa", fa,
+                            "--out", out, "--threads", str(a.threads), "--chunk-mb", str(a.chunk_mb),
+                            "--level", str(a.level)], stdout=subprocess.PIPE, text=True, timeout=900)
+        if p.returncode != 0:
+            print(p.stdout[-2000:], file=sys.stderr)
+            return p.returncode
+        r = json.loads(p.stdout.strip().splitlines()[-1])
+        r["families_per_s"] = round(a.families / r["seconds"], 1)
+        res[mode] = r
+        outs[mode] = out
+    res["outputs_identical"] = open(outs["stream"], "rb").read() == open(outs["whole"], "rb").read()
+    print(json.dumps(res))
+    return 0
+
+
+if __name__ == "__main__":
+    sys.exit(main())

@@ -14,10 +14,14 @@ per = collections.defaultdict(lambda: collections.defaultdict(lambda: collection
 for f in sorted(glob.glob(d + "/p*/**/*counter_collection.csv", recursive=True)):
     for r in csv.DictReader(open(f)):
         per[r["Kernel_Name"]][(f, int(r["Dispatch_Id"]))][r["Counter_Name"]] += float(r["Counter_Value"])
-out = {}
+# every template instance of a kernel (k_large<true, 256>, <true, 512>, <false, 512>; one
+# dispatch per bucket) under its name: mean per dispatch x dispatches per launch set = per set
+grouped = collections.defaultdict(dict)
 for k, disp in per.items():
     m = re.search(r"(k_small|k_large)", k)
-    name = m.group(1) if m else k[:60]
+    grouped[m.group(1) if m else k[:60]].update({(k,) + key: v for key, v in disp.items()})
+out = {}
+for name, disp in grouped.items():
     sums = collections.defaultdict(float)
     cnt = collections.defaultdict(int)
     for _, cs in disp.items():
@@ -25,8 +29,6 @@ for k, disp in per.items():
             sums[c] += v
             cnt[c] += 1
     means = {c: sums[c] / cnt[c] for c in sums}
-    if name in out:  # k_large<true> / k_large<false>: keep the first seen
-        name = name + "_2"
     o = {"dispatches_per_counter": max(cnt.values()), "mean_per_dispatch": {c: round(v, 1) for c, v in sorted(means.items())}}
     if "SQ_WAVES" in means and means["SQ_WAVES"]:
         w = means["SQ_WAVES"]

@@ -1,0 +1,40 @@
+"""The streaming, pipelined file-level step 5 (bam.step5_stream: bounded-memory reader, C++ family
+formation per chunk, GPU batches, streaming writer) writes the bytes the whole-file step 5
+(bam.step5) writes, on a coordinate-sorted synthetic BAM cut into many chunks."""
+import numpy as np
+import pytest
+
+from bsseqconsensusreads_amd import bam, synth
+from bsseqconsensusreads_amd import records as R
+
+pytestmark = pytest.mark.gpu
+
+
+def _inputs(tmp_path, cfg, n_fam, messy, seed):
+    s = synth.generate(cfg, n_fam, seed=seed, device="cpu", genome_len=300_000)
+    raw = synth.messify(s.raw, frac=messy, seed=seed) if messy else s.raw
+    raw = R.take(raw, np.lexsort((raw.pos, raw.tid)))
+    text = "@HD\tVN:1.6\tSO:coordinate\n" + "".join("@SQ\tSN:%s\tLN:%d\n" % (n, l) for n, l in
+                                                    zip(s.ref.names, s.ref.lengths)) + "@RG\tID:A\tSM:s\tLB:L\n"
+    hdr = bam.BamHeader(text, list(s.ref.names), np.asarray(s.ref.lengths, np.int64))
+    inp = str(tmp_path / "in.bam")
+    bam.write_bam(inp, hdr, bam.records_to_bam(raw), level=1, threads=4)
+    fa = str(tmp_path / "g.fa")
+    codes = R.unpack_nibbles(s.ref.packed, s.ref.n_nibbles)
+    with open(fa, "wb") as fh:
+        fh.write((">%s\n" % s.ref.names[0]).encode() + R.NT16_TO_ASCII[codes].tobytes() + b"\n")
+    return inp, fa
+
+
+@pytest.mark.parametrize("cfg,messy", [("C2", 0.0), ("C1", 0.2)])
+def test_stream_writes_the_whole_file_bytes(engine, tmp_path, cfg, messy):
+    inp, fa = _inputs(tmp_path, cfg, 1200, messy, 17)
+    a, b = str(tmp_path / "whole.bam"), str(tmp_path / "stream.bam")
+    ia = bam.step5(inp, fa, a, engine=engine, threads=4, level=5)
+    stats = {}
+    ib = bam.step5_stream(inp, fa, b, engine=engine, threads=4, level=5, chunk_bytes=80_000, slack=2000,
+                          stats=stats)
+    assert ib["chunks"] > 3
+    for k in ("records_in", "families", "families_emitted", "records_out"):
+        assert ia[k] == ib[k], k
+    assert open(a, "rb").read() == open(b, "rb").read()
