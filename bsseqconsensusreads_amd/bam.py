@@ -85,6 +85,12 @@ def _load():
     lib.bsdc_bam_writer_add.restype = C.c_int32
     lib.bsdc_bam_writer_close.argtypes = [_P, C.c_int32]
     lib.bsdc_bam_writer_close.restype = C.c_int32
+    lib.bsdc_fastq_writer_open.argtypes = [C.c_char_p, C.c_char_p, C.c_int32, C.POINTER(_P)]
+    lib.bsdc_fastq_writer_open.restype = C.c_int32
+    lib.bsdc_fastq_writer_add.argtypes = [_P, C.POINTER(_Records), C.c_int32]
+    lib.bsdc_fastq_writer_add.restype = C.c_int32
+    lib.bsdc_fastq_writer_close.argtypes = [_P, C.c_int32]
+    lib.bsdc_fastq_writer_close.restype = C.c_int32
     lib.bsdc_bam_write.argtypes = [C.c_char_p, C.c_char_p, C.c_int64, C.c_int32, _P, _P, _P, C.POINTER(_Records),
                                    C.c_int32, C.c_int32]
     lib.bsdc_bam_write.restype = C.c_int32
@@ -97,6 +103,12 @@ def _load():
     lib.bsdc_consensus_tags.argtypes = [C.c_int64, _P, _P, _P, C.c_int32, C.c_int32, _P, _P, _P, _P, _P, _P,
                                         C.c_int32]
     lib.bsdc_consensus_tags.restype = C.c_int64
+    lib.bsdc_table_concat.argtypes = [C.c_int64, C.c_int32, C.POINTER(_P), C.POINTER(_P), _P, _P, _P, C.c_int32]
+    lib.bsdc_table_concat.restype = C.c_int64
+    lib.bsdc_table_rank.argtypes = [C.c_int64, _P, _P, _P, C.c_int32]
+    lib.bsdc_table_rank.restype = None
+    lib.bsdc_table_take.argtypes = [C.c_int64, _P, _P, _P, _P, _P, C.c_int32]
+    lib.bsdc_table_take.restype = C.c_int64
     if lib.bsdc_io_abi_version() != BSDC_IO_ABI_VERSION:
         raise RuntimeError("libbsdc_io ABI %d != %d" % (lib.bsdc_io_abi_version(), BSDC_IO_ABI_VERSION))
     _lib = lib
@@ -234,7 +246,7 @@ def read_bam_header(path: str) -> BamHeader:
 
 
 def stream_bam(path: str, threads: int = 0, chunk_bytes: int = DEFAULT_CHUNK_BYTES, slack: int = DEFAULT_SLACK,
-               read_size: int = 64 << 20):
+               read_size: int = 8 << 20):
     """Chunks of a coordinate-sorted BAM in bounded memory: yields (BamHeader, RawRecords) per chunk,
     cut where no template or MI family straddles two chunks (include/bsdc_io.h,
     bsdc_bam_stream_next); names and MI ids are chunk-local."""
@@ -308,36 +320,56 @@ def _ascii_int(x: np.ndarray):
 
 
 def _concat_fields(parts, n):
-    """Per-record byte fields (each (buf, off) or a constant bytes) -> one packed StringTable."""
-    lens = np.zeros(n, np.int64)
-    for p in parts:
-        lens += len(p) if isinstance(p, bytes) else (p[1][1:] - p[1][:-1])
-    off = np.zeros(n + 1, np.int64)
-    off[1:] = np.cumsum(lens)
-    buf = np.zeros(int(off[-1]), np.uint8)
-    cur = off[:-1].copy()
-    for p in parts:
+    """Per-record byte fields (each (buf, off) or a constant bytes) -> one packed StringTable
+    (libbsdc_io bsdc_table_concat: parallel copies, no per-byte index arrays)."""
+    lib = _load()
+    k = len(parts)
+    offs = (_P * k)()
+    bufs = (_P * k)()
+    clen = np.zeros(k, np.int64)
+    keep = []
+    for j, p in enumerate(parts):
         if isinstance(p, bytes):
-            if p:
-                b = np.frombuffer(p, np.uint8)
-                buf[(cur[:, None] + np.arange(len(p))[None, :]).reshape(-1)] = np.tile(b, n)
-                cur += len(p)
+            b = np.frombuffer(p if p else b"\0", np.uint8).copy()
+            keep.append(b)
+            offs[j], bufs[j], clen[j] = None, _ptr(b), len(p)
         else:
-            pb, po = p
-            ln = po[1:] - po[:-1]
-            dst = np.repeat(cur - po[:-1], ln) + np.arange(int(ln.sum()), dtype=np.int64)
-            buf[dst] = pb
-            cur += ln
-    return StringTable(buf, off)
+            pb = np.ascontiguousarray(p[0], np.uint8)
+            po = np.ascontiguousarray(p[1], np.int64)
+            if pb.size == 0:
+                pb = np.zeros(1, np.uint8)
+            keep += [pb, po]
+            offs[j], bufs[j] = _ptr(po), _ptr(pb)
+    off = np.zeros(n + 1, np.int64)
+    total = lib.bsdc_table_concat(int(n), k, offs, bufs, _ptr(clen), _ptr(off), None, 0)
+    buf = np.empty(max(int(total), 1), np.uint8)
+    lib.bsdc_table_concat(int(n), k, offs, bufs, _ptr(clen), _ptr(off), _ptr(buf), 0)
+    return StringTable(buf[:int(total)], off)
+
+
+def table_ranks(t: StringTable) -> np.ndarray:
+    """Byte-order rank of every entry of a packed table (equal entries share a rank; libbsdc_io)."""
+    lib = _load()
+    n = len(t)
+    rank = np.zeros(max(n, 1), np.int64)
+    if n:
+        buf = np.ascontiguousarray(t.buf, np.uint8) if t.buf.size else np.zeros(1, np.uint8)
+        lib.bsdc_table_rank(n, _ptr(np.ascontiguousarray(t.off, np.int64)), _ptr(buf), _ptr(rank), 0)
+    return rank[:n]
 
 
 def _take_table(t: StringTable, idx: np.ndarray) -> StringTable:
-    """Entries idx[0], idx[1], ... of a packed table."""
-    ln = (t.off[1:] - t.off[:-1])[idx]
-    off = np.zeros(idx.shape[0] + 1, np.int64)
-    off[1:] = np.cumsum(ln)
-    src = np.repeat(t.off[:-1][idx] - off[:-1], ln) + np.arange(int(off[-1]), dtype=np.int64)
-    return StringTable(t.buf[src], off)
+    """Entries idx[0], idx[1], ... of a packed table (libbsdc_io bsdc_table_take)."""
+    lib = _load()
+    idx = np.ascontiguousarray(idx, np.int64)
+    n = int(idx.shape[0])
+    src_off = np.ascontiguousarray(t.off, np.int64)
+    src = np.ascontiguousarray(t.buf, np.uint8) if t.buf.size else np.zeros(1, np.uint8)
+    off = np.zeros(n + 1, np.int64)
+    total = lib.bsdc_table_take(n, _ptr(idx), _ptr(src_off), _ptr(src), _ptr(off), None, 0)
+    buf = np.empty(max(int(total), 1), np.uint8)
+    lib.bsdc_table_take(n, _ptr(idx), _ptr(src_off), _ptr(src), _ptr(off), _ptr(buf), 0)
+    return StringTable(buf[:int(total)], off)
 
 
 def take_records(recs: "OutRecordsBam", idx: np.ndarray) -> "OutRecordsBam":
@@ -519,6 +551,30 @@ class BamWriter:
                 raise OSError("%s: %s" % (self.path, self.lib.bsdc_io_last_error().decode()))
 
 
+class FastqWriter:
+    """Streaming paired-FASTQ writer (bsdc_fastq_writer): the bytes write_fastq writes for all the
+    records at once; every add holds whole pairs."""
+
+    def __init__(self, path1: str, path2: str, level: int = 6):
+        self.lib = _load()
+        self.path = path1
+        self.h = _P()
+        if self.lib.bsdc_fastq_writer_open(path1.encode(), path2.encode(), int(level), C.byref(self.h)) != 0:
+            raise OSError("%s: %s" % (path1, self.lib.bsdc_io_last_error().decode()))
+
+    def add(self, recs: OutRecordsBam, threads: int = 0):
+        keep = []
+        r = _records_struct(recs, keep)
+        if self.lib.bsdc_fastq_writer_add(self.h, C.byref(r), int(threads)) != 0:
+            raise OSError("%s: %s" % (self.path, self.lib.bsdc_io_last_error().decode()))
+
+    def close(self, threads: int = 0):
+        if self.h:
+            h, self.h = self.h, _P()
+            if self.lib.bsdc_fastq_writer_close(h, int(threads)) != 0:
+                raise OSError("%s: %s" % (self.path, self.lib.bsdc_io_last_error().decode()))
+
+
 def read_fasta(path: str, header: BamHeader) -> R.Reference:
     """FASTA -> the packed reference in the BAM header's tid order (contigs the FASTA lacks are
     absent: tool 1 then converts against N, tools/1.convert_AG_to_CT.py:103-117)."""
@@ -618,13 +674,13 @@ def duplex_records(cons, raw: R.RawRecords, prefix: str, threads: int = 0, molec
     # names "prefix:MI" and aux RG/MI/RX, both mates of a family alike (packed tables, no per-family
     # Python objects for the byte work)
     mi_ids = cons.fam_mi[em].astype(np.int64)
-    uniq, inv = np.unique(mi_ids, return_inverse=True)
-    mt = StringTable.from_list([(lambda m: m if isinstance(m, bytes) else m.encode())(raw.mi_names[int(i)])
-                                for i in uniq])
-    mlen = mt.off[1:] - mt.off[:-1]
-    mi = (mt.buf[np.repeat(mt.off[:-1][inv] - np.concatenate([[0], np.cumsum(mlen[inv])[:-1]]), mlen[inv])
-                 + np.arange(int(mlen[inv].sum()), dtype=np.int64)] if F else np.zeros(0, np.uint8),
-          np.concatenate([[0], np.cumsum(mlen[inv])]).astype(np.int64))
+    if isinstance(raw.mi_names, StringTable):  # decoded BAM: a packed table already
+        mt = _take_table(raw.mi_names, mi_ids)
+    else:
+        uniq, inv = np.unique(mi_ids, return_inverse=True)
+        mt = _take_table(StringTable.from_list([(lambda m: m if isinstance(m, bytes) else m.encode())(
+            raw.mi_names[int(i)]) for i in uniq]), inv)
+    mi = (mt.buf, mt.off)
     if width > 0:
         rl = rx_len[em].astype(np.int64)
         has = rl > 0
@@ -708,8 +764,9 @@ def step5(in_bam: str, fasta: str, out_bam: Optional[str], engine=None, prefix: 
             "families_emitted": int(((cons.status & 1) != 0).sum()), "records_out": recs.n}
 
 
-def step5_stream(in_bam: str, fasta: str, out_bam: str, engine=None, prefix: Optional[str] = None, threads: int = 0,
-                 level: int = 6, tags: bool = True, chunk_bytes: int = DEFAULT_CHUNK_BYTES, slack: int = DEFAULT_SLACK,
+def step5_stream(in_bam: str, fasta: str, out_bam: Optional[str], engine=None, prefix: Optional[str] = None,
+                 threads: int = 0, level: int = 6, fastq: Optional[Tuple[str, str]] = None, tags: bool = True,
+                 chunk_bytes: int = DEFAULT_CHUNK_BYTES, slack: int = DEFAULT_SLACK,
                  batch_bases: Optional[int] = None, stats: Optional[dict] = None) -> dict:
     """step5 in bounded memory, pipelined: a reader thread decodes the next chunk of the
     coordinate-sorted input (stream_bam: cut where no template or MI family straddles) and forms
@@ -730,7 +787,7 @@ def step5_stream(in_bam: str, fasta: str, out_bam: str, engine=None, prefix: Opt
     outs: "queue.Queue" = queue.Queue(maxsize=1)
     err: list = []
     info = {"records_in": 0, "families": 0, "families_emitted": 0, "records_out": 0, "chunks": 0}
-    T = {"decode+plan": 0.0, "gpu": 0.0, "records+encode": 0.0}
+    T = {"decode+plan": 0.0, "gpu": 0.0, "records": 0.0, "encode": 0.0}
     first = {}
 
     def reader():
@@ -746,23 +803,28 @@ def step5_stream(in_bam: str, fasta: str, out_bam: str, engine=None, prefix: Opt
             chunks.put(None)
 
     def writer():
-        w = None
         try:
+            w = BamWriter(out_bam, output_header(first["header"]), level) if out_bam is not None else None
+            fq = FastqWriter(fastq[0], fastq[1], level) if fastq is not None else None
             while True:
                 item = outs.get()
                 if item is None:
                     break
                 cons, raw = item
                 t0 = time.perf_counter()
-                if w is None:
-                    w = BamWriter(out_bam, output_header(first["header"]), level)
                 recs = duplex_records(cons, raw, first["prefix"], threads)
-                w.add(recs, threads)
+                t1 = time.perf_counter()
+                if w is not None:
+                    w.add(recs, threads)
+                if fq is not None:
+                    fq.add(recs, threads)
                 info["records_out"] += recs.n
-                T["records+encode"] += time.perf_counter() - t0
-            if w is None:
-                w = BamWriter(out_bam, output_header(first["header"]), level)
-            w.close(threads)
+                T["records"] += t1 - t0
+                T["encode"] += time.perf_counter() - t1
+            if w is not None:
+                w.close(threads)
+            if fq is not None:
+                fq.close(threads)
         except BaseException as e:  # noqa: BLE001
             err.append(e)
             while outs.get() is not None:  # drain so the main thread never blocks
@@ -788,11 +850,12 @@ def step5_stream(in_bam: str, fasta: str, out_bam: str, engine=None, prefix: Opt
                     break
                 raw, plan = item
                 t0 = time.perf_counter()
+                tg = tags and out_bam is not None  # the FASTQ pair carries no tags
                 if plan.split_ext:
-                    cons = pipeline.run_step5(eng, raw, tags=tags, batch_bases=batch_bases)[0]
+                    cons = pipeline.run_step5(eng, raw, tags=tg, batch_bases=batch_bases)[0]
                 else:
                     cons = pipeline.concat_consensus(
-                        pipeline.run_ranges(eng, plan, pipeline.plan_ranges(plan, batch_bases), mode, tags))
+                        pipeline.run_ranges(eng, plan, pipeline.plan_ranges(plan, batch_bases), mode, tg))
                 T["gpu"] += time.perf_counter() - t0
                 info["records_in"] += raw.n
                 info["families"] += int(cons.status.shape[0])

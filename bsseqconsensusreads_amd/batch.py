@@ -317,6 +317,9 @@ def lex_rank(strings, ids: np.ndarray) -> np.ndarray:
     ids = np.asarray(ids, np.int64)
     if hasattr(strings, "lex_key"):  # synthetic names: computed, not materialised
         return strings.lex_key(ids)
+    from .bam import StringTable, table_ranks
+    if isinstance(strings, StringTable):  # a decoded BAM's packed table: ranked in C++
+        return table_ranks(strings)[ids] if ids.shape[0] else np.zeros(0, np.int64)
     if ids.shape[0] == 0:
         return np.zeros(0, np.int64)
     u, inv = np.unique(ids, return_inverse=True)

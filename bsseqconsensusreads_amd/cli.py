@@ -10,6 +10,8 @@ OUT.bam may be '-' to skip the BAM when only the FASTQ pair is wanted.  Errors e
 the message on stderr, so Snakemake aborts the rule and removes partial outputs, as it does for
 the reference tools (tools/2.extend_gap.py:179-180 raises on a record without MI).
 
+step5 on one GPU streams (--stream true, the default): bounded memory whatever the input size,
+decode / GPU / encode overlapped, output identical to the whole-file path (bam.step5_stream).
 step5 --gpus N: one process per GPU (spawned here, or under torch.distributed.run); the family
 batches are dealt to the ranks and rank 0 writes the outputs, identical to --gpus 1
 (bam.consensus_sharded).  --devices maps ranks to device ids (default rank r -> GPU r).
@@ -41,6 +43,10 @@ def parse(argv):
             p.add_argument("--gpus", type=int, default=1, help="one process per GPU, family batches dealt to them")
             p.add_argument("--devices", default=None, help="comma-separated device id per rank (default 0..gpus-1)")
             p.add_argument("--batch-bases", type=int, default=None, help="device batch budget in bases")
+            p.add_argument("--stream", default="true", choices=["true", "false"],
+                           help="bounded-memory pipelined step (bam.step5_stream; coordinate-sorted input, one GPU); "
+                                "false = read the whole BAM first (bam.step5)")
+            p.add_argument("--chunk-mb", type=int, default=256, help="--stream: record MiB per chunk")
         p.add_argument("--output-per-base-tags", default="true", choices=["true", "false"],
                        help="fgbio's consensus tags (per-read and per-base statistics); off = name/SEQ/QUAL/RG/MI/RX")
     a = ap.parse_args(argv)
@@ -77,7 +83,11 @@ def main(argv=None) -> int:
         dist = shard.init("gloo") if world > 1 else None  # host gather of the batch outputs only
         eng = Engine(device)
         try:
-            if a.cmd == "step5":
+            if a.cmd == "step5" and world == 1 and a.stream == "true":
+                info = bam.step5_stream(a.input, a.reference, out, eng, a.read_name_prefix, a.threads, a.compression,
+                                        fq, tags=a.output_per_base_tags == "true", chunk_bytes=a.chunk_mb << 20,
+                                        batch_bases=a.batch_bases)
+            elif a.cmd == "step5":
                 info = bam.step5(a.input, a.reference, out, eng, a.read_name_prefix, a.threads, a.compression, fq,
                                  tags=a.output_per_base_tags == "true", batch_bases=a.batch_bases, dist=dist)
             else:

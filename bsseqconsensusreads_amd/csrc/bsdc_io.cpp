@@ -21,6 +21,7 @@
 #include <vector>
 #ifdef _OPENMP
 #include <omp.h>
+#include <parallel/algorithm>
 #endif
 
 namespace {
@@ -497,58 +498,53 @@ namespace {
 int32_t stream_split(bsdc_bam_stream *s) {
     const uint8_t *d = s->pend.data();
     const int64_t dn = (int64_t)s->pend.size();
+    // record boundaries (sequential), then each record's family key and positions (parallel)
+    std::vector<int64_t> starts;
     int64_t p = 0;
     while (p + 4 <= dn) {
         const int64_t bs = rd32(d + p);
         if (bs < 32) return fail(BSDC_IO_EFORMAT, "truncated BAM record");
         if (p + 4 + bs > dn) break;
-        const uint8_t *r = d + p;
+        starts.push_back(p);
+        p += 4 + bs;
+    }
+    const int64_t nr = (int64_t)starts.size();
+    struct Parsed {
+        std::string_view mi;
+        int64_t c, e;
+        TcKey key;
+    };
+    std::vector<Parsed> P((size_t)nr);
+    int bad = 0;
+#pragma omp parallel for schedule(static) reduction(| : bad)
+    for (int64_t k = 0; k < nr; k++) {
+        const uint8_t *r = d + starts[(size_t)k];
+        const int64_t bs = rd32(r);
         const uint8_t *end = r + 4 + bs;
         const int l_name = r[12];
         const int n_cig = rd16(r + 16);
         const int32_t l_seq = rdi32(r + 20);
         const int64_t body = 36 + (int64_t)l_name + 4 * (int64_t)n_cig + ((int64_t)l_seq + 1) / 2 + (int64_t)l_seq;
-        if (l_seq < 0 || l_name < 1 || body > 4 + bs) return fail(BSDC_IO_EFORMAT, "malformed BAM record (lengths or aux)");
+        if (l_seq < 0 || l_name < 1 || body > 4 + bs) {
+            bad |= 1;
+            continue;
+        }
         std::string_view mi, mc;
         for (const uint8_t *a = r + body; a + 3 <= end;) {
             const int64_t vs = aux_value_size(a, end);
-            if (vs < 0 || vs > (end - a) - 3) return fail(BSDC_IO_EFORMAT, "malformed BAM record (lengths or aux)");
+            if (vs < 0 || vs > (end - a) - 3) {
+                bad |= 1;
+                break;
+            }
             if (a[0] == 'M' && a[1] == 'I' && a[2] == 'Z') mi = std::string_view((const char *)a + 3, (size_t)vs - 1);
             if (a[0] == 'M' && a[1] == 'C' && a[2] == 'Z') mc = std::string_view((const char *)a + 3, (size_t)vs - 1);
             a += 3 + vs;
         }
         const size_t slash = mi.find('/');
         if (slash != std::string_view::npos) mi = mi.substr(0, slash);
-        int32_t fam;
-        if (!mi.empty()) {
-            auto it = s->fam_of.find(std::string(mi));
-            if (it == s->fam_of.end() || s->fams[(size_t)it->second].n == 0) {
-                if (!s->free_fams.empty()) {
-                    fam = s->free_fams.back();
-                    s->free_fams.pop_back();
-                    s->fams[(size_t)fam] = StreamFam();
-                } else {
-                    fam = (int32_t)s->fams.size();
-                    s->fams.emplace_back();
-                }
-                s->fam_of[std::string(mi)] = fam;
-            } else {
-                fam = it->second;
-            }
-        } else {
-            if (!s->free_fams.empty()) {
-                fam = s->free_fams.back();
-                s->free_fams.pop_back();
-                s->fams[(size_t)fam] = StreamFam();
-            } else {
-                fam = (int32_t)s->fams.size();
-                s->fams.emplace_back();
-            }
-        }
         const int32_t tid = rdi32(r + 4), pos = rdi32(r + 8), ntid = rdi32(r + 24), npos = rdi32(r + 28);
         const int flag = rd16(r + 18);
         const int64_t c = coord(tid, pos);
-        const int64_t e = ntid >= 0 ? std::max(c, coord(ntid, npos)) : c;
         // the template's key (batch.template_coordinate_order): the lower end's contig, then the
         // other end's (BIG for an unpaired record or unmapped mate), then the lower end's unclipped
         // 5' position -- from the input's cigar and MC, so within kKeyDelta of the key of the
@@ -601,17 +597,51 @@ int32_t stream_split(bsdc_bam_stream *s) {
         else if (tid == ntid) key = {(t1 << 32) | t1, std::min(p_own, p_mate)};
         else if (tid >= 0 && tid < ntid) key = {(t1 << 32) | (int64_t)ntid, p_own};
         else key = {((int64_t)ntid << 32) | t1, p_mate};
-        StreamFam &F = s->fams[(size_t)fam];
-        F.lo = std::min(F.lo, c);
-        F.hi = std::max(F.hi, e);
-        F.klo = std::min(F.klo, key);
-        F.khi = std::max(F.khi, key);
-        F.n++;
-        s->cursor = std::max(s->cursor, c);
-        s->recs.push_back(StreamRec{(int64_t)s->buf.size(), 4 + bs, fam});
-        s->buf.insert(s->buf.end(), r, end);
-        p += 4 + bs;
+        P[(size_t)k] = Parsed{mi, c, ntid >= 0 ? std::max(c, coord(ntid, npos)) : c, key};
     }
+    if (bad) return fail(BSDC_IO_EFORMAT, "malformed BAM record (lengths or aux)");
+    // families (sequential: the MI map), then the records' bytes in one copy
+    auto new_fam = [&]() {
+        int32_t fam;
+        if (!s->free_fams.empty()) {
+            fam = s->free_fams.back();
+            s->free_fams.pop_back();
+            s->fams[(size_t)fam] = StreamFam();
+        } else {
+            fam = (int32_t)s->fams.size();
+            s->fams.emplace_back();
+        }
+        return fam;
+    };
+    const int64_t base = (int64_t)s->buf.size();
+    for (int64_t k = 0; k < nr; k++) {
+        const Parsed &q = P[(size_t)k];
+        if (q.c < s->cursor)
+            return fail(BSDC_IO_EFORMAT, "input is not coordinate-sorted (the streaming step needs the "
+                                         "coordinate order of the step-5 input; read it whole instead)");
+        int32_t fam;
+        if (!q.mi.empty()) {
+            auto it = s->fam_of.find(std::string(q.mi));
+            if (it == s->fam_of.end() || s->fams[(size_t)it->second].n == 0) {
+                fam = new_fam();
+                s->fam_of[std::string(q.mi)] = fam;
+            } else {
+                fam = it->second;
+            }
+        } else {
+            fam = new_fam();  // a record without MI: a family of its own
+        }
+        StreamFam &F = s->fams[(size_t)fam];
+        F.lo = std::min(F.lo, q.c);
+        F.hi = std::max(F.hi, q.e);
+        F.klo = std::min(F.klo, q.key);
+        F.khi = std::max(F.khi, q.key);
+        F.n++;
+        s->cursor = std::max(s->cursor, q.c);
+        const int64_t len = (k + 1 < nr ? starts[(size_t)k + 1] : p) - starts[(size_t)k];
+        s->recs.push_back(StreamRec{base + starts[(size_t)k], len, fam});
+    }
+    s->buf.insert(s->buf.end(), s->pend.begin(), s->pend.begin() + p);
     s->pend.erase(s->pend.begin(), s->pend.begin() + p);
     return 0;
 }
@@ -637,9 +667,8 @@ int32_t bsdc_bam_stream_next(bsdc_bam_stream *s, int64_t min_bytes, int64_t slac
         if (end && !s->pend.empty()) return fail(BSDC_IO_EFORMAT, "truncated BAM record");
         take.assign(s->fams.size(), 0);
         int64_t bytes = 0;
-        if (end) {
-            for (auto &r : s->recs) take[(size_t)r.fam] = 1;
-            bytes = (int64_t)s->buf.size();
+        if (end) {  // every family is complete and nothing is left to read
+            for (size_t m = 0; m < s->fams.size(); m++) take[m] = s->fams[m].n > 0;
         } else if (s->cursor != INT64_MIN) {
             const int64_t ct = s->cursor >> 32, cp = s->cursor & 0xFFFFFFFFll;
             const int64_t ctid = s->cursor >= INT64_MAX / 4 ? kBigTid : ct;
@@ -666,7 +695,26 @@ int32_t bsdc_bam_stream_next(bsdc_bam_stream *s, int64_t min_bytes, int64_t slac
                 const StreamFam &F = s->fams[m];
                 take[m] = F.n > 0 && F.hi + slack < s->cursor && hi_of(F) < T;
             }
-            for (auto &r : s->recs) bytes += take[(size_t)r.fam] ? r.len : 0;
+        }
+        {
+            // bounded chunks: of the families that may go, only a key prefix of about min_bytes,
+            // cut between two families whose key ranges do not meet (the rest stays for the next
+            // call, where it may go again)
+            std::vector<int64_t> fb(s->fams.size(), 0);
+            for (auto &r : s->recs) fb[(size_t)r.fam] += take[(size_t)r.fam] ? r.len : 0;
+            std::vector<int32_t> ord;
+            for (size_t m = 0; m < s->fams.size(); m++)
+                if (take[m]) ord.push_back((int32_t)m);
+            std::sort(ord.begin(), ord.end(), [&](int32_t a, int32_t b) { return s->fams[(size_t)a].klo < s->fams[(size_t)b].klo; });
+            TcKey reach{INT64_MIN, INT64_MIN};
+            size_t i = 0;
+            for (; i < ord.size(); i++) {
+                const StreamFam &F = s->fams[(size_t)ord[i]];
+                if (bytes > 0 && bytes >= min_bytes && reach < TcKey{F.klo.first, F.klo.second - 2 * kKeyDelta}) break;
+                bytes += fb[(size_t)ord[i]];
+                reach = std::max(reach, F.khi);
+            }
+            for (; i < ord.size(); i++) take[(size_t)ord[i]] = 0;
         }
         if (end || (bytes > 0 && bytes >= min_bytes)) {
             if (bytes == 0) return 0;  // the end of the stream
@@ -1299,9 +1347,10 @@ extern "C" int64_t bsdc_consensus_tags(int64_t n, const int64_t *row_a, const in
     return off[n];
 }
 
-extern "C" int32_t bsdc_fastq_write(const char *path1, const char *path2, const bsdc_bam_records *r, int32_t level,
-                                    int32_t n_threads) {
-    set_threads(n_threads);
+namespace {
+// Paired FASTQ text of records appended to buf[0] (first of pair) / buf[1] (second), as
+// bsdc_fastq_write formats it; the pairing checks of include/bsdc_io.h.
+int32_t format_fastq(const bsdc_bam_records *r, std::vector<uint8_t> *buf) {
     const int64_t nr = r->n_rec;
     // record k -> its file (0: first of pair, 1: second) or -1 (not written); pairs must be adjacent
     std::vector<int8_t> dst((size_t)nr, -1);
@@ -1327,7 +1376,7 @@ extern "C" int32_t bsdc_fastq_write(const char *path1, const char *path2, const 
     if (want) return fail(BSDC_IO_EFORMAT, "a first-of-pair record has no mate");
     // "@name/N\nSEQ\n+\nQUAL\n" per record, sizes -> offsets per file -> parallel format
     std::vector<int64_t> off[2] = {std::vector<int64_t>((size_t)nr + 1), std::vector<int64_t>((size_t)nr + 1)};
-    int64_t tot[2] = {0, 0};
+    int64_t tot[2] = {(int64_t)buf[0].size(), (int64_t)buf[1].size()};
     for (int64_t k = 0; k < nr; k++) {
         off[0][(size_t)k] = tot[0];
         off[1][(size_t)k] = tot[1];
@@ -1336,7 +1385,8 @@ extern "C" int32_t bsdc_fastq_write(const char *path1, const char *path2, const 
         const int64_t ln = r->name_off[k + 1] - r->name_off[k], ls = r->seq_off[k + 1] - r->seq_off[k];
         tot[d] += 1 + ln + 2 + 1 + ls + 1 + 2 + ls + 1;
     }
-    std::vector<uint8_t> buf[2] = {std::vector<uint8_t>((size_t)tot[0]), std::vector<uint8_t>((size_t)tot[1])};
+    buf[0].resize((size_t)tot[0]);
+    buf[1].resize((size_t)tot[1]);
 #pragma omp parallel for schedule(static)
     for (int64_t k = 0; k < nr; k++) {
         const int d = dst[(size_t)k];
@@ -1358,11 +1408,137 @@ extern "C" int32_t bsdc_fastq_write(const char *path1, const char *path2, const 
         for (int64_t i = 0; i < ls; i++) *p++ = (uint8_t)(33 + (rev ? q[ls - 1 - i] : q[i]));
         *p++ = '\n';
     }
+    return 0;
+}
+}  // namespace
+
+extern "C" int32_t bsdc_fastq_write(const char *path1, const char *path2, const bsdc_bam_records *r, int32_t level,
+                                    int32_t n_threads) {
+    set_threads(n_threads);
+    std::vector<uint8_t> buf[2];
+    const int32_t rc = format_fastq(r, buf);
+    if (rc != 0) return rc;
     for (int d = 0; d < 2; d++) {
-        const int32_t rc = write_bgzf(d == 0 ? path1 : path2, buf[d], level);
-        if (rc != 0) return rc;
+        const int32_t rc2 = write_bgzf(d == 0 ? path1 : path2, buf[d], level);
+        if (rc2 != 0) return rc2;
     }
     return 0;
+}
+
+// streaming paired-FASTQ writer: the bytes of bsdc_fastq_write over all the records at once
+struct bsdc_fastq_writer {
+    FILE *f[2] = {nullptr, nullptr};
+    int32_t level = 6;
+    std::vector<uint8_t> tail[2];
+};
+
+extern "C" int32_t bsdc_fastq_writer_open(const char *path1, const char *path2, int32_t level, bsdc_fastq_writer **out) {
+    *out = nullptr;
+    auto *w = new bsdc_fastq_writer();
+    w->level = level;
+    for (int d = 0; d < 2; d++) {
+        w->f[d] = fopen(d == 0 ? path1 : path2, "wb");
+        if (!w->f[d]) {
+            if (d == 1) fclose(w->f[0]);
+            delete w;
+            return fail(BSDC_IO_EIO, std::string("cannot create ") + (d == 0 ? path1 : path2));
+        }
+    }
+    *out = w;
+    return 0;
+}
+
+extern "C" int32_t bsdc_fastq_writer_add(bsdc_fastq_writer *w, const bsdc_bam_records *r, int32_t n_threads) {
+    set_threads(n_threads);
+    int32_t rc = format_fastq(r, w->tail);
+    if (rc != 0) return rc;
+    for (int d = 0; d < 2; d++) {
+        const int64_t whole = ((int64_t)w->tail[d].size() / kBlock) * kBlock;
+        if (whole > 0) {
+            rc = deflate_write(w->f[d], w->tail[d].data(), whole, w->level);
+            if (rc != 0) return rc;
+            w->tail[d].erase(w->tail[d].begin(), w->tail[d].begin() + whole);
+        }
+    }
+    return 0;
+}
+
+extern "C" int32_t bsdc_fastq_writer_close(bsdc_fastq_writer *w, int32_t n_threads) {
+    if (!w) return 0;
+    set_threads(n_threads);
+    int32_t rc = 0;
+    for (int d = 0; d < 2; d++) {
+        if (rc == 0) rc = deflate_write(w->f[d], w->tail[d].data(), (int64_t)w->tail[d].size(), w->level);
+        if (rc == 0 && fwrite(kBgzfEof, 1, 28, w->f[d]) != 28) rc = fail(BSDC_IO_EIO, "BGZF write failed");
+        if (fclose(w->f[d]) != 0 && rc == 0) rc = fail(BSDC_IO_EIO, "BGZF close failed");
+    }
+    delete w;
+    return rc;
+}
+
+// Packed byte tables (entry r of a table = buf[off[r], off[r + 1])): per entry, the concatenation
+// of k parts (a table, or a constant: off NULL, buf const_len bytes).  out_buf NULL: fills out_off
+// [n + 1] and returns the total; else fills out_buf in parallel.
+extern "C" int64_t bsdc_table_concat(int64_t n, int32_t k, const int64_t *const *offs, const uint8_t *const *bufs,
+                                     const int64_t *const_len, int64_t *out_off, uint8_t *out_buf, int32_t n_threads) {
+    set_threads(n_threads);
+    if (!out_buf) {
+        int64_t t = 0;
+        for (int64_t r = 0; r < n; r++) {
+            out_off[r] = t;
+            for (int32_t j = 0; j < k; j++) t += offs[j] ? offs[j][r + 1] - offs[j][r] : const_len[j];
+        }
+        out_off[n] = t;
+        return t;
+    }
+#pragma omp parallel for schedule(static)
+    for (int64_t r = 0; r < n; r++) {
+        uint8_t *d = out_buf + out_off[r];
+        for (int32_t j = 0; j < k; j++) {
+            const int64_t l = offs[j] ? offs[j][r + 1] - offs[j][r] : const_len[j];
+            memcpy(d, offs[j] ? bufs[j] + offs[j][r] : bufs[j], (size_t)l);
+            d += l;
+        }
+    }
+    return out_off[n];
+}
+
+// rank[i] = byte-order rank of entry i of a packed table among its entries (equal entries share a
+// rank): the TemplateCoordinate key's MI and name components (batch.lex_rank).
+extern "C" void bsdc_table_rank(int64_t n, const int64_t *off, const uint8_t *buf, int64_t *rank, int32_t n_threads) {
+    set_threads(n_threads);
+    std::vector<int64_t> ord((size_t)n);
+    for (int64_t i = 0; i < n; i++) ord[(size_t)i] = i;
+    auto sv = [&](int64_t i) { return std::string_view((const char *)buf + off[i], (size_t)(off[i + 1] - off[i])); };
+    auto less = [&](int64_t a, int64_t b) { return sv(a) < sv(b); };
+#ifdef _OPENMP
+    __gnu_parallel::sort(ord.begin(), ord.end(), less);
+#else
+    std::sort(ord.begin(), ord.end(), less);
+#endif
+    int64_t r = -1;
+    for (int64_t k = 0; k < n; k++) {
+        if (k == 0 || sv(ord[(size_t)k]) != sv(ord[(size_t)k - 1])) r++;
+        rank[ord[(size_t)k]] = r;
+    }
+}
+
+// Entries idx[0], idx[1], ... of a packed table; two-phase as bsdc_table_concat.
+extern "C" int64_t bsdc_table_take(int64_t n, const int64_t *idx, const int64_t *off, const uint8_t *buf, int64_t *out_off,
+                                   uint8_t *out_buf, int32_t n_threads) {
+    set_threads(n_threads);
+    if (!out_buf) {
+        int64_t t = 0;
+        for (int64_t r = 0; r < n; r++) {
+            out_off[r] = t;
+            t += off[idx[r] + 1] - off[idx[r]];
+        }
+        out_off[n] = t;
+        return t;
+    }
+#pragma omp parallel for schedule(static)
+    for (int64_t r = 0; r < n; r++) memcpy(out_buf + out_off[r], buf + off[idx[r]], (size_t)(off[idx[r] + 1] - off[idx[r]]));
+    return out_off[n];
 }
 
 extern "C" int32_t bsdc_family_image(int64_t n_rec, const int64_t *src_off, const int64_t *len, const int64_t *dst_off,

@@ -132,6 +132,23 @@ int32_t bsdc_bam_writer_close(bsdc_bam_writer *w, int32_t n_threads);
 int32_t bsdc_fastq_write(const char *path1, const char *path2, const bsdc_bam_records *r, int32_t level,
                          int32_t n_threads);
 
+/* Streaming paired-FASTQ writer: the bytes bsdc_fastq_write writes for all the records at once
+ * (each add must hold whole pairs). */
+typedef struct bsdc_fastq_writer bsdc_fastq_writer;
+int32_t bsdc_fastq_writer_open(const char *path1, const char *path2, int32_t level, bsdc_fastq_writer **out);
+int32_t bsdc_fastq_writer_add(bsdc_fastq_writer *w, const bsdc_bam_records *r, int32_t n_threads);
+int32_t bsdc_fastq_writer_close(bsdc_fastq_writer *w, int32_t n_threads);
+
+/* Packed byte tables (entry r = buf[off[r], off[r + 1])), for the output records: per entry the
+ * concatenation of k parts (a table, or a constant when offs[j] is NULL: bufs[j], const_len[j]
+ * bytes), and a gather of entries.  Two phases: out_buf NULL fills out_off [n + 1] and returns the
+ * total bytes; then the bytes, in parallel. */
+int64_t bsdc_table_concat(int64_t n, int32_t k, const int64_t *const *offs, const uint8_t *const *bufs,
+                          const int64_t *const_len, int64_t *out_off, uint8_t *out_buf, int32_t n_threads);
+void bsdc_table_rank(int64_t n, const int64_t *off, const uint8_t *buf, int64_t *rank, int32_t n_threads);
+int64_t bsdc_table_take(int64_t n, const int64_t *idx, const int64_t *off, const uint8_t *buf, int64_t *out_off,
+                        uint8_t *out_buf, int32_t n_threads);
+
 /* Host side of the family batch (bsseqconsensusreads_amd/batch.py, include/bsdc.h layout): record r's
  * len[r] bases and quals, from seq/qual (nt16 codes and phred, one per byte) at src_off[r], go to
  * nibble / byte dst_off[r] + 1 of the image (dst_off even; the caller zeroes both outputs):

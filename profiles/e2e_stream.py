@@ -3,7 +3,8 @@ synthetic coordinate-sorted C2 BAM + FASTA on local disk, then, each in a fresh 
 (so that its peak RSS is its own):
   whole   bam.step5: read the whole BAM, form every family, GPU batches, write the BAM
   stream  bam.step5_stream: bounded chunks, reader / GPU / writer threads overlapped
-Both outputs are compared byte for byte.  Usage:
+  stream_fastq  the same, writing the FASTQ pair of the next rule instead of the BAM
+The two BAMs are compared byte for byte.  Usage:
   python profiles/e2e_stream.py [--families N] [--threads T] [--chunk-mb M] [--level L]"""
 import argparse
 import json
@@ -47,6 +48,10 @@ def child(args):
     t0 = time.perf_counter()
     if args.mode == "whole":
         info = bam.step5(args.inp, args.fa, args.out, engine=eng, threads=args.threads, level=args.level)
+    elif args.mode == "stream_fastq":  # the fused FASTQ emission (main.snake.py:167-177), no BAM
+        info = bam.step5_stream(args.inp, args.fa, None, engine=eng, threads=args.threads, level=args.level,
+                                fastq=(args.out + ".1.fq.gz", args.out + ".2.fq.gz"),
+                                chunk_bytes=args.chunk_mb << 20, stats=stats)
     else:
         info = bam.step5_stream(args.inp, args.fa, args.out, engine=eng, threads=args.threads, level=args.level,
                                 chunk_bytes=args.chunk_mb << 20, stats=stats)
@@ -86,7 +91,7 @@ def main():
            "host_threads": a.threads, "level": a.level, "chunk_MiB": a.chunk_mb, "prep_s": round(prep, 1)}
     print("prepared", json.dumps(res), flush=True)
     outs = {}
-    for mode in ("stream", "whole"):
+    for mode in ("stream", "stream_fastq", "whole"):
         out = os.path.join(d, mode + ".bam")
         p = subprocess.run([sys.executable, os.path.abspath(__file__), "--mode", mode, "--inp", inp, "--fa", fa,
                             "--out", out, "--threads", str(a.threads), "--chunk-mb", str(a.chunk_mb),

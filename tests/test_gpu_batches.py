@@ -101,7 +101,8 @@ def test_large_kernel_dump_vs_oracle_contig_ends(engine, monkeypatch):
 
 def test_cli_step5_two_ranks_equal_one(tmp_path):
     """`cli step5 --gpus 2` (two spawned ranks, here both on GPU 0 via --devices 0,0; tiny device
-    batches dealt round-robin, gathered on rank 0) writes the same BAM and FASTQ bytes as --gpus 1."""
+    batches dealt round-robin, gathered on rank 0) writes the same BAM and FASTQ bytes as --gpus 1
+    (which streams the input in small chunks: --chunk-mb 0 cuts at every complete family)."""
     import os
     import subprocess
     import sys
@@ -110,6 +111,7 @@ def test_cli_step5_two_ranks_equal_one(tmp_path):
 
     s = synth.generate("C2", 700, seed=23, device="cpu", genome_len=80_000)
     raw = synth.messify(s.raw, frac=0.1, seed=2)
+    raw = R.take(raw, np.lexsort((raw.pos, raw.tid)))  # coordinate-sorted: --gpus 1 streams it
     codes = R.unpack_nibbles(s.ref.packed, s.ref.n_nibbles)
     fa = tmp_path / "g.fa"
     fa.write_text(">%s\n%s\n" % (s.ref.names[0], R.NT16_TO_ASCII[codes].tobytes().decode()))
@@ -128,7 +130,7 @@ def test_cli_step5_two_ranks_equal_one(tmp_path):
         p = subprocess.run(cmd, env=env, capture_output=True, text=True, timeout=240)
         assert p.returncode == 0, p.stderr[-3000:]
 
-    cli("one")
+    cli("one", "--chunk-mb", "0")
     cli("two", "--gpus", "2", "--devices", "0,0")
     for suffix in (".bam", "1.fq.gz", "2.fq.gz"):
         a = (tmp_path / ("one" + suffix)).read_bytes()

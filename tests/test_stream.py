@@ -69,7 +69,8 @@ def test_chunks_partition_the_file(tmp_path):
 def test_no_family_or_template_straddles_chunks(tmp_path):
     s, p = _sorted_bam(tmp_path, messy=0.0)
     seen_mi, seen_name = {}, {}
-    for i, (_, r) in enumerate(bam.stream_bam(p, threads=2, chunk_bytes=40_000, slack=2000, read_size=16_384)):
+    # the default read size holds the whole file: chunks stay about chunk_bytes anyway
+    for i, (_, r) in enumerate(bam.stream_bam(p, threads=2, chunk_bytes=40_000, slack=2000)):
         for k in range(r.n):
             if r.mi_id[k] >= 0:
                 assert seen_mi.setdefault(r.mi_names[int(r.mi_id[k])], i) == i
@@ -129,3 +130,13 @@ def test_header_only_read(tmp_path):
     h2, _ = bam.read_bam(p)
     assert h.text == h2.text and h.ref_names == h2.ref_names and np.array_equal(h.ref_lens, h2.ref_lens)
     assert os.path.getsize(p) > 0
+
+
+def test_unsorted_input_fails_loudly(tmp_path):
+    s = synth.generate("C2", 200, seed=3, device="cpu", genome_len=100_000)
+    p = str(tmp_path / "u.bam")
+    raw = R.take(s.raw, np.random.default_rng(0).permutation(s.raw.n))
+    bam.write_bam(p, _header(s.ref), bam.records_to_bam(raw), level=1)
+    with pytest.raises(OSError, match="coordinate-sorted"):
+        for _ in bam.stream_bam(p, threads=2, chunk_bytes=10_000):
+            pass
