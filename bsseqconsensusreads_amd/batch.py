@@ -77,8 +77,9 @@ def large_arena_bytes(n, slot_bytes, max_len, complex_ops):
     """Mirror of ArenaLayout (csrc/bsdc_kernels.hip) / bsdc_family_arena_bytes."""
     n = np.asarray(n, dtype=np.int64)
     ssw = round16(np.asarray(max_len, dtype=np.int64) + 2)
-    # RecMeta per record, or (vote) the second wave part's column sums and ORs: 36 B per column
-    total = np.maximum(round16(n * 48), 36 * ssw) + round16(n * 8) + 8 * ssw
+    # RecMeta per record + the converted-record list, or (vote) the second wave part's column sums
+    # and ORs: 36 B per column
+    total = np.maximum(round16(n * 48) + round16(2 * n), 36 * ssw) + round16(n * 8) + 8 * ssw
     cops = np.asarray(complex_ops, dtype=np.int64)
     total = total + np.where(cops > 0, round16(4 * (cops + 4 * n)), 0)
     total = total + round16(np.asarray(slot_bytes, dtype=np.int64))

@@ -10,8 +10,10 @@ OUT.bam may be '-' to skip the BAM when only the FASTQ pair is wanted.  Errors e
 the message on stderr, so Snakemake aborts the rule and removes partial outputs, as it does for
 the reference tools (tools/2.extend_gap.py:179-180 raises on a record without MI).
 
-step5 on one GPU streams (--stream true, the default): bounded memory whatever the input size,
-decode / GPU / encode overlapped, output identical to the whole-file path (bam.step5_stream).
+step5 on one GPU streams a coordinate-sorted input (--stream auto, the default: when the header
+says SO:coordinate): bounded memory whatever the input size, decode / GPU / encode overlapped,
+output identical to the whole-file path (bam.step5_stream).  Other inputs are read whole
+(bam.step5); --stream true insists on streaming (an unsorted input is then an error).
 step5 --gpus N: one process per GPU (spawned here, or under torch.distributed.run); the family
 batches are dealt to the ranks and rank 0 writes the outputs, identical to --gpus 1
 (bam.consensus_sharded).  --devices maps ranks to device ids (default rank r -> GPU r).
@@ -43,9 +45,10 @@ def parse(argv):
             p.add_argument("--gpus", type=int, default=1, help="one process per GPU, family batches dealt to them")
             p.add_argument("--devices", default=None, help="comma-separated device id per rank (default 0..gpus-1)")
             p.add_argument("--batch-bases", type=int, default=None, help="device batch budget in bases")
-            p.add_argument("--stream", default="true", choices=["true", "false"],
+            p.add_argument("--stream", default="auto", choices=["auto", "true", "false"],
                            help="bounded-memory pipelined step (bam.step5_stream; coordinate-sorted input, one GPU); "
-                                "false = read the whole BAM first (bam.step5)")
+                                "false = read the whole BAM first (bam.step5); auto = stream when the header "
+                                "says SO:coordinate")
             p.add_argument("--chunk-mb", type=int, default=256, help="--stream: record MiB per chunk")
         p.add_argument("--output-per-base-tags", default="true", choices=["true", "false"],
                        help="fgbio's consensus tags (per-read and per-base statistics); off = name/SEQ/QUAL/RG/MI/RX")
@@ -55,6 +58,14 @@ def parse(argv):
     if a.output == "-" and a.fastq1 is None:
         ap.error("nothing to write: give OUT.bam or --fastq1/--fastq2")
     return a
+
+
+def _coordinate_sorted(bam, path: str) -> bool:
+    """The header's @HD SO tag says coordinate (what the streaming reader needs)."""
+    for line in bam.read_bam_header(path).text.splitlines():
+        if line.startswith("@HD"):
+            return "\tSO:coordinate" in "\t" + line.split("\t", 1)[-1]
+    return False
 
 
 def main(argv=None) -> int:
@@ -83,7 +94,9 @@ def main(argv=None) -> int:
         dist = shard.init("gloo") if world > 1 else None  # host gather of the batch outputs only
         eng = Engine(device)
         try:
-            if a.cmd == "step5" and world == 1 and a.stream == "true":
+            stream = a.cmd == "step5" and world == 1 and (
+                a.stream == "true" or (a.stream == "auto" and _coordinate_sorted(bam, a.input)))
+            if stream:
                 info = bam.step5_stream(a.input, a.reference, out, eng, a.read_name_prefix, a.threads, a.compression,
                                         fq, tags=a.output_per_base_tags == "true", chunk_bytes=a.chunk_mb << 20,
                                         batch_bases=a.batch_bases)

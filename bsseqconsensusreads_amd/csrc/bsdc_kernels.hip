@@ -68,6 +68,14 @@ constexpr int kOvlChunks = LARGE_OVL_CHUNKS;
 #endif
 constexpr int kConvH = LARGE_CONV_H;
 static_assert(kConvH == 1 || kConvH == 2, "16 reference nibbles cover at most 9 positions");
+#ifndef LARGE_CONV_U
+#define LARGE_CONV_U 4  // k_large convert: tasks per thread per round (their reference loads in flight together)
+#endif
+constexpr int kLConvU = LARGE_CONV_U;
+#ifndef LARGE_STAGE_U
+#define LARGE_STAGE_U 8  // k_large staging: 16-B image chunks per thread in flight
+#endif
+constexpr int kLStageU = LARGE_STAGE_U;
 constexpr int kSmallMaxWaves = 8;              // wavefronts (families) per small-kernel workgroup, at most
 constexpr int kSmallMinWaves = SMALL_WAVES >= 8 ? 8 : 6;  // occupancy target the register budget is cut for
 constexpr int kSmallSimdWaves = SMALL_WAVES;   // waves per SIMD its registers allow
@@ -1506,9 +1514,30 @@ __device__ __forceinline__ int block_max(int v, int *red) {
     return s;
 }
 
+// the sum of a and the max of b over the workgroup, one barrier (red: 2 G / 64 ints)
 template <int G>
-__device__ void process_large(const KParams &P, uint8_t *A, const int32_t *lr, const float *thr, uint4 ent, int *red,
-                              int *s_cnt, int *s_lc, int *s_cur) {
+__device__ __forceinline__ void block_sum_max(int a, int b, int *red, int &sum, int &mx) {
+#pragma unroll
+    for (int o = 32; o >= 1; o >>= 1) {
+        a += __shfl_xor(a, o, kWave);
+        b = ::max(b, __shfl_xor(b, o, kWave));
+    }
+    if ((threadIdx.x & 63) == 0) {
+        red[threadIdx.x >> 6] = a;
+        red[G / kWave + (threadIdx.x >> 6)] = b;
+    }
+    __syncthreads();
+    sum = 0;
+    mx = red[G / kWave];
+    for (int w = 0; w < G / kWave; w++) {
+        sum += red[w];
+        mx = ::max(mx, red[G / kWave + w]);
+    }
+}
+
+template <int G>
+__device__ void process_large(const KParams &P, uint8_t *A, uint8_t *s_tab, const int32_t *lr, const float *thr, uint4 ent,
+                              int *red, int *s_cnt, int *s_lc, int *s_cur) {
     const int tt = threadIdx.x;
     const bsdc_family_batch &B = P.B;
     const uint32_t fam = ent.x, r0 = ent.y, img = ent.w;  // list entry: family, first record, n, image bytes
@@ -1520,30 +1549,42 @@ __device__ void process_large(const KParams &P, uint8_t *A, const int32_t *lr, c
     const uint32_t off0 = n > 0 ? REC[r0].x : 0u;
     const int stop = (P.mode >> BSDC_MODE_STOP_SHIFT) & 15;  // profiling ablation (0 = full kernel)
 
-    int c = 0, ml = 0;
-    for (int r = tt; r < n; r += G) {
-        const uint4 rc = REC[r0 + r];
-        if (rc.w & BSDC_LINK_COMPLEX) c += (int)(B.cig_info[r0 + r] & 0xFFFF);
-        ml = ::max(ml, (int)(rc.z & 0xFFFF));
-    }
-    const int cops = block_sum<G>(c, red);
-    const int maxlen_f = block_max<G>(ml, red);
-    const ArenaLayout Lo(n, 0, maxlen_f, cops);
-    RecMeta *M = reinterpret_cast<RecMeta *>(A + Lo.meta);
-    uint16_t *lists = reinterpret_cast<uint16_t *>(A + Lo.lists);
-    uint8_t *ssb = A + Lo.ssb;
-    uint8_t *ssq = A + Lo.ssq;
-    uint32_t *simp = reinterpret_cast<uint32_t *>(A + Lo.simp);
+    // ---- one round of global loads for everything the family needs first: the tables (s_cnt[0]
+    // cleared by the caller), up to kLStageU 16-byte image chunks per thread (quals, packed bases)
+    // and the record metadata.  The image and the metadata sit at offsets the list entry alone
+    // gives (ArenaLayout), so nothing waits for the family's max length / cigar size ----
     // the family image as in HBM: bases (one byte each) at slots + slot, quals at slots + img + slot
     // (RecMeta::cap = img, so `base + cap` addresses a base's qual)
-    uint8_t *slots = A + Lo.slots;
+    const ArenaLayout L0(n, 2 * (int64_t)img, 0, 0);  // meta / clist / slots only
+    uint8_t *slots = A + L0.slots;
     uint8_t *qimg = slots + img;
-    const int ssw = Lo.ssw;
-
-    // ---- record metadata ----
+    RecMeta *M = reinterpret_cast<RecMeta *>(A + L0.meta);
+    uint16_t *clist = reinterpret_cast<uint16_t *>(A + L0.clist);  // the converted records
+    uint32_t qor = 0;  // OR of the family's quals: a byte >= 128 keeps the overlap off the SWAR path
+    const int nqc = (int)(img >> 4), nch = nqc + (int)(img >> 5);  // 16-B chunks: quals, then packed bases
+    auto load_chunk = [&](int k) {
+        const uint8_t *src = k < nqc ? B.qual + off0 + 16 * (uint32_t)k : B.seq + (off0 >> 1) + 16 * (uint32_t)(k - nqc);
+        return *reinterpret_cast<const uint4 *>(src);
+    };
+    auto store_chunk = [&](int k, uint4 v) {
+        if (k < nqc) {
+            *reinterpret_cast<uint4 *>(qimg + 16 * k) = v;
+            qor |= v.x | v.y | v.z | v.w;
+        } else {
+            unpack32<false>(v, slots + 32 * (k - nqc));
+        }
+    };
+    uint4 v[kLStageU];
+#pragma unroll
+    for (int u = 0; u < kLStageU; u++)
+        if (tt + u * G < nch) v[u] = load_chunk(tt + u * G);
+    uint4 tv = make_uint4(0, 0, 0, 0);
+    if (tt < kTabBytesL / 16) tv = reinterpret_cast<const uint4 *>(&P.tab->t)[tt];
+    int c = 0, ml = 0;
     for (int r = tt; r < n; r += G) {
         const uint32_t gi = r0 + r;
         const uint4 rc = REC[gi];
+        const uint32_t ci = B.cig_info[gi], wn = B.rec_win[2 * (size_t)gi];
         RecMeta m;
         m.in_len = (int32_t)(rc.z & 0xFFFF);
         m.flag = (uint16_t)(rc.z >> 16);
@@ -1554,64 +1595,51 @@ __device__ void process_large(const KParams &P, uint8_t *A, const int32_t *lr, c
         m.start = 1;
         m.link = rc.w;
         m.gidx = gi;
-        m.win = (do_convert && (m.link & BSDC_LINK_CONVERT)) ? B.rec_win[2 * (size_t)gi] : 0u;
+        const bool conv = do_convert && (m.link & BSDC_LINK_CONVERT);
+        m.win = conv ? wn : 0u;
         m.srclen = 0;
-        m.reflen = (m.link & BSDC_LINK_COMPLEX) ? (int32_t)(B.cig_info[gi] >> 16) : m.in_len;
+        const bool cx = m.link & BSDC_LINK_COMPLEX;
+        m.reflen = cx ? (int32_t)(ci >> 16) : m.in_len;
         m.rd = 0;
         m.set = 0xFF;
         M[r] = m;
+        if (cx) c += (int)(ci & 0xFFFF);
+        ml = ::max(ml, m.in_len);
+        if (conv) clist[atomicAdd(&s_cnt[0], 1)] = (uint16_t)r;
     }
-    __syncthreads();
-
-    // ---- stage the image: every 16-byte chunk, quals as they are, packed bases unpacked ----
-    uint32_t qor = 0;  // OR of the family's quals: a byte >= 128 keeps the overlap off the SWAR path
-    {
-        // 16-B chunks: [0, nqc) quals, [nqc, nch) packed bases; kStageU loads per thread in flight
-        constexpr int kStageU = 4;
-        const int nqc = (int)(img >> 4), nch = nqc + (int)(img >> 5);
-        for (int k0 = tt; k0 < nch; k0 += kStageU * G) {
-            uint4 v[kStageU];
 #pragma unroll
-            for (int u = 0; u < kStageU; u++) {
-                const int k = k0 + u * G;
-                if (k < nch) {
-                    const uint8_t *src = k < nqc ? B.qual + off0 + 16 * (uint32_t)k
-                                                 : B.seq + (off0 >> 1) + 16 * (uint32_t)(k - nqc);
-                    v[u] = *reinterpret_cast<const uint4 *>(src);
-                }
-            }
+    for (int u = 0; u < kLStageU; u++)
+        if (tt + u * G < nch) store_chunk(tt + u * G, v[u]);
+    if (tt < kTabBytesL / 16) reinterpret_cast<uint4 *>(s_tab)[tt] = tv;
+    for (int k0 = tt + kLStageU * G; k0 < nch; k0 += kLStageU * G) {  // families of more chunks
 #pragma unroll
-            for (int u = 0; u < kStageU; u++) {
-                const int k = k0 + u * G;
-                if (k < nqc) {
-                    *reinterpret_cast<uint4 *>(qimg + 16 * k) = v[u];
-                    qor |= v[u].x | v[u].y | v[u].z | v[u].w;
-                } else if (k < nch) {
-                    unpack32<false>(v[u], slots + 32 * (k - nqc));
-                }
-            }
-        }
+        for (int u = 0; u < kLStageU; u++)
+            if (k0 + u * G < nch) v[u] = load_chunk(k0 + u * G);
+#pragma unroll
+        for (int u = 0; u < kLStageU; u++)
+            if (k0 + u * G < nch) store_chunk(k0 + u * G, v[u]);
     }
-    __syncthreads();
+    int cops, maxlen_f;
+    block_sum_max<G>(c, ml, red, cops, maxlen_f);  // (its barrier publishes the arena and the tables)
+    const ArenaLayout Lo(n, 2 * (int64_t)img, maxlen_f, cops);
+    uint16_t *lists = reinterpret_cast<uint16_t *>(A + Lo.lists);
+    uint8_t *ssb = A + Lo.ssb;
+    uint8_t *ssq = A + Lo.ssq;
+    uint32_t *simp = reinterpret_cast<uint32_t *>(A + Lo.simp);
+    const int ssw = Lo.ssw;
     if (stop == 1) return;
 
     // ---- tool 1 (tools/1.convert_AG_to_CT.py:84-183): every converted record at once, 4 positions
     // per thread, flattened over (converted record, dword).  Each chunk of G dwords reads first and
     // writes after a barrier: a dword's rule also reads the next dword's original bases ----
     if (do_convert) {
-        uint16_t *clist = lists;  // the converted records (until the read lists are built)
-        if (tt == 0) s_cnt[0] = 0;
-        __syncthreads();
-        for (int r = tt; r < n; r += G)
-            if (M[r].link & BSDC_LINK_CONVERT) clist[atomicAdd(&s_cnt[0], 1)] = (uint16_t)r;
-        __syncthreads();
         const int nc = s_cnt[0];
         // a task is kConvH dwords (4 positions each) of one converted record; the 16 reference
         // nibbles at the task's aligned 8 bytes cover 4 * kConvH + 1 positions for kConvH <= 2
         constexpr int H = kConvH, TP = 4 * kConvH;
         const int SD = (maxlen_f + 1 + TP - 1) / TP;  // tasks per converted record, at most
         const int total = nc * SD;
-        constexpr int kConvU = 4 / kConvH;  // tasks per thread per round: their global loads go out together
+        constexpr int kConvU = kLConvU;  // tasks per thread per round: their global loads go out together
         for (int base = 0; base < total; base += kConvU * G) {
             int rr[kConvU], jj[kConvU], av[kConvU];
             uint32_t w0[kConvU], w1[kConvU];
@@ -2259,19 +2287,23 @@ static_assert(sizeof(TablesL) == kTabBytesL, "TablesL image");
 template <bool IN_LDS, int G>
 __global__ __launch_bounds__(G, G == 256 ? 5 : 2) void k_large(KParams P, const uint4 *fams, int64_t nfams, int32_t arena) {
     extern __shared__ __attribute__((aligned(16))) uint8_t smem[];  // the family's arena (IN_LDS)
-    __shared__ __attribute__((aligned(16))) TablesL s_tab;
-    __shared__ int red[G / kWave];
+    __shared__ __attribute__((aligned(16))) TablesL s_tab;  // loaded by process_large with the image
+    __shared__ int red[2 * G / kWave];
     __shared__ int s_cnt[4], s_lc[4], s_cur[8];
     const TablesL *T = &s_tab;
     if (((P.mode >> BSDC_MODE_STOP_SHIFT) & 15) == 15) return;  // profiling: launch cost alone
-    load_tables<kTabBytesL>(&P.tab->t, reinterpret_cast<uint8_t *>(&s_tab));
-    if (((P.mode >> BSDC_MODE_STOP_SHIFT) & 15) == 14) return;  // profiling: + the table copy
+    if (((P.mode >> BSDC_MODE_STOP_SHIFT) & 15) == 14) {        // profiling: + the table copy
+        load_tables<kTabBytesL>(&P.tab->t, reinterpret_cast<uint8_t *>(&s_tab));
+        return;
+    }
     const int32_t *lr = T->lr;
     const float *thr = T->thr;
     const int64_t i = blockIdx.x;
     if (i >= nfams) return;
+    if (threadIdx.x == 0) s_cnt[0] = 0;  // the converted-record count (process_large's first phase)
+    __syncthreads();
     uint8_t *A = IN_LDS ? smem : P.O.scratch + (size_t)i * (size_t)arena;
-    process_large<G>(P, A, lr, thr, fams[i], red, s_cnt, s_lc, s_cur);
+    process_large<G>(P, A, reinterpret_cast<uint8_t *>(&s_tab), lr, thr, fams[i], red, s_cnt, s_lc, s_cur);
 }
 
 }  // namespace

@@ -57,15 +57,23 @@ struct SmallLayout {
     }
 };
 
-// Arena layout of one large family (offsets from the arena base).
+// Arena layout of one large family (offsets from the arena base).  The family image comes first
+// and the record metadata right after it: both offsets are known from the list entry alone, so
+// the kernel stages the image and writes the metadata before it knows the family's longest read
+// and cigar size (which place the regions after them).
 struct ArenaLayout {
-    uint32_t meta, lists, ssb, ssq, simp, slots, total;
+    uint32_t meta, clist, lists, ssb, ssq, simp, slots, total;
     int32_t ssw;
     BSDC_HD ArenaLayout(int n, int64_t slot_bytes, int max_len, int64_t complex_ops) {
         ssw = (int32_t)round16(max_len + 2);
         int64_t o = 0;
-        meta = (uint32_t)o;  // RecMeta per record; in the vote (RecMeta dead) the second wave part's sums
-        const int64_t mb = round16((int64_t)n * (int64_t)kRecMetaBytes), vb = 36 * (int64_t)ssw;
+        slots = (uint32_t)o;
+        o += round16(slot_bytes);
+        // RecMeta per record + the converted-record list (u16); in the vote (both dead) the second
+        // wave part's sums
+        meta = (uint32_t)o;
+        clist = (uint32_t)(o + round16((int64_t)n * (int64_t)kRecMetaBytes));
+        const int64_t mb = round16((int64_t)n * (int64_t)kRecMetaBytes) + round16(2 * (int64_t)n), vb = 36 * (int64_t)ssw;
         o += mb > vb ? mb : vb;
         lists = (uint32_t)o;
         o += round16((int64_t)n * 8);
@@ -75,8 +83,6 @@ struct ArenaLayout {
         o += 4 * (int64_t)ssw;
         simp = (uint32_t)o;
         if (complex_ops > 0) o += round16(4 * (complex_ops + 4 * (int64_t)n));
-        slots = (uint32_t)o;
-        o += round16(slot_bytes);
         total = (uint32_t)o;
     }
 };

@@ -283,6 +283,15 @@ def test_cli_step5_and_molecular_files(engine, tmp_path):
                      "--fastq2", p("d2.fq.gz"), "--threads", "4"]) == 0
     assert cli.main(["molecular", inp, "-", "--fastq1", p("m1.fq.gz"), "--fastq2", p("m2.fq.gz")]) == 0
     assert cli.main(["molecular", p("missing.bam"), p("x.bam")]) == 1
+    # an unsorted input is read whole under the default --stream auto; insisting on the stream fails
+    assert cli.main(["step5", "--reference", str(fa), inp, p("u.bam"), "--stream", "true"]) == 1
+    # a coordinate-sorted input streams by default, with the bytes of the whole-file path
+    sinp = str(tmp_path / "in.sorted.bam")
+    shdr = bam.BamHeader(hdr.text.replace("SO:unsorted", "SO:coordinate"), hdr.ref_names, hdr.ref_lens)
+    bam.write_bam(sinp, shdr, bam.records_to_bam(R.take(raw, np.lexsort((raw.pos, raw.tid)))))
+    assert cli.main(["step5", "--reference", str(fa), sinp, p("s_stream.bam"), "--chunk-mb", "1"]) == 0
+    assert cli.main(["step5", "--reference", str(fa), sinp, p("s_whole.bam"), "--stream", "false"]) == 0
+    assert open(p("s_stream.bam"), "rb").read() == open(p("s_whole.bam"), "rb").read()
     _, d = bam.read_bam(p("d.bam"))
     ref = oracle.run(raw, s.ref)
     em = np.nonzero(ref.status == 1)[0]
