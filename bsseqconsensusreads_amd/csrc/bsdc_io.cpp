@@ -9,6 +9,7 @@
 // blocks deflated in parallel -> one write, then the 28-byte EOF block.
 #include "../../include/bsdc_io.h"
 
+#include <dlfcn.h>
 #include <zlib.h>
 
 #include <algorithm>
@@ -42,6 +43,100 @@ inline void wr16(uint8_t *p, uint16_t v) {
 }
 inline void wr32(uint8_t *p, uint32_t v) {
     for (int i = 0; i < 4; i++) p[i] = (uint8_t)(v >> (8 * i));
+}
+
+// libdeflate (the system's libdeflate.so.0, loaded at run time; its published v1 C API) inflates,
+// deflates and CRCs BGZF blocks 2-3x faster than zlib.  Without it (or with BSDC_ZLIB set) the
+// codec uses zlib; both read every valid BGZF file, and each writes valid BGZF (the compressed
+// bytes differ between the two).
+struct Libdeflate {
+    void *(*alloc_d)() = nullptr;
+    void (*free_d)(void *) = nullptr;
+    int (*decompress)(void *, const void *, size_t, void *, size_t, size_t *) = nullptr;
+    void *(*alloc_c)(int) = nullptr;
+    void (*free_c)(void *) = nullptr;
+    size_t (*compress)(void *, const void *, size_t, void *, size_t) = nullptr;
+    size_t (*bound)(void *, size_t) = nullptr;
+    uint32_t (*crc)(uint32_t, const void *, size_t) = nullptr;
+    bool ok = false;
+    Libdeflate() {
+        if (getenv("BSDC_ZLIB")) return;
+        void *h = dlopen("libdeflate.so.0", RTLD_NOW | RTLD_LOCAL);
+        if (!h) return;
+        alloc_d = (void *(*)())dlsym(h, "libdeflate_alloc_decompressor");
+        free_d = (void (*)(void *))dlsym(h, "libdeflate_free_decompressor");
+        decompress = (int (*)(void *, const void *, size_t, void *, size_t, size_t *))dlsym(h, "libdeflate_deflate_decompress");
+        alloc_c = (void *(*)(int))dlsym(h, "libdeflate_alloc_compressor");
+        free_c = (void (*)(void *))dlsym(h, "libdeflate_free_compressor");
+        compress = (size_t(*)(void *, const void *, size_t, void *, size_t))dlsym(h, "libdeflate_deflate_compress");
+        bound = (size_t(*)(void *, size_t))dlsym(h, "libdeflate_deflate_compress_bound");
+        crc = (uint32_t(*)(uint32_t, const void *, size_t))dlsym(h, "libdeflate_crc32");
+        ok = alloc_d && free_d && decompress && alloc_c && free_c && compress && bound && crc;
+    }
+};
+const Libdeflate &libdeflate() {
+    static const Libdeflate L;
+    return L;
+}
+// one decompressor / compressor per thread, kept for the thread's life
+struct DeflateState {
+    void *d = nullptr, *c = nullptr;
+    int level = -1;
+    ~DeflateState() {
+        if (d) libdeflate().free_d(d);
+        if (c) libdeflate().free_c(c);
+    }
+};
+DeflateState &deflate_state() {
+    thread_local DeflateState s;
+    return s;
+}
+uint32_t crc32_of(const uint8_t *p, int64_t n) {
+    const Libdeflate &L = libdeflate();
+    return L.ok ? L.crc(0, p, (size_t)n) : (uint32_t)crc32(0L, p, (uInt)n);
+}
+// raw deflate stream in[0, n) -> exactly `want` bytes at out; false on any error
+bool raw_inflate(const uint8_t *in, int64_t n, uint8_t *out, int64_t want) {
+    const Libdeflate &L = libdeflate();
+    if (L.ok) {
+        DeflateState &st = deflate_state();
+        if (!st.d) st.d = L.alloc_d();
+        size_t got = 0;
+        return st.d && L.decompress(st.d, in, (size_t)n, out, (size_t)want, &got) == 0 && (int64_t)got == want;
+    }
+    z_stream zs;
+    memset(&zs, 0, sizeof zs);
+    if (inflateInit2(&zs, -15) != Z_OK) return false;
+    zs.next_in = const_cast<uint8_t *>(in);
+    zs.avail_in = (uInt)n;
+    zs.next_out = out;
+    zs.avail_out = (uInt)want;
+    const int rc = inflate(&zs, Z_FINISH);
+    inflateEnd(&zs);
+    return rc == Z_STREAM_END && (int64_t)zs.total_out == want;
+}
+// raw deflate of in[0, n) at `level` into out[0, cap) -> compressed size, 0 on failure
+int64_t raw_deflate(const uint8_t *in, int64_t n, int level, uint8_t *out, int64_t cap) {
+    const Libdeflate &L = libdeflate();
+    if (L.ok && level > 0) {  // (stored blocks, level 0, through zlib)
+        DeflateState &st = deflate_state();
+        if (!st.c || st.level != level) {
+            if (st.c) L.free_c(st.c);
+            st.c = L.alloc_c(level);
+            st.level = level;
+        }
+        return st.c ? (int64_t)L.compress(st.c, in, (size_t)n, out, (size_t)cap) : 0;
+    }
+    z_stream zs;
+    memset(&zs, 0, sizeof zs);
+    if (deflateInit2(&zs, level, Z_DEFLATED, -15, 8, Z_DEFAULT_STRATEGY) != Z_OK) return 0;
+    zs.next_in = const_cast<uint8_t *>(in);
+    zs.avail_in = (uInt)n;
+    zs.next_out = out;
+    zs.avail_out = (uInt)cap;
+    const int rc = deflate(&zs, Z_FINISH);
+    deflateEnd(&zs);
+    return rc == Z_STREAM_END ? (int64_t)zs.total_out : 0;
 }
 
 void set_threads(int n) {
@@ -106,10 +201,13 @@ static void intern(const std::vector<std::string_view> &keys, const std::vector<
     const int64_t n = (int64_t)keys.size();
     constexpr int S = 256;
     std::vector<uint32_t> shard((size_t)n);
+    std::vector<uint64_t> hv((size_t)n);
 #pragma omp parallel for schedule(static)
     for (int64_t k = 0; k < n; k++) {
         const bool ok = present == nullptr || !(*present)[(size_t)k].empty();
-        shard[(size_t)k] = ok ? (uint32_t)(std::hash<std::string_view>{}(keys[(size_t)k]) % S) : (uint32_t)S;
+        const uint64_t h = std::hash<std::string_view>{}(keys[(size_t)k]);
+        hv[(size_t)k] = h;
+        shard[(size_t)k] = ok ? (uint32_t)(h % S) : (uint32_t)S;
     }
     std::vector<int64_t> start(S + 2, 0);
     for (int64_t k = 0; k < n; k++) start[shard[(size_t)k] + 1]++;
@@ -118,15 +216,24 @@ static void intern(const std::vector<std::string_view> &keys, const std::vector<
     for (int64_t k = 0; k < n; k++) order[(size_t)fill[shard[(size_t)k]]++] = k;  // ascending k per shard
     std::vector<int32_t> local((size_t)n, -1);
     std::vector<std::vector<int64_t>> first(S);
+    // per shard: an open-addressing table (linear probing) of the shard's distinct keys
 #pragma omp parallel for schedule(dynamic, 4)
     for (int s = 0; s < S; s++) {
-        std::unordered_map<std::string_view, int32_t> m;
-        m.reserve((size_t)(start[s + 1] - start[s]));
+        const int64_t cnt = start[s + 1] - start[s];
+        size_t cap = 16;
+        while ((int64_t)cap < 2 * cnt) cap <<= 1;
+        std::vector<int32_t> slot(cap, -1);
+        std::vector<int64_t> &fs = first[s];
         for (int64_t i = start[s]; i < start[s + 1]; i++) {
             const int64_t k = order[(size_t)i];
-            auto it = m.emplace(keys[(size_t)k], (int32_t)first[s].size());
-            if (it.second) first[s].push_back(k);
-            local[(size_t)k] = it.first->second;
+            const std::string_view key = keys[(size_t)k];
+            size_t pos = (size_t)(hv[(size_t)k] / S) & (cap - 1);
+            while (slot[pos] >= 0 && keys[(size_t)fs[(size_t)slot[pos]]] != key) pos = (pos + 1) & (cap - 1);
+            if (slot[pos] < 0) {
+                slot[pos] = (int32_t)fs.size();
+                fs.push_back(k);
+            }
+            local[(size_t)k] = slot[pos];
         }
     }
     std::vector<int64_t> firsts;
@@ -209,6 +316,8 @@ int32_t inflate_blocks(const uint8_t *comp, int64_t n, bool final, std::vector<u
         u += rd32(h + bsize - 4);
         o += bsize;
     }
+    // (+8: the readers pad the stream for dword loads; geometric growth for the streaming buffer)
+    if (out.capacity() < (size_t)u + 8) out.reserve(std::max((size_t)u + 8, 2 * out.capacity()));
     out.resize((size_t)u);
     const int64_t nb = (int64_t)boff.size();
     int bad = 0;
@@ -224,19 +333,7 @@ int32_t inflate_blocks(const uint8_t *comp, int64_t n, bool final, std::vector<u
             bad |= 1;
             continue;
         }
-        z_stream zs;
-        memset(&zs, 0, sizeof zs);
-        if (inflateInit2(&zs, -15) != Z_OK) {
-            bad |= 1;
-            continue;
-        }
-        zs.next_in = const_cast<uint8_t *>(cdata);
-        zs.avail_in = (uInt)clen;
-        zs.next_out = out.data() + uoff[i];
-        zs.avail_out = isize;
-        const int rc = inflate(&zs, Z_FINISH);
-        inflateEnd(&zs);
-        if (rc != Z_STREAM_END || zs.total_out != isize || crc32(0L, out.data() + uoff[i], isize) != crc) bad |= 1;
+        if (!raw_inflate(cdata, clen, out.data() + uoff[i], isize) || crc32_of(out.data() + uoff[i], isize) != crc) bad |= 1;
     }
     if (bad) return fail(BSDC_IO_EFORMAT, "corrupt BGZF block (inflate or CRC32)");
     *used = o;
@@ -424,13 +521,19 @@ struct bsdc_bam_stream {
     FILE *f = nullptr;
     bsdc_bam hdr;                 // header text and references only
     std::vector<uint8_t> comp;    // compressed bytes read but not yet inflated (a partial block)
-    std::vector<uint8_t> pend;    // inflated bytes not yet split into records (starts at a record)
+    // buf = [buffered records (recs) | inflated bytes not yet split, from `tail`]; inflated blocks
+    // land at its end and records are split in place (no copy); `spare` keeps the capacity the
+    // kept records move to when a chunk goes out
+    int64_t tail = 0;
+    std::vector<uint8_t> spare;
     bool eof = false;
     int64_t read_size = 0;
     // buffered records (file order) and their families
     std::vector<uint8_t> buf;
     std::vector<StreamRec> recs;
-    std::unordered_map<std::string, int32_t> fam_of;  // MI base -> family
+    std::unordered_map<uint64_t, int32_t> fam_of;  // hash of the MI base -> family
+    std::unordered_map<std::string, int32_t> fam_exact;  // MI bases whose hash another live family holds
+    std::vector<std::string> fam_key;               // per family: its MI base
     std::vector<StreamFam> fams;
     std::vector<int32_t> free_fams;
     int64_t cursor = INT64_MIN;  // the last record's position
@@ -448,18 +551,19 @@ int32_t bsdc_bam_stream_open(const char *path, int32_t n_threads, int64_t read_s
     for (;;) {
         int64_t p = 0;
         bsdc_bam probe;
-        const bool have = s->pend.size() >= 12 &&
-                          parse_header(s->pend.data(), (int64_t)s->pend.size(), &probe, &p) == 0;
+        const bool have = s->buf.size() >= 12 &&
+                          parse_header(s->buf.data(), (int64_t)s->buf.size(), &probe, &p) == 0;
         if (have) {
             s->hdr.header = probe.header;
             s->hdr.ref_names = probe.ref_names;
             s->hdr.ref_len = probe.ref_len;
-            s->pend.erase(s->pend.begin(), s->pend.begin() + p);
+            s->buf.erase(s->buf.begin(), s->buf.begin() + p);
+            s->tail = 0;
             break;
         }
         if (s->eof) {
-            const int64_t dn = (int64_t)s->pend.size();
-            const int32_t rc = parse_header(s->pend.data(), dn, &probe, &p);
+            const int64_t dn = (int64_t)s->buf.size();
+            const int32_t rc = parse_header(s->buf.data(), dn, &probe, &p);
             bsdc_bam_stream_close(s);
             return rc != 0 ? rc : fail(BSDC_IO_EFORMAT, "missing BAM header");
         }
@@ -473,7 +577,7 @@ int32_t bsdc_bam_stream_open(const char *path, int32_t n_threads, int64_t read_s
     return 0;
 }
 
-// Reads read_size more compressed bytes and inflates the whole blocks into pend.
+// Reads read_size more compressed bytes and inflates the whole blocks onto the end of buf.
 int32_t bsdc_bam_stream_fill(bsdc_bam_stream *s) {
     if (s->eof) return 0;
     const size_t have = s->comp.size();
@@ -485,19 +589,19 @@ int32_t bsdc_bam_stream_fill(bsdc_bam_stream *s) {
         s->eof = true;
     }
     int64_t used = 0;
-    const int32_t rc = inflate_blocks(s->comp.data(), (int64_t)s->comp.size(), s->eof, s->pend, &used);
+    const int32_t rc = inflate_blocks(s->comp.data(), (int64_t)s->comp.size(), s->eof, s->buf, &used);
     if (rc != 0) return rc;
     s->comp.erase(s->comp.begin(), s->comp.begin() + used);
     return 0;
 }
 
 namespace {
-// The whole records of s->pend moved into the buffer, each with its MI family.  A record's family
+// The whole records of buf's unsplit tail added to the buffered records, each with its MI family.  A record's family
 // is its MI base (the MI up to the first '/', as the reader interns it); a record without MI is a
 // family of its own.
 int32_t stream_split(bsdc_bam_stream *s) {
-    const uint8_t *d = s->pend.data();
-    const int64_t dn = (int64_t)s->pend.size();
+    const uint8_t *d = s->buf.data() + s->tail;
+    const int64_t dn = (int64_t)s->buf.size() - s->tail;
     // record boundaries (sequential), then each record's family key and positions (parallel)
     std::vector<int64_t> starts;
     int64_t p = 0;
@@ -511,6 +615,7 @@ int32_t stream_split(bsdc_bam_stream *s) {
     const int64_t nr = (int64_t)starts.size();
     struct Parsed {
         std::string_view mi;
+        uint64_t h;  // hash of mi
         int64_t c, e;
         TcKey key;
     };
@@ -597,7 +702,7 @@ int32_t stream_split(bsdc_bam_stream *s) {
         else if (tid == ntid) key = {(t1 << 32) | t1, std::min(p_own, p_mate)};
         else if (tid >= 0 && tid < ntid) key = {(t1 << 32) | (int64_t)ntid, p_own};
         else key = {((int64_t)ntid << 32) | t1, p_mate};
-        P[(size_t)k] = Parsed{mi, c, ntid >= 0 ? std::max(c, coord(ntid, npos)) : c, key};
+        P[(size_t)k] = Parsed{mi, std::hash<std::string_view>{}(mi), c, ntid >= 0 ? std::max(c, coord(ntid, npos)) : c, key};
     }
     if (bad) return fail(BSDC_IO_EFORMAT, "malformed BAM record (lengths or aux)");
     // families (sequential: the MI map), then the records' bytes in one copy
@@ -610,10 +715,28 @@ int32_t stream_split(bsdc_bam_stream *s) {
         } else {
             fam = (int32_t)s->fams.size();
             s->fams.emplace_back();
+            s->fam_key.emplace_back();
         }
         return fam;
     };
-    const int64_t base = (int64_t)s->buf.size();
+    // the family of an MI base: the map holds hashes and each family keeps its key; a key whose
+    // hash a different live key holds (a 64-bit collision) goes to the exact map, looked up first
+    auto fam_of_mi = [&](std::string_view mi, uint64_t h) {
+        if (!s->fam_exact.empty()) {
+            auto ie = s->fam_exact.find(std::string(mi));
+            if (ie != s->fam_exact.end() && s->fams[(size_t)ie->second].n > 0) return ie->second;
+        }
+        auto it = s->fam_of.find(h);
+        if (it != s->fam_of.end() && s->fams[(size_t)it->second].n > 0 && s->fam_key[(size_t)it->second] == mi)
+            return it->second;
+        const int32_t fam = new_fam();
+        s->fam_key[(size_t)fam].assign(mi.data(), mi.size());
+        if (it == s->fam_of.end()) s->fam_of.emplace(h, fam);
+        else if (s->fams[(size_t)it->second].n == 0) it->second = fam;
+        else s->fam_exact[std::string(mi)] = fam;  // collision with a live family
+        return fam;
+    };
+    const int64_t base = s->tail;
     for (int64_t k = 0; k < nr; k++) {
         const Parsed &q = P[(size_t)k];
         if (q.c < s->cursor)
@@ -621,13 +744,7 @@ int32_t stream_split(bsdc_bam_stream *s) {
                                          "coordinate order of the step-5 input; read it whole instead)");
         int32_t fam;
         if (!q.mi.empty()) {
-            auto it = s->fam_of.find(std::string(q.mi));
-            if (it == s->fam_of.end() || s->fams[(size_t)it->second].n == 0) {
-                fam = new_fam();
-                s->fam_of[std::string(q.mi)] = fam;
-            } else {
-                fam = it->second;
-            }
+            fam = fam_of_mi(q.mi, q.h);
         } else {
             fam = new_fam();  // a record without MI: a family of its own
         }
@@ -641,8 +758,7 @@ int32_t stream_split(bsdc_bam_stream *s) {
         const int64_t len = (k + 1 < nr ? starts[(size_t)k + 1] : p) - starts[(size_t)k];
         s->recs.push_back(StreamRec{base + starts[(size_t)k], len, fam});
     }
-    s->buf.insert(s->buf.end(), s->pend.begin(), s->pend.begin() + p);
-    s->pend.erase(s->pend.begin(), s->pend.begin() + p);
+    s->tail += p;
     return 0;
 }
 }  // namespace
@@ -660,11 +776,16 @@ int32_t stream_split(bsdc_bam_stream *s) {
 int32_t bsdc_bam_stream_next(bsdc_bam_stream *s, int64_t min_bytes, int64_t slack, bsdc_bam **out) {
     *out = nullptr;
     std::vector<uint8_t> take;  // per buffered family: goes out now
+    // room for a chunk, what stays behind and the fills in flight, reserved once (no regrowth,
+    // no fresh pages per fill)
+    const size_t want = (size_t)std::max<int64_t>(min_bytes, 0) * 5 / 4 + (size_t)s->read_size * 16;
+    if (s->buf.capacity() < want) s->buf.reserve(want);
+    if (s->spare.capacity() < want) s->spare.reserve(want);
     for (;;) {
         int32_t rc = stream_split(s);
         if (rc != 0) return rc;
         const bool end = s->eof && s->comp.empty();
-        if (end && !s->pend.empty()) return fail(BSDC_IO_EFORMAT, "truncated BAM record");
+        if (end && s->tail < (int64_t)s->buf.size()) return fail(BSDC_IO_EFORMAT, "truncated BAM record");
         take.assign(s->fams.size(), 0);
         int64_t bytes = 0;
         if (end) {  // every family is complete and nothing is left to read
@@ -722,19 +843,33 @@ int32_t bsdc_bam_stream_next(bsdc_bam_stream *s, int64_t min_bytes, int64_t slac
             b->header = s->hdr.header;
             b->ref_names = s->hdr.ref_names;
             b->ref_len = s->hdr.ref_len;
-            b->data.reserve((size_t)bytes + 8);
-            std::vector<uint8_t> keep;
+            // destinations by prefix sums (taken records to the chunk, the rest to `spare`, then
+            // the unsplit tail after them), then the copies in parallel
+            const int64_t nrec = (int64_t)s->recs.size();
+            std::vector<int64_t> dst((size_t)nrec);
             std::vector<StreamRec> krecs;
-            keep.reserve(s->buf.size() - (size_t)bytes);
-            for (auto &r : s->recs) {
-                const uint8_t *src = s->buf.data() + r.off;
+            int64_t ot = 0, ok = 0;
+            for (int64_t i = 0; i < nrec; i++) {
+                const StreamRec &r = s->recs[(size_t)i];
                 if (take[(size_t)r.fam]) {
-                    b->data.insert(b->data.end(), src, src + r.len);
+                    dst[(size_t)i] = ot;
+                    ot += r.len;
                 } else {
-                    krecs.push_back(StreamRec{(int64_t)keep.size(), r.len, r.fam});
-                    keep.insert(keep.end(), src, src + r.len);
+                    dst[(size_t)i] = -1 - ok;
+                    krecs.push_back(StreamRec{ok, r.len, r.fam});
+                    ok += r.len;
                 }
             }
+            const int64_t tail_n = (int64_t)s->buf.size() - s->tail;
+            b->data.resize((size_t)bytes + 8);
+            s->spare.resize((size_t)(ok + tail_n));
+#pragma omp parallel for schedule(dynamic, 1024)
+            for (int64_t i = 0; i < nrec; i++) {
+                const StreamRec &r = s->recs[(size_t)i];
+                uint8_t *to = dst[(size_t)i] >= 0 ? b->data.data() + dst[(size_t)i] : s->spare.data() + (-1 - dst[(size_t)i]);
+                memcpy(to, s->buf.data() + r.off, (size_t)r.len);
+            }
+            if (tail_n > 0) memcpy(s->spare.data() + ok, s->buf.data() + s->tail, (size_t)tail_n);
             for (size_t m = 0; m < s->fams.size(); m++)
                 if (take[m]) {
                     s->fams[m].n = 0;
@@ -742,9 +877,11 @@ int32_t bsdc_bam_stream_next(bsdc_bam_stream *s, int64_t min_bytes, int64_t slac
                 }
             for (auto it = s->fam_of.begin(); it != s->fam_of.end();)  // forget the emitted MI bases
                 it = s->fams[(size_t)it->second].n == 0 ? s->fam_of.erase(it) : std::next(it);
-            s->buf.swap(keep);
+            for (auto it = s->fam_exact.begin(); it != s->fam_exact.end();)
+                it = s->fams[(size_t)it->second].n == 0 ? s->fam_exact.erase(it) : std::next(it);
+            s->buf.swap(s->spare);
+            s->tail = ok;
             s->recs.swap(krecs);
-            b->data.resize((size_t)bytes + 8);
             rc = parse_records(b, 0, bytes);
             if (rc != 0) {
                 delete b;
@@ -915,35 +1052,20 @@ int32_t deflate_write(FILE *f, const uint8_t *src0, int64_t total, int32_t level
         const int64_t len = std::min(kBlock, total - i * kBlock);
         std::vector<uint8_t> &o = blocks[(size_t)i];
         o.resize(18 + (size_t)compressBound((uLong)len) + 8 + 64);
-        z_stream zs;
-        memset(&zs, 0, sizeof zs);
-        int lv = level;
-        for (int attempt = 0; attempt < 2; attempt++) {
-            if (deflateInit2(&zs, lv, Z_DEFLATED, -15, 8, Z_DEFAULT_STRATEGY) != Z_OK) {
-                bad |= 1;
-                break;
-            }
-            zs.next_in = const_cast<uint8_t *>(src);
-            zs.avail_in = (uInt)len;
-            zs.next_out = o.data() + 18;
-            zs.avail_out = (uInt)(o.size() - 26);
-            const int rc = deflate(&zs, Z_FINISH);
-            deflateEnd(&zs);
-            if (rc != Z_STREAM_END) {
-                bad |= 1;
-                break;
-            }
-            if (18 + zs.total_out + 8 <= 65536) break;
-            lv = 0;  // incompressible: store
-            memset(&zs, 0, sizeof zs);
+        // a block that does not shrink to fit BSIZE (incompressible) is stored (level 0)
+        int64_t clen = raw_deflate(src, len, level, o.data() + 18, 65536 - 26);
+        if (clen <= 0) clen = raw_deflate(src, len, 0, o.data() + 18, (int64_t)o.size() - 26);
+        if (clen <= 0 || 18 + clen + 8 > 65536) {
+            bad |= 1;
+            continue;
         }
-        const int64_t bsize = 18 + (int64_t)zs.total_out + 8;
+        const int64_t bsize = 18 + clen + 8;
         uint8_t *h = o.data();
         const uint8_t hdr[16] = {31, 139, 8, 4, 0, 0, 0, 0, 0, 255, 6, 0, 'B', 'C', 2, 0};
         memcpy(h, hdr, 16);
         wr16(h + 16, (uint16_t)(bsize - 1));
-        wr32(h + 18 + zs.total_out, (uint32_t)crc32(0L, src, (uInt)len));
-        wr32(h + 18 + zs.total_out + 4, (uint32_t)len);
+        wr32(h + 18 + clen, crc32_of(src, len));
+        wr32(h + 18 + clen + 4, (uint32_t)len);
         o.resize((size_t)bsize);
     }
     if (bad) return fail(BSDC_IO_EFORMAT, "deflate failed");

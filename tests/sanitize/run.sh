@@ -12,7 +12,7 @@ OUT="$ROOT/build/sanitize"
 mkdir -p "$OUT"
 SAN="-fsanitize=address,undefined -fno-sanitize-recover=undefined -fno-omit-frame-pointer -g -O1"
 g++ -std=c++17 -fopenmp -fPIC -shared -Wall $SAN -o "$OUT/libbsdc_io.so" \
-    "$ROOT/bsseqconsensusreads_amd/csrc/bsdc_io.cpp" "$ROOT/bsseqconsensusreads_amd/csrc/bsdc_host.cpp" -lz
+    "$ROOT/bsseqconsensusreads_amd/csrc/bsdc_io.cpp" "$ROOT/bsseqconsensusreads_amd/csrc/bsdc_host.cpp" -lz -ldl
 gcc -fopenmp -fPIC -shared -ffp-contract=off -Wall $SAN -o "$OUT/liboracle.so" "$ROOT/oracle/bsdc_oracle.c" -lm
 # python itself is not instrumented: the runtimes go in first; leak checking is off (the
 # interpreter keeps its arenas to exit)
