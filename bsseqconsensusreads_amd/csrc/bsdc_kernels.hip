@@ -63,6 +63,10 @@ constexpr int kVoteU = LARGE_VOTE_U;  // large buckets q >= this (2, 1 workgroup
 #define LARGE_OVL_CHUNKS 2  // k_large overlap: SWAR dwords (4 positions each) per task
 #endif
 constexpr int kOvlChunks = LARGE_OVL_CHUNKS;
+#ifndef LARGE_OVL_U
+#define LARGE_OVL_U 2  // k_large overlap: tasks per thread whose loads are in flight together
+#endif
+constexpr int kOvlU = LARGE_OVL_U;
 #ifndef LARGE_CONV_H
 #define LARGE_CONV_H 2  // k_large convert: SWAR dwords (4 positions each) per task, 1 or 2
 #endif
@@ -628,6 +632,53 @@ __device__ __forceinline__ void overlap_dw(uint8_t *bimg, uint8_t *qimg, uint32_
         }
     }
 }
+// overlap_dw in two halves, so a thread can have several dwords' loads in flight before any of
+// their stores (the dwords of different tasks share no byte): ovl_dw_load reads and masks,
+// ovl_dw_store computes and writes
+struct OvlDw {
+    Ovl4 in;
+    uint32_t A0, inm;
+    int32_t B0;
+    int lo, hi;
+};
+__device__ __forceinline__ OvlDw ovl_dw_load(const uint8_t *bimg, const uint8_t *qimg, uint32_t xa, uint32_t xb, int ovl,
+                                            int d) {
+    OvlDw t;
+    const int p0 = 4 * d - (int)(xa & 3u);
+    t.A0 = (xa & ~3u) + 4u * (uint32_t)d;
+    t.B0 = (int32_t)xb + p0;
+    t.lo = ::max(-p0, 0);
+    t.hi = ::min(ovl - p0, 4);
+    t.inm = t.hi > t.lo ? (0xFFFFFFFFu >> (32 - 8 * (t.hi - t.lo))) << (8 * t.lo) : 0u;
+    if (t.hi > t.lo) {
+        const int32_t Bl = t.B0 + t.lo;
+        const uint32_t sh = 8u * (uint32_t)t.lo;
+        t.in = Ovl4{lds32(bimg + t.A0), lds_any32(bimg, Bl) << sh, lds32(qimg + t.A0), lds_any32(qimg, Bl) << sh};
+    }
+    return t;
+}
+__device__ __forceinline__ void ovl_dw_store(uint8_t *bimg, uint8_t *qimg, const OvlDw &t) {
+    if (t.hi <= t.lo) return;
+    const Ovl4 o = ovl4_compute_m(t.in, t.inm);
+    const bool whole = t.inm == 0xFFFFFFFFu;  // (as overlap_dw)
+    if (whole) {
+        st32(bimg + t.A0, o.x);
+        st32(qimg + t.A0, o.qa);
+    }
+    if (whole && (t.B0 & 3) == 0) {
+        st32(bimg + t.B0, o.y);
+        st32(qimg + t.B0, o.qb);
+    } else {
+        for (int k = t.lo; k < t.hi; k++) {
+            if (!whole) {
+                bimg[t.A0 + k] = (uint8_t)(o.x >> (8 * k));
+                qimg[t.A0 + k] = (uint8_t)(o.qa >> (8 * k));
+            }
+            bimg[t.B0 + k] = (uint8_t)(o.y >> (8 * k));
+            qimg[t.B0 + k] = (uint8_t)(o.qb >> (8 * k));
+        }
+    }
+}
 __device__ __forceinline__ void ovl4_store(uint8_t *bimg, uint8_t *qimg, uint32_t ia, uint32_t ib, int rem, const Ovl4 &o) {
     if (rem >= 4) {
         stu32(bimg + ia, o.x);
@@ -673,8 +724,11 @@ __device__ __forceinline__ void lookup4v(const int32_t *lr2, uint32_t v, uint32_
 }
 // 0x01 in every byte of x (plain nt16 codes, <= 15) that is one-hot (A, C, G or T), 0 elsewhere
 __device__ __forceinline__ uint32_t onehot01(uint32_t x) {
-    const uint32_t t = x & ((x | 0x80808080u) - 0x01010101u);  // x & (x - 1) per byte, 0 for x = 0
-    return (~(t + 0x7F7F7F7Fu) & (x + 0x7F7F7F7Fu) & 0x80808080u) >> 7;  // t == 0 && x != 0
+    // one v_perm as a 16-entry byte table: selectors 0-7 pick the table bytes {0, 0x81, 1, 0, 1, 0,
+    // 0, 0}; 8 (T) sign-extends table byte 1 (0x81: 0xFF); 9-11 sign-extend bytes 3, 5, 7 (0);
+    // 12 gives 0 and 13-15 give 0xFF, cleared by the x >= 13 test (x + 3 reaches bit 4)
+    const uint32_t r = __builtin_amdgcn_perm(0x00000001u, 0x00018100u, x);
+    return r & ~((x + 0x03030303u) >> 4) & 0x01010101u;
 }
 // Mask of the bytes of a lane's dword that lie at or past a read's end, given k8 = 8 x (columns
 // the read still covers from this lane's first column), for a forward read (bytes ascend) or a
@@ -1828,12 +1882,24 @@ __device__ void process_large(const KParams &P, uint8_t *A, uint8_t *s_tab, cons
         // template map, the entry loads and the address math are paid once per task
         // aligned on mate a: the longest overlap spans (maxlen + 2 + 3) / 4 + 1 dwords of a
         const int SDo = ((maxlen_f + 2 + 3) / 4 + 1 + kOvlChunks - 1) / kOvlChunks;  // tasks of the longest overlap
-        for (int k = tt; k < nfast * SDo; k += G) {
-            const int g = k / SDo, d0 = kOvlChunks * (k - g * SDo);
-            const uint32_t xa = tl[3 * g], xb = tl[3 * g + 1];
-            const int ovl = (int)tl[3 * g + 2];
+        // kOvlU tasks per thread per round: all their loads, then all their stores (no byte of
+        // the image belongs to two tasks)
+        for (int k0 = tt; k0 < nfast * SDo; k0 += kOvlU * G) {
+            OvlDw t[kOvlU][kOvlChunks];
 #pragma unroll
-            for (int c = 0; c < kOvlChunks; c++) overlap_dw(slots, qimg, xa, xb, ovl, d0 + c);
+            for (int u = 0; u < kOvlU; u++) {
+                const int k = k0 + u * G;
+                const bool act = k < nfast * SDo;
+                const int g = act ? k / SDo : 0, d0 = kOvlChunks * (k - g * SDo);
+                const uint32_t xa = tl[3 * g], xb = tl[3 * g + 1];
+                const int ovl = act ? (int)tl[3 * g + 2] : 0;
+#pragma unroll
+                for (int c = 0; c < kOvlChunks; c++) t[u][c] = ovl_dw_load(slots, qimg, xa, xb, ovl, d0 + c);
+            }
+#pragma unroll
+            for (int u = 0; u < kOvlU; u++)
+#pragma unroll
+                for (int c = 0; c < kOvlChunks; c++) ovl_dw_store(slots, qimg, t[u][c]);
         }
         for (int i = tt >> 6; i < nslow; i += G / kWave) {
             const int r = (int)tl[2 * n - 1 - i];
@@ -2038,10 +2104,11 @@ __device__ void process_large(const KParams &P, uint8_t *A, uint8_t *s_tab, cons
     // Pass A: a lane owns 4 columns and walks the wave's reads, forward ones then reverse ones,
     // 4 in flight; descriptors are read 64 at a time, one per lane, and broadcast with v_readlane.
     // Per column: one likelihood sum over the reads showing an A/C/G/T there (Tables zero / lr
-    // rows: a non-ACGT code adds 0) and the OR of the codes.  A column whose OR is one A/C/G/T
+    // rows: a non-ACGT code adds 0) and the OR of those A/C/G/T codes.  A column whose OR is one
     // code, with a sum above one unit per read (no near tie with the unseen bases' 0), is resolved
-    // from the sum alone: S = 3 e^-T, as the four-sum path computes it.  Every other column (a
-    // disagreement, an N or IUPAC code, a small or negative sum) is marked (ssq = 0).
+    // from the sum alone: S = 3 e^-T, as the four-sum path computes it (an N or IUPAC code there
+    // adds nothing to any of the four sums).  Every other column (a disagreement, no A/C/G/T at
+    // all, a small or negative sum) is marked (ssq = 0).
     // Pass B: the marked columns, 8 lanes each: the lanes split the reads, sum per base, reduce
     // by lane shuffles, and the first lane makes the general call (resolve).
     constexpr int NW = G / kWave, PARTS = NW >= 8 ? 2 : 1;
@@ -2066,8 +2133,9 @@ __device__ void process_large(const KParams &P, uint8_t *A, uint8_t *s_tab, cons
                     const uint32_t keep = ~bytes_past(8 * sl - c8, false);
                     const int32_t a = (int32_t)ex + (sl > c ? c : 0);
                     const uint32_t b = lds_any32(slots, a) & keep, q = lds_any32(qimg, a);
-                    orm |= b;
-                    lookup4v(lr2, onehot01(b), q, t0, t1, t2, t3);
+                    const uint32_t v = onehot01(b);
+                    orm |= b & (v * 0xFFu);
+                    lookup4v(lr2, v, q, t0, t1, t2, t3);
                 };
                 auto rev = [&](uint32_t ex, uint32_t ey) {  // bytes run backwards from the read's last base
                     const int sl = (int)(ey & 0x7FFFFFFFu);
@@ -2075,8 +2143,9 @@ __device__ void process_large(const KParams &P, uint8_t *A, uint8_t *s_tab, cons
                     const int32_t a = (int32_t)ex - (sl > c ? c : 0) - 3;
                     const uint32_t b = comp4(__builtin_bswap32(lds_any32(slots, a) & keep));
                     const uint32_t q = __builtin_bswap32(lds_any32(qimg, a));
-                    orm |= b;
-                    lookup4v(lr2, onehot01(b), q, t0, t1, t2, t3);
+                    const uint32_t v = onehot01(b);
+                    orm |= b & (v * 0xFFu);
+                    lookup4v(lr2, v, q, t0, t1, t2, t3);
                 };
                 auto flush = [&]() {  // int32 partials over <= 64 reads: exact
                     T0 += t0;
