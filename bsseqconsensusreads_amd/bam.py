@@ -109,6 +109,8 @@ def _load():
     lib.bsdc_table_rank.restype = None
     lib.bsdc_table_take.argtypes = [C.c_int64, _P, _P, _P, _P, _P, C.c_int32]
     lib.bsdc_table_take.restype = C.c_int64
+    lib.bsdc_rows_gather.argtypes = [C.c_int64, _P, _P, C.c_int64, _P, _P, _P, C.c_int32]
+    lib.bsdc_rows_gather.restype = None
     if lib.bsdc_io_abi_version() != BSDC_IO_ABI_VERSION:
         raise RuntimeError("libbsdc_io ABI %d != %d" % (lib.bsdc_io_abi_version(), BSDC_IO_ABI_VERSION))
     _lib = lib
@@ -698,14 +700,18 @@ def duplex_records(cons, raw: R.RawRecords, prefix: str, threads: int = 0, molec
     if getattr(cons, "ss", None) is not None:
         tg = consensus_tags(cons, em, molecular, threads)
         auxs_t = _concat_fields([(auxs_t.buf, auxs_t.off), (tg.buf, tg.off)], n)
-    L = cons.length[em].astype(np.int64).reshape(-1)            # R1, R2, R1, R2 ...
+    L = np.ascontiguousarray(cons.length[em].reshape(-1), np.int32)  # R1, R2, R1, R2 ...
     seq_off = np.zeros(n + 1, np.int64)
     seq_off[1:] = np.cumsum(L)
     stride = cons.seq.shape[2]
-    flat = (np.repeat(em, 2) * 2 + np.tile([0, 1], F)) * stride  # row of (family, end)
-    idx = np.repeat(flat - seq_off[:-1], L) + np.arange(int(L.sum()), dtype=np.int64)
-    seq = cons.seq.reshape(-1)[idx]
-    qual = cons.qual.reshape(-1)[idx]
+    rows = np.ascontiguousarray(np.repeat(em.astype(np.int64), 2) * 2 + np.tile(np.asarray([0, 1], np.int64), F))
+    total = int(seq_off[-1])
+    seq = np.empty(max(total, 1), np.uint8)[:total]
+    qual = np.empty(max(total, 1), np.uint8)[:total]
+    for src, dst in ((cons.seq, seq), (cons.qual, qual)):  # the (family, end) rows, in record order
+        src = np.ascontiguousarray(src, np.uint8)
+        if n:
+            lib.bsdc_rows_gather(n, _ptr(rows), _ptr(L), int(stride), _ptr(src), _ptr(seq_off), _ptr(dst), int(threads))
     return OutRecordsBam(
         flag=np.tile(np.asarray([77, 141], np.uint16), F), tid=np.full(n, -1, np.int32), pos=np.full(n, -1, np.int32),
         mapq=np.zeros(n, np.uint8), next_tid=np.full(n, -1, np.int32), next_pos=np.full(n, -1, np.int32),

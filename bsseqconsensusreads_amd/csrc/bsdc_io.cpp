@@ -1663,6 +1663,13 @@ extern "C" int64_t bsdc_table_take(int64_t n, const int64_t *idx, const int64_t 
     return out_off[n];
 }
 
+extern "C" void bsdc_rows_gather(int64_t n, const int64_t *row, const int32_t *len, int64_t stride, const uint8_t *src,
+                                 const int64_t *out_off, uint8_t *out, int32_t n_threads) {
+    set_threads(n_threads);
+#pragma omp parallel for schedule(static)
+    for (int64_t i = 0; i < n; i++) memcpy(out + out_off[i], src + row[i] * stride, (size_t)len[i]);
+}
+
 extern "C" int32_t bsdc_family_image(int64_t n_rec, const int64_t *src_off, const int64_t *len, const int64_t *dst_off,
                                      const uint8_t *seq, const uint8_t *qual, int64_t n_slots, uint8_t *packed,
                                      uint8_t *qual_out, int32_t n_threads) {

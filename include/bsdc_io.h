@@ -148,6 +148,10 @@ int64_t bsdc_table_concat(int64_t n, int32_t k, const int64_t *const *offs, cons
 void bsdc_table_rank(int64_t n, const int64_t *off, const uint8_t *buf, int64_t *rank, int32_t n_threads);
 int64_t bsdc_table_take(int64_t n, const int64_t *idx, const int64_t *off, const uint8_t *buf, int64_t *out_off,
                         uint8_t *out_buf, int32_t n_threads);
+/* Fixed-stride rows -> a packed table: out[out_off[i], + len[i]) = src[row[i] * stride, + len[i])
+ * (the consensus rows of the emitted families, in record order; len[i] <= stride). */
+void bsdc_rows_gather(int64_t n, const int64_t *row, const int32_t *len, int64_t stride, const uint8_t *src,
+                      const int64_t *out_off, uint8_t *out, int32_t n_threads);
 
 /* Host side of the family batch (bsseqconsensusreads_amd/batch.py, include/bsdc.h layout): record r's
  * len[r] bases and quals, from seq/qual (nt16 codes and phred, one per byte) at src_off[r], go to
