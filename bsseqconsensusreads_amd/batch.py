@@ -316,11 +316,11 @@ def predict_rd(raw: R.RawRecords, ref: R.Reference, sel: np.ndarray, sL: np.ndar
 def lex_rank(strings, ids: np.ndarray) -> np.ndarray:
     """A key per element of ids that orders them as strings[id] sort in byte order."""
     ids = np.asarray(ids, np.int64)
-    if hasattr(strings, "lex_key"):  # synthetic names: computed, not materialised
-        return strings.lex_key(ids)
     from .bam import StringTable, table_ranks
     if isinstance(strings, StringTable):  # a decoded BAM's packed table: ranked in C++
         return table_ranks(strings)[ids] if ids.shape[0] else np.zeros(0, np.int64)
+    if hasattr(strings, "lex_key"):  # synthetic names: computed, not materialised
+        return strings.lex_key(ids)
     if ids.shape[0] == 0:
         return np.zeros(0, np.int64)
     u, inv = np.unique(ids, return_inverse=True)
