@@ -76,6 +76,8 @@ def _load():
     lib.bsdc_bam_stream_next.argtypes = [_P, C.c_int64, C.c_int64, C.POINTER(_P)]
     lib.bsdc_bam_stream_next.restype = C.c_int32
     lib.bsdc_bam_stream_close.argtypes = [_P]
+    lib.bsdc_bam_stream_recycle.argtypes = [_P, _P]
+    lib.bsdc_bam_stream_recycle.restype = None
     lib.bsdc_bam_stream_header.argtypes = [_P, C.POINTER(_P)]
     lib.bsdc_bam_stream_header.restype = C.c_int32
     lib.bsdc_bam_writer_open.argtypes = [C.c_char_p, C.c_char_p, C.c_int64, C.c_int32, _P, _P, _P, C.c_int32,
@@ -268,7 +270,7 @@ def stream_bam(path: str, threads: int = 0, chunk_bytes: int = DEFAULT_CHUNK_BYT
             try:
                 hdr, raw = _decode(lib, h, path)
             finally:
-                lib.bsdc_bam_free(h)
+                lib.bsdc_bam_stream_recycle(st, h)
             yield hdr, raw
     finally:
         lib.bsdc_bam_stream_close(st)
@@ -793,15 +795,22 @@ def step5_stream(in_bam: str, fasta: str, out_bam: Optional[str], engine=None, p
     outs: "queue.Queue" = queue.Queue(maxsize=1)
     err: list = []
     info = {"records_in": 0, "families": 0, "families_emitted": 0, "records_out": 0, "chunks": 0}
-    T = {"decode+plan": 0.0, "gpu": 0.0, "records": 0.0, "encode": 0.0}
+    T = {"decode": 0.0, "plan": 0.0, "gpu": 0.0, "records": 0.0, "encode": 0.0, "gpu_wait": 0.0, "writer_wait": 0.0}
     first = {}
 
     def reader():
         try:
-            for hdr, raw in stream_bam(in_bam, threads, chunk_bytes, slack):
+            it = stream_bam(in_bam, threads, chunk_bytes, slack)
+            while True:
+                t0 = time.perf_counter()
+                nxt = next(it, None)
+                T["decode"] += time.perf_counter() - t0
+                if nxt is None:
+                    break
+                raw = nxt[1]
                 t0 = time.perf_counter()
                 plan = pipeline.plan_families(raw, "full", first["ref"])
-                T["decode+plan"] += time.perf_counter() - t0
+                T["plan"] += time.perf_counter() - t0
                 chunks.put((raw, plan))
         except BaseException as e:  # noqa: BLE001 -- handed to the main thread
             err.append(e)
@@ -813,7 +822,9 @@ def step5_stream(in_bam: str, fasta: str, out_bam: Optional[str], engine=None, p
             w = BamWriter(out_bam, output_header(first["header"]), level) if out_bam is not None else None
             fq = FastqWriter(fastq[0], fastq[1], level) if fastq is not None else None
             while True:
+                t0 = time.perf_counter()
                 item = outs.get()
+                T["writer_wait"] += time.perf_counter() - t0
                 if item is None:
                     break
                 cons, raw = item
@@ -851,7 +862,9 @@ def step5_stream(in_bam: str, fasta: str, out_bam: Optional[str], engine=None, p
         mode = pipeline.MODE_CONVERT | pipeline.MODE_EXTEND | pipeline.MODE_VOTE
         try:
             while True:
+                t0 = time.perf_counter()
                 item = chunks.get()
+                T["gpu_wait"] += time.perf_counter() - t0
                 if item is None:
                     break
                 raw, plan = item

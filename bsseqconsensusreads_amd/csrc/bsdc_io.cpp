@@ -367,15 +367,23 @@ int32_t parse_header(const uint8_t *d, int64_t dn, bsdc_bam *b, int64_t *p_out) 
 }
 
 // The records of b->data from offset p to dn (whole records only): boundaries, tags, interning.
+// (rec_start already filled: the records at those offsets, each whole inside [0, dn), as the
+// streaming reader hands them over)
 int32_t parse_records(bsdc_bam *b, int64_t p, int64_t dn) {
     const uint8_t *d = b->data.data();
-    while (p + 4 <= dn) {
-        const int64_t bs = rd32(d + p);
-        if (bs < 32 || p + 4 + bs > dn) return fail(BSDC_IO_EFORMAT, "truncated BAM record");
-        b->rec_start.push_back(p);
-        p += 4 + bs;
+    if (b->rec_start.empty()) {
+        while (p + 4 <= dn) {
+            const int64_t bs = rd32(d + p);
+            if (bs < 32 || p + 4 + bs > dn) return fail(BSDC_IO_EFORMAT, "truncated BAM record");
+            b->rec_start.push_back(p);
+            p += 4 + bs;
+        }
+        if (p != dn) return fail(BSDC_IO_EFORMAT, "truncated BAM record");
+    } else {
+        for (const int64_t q : b->rec_start)
+            if (q < 0 || q + 4 > dn || rd32(d + q) < 32 || q + 4 + (int64_t)rd32(d + q) > dn)
+                return fail(BSDC_IO_EFORMAT, "truncated BAM record");
     }
-    if (p != dn) return fail(BSDC_IO_EFORMAT, "truncated BAM record");
     const int64_t nr = (int64_t)b->rec_start.size();
     // ---- per record: tags, sizes ----
     b->la.assign(nr, -1);
@@ -845,31 +853,33 @@ int32_t bsdc_bam_stream_next(bsdc_bam_stream *s, int64_t min_bytes, int64_t slac
             b->ref_len = s->hdr.ref_len;
             // destinations by prefix sums (taken records to the chunk, the rest to `spare`, then
             // the unsplit tail after them), then the copies in parallel
+            // the chunk takes the whole buffer (its records stay where they are, listed in file
+            // order); the records kept back and the unsplit tail move to `spare`, the next buffer
             const int64_t nrec = (int64_t)s->recs.size();
-            std::vector<int64_t> dst((size_t)nrec);
+            std::vector<int64_t> src_k;
             std::vector<StreamRec> krecs;
-            int64_t ot = 0, ok = 0;
+            b->rec_start.reserve((size_t)nrec);
+            int64_t ok = 0;
             for (int64_t i = 0; i < nrec; i++) {
                 const StreamRec &r = s->recs[(size_t)i];
                 if (take[(size_t)r.fam]) {
-                    dst[(size_t)i] = ot;
-                    ot += r.len;
+                    b->rec_start.push_back(r.off);
                 } else {
-                    dst[(size_t)i] = -1 - ok;
+                    src_k.push_back(r.off);
                     krecs.push_back(StreamRec{ok, r.len, r.fam});
                     ok += r.len;
                 }
             }
             const int64_t tail_n = (int64_t)s->buf.size() - s->tail;
-            b->data.resize((size_t)bytes + 8);
             s->spare.resize((size_t)(ok + tail_n));
+            const int64_t nk = (int64_t)krecs.size();
 #pragma omp parallel for schedule(dynamic, 1024)
-            for (int64_t i = 0; i < nrec; i++) {
-                const StreamRec &r = s->recs[(size_t)i];
-                uint8_t *to = dst[(size_t)i] >= 0 ? b->data.data() + dst[(size_t)i] : s->spare.data() + (-1 - dst[(size_t)i]);
-                memcpy(to, s->buf.data() + r.off, (size_t)r.len);
-            }
+            for (int64_t i = 0; i < nk; i++)
+                memcpy(s->spare.data() + krecs[(size_t)i].off, s->buf.data() + src_k[(size_t)i], (size_t)krecs[(size_t)i].len);
             if (tail_n > 0) memcpy(s->spare.data() + ok, s->buf.data() + s->tail, (size_t)tail_n);
+            const int64_t dn = (int64_t)s->buf.size();
+            b->data.swap(s->buf);
+            b->data.resize((size_t)dn + 8);
             for (size_t m = 0; m < s->fams.size(); m++)
                 if (take[m]) {
                     s->fams[m].n = 0;
@@ -879,10 +889,10 @@ int32_t bsdc_bam_stream_next(bsdc_bam_stream *s, int64_t min_bytes, int64_t slac
                 it = s->fams[(size_t)it->second].n == 0 ? s->fam_of.erase(it) : std::next(it);
             for (auto it = s->fam_exact.begin(); it != s->fam_exact.end();)
                 it = s->fams[(size_t)it->second].n == 0 ? s->fam_exact.erase(it) : std::next(it);
-            s->buf.swap(s->spare);
+            s->buf.swap(s->spare);  // (spare is now the chunk's old, empty vector: reserved on the next call)
             s->tail = ok;
             s->recs.swap(krecs);
-            rc = parse_records(b, 0, bytes);
+            rc = parse_records(b, 0, dn);
             if (rc != 0) {
                 delete b;
                 return rc;
@@ -893,6 +903,14 @@ int32_t bsdc_bam_stream_next(bsdc_bam_stream *s, int64_t min_bytes, int64_t slac
         rc = bsdc_bam_stream_fill(s);
         if (rc != 0) return rc;
     }
+}
+
+void bsdc_bam_stream_recycle(bsdc_bam_stream *s, bsdc_bam *b) {
+    if (s && b && s->spare.capacity() < b->data.capacity()) {
+        s->spare.swap(b->data);
+        s->spare.clear();
+    }
+    delete b;
 }
 
 // The stream's header and references as a record-less bsdc_bam.

@@ -111,30 +111,42 @@ class DeviceBatch:
                 self.len[:2 * F].cpu().numpy().view(np.uint16).astype(np.int32).reshape(F, 2))
 
     def fetch(self):
-        """-> dict of numpy arrays (consensus and, if dumped, the post-tool records)."""
+        """-> dict of numpy arrays (consensus and, if dumped, the post-tool records).  The copies
+        are queued together on the current stream into pinned host memory (torch's caching host
+        allocator), then one synchronize."""
         F = self.n_fam
+        t = {"status": self.status[:F], "len": self.len[:2 * F], "seq": self.seq[:F * self.stride],
+             "qual": self.qual[:2 * F * self.stride]}
+        n = 4 * F * self.stride
+        if self.tags:
+            t.update(ss_len=self.ss_len[:4 * F], ss_base=self.ss_base[:n], ss_qual=self.ss_qual[:n],
+                     ss_depth=self.ss_depth[:n], ss_err=self.ss_err[:n])
+        Rn = self.n_rec
+        if self.dump:
+            t.update(dump_pos=self.dump_pos[:Rn], dump_len=self.dump_len[:Rn], dump_tags=self.dump_tags[:Rn],
+                     dump_seq=self.dump_seq, dump_qual=self.dump_qual)
+        h = {k: v.to("cpu", non_blocking=True) for k, v in t.items()}
+        torch.cuda.current_stream(self.device).synchronize()
+        a = {k: v.numpy() for k, v in h.items()}
         out = {
-            "status": self.status[:F].cpu().numpy(),
-            "len": self.len[:2 * F].cpu().numpy().view(np.uint16).astype(np.int32).reshape(F, 2),
-            "seq": self.seq[:F * self.stride].cpu().numpy().reshape(F, 2, self.stride // 2),
-            "qual": self.qual[:2 * F * self.stride].cpu().numpy().reshape(F, 2, self.stride),
+            "status": a["status"],
+            "len": a["len"].view(np.uint16).astype(np.int32).reshape(F, 2),
+            "seq": a["seq"].reshape(F, 2, self.stride // 2),
+            "qual": a["qual"].reshape(F, 2, self.stride),
             "stride": self.stride,
         }
         if self.tags:
-            n = 4 * F * self.stride
-            u16 = lambda t: t.cpu().numpy().view(np.uint16)
-            out["ss_len"] = u16(self.ss_len[:4 * F]).astype(np.int32).reshape(F, 4)
-            out["ss_base"] = self.ss_base[:n].cpu().numpy().reshape(F, 4, self.stride)
-            out["ss_qual"] = self.ss_qual[:n].cpu().numpy().reshape(F, 4, self.stride)
-            out["ss_depth"] = u16(self.ss_depth[:n]).reshape(F, 4, self.stride)
-            out["ss_err"] = u16(self.ss_err[:n]).reshape(F, 4, self.stride)
+            out["ss_len"] = a["ss_len"].view(np.uint16).astype(np.int32).reshape(F, 4)
+            out["ss_base"] = a["ss_base"].reshape(F, 4, self.stride)
+            out["ss_qual"] = a["ss_qual"].reshape(F, 4, self.stride)
+            out["ss_depth"] = a["ss_depth"].view(np.uint16).reshape(F, 4, self.stride)
+            out["ss_err"] = a["ss_err"].view(np.uint16).reshape(F, 4, self.stride)
         if self.dump:
-            Rn = self.n_rec
-            out["dump_pos"] = self.dump_pos[:Rn].cpu().numpy()
-            out["dump_len"] = self.dump_len[:Rn].cpu().numpy().view(np.uint16).astype(np.int32)
-            out["dump_tags"] = self.dump_tags[:Rn].cpu().numpy()
-            out["dump_seq"] = self.dump_seq.cpu().numpy()
-            out["dump_qual"] = self.dump_qual.cpu().numpy()
+            out["dump_pos"] = a["dump_pos"]
+            out["dump_len"] = a["dump_len"].view(np.uint16).astype(np.int32)
+            out["dump_tags"] = a["dump_tags"]
+            out["dump_seq"] = a["dump_seq"]
+            out["dump_qual"] = a["dump_qual"]
         return out
 
 

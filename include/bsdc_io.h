@@ -91,6 +91,9 @@ int32_t bsdc_bam_stream_fill(bsdc_bam_stream *s);
 int32_t bsdc_bam_stream_next(bsdc_bam_stream *s, int64_t min_bytes, int64_t slack, bsdc_bam **out);
 int32_t bsdc_bam_stream_header(const bsdc_bam_stream *s, bsdc_bam **out); /* header only, no records */
 void bsdc_bam_stream_close(bsdc_bam_stream *s);
+/* bsdc_bam_free for a chunk of this stream that has been copied out: its buffer goes back to the
+ * stream for the next chunk (no fresh pages per chunk). */
+void bsdc_bam_stream_recycle(bsdc_bam_stream *s, bsdc_bam *b);
 
 /* Records to write (n_rec entries; every *_off array has n_rec + 1 entries). */
 typedef struct {
