@@ -776,11 +776,11 @@ def step5_stream(in_bam: str, fasta: str, out_bam: Optional[str], engine=None, p
                  threads: int = 0, level: int = 6, fastq: Optional[Tuple[str, str]] = None, tags: bool = True,
                  chunk_bytes: int = DEFAULT_CHUNK_BYTES, slack: int = DEFAULT_SLACK,
                  batch_bases: Optional[int] = None, stats: Optional[dict] = None) -> dict:
-    """step5 in bounded memory, pipelined: a reader thread decodes the next chunk of the
-    coordinate-sorted input (stream_bam: cut where no template or MI family straddles) and forms
-    its families (C++ plan); this thread runs the chunk's family batches on the GPU; a writer
-    thread builds the output records of the previous chunk and appends them to the BAM
-    (BamWriter).  Peak host memory is about three chunks, whatever the file size.  The output is
+    """step5 in bounded memory, pipelined: a decoder thread decodes the next chunk of the
+    coordinate-sorted input (stream_bam: cut where no template or MI family straddles), a reader
+    thread forms the previous chunk's families (C++ plan); this thread runs the chunk's family
+    batches on the GPU; a writer thread builds the output records of the chunk before and appends
+    them to the BAM (BamWriter).  Peak host memory is about five chunks, whatever the file size.  The output is
     byte-identical to step5's (tests/test_stream.py): every chunk's TemplateCoordinate keys sort
     before the next chunk's, so the chunks' families in order are the whole file's."""
     import queue
@@ -798,7 +798,9 @@ def step5_stream(in_bam: str, fasta: str, out_bam: Optional[str], engine=None, p
     T = {"decode": 0.0, "plan": 0.0, "gpu": 0.0, "records": 0.0, "encode": 0.0, "gpu_wait": 0.0, "writer_wait": 0.0}
     first = {}
 
-    def reader():
+    raws: "queue.Queue" = queue.Queue(maxsize=1)
+
+    def decoder():  # the next chunk decodes while the previous one's families form
         try:
             it = stream_bam(in_bam, threads, chunk_bytes, slack)
             while True:
@@ -807,13 +809,26 @@ def step5_stream(in_bam: str, fasta: str, out_bam: Optional[str], engine=None, p
                 T["decode"] += time.perf_counter() - t0
                 if nxt is None:
                     break
-                raw = nxt[1]
+                raws.put(nxt[1])
+        except BaseException as e:  # noqa: BLE001 -- handed to the main thread
+            err.append(e)
+        finally:
+            raws.put(None)
+
+    def reader():
+        try:
+            while True:
+                raw = raws.get()
+                if raw is None:
+                    break
                 t0 = time.perf_counter()
                 plan = pipeline.plan_families(raw, "full", first["ref"])
                 T["plan"] += time.perf_counter() - t0
                 chunks.put((raw, plan))
         except BaseException as e:  # noqa: BLE001 -- handed to the main thread
             err.append(e)
+            while raws.get() is not None:  # let the decoder finish
+                pass
         finally:
             chunks.put(None)
 
@@ -855,8 +870,10 @@ def step5_stream(in_bam: str, fasta: str, out_bam: Optional[str], engine=None, p
     first["prefix"] = read_name_prefix(hdr0) if prefix is None else prefix
     try:
         eng.load_reference(ref)
+        td = threading.Thread(target=decoder, daemon=True)
         tr = threading.Thread(target=reader, daemon=True)
         tw = threading.Thread(target=writer, daemon=True)
+        td.start()
         tr.start()
         tw.start()
         mode = pipeline.MODE_CONVERT | pipeline.MODE_EXTEND | pipeline.MODE_VOTE
@@ -889,6 +906,7 @@ def step5_stream(in_bam: str, fasta: str, out_bam: Optional[str], engine=None, p
             outs.put(None)
             tw.join()
             tr.join()
+            td.join()
     finally:
         if own:
             eng.close()
