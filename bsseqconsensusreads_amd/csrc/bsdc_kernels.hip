@@ -2237,7 +2237,21 @@ __device__ void process_large(const KParams &P, uint8_t *A, uint8_t *s_tab, cons
     {
         const int s = ws, na = cnt[s], nm = s_lc[s];
         const uint2 *dl = desc + soff[s];
-        for (int k0 = kWave * wpart; k0 < nm; k0 += kWave * PARTS) {
+        // With two waves per set (PARTS = 2) both take the same 64 marked columns and split the
+        // set's reads; part 1's four sums meet part 0's through LDS (int32: exact for <= 127
+        // reads a part, |lr| < 2^24), after mlist in the part-sum region.  Workgroup-uniform:
+        // every set must fit, and every wave runs the same number of blocks (barriers inside).
+        const int64_t region = ::max((int64_t)round16((int64_t)n * (int64_t)bsdc_layout::kRecMetaBytes) + round16(2 * (int64_t)n),
+                                     (int64_t)36 * ssw);
+        const int64_t pbo = round16(8 * (int64_t)ssw);
+        const bool split = PARTS == 2 && pbo + 4 * kWave * 16 <= region &&
+                           ::max(::max(cnt[0], cnt[1]), ::max(cnt[2], cnt[3])) <= 254;
+        int32_t *pb = reinterpret_cast<int32_t *>(reinterpret_cast<uint8_t *>(psum) + pbo);  // [4][64][4]
+        const int nmax = ::max(::max(s_lc[0], s_lc[1]), ::max(s_lc[2], s_lc[3]));
+        const int rb = split ? (wpart == 0 ? 0 : na / 2) : 0, re = split ? (wpart == 0 ? na / 2 : na) : na;
+        const int kstart = split ? 0 : kWave * wpart, kstep = split ? kWave : kWave * PARTS;
+        const int kend = split ? nmax : nm;
+        for (int k0 = kstart; k0 < kend; k0 += kstep) {
             const bool act = k0 + lane < nm;
             const int col = act ? mlist[s * ssw + k0 + lane] : 0;
             long long D0 = 0, D1 = 0, D2 = 0, D3 = 0;
@@ -2253,9 +2267,9 @@ __device__ void process_large(const KParams &P, uint8_t *A, uint8_t *s_tab, cons
                 d2 += bb == kG ? v : 0;
                 d3 += bb == kT ? v : 0;
             };
-            for (int r0 = 0; r0 < na; r0 += kWave) {
-                const uint2 dr = r0 + lane < na ? dl[r0 + lane] : make_uint2(0u, 0u);
-                const int nr = ::min(kWave, na - r0);
+            for (int r0 = rb; r0 < re && k0 < nm; r0 += kWave) {
+                const uint2 dr = r0 + lane < re ? dl[r0 + lane] : make_uint2(0u, 0u);
+                const int nr = ::min(kWave, re - r0);
                 int i = 0;
                 for (; i + 7 < nr; i += 8) {  // 8 reads' loads in flight
 #pragma unroll
@@ -2268,7 +2282,20 @@ __device__ void process_large(const KParams &P, uint8_t *A, uint8_t *s_tab, cons
                 D3 += d3;
                 d0 = d1 = d2 = d3 = 0;
             }
-            if (act) resolve(s, col, D0, D1, D2, D3);
+            if (split) {
+                int32_t *pw = pb + 4 * (s * kWave + lane);
+                if (wpart == 1 && act) {
+                    pw[0] = (int32_t)D0;
+                    pw[1] = (int32_t)D1;
+                    pw[2] = (int32_t)D2;
+                    pw[3] = (int32_t)D3;
+                }
+                __syncthreads();
+                if (wpart == 0 && act) resolve(s, col, D0 + pw[0], D1 + pw[1], D2 + pw[2], D3 + pw[3]);
+                __syncthreads();
+            } else if (act) {
+                resolve(s, col, D0, D1, D2, D3);
+            }
         }
     }
     __syncthreads();
