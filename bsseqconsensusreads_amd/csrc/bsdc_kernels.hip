@@ -67,6 +67,12 @@ constexpr int kOvlChunks = LARGE_OVL_CHUNKS;
 #define LARGE_OVL_U 2  // k_large overlap: tasks per thread whose loads are in flight together
 #endif
 constexpr int kOvlU = LARGE_OVL_U;
+#ifndef LARGE_OVL_BSTORE
+#define LARGE_OVL_BSTORE 1  // k_large overlap, mate b's unaligned whole dwords: 0 bytes, 1 one unaligned dword, 2 16-bit halves
+#endif
+#ifndef SMALL_OVL_BSTORE
+#define SMALL_OVL_BSTORE 1  // the same for k_small's overlap (overlap_dw): 0 bytes, 1 one unaligned dword
+#endif
 #ifndef LARGE_CONV_H
 #define LARGE_CONV_H 2  // k_large convert: SWAR dwords (4 positions each) per task, 1 or 2
 #endif
@@ -546,6 +552,7 @@ __device__ __forceinline__ uint32_t ldsu32(const uint8_t *p) {
     return v;
 }
 __device__ __forceinline__ void stu32(uint8_t *p, uint32_t v) { __builtin_memcpy(p, &v, 4); }
+__device__ __forceinline__ void st16(uint8_t *p, uint16_t v) { *reinterpret_cast<uint16_t *>(p) = v; }  // 2-aligned p
 // The LDS dword at any byte offset p of `base` (16-aligned) from two aligned loads and a byte
 // align: gfx950 LDS stalls an unaligned dword access (SQ_LDS_UNALIGNED_STALL)
 __device__ __forceinline__ uint32_t lds_any32(const uint8_t *base, int32_t p) {
@@ -621,6 +628,11 @@ __device__ __forceinline__ void overlap_dw(uint8_t *bimg, uint8_t *qimg, uint32_
     if (whole && (B0 & 3) == 0) {
         st32(bimg + B0, o.y);
         st32(qimg + B0, o.qb);
+#if SMALL_OVL_BSTORE == 1
+    } else if (whole) {  // b's unaligned dword: one unaligned ds_write_b32 each (fewer LDS ops than 4 bytes)
+        stu32(bimg + B0, o.y);
+        stu32(qimg + B0, o.qb);
+#endif
     } else {
         for (int k = lo; k < hi; k++) {
             if (!whole) {
@@ -668,6 +680,24 @@ __device__ __forceinline__ void ovl_dw_store(uint8_t *bimg, uint8_t *qimg, const
     if (whole && (t.B0 & 3) == 0) {
         st32(bimg + t.B0, o.y);
         st32(qimg + t.B0, o.qb);
+#if LARGE_OVL_BSTORE == 1
+    } else if (whole) {  // b's unaligned dword: one unaligned ds_write_b32 each
+        stu32(bimg + t.B0, o.y);
+        stu32(qimg + t.B0, o.qb);
+#elif LARGE_OVL_BSTORE == 2
+    } else if (whole && (t.B0 & 1) == 0) {  // b's dword on a 2-byte boundary: two ds_write_b16 each
+        st16(bimg + t.B0, (uint16_t)o.y);
+        st16(bimg + t.B0 + 2, (uint16_t)(o.y >> 16));
+        st16(qimg + t.B0, (uint16_t)o.qb);
+        st16(qimg + t.B0 + 2, (uint16_t)(o.qb >> 16));
+    } else if (whole) {  // odd: byte, 16-bit, byte
+        bimg[t.B0] = (uint8_t)o.y;
+        st16(bimg + t.B0 + 1, (uint16_t)(o.y >> 8));
+        bimg[t.B0 + 3] = (uint8_t)(o.y >> 24);
+        qimg[t.B0] = (uint8_t)o.qb;
+        st16(qimg + t.B0 + 1, (uint16_t)(o.qb >> 8));
+        qimg[t.B0 + 3] = (uint8_t)(o.qb >> 24);
+#endif
     } else {
         for (int k = t.lo; k < t.hi; k++) {
             if (!whole) {
