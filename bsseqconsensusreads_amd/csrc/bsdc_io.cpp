@@ -518,6 +518,8 @@ struct StreamRec {
 using TcKey = std::pair<int64_t, int64_t>;
 constexpr int64_t kBigTid = 0x7FFFFFFF;
 constexpr int64_t kKeyDelta = 4;  // |key position before tools 1 + 2 - after| <= 2, twice
+constexpr int kFamShards = 64;
+inline int fam_shard(uint64_t h) { return (int)(h >> 58); }
 struct StreamFam {
     int64_t lo = INT64_MAX, hi = INT64_MIN;  // min own position, max own or mate position (coord)
     TcKey klo{INT64_MAX, INT64_MAX}, khi{INT64_MIN, INT64_MIN};  // bounds of its records' keys
@@ -539,12 +541,15 @@ struct bsdc_bam_stream {
     // buffered records (file order) and their families
     std::vector<uint8_t> buf;
     std::vector<StreamRec> recs;
-    std::unordered_map<uint64_t, int32_t> fam_of;  // hash of the MI base -> family
+    // hash of the MI base -> family, in kFamShards shards by the hash's top bits (the shards are
+    // filled in parallel, one thread each)
+    std::vector<std::unordered_map<uint64_t, int32_t>> fam_of = std::vector<std::unordered_map<uint64_t, int32_t>>(kFamShards);
     std::unordered_map<std::string, int32_t> fam_exact;  // MI bases whose hash another live family holds
     std::vector<std::string> fam_key;               // per family: its MI base
     std::vector<StreamFam> fams;
     std::vector<int32_t> free_fams;
     int64_t cursor = INT64_MIN;  // the last record's position
+    int64_t par_min = 1 << 14;   // records per split from which families are assigned in parallel
 };
 
 int32_t bsdc_bam_stream_open(const char *path, int32_t n_threads, int64_t read_size, bsdc_bam_stream **out) {
@@ -555,6 +560,7 @@ int32_t bsdc_bam_stream_open(const char *path, int32_t n_threads, int64_t read_s
     auto *s = new bsdc_bam_stream();
     s->f = f;
     s->read_size = read_size > 0 ? read_size : ((int64_t)64 << 20);
+    if (const char *e = getenv("BSDC_STREAM_PAR_MIN")) s->par_min = atoll(e);  // (tests: 0 = always parallel)
     // inflate until the header is whole
     for (;;) {
         int64_t p = 0;
@@ -734,17 +740,140 @@ int32_t stream_split(bsdc_bam_stream *s) {
             auto ie = s->fam_exact.find(std::string(mi));
             if (ie != s->fam_exact.end() && s->fams[(size_t)ie->second].n > 0) return ie->second;
         }
-        auto it = s->fam_of.find(h);
-        if (it != s->fam_of.end() && s->fams[(size_t)it->second].n > 0 && s->fam_key[(size_t)it->second] == mi)
+        auto &fm = s->fam_of[(size_t)fam_shard(h)];
+        auto it = fm.find(h);
+        if (it != fm.end() && s->fams[(size_t)it->second].n > 0 && s->fam_key[(size_t)it->second] == mi)
             return it->second;
         const int32_t fam = new_fam();
         s->fam_key[(size_t)fam].assign(mi.data(), mi.size());
-        if (it == s->fam_of.end()) s->fam_of.emplace(h, fam);
+        if (it == fm.end()) fm.emplace(h, fam);
         else if (s->fams[(size_t)it->second].n == 0) it->second = fam;
         else s->fam_exact[std::string(mi)] = fam;  // collision with a live family
         return fam;
     };
     const int64_t base = s->tail;
+    if (nr > 0 && nr >= s->par_min && s->fam_exact.empty()) {
+        // ---- the same in parallel: families by hash shard (a family's records all fall in one
+        // shard), new families numbered in shard order, 64-bit collisions resolved serially ----
+        int unsorted = 0;
+#pragma omp parallel for schedule(static) reduction(| : unsorted)
+        for (int64_t k = 0; k < nr; k++)
+            unsorted |= P[(size_t)k].c < (k > 0 ? P[(size_t)k - 1].c : s->cursor);
+        if (unsorted)
+            return fail(BSDC_IO_EFORMAT, "input is not coordinate-sorted (the streaming step needs the "
+                                         "coordinate order of the step-5 input; read it whole instead)");
+        constexpr int S = kFamShards;  // + bucket S: records without MI
+        std::vector<int64_t> sstart(S + 2, 0);
+        std::vector<uint8_t> shard_of((size_t)nr);
+        for (int64_t k = 0; k < nr; k++) {
+            const int sh = P[(size_t)k].mi.empty() ? S : fam_shard(P[(size_t)k].h);
+            shard_of[(size_t)k] = (uint8_t)sh;
+            sstart[(size_t)sh + 1]++;
+        }
+        for (int sh = 0; sh <= S; sh++) sstart[(size_t)sh + 1] += sstart[(size_t)sh];
+        std::vector<int64_t> sorder((size_t)nr), sfill(sstart.begin(), sstart.end() - 1);
+        for (int64_t k = 0; k < nr; k++) sorder[(size_t)sfill[shard_of[(size_t)k]]++] = k;
+        // fam[k]: >= 0 an existing family; -1 no MI; -2 a collision; <= -3 new family -3 - i of the shard
+        std::vector<int32_t> famv((size_t)nr);
+        std::vector<std::vector<int64_t>> newfirst(S + 1);
+#pragma omp parallel for schedule(dynamic, 1)
+        for (int sh = 0; sh <= S; sh++) {
+            if (sh == S) {
+                for (int64_t i = sstart[S]; i < sstart[S + 1]; i++) famv[(size_t)sorder[(size_t)i]] = -1;
+                continue;
+            }
+            auto &fm = s->fam_of[(size_t)sh];
+            std::unordered_map<uint64_t, int32_t> nw;
+            std::vector<int64_t> &nf = newfirst[(size_t)sh];
+            for (int64_t i = sstart[(size_t)sh]; i < sstart[(size_t)sh + 1]; i++) {
+                const int64_t k = sorder[(size_t)i];
+                const Parsed &q = P[(size_t)k];
+                auto it = fm.find(q.h);
+                if (it != fm.end() && s->fams[(size_t)it->second].n > 0) {
+                    famv[(size_t)k] = s->fam_key[(size_t)it->second] == q.mi ? it->second : -2;
+                    continue;
+                }
+                auto jt = nw.find(q.h);
+                if (jt == nw.end()) {
+                    nw.emplace(q.h, (int32_t)nf.size());
+                    famv[(size_t)k] = -3 - (int32_t)nf.size();
+                    nf.push_back(k);
+                } else {
+                    famv[(size_t)k] = P[(size_t)nf[(size_t)jt->second]].mi == q.mi ? -3 - jt->second : -2;
+                }
+            }
+        }
+        // new families get ids (free list first), shard by shard; then the records without MI and
+        // the collisions, in file order (the exact map)
+        std::vector<std::vector<int32_t>> gid(S);
+        std::vector<uint8_t> fresh;  // families created by this split (live before their records count)
+        auto mark_fresh = [&](int32_t f) {
+            if ((size_t)f >= fresh.size()) fresh.resize((size_t)f + 1, 0);
+            fresh[(size_t)f] = 1;
+        };
+        for (int sh = 0; sh < S; sh++)
+            for (size_t i = 0; i < newfirst[(size_t)sh].size(); i++) {
+                const int32_t f = new_fam();
+                mark_fresh(f);
+                gid[(size_t)sh].push_back(f);
+            }
+#pragma omp parallel for schedule(dynamic, 1)
+        for (int sh = 0; sh < S; sh++) {  // their keys and map entries (a stale entry is taken over)
+            auto &fm = s->fam_of[(size_t)sh];
+            const std::vector<int64_t> &nf = newfirst[(size_t)sh];
+            for (size_t i = 0; i < nf.size(); i++) {
+                const Parsed &q = P[(size_t)nf[i]];
+                const int32_t f = gid[(size_t)sh][i];
+                s->fam_key[(size_t)f].assign(q.mi.data(), q.mi.size());
+                fm[q.h] = f;
+            }
+        }
+        for (int64_t k = 0; k < nr; k++) {
+            if (famv[(size_t)k] == -1) {
+                famv[(size_t)k] = new_fam();
+                mark_fresh(famv[(size_t)k]);
+            } else if (famv[(size_t)k] == -2) {
+                const std::string key(P[(size_t)k].mi);
+                auto ie = s->fam_exact.find(key);
+                if (ie != s->fam_exact.end() &&
+                    (s->fams[(size_t)ie->second].n > 0 || ((size_t)ie->second < fresh.size() && fresh[(size_t)ie->second]))) {
+                    famv[(size_t)k] = ie->second;
+                } else {
+                    const int32_t f = new_fam();
+                    mark_fresh(f);
+                    s->fam_key[(size_t)f] = key;
+                    s->fam_exact[key] = f;
+                    famv[(size_t)k] = f;
+                }
+            }
+        }
+        // ids and per-family bounds, shard by shard (disjoint families), then the records
+#pragma omp parallel for schedule(dynamic, 1)
+        for (int sh = 0; sh <= S; sh++) {
+            for (int64_t i = sstart[(size_t)sh]; i < sstart[(size_t)sh + 1]; i++) {
+                const int64_t k = sorder[(size_t)i];
+                int32_t &f = famv[(size_t)k];
+                if (f <= -3) f = gid[(size_t)sh][(size_t)(-3 - f)];
+                const Parsed &q = P[(size_t)k];
+                StreamFam &F = s->fams[(size_t)f];
+                F.lo = std::min(F.lo, q.c);
+                F.hi = std::max(F.hi, q.e);
+                F.klo = std::min(F.klo, q.key);
+                F.khi = std::max(F.khi, q.key);
+                F.n++;
+            }
+        }
+        const size_t r0 = s->recs.size();
+        s->recs.resize(r0 + (size_t)nr);
+#pragma omp parallel for schedule(static)
+        for (int64_t k = 0; k < nr; k++) {
+            const int64_t len = (k + 1 < nr ? starts[(size_t)k + 1] : p) - starts[(size_t)k];
+            s->recs[r0 + (size_t)k] = StreamRec{base + starts[(size_t)k], len, famv[(size_t)k]};
+        }
+        s->cursor = std::max(s->cursor, P[(size_t)nr - 1].c);
+        s->tail += p;
+        return 0;
+    }
     for (int64_t k = 0; k < nr; k++) {
         const Parsed &q = P[(size_t)k];
         if (q.c < s->cursor)
@@ -885,8 +1014,12 @@ int32_t bsdc_bam_stream_next(bsdc_bam_stream *s, int64_t min_bytes, int64_t slac
                     s->fams[m].n = 0;
                     s->free_fams.push_back((int32_t)m);
                 }
-            for (auto it = s->fam_of.begin(); it != s->fam_of.end();)  // forget the emitted MI bases
-                it = s->fams[(size_t)it->second].n == 0 ? s->fam_of.erase(it) : std::next(it);
+#pragma omp parallel for schedule(dynamic, 1)
+            for (int sh = 0; sh < kFamShards; sh++) {  // forget the emitted MI bases
+                auto &fm = s->fam_of[(size_t)sh];
+                for (auto it = fm.begin(); it != fm.end();)
+                    it = s->fams[(size_t)it->second].n == 0 ? fm.erase(it) : std::next(it);
+            }
             for (auto it = s->fam_exact.begin(); it != s->fam_exact.end();)
                 it = s->fams[(size_t)it->second].n == 0 ? s->fam_exact.erase(it) : std::next(it);
             s->buf.swap(s->spare);  // (spare is now the chunk's old, empty vector: reserved on the next call)

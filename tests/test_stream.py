@@ -12,6 +12,14 @@ from bsseqconsensusreads_amd import bam, batch, synth
 from bsseqconsensusreads_amd import records as R
 
 
+@pytest.fixture(autouse=True, params=["serial", "parallel"])
+def family_assignment(request, monkeypatch):
+    """Every test runs with the stream's MI family assignment serial and in parallel (sharded by
+    hash; bsdc_io.cpp stream_split uses it from BSDC_STREAM_PAR_MIN records per split on)."""
+    monkeypatch.setenv("BSDC_STREAM_PAR_MIN", "1000000000" if request.param == "serial" else "0")
+    return request.param
+
+
 def _header(ref):
     text = "@HD\tVN:1.6\tSO:coordinate\n" + "".join("@SQ\tSN:%s\tLN:%d\n" % (n, l) for n, l in
                                                     zip(ref.names, ref.lengths)) + "@RG\tID:rg1\tSM:s1\tLB:libA\n"
