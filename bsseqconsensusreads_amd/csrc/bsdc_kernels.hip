@@ -1558,7 +1558,7 @@ struct RecMeta {  // 48 B, one per record of the family, in the arena
     int32_t pos;     // current leftmost position
     int32_t len;     // current length
     uint32_t slot;   // arena offset of the base slot (quals at slot + cap)
-    int32_t cap;     // slot capacity (input length + 2)
+    int32_t avail;   // converted: valid reference nibbles of its window (rec_win[1])
     int32_t start;   // index of the first base inside the slot
     uint32_t link;
     uint32_t gidx;   // global record index
@@ -1638,7 +1638,7 @@ __device__ void process_large(const KParams &P, uint8_t *A, uint8_t *s_tab, cons
     // and the record metadata.  The image and the metadata sit at offsets the list entry alone
     // gives (ArenaLayout), so nothing waits for the family's max length / cigar size ----
     // the family image as in HBM: bases (one byte each) at slots + slot, quals at slots + img + slot
-    // (RecMeta::cap = img, so `base + cap` addresses a base's qual)
+    // (a base at slots + x has its qual at slots + img + x)
     const ArenaLayout L0(n, 2 * (int64_t)img, 0, 0);  // meta / clist / slots only
     uint8_t *slots = A + L0.slots;
     uint8_t *qimg = slots + img;
@@ -1668,19 +1668,21 @@ __device__ void process_large(const KParams &P, uint8_t *A, uint8_t *s_tab, cons
     for (int r = tt; r < n; r += G) {
         const uint32_t gi = r0 + r;
         const uint4 rc = REC[gi];
-        const uint32_t ci = B.cig_info[gi], wn = B.rec_win[2 * (size_t)gi];
+        const uint32_t ci = B.cig_info[gi];
+        const uint2 wn = reinterpret_cast<const uint2 *>(B.rec_win)[gi];
         RecMeta m;
         m.in_len = (int32_t)(rc.z & 0xFFFF);
         m.flag = (uint16_t)(rc.z >> 16);
         m.pos = (int32_t)rc.y;
         m.len = m.in_len;
-        m.cap = (int32_t)img;
+
         m.slot = rc.x - off0;
         m.start = 1;
         m.link = rc.w;
         m.gidx = gi;
         const bool conv = do_convert && (m.link & BSDC_LINK_CONVERT);
-        m.win = conv ? wn : 0u;
+        m.win = conv ? wn.x : 0u;
+        m.avail = conv ? (int32_t)wn.y : 0;
         m.srclen = 0;
         const bool cx = m.link & BSDC_LINK_COMPLEX;
         m.reflen = cx ? (int32_t)(ci >> 16) : m.in_len;
@@ -1743,7 +1745,7 @@ __device__ void process_large(const KParams &P, uint8_t *A, uint8_t *s_tab, cons
                         const uint32_t *rw = reinterpret_cast<const uint32_t *>(P.ref + ((x0 >> 1) & ~3ull));
                         w0[u] = rw[0];
                         w1[u] = rw[1];
-                        av[u] = (int32_t)B.rec_win[2 * (size_t)M[r].gidx + 1];
+                        av[u] = M[r].avail;
                     }
                 }
             }
@@ -1821,7 +1823,7 @@ __device__ void process_large(const KParams &P, uint8_t *A, uint8_t *s_tab, cons
             const RecMeta pm = M[p];
             uint8_t *sb = slots + m.slot;
             sb[0] = slots[pm.slot + pm.start];
-            sb[m.cap] = slots[pm.slot + pm.cap + pm.start];
+            sb[img] = slots[pm.slot + img + pm.start];
             RecMeta &w = M[r];
             w.start = 0;
             w.len = m.len + 1;
@@ -1837,7 +1839,7 @@ __device__ void process_large(const KParams &P, uint8_t *A, uint8_t *s_tab, cons
             uint8_t *sb = slots + m.slot;
             const int li = pm.start + pm.len - 1;
             sb[m.start + m.len] = slots[pm.slot + li];
-            sb[m.cap + m.start + m.len] = slots[pm.slot + pm.cap + li];
+            sb[img + m.start + m.len] = slots[pm.slot + img + li];
             RecMeta &w = M[r];
             w.len = m.len + 1;
             w.reflen = m.reflen + 1;
@@ -1852,7 +1854,7 @@ __device__ void process_large(const KParams &P, uint8_t *A, uint8_t *s_tab, cons
             const uint8_t *sb = slots + m.slot + m.start;
             for (int j = tt; j < m.len; j += G) {
                 P.O.dump_seq[d + j] = sb[j];
-                P.O.dump_qual[d + j] = sb[m.cap + j];
+                P.O.dump_qual[d + j] = sb[img + j];
             }
             if (tt == 0) {
                 P.O.dump_pos[m.gidx] = m.pos;
