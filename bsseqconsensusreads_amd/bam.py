@@ -111,6 +111,8 @@ def _load():
     lib.bsdc_table_rank.restype = None
     lib.bsdc_table_take.argtypes = [C.c_int64, _P, _P, _P, _P, _P, C.c_int32]
     lib.bsdc_table_take.restype = C.c_int64
+    lib.bsdc_unpack_nibbles.argtypes = [C.c_int64, _P, _P, C.c_int32]
+    lib.bsdc_unpack_nibbles.restype = None
     lib.bsdc_rows_gather.argtypes = [C.c_int64, _P, _P, C.c_int64, _P, _P, _P, C.c_int32]
     lib.bsdc_rows_gather.restype = None
     if lib.bsdc_io_abi_version() != BSDC_IO_ABI_VERSION:
@@ -360,6 +362,16 @@ def table_ranks(t: StringTable) -> np.ndarray:
         buf = np.ascontiguousarray(t.buf, np.uint8) if t.buf.size else np.zeros(1, np.uint8)
         lib.bsdc_table_rank(n, _ptr(np.ascontiguousarray(t.off, np.int64)), _ptr(buf), _ptr(rank), 0)
     return rank[:n]
+
+
+def unpack_nibbles(packed: np.ndarray, threads: int = 0) -> np.ndarray:
+    """Packed nt16 bytes (high nibble first) -> one code per byte, same leading shape, last axis x2
+    (libbsdc_io, parallel)."""
+    a = np.ascontiguousarray(packed, np.uint8)
+    out = np.empty(a.shape[:-1] + (2 * a.shape[-1],), np.uint8)
+    if a.size:
+        _load().bsdc_unpack_nibbles(int(a.size), _ptr(a), _ptr(out), int(threads))
+    return out
 
 
 def _take_table(t: StringTable, idx: np.ndarray) -> StringTable:

@@ -1814,6 +1814,19 @@ extern "C" int64_t bsdc_table_take(int64_t n, const int64_t *idx, const int64_t 
     return out_off[n];
 }
 
+extern "C" void bsdc_unpack_nibbles(int64_t n_bytes, const uint8_t *in, uint8_t *out, int32_t n_threads) {
+    set_threads(n_threads);
+    const int64_t nb = (n_bytes + 4095) / 4096;
+#pragma omp parallel for schedule(static)
+    for (int64_t b = 0; b < nb; b++) {
+        const int64_t e = std::min(n_bytes, (b + 1) * 4096);
+        for (int64_t i = b * 4096; i < e; i++) {
+            out[2 * i] = in[i] >> 4;
+            out[2 * i + 1] = in[i] & 15;
+        }
+    }
+}
+
 extern "C" void bsdc_rows_gather(int64_t n, const int64_t *row, const int32_t *len, int64_t stride, const uint8_t *src,
                                  const int64_t *out_off, uint8_t *out, int32_t n_threads) {
     set_threads(n_threads);

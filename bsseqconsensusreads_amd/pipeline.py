@@ -220,10 +220,8 @@ def run_tool2(engine: Engine, raw: R.RawRecords) -> OutRecords:
 def consensus_from_output(fb: FamilyBatch, out: dict) -> Consensus:
     F = fb.n_fam
     stride = out["stride"]
-    packed = out["seq"].reshape(F, 2, stride // 2)
-    seq = np.empty((F, 2, stride), np.uint8)
-    seq[:, :, 0::2] = packed >> 4
-    seq[:, :, 1::2] = packed & 0xF
+    from .bam import unpack_nibbles
+    seq = unpack_nibbles(out["seq"].reshape(F, 2, stride // 2))
     ss = None
     if "ss_len" in out:
         ss = {"len": out["ss_len"], "base": out["ss_base"], "qual": out["ss_qual"], "depth": out["ss_depth"],

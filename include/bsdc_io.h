@@ -153,6 +153,9 @@ int64_t bsdc_table_take(int64_t n, const int64_t *idx, const int64_t *off, const
                         uint8_t *out_buf, int32_t n_threads);
 /* Fixed-stride rows -> a packed table: out[out_off[i], + len[i]) = src[row[i] * stride, + len[i])
  * (the consensus rows of the emitted families, in record order; len[i] <= stride). */
+/* Packed nt16 (two per byte, high nibble first) -> one code per byte: out[2i] = in[i] >> 4,
+ * out[2i + 1] = in[i] & 15 (the consensus rows the kernels write). */
+void bsdc_unpack_nibbles(int64_t n_bytes, const uint8_t *in, uint8_t *out, int32_t n_threads);
 void bsdc_rows_gather(int64_t n, const int64_t *row, const int32_t *len, int64_t stride, const uint8_t *src,
                       const int64_t *out_off, uint8_t *out, int32_t n_threads);
 

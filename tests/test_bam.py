@@ -495,3 +495,13 @@ def test_malformed_bam_fields_fail_loudly(tmp_path, what):
     _py_bgzf_write(str(q), bytes(data), block=5000)
     with pytest.raises(OSError):
         bam.read_bam(str(q))
+
+
+def test_unpack_nibbles_matches_numpy():
+    """The consensus rows' nibble unpack (libbsdc_io) = the numpy statement."""
+    a = np.random.default_rng(7).integers(0, 256, size=(1000, 2, 40), dtype=np.uint8)
+    want = np.empty((1000, 2, 80), np.uint8)
+    want[:, :, 0::2] = a >> 4
+    want[:, :, 1::2] = a & 0xF
+    assert np.array_equal(bam.unpack_nibbles(a, threads=3), want)
+    assert bam.unpack_nibbles(np.zeros((0, 2, 8), np.uint8)).shape == (0, 2, 16)
