@@ -2283,9 +2283,14 @@ __device__ void process_large(const KParams &P, uint8_t *A, uint8_t *s_tab, cons
         const int rb = split ? (wpart == 0 ? 0 : na / 2) : 0, re = split ? (wpart == 0 ? na / 2 : na) : na;
         const int kstart = split ? 0 : kWave * wpart, kstep = split ? kWave : kWave * PARTS;
         const int kend = split ? nmax : nm;
+        // One wave on a set with <= 32 marked columns: its two halves take the same columns and
+        // half the reads each (the lower half reads [0, h), the upper [h, na)), then add up.
+        const bool half = !split && nm <= 32 && na >= 16;
+        const int h = (na + 1) >> 1, hl = lane & 31;
         for (int k0 = kstart; k0 < kend; k0 += kstep) {
-            const bool act = k0 + lane < nm;
-            const int col = act ? mlist[s * ssw + k0 + lane] : 0;
+            const int cl = half ? hl : lane;
+            const bool act = k0 + cl < nm && (!half || lane < 32);
+            const int col = k0 + cl < nm ? mlist[s * ssw + k0 + cl] : 0;
             long long D0 = 0, D1 = 0, D2 = 0, D3 = 0;
             int32_t d0 = 0, d1 = 0, d2 = 0, d3 = 0;
             auto one = [&](uint32_t ex, uint32_t ey) {
@@ -2299,7 +2304,36 @@ __device__ void process_large(const KParams &P, uint8_t *A, uint8_t *s_tab, cons
                 d2 += bb == kG ? v : 0;
                 d3 += bb == kT ? v : 0;
             };
-            for (int r0 = rb; r0 < re && k0 < nm; r0 += kWave) {
+            if (half) {
+                for (int r0 = 0; r0 < h; r0 += 32) {
+                    // lane j < 32: read r0 + j; lane 32 + j: read h + r0 + j (0 descriptors add nothing)
+                    const int rj = (lane < 32 ? 0 : h) + r0 + hl;
+                    const bool okj = r0 + hl < h && rj < na;
+                    const uint2 dr = okj ? dl[rj] : make_uint2(0u, 0u);
+                    const int nr = ::min(32, h - r0);
+                    auto pick = [&](uint32_t v, int i) { return lane < 32 ? rlu(v, i) : rlu(v, 32 + i); };
+                    int i = 0;
+                    for (; i + 7 < nr; i += 8) {  // 8 reads' loads in flight
+#pragma unroll
+                        for (int u = 0; u < 8; u++) one(pick(dr.x, i + u), pick(dr.y, i + u));
+                    }
+                    for (; i < nr; i++) one(pick(dr.x, i), pick(dr.y, i));
+                    D0 += d0;  // int32 partials over <= 32 reads: exact
+                    D1 += d1;
+                    D2 += d2;
+                    D3 += d3;
+                    d0 = d1 = d2 = d3 = 0;
+                }
+                auto add_up = [&](long long &x) {  // + the upper half's partial (lane + 32)
+                    const int lo = __shfl_xor((int)(uint32_t)x, 32, kWave), hi = __shfl_xor((int)(x >> 32), 32, kWave);
+                    x += (long long)(((uint64_t)(uint32_t)hi << 32) | (uint32_t)lo);
+                };
+                add_up(D0);
+                add_up(D1);
+                add_up(D2);
+                add_up(D3);
+            }
+            for (int r0 = rb; r0 < re && k0 < nm && !half; r0 += kWave) {
                 const uint2 dr = r0 + lane < re ? dl[r0 + lane] : make_uint2(0u, 0u);
                 const int nr = ::min(kWave, re - r0);
                 int i = 0;
