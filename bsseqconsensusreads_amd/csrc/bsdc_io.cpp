@@ -520,6 +520,7 @@ constexpr int64_t kBigTid = 0x7FFFFFFF;
 constexpr int64_t kKeyDelta = 4;  // |key position before tools 1 + 2 - after| <= 2, twice
 constexpr int kFamShards = 64;
 inline int fam_shard(uint64_t h) { return (int)(h >> 58); }
+inline double now_s() { return omp_get_wtime(); }
 struct StreamFam {
     int64_t lo = INT64_MAX, hi = INT64_MIN;  // min own position, max own or mate position (coord)
     TcKey klo{INT64_MAX, INT64_MAX}, khi{INT64_MIN, INT64_MIN};  // bounds of its records' keys
@@ -550,6 +551,7 @@ struct bsdc_bam_stream {
     std::vector<int32_t> free_fams;
     int64_t cursor = INT64_MIN;  // the last record's position
     int64_t par_min = 1 << 14;   // records per split from which families are assigned in parallel
+    double prof[5] = {0, 0, 0, 0, 0};  // seconds: fill, split, select, emit, parse (BSDC_STREAM_PROF)
 };
 
 int32_t bsdc_bam_stream_open(const char *path, int32_t n_threads, int64_t read_size, bsdc_bam_stream **out) {
@@ -919,8 +921,11 @@ int32_t bsdc_bam_stream_next(bsdc_bam_stream *s, int64_t min_bytes, int64_t slac
     if (s->buf.capacity() < want) s->buf.reserve(want);
     if (s->spare.capacity() < want) s->spare.reserve(want);
     for (;;) {
+        double t0 = now_s();
         int32_t rc = stream_split(s);
         if (rc != 0) return rc;
+        s->prof[1] += now_s() - t0;
+        t0 = now_s();
         const bool end = s->eof && s->comp.empty();
         if (end && s->tail < (int64_t)s->buf.size()) return fail(BSDC_IO_EFORMAT, "truncated BAM record");
         take.assign(s->fams.size(), 0);
@@ -974,6 +979,8 @@ int32_t bsdc_bam_stream_next(bsdc_bam_stream *s, int64_t min_bytes, int64_t slac
             }
             for (; i < ord.size(); i++) take[(size_t)ord[i]] = 0;
         }
+        s->prof[2] += now_s() - t0;
+        t0 = now_s();
         if (end || (bytes > 0 && bytes >= min_bytes)) {
             if (bytes == 0) return 0;  // the end of the stream
             auto *b = new bsdc_bam();
@@ -1025,16 +1032,20 @@ int32_t bsdc_bam_stream_next(bsdc_bam_stream *s, int64_t min_bytes, int64_t slac
             s->buf.swap(s->spare);  // (spare is now the chunk's old, empty vector: reserved on the next call)
             s->tail = ok;
             s->recs.swap(krecs);
+            s->prof[3] += now_s() - t0;
+            t0 = now_s();
             rc = parse_records(b, 0, dn);
             if (rc != 0) {
                 delete b;
                 return rc;
             }
+            s->prof[4] += now_s() - t0;
             *out = b;
             return 0;
         }
         rc = bsdc_bam_stream_fill(s);
         if (rc != 0) return rc;
+        s->prof[0] += now_s() - t0;
     }
 }
 
@@ -1060,6 +1071,9 @@ int32_t bsdc_bam_stream_header(const bsdc_bam_stream *s, bsdc_bam **out) {
 void bsdc_bam_stream_close(bsdc_bam_stream *s) {
     if (!s) return;
     if (s->f) fclose(s->f);
+    if (getenv("BSDC_STREAM_PROF"))
+        fprintf(stderr, "bsdc stream s: fill %.3f split %.3f select %.3f emit %.3f parse %.3f\n", s->prof[0], s->prof[1],
+                s->prof[2], s->prof[3], s->prof[4]);
     delete s;
 }
 
