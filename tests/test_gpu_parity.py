@@ -52,22 +52,50 @@ def assert_ss_equal(cons, ref, what=""):
                         what, f, s, k, d[:8], g[d[:8]], r[d[:8]]))
 
 
-def test_tool1_fuzz_matches_reference(engine):
+def force_large(monkeypatch, where):
+    """Route every family of every batch through k_large: arena in LDS ("lds") or, with every
+    family in the last bucket, in HBM scratch ("global"); None leaves the planner's choice."""
+    if where is None:
+        return
+    real = batch.materialize
+
+    def forced(plan, f0, f1, small_cap=0):
+        fb = real(plan, f0, f1, small_cap=0)
+        if where == "global":
+            nb = len(fb.large_buckets)
+            fb.large_buckets = [np.zeros((0, 4), np.uint32)] * (nb - 1) + [fb.large_fams]
+            fb.large_arenas = [16] * (nb - 1) + [max(max(fb.large_arenas), batch.LARGE_LDS_MAX + 16)]
+        return fb
+
+    monkeypatch.setattr(batch, "materialize", forced)
+    monkeypatch.setattr(pipeline, "materialize", forced)
+
+
+KERNELS = pytest.mark.parametrize("where", [None, "lds", "global"], ids=["planner", "large-lds", "large-hbm"])
+
+
+@KERNELS
+def test_tool1_fuzz_matches_reference(engine, where, monkeypatch):
+    """tool 1 byte for byte against the reference tool's output, through k_small (the planner's
+    choice for one-record families) and through both k_large arenas (contig-end windows, RD)."""
+    force_large(monkeypatch, where)
     g = load_golden("tool1_fuzz.json.gz")
     raw, ref = golden_inputs(g)
     engine.load_reference(ref)
     out = pipeline.run_tool1(engine, raw)
-    compare_records(g["tool1"], out, raw, g["input"], "gpu tool1 fuzz")
+    compare_records(g["tool1"], out, raw, g["input"], "gpu tool1 fuzz %s" % where)
 
 
-def test_tools12_families_match_reference(engine):
+@KERNELS
+def test_tools12_families_match_reference(engine, where, monkeypatch):
+    force_large(monkeypatch, where)
     g = load_golden("tool12_families.json.gz")
     raw, ref = golden_inputs(g)
     engine.load_reference(ref)
-    compare_records(g["tool1"], pipeline.run_tool1(engine, raw), raw, g["input"], "gpu tool1 families")
+    compare_records(g["tool1"], pipeline.run_tool1(engine, raw), raw, g["input"], "gpu tool1 families %s" % where)
     cons, t2 = pipeline.run_step5(engine, raw, dump=True)
-    compare_records(g["tool2"], t2, raw, g["input"], "gpu fused tool2 dump")
-    assert_consensus_equal(cons, oracle.run(raw, ref), "golden families consensus")
+    compare_records(g["tool2"], t2, raw, g["input"], "gpu fused tool2 dump %s" % where)
+    assert_consensus_equal(cons, oracle.run(raw, ref), "golden families consensus %s" % where)
 
 
 def test_tool2_alone_on_reference_tool1_output(engine):
@@ -146,22 +174,14 @@ def test_large_family_kernel(engine, where, monkeypatch):
     """every family through the workgroup-per-family kernel (arena in LDS, or in HBM scratch)."""
     s = synth.generate("C2", 700, seed=12, device="cpu", genome_len=200_000)
     raw = synth.messify(s.raw, frac=0.1, seed=2)
-    real = batch.materialize
-
-    def forced(plan, f0, f1, small_cap=0):
-        fb = real(plan, f0, f1, small_cap=0)
-        if where == "global":  # every large family in the last (HBM scratch) bucket
-            nb = len(fb.large_buckets)
-            fb.large_buckets = [np.zeros((0, 4), np.uint32)] * (nb - 1) + [fb.large_fams]
-            fb.large_arenas = [16] * (nb - 1) + [max(max(fb.large_arenas), batch.LARGE_LDS_MAX + 16)]
-        return fb
-
-    monkeypatch.setattr(pipeline, "materialize", forced)
+    force_large(monkeypatch, where)
     engine.load_reference(s.ref)
-    cons, _ = pipeline.run_step5(engine, raw, tags=True)
+    cons, t2 = pipeline.run_step5(engine, raw, dump=True, tags=True)
     ref = oracle.run(raw, s.ref)
     assert_consensus_equal(cons, ref, "large-" + where)
     assert_ss_equal(cons, ref, "large-" + where)
+    for k in ("src", "pos", "seq", "qual", "cigar"):  # k_large's tool-2 state (extend + dump phases)
+        assert np.array_equal(getattr(t2, k), getattr(ref.tool2, k)), "large-%s tool-2 %s" % (where, k)
 
 
 def test_vote_only_on_tool2_output(engine):
