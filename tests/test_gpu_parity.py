@@ -54,9 +54,7 @@ def assert_ss_equal(cons, ref, what=""):
 
 def force_large(monkeypatch, where):
     """Route every family of every batch through k_large: arena in LDS ("lds") or, with every
-    family in the last bucket, in HBM scratch ("global"); None leaves the planner's choice."""
-    if where is None:
-        return
+    family in the last bucket, in HBM scratch ("global")."""
     real = batch.materialize
 
     def forced(plan, f0, f1, small_cap=0):
@@ -71,31 +69,23 @@ def force_large(monkeypatch, where):
     monkeypatch.setattr(pipeline, "materialize", forced)
 
 
-KERNELS = pytest.mark.parametrize("where", [None, "lds", "global"], ids=["planner", "large-lds", "large-hbm"])
-
-
-@KERNELS
-def test_tool1_fuzz_matches_reference(engine, where, monkeypatch):
-    """tool 1 byte for byte against the reference tool's output, through k_small (the planner's
-    choice for one-record families) and through both k_large arenas (contig-end windows, RD)."""
-    force_large(monkeypatch, where)
+# (the same golden vectors through k_large: tests/test_gpu_batches.py)
+def test_tool1_fuzz_matches_reference(engine):
     g = load_golden("tool1_fuzz.json.gz")
     raw, ref = golden_inputs(g)
     engine.load_reference(ref)
     out = pipeline.run_tool1(engine, raw)
-    compare_records(g["tool1"], out, raw, g["input"], "gpu tool1 fuzz %s" % where)
+    compare_records(g["tool1"], out, raw, g["input"], "gpu tool1 fuzz")
 
 
-@KERNELS
-def test_tools12_families_match_reference(engine, where, monkeypatch):
-    force_large(monkeypatch, where)
+def test_tools12_families_match_reference(engine):
     g = load_golden("tool12_families.json.gz")
     raw, ref = golden_inputs(g)
     engine.load_reference(ref)
-    compare_records(g["tool1"], pipeline.run_tool1(engine, raw), raw, g["input"], "gpu tool1 families %s" % where)
+    compare_records(g["tool1"], pipeline.run_tool1(engine, raw), raw, g["input"], "gpu tool1 families")
     cons, t2 = pipeline.run_step5(engine, raw, dump=True)
-    compare_records(g["tool2"], t2, raw, g["input"], "gpu fused tool2 dump %s" % where)
-    assert_consensus_equal(cons, oracle.run(raw, ref), "golden families consensus %s" % where)
+    compare_records(g["tool2"], t2, raw, g["input"], "gpu fused tool2 dump")
+    assert_consensus_equal(cons, oracle.run(raw, ref), "golden families consensus")
 
 
 def test_tool2_alone_on_reference_tool1_output(engine):
