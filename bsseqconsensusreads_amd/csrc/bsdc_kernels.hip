@@ -2473,6 +2473,11 @@ __global__ __launch_bounds__(G, G == 256 ? 5 : 2) void k_large(KParams P, const 
 // ------------------------------------------------------------------------------------------
 // C-ABI
 // ------------------------------------------------------------------------------------------
+#ifndef BSDC_FORK
+#define BSDC_FORK 1
+#endif
+constexpr int kForkStreams = 3;
+
 struct bsdc_ctx {
     int device;
     bsdc_params params;
@@ -2481,6 +2486,10 @@ struct bsdc_ctx {
     uint8_t *ref_seq = nullptr;
     int64_t ref_nibbles = 0;
     std::string err;
+    // (BSDC_FORK) side streams the bucket dispatches of one call fan out to, joined back to the
+    // caller's stream by events, so one dispatch's tail overlaps the next
+    hipStream_t side[kForkStreams] = {};
+    hipEvent_t ev_fork = nullptr, ev_join[kForkStreams] = {};
 };
 
 static float det_expf_host(float x) {
@@ -2657,6 +2666,11 @@ void bsdc_ctx_destroy(bsdc_ctx *c) {
     (void)hipSetDevice(c->device);
     (void)hipFree(c->dev_tab);
     (void)hipFree(c->ref_seq);
+    for (int i = 0; i < kForkStreams; i++) {
+        if (c->side[i]) (void)hipStreamDestroy(c->side[i]);
+        if (c->ev_join[i]) (void)hipEventDestroy(c->ev_join[i]);
+    }
+    if (c->ev_fork) (void)hipEventDestroy(c->ev_fork);
     delete c;
 }
 
@@ -2733,6 +2747,25 @@ int32_t bsdc_run(bsdc_ctx *c, const bsdc_family_batch *b, bsdc_consensus *o, int
     P.overlap = c->params.consensus_call_overlapping_bases;
     P.ref_chunks = ref_chunks(b->max_len);
     P.ref_chunks_inv = (uint32_t)((((uint64_t)1 << 32) + (uint64_t)P.ref_chunks - 1) / (uint64_t)P.ref_chunks);
+    // the dispatches: on `s`, or (BSDC_FORK) spread over the side streams after an event on `s`
+    int nd = 0, used = 0;
+    auto next_stream = [&]() -> hipStream_t {
+        if (!BSDC_FORK) return s;
+        if (!c->ev_fork) {
+            if (hipEventCreateWithFlags(&c->ev_fork, hipEventDisableTiming) != hipSuccess) return nullptr;
+            for (int i = 0; i < kForkStreams; i++)
+                if (hipStreamCreateWithFlags(&c->side[i], hipStreamNonBlocking) != hipSuccess ||
+                    hipEventCreateWithFlags(&c->ev_join[i], hipEventDisableTiming) != hipSuccess)
+                    return nullptr;
+        }
+        if (nd == 0 && hipEventRecord(c->ev_fork, s) != hipSuccess) return nullptr;
+        const int i = nd++ % kForkStreams;
+        if (!(used & (1 << i))) {
+            if (hipStreamWaitEvent(c->side[i], c->ev_fork, 0) != hipSuccess) return nullptr;
+            used |= 1 << i;
+        }
+        return c->side[i];
+    };
     if (!(mode & BSDC_MODE_SKIP_SMALL)) {
         const uint32_t *f = b->small_fams;
         for (int q = 0; q < BSDC_SMALL_BUCKETS; q++) {
@@ -2748,11 +2781,16 @@ int32_t bsdc_run(bsdc_ctx *c, const bsdc_family_batch *b, bsdc_consensus *o, int
                 const int nw = w8 > w4 ? 8 : 4;
                 const size_t lds = (size_t)nw * (size_t)b->small_arena[q] + (size_t)g2;  // + the static tables
                 const int64_t blocks = (nf + nw - 1) / nw;
+                const hipStream_t ls = next_stream();
+                if (!ls && BSDC_FORK) {
+                    c->err = "side stream setup failed";
+                    return BSDC_EDEVICE;
+                }
                 if (mode & BSDC_MODE_TAGS)
-                    hipLaunchKernelGGL(k_small<true>, dim3((unsigned)blocks), dim3(kWave * nw), lds, s, P, f, nf,
+                    hipLaunchKernelGGL(k_small<true>, dim3((unsigned)blocks), dim3(kWave * nw), lds, ls, P, f, nf,
                                        b->small_arena[q]);
                 else
-                    hipLaunchKernelGGL(k_small<false>, dim3((unsigned)blocks), dim3(kWave * nw), lds, s, P, f, nf,
+                    hipLaunchKernelGGL(k_small<false>, dim3((unsigned)blocks), dim3(kWave * nw), lds, ls, P, f, nf,
                                        b->small_arena[q]);
                 HIP_OK(c, hipGetLastError());
             }
@@ -2767,17 +2805,27 @@ int32_t bsdc_run(bsdc_ctx *c, const bsdc_family_batch *b, bsdc_consensus *o, int
             const int32_t a = b->large_arena[q];
             if (nf > 0) {
                 const bool big = q >= kLargeBigBucket;  // 2 or 1 workgroups per CU, or HBM scratch
+                const hipStream_t ls = next_stream();
+                if (!ls && BSDC_FORK) {
+                    c->err = "side stream setup failed";
+                    return BSDC_EDEVICE;
+                }
                 if (a <= BSDC_LARGE_LDS_MAX && !big)
-                    hipLaunchKernelGGL((k_large<true, kLargeThreads>), dim3((unsigned)nf), dim3(kLargeThreads), (size_t)a, s, P, f, nf, a);
+                    hipLaunchKernelGGL((k_large<true, kLargeThreads>), dim3((unsigned)nf), dim3(kLargeThreads), (size_t)a, ls, P, f, nf, a);
                 else if (a <= BSDC_LARGE_LDS_MAX)
-                    hipLaunchKernelGGL((k_large<true, kLargeThreadsBig>), dim3((unsigned)nf), dim3(kLargeThreadsBig), (size_t)a, s, P, f, nf, a);
+                    hipLaunchKernelGGL((k_large<true, kLargeThreadsBig>), dim3((unsigned)nf), dim3(kLargeThreadsBig), (size_t)a, ls, P, f, nf, a);
                 else
-                    hipLaunchKernelGGL((k_large<false, kLargeThreadsBig>), dim3((unsigned)nf), dim3(kLargeThreadsBig), 0, s, P, f, nf, a);
+                    hipLaunchKernelGGL((k_large<false, kLargeThreadsBig>), dim3((unsigned)nf), dim3(kLargeThreadsBig), 0, ls, P, f, nf, a);
                 HIP_OK(c, hipGetLastError());
             }
             f += nf;
         }
     }
+    for (int i = 0; i < kForkStreams; i++)  // join: `s` waits for every side stream used
+        if (used & (1 << i)) {
+            HIP_OK(c, hipEventRecord(c->ev_join[i], c->side[i]));
+            HIP_OK(c, hipStreamWaitEvent(s, c->ev_join[i], 0));
+        }
     return 0;
 }
 
