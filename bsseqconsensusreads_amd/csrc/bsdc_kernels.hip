@@ -2476,7 +2476,10 @@ __global__ __launch_bounds__(G, G == 256 ? 5 : 2) void k_large(KParams P, const 
 #ifndef BSDC_FORK
 #define BSDC_FORK 1
 #endif
-constexpr int kForkStreams = 3;
+#ifndef BSDC_FORK_STREAMS
+#define BSDC_FORK_STREAMS 4
+#endif
+constexpr int kForkStreams = BSDC_FORK_STREAMS;
 
 struct bsdc_ctx {
     int device;
