@@ -14,8 +14,10 @@
  * Conventions: every function returns 0 on success and a negative errno-style code on failure
  * (message via bsdc_last_error).  Batch and output pointers are DEVICE pointers owned by the
  * caller; work is enqueued on `stream` (a hipStream_t, NULL = the null stream) and is
- * asynchronous.  The reference genome is copied into library-owned device memory.  One context
- * per GPU per host thread; no global mutable state.  Output order == input family order.
+ * asynchronous: the bucket dispatches fan out over four context-owned side streams after an
+ * event on `stream`, and `stream` waits for all of them before any later work on it runs.  The
+ * reference genome is copied into library-owned device memory.  One context per GPU per host
+ * thread; no global mutable state.  Output order == input family order.
  */
 #ifndef BSDC_H
 #define BSDC_H
