@@ -15,6 +15,8 @@ for c in C2 C3; do
     || { echo "rocprof $c failed"; tail -20 "$OUT/prof_$c.log"; exit 1; }
   tail -1 "$OUT/prof_$c.log" | cut -c1-200
   find "$OUT/prof_$c" -name '*kernel_stats.csv' -exec cat {} \;
+  # launch-set spans (the side streams overlap a set's dispatches: DESIGN.md 5.4)
+  python profiles/trace_span.py "$(find "$OUT/prof_$c" -name '*kernel_trace.csv' | head -1)" "$OUT/prof_$c.log" "$OUT/span_$c.json" || exit 1
 done
 for c in C2 C3; do
   echo "[$(date +%T)] pmc $c"
