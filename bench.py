@@ -35,7 +35,7 @@ sys.path.insert(0, ROOT)
 from bsseqconsensusreads_amd import batch as B  # noqa: E402
 from bsseqconsensusreads_amd import shard, synth  # noqa: E402
 from bsseqconsensusreads_amd._lib import (MODE_CONVERT, MODE_EXTEND, MODE_SKIP_LARGE, MODE_SKIP_SMALL,  # noqa: E402
-                                          MODE_VOTE)
+                                          MODE_TAGS, MODE_VOTE)
 
 METRIC = "duplex families/sec (node) at 1/2/4/8 MI355X; % HBM roofline; speedup vs CPU"
 HBM_PEAK_GBS = 8000.0  # MI355X_MICROARCH.md: HBM3E 8.0 TB/s spec
@@ -50,6 +50,9 @@ WORKLOADS = {
 }
 DEFAULT_FAMILIES = {"C3": 200_000, "C5": 12_500_000}
 FULL_MODE = MODE_CONVERT | MODE_EXTEND | MODE_VOTE
+# the arithmetic the vote computes in (the data are u8 bases / quals)
+DTYPE = ("int64 fixed-point log-likelihood sums (2^-20 nats) + fp32 exp; fp64 read-order sums on near ties; "
+         "u8 nt16 bases / phred quals")
 
 
 def family_input_bytes(fb: B.FamilyBatch) -> np.ndarray:
@@ -79,8 +82,8 @@ def cpu_baseline(raw, ref, n_fam_sample: int, threads: int):
 class Resident:
     """One device batch kept in HBM for the timed steps, with its host-side accounting."""
 
-    def __init__(self, eng, fb: B.FamilyBatch):
-        self.db = eng.upload(fb)
+    def __init__(self, eng, fb: B.FamilyBatch, tags: bool = False):
+        self.db = eng.upload(fb, tags=tags)
         self.in_bytes = family_input_bytes(fb)
         self.small = fb.small_fams.astype(np.int64)
         self.n_large = int(fb.large_fams.shape[0])
@@ -96,7 +99,7 @@ def build(args, rank: int, dev, eng):
     if args.config != "C5":
         s = synth.generate(args.config, args.families, seed=args.seed + rank, device=dev)
         eng.load_reference(s.ref)
-        return [Resident(eng, B.build_family_batch(s.raw, "full", s.ref))], s
+        return [Resident(eng, B.build_family_batch(s.raw, "full", s.ref), tags=True)], s
     # C5: the rank's share as a stream of batches, each its own seeded chunk of families (the
     # chunk index is part of the seed) on the rank's one genome
     out, first = [], None
@@ -176,6 +179,16 @@ def run(args):
         e1.record(stream)
         torch.cuda.synchronize()
         t_large = e0.elapsed_time(e1) / 1e3 / ks
+    # the drop-in's default BAM output carries fgbio's per-base consensus tags (cli.py, main.snake.py:159):
+    # the same resident batches with BSDC_MODE_TAGS, timed after the headline (C5 keeps no tag buffers)
+    tags_ms = None
+    if all(r.db.tags for r in res):
+        e0.record(stream)
+        for _ in range(ks):
+            step(FULL_MODE | MODE_TAGS)
+        e1.record(stream)
+        torch.cuda.synchronize()
+        tags_ms = e0.elapsed_time(e1) / ks
     n_disp = sum(r.n_disp for r in res)
     bytes_small, bytes_all = 0, 0
     for r, (st, ln) in zip(res, outs):
@@ -241,7 +254,7 @@ def run(args):
             "higher_is_better": True,
             "scaling": "weak",
             "vs_baseline": None,
-            "dtype": "u8",
+            "dtype": DTYPE,
             "data": "synthetic (seeded EM-seq duplex model generated on the GPU, SURVEY.md 8d)",
             "config": {"workload": args.config + " -- " + WORKLOADS[args.config],
                        "families_per_gpu": molecules, "consensus_families_per_gpu": sum(r.n_fam for r in res),
@@ -263,6 +276,8 @@ def run(args):
                          "step_algorithmic_GBps": round(bytes_all / (elapsed / args.steps) / 1e9, 1),
                          "issue": issue},
             "cpu_baseline": cpu,
+            "tags_ms_per_step": round(tags_ms, 4) if tags_ms is not None else None,
+            "tags_families_per_s": round(molecules / (tags_ms / 1e3), 1) if tags_ms else None,
             "families_emitted": int(emitted_total),
             "setup_s": round(setup_s, 1),
         }

@@ -8,7 +8,7 @@ HERE = os.path.dirname(os.path.abspath(__file__))
 # BSDC_LIB_PATH: an alternative build of the same library (profiling A/B runs only)
 LIB_PATH = os.environ.get("BSDC_LIB_PATH") or os.path.join(HERE, "libbsdc.so")
 
-BSDC_ABI_VERSION = 7
+BSDC_ABI_VERSION = 8
 SMALL_BUCKETS = 8  # BSDC_SMALL_BUCKETS
 LARGE_BUCKETS = 6  # BSDC_LARGE_BUCKETS
 MODE_CONVERT, MODE_EXTEND, MODE_VOTE, MODE_DUMP = 1, 2, 4, 8
@@ -44,7 +44,7 @@ class ConsensusC(C.Structure):
 EXPORTS = ("bsdc_abi_version", "bsdc_ctx_create", "bsdc_ctx_destroy", "bsdc_last_error",
            "bsdc_load_reference", "bsdc_run", "bsdc_convert", "bsdc_extend", "bsdc_duplex_call",
            "bsdc_family_arena_bytes", "bsdc_small_arena_bytes", "bsdc_get_tables", "bsdc_model_tables",
-           "bsdc_model_tables40", "bsdc_agree_tables", "bsdc_phred_buckets")
+           "bsdc_model_tables_fp64", "bsdc_agree_tables", "bsdc_phred_buckets")
 
 _lib = None
 
@@ -81,8 +81,8 @@ def load(path: str = LIB_PATH):
     lib.bsdc_get_tables.restype = C.c_int32
     lib.bsdc_model_tables.argtypes = [C.c_double, C.c_double, C.c_void_p, C.c_void_p]
     lib.bsdc_model_tables.restype = None
-    lib.bsdc_model_tables40.argtypes = [C.c_double, C.c_double, C.c_void_p]
-    lib.bsdc_model_tables40.restype = None
+    lib.bsdc_model_tables_fp64.argtypes = [C.c_double, C.c_double, C.c_void_p, C.c_void_p]
+    lib.bsdc_model_tables_fp64.restype = None
     lib.bsdc_agree_tables.argtypes = [C.c_double, C.c_double, C.c_void_p, C.c_void_p]
     lib.bsdc_agree_tables.restype = None
     lib.bsdc_phred_buckets.argtypes = [C.c_double, C.c_double, C.c_void_p]

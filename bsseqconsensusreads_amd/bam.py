@@ -809,13 +809,14 @@ def step5_stream(in_bam: str, fasta: str, out_bam: Optional[str], engine=None, p
     info = {"records_in": 0, "families": 0, "families_emitted": 0, "records_out": 0, "chunks": 0}
     T = {"decode": 0.0, "plan": 0.0, "gpu": 0.0, "records": 0.0, "encode": 0.0, "gpu_wait": 0.0, "writer_wait": 0.0}
     first = {}
+    stop = threading.Event()  # set on any failure: the decoder and planner stop at their next chunk
 
     raws: "queue.Queue" = queue.Queue(maxsize=1)
 
     def decoder():  # the next chunk decodes while the previous one's families form
         try:
             it = stream_bam(in_bam, threads, chunk_bytes, slack)
-            while True:
+            while not stop.is_set():
                 t0 = time.perf_counter()
                 nxt = next(it, None)
                 T["decode"] += time.perf_counter() - t0
@@ -824,6 +825,7 @@ def step5_stream(in_bam: str, fasta: str, out_bam: Optional[str], engine=None, p
                 raws.put(nxt[1])
         except BaseException as e:  # noqa: BLE001 -- handed to the main thread
             err.append(e)
+            stop.set()
         finally:
             raws.put(None)
 
@@ -833,12 +835,15 @@ def step5_stream(in_bam: str, fasta: str, out_bam: Optional[str], engine=None, p
                 raw = raws.get()
                 if raw is None:
                     break
+                if stop.is_set():
+                    continue  # drain to the decoder's None without planning
                 t0 = time.perf_counter()
                 plan = pipeline.plan_families(raw, "full", first["ref"])
                 T["plan"] += time.perf_counter() - t0
                 chunks.put((raw, plan))
         except BaseException as e:  # noqa: BLE001 -- handed to the main thread
             err.append(e)
+            stop.set()
             while raws.get() is not None:  # let the decoder finish
                 pass
         finally:
@@ -871,6 +876,7 @@ def step5_stream(in_bam: str, fasta: str, out_bam: Optional[str], engine=None, p
                 fq.close(threads)
         except BaseException as e:  # noqa: BLE001
             err.append(e)
+            stop.set()
             while outs.get() is not None:  # drain so the main thread never blocks
                 pass
 
@@ -889,12 +895,16 @@ def step5_stream(in_bam: str, fasta: str, out_bam: Optional[str], engine=None, p
         tr.start()
         tw.start()
         mode = pipeline.MODE_CONVERT | pipeline.MODE_EXTEND | pipeline.MODE_VOTE
+        drained = False
         try:
             while True:
                 t0 = time.perf_counter()
                 item = chunks.get()
                 T["gpu_wait"] += time.perf_counter() - t0
                 if item is None:
+                    drained = True
+                    break
+                if stop.is_set():  # another stage failed: stop working, drain below
                     break
                 raw, plan = item
                 t0 = time.perf_counter()
@@ -911,10 +921,13 @@ def step5_stream(in_bam: str, fasta: str, out_bam: Optional[str], engine=None, p
                 info["chunks"] += 1
                 outs.put((cons, raw))
         except BaseException:
-            while chunks.get() is not None:  # let the reader finish
-                pass
+            stop.set()
             raise
         finally:
+            if not drained:  # let the reader finish (it stops planning once `stop` is set)
+                stop.set()
+                while chunks.get() is not None:
+                    pass
             outs.put(None)
             tw.join()
             tr.join()

@@ -20,7 +20,9 @@
 //    record's lane; loops over records are wave-uniform and read it with readlane.
 //  * k_large -- one 256-thread workgroup per family, generic (arena in LDS or HBM scratch).
 // All integer / byte work; the vote's likelihood sums are exact fixed-point integers (2^-20 nats),
-// so any summation order is bit-identical to the CPU restatement (oracle/).
+// so any summation order is bit-identical to the CPU restatement (oracle/).  The one exception is
+// the rare near-tie column, which takes fgbio's own pick: its double-precision sums, added in
+// fgbio's read order (fp64_pick).
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
@@ -110,12 +112,13 @@ struct Tables {
     uint8_t qlo[2048];  // agreement case (S = 3 e^-D): Q at D = 2^16 k
     int32_t dthr[48];   // agreement case: smallest D with Q >= q (INT32_MAX: never)
 };
-// The device copy: the LDS image above plus the near-tie residuals, read from HBM on the rare
-// near-tie path only.  r40[q] = round(x 2^40) - lr[q] 2^20 (|r40| <= 2^19 + 1), x the same
-// log-likelihood ratio: a 2^-40 sum is D 2^20 + sum r40.
+// The device copy: the LDS image above plus fgbio's per-read terms in double precision, read from
+// HBM on the rare near-tie path only: lnc[q] = ln P(correct), lne3[q] = ln P(error) / 3 of a Q base
+// after the post-UMI step, computed the way fgbio's LogProbability computes them (make_fp64).
 struct DevTables {
     Tables t;
-    int32_t r40[256];
+    double lnc[256];
+    double lne3[256];
 };
 
 using bsdc_layout::ArenaLayout;
@@ -182,30 +185,24 @@ __device__ __forceinline__ int phred_of(float S, const float *thr) {
 // 32767 (fgbio stores Shorts).  D: likelihood sums (2^-20 nats), n: reads per base.
 struct SsAcc {
     long long D[4];
-    long long R[4];  // sums of DevTables::r40 (the near-tie refinement)
     uint32_t n[4];
     __device__ __forceinline__ void clear() {
 #pragma unroll
         for (int x = 0; x < 4; x++) {
             D[x] = 0;
-            R[x] = 0;
             n[x] = 0;
         }
     }
-    // one read's base (plain nt16 code, sequencing orientation), its lr and r40 values
-    __device__ __forceinline__ void add(uint32_t code, int32_t v, int32_t r) {
+    // one read's base (plain nt16 code, sequencing orientation) and its lr value
+    __device__ __forceinline__ void add(uint32_t code, int32_t v) {
 #pragma unroll
         for (int x = 0; x < 4; x++) {
             const bool hit = code == (1u << x);
             D[x] += hit ? v : 0;
-            R[x] += hit ? r : 0;
             n[x] += hit ? 1u : 0u;
         }
     }
 };
-// Near tie (DESIGN.md section 3.5): each read's 2^-20 term is rounded by up to half a unit, so a
-// gap between the best and the second sum of at most one unit per read of the set (nset) can hide
-// the true order.  Then the 2^-40 sums D 2^20 + R decide (first maximum).  Returns the best base.
 template <typename T>
 __device__ __forceinline__ int first_max4(T d0, T d1, T d2, T d3) {
     int best = 0;
@@ -215,6 +212,9 @@ __device__ __forceinline__ int first_max4(T d0, T d1, T d2, T d3) {
     if (d3 > m) { best = 3; }
     return best;
 }
+// Near tie (DESIGN.md section 3.5): each read's 2^-20 term is rounded by up to half a unit, so a
+// gap between the best and the second sum of at most one unit per read of the set (nset) can hide
+// fgbio's order.  Those columns take fgbio's own pick (fp64_pick).
 template <typename T>
 __device__ __forceinline__ bool near_tie(T d0, T d1, T d2, T d3, int best, int nset) {
     const T m = best == 0 ? d0 : best == 1 ? d1 : best == 2 ? d2 : d3;
@@ -222,14 +222,77 @@ __device__ __forceinline__ bool near_tie(T d0, T d1, T d2, T d3, int best, int n
     if (best != 1 && d1 > sec) sec = d1;
     if (best != 2 && d2 > sec) sec = d2;
     if (best != 3 && d3 > sec) sec = d3;
-    return nset > 1 && (long long)m - (long long)sec <= (long long)nset;
+    return (long long)m - (long long)sec <= (long long)nset;
 }
-__device__ __forceinline__ void ss_store(const SsAcc &a, const float *thr, int nset, uint8_t *b, uint8_t *q,
+// fgbio's pick on a near tie: ConsensusBaseBuilder.add's four double-precision log-likelihood sums
+// (lnc for the read's base, lne3 for each other base), accumulated read by read in fgbio's read
+// order, then the first maximum by strict >.  That order is filterToMostCommonAlignment's output:
+// source length descending, ties in family record order, which is ascending image address here
+// (a family's slots are laid out in record order).  It reproduces fgbio's rounding too, so an exact
+// tie of quality multisets resolves as fgbio's summation order resolves it.  Rare, so the order
+// is found by selection: each step takes the smallest (length desc, address) key above the last.
+// Desc::get(i, addr, len, rev): the set's i-th read; its column col is image byte addr + col
+// (forward) or addr - col (reverse); bases at bimg, quals at qimg, same offsets.
+template <class Desc>
+__device__ int fp64_pick(const Desc &ds, int n, int col, const uint8_t *bimg, const uint8_t *qimg, const double *lnc,
+                         const double *lne3) {
+    double L0 = 0.0, L1 = 0.0, L2 = 0.0, L3 = 0.0;
+    uint64_t lo = 0;
+    for (;;) {
+        uint64_t kb = ~0ull;
+        uint32_t ab = 0;
+        bool rb = false;
+        for (int i = 0; i < n; i++) {
+            uint32_t a;
+            int len;
+            bool rv;
+            ds.get(i, a, len, rv);
+            if (len <= col) continue;
+            const uint64_t key = ((uint64_t)(0xFFFFu - (uint32_t)len) << 32) | a;
+            if (key >= lo && key < kb) {
+                kb = key;
+                ab = a;
+                rb = rv;
+            }
+        }
+        if (kb == ~0ull) break;
+        lo = kb + 1;
+        const uint32_t x = rb ? ab - (uint32_t)col : ab + (uint32_t)col;
+        const uint32_t code = rb ? comp_nt16(bimg[x]) : (bimg[x] & 0x0Fu);
+        if (!is_acgt(code)) continue;  // fgbio adds no N
+        const int q = qimg[x];
+        const double c = lnc[q], e = lne3[q];
+        L0 += code == kA ? c : e;
+        L1 += code == kC ? c : e;
+        L2 += code == kG ? c : e;
+        L3 += code == kT ? c : e;
+    }
+    return first_max4(L0, L1, L2, L3);
+}
+struct SmallDesc {  // k_small: u32 {address, length << 16 (15 bits), reverse << 31}
+    const uint32_t *d;
+    __device__ __forceinline__ void get(int i, uint32_t &a, int &len, bool &rv) const {
+        const uint32_t x = d[i];
+        a = x & 0xFFFFu;
+        len = (int)((x >> 16) & 0x7FFFu);
+        rv = (x >> 31) != 0;
+    }
+};
+struct LargeDesc {  // k_large: uint2 {address, length | reverse << 31}
+    const uint2 *d;
+    __device__ __forceinline__ void get(int i, uint32_t &a, int &len, bool &rv) const {
+        const uint2 x = d[i];
+        a = x.x;
+        len = (int)(x.y & 0x7FFFFFFFu);
+        rv = (x.y >> 31) != 0;
+    }
+};
+// the call of one single-strand column with its statistics; pick() gives fgbio's base on a near tie
+template <class Pick>
+__device__ __forceinline__ void ss_store(const SsAcc &a, const float *thr, int nset, Pick pick, uint8_t *b, uint8_t *q,
                                          uint16_t *dp, uint16_t *er) {
     int best = first_max4(a.D[0], a.D[1], a.D[2], a.D[3]);
-    if (near_tie(a.D[0], a.D[1], a.D[2], a.D[3], best, nset))
-        best = first_max4((a.D[0] << 20) + a.R[0], (a.D[1] << 20) + a.R[1], (a.D[2] << 20) + a.R[2],
-                          (a.D[3] << 20) + a.R[3]);
+    if (near_tie(a.D[0], a.D[1], a.D[2], a.D[3], best, nset)) best = pick();
     const long long Db = a.D[best];
     float S = 0.0f;
 #pragma unroll
@@ -851,7 +914,6 @@ __global__ __launch_bounds__(kWave *kSmallMaxWaves, kSmallMinWaves) __attribute_
     const float *thr = T->thr;
     const uint8_t *qlo = T->qlo;
     const int32_t *dthr = T->dthr;
-    const int32_t *r40g = P.tab->r40;  // HBM: the near-tie path only
     if (((P.mode >> BSDC_MODE_STOP_SHIFT) & 15) == 15) return;  // profiling: launch cost alone
     load_tables<kTabBytes>(&P.tab->t, reinterpret_cast<uint8_t *>(&s_tab));
     if (((P.mode >> BSDC_MODE_STOP_SHIFT) & 15) == 14) return;  // profiling: + the table copy
@@ -1454,23 +1516,8 @@ __global__ __launch_bounds__(kWave *kSmallMaxWaves, kSmallMinWaves) __attribute_
                     D3 += bb == kT ? v : 0;
                 }
                 int best = first_max4(D0, D1, D2, D3);
-                if (near_tie(D0, D1, D2, D3, best, ns)) {  // rare: the 2^-40 sums decide
-                    int32_t E0 = 0, E1 = 0, E2 = 0, E3 = 0;
-                    for (int i = 0; i < ns; i++) {
-                        const uint32_t d = dlist[os + i];
-                        if (c >= (int)((d >> 16) & 0x7FFF)) continue;
-                        const uint32_t idx = (d & 0x80000000u) ? (d & 0xFFFF) - c : (d & 0xFFFF) + c;
-                        const uint32_t braw = bimg[idx];
-                        const int32_t v = ((braw >> 4) & 1u) ? r40g[qimg[idx]] : 0;
-                        const uint32_t bb = (d & 0x80000000u) ? comp_nt16(braw) : (braw & 0x0F);
-                        E0 += bb == kA ? v : 0;
-                        E1 += bb == kC ? v : 0;
-                        E2 += bb == kG ? v : 0;
-                        E3 += bb == kT ? v : 0;
-                    }
-                    best = first_max4(((long long)D0 << 20) + E0, ((long long)D1 << 20) + E1,
-                                      ((long long)D2 << 20) + E2, ((long long)D3 << 20) + E3);
-                }
+                if (near_tie(D0, D1, D2, D3, best, ns))  // rare: fgbio's fp64 read-order pick
+                    best = fp64_pick(SmallDesc{dlist + os}, ns, c, bimg, qimg, P.tab->lnc, P.tab->lne3);
                 const int32_t Db = best == 0 ? D0 : best == 1 ? D1 : best == 2 ? D2 : D3;
                 float S = 0.0f;  // |D| < 2^30 here (<= 64 reads)
                 if (best != 0) S += term32(D0 - Db);
@@ -1533,9 +1580,10 @@ __global__ __launch_bounds__(kWave *kSmallMaxWaves, kSmallMinWaves) __attribute_
                     const uint32_t idx = (d & 0x80000000u) ? (d & 0xFFFF) - c : (d & 0xFFFF) + c;
                     const uint32_t braw = bimg[idx];
                     const uint32_t bb = (d & 0x80000000u) ? comp_nt16(braw) : (braw & 0x0F);
-                    acc.add(bb, lr2[256 + qimg[idx]], r40g[qimg[idx]]);  // only one-hot codes count
+                    acc.add(bb, lr2[256 + qimg[idx]]);  // only one-hot codes count
                 }
-                ss_store(acc, thr, cnt[s], P.O.ss_base + row + c, P.O.ss_qual + row + c, P.O.ss_depth + row + c,
+                auto pick = [&]() { return fp64_pick(SmallDesc{dlist + off[s]}, cnt[s], c, bimg, qimg, P.tab->lnc, P.tab->lne3); };
+                ss_store(acc, thr, cnt[s], pick, P.O.ss_base + row + c, P.O.ss_qual + row + c, P.O.ss_depth + row + c,
                          P.O.ss_err + row + c);
             }
             if (t == 0) P.O.ss_len[4 * fam + s] = (uint16_t)ls;
@@ -2105,22 +2153,10 @@ __device__ void process_large(const KParams &P, uint8_t *A, uint8_t *s_tab, cons
     // the read's end cleared, lr[q] added to the base's sum.  Sets of <= 128 reads: 4 columns per
     // thread, int32 sums (exact: |lr| < 2^24).  Deeper sets: 2 columns per thread, int32 sums
     // flushed to int64 every 128 reads.
-    const int32_t *r40g = P.tab->r40;  // HBM: the near-tie path only
     auto resolve = [&](int s, int col, long long D0, long long D1, long long D2, long long D3) {
         int best = first_max4(D0, D1, D2, D3);
-        if (near_tie(D0, D1, D2, D3, best, cnt[s])) {  // rare: the 2^-40 sums decide
-            long long E[4] = {0, 0, 0, 0};
-            const uint2 *dl = desc + soff[s];
-            for (int i = 0; i < cnt[s]; i++) {
-                const uint2 e = dl[i];
-                if (col >= (int)(e.y & 0x7FFFFFFFu)) continue;
-                const bool rv = e.y >> 31;
-                const int32_t a = rv ? (int32_t)e.x - col : (int32_t)e.x + col;
-                const uint32_t braw = slots[a] & 0x0Fu, bb = rv ? comp_nt16(braw) : braw;
-                if (is_acgt(bb)) E[acgt_idx(bb)] += r40g[qimg[a]];
-            }
-            best = first_max4((D0 << 20) + E[0], (D1 << 20) + E[1], (D2 << 20) + E[2], (D3 << 20) + E[3]);
-        }
+        if (near_tie(D0, D1, D2, D3, best, cnt[s]))  // rare: fgbio's fp64 read-order pick
+            best = fp64_pick(LargeDesc{desc + soff[s]}, cnt[s], col, slots, qimg, P.tab->lnc, P.tab->lne3);
         const long long Db = best == 0 ? D0 : best == 1 ? D1 : best == 2 ? D2 : D3;
         float S = 0.0f;
         if (best != 0) S += term(D0 - Db);
@@ -2419,10 +2455,11 @@ __device__ void process_large(const KParams &P, uint8_t *A, uint8_t *s_tab, cons
                 const bool rv = e.y >> 31;
                 const int32_t a = rv ? (int32_t)e.x - c : (int32_t)e.x + c;
                 const uint32_t braw = slots[a] & 0x0Fu;
-                acc.add(rv ? comp_nt16(braw) : braw, lr[qimg[a]], r40g[qimg[a]]);
+                acc.add(rv ? comp_nt16(braw) : braw, lr[qimg[a]]);
             }
             const int64_t at = (4 * (int64_t)fam + s) * stride + c;
-            ss_store(acc, thr, cnt[s], P.O.ss_base + at, P.O.ss_qual + at, P.O.ss_depth + at, P.O.ss_err + at);
+            auto pick = [&]() { return fp64_pick(LargeDesc{dl}, cnt[s], c, slots, qimg, P.tab->lnc, P.tab->lne3); };
+            ss_store(acc, thr, cnt[s], pick, P.O.ss_base + at, P.O.ss_qual + at, P.O.ss_depth + at, P.O.ss_err + at);
         }
         if (tt < 4) P.O.ss_len[4 * fam + tt] = (uint16_t)(hs[tt] ? lcv[tt] : 0);
     }
@@ -2447,7 +2484,8 @@ static_assert(sizeof(TablesL) == kTabBytesL, "TablesL image");
 // G = 256 threads for the buckets that fit 3 or more workgroups per CU, 512 for the LDS-heavy ones
 // (2 or 1 per CU, HBM scratch): twice the wavefronts in flight for the same LDS.
 template <bool IN_LDS, int G>
-__global__ __launch_bounds__(G, G == 256 ? 5 : 2) void k_large(KParams P, const uint4 *fams, int64_t nfams, int32_t arena) {
+__global__ __launch_bounds__(G, G == 256 ? 5 : 2) void k_large(KParams P, const uint4 *fams, int64_t nfams, int32_t arena,
+                                                                int64_t scratch_off) {
     extern __shared__ __attribute__((aligned(16))) uint8_t smem[];  // the family's arena (IN_LDS)
     __shared__ __attribute__((aligned(16))) TablesL s_tab;  // loaded by process_large with the image
     __shared__ int red[2 * G / kWave];
@@ -2464,7 +2502,7 @@ __global__ __launch_bounds__(G, G == 256 ? 5 : 2) void k_large(KParams P, const 
     if (i >= nfams) return;
     if (threadIdx.x == 0) s_cnt[0] = 0;  // the converted-record count (process_large's first phase)
     __syncthreads();
-    uint8_t *A = IN_LDS ? smem : P.O.scratch + (size_t)i * (size_t)arena;
+    uint8_t *A = IN_LDS ? smem : P.O.scratch + scratch_off + (size_t)i * (size_t)arena;
     process_large<G>(P, A, reinterpret_cast<uint8_t *>(&s_tab), lr, thr, fams[i], red, s_cnt, s_lc, s_cur);
 }
 
@@ -2581,15 +2619,25 @@ static void make_tables(double pre, double post, Tables &t) {
     }
 }
 
-// near-tie residuals: r40[q] = round(x 2^40) - lr[q] 2^20, x = ln(1 - a) - ln(a / 3) as in
-// make_tables (keep in step with oracle/bsdc_oracle.c orc_tables40)
-static void make_r40(double post, const Tables &t, int32_t *r40) {
-    const double e_post = pow(10.0, -post / 10.0);
+// fgbio's per-read terms in double precision, its LogProbability arithmetic restated (PARITY
+// UNPINNED): pErr = probabilityOfErrorTwoTrials(ln e_post, ln e(q)); lnc = not(pErr), lne3 = pErr -
+// ln 3.  The near-tie pick adds these, so the operation order is kept in step with oracle/
+// bsdc_oracle.c orc_tables_fp64 and tests/fgbio_vote.py qual_tables (tests/test_fgbio_vote.py
+// compares the three bit for bit).
+static double lp_or(double a, double b) {
+    const double m = a > b ? a : b, n = a > b ? b : a;
+    return m == -INFINITY ? m : m + log1p(exp(n - m));
+}
+static double lp_not(double x) { return x > -log(2.0) ? log(-expm1(x)) : log1p(-exp(x)); }
+static double lp_a_or_not_b(double a, double b) { return b == -INFINITY ? a : a + log1p(-exp(b - a)); }
+static void make_fp64(double post, double *lnc, double *lne3) {
+    const double ln10 = log(10.0), ln3 = log(3.0), ln43 = log(4.0 / 3.0);
+    const double x = -post * ln10 / 10.0;
     for (int q = 0; q < 256; q++) {
-        const double e = pow(10.0, -(double)q / 10.0);
-        const double a = e_post + e - (4.0 / 3.0) * e_post * e;
-        const long long x40 = llround((log1p(-a) - log(a / 3.0)) * 1099511627776.0);
-        r40[q] = (int32_t)(x40 - ((long long)t.lr[q] << 20));
+        const double y = -(double)q * ln10 / 10.0;
+        const double pe = lp_a_or_not_b(lp_or(x, y), ln43 + x + y);
+        lnc[q] = lp_not(pe);
+        lne3[q] = pe - ln3;
     }
 }
 
@@ -2605,6 +2653,7 @@ static void make_r40(double post, const Tables &t, int32_t *r40) {
 extern "C" {
 
 int32_t bsdc_abi_version(void) { return BSDC_ABI_VERSION; }
+void bsdc_ctx_destroy(bsdc_ctx *c);
 
 int64_t bsdc_family_arena_bytes(int32_t n_rec, int64_t slot_bytes, int32_t max_len, int64_t complex_ops) {
     ArenaLayout L(n_rec, slot_bytes, max_len, complex_ops);
@@ -2630,12 +2679,9 @@ void bsdc_agree_tables(double pre, double post, uint8_t *qlo2048, int32_t *dthr4
     memcpy(dthr48, t.dthr, sizeof t.dthr);
 }
 
-void bsdc_model_tables40(double pre, double post, int64_t *lr40_256) {
-    Tables t;
-    make_tables(pre, post, t);
-    int32_t r40[256];
-    make_r40(post, t, r40);
-    for (int i = 0; i < 256; i++) lr40_256[i] = ((int64_t)t.lr[i] << 20) + r40[i];
+void bsdc_model_tables_fp64(double pre, double post, double *lnc256, double *lne3_256) {
+    (void)pre;
+    make_fp64(post, lnc256, lne3_256);
 }
 
 void bsdc_phred_buckets(double pre, double post, uint8_t *sq144) {
@@ -2654,11 +2700,21 @@ int32_t bsdc_ctx_create(int32_t device, const bsdc_params *params, bsdc_ctx **ou
     c->device = device;
     c->params = *params;
     make_tables(params->error_rate_pre_umi, params->error_rate_post_umi, c->host_tab.t);
-    make_r40(params->error_rate_post_umi, c->host_tab.t, c->host_tab.r40);
+    make_fp64(params->error_rate_post_umi, c->host_tab.lnc, c->host_tab.lne3);
     if (hipSetDevice(device) != hipSuccess || hipMalloc(&c->dev_tab, sizeof(DevTables)) != hipSuccess ||
         hipMemcpy(c->dev_tab, &c->host_tab, sizeof(DevTables), hipMemcpyHostToDevice) != hipSuccess) {
-        delete c;
+        bsdc_ctx_destroy(c);
         return BSDC_EDEVICE;
+    }
+    if (BSDC_FORK) {  // the side streams and their events: all of them, or the context fails
+        bool ok = hipEventCreateWithFlags(&c->ev_fork, hipEventDisableTiming) == hipSuccess;
+        for (int i = 0; ok && i < kForkStreams; i++)
+            ok = hipStreamCreateWithFlags(&c->side[i], hipStreamNonBlocking) == hipSuccess &&
+                 hipEventCreateWithFlags(&c->ev_join[i], hipEventDisableTiming) == hipSuccess;
+        if (!ok) {
+            bsdc_ctx_destroy(c);
+            return BSDC_EDEVICE;
+        }
     }
     *out = c;
     return 0;
@@ -2750,28 +2806,34 @@ int32_t bsdc_run(bsdc_ctx *c, const bsdc_family_batch *b, bsdc_consensus *o, int
     P.overlap = c->params.consensus_call_overlapping_bases;
     P.ref_chunks = ref_chunks(b->max_len);
     P.ref_chunks_inv = (uint32_t)((((uint64_t)1 << 32) + (uint64_t)P.ref_chunks - 1) / (uint64_t)P.ref_chunks);
-    // the dispatches: on `s`, or (BSDC_FORK) spread over the side streams after an event on `s`
+    // the dispatches: on `s`, or (BSDC_FORK) spread over the side streams (created with the
+    // context) after an event on `s`
     int nd = 0, used = 0;
+    int32_t rc = 0;
+    auto fail = [&](hipError_t e, const char *what) {
+        c->err = std::string(what) + ": " + hipGetErrorString(e);
+        rc = BSDC_EDEVICE;
+    };
     auto next_stream = [&]() -> hipStream_t {
         if (!BSDC_FORK) return s;
-        if (!c->ev_fork) {
-            if (hipEventCreateWithFlags(&c->ev_fork, hipEventDisableTiming) != hipSuccess) return nullptr;
-            for (int i = 0; i < kForkStreams; i++)
-                if (hipStreamCreateWithFlags(&c->side[i], hipStreamNonBlocking) != hipSuccess ||
-                    hipEventCreateWithFlags(&c->ev_join[i], hipEventDisableTiming) != hipSuccess)
-                    return nullptr;
+        hipError_t e;
+        if (nd == 0 && (e = hipEventRecord(c->ev_fork, s)) != hipSuccess) {
+            fail(e, "hipEventRecord(fork)");
+            return nullptr;
         }
-        if (nd == 0 && hipEventRecord(c->ev_fork, s) != hipSuccess) return nullptr;
         const int i = nd++ % kForkStreams;
         if (!(used & (1 << i))) {
-            if (hipStreamWaitEvent(c->side[i], c->ev_fork, 0) != hipSuccess) return nullptr;
+            if ((e = hipStreamWaitEvent(c->side[i], c->ev_fork, 0)) != hipSuccess) {
+                fail(e, "hipStreamWaitEvent(side)");
+                return nullptr;
+            }
             used |= 1 << i;
         }
         return c->side[i];
     };
     if (!(mode & BSDC_MODE_SKIP_SMALL)) {
         const uint32_t *f = b->small_fams;
-        for (int q = 0; q < BSDC_SMALL_BUCKETS; q++) {
+        for (int q = 0; q < BSDC_SMALL_BUCKETS && rc == 0; q++) {
             const int64_t nf = b->n_small[q];
             if (nf > 0) {
                 // wavefronts per workgroup (they share one copy of the tables): 4 or 8, whichever
@@ -2785,51 +2847,61 @@ int32_t bsdc_run(bsdc_ctx *c, const bsdc_family_batch *b, bsdc_consensus *o, int
                 const size_t lds = (size_t)nw * (size_t)b->small_arena[q] + (size_t)g2;  // + the static tables
                 const int64_t blocks = (nf + nw - 1) / nw;
                 const hipStream_t ls = next_stream();
-                if (!ls && BSDC_FORK) {
-                    c->err = "side stream setup failed";
-                    return BSDC_EDEVICE;
-                }
+                if (rc) break;
                 if (mode & BSDC_MODE_TAGS)
                     hipLaunchKernelGGL(k_small<true>, dim3((unsigned)blocks), dim3(kWave * nw), lds, ls, P, f, nf,
                                        b->small_arena[q]);
                 else
                     hipLaunchKernelGGL(k_small<false>, dim3((unsigned)blocks), dim3(kWave * nw), lds, ls, P, f, nf,
                                        b->small_arena[q]);
-                HIP_OK(c, hipGetLastError());
+                const hipError_t e = hipGetLastError();
+                if (e != hipSuccess) fail(e, "k_small launch");
             }
             f += 4 * nf;
         }
     }
-    if (!(mode & BSDC_MODE_SKIP_LARGE)) {
+    if (!(mode & BSDC_MODE_SKIP_LARGE) && rc == 0) {
         // one dispatch per non-empty bucket: its LDS arena size sets how many workgroups share a CU
         const uint4 *f = reinterpret_cast<const uint4 *>(b->large_fams);
-        for (int q = 0; q < BSDC_LARGE_BUCKETS; q++) {
+        // every bucket beyond the LDS budget has its own region of `scratch` (the dispatches may
+        // run at once on the side streams)
+        int64_t soff = 0;
+        for (int q = 0; q < BSDC_LARGE_BUCKETS && rc == 0; q++) {
             const int64_t nf = b->n_large[q];
             const int32_t a = b->large_arena[q];
             if (nf > 0) {
                 const bool big = q >= kLargeBigBucket;  // 2 or 1 workgroups per CU, or HBM scratch
                 const hipStream_t ls = next_stream();
-                if (!ls && BSDC_FORK) {
-                    c->err = "side stream setup failed";
-                    return BSDC_EDEVICE;
-                }
+                if (rc) break;
                 if (a <= BSDC_LARGE_LDS_MAX && !big)
-                    hipLaunchKernelGGL((k_large<true, kLargeThreads>), dim3((unsigned)nf), dim3(kLargeThreads), (size_t)a, ls, P, f, nf, a);
+                    hipLaunchKernelGGL((k_large<true, kLargeThreads>), dim3((unsigned)nf), dim3(kLargeThreads), (size_t)a, ls, P, f, nf, a,
+                                       (int64_t)0);
                 else if (a <= BSDC_LARGE_LDS_MAX)
-                    hipLaunchKernelGGL((k_large<true, kLargeThreadsBig>), dim3((unsigned)nf), dim3(kLargeThreadsBig), (size_t)a, ls, P, f, nf, a);
-                else
-                    hipLaunchKernelGGL((k_large<false, kLargeThreadsBig>), dim3((unsigned)nf), dim3(kLargeThreadsBig), 0, ls, P, f, nf, a);
-                HIP_OK(c, hipGetLastError());
+                    hipLaunchKernelGGL((k_large<true, kLargeThreadsBig>), dim3((unsigned)nf), dim3(kLargeThreadsBig), (size_t)a, ls, P, f,
+                                       nf, a, (int64_t)0);
+                else {
+                    hipLaunchKernelGGL((k_large<false, kLargeThreadsBig>), dim3((unsigned)nf), dim3(kLargeThreadsBig), 0, ls, P, f, nf, a,
+                                       soff);
+                    soff += nf * (int64_t)a;
+                }
+                const hipError_t e = hipGetLastError();
+                if (e != hipSuccess) fail(e, "k_large launch");
             }
             f += nf;
         }
     }
-    for (int i = 0; i < kForkStreams; i++)  // join: `s` waits for every side stream used
+    // join: `s` waits for every side stream used -- also after a failed launch, so that no work
+    // already queued on a side stream outlives the caller's view of the batch's buffers
+    for (int i = 0; i < kForkStreams; i++)
         if (used & (1 << i)) {
-            HIP_OK(c, hipEventRecord(c->ev_join[i], c->side[i]));
-            HIP_OK(c, hipStreamWaitEvent(s, c->ev_join[i], 0));
+            hipError_t e = hipEventRecord(c->ev_join[i], c->side[i]);
+            if (e == hipSuccess) e = hipStreamWaitEvent(s, c->ev_join[i], 0);
+            if (e != hipSuccess) {  // cannot order it on `s`: wait for the side stream itself
+                (void)hipStreamSynchronize(c->side[i]);
+                if (rc == 0) fail(e, "join");
+            }
         }
-    return 0;
+    return rc;
 }
 
 int32_t bsdc_convert(bsdc_ctx *c, const bsdc_family_batch *b, bsdc_consensus *o, void *stream) {

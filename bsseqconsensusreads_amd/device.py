@@ -69,11 +69,11 @@ class DeviceBatch:
             self.ss_qual = torch.zeros(nss, dtype=torch.uint8, device=device)
             self.ss_depth = torch.zeros(nss, dtype=torch.int16, device=device)
             self.ss_err = torch.zeros(nss, dtype=torch.int16, device=device)
-        # HBM arenas of the large buckets beyond the LDS budget (dispatches run one after another
-        # on the stream, so they share one buffer); + slack: dword reads may run a few bytes past
-        # the last arena (their bytes are masked)
-        need = max([int(b.shape[0]) * a for b, a in zip(fb.large_buckets, fb.large_arenas)
-                    if b.shape[0] and a > LARGE_LDS_MAX] + [0])
+        # HBM arenas of the large buckets beyond the LDS budget, one region per bucket (the bucket
+        # dispatches run concurrently on the library's side streams); + slack: dword reads may run
+        # a few bytes past the last arena (their bytes are masked)
+        need = sum(int(b.shape[0]) * a for b, a in zip(fb.large_buckets, fb.large_arenas)
+                   if b.shape[0] and a > LARGE_LDS_MAX)
         self.scratch = torch.zeros(need + 256, dtype=torch.uint8, device=device) if need else None
         self._b = _lib.FamilyBatchC()
         b = self._b

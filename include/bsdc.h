@@ -26,7 +26,7 @@
 extern "C" {
 #endif
 
-#define BSDC_ABI_VERSION 7
+#define BSDC_ABI_VERSION 8
 #define BSDC_SMALL_BUCKETS 8
 #define BSDC_LARGE_BUCKETS 6
 #define BSDC_LARGE_LDS_MAX 158912 /* LDS arena bytes one large-family workgroup may use */ /* LDS arena size classes of the wavefront-per-family kernel */
@@ -106,8 +106,9 @@ typedef struct {
     uint8_t *dump_tags;          /* [n_rec] bit0 RD=1, bit1 LA present, bit2 prepended M, bit3 appended M */
     uint8_t *dump_seq;           /* [slot start + j] one nt16 code per byte */
     uint8_t *dump_qual;
-    uint8_t *scratch;            /* arenas of the large buckets beyond BSDC_LARGE_LDS_MAX: the largest
-                                    n_large[q] * large_arena[q] of them + 256 bytes */
+    uint8_t *scratch;            /* arenas of the large buckets beyond BSDC_LARGE_LDS_MAX, one region per
+                                    bucket (their dispatches may run concurrently): the sum of
+                                    n_large[q] * large_arena[q] over those buckets + 256 bytes */
     /* optional single-strand consensus reads and their per-column statistics (BSDC_MODE_TAGS),
      * the inputs of fgbio's per-read / per-base consensus tags (aD/aM/aE, ad/ae/ac/aq, ...;
      * cD/cM/cE, cd/ce for the molecular caller).  Row (f, s), s = 0 AB-R1, 1 AB-R2, 2 BA-R1,
@@ -161,8 +162,9 @@ int64_t bsdc_small_arena_bytes(int32_t n_rec, int64_t img, int32_t n_conv, int64
 int32_t bsdc_get_tables(const bsdc_ctx *ctx, int64_t *lr256, float *thresh94);
 /* Same tables for given error rates, without a context (no GPU needed). */
 void bsdc_model_tables(double error_rate_pre_umi, double error_rate_post_umi, int64_t *lr256, float *thresh94);
-/* The near-tie tables: the same log-likelihood ratios in 2^-40 nats. */
-void bsdc_model_tables40(double error_rate_pre_umi, double error_rate_post_umi, int64_t *lr40_256);
+/* The near-tie tables: fgbio's per-read log-space terms in double precision,
+   ln P(correct) and ln P(error) / 3 per phred, which a near-tie column sums in fgbio's read order. */
+void bsdc_model_tables_fp64(double error_rate_pre_umi, double error_rate_post_umi, double *lnc256, double *lne3_256);
 /* The vote's agreement-case tables: Q(D) = qlo[D >> 16] + (D >= dthr[qlo[D >> 16] + 1]). */
 void bsdc_agree_tables(double error_rate_pre_umi, double error_rate_post_umi, uint8_t *qlo2048, int32_t *dthr48);
 /* The general case's phred buckets: Q(S) = the largest k >= sq[j] with S <= thresh[k], j = the

@@ -309,14 +309,27 @@ void orc_tables(double pre, double post, int64_t *lr, float *thr) {
     }
 }
 
-/* the same log-likelihood ratios in 2^-40 nats (the near-tie decision of ss_consensus) */
-void orc_tables40(double pre, double post, int64_t *lr40) {
+/* fgbio's per-read terms in double-precision log space, as fgbio computes them (LogProbability
+ * arithmetic, restated; PARITY UNPINNED): pErr = probabilityOfErrorTwoTrials(ln e_post, ln e(q)),
+ * lnc[q] = not(pErr) (the read's base), lne3[q] = pErr - ln 3 (each other base).  The near-tie
+ * decision of ss_consensus sums these in fgbio's read order.  Keep the operation order in step
+ * with libbsdc (csrc/bsdc_kernels.hip make_fp64) and tests/fgbio_vote.py qual_tables. */
+static double lp_or(double a, double b) {
+    const double m = a > b ? a : b, n = a > b ? b : a;
+    return m == -INFINITY ? m : m + log1p(exp(n - m));
+}
+static double lp_not(double x) { return x > -log(2.0) ? log(-expm1(x)) : log1p(-exp(x)); }
+static double lp_a_or_not_b(double a, double b) { return b == -INFINITY ? a : a + log1p(-exp(b - a)); }
+static double lp_two_trials(double x, double y) { return lp_a_or_not_b(lp_or(x, y), log(4.0 / 3.0) + x + y); }
+
+void orc_tables_fp64(double pre, double post, double *lnc, double *lne3) {
     (void)pre;
-    const double e_post = pow(10.0, -post / 10.0);
+    const double ln10 = log(10.0), ln3 = log(3.0);
+    const double x = -post * ln10 / 10.0;
     for (int q = 0; q < 256; q++) {
-        const double e = pow(10.0, -(double)q / 10.0);
-        const double a = e_post + e - (4.0 / 3.0) * e_post * e;
-        lr40[q] = llround((log1p(-a) - log(a / 3.0)) * 1099511627776.0);
+        const double pe = lp_two_trials(x, -(double)q * ln10 / 10.0);
+        lnc[q] = lp_not(pe);
+        lne3[q] = pe - ln3;
     }
 }
 
@@ -538,12 +551,15 @@ static int cigar_is_prefix(const srcread *a, const uint32_t *bc, int32_t bn) {
     return cig_op(a->cig[i]) == cig_op(bc[i]) && cig_len(a->cig[i]) <= cig_len(bc[i]);
 }
 
-/* fgbio filterToMostCommonAlignment, restated: sets keep[i] */
-static void filter_most_common(srcread **v, int n, int *keep) {
-    for (int i = 0; i < n; i++) keep[i] = 1;
+/* fgbio filterToMostCommonAlignment, restated: sets keep[i] and order[] -- fgbio returns its
+ * keepers in its sorted order (source length descending, ties in input order), which is the order
+ * the consensus caller then adds the reads in */
+static void filter_most_common(srcread **v, int n, int *keep, int *order) {
+    for (int i = 0; i < n; i++) {
+        keep[i] = 1;
+        order[i] = i;
+    }
     if (n < 2) return;
-    int *order = (int *)malloc(sizeof(int) * (size_t)n);
-    for (int i = 0; i < n; i++) order[i] = i;
     /* stable sort by length, descending (insertion sort keeps ties in input order) */
     for (int i = 1; i < n; i++) {
         int x = order[i], j = i - 1;
@@ -581,7 +597,6 @@ static void filter_most_common(srcread **v, int n, int *keep) {
             if (gsize[g] > gsize[best]) best = g;
         for (int i = 0; i < n; i++) keep[i] = member[(size_t)best * n + i];
     }
-    free(order);
     free(gid_of_cig);
     free(gsize);
     free(member);
@@ -599,7 +614,11 @@ typedef struct {
  * per-column depth and errors fgbio keeps for its consensus tags:
  *   errors = if (rawBase == NoCall) depth else depth - builder.observations(rawBase)
  * where rawBase is the likelihood call before the minimum-quality mask (PARITY UNPINNED). */
-static int ss_consensus(srcread **v, int n, const int64_t *lr, const int64_t *lr40, const float *thr, ssread *out) {
+typedef struct {
+    double lnc[256], lne3[256];
+} fp64tab;
+
+static int ss_consensus(srcread **v, int n, const int64_t *lr, const fp64tab *f64, const float *thr, ssread *out) {
     int32_t lc = 0;
     for (int i = 0; i < n; i++)
         if (v[i]->len > lc) lc = v[i]->len;
@@ -623,22 +642,25 @@ static int ss_consensus(srcread **v, int n, const int64_t *lr, const int64_t *lr
         for (int b = 1; b < 4; b++)
             if (D[b] > D[best]) best = b;
         /* near tie: the 2^-20 sums carry up to half a unit of rounding per read, so a gap of at most
-         * one unit per read of the set can hide the true order -- decide it on the 2^-40 sums
-         * (fgbio sums in double precision; 2^-40 resolves every gap that is not an exact tie of the
-         * same qualities) */
+         * one unit per read of the set can hide fgbio's order.  There fgbio's own pick is taken:
+         * ConsensusBaseBuilder.add's four double-precision sums, read by read in the set's order
+         * (v[] is in fgbio's order, see family_call), first maximum by strict >.  That also
+         * reproduces its rounding on exact ties (equal quality multisets on two bases). */
         int64_t second = INT64_MIN;
         for (int b = 0; b < 4; b++)
             if (b != best && D[b] > second) second = D[b];
-        if (n > 1 && D[best] - second <= n) {
-            int64_t E[4] = {0, 0, 0, 0};
+        if (D[best] - second <= n) {
+            double L[4] = {0.0, 0.0, 0.0, 0.0};
             for (int i = 0; i < n; i++) {
                 if (v[i]->len <= c) continue;
                 int bi = base_index(v[i]->b[c]);
-                if (bi >= 0) E[bi] += lr40[v[i]->q[c]];
+                if (bi < 0) continue;
+                const int q = v[i]->q[c];
+                for (int b = 0; b < 4; b++) L[b] += b == bi ? f64->lnc[q] : f64->lne3[q];
             }
             best = 0;
             for (int b = 1; b < 4; b++)
-                if (E[b] > E[best]) best = b;
+                if (L[b] > L[best]) best = b;
         }
         float S = 0.0f;
         for (int b = 0; b < 4; b++) {
@@ -731,7 +753,7 @@ struct orc_result {
 };
 
 static void family_call(orec *recs, int n, const orc_records *in, const orc_params *p, const int64_t *lr,
-                        const int64_t *lr40, const float *thr, struct orc_result *res, int64_t f) {
+                        const fp64tab *f64, const float *thr, struct orc_result *res, int64_t f) {
     res->fam_status[f] = 0;
     res->fam_len[2 * f] = res->fam_len[2 * f + 1] = 0;
     res->fam_b[2 * f] = res->fam_b[2 * f + 1] = NULL;
@@ -784,22 +806,31 @@ static void family_call(orec *recs, int n, const orc_records *in, const orc_para
     }
     int *kx = (int *)malloc(sizeof(int) * (size_t)(nx + 1));
     int *ky = (int *)malloc(sizeof(int) * (size_t)(ny + 1));
-    filter_most_common(X, nx, kx);
-    filter_most_common(Y, ny, ky);
+    int *ox = (int *)malloc(sizeof(int) * (size_t)(nx + 1));
+    int *oy = (int *)malloc(sizeof(int) * (size_t)(ny + 1));
+    filter_most_common(X, nx, kx, ox);
+    filter_most_common(Y, ny, ky, oy);
     srcread **sets[4];
     int ns[4] = {0, 0, 0, 0};
     for (int s = 0; s < 4; s++) sets[s] = (srcread **)malloc(sizeof(srcread *) * (size_t)(n + 1));
-    /* sets: 0 AB-R1, 1 AB-R2, 2 BA-R1, 3 BA-R2 */
-    for (int i = 0; i < nx; i++)
+    /* sets: 0 AB-R1, 1 AB-R2, 2 BA-R1, 3 BA-R2, each in the filter's output order (fgbio splits
+     * its keepers by strand, keeping their order) */
+    for (int k = 0; k < nx; k++) {
+        const int i = ox[k];
         if (kx[i]) {
             int s = X[i]->strand == 0 ? 0 : 3;
             sets[s][ns[s]++] = X[i];
         }
-    for (int i = 0; i < ny; i++)
+    }
+    for (int k = 0; k < ny; k++) {
+        const int i = oy[k];
         if (ky[i]) {
             int s = Y[i]->strand == 0 ? 1 : 2;
             sets[s][ns[s]++] = Y[i];
         }
+    }
+    free(ox);
+    free(oy);
     if (p->keep_sources) {
         int64_t nr = 0, nb = 0;
         for (int s = 0; s < 4; s++) {
@@ -822,7 +853,7 @@ static void family_call(orec *recs, int n, const orc_records *in, const orc_para
     }
     ssread ss[4];
     int has[4];
-    for (int s = 0; s < 4; s++) has[s] = ss_consensus(sets[s], ns[s], lr, lr40, thr, &ss[s]);
+    for (int s = 0; s < 4; s++) has[s] = ss_consensus(sets[s], ns[s], lr, f64, thr, &ss[s]);
     int32_t nreads = 0;
     for (int s = 0; s < 4; s++) nreads += ns[s];
     res->fam_nreads[f] = nreads;
@@ -1082,10 +1113,11 @@ orc_result *orc_run(const orc_records *in, const orc_reference *ref, const orc_p
     free(rec_group);
     free(gfirst);
     /* ---- vote, per family ---- */
-    int64_t lr[256], lr40[256];
+    int64_t lr[256];
     float thr[94];
+    fp64tab f64;
     orc_tables(p->error_rate_pre_umi, p->error_rate_post_umi, lr, thr);
-    orc_tables40(p->error_rate_pre_umi, p->error_rate_post_umi, lr40);
+    orc_tables_fp64(p->error_rate_pre_umi, p->error_rate_post_umi, f64.lnc, f64.lne3);
     res->nfam = ng;
     res->fam_rec_off = (int64_t *)malloc(sizeof(int64_t) * (size_t)(ng + 1));
     res->fam_src = (int64_t *)malloc(sizeof(int64_t) * (size_t)(res->t2.n + 1));
@@ -1111,7 +1143,7 @@ orc_result *orc_run(const orc_records *in, const orc_reference *ref, const orc_p
     }
 #pragma omp parallel for schedule(dynamic, 64)
     for (int64_t g = 0; g < ng; g++)
-        family_call(frecs + fam_off[g], (int)(fam_off[g + 1] - fam_off[g]), in, p, lr, lr40, thr, res, g);
+        family_call(frecs + fam_off[g], (int)(fam_off[g + 1] - fam_off[g]), in, p, lr, &f64, thr, res, g);
     free(frecs);
     free(gorder_mi);
     free(fam_off);

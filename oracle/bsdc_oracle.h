@@ -109,7 +109,8 @@ void orc_get_sources(const orc_result *r, int32_t *set_count, int32_t *len, uint
 
 /* Tables of the likelihood model, for a cross-check against libbsdc's own. */
 void orc_tables(double pre, double post, int64_t *lr_fixed256, float *phred_thresh94);
-void orc_tables40(double pre, double post, int64_t *lr40_fixed256);
+/* fgbio's per-read log-space terms in double precision: ln P(correct) and ln P(error) / 3 per phred */
+void orc_tables_fp64(double pre, double post, double *lnc256, double *lne3_256);
 float orc_det_expf(float x);
 int64_t orc_check_agree(const uint8_t *qlo, const int32_t *dthr, const float *thr, int64_t dmax);
 

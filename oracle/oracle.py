@@ -74,7 +74,7 @@ def load():
         lib.orc_get_consensus.argtypes = [C.c_void_p, C.c_int32] + [C.c_void_p] * 6
         lib.orc_get_ss.argtypes = [C.c_void_p, C.c_int32] + [C.c_void_p] * 5
         lib.orc_tables.argtypes = [C.c_double, C.c_double, C.c_void_p, C.c_void_p]
-        lib.orc_tables40.argtypes = [C.c_double, C.c_double, C.c_void_p]
+        lib.orc_tables_fp64.argtypes = [C.c_double, C.c_double, C.c_void_p, C.c_void_p]
         lib.orc_det_expf.restype = C.c_float
         lib.orc_det_expf.argtypes = [C.c_float]
         lib.orc_sources_size.argtypes = [C.c_void_p, C.c_void_p, C.c_void_p]
@@ -308,10 +308,13 @@ def tables(pre=45.0, post=30.0):
     return lr, thr
 
 
-def tables40(pre=45.0, post=30.0):
-    lr40 = np.zeros(256, np.int64)
-    load().orc_tables40(pre, post, _ptr(lr40))
-    return lr40
+def tables_fp64(pre=45.0, post=30.0):
+    """fgbio's per-read log-space terms (ln P(correct), ln P(error) / 3 per phred) in double precision:
+    what the near-tie decision sums read by read."""
+    lnc = np.zeros(256, np.float64)
+    lne3 = np.zeros(256, np.float64)
+    load().orc_tables_fp64(pre, post, _ptr(lnc), _ptr(lne3))
+    return lnc, lne3
 
 
 def det_expf(x: float) -> float:

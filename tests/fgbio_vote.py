@@ -2,7 +2,8 @@
 INFRASTRUCTURE ONLY -- the checker of the vote's arithmetic, never the product).
 
 The kernels and oracle/ vote in exact fixed point: likelihood sums in
-2^-20 nats (2^-40 on near ties), a float32 exp, float thresholds.  fgbio computes the same model in
+2^-20 nats, a float32 exp, float thresholds; on a near tie they take fgbio's own pick, the four
+double-precision sums added read by read in fgbio's read order.  fgbio computes the whole model in
 double-precision log space.  This module restates fgbio's arithmetic the way fgbio writes it,
 sharing no table and no code with either (main.snake.py:163 for the flags):
 
@@ -61,11 +62,28 @@ def error_two_trials(x, y):
     return _a_or_not_b(_or2(x, y), LN43 + x + y)
 
 
+def _or_s(a, b):
+    m, n = max(a, b), min(a, b)
+    return m if m == -math.inf else m + math.log1p(math.exp(n - m))
+
+
+def _not_s(x):
+    return math.log(-math.expm1(x)) if x > -math.log(2.0) else math.log1p(-math.exp(x))
+
+
+def _a_or_not_b_s(a, b):
+    return a if b == -math.inf else a + math.log1p(-math.exp(b - a))
+
+
 def qual_tables(post: float):
-    """Per phred 0..255: ln P(error), ln P(correct), ln P(error)/3 of one read after the post-UMI step."""
-    q = np.arange(256, dtype=np.float64)
-    p_err = error_two_trials(np.full(256, -post * LN10 / 10.0), -q * LN10 / 10.0)
-    return p_err, _not(p_err), p_err - LN3
+    """Per phred 0..255: ln P(error), ln P(correct), ln P(error)/3 of one read after the post-UMI step.
+    Scalar `math` calls (the C library's log / exp / log1p / expm1, the functions fgbio's JVM math
+    also rounds correctly almost everywhere), not numpy's vectorised ones: the per-read terms are
+    what fgbio adds up, so they must be the exact doubles."""
+    x = -post * LN10 / 10.0
+    p_err = np.array([_a_or_not_b_s(_or_s(x, -q * LN10 / 10.0), LN43 + x + -q * LN10 / 10.0)
+                      for q in range(256)], np.float64)
+    return p_err, np.array([_not_s(v) for v in p_err], np.float64), p_err - LN3
 
 
 def phred_from_ln(ln_p):
@@ -74,12 +92,13 @@ def phred_from_ln(ln_p):
     return np.minimum(q, 93).astype(np.int64)
 
 
-def ss_vote(count, lens, base, qual, stride, pre=45.0, post=30.0, tie_tol=1e-9):
+def ss_vote(count, lens, base, qual, stride, pre=45.0, post=30.0):
     """Single-strand consensus of every (family, set) from its source reads.
 
     count [F, 4] reads per set, lens / flat base (nt16) / qual per read in family / set order.
     -> dict: len [F, 4]; base, qual [F, 4, stride]; gap [F, 4, stride] = L(b*) - L(second)
-    (fp64 nats); tied [F, 4, stride] one-hot mask of the bases within tie_tol of the maximum."""
+    (fp64 nats); tied [F, 4, stride] one-hot mask of the bases whose sum equals the maximum (0 where
+    no read has an A/C/G/T)."""
     F = count.shape[0]
     nrow = 4 * F
     cnt = count.reshape(-1).astype(np.int64)
@@ -106,6 +125,7 @@ def ss_vote(count, lens, base, qual, stride, pre=45.0, post=30.0, tie_tol=1e-9):
     for k in range(4):  # np.bincount sums in entry order: read by read for each column, as fgbio adds them
         w = np.where(b_ok == k, p_cor[q_ok], p_err3[q_ok])
         L[k] = np.bincount(r_ok, weights=w, minlength=nrow * stride)
+    depth = np.bincount(r_ok, minlength=nrow * stride)
     best = np.argmax(L, axis=0)  # first maximum
     m = L[best, np.arange(nrow * stride)]
     tot_ln = m + np.log(np.exp(L - m[None, :]).sum(0))
@@ -116,7 +136,7 @@ def ss_vote(count, lens, base, qual, stride, pre=45.0, post=30.0, tie_tol=1e-9):
     gap = srt[3] - srt[2]
     tied = np.zeros(nrow * stride, np.int64)
     for k in range(4):
-        tied |= np.where(L[k] >= m - tie_tol, 1 << k, 0)
+        tied |= np.where((L[k] == m) & (depth > 0), 1 << k, 0)
     live = np.arange(stride)[None, :] < lc[:, None]
     callb = np.where(Q < 2, N_CODE, 1 << best).reshape(nrow, stride)
     callq = np.where(Q < 2, 2, Q).reshape(nrow, stride)
@@ -160,29 +180,28 @@ def duplex(ss):
     return emit.astype(np.int32), out_l, out_b, out_q
 
 
-def compare_ss(got: dict, ref: dict, tie_tol=1e-9) -> dict:
+def compare_ss(got: dict, ref: dict) -> dict:
     """Kernel / oracle single-strand reads (`got`: len, base, qual [F, 4, stride], nt16) against
-    this restatement (`ref` from ss_vote).  Returns counts: columns compared, base differences
-    outside exact ties, tie columns (fgbio's own pick there is summation-order rounding; the
-    fixed-point vote must pick one of the tied bases), tie columns off the tied set, and the
-    quality differences by size."""
+    this restatement (`ref` from ss_vote).  Returns counts: columns compared, base differences (every
+    column, exact ties included: the vote takes fgbio's fp64 read-order pick on near ties, so a tie
+    of the same quality multiset on two bases must resolve as fgbio's summation rounds it), the
+    exact-tie columns (fp64 gap 0 between two bases, depth > 0) and the base differences among
+    them, and the quality differences by size."""
     assert np.array_equal(got["len"], ref["len"]), "single-strand lengths differ"
     stride = min(got["base"].shape[2], ref["base"].shape[2])
     live = np.arange(stride)[None, None, :] < ref["len"][:, :, None]
     gb, rb = got["base"][:, :, :stride].astype(np.int64), ref["base"][:, :, :stride].astype(np.int64)
     gq, rq = got["qual"][:, :, :stride].astype(np.int64), ref["qual"][:, :, :stride].astype(np.int64)
-    called = live & (rb != N_CODE) & (gb != N_CODE)
-    tie = live & (ref["gap"][:, :, :stride] < tie_tol) & (np.bitwise_count(ref["tied"][:, :, :stride].astype(np.uint64)) > 1)
+    tie = live & (ref["gap"][:, :, :stride] == 0) & (np.bitwise_count(ref["tied"][:, :, :stride].astype(np.uint64)) > 1)
     diff_b = live & (gb != rb)
-    in_tied = (ref["tied"][:, :, :stride] & np.where(gb == N_CODE, 0, gb)) != 0
     dq = np.abs(gq - rq)
     # a base called N on one side only: the quality sits at the Q2 boundary (2 vs 1 -> N); allowed as a +-1
     n_flip = live & ((gb == N_CODE) != (rb == N_CODE))
     return {"columns": int(live.sum()),
-            "base_diff": int((diff_b & ~tie & ~n_flip).sum()),
+            "base_diff": int((diff_b & ~n_flip).sum()),
             "tie_columns": int(tie.sum()),
-            "tie_off_set": int((tie & diff_b & called & ~in_tied).sum()),
+            "tie_diff": int((tie & diff_b & ~n_flip).sum()),
             "n_boundary": int(n_flip.sum()),
             "n_boundary_bad": int((n_flip & (np.maximum(gq, rq) > 2)).sum()),
-            "qual_pm1": int((live & ~tie & (dq == 1)).sum()),
-            "qual_gt1": int((live & ~tie & ~n_flip & (dq > 1)).sum())}
+            "qual_pm1": int((live & (dq == 1)).sum()),
+            "qual_gt1": int((live & ~n_flip & (dq > 1)).sum())}

@@ -49,10 +49,16 @@ def _force_large(monkeypatch, where):
     real_m, real_b = batch.materialize, batch.build_family_batch
 
     def glob(fb):
+        nb = len(fb.large_buckets)
+        top = max(max(fb.large_arenas), batch.LARGE_LDS_MAX + 16)
         if where == "global":  # every large family in the last (HBM scratch) bucket
-            nb = len(fb.large_buckets)
             fb.large_buckets = [np.zeros((0, 4), np.uint32)] * (nb - 1) + [fb.large_fams]
-            fb.large_arenas = [16] * (nb - 1) + [max(max(fb.large_arenas), batch.LARGE_LDS_MAX + 16)]
+            fb.large_arenas = [16] * (nb - 1) + [top]
+        elif where == "two-scratch":  # two buckets beyond the LDS budget, dispatched concurrently
+            lf = fb.large_fams
+            h = lf.shape[0] // 2
+            fb.large_buckets = [np.zeros((0, 4), np.uint32)] * (nb - 2) + [lf[:h], lf[h:]]
+            fb.large_arenas = [16] * (nb - 2) + [top + 4096, top + 8192]
         return fb
     monkeypatch.setattr(pipeline, "materialize", lambda plan, f0, f1, small_cap=0: glob(real_m(plan, f0, f1, 0)))
     monkeypatch.setattr(pipeline, "build_family_batch",
@@ -80,6 +86,18 @@ def test_large_kernel_tools12_match_reference(engine, where, monkeypatch):
     cons, t2 = pipeline.run_step5(engine, raw, dump=True)
     compare_records(g["tool2"], t2, raw, g["input"], "k_large fused tool2 dump " + where)
     assert_consensus_equal(cons, oracle.run(raw, ref), "k_large golden families")
+
+
+def test_two_scratch_buckets_vs_oracle(engine, monkeypatch):
+    """two large buckets beyond the LDS budget run concurrently on the side streams, each
+    in its own region of the HBM scratch buffer (no two dispatches share an arena)."""
+    _force_large(monkeypatch, "two-scratch")
+    s = synth.generate("C3", 60, seed=29, device="cpu", genome_len=200_000)
+    engine.load_reference(s.ref)
+    cons, _ = pipeline.run_step5(engine, s.raw, tags=True)
+    ref = oracle.run(s.raw, s.ref)
+    assert_consensus_equal(cons, ref, "two scratch buckets")
+    assert_ss_equal(cons, ref, "two scratch buckets")
 
 
 def test_large_kernel_dump_vs_oracle_contig_ends(engine, monkeypatch):
