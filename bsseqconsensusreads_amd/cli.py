@@ -14,9 +14,12 @@ step5 on one GPU streams a coordinate-sorted input (--stream auto, the default: 
 says SO:coordinate): bounded memory whatever the input size, decode / GPU / encode overlapped,
 output identical to the whole-file path (bam.step5_stream).  Other inputs are read whole
 (bam.step5); --stream true insists on streaming (an unsorted input is then an error).
-step5 --gpus N: one process per GPU (spawned here, or under torch.distributed.run); the family
-batches are dealt to the ranks and rank 0 writes the outputs, identical to --gpus 1
-(bam.consensus_sharded).  --devices maps ranks to device ids (default rank r -> GPU r).
+step5 --gpus N on a coordinate-sorted input streams too (fleet.step5_stream_multi): this process
+reads the BAM once and writes the outputs in order, N spawned worker processes (one per GPU) run
+the family batches it deals them through shared memory; bounded memory, output identical to
+--gpus 1.  Other inputs (or a run under torch.distributed.run) take the whole-file path: one
+process per GPU, every rank forms the plan, batches dealt to the ranks, rank 0 writes
+(bam.consensus_sharded).  --devices maps workers / ranks to device ids (default 0..N-1).
 """
 from __future__ import annotations
 
@@ -68,12 +71,34 @@ def _coordinate_sorted(bam, path: str) -> bool:
     return False
 
 
+def _step5_fleet(a, gpus: int) -> int:
+    """step5 --gpus N on a coordinate-sorted input: fleet.step5_stream_multi (module docstring)."""
+    from . import fleet
+    devs = [int(x) for x in a.devices.split(",")] if a.devices else list(range(gpus))
+    if len(devs) != gpus:
+        print("--devices needs %d ids" % gpus, file=sys.stderr)
+        return 2
+    try:
+        info = fleet.step5_stream_multi(a.input, a.reference, None if a.output == "-" else a.output, devs,
+                                        a.read_name_prefix, a.threads, a.compression,
+                                        (a.fastq1, a.fastq2) if a.fastq1 else None,
+                                        tags=a.output_per_base_tags == "true", chunk_bytes=a.chunk_mb << 20,
+                                        batch_bases=a.batch_bases)
+    except Exception as e:  # noqa: BLE001 -- the rule fails with the message
+        print("%s: %s" % (type(e).__name__, e), file=sys.stderr)
+        return 1
+    print(json.dumps(info), file=sys.stderr)
+    return 0
+
+
 def main(argv=None) -> int:
     argv = sys.argv[1:] if argv is None else list(argv)
     a = parse(argv)
     from . import bam, shard
     gpus = getattr(a, "gpus", 1)
     if gpus > 1 and "WORLD_SIZE" not in os.environ:
+        if a.stream == "true" or (a.stream == "auto" and _coordinate_sorted(bam, a.input)):
+            return _step5_fleet(a, gpus)  # this process never touches the GPU
         return shard.launch(gpus, main, (argv,))  # this process never touches the GPU
     rank, world, local = shard.env_rank()
     if world != gpus:

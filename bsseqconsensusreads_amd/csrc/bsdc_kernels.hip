@@ -48,6 +48,9 @@ constexpr int kWave = 64;
 #define SMALL_STAGE_U 4  // k_small staging: image chunk loads in flight per lane
 #endif
 constexpr int kStageU = SMALL_STAGE_U;
+#ifndef SMALL_PROBE
+#define SMALL_PROBE 0  // timing probes only (wrong results): 1 no window loads, 2 no base unpack
+#endif
 #ifndef LARGE_THREADS
 #define LARGE_THREADS 256  // k_large workgroup size (a multiple of 64)
 #endif
@@ -968,9 +971,12 @@ __global__ __launch_bounds__(kWave *kSmallMaxWaves, kSmallMinWaves) __attribute_
         if (k < nqc) {
             *reinterpret_cast<uint4 *>(qimg + 16 * k) = v;
             qor |= v.x | v.y | v.z | v.w;
-        } else
-        if (k >= nqc && k < nch)
-            unpack32<true>(v, bimg + 32 * (k - nqc));
+        } else if (k >= nqc && k < nch) {
+            if (SMALL_PROBE == 2)
+                *reinterpret_cast<uint4 *>(bimg + 32 * (k - nqc)) = v;
+            else
+                unpack32<true>(v, bimg + 32 * (k - nqc));
+        }
     };
     // lanes take qual chunks and packed-base chunks in separate rounds (the unpack runs once per
     // round of base chunks instead of in every round where some lane has one): chunk k of round u
@@ -1015,7 +1021,7 @@ __global__ __launch_bounds__(kWave *kSmallMaxWaves, kSmallMinWaves) __attribute_
     // window chunk k -> (converted record k / rcn, part k % rcn); rcn and its 2^32 reciprocal are
     // launch constants (floor(k * rinv / 2^32) is exact for k, rcn < 2^16)
     const uint32_t rcn = (uint32_t)P.ref_chunks, rinv = P.ref_chunks_inv;
-    const int wtot = nconv * (int)rcn;
+    const int wtot = SMALL_PROBE == 1 ? 0 : nconv * (int)rcn;
     auto load_win = [&](int k) {
         uint4 x = make_uint4(0, 0, 0, 0);
         if (k < wtot) {

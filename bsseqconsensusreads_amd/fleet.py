@@ -1,0 +1,462 @@
+"""Step 5 over N GPUs of one node, streaming: one reader, N GPU workers, one ordered writer.
+
+MI families are independent, so the GPUs never talk to each other.  This process
+(the coordinator) never touches a GPU.  It spawns one worker process per device, then runs the
+one-GPU stream's front end (bam.step5_stream): a decoder thread reads the coordinate-sorted BAM
+once, in bounded chunks (bam.stream_bam), and a planner thread forms each chunk's families
+(batch.plan_families, the fgbio TemplateCoordinate runs).  The coordinator cuts every chunk's
+families into device batches (pipeline.plan_ranges), builds each batch (C++ materialize) and hands
+it to the least-loaded worker through shared memory: arrays travel as torch.multiprocessing
+shared-memory tensors (one copy in, no pickled array data, no process-group traffic).  A worker
+uploads the batch to its GPU, runs the kernels (libbsdc, the same launch as one GPU) and hands
+the consensus arrays back the same way.  A collector thread puts the batches back in input order
+and a writer thread turns each complete chunk into records and appends them to the BAM / FASTQ
+(bam.duplex_records, BamWriter, FastqWriter): the output is byte-identical to the one-GPU stream.
+
+Memory is bounded whatever the input size: at most `inflight` batches per worker, and the
+decoder / planner / writer hand-offs hold one chunk each (reference: the 100 GB note of
+README.md:83 and tool 2's whole-file dict, tools/2.extend_gap.py:155-178).
+
+A chunk whose tool-2 extension partners straddle its families (plan.split_ext: inconsistent mate
+fields) goes to one worker whole, which runs pipeline.run_step5's two-launch fallback on it.
+
+Workers run a pluggable runner (``runner``: "module:Class"); the default is GpuRunner (libbsdc on
+the worker's device).  tests/fleet_standin.py is a CPU stand-in that computes the same arrays with
+oracle/, so the whole multi-process path (spawn, chunks, shared memory, order, writer) is tested
+on CPU.
+"""
+from __future__ import annotations
+
+import dataclasses
+import importlib
+import os
+import queue
+import threading
+import time
+import traceback
+from typing import Dict, List, Optional, Sequence, Tuple
+
+import numpy as np
+import torch
+import torch.multiprocessing as tmp
+
+from . import records as R
+
+_SMALL = 4096  # arrays below this many bytes travel pickled with the message
+
+
+# ------------------------------------------------------------------------------------------
+# shared-memory packing of the batch / result objects
+# ------------------------------------------------------------------------------------------
+def _share_array(a: np.ndarray):
+    a = np.ascontiguousarray(a)
+    if a.nbytes < _SMALL:
+        return ("np", a)
+    t = torch.empty(a.nbytes, dtype=torch.uint8).share_memory_()
+    np.copyto(t.numpy(), a.reshape(-1).view(np.uint8))
+    return ("sh", t, a.dtype.str, a.shape)
+
+
+def pack(obj):
+    """obj (dataclass / dict / list of numpy arrays, StringTables, scalars) -> a picklable tree whose
+    large arrays are shared-memory tensors."""
+    from .bam import StringTable
+    if isinstance(obj, np.ndarray):
+        return _share_array(obj)
+    if isinstance(obj, StringTable):
+        return ("st", pack(obj.buf), pack(obj.off), obj.as_str)
+    if dataclasses.is_dataclass(obj) and not isinstance(obj, type):
+        return ("dc", type(obj), {f.name: pack(getattr(obj, f.name)) for f in dataclasses.fields(obj)})
+    if isinstance(obj, dict):
+        return ("di", {k: pack(v) for k, v in obj.items()})
+    if isinstance(obj, (list, tuple)) and any(isinstance(x, np.ndarray) for x in obj):
+        return ("li", [pack(x) for x in obj])
+    return ("v", obj)
+
+
+def unpack(tree):
+    """The inverse of pack: numpy views of the shared tensors (they stay alive with the views)."""
+    from .bam import StringTable
+    kind = tree[0]
+    if kind == "np":
+        return tree[1]
+    if kind == "sh":
+        _, t, dt, shape = tree
+        return t.numpy().view(np.dtype(dt)).reshape(shape)
+    if kind == "st":
+        return StringTable(unpack(tree[1]), unpack(tree[2]), tree[3])
+    if kind == "dc":
+        return tree[1](**{k: unpack(v) for k, v in tree[2].items()})
+    if kind == "di":
+        return {k: unpack(v) for k, v in tree[1].items()}
+    if kind == "li":
+        return [unpack(x) for x in tree[1]]
+    return tree[1]
+
+
+# ------------------------------------------------------------------------------------------
+# workers
+# ------------------------------------------------------------------------------------------
+class GpuRunner:
+    """A worker's compute: libbsdc on one device (device.Engine)."""
+
+    needs_raw = False
+
+    def __init__(self, device: int):
+        from .device import Engine
+        self.eng = Engine(device)
+
+    def load_reference(self, ref):
+        self.eng.load_reference(ref)
+
+    def run_batch(self, fb, mode: int, tags: bool, raw_sub=None) -> dict:
+        from ._lib import MODE_TAGS
+        db = self.eng.upload(fb, tags=tags)
+        self.eng.run(db, mode | (MODE_TAGS if tags else 0))
+        return db.fetch()
+
+    def run_chunk(self, raw, tags: bool, batch_bases):
+        from . import pipeline
+        return pipeline.run_step5(self.eng, raw, tags=tags, batch_bases=batch_bases)[0]
+
+    def close(self):
+        self.eng.close()
+
+
+def _make_runner(spec: Optional[str], device: int):
+    if spec is None:
+        return GpuRunner(device)
+    mod, cls = spec.split(":")
+    return getattr(importlib.import_module(mod), cls)(device)
+
+
+def _worker(wid: int, device: int, runner_spec: Optional[str], tq, rq):
+    """One GPU worker (a spawned process: it is the first thing here to touch the GPU)."""
+    runner = None
+    try:
+        runner = _make_runner(runner_spec, device)
+        rq.put(("ready", wid, bool(getattr(runner, "needs_raw", False))))
+        while True:
+            msg = tq.get()
+            if msg is None:
+                break
+            kind = msg[0]
+            if kind == "ref":
+                runner.load_reference(unpack(msg[1]))
+            elif kind == "batch":
+                _, key, fb_t, mode, tags, raw_t = msg
+                out = runner.run_batch(unpack(fb_t), mode, tags, unpack(raw_t) if raw_t is not None else None)
+                del fb_t, raw_t
+                rq.put(("batch", wid, key, pack(out)))
+            elif kind == "chunk":
+                _, key, raw_t, tags, batch_bases = msg
+                cons = runner.run_chunk(unpack(raw_t), tags, batch_bases)
+                del raw_t
+                rq.put(("chunk", wid, key, pack(cons)))
+    except BaseException as e:  # noqa: BLE001 -- reported to the coordinator, which raises it
+        rq.put(("error", wid, "%s: %s\n%s" % (type(e).__name__, e, traceback.format_exc())))
+        # stay until the coordinator ends the fleet: results this worker sent earlier hold shared
+        # memory whose descriptors the coordinator fetches from this process when it reads them
+        try:
+            while tq.get(timeout=600) is not None:
+                pass
+        except Exception:  # noqa: BLE001
+            pass
+    finally:
+        if runner is not None:
+            try:
+                runner.close()
+            except Exception:  # noqa: BLE001
+                pass
+
+
+class Fleet:
+    """N worker processes, spawned before this process touches any GPU (spawn context: a fresh
+    interpreter per worker; nothing is forked or exec'd from a GPU process)."""
+
+    def __init__(self, devices: Sequence[int], runner: Optional[str] = None, inflight: int = 2):
+        ctx = tmp.get_context("spawn")
+        self.rq = ctx.Queue()
+        self.tqs = [ctx.Queue() for _ in devices]
+        self.procs = [ctx.Process(target=_worker, args=(i, int(d), runner, self.tqs[i], self.rq), daemon=True)
+                      for i, d in enumerate(devices)]
+        for p in self.procs:
+            p.start()
+        self.n = len(devices)
+        self.load = [0] * self.n
+        self.slots = threading.Semaphore(max(1, inflight) * self.n)
+        self.needs_raw = False
+        try:
+            for _ in range(self.n):
+                m = self.get()
+                if m[0] != "ready":
+                    raise RuntimeError("fleet worker failed to start: %s" % (m,))
+                self.needs_raw |= m[2]
+        except BaseException:
+            self.close(timeout=30.0)
+            raise
+
+    def get(self, timeout: Optional[float] = None):
+        """The next worker message (None after `timeout` seconds without one); raises if a worker
+        reported an error or died."""
+        t0 = time.time()
+        while True:
+            try:
+                m = self.rq.get(timeout=1.0 if timeout is None else min(1.0, timeout))
+            except queue.Empty:
+                dead = [i for i, p in enumerate(self.procs) if not p.is_alive()]
+                if dead:
+                    raise RuntimeError("fleet worker %d exited (code %s)" % (dead[0], self.procs[dead[0]].exitcode))
+                if timeout is not None and time.time() - t0 >= timeout:
+                    return None
+                continue
+            if m[0] == "error":
+                raise RuntimeError("fleet worker %d: %s" % (m[1], m[2]))
+            return m
+
+    def broadcast(self, msg):
+        for q in self.tqs:
+            q.put(msg)
+
+    def submit(self, msg, stop: Optional[threading.Event] = None) -> int:
+        """Queue a job on the least-loaded worker (blocks while every worker holds `inflight`);
+        -1 when `stop` is set first."""
+        while not self.slots.acquire(timeout=0.5):
+            if stop is not None and stop.is_set():
+                return -1
+        w = min(range(self.n), key=lambda i: self.load[i])
+        self.load[w] += 1
+        self.tqs[w].put(msg)
+        return w
+
+    def done(self, wid: int):
+        self.load[wid] -= 1
+        self.slots.release()
+
+    def close(self, timeout: float = 60.0):
+        for q in self.tqs:
+            try:
+                q.put(None)
+            except Exception:  # noqa: BLE001
+                pass
+        t0 = time.time()
+        for p in self.procs:
+            p.join(max(0.1, timeout - (time.time() - t0)))
+            if p.is_alive():
+                p.terminate()
+                p.join(5)
+
+
+# ------------------------------------------------------------------------------------------
+# the coordinator
+# ------------------------------------------------------------------------------------------
+@dataclasses.dataclass
+class _FamilyIndex:
+    """What the coordinator keeps of a sent batch: enough for pipeline.consensus_from_output."""
+
+    fam_mi: np.ndarray
+    fam_off: np.ndarray
+    src: np.ndarray
+
+    @property
+    def n_fam(self) -> int:
+        return int(self.fam_off.shape[0]) - 1
+
+
+def step5_stream_multi(in_bam: str, fasta: str, out_bam: Optional[str], devices: Sequence[int],
+                       prefix: Optional[str] = None, threads: int = 0, level: int = 6,
+                       fastq: Optional[Tuple[str, str]] = None, tags: bool = True, chunk_bytes: Optional[int] = None,
+                       slack: Optional[int] = None, batch_bases: Optional[int] = None, inflight: int = 2,
+                       runner: Optional[str] = None, stats: Optional[dict] = None) -> dict:
+    """bam.step5_stream over len(devices) GPU workers (see the module docstring).  Same file
+    contract and output bytes as bam.step5 / bam.step5_stream (main.snake.py:121-164)."""
+    from . import bam, pipeline
+    chunk_bytes = bam.DEFAULT_CHUNK_BYTES if chunk_bytes is None else chunk_bytes
+    slack = bam.DEFAULT_SLACK if slack is None else slack
+    T = {"decode": 0.0, "plan": 0.0, "materialize": 0.0, "submit_wait": 0.0, "records": 0.0, "encode": 0.0}
+    info = {"records_in": 0, "families": 0, "families_emitted": 0, "records_out": 0, "chunks": 0, "batches": 0,
+            "workers": len(devices)}
+    hdr0 = bam.read_bam_header(in_bam)
+    ref = bam.read_fasta(fasta, hdr0)
+    pre = bam.read_name_prefix(hdr0) if prefix is None else prefix
+    tg = tags and out_bam is not None  # the FASTQ pair carries no tags
+    mode = pipeline.MODE_CONVERT | pipeline.MODE_EXTEND | pipeline.MODE_VOTE
+    fleet = Fleet(devices, runner, inflight)
+    stop = threading.Event()
+    err: List[BaseException] = []
+    raws: "queue.Queue" = queue.Queue(maxsize=1)
+    chunks: "queue.Queue" = queue.Queue(maxsize=1)
+    outs: "queue.Queue" = queue.Queue(maxsize=1)
+    # chunk id -> {"raw", "n" (batches; None until the dealer has sent them all), "parts": {i:
+    # Consensus}, "index": {i: _FamilyIndex}}, filled by the dealer and the collector
+    pend: Dict[int, dict] = {}
+    eof: List[Optional[int]] = [None]  # number of chunks, once the dealer has seen them all
+    plock = threading.Condition()
+
+    def fail(e: BaseException):
+        err.append(e)
+        stop.set()
+        with plock:
+            plock.notify_all()
+
+    def decoder():
+        try:
+            for _, raw in bam.stream_bam(in_bam, threads, chunk_bytes, slack):
+                if stop.is_set():
+                    break
+                raws.put(raw)
+        except BaseException as e:  # noqa: BLE001
+            fail(e)
+        finally:
+            raws.put(None)
+
+    def planner():
+        try:
+            while True:
+                t0 = time.perf_counter()
+                raw = raws.get()
+                if raw is None:
+                    break
+                if stop.is_set():
+                    continue  # drain to the decoder's None
+                t1 = time.perf_counter()
+                plan = pipeline.plan_families(raw, "full", ref)
+                T["plan"] += time.perf_counter() - t1
+                T["decode"] += t1 - t0  # the wait for the decoder
+                chunks.put((raw, plan))
+        except BaseException as e:  # noqa: BLE001
+            fail(e)
+            while raws.get() is not None:
+                pass
+        finally:
+            chunks.put(None)
+
+    def collector():
+        """Worker results -> pend; complete chunks go to the writer in input order."""
+        nxt = 0
+        try:
+            while not stop.is_set():
+                ready = []
+                with plock:
+                    while nxt in pend and pend[nxt]["n"] is not None and len(pend[nxt]["parts"]) == pend[nxt]["n"]:
+                        ready.append(pend.pop(nxt))
+                        nxt += 1
+                    if ready:
+                        plock.notify_all()
+                    finished = eof[0] is not None and nxt >= eof[0]
+                for c in ready:
+                    outs.put(c)
+                if finished:
+                    break
+                m = fleet.get(timeout=0.5)
+                if m is None:
+                    continue
+                kind, wid, (cid, i), res = m[0], m[1], m[2], unpack(m[3])
+                with plock:
+                    c = pend[cid]
+                    c["parts"][i] = pipeline.consensus_from_output(c["index"].pop(i), res) if kind == "batch" else res
+                    plock.notify_all()
+                fleet.done(wid)
+        except BaseException as e:  # noqa: BLE001
+            fail(e)
+        finally:
+            outs.put(None)
+
+    def writer():
+        try:
+            w = bam.BamWriter(out_bam, bam.output_header(hdr0), level) if out_bam is not None else None
+            fq = bam.FastqWriter(fastq[0], fastq[1], level) if fastq is not None else None
+            while True:
+                c = outs.get()
+                if c is None:
+                    break
+                if stop.is_set():
+                    continue
+                cons = pipeline.concat_consensus([c["parts"][i] for i in range(c["n"])])
+                info["families"] += int(cons.status.shape[0])
+                info["families_emitted"] += int(((cons.status & 1) != 0).sum())
+                t0 = time.perf_counter()
+                recs = bam.duplex_records(cons, c["raw"], pre, threads)
+                t1 = time.perf_counter()
+                if w is not None:
+                    w.add(recs, threads)
+                if fq is not None:
+                    fq.add(recs, threads)
+                info["records_out"] += recs.n
+                T["records"] += t1 - t0
+                T["encode"] += time.perf_counter() - t1
+            if not stop.is_set():
+                if w is not None:
+                    w.close(threads)
+                if fq is not None:
+                    fq.close(threads)
+        except BaseException as e:  # noqa: BLE001
+            fail(e)
+            while outs.get() is not None:
+                pass
+
+    workers = [threading.Thread(target=f, daemon=True) for f in (decoder, planner, collector, writer)]
+    drained = False
+    try:
+        fleet.broadcast(("ref", pack(dataclasses.replace(ref, letters={}))))
+        for t in workers:
+            t.start()
+        cid = 0
+        while not stop.is_set():
+            item = chunks.get()
+            if item is None:
+                drained = True
+                break
+            raw, plan = item
+            info["records_in"] += raw.n
+            info["chunks"] += 1
+            with plock:  # a bounded number of chunks between the dealer and the writer
+                while len(pend) >= 2 * fleet.n + 2 and not stop.is_set():
+                    plock.wait(0.5)
+                pend[cid] = {"raw": raw, "n": None, "parts": {}, "index": {}}
+            n = 0
+            if plan.split_ext:
+                if fleet.submit(("chunk", (cid, 0), pack(raw), tg, batch_bases), stop) >= 0:
+                    n = 1
+            else:
+                for a, b in pipeline.plan_ranges(plan, batch_bases):
+                    t0 = time.perf_counter()
+                    fb = pipeline.materialize(plan, a, b)
+                    T["materialize"] += time.perf_counter() - t0
+                    with plock:
+                        pend[cid]["index"][n] = _FamilyIndex(fb.fam_mi.copy(), fb.fam_off.astype(np.int64),
+                                                             fb.src.astype(np.int64))
+                    raw_sub = pack(R.take(raw, fb.src.astype(np.int64))) if fleet.needs_raw else None
+                    # the worker needs the device arrays only (host bookkeeping stays here)
+                    slim = dataclasses.replace(fb, src=np.zeros(0, np.int64), fam_mi=np.zeros(0, np.int32),
+                                               t2_rank=np.zeros(0, np.int64), rec_tid=np.zeros(0, np.int32))
+                    t0 = time.perf_counter()
+                    w = fleet.submit(("batch", (cid, n), pack(slim), mode, tg, raw_sub), stop)
+                    T["submit_wait"] += time.perf_counter() - t0
+                    del fb, slim
+                    if w < 0:
+                        break
+                    n += 1
+                    info["batches"] += 1
+            with plock:
+                pend[cid]["n"] = n
+                plock.notify_all()
+            cid += 1
+        with plock:
+            eof[0] = cid
+            plock.notify_all()
+    except BaseException as e:  # noqa: BLE001
+        fail(e)
+    finally:
+        if not drained:  # let the planner and the decoder finish (they stop at their next chunk)
+            stop.set()
+            while chunks.get() is not None:
+                pass
+        for t in workers:
+            t.join(timeout=600)
+        fleet.close()
+    if err:
+        raise err[0]
+    if stats is not None:
+        stats.update({k: round(v, 4) for k, v in T.items()})
+    return info

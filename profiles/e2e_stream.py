@@ -4,8 +4,11 @@ synthetic coordinate-sorted C2 BAM + FASTA on local disk, then, each in a fresh 
   whole   bam.step5: read the whole BAM, form every family, GPU batches, write the BAM
   stream  bam.step5_stream: bounded chunks, reader / GPU / writer threads overlapped
   stream_fastq  the same, writing the FASTQ pair of the next rule instead of the BAM
-The two BAMs are compared byte for byte.  Usage:
-  python profiles/e2e_stream.py [--families N] [--threads T] [--chunk-mb M] [--level L]"""
+  fleet   fleet.step5_stream_multi: this child reads and writes (it never touches the GPU), --workers
+          spawned GPU worker processes (all on GPU 0 on a one-GPU box) run the batches
+The BAMs are compared byte for byte.  Usage:
+  python profiles/e2e_stream.py [--families N] [--threads T] [--chunk-mb M] [--level L]
+                                [--modes stream,stream_fastq,whole,fleet] [--workers W]"""
 import argparse
 import json
 import os
@@ -42,9 +45,21 @@ def child(args):
     import torch  # noqa: F401  (the GPU runtime, as the CLI loads it)
 
     from bsseqconsensusreads_amd import bam
+    stats = {}
+    if args.mode == "fleet":  # the coordinator never touches the GPU: its workers do
+        from bsseqconsensusreads_amd import fleet
+        t0 = time.perf_counter()
+        info = fleet.step5_stream_multi(args.inp, args.fa, args.out, [0] * args.workers, threads=args.threads,
+                                        level=args.level, chunk_bytes=args.chunk_mb << 20, stats=stats)
+        dt = time.perf_counter() - t0
+        rss = resource.getrusage(resource.RUSAGE_SELF).ru_maxrss / 1024
+        crss = resource.getrusage(resource.RUSAGE_CHILDREN).ru_maxrss / 1024
+        print(json.dumps({"mode": args.mode, "workers": args.workers, "seconds": round(dt, 3),
+                          "peak_rss_MiB": round(rss, 1), "worker_peak_rss_MiB": round(crss, 1),
+                          "stage_busy_s": stats, **info}))
+        return 0
     from bsseqconsensusreads_amd.device import Engine
     eng = Engine(0)
-    stats = {}
     t0 = time.perf_counter()
     if args.mode == "whole":
         info = bam.step5(args.inp, args.fa, args.out, engine=eng, threads=args.threads, level=args.level)
@@ -69,6 +84,8 @@ def main():
     ap.add_argument("--chunk-mb", type=int, default=256)
     ap.add_argument("--level", type=int, default=5)
     ap.add_argument("--mode", default=None)
+    ap.add_argument("--modes", default="stream,stream_fastq,whole")
+    ap.add_argument("--workers", type=int, default=2)
     ap.add_argument("--inp")
     ap.add_argument("--fa")
     ap.add_argument("--out")
@@ -91,11 +108,12 @@ def main():
            "host_threads": a.threads, "level": a.level, "chunk_MiB": a.chunk_mb, "prep_s": round(prep, 1)}
     print("prepared", json.dumps(res), flush=True)
     outs = {}
-    for mode in ("stream", "stream_fastq", "whole"):
+    for mode in a.modes.split(","):
         out = os.path.join(d, mode + ".bam")
         p = subprocess.run([sys.executable, os.path.abspath(__file__), "--mode", mode, "--inp", inp, "--fa", fa,
                             "--out", out, "--threads", str(a.threads), "--chunk-mb", str(a.chunk_mb),
-                            "--level", str(a.level)], stdout=subprocess.PIPE, text=True, timeout=900)
+                            "--level", str(a.level), "--workers", str(a.workers)], stdout=subprocess.PIPE, text=True,
+                           timeout=900)
         if p.returncode != 0:
             print(p.stdout[-2000:], file=sys.stderr)
             return p.returncode
@@ -103,7 +121,9 @@ def main():
         r["families_per_s"] = round(a.families / r["seconds"], 1)
         res[mode] = r
         outs[mode] = out
-    res["outputs_identical"] = open(outs["stream"], "rb").read() == open(outs["whole"], "rb").read()
+        print(mode, json.dumps(r), flush=True)
+    bams = [open(outs[m], "rb").read() for m in outs if m != "stream_fastq"]
+    res["outputs_identical"] = all(b == bams[0] for b in bams)
     print(json.dumps(res))
     return 0
 

@@ -106,3 +106,28 @@ def near_tie_votes(raw, n_pos=6, seed=3, qlo=80, qhi=93, p_n=0.1):
                 seq[o] = alle[f, i, int(rng.integers(0, 2))]
                 qual[o] = int(rng.integers(qlo, qhi + 1))
     return dataclasses.replace(raw, seq=seq, qual=qual)
+
+
+def assert_bam_matches_oracle(out_bam, in_bam, fasta, what=""):
+    """The step-5 output BAM, record by record (R1, R2 per emitted family, TemplateCoordinate
+    order): name suffix, SEQ and QUAL against oracle/ on the whole input file."""
+    from bsseqconsensusreads_amd import bam
+    from oracle import oracle
+    _, whole = bam.read_bam(in_bam, threads=4)
+    ref = bam.read_fasta(fasta, bam.read_bam_header(in_bam))
+    r = oracle.run(whole, ref, threads=8)
+    em = np.nonzero(r.status == 1)[0]
+    _, out = bam.read_bam(out_bam, threads=4)
+    assert out.n == 2 * em.shape[0], "%s: %d records vs %d" % (what, out.n, 2 * em.shape[0])
+    for j, f in enumerate(em):
+        mi = whole.mi_names[int(r.fam_mi[f])]
+        mi = mi if isinstance(mi, bytes) else mi.encode()
+        for e in range(2):
+            k = 2 * j + e
+            n = int(r.cons_len[f, e])
+            ctx = "%s family %d end %d" % (what, f, e)
+            assert int(out.l_seq[k]) == n, ctx
+            assert np.array_equal(out.record_seq(k), r.cons_seq[f, e, :n]), ctx + ": SEQ"
+            assert np.array_equal(out.record_qual(k), r.cons_qual[f, e, :n]), ctx + ": QUAL"
+            assert out.qname(k).endswith(b":" + mi), ctx + ": name"
+    return int(out.n)

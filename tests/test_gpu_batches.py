@@ -115,45 +115,3 @@ def test_large_kernel_dump_vs_oracle_contig_ends(engine, monkeypatch):
     assert np.array_equal(t2.seq, ref.tool2.seq) and np.array_equal(t2.qual, ref.tool2.qual)
     assert np.array_equal(t2.cigar, ref.tool2.cigar)
     assert_consensus_equal(cons, ref, "k_large contig ends")
-
-
-def test_cli_step5_two_ranks_equal_one(tmp_path):
-    """`cli step5 --gpus 2` (two spawned ranks, here both on GPU 0 via --devices 0,0; tiny device
-    batches dealt round-robin, gathered on rank 0) writes the same BAM and FASTQ bytes as --gpus 1
-    (which streams the input in small chunks: --chunk-mb 0 cuts at every complete family)."""
-    import os
-    import subprocess
-    import sys
-
-    from bsseqconsensusreads_amd import bam
-
-    s = synth.generate("C2", 700, seed=23, device="cpu", genome_len=80_000)
-    raw = synth.messify(s.raw, frac=0.1, seed=2)
-    raw = R.take(raw, np.lexsort((raw.pos, raw.tid)))  # coordinate-sorted: --gpus 1 streams it
-    codes = R.unpack_nibbles(s.ref.packed, s.ref.n_nibbles)
-    fa = tmp_path / "g.fa"
-    fa.write_text(">%s\n%s\n" % (s.ref.names[0], R.NT16_TO_ASCII[codes].tobytes().decode()))
-    hdr = bam.BamHeader("@HD\tVN:1.6\tSO:coordinate\n@SQ\tSN:%s\tLN:%d\n@RG\tID:x\tLB:L1\n" % (
-        s.ref.names[0], len(codes)), [s.ref.names[0]], np.asarray([len(codes)], np.int64))
-    inp = str(tmp_path / "in.bam")
-    bam.write_bam(inp, hdr, bam.records_to_bam(raw))
-    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
-    env = {k: v for k, v in os.environ.items() if k not in ("WORLD_SIZE", "RANK", "LOCAL_RANK")}
-    env["PYTHONPATH"] = root + os.pathsep + env.get("PYTHONPATH", "")
-
-    def cli(tag, *extra):
-        cmd = [sys.executable, "-m", "bsseqconsensusreads_amd.cli", "step5", "--reference", str(fa), inp,
-               str(tmp_path / ("%s.bam" % tag)), "--fastq1", str(tmp_path / ("%s1.fq.gz" % tag)),
-               "--fastq2", str(tmp_path / ("%s2.fq.gz" % tag)), "--threads", "4", "--batch-bases", "15000"] + list(extra)
-        p = subprocess.run(cmd, env=env, capture_output=True, text=True, timeout=240)
-        assert p.returncode == 0, p.stderr[-3000:]
-
-    cli("one", "--chunk-mb", "0")
-    cli("two", "--gpus", "2", "--devices", "0,0")
-    for suffix in (".bam", "1.fq.gz", "2.fq.gz"):
-        a = (tmp_path / ("one" + suffix)).read_bytes()
-        b = (tmp_path / ("two" + suffix)).read_bytes()
-        assert a == b, suffix
-    _, out = bam.read_bam(str(tmp_path / "two.bam"))
-    ref = oracle.run(raw, s.ref)
-    assert out.n == 2 * int((ref.status == 1).sum())

@@ -5,7 +5,8 @@
   second step over the same resident batch writes the same bytes) and output invariants (bases
   A/C/G/T/N, quals in [1, 93], lengths bounded by the longest record + 1);
 - C3 (configs[2]): all 200K deep families (20-100 templates), same checks;
-- C4 (configs[3]): a 20K-family sample of the skewed model;
+- C4 (configs[3]): the 1M-family batch `bench.py --config C4` times, every family, and a
+  20K-family sample;
 - C5 (configs[4], per-GPU shape): a C2-shaped stream larger than one batch's 32-bit slot range,
   cut into bounded batches that run back to back on one GPU and are gathered in order -- what each
   rank of a 2/4/8-GPU run does with its share of the 100M families.
@@ -97,6 +98,19 @@ def test_c3_full_size_every_family(engine):
     del fb, a, b
     ref = oracle.run(s.raw, s.ref, threads=THREADS)
     live = _compare_all(cons, ref, "C3 200K")
+    _invariants(cons, live, int(s.raw.l_seq.max()) + 1)
+
+
+@pytest.mark.timeout(900)
+def test_c4_bench_batch_every_family(engine):
+    """bench.py --config C4's rank-0 input (1M skewed families, seed 42), through the step's own
+    batching (pipeline.run_step5: the fused launch, or the two-launch fallback if a tool-2 partner
+    straddles families), every family against oracle/."""
+    s = synth.generate("C4", 1_000_000, seed=42, device="cuda")
+    engine.load_reference(s.ref)
+    cons, _ = pipeline.run_step5(engine, s.raw)
+    ref = oracle.run(s.raw, s.ref, threads=THREADS)
+    live = _compare_all(cons, ref, "C4 1M")
     _invariants(cons, live, int(s.raw.l_seq.max()) + 1)
 
 

@@ -104,14 +104,15 @@ def test_missing_mi_raises(engine):
 
 @pytest.mark.parametrize("cfg", ["C0", "C1", "C2", "C3", "C4"])
 def test_synthetic_configs_vs_oracle(engine, cfg):
-    n = {"C0": 3000, "C1": 1500, "C2": 3000, "C3": 150, "C4": 1200}[cfg]
-    s = synth.generate(cfg, n, seed=11, device="cpu", genome_len=400_000)
+    # C1 at its stated size (BASELINE.json configs[0]: 10K families)
+    n = {"C0": 3000, "C1": 10_000, "C2": 3000, "C3": 150, "C4": 1200}[cfg]
+    s = synth.generate(cfg, n, seed=11, device="cpu", genome_len=2_000_000 if cfg == "C1" else 400_000)
     if cfg == "C4":  # the deep-set vote path (a strand/end set of more than 128 reads) is exercised
         fb = batch.build_family_batch(s.raw, "full", s.ref)
         assert np.diff(fb.fam_off.astype(np.int64)).max() > 600
     engine.load_reference(s.ref)
     cons, t2 = pipeline.run_step5(engine, s.raw, dump=True, tags=True)
-    ref = oracle.run(s.raw, s.ref)
+    ref = oracle.run(s.raw, s.ref, threads=8)
     assert_consensus_equal(cons, ref, cfg)
     assert_ss_equal(cons, ref, cfg)
     # the fused kernel's tool-2 state equals the restatement's tool-2 records

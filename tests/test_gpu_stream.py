@@ -1,11 +1,13 @@
 """The streaming, pipelined file-level step 5 (bam.step5_stream: bounded-memory reader, C++ family
 formation per chunk, GPU batches, streaming writer) writes the bytes the whole-file step 5
-(bam.step5) writes, on a coordinate-sorted synthetic BAM cut into many chunks."""
+(bam.step5) writes, on a coordinate-sorted synthetic BAM cut into many chunks, and those records
+are oracle/'s on the whole file, record by record."""
 import numpy as np
 import pytest
 
 from bsseqconsensusreads_amd import bam, synth
 from bsseqconsensusreads_amd import records as R
+from helpers import assert_bam_matches_oracle
 
 pytestmark = pytest.mark.gpu
 
@@ -38,3 +40,4 @@ def test_stream_writes_the_whole_file_bytes(engine, tmp_path, cfg, messy):
     for k in ("records_in", "families", "families_emitted", "records_out"):
         assert ia[k] == ib[k], k
     assert open(a, "rb").read() == open(b, "rb").read()
+    assert assert_bam_matches_oracle(b, inp, fa, "stream %s" % cfg) == ib["records_out"]
