@@ -182,7 +182,7 @@ def run(args):
     # the drop-in's default BAM output carries fgbio's per-base consensus tags (cli.py, main.snake.py:159):
     # the same resident batches with BSDC_MODE_TAGS, timed after the headline (C5 keeps no tag buffers)
     tags_ms = None
-    if all(r.db.tags for r in res):
+    if args.tags_leg and all(r.db.tags for r in res):
         e0.record(stream)
         for _ in range(ks):
             step(FULL_MODE | MODE_TAGS)
@@ -301,6 +301,8 @@ def parse(argv=None):
                     help="families for the all-cores CPU baseline (0 = skip)")
     ap.add_argument("--cpu-sample-1core", type=int, default=100_000, help="families for the 1-core CPU baseline")
     ap.add_argument("--seed", type=int, default=42)
+    ap.add_argument("--no-tags-leg", dest="tags_leg", action="store_false",
+                    help="skip the timed BSDC_MODE_TAGS leg (the PMC passes count the headline kernels only)")
     a = ap.parse_args(argv)
     if a.families is None:
         a.families = DEFAULT_FAMILIES.get(a.config, 1_000_000)

@@ -683,14 +683,12 @@ __device__ __forceinline__ void overlap_dw(uint8_t *bimg, uint8_t *qimg, uint32_
     const uint32_t sh = 8u * (uint32_t)lo;
     const Ovl4 o = ovl4_compute_m(
         Ovl4{lds32(bimg + A0), lds_any32(bimg, Bl) << sh, lds32(qimg + A0), lds_any32(qimg, Bl) << sh}, inm);
-    // a partial dword of a goes back byte by byte too: its other bytes may belong to the record
-    // before a (an extended record starts one byte before its slot), which another template's
-    // lanes may be writing in the same instruction
+    // a's dword goes back whole even when the overlap covers part of it: slots are 4-aligned and
+    // hold one record each (bsdc.h), so its other bytes are a's own, outside the overlap, and
+    // ovl4_compute_m returns them as loaded; no other lane writes them in this phase
     const bool whole = inm == 0xFFFFFFFFu;
-    if (whole) {
-        st32(bimg + A0, o.x);
-        st32(qimg + A0, o.qa);
-    }
+    st32(bimg + A0, o.x);
+    st32(qimg + A0, o.qa);
     if (whole && (B0 & 3) == 0) {
         st32(bimg + B0, o.y);
         st32(qimg + B0, o.qb);
@@ -699,12 +697,8 @@ __device__ __forceinline__ void overlap_dw(uint8_t *bimg, uint8_t *qimg, uint32_
         stu32(bimg + B0, o.y);
         stu32(qimg + B0, o.qb);
 #endif
-    } else {
+    } else {  // b's partial dword: bytes (b's bytes just outside the overlap may precede b's slot)
         for (int k = lo; k < hi; k++) {
-            if (!whole) {
-                bimg[A0 + k] = (uint8_t)(o.x >> (8 * k));
-                qimg[A0 + k] = (uint8_t)(o.qa >> (8 * k));
-            }
             bimg[B0 + k] = (uint8_t)(o.y >> (8 * k));
             qimg[B0 + k] = (uint8_t)(o.qb >> (8 * k));
         }
@@ -738,11 +732,9 @@ __device__ __forceinline__ OvlDw ovl_dw_load(const uint8_t *bimg, const uint8_t 
 __device__ __forceinline__ void ovl_dw_store(uint8_t *bimg, uint8_t *qimg, const OvlDw &t) {
     if (t.hi <= t.lo) return;
     const Ovl4 o = ovl4_compute_m(t.in, t.inm);
-    const bool whole = t.inm == 0xFFFFFFFFu;  // (as overlap_dw)
-    if (whole) {
-        st32(bimg + t.A0, o.x);
-        st32(qimg + t.A0, o.qa);
-    }
+    const bool whole = t.inm == 0xFFFFFFFFu;  // (as overlap_dw: a's dword goes back whole)
+    st32(bimg + t.A0, o.x);
+    st32(qimg + t.A0, o.qa);
     if (whole && (t.B0 & 3) == 0) {
         st32(bimg + t.B0, o.y);
         st32(qimg + t.B0, o.qb);
@@ -766,10 +758,6 @@ __device__ __forceinline__ void ovl_dw_store(uint8_t *bimg, uint8_t *qimg, const
 #endif
     } else {
         for (int k = t.lo; k < t.hi; k++) {
-            if (!whole) {
-                bimg[t.A0 + k] = (uint8_t)(o.x >> (8 * k));
-                qimg[t.A0 + k] = (uint8_t)(o.qa >> (8 * k));
-            }
             bimg[t.B0 + k] = (uint8_t)(o.y >> (8 * k));
             qimg[t.B0 + k] = (uint8_t)(o.qb >> (8 * k));
         }

@@ -19,7 +19,10 @@ for f in sorted(glob.glob(d + "/p*/**/*counter_collection.csv", recursive=True))
 grouped = collections.defaultdict(dict)
 for k, disp in per.items():
     m = re.search(r"(k_small|k_large)", k)
-    grouped[m.group(1) if m else k[:60]].update({(k,) + key: v for key, v in disp.items()})
+    name = m.group(1) if m else k[:60]
+    if name == "k_small" and "<true>" in k:  # the consensus-tag instance (BSDC_MODE_TAGS) on its own
+        name = "k_small_tags"
+    grouped[name].update({(k,) + key: v for key, v in disp.items()})
 out = {}
 for name, disp in grouped.items():
     sums = collections.defaultdict(float)

@@ -8,7 +8,8 @@ import sys
 d = sys.argv[1]
 PH = ["launch", "tables", "staging", "convert", "extend", "overlap", "srcreads+lists", "vote-preamble", "vote-main", "vote-queue", "full"]
 if len(sys.argv) > 2 and sys.argv[2] == "large":  # profiles/ablate.py LARGE_PHASES
-    PH = ["launch", "tables", "staging", "convert", "extend", "overlap", "srcreads", "filter+lists", "vote", "full"]
+    PH = ["launch", "tables", "staging", "convert", "extend", "overlap-wild", "overlap-templates", "overlap", "srcreads",
+          "filter+lists", "vote-sums", "vote", "full"]
 RUNS = 12  # 2 warmup + 10 timed per phase
 res = collections.defaultdict(lambda: collections.defaultdict(float))
 for f in sorted(glob.glob(d + "/p*/**/*counter_collection.csv", recursive=True)):

@@ -8,7 +8,7 @@ R=$(pwd)
 OUT="$R/gpurun_out/$TAG"
 mkdir -p "$OUT"
 export TMPDIR=/tmp
-for c in C2 C3; do
+for c in ${CONFIGS:-C2 C3}; do
   echo "[$(date +%T)] stats $c"
   (cd /tmp && timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d "$OUT/prof_$c" -o bench -- \
       python3 "$R/bench.py" --config $c --steps 20 --cpu-sample 0 --cpu-sample-1core 0 > "$OUT/prof_$c.log" 2>&1) \
@@ -18,7 +18,7 @@ for c in C2 C3; do
   # launch-set spans (the side streams overlap a set's dispatches: DESIGN.md 5.4)
   python profiles/trace_span.py "$(find "$OUT/prof_$c" -name '*kernel_trace.csv' | head -1)" "$OUT/prof_$c.log" "$OUT/span_$c.json" || exit 1
 done
-for c in C2 C3; do
+for c in ${CONFIGS:-C2 C3}; do
   echo "[$(date +%T)] pmc $c"
   bash profiles/collect_pmc.sh "$OUT/pmc_$c" --config $c || exit 1
   python profiles/pmc_bench_summary.py "$OUT/pmc_$c" "$OUT/pmc_$c.json" > /dev/null || exit 1
