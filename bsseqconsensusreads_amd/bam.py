@@ -30,7 +30,7 @@ from . import records as R
 
 IO_LIB_PATH = os.environ.get("BSDC_IO_LIB_PATH") or os.path.join(os.path.dirname(os.path.abspath(__file__)),
                                                                  "libbsdc_io.so")
-BSDC_IO_ABI_VERSION = 4
+BSDC_IO_ABI_VERSION = 5
 _P = C.c_void_p
 
 
@@ -50,7 +50,7 @@ class _Arrays(C.Structure):
 class _Records(C.Structure):
     _fields_ = [("n_rec", C.c_int64)] + [(k, _P) for k in (
         "flag", "tid", "pos", "mapq", "next_tid", "next_pos", "tlen", "name_off", "name_buf", "cig_off", "cigar",
-        "seq_off", "seq", "qual", "aux_off", "aux")]
+        "seq_off", "seq", "qual", "aux_off", "aux", "aux2_off", "aux2")]
 
 
 _lib = None
@@ -62,7 +62,7 @@ def _load():
         return _lib
     if not os.path.exists(IO_LIB_PATH):
         raise RuntimeError("%s is missing: run __graft_entry__.build()" % IO_LIB_PATH)
-    lib = C.CDLL(IO_LIB_PATH)
+    lib = C.CDLL(IO_LIB_PATH)  # (OMP_WAIT_POLICY: see the package __init__)
     lib.bsdc_io_abi_version.restype = C.c_int32
     lib.bsdc_io_last_error.restype = C.c_char_p
     lib.bsdc_bam_read.argtypes = [C.c_char_p, C.c_int32, C.POINTER(_P)]
@@ -75,6 +75,10 @@ def _load():
     lib.bsdc_bam_stream_open.restype = C.c_int32
     lib.bsdc_bam_stream_next.argtypes = [_P, C.c_int64, C.c_int64, C.POINTER(_P)]
     lib.bsdc_bam_stream_next.restype = C.c_int32
+    lib.bsdc_bam_stream_next_raw.argtypes = [_P, C.c_int64, C.c_int64, C.POINTER(_P)]
+    lib.bsdc_bam_stream_next_raw.restype = C.c_int32
+    lib.bsdc_bam_parse.argtypes = [_P, C.c_int32]
+    lib.bsdc_bam_parse.restype = C.c_int32
     lib.bsdc_bam_stream_close.argtypes = [_P]
     lib.bsdc_bam_stream_recycle.argtypes = [_P, _P]
     lib.bsdc_bam_stream_recycle.restype = None
@@ -251,11 +255,36 @@ def read_bam_header(path: str) -> BamHeader:
         lib.bsdc_bam_stream_close(st)
 
 
-def stream_bam(path: str, threads: int = 0, chunk_bytes: int = DEFAULT_CHUNK_BYTES, slack: int = DEFAULT_SLACK,
-               read_size: int = 8 << 20):
-    """Chunks of a coordinate-sorted BAM in bounded memory: yields (BamHeader, RawRecords) per chunk,
-    cut where no template or MI family straddles two chunks (include/bsdc_io.h,
-    bsdc_bam_stream_next); names and MI ids are chunk-local."""
+class StreamChunk:
+    """A chunk cut from a BAM stream but not yet decoded (bsdc_bam_stream_next_raw).  decode()
+    parses it and copies it out (any thread: the stream meanwhile cuts the next chunk); discard()
+    drops it.  Either returns its buffer to the stream; exactly one of them must be called."""
+
+    def __init__(self, lib, st, h, path: str):
+        self._lib, self._st, self._h, self._path = lib, st, h, path
+
+    def decode(self, threads: int = 0):
+        """-> (BamHeader, RawRecords)"""
+        lib, h = self._lib, self._h
+        self._h = None
+        try:
+            if lib.bsdc_bam_parse(h, int(threads)) != 0:
+                raise OSError("%s: %s" % (self._path, lib.bsdc_io_last_error().decode()))
+            return _decode(lib, h, self._path)
+        finally:
+            lib.bsdc_bam_stream_recycle(self._st, h)
+
+    def discard(self):
+        if self._h is not None:
+            h, self._h = self._h, None
+            self._lib.bsdc_bam_stream_recycle(self._st, h)
+
+
+def stream_chunks(path: str, threads: int = 0, chunk_bytes: int = DEFAULT_CHUNK_BYTES, slack: int = DEFAULT_SLACK,
+                  read_size: int = 8 << 20):
+    """The chunks of a coordinate-sorted BAM in bounded memory, undecoded (StreamChunk): cut where no
+    template or MI family straddles two chunks (include/bsdc_io.h, bsdc_bam_stream_next_raw).  The
+    stream itself is freed once it is exhausted and every chunk has been decoded or discarded."""
     lib = _load()
     st = _P()
     rc = lib.bsdc_bam_stream_open(path.encode(), int(threads), int(read_size), C.byref(st))
@@ -264,18 +293,23 @@ def stream_bam(path: str, threads: int = 0, chunk_bytes: int = DEFAULT_CHUNK_BYT
     try:
         while True:
             h = _P()
-            rc = lib.bsdc_bam_stream_next(st, int(chunk_bytes), int(slack), C.byref(h))
+            rc = lib.bsdc_bam_stream_next_raw(st, int(chunk_bytes), int(slack), C.byref(h))
             if rc != 0:
                 raise OSError("%s: %s" % (path, lib.bsdc_io_last_error().decode()))
             if not h:
                 return
-            try:
-                hdr, raw = _decode(lib, h, path)
-            finally:
-                lib.bsdc_bam_stream_recycle(st, h)
-            yield hdr, raw
+            yield StreamChunk(lib, st, h, path)
     finally:
         lib.bsdc_bam_stream_close(st)
+
+
+def stream_bam(path: str, threads: int = 0, chunk_bytes: int = DEFAULT_CHUNK_BYTES, slack: int = DEFAULT_SLACK,
+               read_size: int = 8 << 20):
+    """Chunks of a coordinate-sorted BAM in bounded memory: yields (BamHeader, RawRecords) per chunk,
+    cut where no template or MI family straddles two chunks (include/bsdc_io.h,
+    bsdc_bam_stream_next); names and MI ids are chunk-local."""
+    for c in stream_chunks(path, threads, chunk_bytes, slack, read_size):
+        yield c.decode(threads)
 
 
 def _aux_table(raw: R.RawRecords) -> StringTable:
@@ -304,6 +338,7 @@ class OutRecordsBam:
     seq: np.ndarray         # nt16 codes
     qual: np.ndarray
     aux: StringTable
+    aux2: Optional[StringTable] = None  # more aux bytes written after aux (the consensus tags)
 
     @property
     def n(self) -> int:
@@ -404,7 +439,8 @@ def take_records(recs: "OutRecordsBam", idx: np.ndarray) -> "OutRecordsBam":
     return OutRecordsBam(flag=recs.flag[idx], tid=recs.tid[idx], pos=recs.pos[idx], mapq=recs.mapq[idx],
                          next_tid=recs.next_tid[idx], next_pos=recs.next_pos[idx], tlen=recs.tlen[idx],
                          names=_take_table(recs.names, idx), cig_off=co, cigar=cig, seq_off=so, seq=seq, qual=qual,
-                         aux=_take_table(recs.aux, idx))
+                         aux=_take_table(recs.aux, idx),
+                         aux2=_take_table(recs.aux2, idx) if recs.aux2 is not None else None)
 
 
 def _synthetic_fields(raw: R.RawRecords):
@@ -475,7 +511,9 @@ def _records_struct(recs: OutRecordsBam, keep: list) -> _Records:
                     c(recs.tlen, np.int32), c(recs.names.off, np.int64), c(recs.names.buf, np.uint8),
                     c(recs.cig_off, np.int64), c(recs.cigar, np.uint32), c(recs.seq_off, np.int64),
                     c(recs.seq, np.uint8), c(recs.qual, np.uint8), c(recs.aux.off, np.int64),
-                    c(recs.aux.buf, np.uint8))
+                    c(recs.aux.buf, np.uint8),
+                    c(recs.aux2.off, np.int64) if recs.aux2 is not None else None,
+                    c(recs.aux2.buf, np.uint8) if recs.aux2 is not None else None)
 
 
 def family_image(src_off, length, dst_off, seq, qual, n_slots: int, packed: np.ndarray, qual_out: np.ndarray,
@@ -661,7 +699,7 @@ def consensus_tags(cons, em: np.ndarray, molecular: bool = False, threads: int =
     args = (n, _ptr(row_a), _ptr(row_b), _ptr(out_len), 1 if molecular else 0, stride, _ptr(base), _ptr(qual),
             _ptr(depth), _ptr(err), _ptr(off))
     total = lib.bsdc_consensus_tags(*args, None, int(threads))
-    buf = np.zeros(max(int(total), 1), np.uint8)
+    buf = np.empty(max(int(total), 1), np.uint8)
     lib.bsdc_consensus_tags(*args, _ptr(buf), int(threads))
     return StringTable(buf[:int(total)], off)
 
@@ -711,9 +749,7 @@ def duplex_records(cons, raw: R.RawRecords, prefix: str, threads: int = 0, molec
     fam_names = _concat_fields([prefix.encode() + b":", mi], F)
     two = np.repeat(np.arange(F, dtype=np.int64), 2)
     names_t, auxs_t = _take_table(fam_names, two), _take_table(fam_aux, two)
-    if getattr(cons, "ss", None) is not None:
-        tg = consensus_tags(cons, em, molecular, threads)
-        auxs_t = _concat_fields([(auxs_t.buf, auxs_t.off), (tg.buf, tg.off)], n)
+    tg = consensus_tags(cons, em, molecular, threads) if getattr(cons, "ss", None) is not None else None
     L = np.ascontiguousarray(cons.length[em].reshape(-1), np.int32)  # R1, R2, R1, R2 ...
     seq_off = np.zeros(n + 1, np.int64)
     seq_off[1:] = np.cumsum(L)
@@ -730,7 +766,7 @@ def duplex_records(cons, raw: R.RawRecords, prefix: str, threads: int = 0, molec
         flag=np.tile(np.asarray([77, 141], np.uint16), F), tid=np.full(n, -1, np.int32), pos=np.full(n, -1, np.int32),
         mapq=np.zeros(n, np.uint8), next_tid=np.full(n, -1, np.int32), next_pos=np.full(n, -1, np.int32),
         tlen=np.zeros(n, np.int32), names=names_t, cig_off=np.zeros(n + 1, np.int64),
-        cigar=np.zeros(0, np.uint32), seq_off=seq_off, seq=seq, qual=qual, aux=auxs_t)
+        cigar=np.zeros(0, np.uint32), seq_off=seq_off, seq=seq, qual=qual, aux=auxs_t, aux2=tg)
 
 
 def consensus_sharded(eng, raw: R.RawRecords, tags: bool, batch_bases: Optional[int] = None, dist=None):
@@ -807,52 +843,64 @@ def step5_stream(in_bam: str, fasta: str, out_bam: Optional[str], engine=None, p
     outs: "queue.Queue" = queue.Queue(maxsize=1)
     err: list = []
     info = {"records_in": 0, "families": 0, "families_emitted": 0, "records_out": 0, "chunks": 0}
-    T = {"decode": 0.0, "plan": 0.0, "gpu": 0.0, "records": 0.0, "encode": 0.0, "gpu_wait": 0.0, "writer_wait": 0.0}
+    T = {"decode": 0.0, "parse": 0.0, "plan": 0.0, "gpu": 0.0, "records": 0.0, "encode": 0.0, "gpu_wait": 0.0,
+         "writer_wait": 0.0}
     first = {}
     stop = threading.Event()  # set on any failure: the decoder and planner stop at their next chunk
 
     raws: "queue.Queue" = queue.Queue(maxsize=1)
 
-    def decoder():  # the next chunk decodes while the previous one's families form
+    def decoder():  # cuts the next chunk (inflate, split, family-complete selection) while the
+        # reader thread decodes and plans the one before
+        it = None
         try:
-            it = stream_bam(in_bam, threads, chunk_bytes, slack)
+            it = stream_chunks(in_bam, threads, chunk_bytes, slack)
             while not stop.is_set():
                 t0 = time.perf_counter()
                 nxt = next(it, None)
                 T["decode"] += time.perf_counter() - t0
                 if nxt is None:
                     break
-                raws.put(nxt[1])
+                raws.put(nxt)
         except BaseException as e:  # noqa: BLE001 -- handed to the main thread
             err.append(e)
             stop.set()
         finally:
+            if it is not None:
+                it.close()  # (the stream is freed once every chunk is back)
             raws.put(None)
 
     def reader():
         try:
             while True:
-                raw = raws.get()
-                if raw is None:
+                ch = raws.get()
+                if ch is None:
                     break
                 if stop.is_set():
+                    ch.discard()
                     continue  # drain to the decoder's None without planning
                 t0 = time.perf_counter()
+                raw = ch.decode(threads)[1]
+                t1 = time.perf_counter()
                 plan = pipeline.plan_families(raw, "full", first["ref"])
-                T["plan"] += time.perf_counter() - t0
+                T["parse"] += t1 - t0
+                T["plan"] += time.perf_counter() - t1
                 chunks.put((raw, plan))
         except BaseException as e:  # noqa: BLE001 -- handed to the main thread
             err.append(e)
             stop.set()
-            while raws.get() is not None:  # let the decoder finish
-                pass
+            while True:  # let the decoder finish
+                ch = raws.get()
+                if ch is None:
+                    break
+                ch.discard()
         finally:
             chunks.put(None)
 
-    def writer():
+    recq: "queue.Queue" = queue.Queue(maxsize=1)  # built records -> encoder
+
+    def builder():  # the output records of a chunk, while the encoder compresses the one before
         try:
-            w = BamWriter(out_bam, output_header(first["header"]), level) if out_bam is not None else None
-            fq = FastqWriter(fastq[0], fastq[1], level) if fastq is not None else None
             while True:
                 t0 = time.perf_counter()
                 item = outs.get()
@@ -862,13 +910,30 @@ def step5_stream(in_bam: str, fasta: str, out_bam: Optional[str], engine=None, p
                 cons, raw = item
                 t0 = time.perf_counter()
                 recs = duplex_records(cons, raw, first["prefix"], threads)
+                T["records"] += time.perf_counter() - t0
+                recq.put(recs)
+        except BaseException as e:  # noqa: BLE001
+            err.append(e)
+            stop.set()
+            while outs.get() is not None:  # drain so the main thread never blocks
+                pass
+        finally:
+            recq.put(None)
+
+    def writer():
+        try:
+            w = BamWriter(out_bam, output_header(first["header"]), level) if out_bam is not None else None
+            fq = FastqWriter(fastq[0], fastq[1], level) if fastq is not None else None
+            while True:
+                recs = recq.get()
+                if recs is None:
+                    break
                 t1 = time.perf_counter()
                 if w is not None:
                     w.add(recs, threads)
                 if fq is not None:
                     fq.add(recs, threads)
                 info["records_out"] += recs.n
-                T["records"] += t1 - t0
                 T["encode"] += time.perf_counter() - t1
             if w is not None:
                 w.close(threads)
@@ -877,7 +942,7 @@ def step5_stream(in_bam: str, fasta: str, out_bam: Optional[str], engine=None, p
         except BaseException as e:  # noqa: BLE001
             err.append(e)
             stop.set()
-            while outs.get() is not None:  # drain so the main thread never blocks
+            while recq.get() is not None:  # drain so the builder never blocks
                 pass
 
     # the header and the reference come first: the plan of a chunk needs the reference
@@ -890,9 +955,11 @@ def step5_stream(in_bam: str, fasta: str, out_bam: Optional[str], engine=None, p
         eng.load_reference(ref)
         td = threading.Thread(target=decoder, daemon=True)
         tr = threading.Thread(target=reader, daemon=True)
+        tb = threading.Thread(target=builder, daemon=True)
         tw = threading.Thread(target=writer, daemon=True)
         td.start()
         tr.start()
+        tb.start()
         tw.start()
         mode = pipeline.MODE_CONVERT | pipeline.MODE_EXTEND | pipeline.MODE_VOTE
         drained = False
@@ -929,6 +996,7 @@ def step5_stream(in_bam: str, fasta: str, out_bam: Optional[str], engine=None, p
                 while chunks.get() is not None:
                     pass
             outs.put(None)
+            tb.join()
             tw.join()
             tr.join()
             td.join()

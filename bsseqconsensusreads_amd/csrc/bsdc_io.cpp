@@ -19,10 +19,33 @@
 #include <string>
 #include <string_view>
 #include <unordered_map>
+#include <mutex>
 #include <vector>
 #ifdef _OPENMP
 #include <omp.h>
 #include <parallel/algorithm>
+
+// Byte buffers that grow without zero-filling: every byte is written before it is read (inflate,
+// record encode, deflate slots), and value-initialising gigabytes per chunk was serial memset time
+template <class T>
+struct NoInit : std::allocator<T> {
+    template <class U>
+    struct rebind {
+        using other = NoInit<U>;
+    };
+    NoInit() = default;
+    template <class U>
+    NoInit(const NoInit<U> &) {}
+    template <class U>
+    void construct(U *p) noexcept {
+        ::new (static_cast<void *>(p)) U;
+    }
+    template <class U, class... A>
+    void construct(U *p, A &&...a) {
+        ::new (static_cast<void *>(p)) U(std::forward<A>(a)...);
+    }
+};
+using Bytes = std::vector<uint8_t, NoInit<uint8_t>>;
 #endif
 
 namespace {
@@ -254,7 +277,7 @@ static void intern(const std::vector<std::string_view> &keys, const std::vector<
 }
 
 struct bsdc_bam {
-    std::vector<uint8_t> data;  // the uncompressed stream
+    Bytes data;  // the uncompressed stream
     std::string header;
     std::vector<std::string> ref_names;
     std::vector<int64_t> ref_len;
@@ -267,6 +290,8 @@ struct bsdc_bam {
     std::vector<int64_t> mc_tag_off;  // offset of the MC string in data, -1 = none
     std::vector<int32_t> mc_n;
     int64_t n_bases = 0, n_cigar = 0, n_mc = 0, aux_bytes = 0;
+    int64_t dn = 0;       // record bytes in data (a stream chunk before bsdc_bam_parse)
+    bool parsed = true;   // false: a raw stream chunk (bsdc_bam_stream_next_raw)
 };
 
 extern "C" {
@@ -281,7 +306,7 @@ namespace {
 // Whole BGZF blocks of comp[0, n) inflated (in parallel) and appended to `out`; *used = the bytes
 // of the whole blocks (a trailing partial block is left for the caller unless `final`, where it
 // is an error).  Every block is CRC-checked.
-int32_t inflate_blocks(const uint8_t *comp, int64_t n, bool final, std::vector<uint8_t> &out, int64_t *used) {
+int32_t inflate_blocks(const uint8_t *comp, int64_t n, bool final, Bytes &out, int64_t *used) {
     std::vector<int64_t> boff, bsz, uoff;
     int64_t o = 0, u = (int64_t)out.size();
     *used = 0;
@@ -474,7 +499,7 @@ int32_t bsdc_bam_read(const char *path, int32_t n_threads, bsdc_bam **out) {
     set_threads(n_threads);
     FILE *f = fopen(path, "rb");
     if (!f) return fail(BSDC_IO_EIO, std::string("cannot open ") + path);
-    std::vector<uint8_t> comp;
+    Bytes comp;
     {
         fseek(f, 0, SEEK_END);
         const long sz = ftell(f);
@@ -492,6 +517,7 @@ int32_t bsdc_bam_read(const char *path, int32_t n_threads, bsdc_bam **out) {
     const int64_t dn = (int64_t)b->data.size();
     if (rc == 0) rc = parse_header(b->data.data(), dn, b, &p);
     b->data.resize((size_t)dn + 8);
+    memset(b->data.data() + dn, 0, 8);  // the pad (a no-init buffer)
     if (rc == 0) rc = parse_records(b, p, dn);
     if (rc != 0) {
         delete b;
@@ -531,16 +557,16 @@ struct StreamFam {
 struct bsdc_bam_stream {
     FILE *f = nullptr;
     bsdc_bam hdr;                 // header text and references only
-    std::vector<uint8_t> comp;    // compressed bytes read but not yet inflated (a partial block)
+    Bytes comp;    // compressed bytes read but not yet inflated (a partial block)
     // buf = [buffered records (recs) | inflated bytes not yet split, from `tail`]; inflated blocks
     // land at its end and records are split in place (no copy); `spare` keeps the capacity the
     // kept records move to when a chunk goes out
     int64_t tail = 0;
-    std::vector<uint8_t> spare;
+    Bytes spare;
     bool eof = false;
     int64_t read_size = 0;
     // buffered records (file order) and their families
-    std::vector<uint8_t> buf;
+    Bytes buf;
     std::vector<StreamRec> recs;
     // hash of the MI base -> family, in kFamShards shards by the hash's top bits (the shards are
     // filled in parallel, one thread each)
@@ -552,6 +578,13 @@ struct bsdc_bam_stream {
     int64_t cursor = INT64_MIN;  // the last record's position
     int64_t par_min = 1 << 14;   // records per split from which families are assigned in parallel
     double prof[5] = {0, 0, 0, 0, 0};  // seconds: fill, split, select, emit, parse (BSDC_STREAM_PROF)
+    // chunks handed out and not yet recycled, and their buffers coming back: a chunk may be parsed
+    // and copied out on another thread while this one reads the next (bsdc_bam_stream_next_raw);
+    // the stream is deleted once it is closed and every chunk is back
+    std::mutex mu;
+    std::vector<Bytes> pool;  // returned chunk buffers (at most 2 kept)
+    int64_t outstanding = 0;
+    bool closed = false;
 };
 
 int32_t bsdc_bam_stream_open(const char *path, int32_t n_threads, int64_t read_size, bsdc_bam_stream **out) {
@@ -912,13 +945,21 @@ int32_t stream_split(bsdc_bam_stream *s) {
 // klo_m - kKeyDelta of the incomplete families and of the complete ones kept back; a complete
 // family goes out when khi_m + kKeyDelta < T.  (Templates whose mate is on another contig or unmapped sort after every
 // template of their contig with both ends on it, so they wait for the contig's end.)
-int32_t bsdc_bam_stream_next(bsdc_bam_stream *s, int64_t min_bytes, int64_t slack, bsdc_bam **out) {
+int32_t bsdc_bam_stream_next_raw(bsdc_bam_stream *s, int64_t min_bytes, int64_t slack, bsdc_bam **out) {
     *out = nullptr;
     std::vector<uint8_t> take;  // per buffered family: goes out now
     // room for a chunk, what stays behind and the fills in flight, reserved once (no regrowth,
-    // no fresh pages per fill)
+    // no fresh pages per fill); a recycled chunk buffer serves when one is back
     const size_t want = (size_t)std::max<int64_t>(min_bytes, 0) * 5 / 4 + (size_t)s->read_size * 16;
     if (s->buf.capacity() < want) s->buf.reserve(want);
+    if (s->spare.capacity() < want) {
+        std::lock_guard<std::mutex> lk(s->mu);
+        for (auto &v : s->pool)
+            if (v.capacity() >= want) {
+                s->spare.swap(v);
+                break;
+            }
+    }
     if (s->spare.capacity() < want) s->spare.reserve(want);
     for (;;) {
         double t0 = now_s();
@@ -1016,6 +1057,7 @@ int32_t bsdc_bam_stream_next(bsdc_bam_stream *s, int64_t min_bytes, int64_t slac
             const int64_t dn = (int64_t)s->buf.size();
             b->data.swap(s->buf);
             b->data.resize((size_t)dn + 8);
+    memset(b->data.data() + dn, 0, 8);  // the pad (a no-init buffer)
             for (size_t m = 0; m < s->fams.size(); m++)
                 if (take[m]) {
                     s->fams[m].n = 0;
@@ -1033,13 +1075,12 @@ int32_t bsdc_bam_stream_next(bsdc_bam_stream *s, int64_t min_bytes, int64_t slac
             s->tail = ok;
             s->recs.swap(krecs);
             s->prof[3] += now_s() - t0;
-            t0 = now_s();
-            rc = parse_records(b, 0, dn);
-            if (rc != 0) {
-                delete b;
-                return rc;
+            b->dn = dn;
+            b->parsed = false;
+            {
+                std::lock_guard<std::mutex> lk(s->mu);
+                s->outstanding++;
             }
-            s->prof[4] += now_s() - t0;
             *out = b;
             return 0;
         }
@@ -1049,12 +1090,49 @@ int32_t bsdc_bam_stream_next(bsdc_bam_stream *s, int64_t min_bytes, int64_t slac
     }
 }
 
+// Parses a raw chunk (records, tags, interned names and MI bases); a no-op for a parsed one.
+int32_t bsdc_bam_parse(bsdc_bam *b, int32_t n_threads) {
+    if (b->parsed) return 0;
+    set_threads(n_threads);
+    const int32_t rc = parse_records(b, 0, b->dn);
+    if (rc == 0) b->parsed = true;
+    return rc;
+}
+
+int32_t bsdc_bam_stream_next(bsdc_bam_stream *s, int64_t min_bytes, int64_t slack, bsdc_bam **out) {
+    const int32_t rc = bsdc_bam_stream_next_raw(s, min_bytes, slack, out);
+    if (rc != 0 || *out == nullptr) return rc;
+    const double t0 = now_s();
+    const int32_t pc = parse_records(*out, 0, (*out)->dn);
+    s->prof[4] += now_s() - t0;
+    if (pc != 0) {
+        bsdc_bam_stream_recycle(s, *out);
+        *out = nullptr;
+        return pc;
+    }
+    (*out)->parsed = true;
+    return 0;
+}
+
 void bsdc_bam_stream_recycle(bsdc_bam_stream *s, bsdc_bam *b) {
-    if (s && b && s->spare.capacity() < b->data.capacity()) {
-        s->spare.swap(b->data);
-        s->spare.clear();
+    if (!s) {
+        delete b;
+        return;
+    }
+    bool last = false;
+    {
+        std::lock_guard<std::mutex> lk(s->mu);
+        if (b) {
+            if (s->pool.size() < 2 && b->data.capacity() > 0) {
+                b->data.clear();
+                s->pool.push_back(std::move(b->data));
+            }
+            s->outstanding--;
+        }
+        last = s->closed && s->outstanding == 0;
     }
     delete b;
+    if (last) delete s;
 }
 
 // The stream's header and references as a record-less bsdc_bam.
@@ -1063,7 +1141,7 @@ int32_t bsdc_bam_stream_header(const bsdc_bam_stream *s, bsdc_bam **out) {
     b->header = s->hdr.header;
     b->ref_names = s->hdr.ref_names;
     b->ref_len = s->hdr.ref_len;
-    b->data.resize(8);
+    b->data.assign(8, 0);
     *out = b;
     return 0;
 }
@@ -1071,10 +1149,17 @@ int32_t bsdc_bam_stream_header(const bsdc_bam_stream *s, bsdc_bam **out) {
 void bsdc_bam_stream_close(bsdc_bam_stream *s) {
     if (!s) return;
     if (s->f) fclose(s->f);
+    s->f = nullptr;
     if (getenv("BSDC_STREAM_PROF"))
         fprintf(stderr, "bsdc stream s: fill %.3f split %.3f select %.3f emit %.3f parse %.3f\n", s->prof[0], s->prof[1],
                 s->prof[2], s->prof[3], s->prof[4]);
-    delete s;
+    bool last;
+    {
+        std::lock_guard<std::mutex> lk(s->mu);
+        s->closed = true;
+        last = s->outstanding == 0;
+    }
+    if (last) delete s;  // else the last bsdc_bam_stream_recycle deletes it
 }
 
 void bsdc_bam_sizes_of(const bsdc_bam *b, bsdc_bam_sizes *s) {
@@ -1094,6 +1179,7 @@ void bsdc_bam_sizes_of(const bsdc_bam *b, bsdc_bam_sizes *s) {
 }
 
 int32_t bsdc_bam_copy(const bsdc_bam *b, const bsdc_bam_arrays *a) {
+    if (!b->parsed) return fail(BSDC_IO_EFORMAT, "stream chunk not parsed (bsdc_bam_parse)");
     const int64_t nr = (int64_t)b->rec_start.size();
     const uint8_t *d = b->data.data();
     // running offsets (sequential prefix sums)
@@ -1209,39 +1295,41 @@ constexpr int64_t kBlock = 0xff00;  // uncompressed bytes per BGZF block (htslib
 // in parallel and written to f.
 int32_t deflate_write(FILE *f, const uint8_t *src0, int64_t total, int32_t level) {
     const int64_t nb = (total + kBlock - 1) / kBlock;
-    std::vector<std::vector<uint8_t>> blocks((size_t)nb);
+    // each block compresses into its own 64 KiB slot of one buffer (BSIZE <= 65536 by format)
+    Bytes slots((size_t)std::max<int64_t>(nb, 1) << 16);
+    std::vector<int32_t> bsz((size_t)std::max<int64_t>(nb, 1));
     int bad = 0;
 #pragma omp parallel for schedule(dynamic, 4) reduction(| : bad)
     for (int64_t i = 0; i < nb; i++) {
         const uint8_t *src = src0 + i * kBlock;
         const int64_t len = std::min(kBlock, total - i * kBlock);
-        std::vector<uint8_t> &o = blocks[(size_t)i];
-        o.resize(18 + (size_t)compressBound((uLong)len) + 8 + 64);
-        // a block that does not shrink to fit BSIZE (incompressible) is stored (level 0)
-        int64_t clen = raw_deflate(src, len, level, o.data() + 18, 65536 - 26);
-        if (clen <= 0) clen = raw_deflate(src, len, 0, o.data() + 18, (int64_t)o.size() - 26);
+        uint8_t *h = slots.data() + ((size_t)i << 16);
+        // a block that does not shrink to fit BSIZE (incompressible) is stored (level 0; a stored
+        // 0xff00-byte block is 0xff05 bytes of deflate, inside the slot)
+        int64_t clen = raw_deflate(src, len, level, h + 18, 65536 - 26);
+        if (clen <= 0) clen = raw_deflate(src, len, 0, h + 18, 65536 - 26);
         if (clen <= 0 || 18 + clen + 8 > 65536) {
             bad |= 1;
             continue;
         }
         const int64_t bsize = 18 + clen + 8;
-        uint8_t *h = o.data();
         const uint8_t hdr[16] = {31, 139, 8, 4, 0, 0, 0, 0, 0, 255, 6, 0, 'B', 'C', 2, 0};
         memcpy(h, hdr, 16);
         wr16(h + 16, (uint16_t)(bsize - 1));
         wr32(h + 18 + clen, crc32_of(src, len));
         wr32(h + 18 + clen + 4, (uint32_t)len);
-        o.resize((size_t)bsize);
+        bsz[(size_t)i] = (int32_t)bsize;
     }
     if (bad) return fail(BSDC_IO_EFORMAT, "deflate failed");
-    for (auto &bk : blocks)
-        if (fwrite(bk.data(), 1, bk.size(), f) != bk.size()) return fail(BSDC_IO_EIO, "BGZF write failed");
+    for (int64_t i = 0; i < nb; i++)
+        if (fwrite(slots.data() + ((size_t)i << 16), 1, (size_t)bsz[(size_t)i], f) != (size_t)bsz[(size_t)i])
+            return fail(BSDC_IO_EIO, "BGZF write failed");
     return 0;
 }
 
 const uint8_t kBgzfEof[28] = {31, 139, 8, 4, 0, 0, 0, 0, 0, 255, 6, 0, 66, 67, 2, 0, 27, 0, 3, 0, 0, 0, 0, 0, 0, 0, 0, 0};
 
-int32_t write_bgzf(const char *path, const std::vector<uint8_t> &buf, int32_t level) {
+int32_t write_bgzf(const char *path, const Bytes &buf, int32_t level) {
     FILE *f = fopen(path, "wb");
     if (!f) return fail(BSDC_IO_EIO, std::string("cannot create ") + path);
     int32_t rc = deflate_write(f, buf.data(), (int64_t)buf.size(), level);
@@ -1251,7 +1339,7 @@ int32_t write_bgzf(const char *path, const std::vector<uint8_t> &buf, int32_t le
 }
 
 // BAM header bytes (magic, text, references)
-void encode_header(std::vector<uint8_t> &head, const char *header_text, int64_t header_len, int32_t n_ref,
+void encode_header(Bytes &head, const char *header_text, int64_t header_len, int32_t n_ref,
                    const int64_t *ref_name_off, const char *ref_name_buf, const int64_t *ref_len) {
     auto put32 = [&](uint32_t v) {
         uint8_t t[4];
@@ -1272,7 +1360,7 @@ void encode_header(std::vector<uint8_t> &head, const char *header_text, int64_t 
 }
 
 // The records' BAM bytes appended to buf (encoded in parallel)
-int32_t encode_records(const bsdc_bam_records *r, std::vector<uint8_t> &buf) {
+int32_t encode_records(const bsdc_bam_records *r, Bytes &buf) {
     const int64_t nr = r->n_rec;
     std::vector<int64_t> off(nr + 1);
     off[0] = (int64_t)buf.size();
@@ -1280,7 +1368,8 @@ int32_t encode_records(const bsdc_bam_records *r, std::vector<uint8_t> &buf) {
         const int64_t l_name = r->name_off[k + 1] - r->name_off[k] + 1;
         const int64_t n_cig = r->cig_off[k + 1] - r->cig_off[k];
         const int64_t l_seq = r->seq_off[k + 1] - r->seq_off[k];
-        const int64_t l_aux = r->aux_off[k + 1] - r->aux_off[k];
+        const int64_t l_aux1 = r->aux_off[k + 1] - r->aux_off[k];
+        const int64_t l_aux = l_aux1 + (r->aux2_off ? r->aux2_off[k + 1] - r->aux2_off[k] : 0);
         if (l_name > 254 || n_cig > 0xFFFF) return fail(BSDC_IO_EFORMAT, "record name or cigar too long for BAM");
         off[k + 1] = off[k] + 4 + 32 + l_name + 4 * n_cig + (l_seq + 1) / 2 + l_seq + l_aux;
     }
@@ -1291,7 +1380,8 @@ int32_t encode_records(const bsdc_bam_records *r, std::vector<uint8_t> &buf) {
         const int64_t l_name = r->name_off[k + 1] - r->name_off[k] + 1;
         const int64_t n_cig = r->cig_off[k + 1] - r->cig_off[k];
         const int64_t l_seq = r->seq_off[k + 1] - r->seq_off[k];
-        const int64_t l_aux = r->aux_off[k + 1] - r->aux_off[k];
+        const int64_t l_aux1 = r->aux_off[k + 1] - r->aux_off[k];
+        const int64_t l_aux = l_aux1 + (r->aux2_off ? r->aux2_off[k + 1] - r->aux2_off[k] : 0);
         const uint32_t *cg = r->cigar + r->cig_off[k];
         int64_t reflen = 0;
         for (int64_t i = 0; i < n_cig; i++) {
@@ -1323,7 +1413,8 @@ int32_t encode_records(const bsdc_bam_records *r, std::vector<uint8_t> &buf) {
         q += (l_seq + 1) / 2;
         memcpy(q, r->qual + r->seq_off[k], (size_t)l_seq);
         q += l_seq;
-        memcpy(q, r->aux + r->aux_off[k], (size_t)l_aux);
+        memcpy(q, r->aux + r->aux_off[k], (size_t)l_aux1);
+        if (r->aux2_off) memcpy(q + l_aux1, r->aux2 + r->aux2_off[k], (size_t)(l_aux - l_aux1));
     }
     return 0;
 }
@@ -1333,7 +1424,7 @@ extern "C" int32_t bsdc_bam_write(const char *path, const char *header_text, int
                                   const int64_t *ref_name_off, const char *ref_name_buf, const int64_t *ref_len,
                                   const bsdc_bam_records *r, int32_t level, int32_t n_threads) {
     set_threads(n_threads);
-    std::vector<uint8_t> buf;
+    Bytes buf;
     encode_header(buf, header_text, header_len, n_ref, ref_name_off, ref_name_buf, ref_len);
     const int32_t rc = encode_records(r, buf);
     if (rc != 0) return rc;
@@ -1347,7 +1438,7 @@ extern "C" int32_t bsdc_bam_write(const char *path, const char *header_text, int
 struct bsdc_bam_writer {
     FILE *f = nullptr;
     int32_t level = 6;
-    std::vector<uint8_t> tail;
+    Bytes tail;
 };
 
 extern "C" int32_t bsdc_bam_writer_open(const char *path, const char *header_text, int64_t header_len, int32_t n_ref,
@@ -1637,7 +1728,7 @@ extern "C" int64_t bsdc_consensus_tags(int64_t n, const int64_t *row_a, const in
 namespace {
 // Paired FASTQ text of records appended to buf[0] (first of pair) / buf[1] (second), as
 // bsdc_fastq_write formats it; the pairing checks of include/bsdc_io.h.
-int32_t format_fastq(const bsdc_bam_records *r, std::vector<uint8_t> *buf) {
+int32_t format_fastq(const bsdc_bam_records *r, Bytes *buf) {
     const int64_t nr = r->n_rec;
     // record k -> its file (0: first of pair, 1: second) or -1 (not written); pairs must be adjacent
     std::vector<int8_t> dst((size_t)nr, -1);
@@ -1702,7 +1793,7 @@ int32_t format_fastq(const bsdc_bam_records *r, std::vector<uint8_t> *buf) {
 extern "C" int32_t bsdc_fastq_write(const char *path1, const char *path2, const bsdc_bam_records *r, int32_t level,
                                     int32_t n_threads) {
     set_threads(n_threads);
-    std::vector<uint8_t> buf[2];
+    Bytes buf[2];
     const int32_t rc = format_fastq(r, buf);
     if (rc != 0) return rc;
     for (int d = 0; d < 2; d++) {
@@ -1716,7 +1807,7 @@ extern "C" int32_t bsdc_fastq_write(const char *path1, const char *path2, const 
 struct bsdc_fastq_writer {
     FILE *f[2] = {nullptr, nullptr};
     int32_t level = 6;
-    std::vector<uint8_t> tail[2];
+    Bytes tail[2];
 };
 
 extern "C" int32_t bsdc_fastq_writer_open(const char *path1, const char *path2, int32_t level, bsdc_fastq_writer **out) {

@@ -299,35 +299,47 @@ def step5_stream_multi(in_bam: str, fasta: str, out_bam: Optional[str], devices:
         with plock:
             plock.notify_all()
 
-    def decoder():
+    def decoder():  # cuts the next chunk while the planner decodes and plans the one before
+        it = None
         try:
-            for _, raw in bam.stream_bam(in_bam, threads, chunk_bytes, slack):
+            it = bam.stream_chunks(in_bam, threads, chunk_bytes, slack)
+            for ch in it:
                 if stop.is_set():
+                    ch.discard()
                     break
-                raws.put(raw)
+                raws.put(ch)
         except BaseException as e:  # noqa: BLE001
             fail(e)
         finally:
+            if it is not None:
+                it.close()
             raws.put(None)
 
     def planner():
         try:
             while True:
                 t0 = time.perf_counter()
-                raw = raws.get()
-                if raw is None:
+                ch = raws.get()
+                if ch is None:
                     break
                 if stop.is_set():
+                    ch.discard()
                     continue  # drain to the decoder's None
                 t1 = time.perf_counter()
+                raw = ch.decode(threads)[1]
+                t2 = time.perf_counter()
                 plan = pipeline.plan_families(raw, "full", ref)
-                T["plan"] += time.perf_counter() - t1
+                T["plan"] += time.perf_counter() - t2
+                T["parse"] = T.get("parse", 0.0) + t2 - t1
                 T["decode"] += t1 - t0  # the wait for the decoder
                 chunks.put((raw, plan))
         except BaseException as e:  # noqa: BLE001
             fail(e)
-            while raws.get() is not None:
-                pass
+            while True:
+                ch = raws.get()
+                if ch is None:
+                    break
+                ch.discard()
         finally:
             chunks.put(None)
 

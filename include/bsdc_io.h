@@ -17,7 +17,7 @@
 extern "C" {
 #endif
 
-#define BSDC_IO_ABI_VERSION 4
+#define BSDC_IO_ABI_VERSION 5
 #define BSDC_IO_EFORMAT (-10) /* not BGZF/BAM, truncated, bad CRC */
 #define BSDC_IO_EIO (-11)     /* open/read/write failed */
 
@@ -92,8 +92,14 @@ int32_t bsdc_bam_stream_next(bsdc_bam_stream *s, int64_t min_bytes, int64_t slac
 int32_t bsdc_bam_stream_header(const bsdc_bam_stream *s, bsdc_bam **out); /* header only, no records */
 void bsdc_bam_stream_close(bsdc_bam_stream *s);
 /* bsdc_bam_free for a chunk of this stream that has been copied out: its buffer goes back to the
- * stream for the next chunk (no fresh pages per chunk). */
+ * stream for the next chunk (no fresh pages per chunk).  Any thread may recycle a chunk while the
+ * stream reads the next one; a closed stream is deleted when its last chunk comes back. */
 void bsdc_bam_stream_recycle(bsdc_bam_stream *s, bsdc_bam *b);
+/* The next chunk unparsed (records listed, not decoded): bsdc_bam_parse it, on any thread, before
+ * bsdc_bam_sizes_of / bsdc_bam_copy.  bsdc_bam_stream_next = next_raw + parse.  Lets one thread cut
+ * the next chunk while another decodes this one (bam.step5_stream). */
+int32_t bsdc_bam_stream_next_raw(bsdc_bam_stream *s, int64_t min_bytes, int64_t slack, bsdc_bam **out);
+int32_t bsdc_bam_parse(bsdc_bam *b, int32_t n_threads);
 
 /* Records to write (n_rec entries; every *_off array has n_rec + 1 entries). */
 typedef struct {
@@ -111,6 +117,9 @@ typedef struct {
     const uint8_t *qual;
     const int64_t *aux_off;
     const uint8_t *aux;
+    const int64_t *aux2_off; /* optional (NULL = none): more aux bytes written after aux (the consensus
+                                tags, so they are never concatenated to the per-family tags first) */
+    const uint8_t *aux2;
 } bsdc_bam_records;
 
 /* Writes header + records as BGZF (blocks deflated in parallel at `level`), with the EOF block. */

@@ -42,6 +42,7 @@ def prep(args):
 def child(args):
     if args.mode == "prep":
         return prep(args)
+    import bsseqconsensusreads_amd  # noqa: F401  (first, as in the CLI: its OpenMP wait policy)
     import torch  # noqa: F401  (the GPU runtime, as the CLI loads it)
 
     from bsseqconsensusreads_amd import bam
@@ -60,6 +61,8 @@ def child(args):
         return 0
     from bsseqconsensusreads_amd.device import Engine
     eng = Engine(0)
+    ru0 = resource.getrusage(resource.RUSAGE_SELF)
+    cpu0 = ru0.ru_utime + ru0.ru_stime
     t0 = time.perf_counter()
     if args.mode == "whole":
         info = bam.step5(args.inp, args.fa, args.out, engine=eng, threads=args.threads, level=args.level)
@@ -72,8 +75,11 @@ def child(args):
                                 chunk_bytes=args.chunk_mb << 20, stats=stats)
     dt = time.perf_counter() - t0
     eng.close()
-    rss = resource.getrusage(resource.RUSAGE_SELF).ru_maxrss / 1024  # MiB
+    ru = resource.getrusage(resource.RUSAGE_SELF)
+    rss = ru.ru_maxrss / 1024  # MiB
+    cpu = ru.ru_utime + ru.ru_stime - cpu0  # host CPU seconds of the run (all threads)
     print(json.dumps({"mode": args.mode, "seconds": round(dt, 3), "peak_rss_MiB": round(rss, 1),
+                      "cpu_s": round(cpu, 2), "cores_busy": round(cpu / dt, 2),
                       "stage_busy_s": stats, **info}))
 
 

@@ -7,6 +7,7 @@ Usage: python profiles/host_stages.py [--families N] [--threads T] [--fastq]"""
 import argparse
 import json
 import os
+import resource
 import sys
 import tempfile
 import time
@@ -57,17 +58,25 @@ def main():
     w = None if a.fastq else bam.BamWriter(out, bam.output_header(hdr), 5)
     fq = bam.FastqWriter(out + ".1.fq.gz", out + ".2.fq.gz", 5) if a.fastq else None
     nfam = 0
+    C = {k: 0.0 for k in T}  # host CPU seconds per stage (all threads; OpenMP spin-waits included)
+
+    def cpu():
+        r = resource.getrusage(resource.RUSAGE_SELF)
+        return r.ru_utime + r.ru_stime
     t_all = time.perf_counter()
     it = bam.stream_bam(inp, a.threads, a.chunk_mb << 20)
     while True:
         t0 = time.perf_counter()
+        c0 = cpu()
         try:
             h, chunk = next(it)
         except StopIteration:
             break
         t1 = time.perf_counter()
+        c1 = cpu()
         plan = plan_families(chunk, "full", s.ref)
         t2 = time.perf_counter()
+        c2 = cpu()
         parts = []
         for f0, f1 in pipeline.plan_ranges(plan):
             fb = materialize(plan, f0, f1, 24 * 1024)
@@ -76,13 +85,21 @@ def main():
             T["fake_gpu"] += time.perf_counter() - t3
         cons = pipeline.concat_consensus(parts)
         t4 = time.perf_counter()
+        c4 = cpu()
         recs = bam.duplex_records(cons, chunk, "L1", a.threads)
         t5 = time.perf_counter()
+        c5 = cpu()
         if w is not None:
             w.add(recs, a.threads)
         if fq is not None:
             fq.add(recs, a.threads)
         t6 = time.perf_counter()
+        c6 = cpu()
+        C["decode"] += c1 - c0
+        C["plan"] += c2 - c1
+        C["materialize"] += c4 - c2
+        C["records"] += c5 - c4
+        C["encode"] += c6 - c5
         T["decode"] += t1 - t0
         T["plan"] += t2 - t1
         T["materialize"] += t4 - t2
@@ -98,6 +115,7 @@ def main():
     print(json.dumps({"families": a.families, "consensus_families": nfam, "records": int(raw.n), "threads": a.threads,
                       "input_MB": round(os.path.getsize(inp) / 1e6, 1), "seconds": {k: round(v, 3) for k, v in T.items()},
                       "serial_wall_s": round(wall, 3),
+                      "cpu_seconds": {k: round(v, 2) for k, v in C.items() if k != "fake_gpu"},
                       "families_per_s_per_stage": {k: round(a.families / v) for k, v in T.items() if v > 0}}))
 
 
