@@ -845,6 +845,7 @@ def step5_stream(in_bam: str, fasta: str, out_bam: Optional[str], engine=None, p
     info = {"records_in": 0, "families": 0, "families_emitted": 0, "records_out": 0, "chunks": 0}
     T = {"decode": 0.0, "parse": 0.0, "plan": 0.0, "gpu": 0.0, "records": 0.0, "encode": 0.0, "gpu_wait": 0.0,
          "writer_wait": 0.0}
+    G: dict = {}  # the GPU stage's host steps (pipeline.run_ranges timing)
     first = {}
     stop = threading.Event()  # set on any failure: the decoder and planner stop at their next chunk
 
@@ -980,7 +981,7 @@ def step5_stream(in_bam: str, fasta: str, out_bam: Optional[str], engine=None, p
                     cons = pipeline.run_step5(eng, raw, tags=tg, batch_bases=batch_bases)[0]
                 else:
                     cons = pipeline.concat_consensus(
-                        pipeline.run_ranges(eng, plan, pipeline.plan_ranges(plan, batch_bases), mode, tg))
+                        pipeline.run_ranges(eng, plan, pipeline.plan_ranges(plan, batch_bases), mode, tg, G))
                 T["gpu"] += time.perf_counter() - t0
                 info["records_in"] += raw.n
                 info["families"] += int(cons.status.shape[0])
@@ -1007,6 +1008,7 @@ def step5_stream(in_bam: str, fasta: str, out_bam: Optional[str], engine=None, p
         raise err[0]
     if stats is not None:
         stats.update({k: round(v, 4) for k, v in T.items()})
+        stats.update({"gpu_" + k: round(v, 4) for k, v in G.items()})
     return info
 
 

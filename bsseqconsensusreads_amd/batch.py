@@ -605,12 +605,12 @@ def plan_families_py(raw: R.RawRecords, mode: str = "full", ref: Optional[R.Refe
                       kfirst=kfirst, kn=kn, fam_split=fam_split)
 
 
-def materialize(plan: FamilyPlan, f0: int, f1: int, small_cap: int = SMALL_ARENA_CAP) -> FamilyBatch:
+def materialize(plan: FamilyPlan, f0: int, f1: int, small_cap: int = SMALL_ARENA_CAP, images=None) -> FamilyBatch:
     """The device batch of plan families [f0, f1) (family ids renumbered from 0): C++ (hostplan)
-    for the step-5 modes, materialize_py otherwise."""
+    for the step-5 modes, materialize_py otherwise.  images: see hostplan.materialize."""
     from . import hostplan
     if plan.mode in ("full", "vote") and hostplan.enabled():
-        return hostplan.materialize(plan, f0, f1, small_cap)
+        return hostplan.materialize(plan, f0, f1, small_cap, images=images)
     return materialize_py(plan, f0, f1, small_cap)
 
 

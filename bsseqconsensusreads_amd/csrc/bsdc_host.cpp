@@ -544,19 +544,30 @@ int32_t bsdc_materialize_fill(bsdc_batch *b, const bsdc_batch_arrays *o, int64_t
         reflen[i] = (!full && !cx) ? pv.L[k] : rl;  // vote mode: a simple record's length (batch.py)
         if (cx && (m > 0xFFFF || rl > 0xFFFF)) bad |= 1;
         // the record's bases / quals: nibble / byte rec_off + 1 (odd) of the images; two records
-        // never share a byte of the packed image (slots are 4-aligned)
-        const int64_t L = pv.L[k], so = R->seq_off[k] + pv.sL[k], d = b->rec_off[i] + 1;
+        // never share a byte of the packed image (slots are 4-aligned).  Every byte from the slot
+        // to the next record's slot (or the image end) is written here, the tools' room and the
+        // family alignment as zeros, so the images need no zeroed (fresh) memory
+        const int64_t L = pv.L[k], so = R->seq_off[k] + pv.sL[k], S = b->rec_off[i], d = S + 1;
+        const int64_t end = i + 1 < nr ? b->rec_off[i + 1] : b->n_slots;
+        o->qual[S] = 0;
         std::memcpy(o->qual + d, R->qual + so, (size_t)L);
+        std::memset(o->qual + d + L, 0, (size_t)(end - d - L));
         const uint8_t *s = R->seq + so;
-        uint8_t *p = o->seq + (d >> 1);
+        uint8_t *p = o->seq + (S >> 1);
         int64_t j = 0;
-        if (L > 0) {  // nibble d is the low half of byte d / 2, then whole bytes, then a high nibble
-            *p = (uint8_t)((*p & 0xF0) | (s[0] & 15));
-            p++;
-            j = 1;
-        }
+        *p = L > 0 ? (uint8_t)(s[0] & 15) : 0;  // nibble S (room) and d, the low half of byte S / 2
+        p++;
+        j = 1;
         for (; j + 1 < L; j += 2) *p++ = (uint8_t)(((s[j] & 15) << 4) | (s[j + 1] & 15));
-        if (j < L) *p = (uint8_t)(((s[j] & 15) << 4) | (*p & 0x0F));
+        if (j < L) *p++ = (uint8_t)((s[j] & 15) << 4);  // a high nibble, then zeros
+        std::memset(p, 0, (size_t)(o->seq + (end >> 1) - p));
+    }
+    if (nr == 0) {
+        std::memset(o->qual, 0, (size_t)b->n_slots);
+        std::memset(o->seq, 0, (size_t)(b->n_slots >> 1));
+    } else if (b->rec_off[0] > 0) {  // (leading empty families)
+        std::memset(o->qual, 0, (size_t)b->rec_off[0]);
+        std::memset(o->seq, 0, (size_t)(b->rec_off[0] >> 1));
     }
     if (bad) return fail(BSDC_EINVAL, "cigar too long");
     int64_t nc = 0;

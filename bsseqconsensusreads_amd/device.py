@@ -45,8 +45,11 @@ class DeviceBatch:
             a = np.ascontiguousarray(v)
             if a.size == 0:
                 a = np.zeros(1, dtype=a.dtype)
-            # torch has no uint32/uint16 arithmetic we need; move raw bytes
-            self.t[k] = torch.from_numpy(a.view(np.uint8)).to(device, non_blocking=False)
+            # torch has no uint32/uint16 arithmetic we need; move raw bytes.  Pinned sources (the
+            # engine's staging images) copy asynchronously on the stream; the engine double-buffers
+            # them, and the batch before is fetched (stream synchronized) before a buffer is refilled
+            h = torch.from_numpy(a.view(np.uint8))
+            self.t[k] = h.to(device, non_blocking=h.is_pinned())
         F, Rn = fb.n_fam, fb.n_rec
         self.stride = fb.stride
         self.status = torch.zeros(max(F, 1), dtype=torch.uint8, device=device)
@@ -160,6 +163,8 @@ class Engine:
         self.device_index = device_index
         self.device = torch.device("cuda", device_index)
         self.params = params or ConsensusParams()
+        self._stage = [None, None]  # pinned family-image staging buffers (stage_images)
+        self._stage_i = 0
         p = _lib.Params(self.params.error_rate_pre_umi, self.params.error_rate_post_umi,
                         self.params.min_input_base_quality, int(self.params.consensus_call_overlapping_bases),
                         self.params.min_reads, 0)
@@ -169,6 +174,20 @@ class Engine:
             raise RuntimeError("bsdc_ctx_create failed (%d)" % rc)
         self.ctx = h
         self.ref: Optional[Reference] = None
+
+    def stage_images(self, n_slots: int):
+        """Pinned host arrays (seq, qual) for the next batch's family images (materialize's
+        `images`), alternating between two buffer pairs that grow on demand: a batch's images
+        upload asynchronously while the next one is filled (pipeline.run_ranges)."""
+        i = self._stage_i
+        self._stage_i ^= 1
+        st = self._stage[i]
+        if st is None or st[1].numel() < n_slots:
+            cap = int(n_slots * 1.25) + 4096
+            st = (torch.empty(cap // 2 + 64, dtype=torch.uint8, pin_memory=True),
+                  torch.empty(cap, dtype=torch.uint8, pin_memory=True))
+            self._stage[i] = st
+        return st[0].numpy(), st[1].numpy()
 
     def close(self):
         if self.ctx:

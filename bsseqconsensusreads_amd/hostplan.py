@@ -174,8 +174,10 @@ def plan_families(raw: R.RawRecords, mode: str = "full", ref: Optional[R.Referen
     return FamilyPlan(raw=raw, mode=mode, ref=ref, **out)
 
 
-def materialize(plan, f0: int, f1: int, small_cap: int, n_threads: int = 0):
-    """batch.materialize in C++ (plans of modes 'full' / 'vote')."""
+def materialize(plan, f0: int, f1: int, small_cap: int, n_threads: int = 0, images=None):
+    """batch.materialize in C++ (plans of modes 'full' / 'vote').  images(n_slots) -> (seq, qual):
+    caller-owned uint8 arrays of at least n_slots / 2 and n_slots bytes for the family images
+    (e.g. pinned staging buffers, Engine.stage_images); the fill writes every byte of them."""
     from . import batch as B
     if plan.mode not in ("full", "vote"):
         raise ValueError("native materialize: mode 'full' or 'vote', not %r" % plan.mode)
@@ -203,7 +205,12 @@ def materialize(plan, f0: int, f1: int, small_cap: int, n_threads: int = 0):
         raise ValueError(_err(lib))
     try:
         nr, nf, n_slots = sz.n_rec, sz.n_fam, sz.n_slots
-        a = dict(seq=np.zeros(n_slots // 2, np.uint8), qual=np.zeros(n_slots, np.uint8),
+        if images is not None:
+            seq_img, qual_img = images(n_slots)
+            seq_img, qual_img = seq_img[:n_slots // 2], qual_img[:n_slots]
+        else:
+            seq_img, qual_img = np.empty(n_slots // 2, np.uint8), np.empty(n_slots, np.uint8)
+        a = dict(seq=seq_img, qual=qual_img,
                  rec=np.empty((nr, 4), np.uint32), rec_win=np.empty((nr, 2), np.uint32), rt=np.empty(4 * nr, np.int32),
                  cig_off=np.empty(nr, np.uint32), cig_info=np.empty(nr, np.uint32),
                  cigar=np.empty(max(sz.n_cigar_max, 1), np.uint32), src=np.empty(nr, np.int64),

@@ -241,20 +241,36 @@ def plan_ranges(plan: FamilyPlan, batch_bases: Optional[int] = None):
     return shard.plan_batches(plan.fam_bases(), DEFAULT_BATCH_BASES if batch_bases is None else batch_bases)
 
 
-def run_ranges(engine: Engine, plan: FamilyPlan, ranges, mode: int, tags: bool = False) -> List[Consensus]:
+def run_ranges(engine: Engine, plan: FamilyPlan, ranges, mode: int, tags: bool = False,
+               timing: Optional[dict] = None) -> List[Consensus]:
     """Plan family ranges through the kernels, one launch each, output per range in range order.
-    The host builds range i + 1 while the kernels of range i run."""
+    The host builds range i + 1 while the kernels of range i run.  `timing`: seconds added per
+    host step (materialize, upload, fetch = wait + copy out, unpack)."""
+    import time
+    T = timing if timing is not None else {}
     parts: List[Consensus] = []
     prev = None
+
+    def out(fb, db):
+        t0 = time.perf_counter()
+        o = db.fetch()
+        t1 = time.perf_counter()
+        parts.append(consensus_from_output(fb, o))
+        T["fetch"] = T.get("fetch", 0.0) + t1 - t0
+        T["unpack"] = T.get("unpack", 0.0) + time.perf_counter() - t1
     for a, b in ranges:
-        fb = materialize(plan, a, b)
+        t0 = time.perf_counter()
+        fb = materialize(plan, a, b, images=engine.stage_images)
+        t1 = time.perf_counter()
         db = engine.upload(fb, tags=tags)
         engine.run(db, mode | (MODE_TAGS if tags else 0))
+        T["materialize"] = T.get("materialize", 0.0) + t1 - t0
+        T["upload"] = T.get("upload", 0.0) + time.perf_counter() - t1
         if prev is not None:
-            parts.append(consensus_from_output(prev[0], prev[1].fetch()))
+            out(*prev)
         prev = (fb, db)
     if prev is not None:
-        parts.append(consensus_from_output(prev[0], prev[1].fetch()))
+        out(*prev)
     return parts
 
 

@@ -60,7 +60,8 @@ def _force_large(monkeypatch, where):
             fb.large_buckets = [np.zeros((0, 4), np.uint32)] * (nb - 2) + [lf[:h], lf[h:]]
             fb.large_arenas = [16] * (nb - 2) + [top + 4096, top + 8192]
         return fb
-    monkeypatch.setattr(pipeline, "materialize", lambda plan, f0, f1, small_cap=0: glob(real_m(plan, f0, f1, 0)))
+    monkeypatch.setattr(pipeline, "materialize",
+                        lambda plan, f0, f1, small_cap=0, images=None: glob(real_m(plan, f0, f1, 0, images=images)))
     monkeypatch.setattr(pipeline, "build_family_batch",
                         lambda r, mode="full", ref=None, small_cap=0, **kw: glob(real_b(r, mode, ref, small_cap=0, **kw)))
 

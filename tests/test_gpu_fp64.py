@@ -69,5 +69,6 @@ def test_gpu_large_kernel_near_ties_vs_fgbio_fp64(engine, qlo, monkeypatch):
     s = synth.generate("C1", 800, seed=13, device="cpu", genome_len=200_000)
     raw = near_tie_votes(s.raw, qlo=qlo, seed=7)
     real = batch.materialize
-    monkeypatch.setattr(pipeline, "materialize", lambda plan, f0, f1, small_cap=0: real(plan, f0, f1, small_cap=0))
+    monkeypatch.setattr(pipeline, "materialize",
+                        lambda plan, f0, f1, small_cap=0, images=None: real(plan, f0, f1, small_cap=0, images=images))
     _gpu_vs_fp64(engine, raw, s.ref, False, "k_large q>=%d" % qlo)

@@ -57,8 +57,8 @@ def force_large(monkeypatch, where):
     family in the last bucket, in HBM scratch ("global")."""
     real = batch.materialize
 
-    def forced(plan, f0, f1, small_cap=0):
-        fb = real(plan, f0, f1, small_cap=0)
+    def forced(plan, f0, f1, small_cap=0, images=None):
+        fb = real(plan, f0, f1, small_cap=0, images=images)
         if where == "global":
             nb = len(fb.large_buckets)
             fb.large_buckets = [np.zeros((0, 4), np.uint32)] * (nb - 1) + [fb.large_fams]
