@@ -44,7 +44,8 @@ class ConsensusC(C.Structure):
 EXPORTS = ("bsdc_abi_version", "bsdc_ctx_create", "bsdc_ctx_destroy", "bsdc_last_error",
            "bsdc_load_reference", "bsdc_run", "bsdc_convert", "bsdc_extend", "bsdc_duplex_call",
            "bsdc_family_arena_bytes", "bsdc_small_arena_bytes", "bsdc_get_tables", "bsdc_model_tables",
-           "bsdc_model_tables_fp64", "bsdc_agree_tables", "bsdc_phred_buckets")
+           "bsdc_model_tables_fp64", "bsdc_agree_tables", "bsdc_phred_buckets", "bsdc_bgzf_scratch_bytes",
+           "bsdc_bgzf_deflate", "bsdc_bgzf_pack")
 
 _lib = None
 
@@ -85,6 +86,12 @@ def load(path: str = LIB_PATH):
     lib.bsdc_model_tables_fp64.restype = None
     lib.bsdc_agree_tables.argtypes = [C.c_double, C.c_double, C.c_void_p, C.c_void_p]
     lib.bsdc_agree_tables.restype = None
+    lib.bsdc_bgzf_scratch_bytes.argtypes = [C.c_int64]
+    lib.bsdc_bgzf_scratch_bytes.restype = C.c_int64
+    lib.bsdc_bgzf_deflate.argtypes = [C.c_void_p, C.c_int64, C.c_int64, C.c_int64, C.c_void_p, C.c_void_p, C.c_void_p]
+    lib.bsdc_bgzf_deflate.restype = C.c_int32
+    lib.bsdc_bgzf_pack.argtypes = [C.c_void_p, C.c_void_p, C.c_void_p, C.c_int64, C.c_int64, C.c_void_p, C.c_void_p]
+    lib.bsdc_bgzf_pack.restype = C.c_int32
     lib.bsdc_phred_buckets.argtypes = [C.c_double, C.c_double, C.c_void_p]
     lib.bsdc_phred_buckets.restype = None
     if lib.bsdc_abi_version() != BSDC_ABI_VERSION:

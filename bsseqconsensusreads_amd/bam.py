@@ -89,6 +89,10 @@ def _load():
     lib.bsdc_bam_writer_open.restype = C.c_int32
     lib.bsdc_bam_writer_add.argtypes = [_P, C.POINTER(_Records), C.c_int32]
     lib.bsdc_bam_writer_add.restype = C.c_int32
+    lib.bsdc_bam_writer_encode.argtypes = [_P, C.POINTER(_Records), C.c_int32, C.POINTER(C.c_void_p)]
+    lib.bsdc_bam_writer_encode.restype = C.c_int64
+    lib.bsdc_bam_writer_put_blocks.argtypes = [_P, C.c_int64, _P, _P, C.c_int32]
+    lib.bsdc_bam_writer_put_blocks.restype = C.c_int32
     lib.bsdc_bam_writer_close.argtypes = [_P, C.c_int32]
     lib.bsdc_bam_writer_close.restype = C.c_int32
     lib.bsdc_fastq_writer_open.argtypes = [C.c_char_p, C.c_char_p, C.c_int32, C.POINTER(_P)]
@@ -568,13 +572,69 @@ def write_bam(path: str, header: BamHeader, recs: OutRecordsBam, level: int = 6,
         raise OSError("%s: %s" % (path, lib.bsdc_io_last_error().decode()))
 
 
+class GpuBgzf:
+    """BGZF compression of a BAM writer's whole blocks on one GPU (libbsdc bsdc_bgzf_*,
+    csrc/bsdc_bgzf.hip): the encoded bytes go to HBM, one workgroup deflates each 65280-byte block,
+    the blocks come back packed; the writer fills their CRC32 / ISIZE and writes them.  Its own HIP
+    stream, so it overlaps the consensus kernels of the next chunk."""
+
+    MAX_BLOCKS = 1024  # blocks per kernel launch (the scratch: bsdc_bgzf_scratch_bytes of these)
+
+    def __init__(self, device):
+        import torch
+
+        from . import _lib
+        self.torch = torch
+        self.lib = _lib.load()
+        self.dev = torch.device(device)
+        self.stream = torch.cuda.Stream(self.dev)
+        self.scratch = torch.empty(int(self.lib.bsdc_bgzf_scratch_bytes(self.MAX_BLOCKS)), dtype=torch.uint8,
+                                   device=self.dev)
+        self.blocks = 0
+        self.bytes_in = 0
+        self.bytes_out = 0
+
+    def compress(self, data_ptr: int, nbytes: int):
+        """host bytes [data_ptr, +nbytes) (whole blocks) -> (packed blocks, sizes int32[nblk])."""
+        torch = self.torch
+        nblk = nbytes // 65280
+        host = np.ctypeslib.as_array(C.cast(data_ptr, C.POINTER(C.c_uint8)), shape=(nbytes,))
+        sizes_h = np.zeros(nblk, np.int32)
+        with torch.cuda.stream(self.stream):
+            din = torch.from_numpy(host).to(self.dev, non_blocking=False)
+            sizes = torch.empty(nblk, dtype=torch.int32, device=self.dev)
+            out = torch.empty(nblk * 65536, dtype=torch.uint8, device=self.dev)
+            offs_h = np.zeros(nblk + 1, np.int64)
+            st = self.stream.cuda_stream
+            for b0 in range(0, nblk, self.MAX_BLOCKS):
+                nb = min(self.MAX_BLOCKS, nblk - b0)
+                if self.lib.bsdc_bgzf_deflate(din.data_ptr(), nbytes, b0, nb, self.scratch.data_ptr(), sizes.data_ptr(),
+                                              st) != 0:
+                    raise RuntimeError("bsdc_bgzf_deflate failed")
+                sz = sizes[b0:b0 + nb].cpu().numpy()  # (synchronizes the stream)
+                sizes_h[b0:b0 + nb] = sz
+                offs_h[b0 + 1:b0 + nb + 1] = offs_h[b0] + np.cumsum(np.maximum(sz, 0).astype(np.int64))
+                offs = torch.from_numpy(offs_h).to(self.dev)
+                if self.lib.bsdc_bgzf_pack(self.scratch.data_ptr(), sizes.data_ptr(), offs.data_ptr(), b0, nb,
+                                           out.data_ptr(), st) != 0:
+                    raise RuntimeError("bsdc_bgzf_pack failed")
+            total = int(offs_h[nblk])
+            packed = out[:total].cpu().numpy() if total else np.zeros(1, np.uint8)
+        self.blocks += nblk
+        self.bytes_in += nbytes
+        self.bytes_out += total
+        return packed, sizes_h
+
+
 class BamWriter:
     """Streaming BAM writer (bsdc_bam_writer): header at open, records added in order, the same
-    bytes as write_bam of all the records at once."""
+    bytes as write_bam of all the records at once -- or, with `gpu` (a GpuBgzf), every whole block
+    deflated on the GPU (valid BGZF, other compressed bytes)."""
 
-    def __init__(self, path: str, header: BamHeader, level: int = 6):
+    def __init__(self, path: str, header: BamHeader, level: int = 6, gpu: Optional["GpuBgzf"] = None):
         self.lib = _load()
         self.path = path
+        self.gpu = gpu
         rn = StringTable.from_list([x.encode() for x in header.ref_names])
         keep = []
 
@@ -595,7 +655,18 @@ class BamWriter:
     def add(self, recs: OutRecordsBam, threads: int = 0):
         keep = []
         r = _records_struct(recs, keep)
-        if self.lib.bsdc_bam_writer_add(self.h, C.byref(r), int(threads)) != 0:
+        if self.gpu is None:
+            if self.lib.bsdc_bam_writer_add(self.h, C.byref(r), int(threads)) != 0:
+                raise OSError("%s: %s" % (self.path, self.lib.bsdc_io_last_error().decode()))
+            return
+        data = C.c_void_p()
+        nbytes = self.lib.bsdc_bam_writer_encode(self.h, C.byref(r), int(threads), C.byref(data))
+        if nbytes < 0:
+            raise OSError("%s: %s" % (self.path, self.lib.bsdc_io_last_error().decode()))
+        if nbytes == 0:
+            return
+        packed, sizes = self.gpu.compress(data.value, int(nbytes))
+        if self.lib.bsdc_bam_writer_put_blocks(self.h, sizes.shape[0], _ptr(packed), _ptr(sizes), int(threads)) != 0:
             raise OSError("%s: %s" % (self.path, self.lib.bsdc_io_last_error().decode()))
 
     def close(self, threads: int = 0):
@@ -823,14 +894,16 @@ def step5(in_bam: str, fasta: str, out_bam: Optional[str], engine=None, prefix: 
 def step5_stream(in_bam: str, fasta: str, out_bam: Optional[str], engine=None, prefix: Optional[str] = None,
                  threads: int = 0, level: int = 6, fastq: Optional[Tuple[str, str]] = None, tags: bool = True,
                  chunk_bytes: int = DEFAULT_CHUNK_BYTES, slack: int = DEFAULT_SLACK,
-                 batch_bases: Optional[int] = None, stats: Optional[dict] = None) -> dict:
+                 batch_bases: Optional[int] = None, stats: Optional[dict] = None, gpu_bgzf: bool = False) -> dict:
     """step5 in bounded memory, pipelined: a decoder thread decodes the next chunk of the
     coordinate-sorted input (stream_bam: cut where no template or MI family straddles), a reader
     thread forms the previous chunk's families (C++ plan); this thread runs the chunk's family
     batches on the GPU; a writer thread builds the output records of the chunk before and appends
     them to the BAM (BamWriter).  Peak host memory is about five chunks, whatever the file size.  The output is
     byte-identical to step5's (tests/test_stream.py): every chunk's TemplateCoordinate keys sort
-    before the next chunk's, so the chunks' families in order are the whole file's."""
+    before the next chunk's, so the chunks' families in order are the whole file's.  gpu_bgzf: the
+    BAM's blocks are deflated on the engine's GPU (GpuBgzf; the same records, other compressed
+    bytes and a larger file)."""
     import queue
     import threading
     import time
@@ -923,7 +996,8 @@ def step5_stream(in_bam: str, fasta: str, out_bam: Optional[str], engine=None, p
 
     def writer():
         try:
-            w = BamWriter(out_bam, output_header(first["header"]), level) if out_bam is not None else None
+            gz = GpuBgzf(eng.device) if gpu_bgzf and out_bam is not None else None
+            w = BamWriter(out_bam, output_header(first["header"]), level, gz) if out_bam is not None else None
             fq = FastqWriter(fastq[0], fastq[1], level) if fastq is not None else None
             while True:
                 recs = recq.get()

@@ -46,6 +46,8 @@ def parse(argv):
         p.add_argument("--device", type=int, default=0)
         if name == "step5":
             p.add_argument("--gpus", type=int, default=1, help="one process per GPU, family batches dealt to them")
+            p.add_argument("--gpu-bgzf", default="false", choices=("true", "false"),
+                           help="deflate the output BAM's blocks on the GPU (streaming, one GPU; larger file)")
             p.add_argument("--devices", default=None, help="comma-separated device id per rank (default 0..gpus-1)")
             p.add_argument("--batch-bases", type=int, default=None, help="device batch budget in bases")
             p.add_argument("--stream", default="auto", choices=["auto", "true", "false"],
@@ -124,7 +126,7 @@ def main(argv=None) -> int:
             if stream:
                 info = bam.step5_stream(a.input, a.reference, out, eng, a.read_name_prefix, a.threads, a.compression,
                                         fq, tags=a.output_per_base_tags == "true", chunk_bytes=a.chunk_mb << 20,
-                                        batch_bases=a.batch_bases)
+                                        batch_bases=a.batch_bases, gpu_bgzf=a.gpu_bgzf == "true")
             elif a.cmd == "step5":
                 info = bam.step5(a.input, a.reference, out, eng, a.read_name_prefix, a.threads, a.compression, fq,
                                  tags=a.output_per_base_tags == "true", batch_bases=a.batch_bases, dist=dist)

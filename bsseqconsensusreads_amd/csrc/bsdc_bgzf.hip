@@ -1,0 +1,469 @@
+// BGZF block compression on the GPU (gfx950): one 256-thread workgroup per 65280-byte block of
+// an uncompressed BAM stream -> a gzip member with one dynamic-Huffman DEFLATE block (RFC 1951),
+// the BGZF header with BSIZE (SAM/BAM spec 4.1).  The host adds CRC32 + ISIZE when it writes the
+// blocks out (it holds the uncompressed bytes), and stores a block whose deflate would not fit.
+//
+// The algorithm is oracle/bgzf_ref.c's, step for step, so the bytes are identical (tests):
+//  A. match candidates in rounds of 256 consecutive positions: every position of the round looks
+//     up its 4-byte hash in the LDS table, then the round inserts its positions (atomicMax: the
+//     largest wins a slot) -- a candidate is the most recent earlier position with the same hash
+//     outside the position's own round;
+//  B. thread t parses its 255-byte segment greedily (the longest of distances 1, 2, 4 and the
+//     candidate's, first on a tie, >= 3, not past the segment), tokens to HBM scratch, symbol
+//     frequencies by LDS atomics;
+//  C. thread 0 builds the length-limited Huffman codes (the restatement's two-queue build), the
+//     run-length coded code lengths and their own code, and writes the block header bits;
+//  D. each thread's bit count, a block scan -> bit offsets;
+//  E. each thread writes its bits: whole 32-bit words as plain stores, its first and last
+//     (shared) words by atomicOr into the zeroed slot.
+// Bytes per block: 65280 in, ~11 KB out for the tagged step-5 output (ratio 5.8 against libdeflate
+// level 5's 7.26: the parse trades ratio for parallelism; profiles/deflate_levels.py).
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+#include "../../include/bsdc.h"
+
+namespace {
+
+constexpr int kT = 256;          // threads per block = positions per candidate round
+constexpr int kSeg = 255;        // bytes per thread segment (kT * kSeg = 65280 = BGZF block)
+constexpr int kBlock = kT * kSeg;
+constexpr int kHashBits = 12;
+constexpr int kMaxDist = 32768;
+constexpr int kOutCap = 65536 - 26;  // deflate bytes that still fit a BGZF block
+
+__constant__ uint16_t cLenBase[29] = {3, 4, 5, 6, 7, 8, 9, 10, 11, 13, 15, 17, 19, 23, 27,
+                                      31, 35, 43, 51, 59, 67, 83, 99, 115, 131, 163, 195, 227, 258};
+__constant__ uint8_t cLenExtra[29] = {0, 0, 0, 0, 0, 0, 0, 0, 1, 1, 1, 1, 2, 2, 2, 2, 3, 3, 3, 3, 4, 4, 4, 4, 5, 5, 5, 5, 0};
+__constant__ uint16_t cDistBase[30] = {1, 2, 3, 4, 5, 7, 9, 13, 17, 25, 33, 49, 65, 97, 129, 193, 257, 385,
+                                       513, 769, 1025, 1537, 2049, 3073, 4097, 6145, 8193, 12289, 16385, 24577};
+__constant__ uint8_t cDistExtra[30] = {0, 0, 0, 0, 1, 1, 2, 2, 3, 3, 4, 4, 5, 5, 6, 6, 7, 7, 8, 8, 9, 9, 10, 10, 11, 11, 12, 12, 13, 13};
+__constant__ uint8_t cClOrder[19] = {16, 17, 18, 0, 8, 7, 9, 6, 10, 5, 11, 4, 12, 3, 13, 2, 14, 1, 15};
+
+__device__ __forceinline__ int len_code(int l) {
+    int c = 0;
+    while (c < 28 && cLenBase[c + 1] <= l) c++;
+    return c;
+}
+__device__ __forceinline__ int dist_code(int d) {
+    int c = 0;
+    while (c < 29 && cDistBase[c + 1] <= d) c++;
+    return c;
+}
+
+// Huffman code lengths (bgzf_ref.c bgzf_huffman_lengths), one thread, scratch in LDS
+struct HuffScratch {
+    uint32_t f[288];
+    int16_t leaf[288];
+    uint32_t w[576];
+    int16_t parent[576];
+};
+__device__ void huffman_lengths(const uint32_t *freq_in, int n, int limit, uint8_t *len, HuffScratch &s) {
+    for (int i = 0; i < n; i++) s.f[i] = freq_in[i];
+    for (;;) {
+        int nl = 0;
+        for (int i = 0; i < n; i++) {
+            len[i] = 0;
+            if (s.f[i]) s.leaf[nl++] = (int16_t)i;
+        }
+        if (nl == 0) return;
+        if (nl == 1) {
+            len[s.leaf[0]] = 1;
+            return;
+        }
+        for (int i = 1; i < nl; i++) {
+            const int x = s.leaf[i];
+            int j = i - 1;
+            while (j >= 0 && (s.f[s.leaf[j]] > s.f[x] || (s.f[s.leaf[j]] == s.f[x] && s.leaf[j] > x))) {
+                s.leaf[j + 1] = s.leaf[j];
+                j--;
+            }
+            s.leaf[j + 1] = (int16_t)x;
+        }
+        for (int i = 0; i < nl; i++) {
+            s.w[i] = s.f[s.leaf[i]];
+            s.parent[i] = -1;
+        }
+        int qa = 0, qi = nl, ni = nl;
+        for (int k = 0; k < nl - 1; k++) {
+            int pick[2];
+            for (int q = 0; q < 2; q++) {
+                if (qa < nl && (qi >= ni || s.w[qa] <= s.w[qi])) pick[q] = qa++;
+                else pick[q] = qi++;
+            }
+            s.w[ni] = s.w[pick[0]] + s.w[pick[1]];
+            s.parent[ni] = -1;
+            s.parent[pick[0]] = s.parent[pick[1]] = (int16_t)ni;
+            ni++;
+        }
+        // depths root-down: parents come after their children (the root is ni - 1); w reused
+        s.w[ni - 1] = 0;
+        int maxd = 0;
+        for (int i = ni - 2; i >= 0; i--) {
+            s.w[i] = s.w[s.parent[i]] + 1;
+            if (i < nl) {
+                len[s.leaf[i]] = (uint8_t)s.w[i];
+                maxd = ::max(maxd, (int)s.w[i]);
+            }
+        }
+        if (maxd <= limit) return;
+        for (int i = 0; i < n; i++)
+            if (s.f[i]) s.f[i] = (s.f[i] >> 1) | 1u;
+    }
+}
+__device__ void canonical_codes(const uint8_t *len, int n, uint16_t *code) {
+    int bl_count[16];
+    for (int b = 0; b < 16; b++) bl_count[b] = 0;
+    for (int i = 0; i < n; i++) bl_count[len[i]]++;
+    bl_count[0] = 0;
+    int next[16], c = 0;
+    next[0] = 0;
+    for (int b = 1; b < 16; b++) {
+        c = (c + bl_count[b - 1]) << 1;
+        next[b] = c;
+    }
+    for (int i = 0; i < n; i++) {
+        code[i] = 0;
+        if (!len[i]) continue;
+        const uint32_t v = (uint32_t)next[len[i]]++;
+        code[i] = (uint16_t)(__builtin_bitreverse32(v) >> (32 - len[i]));
+    }
+}
+
+// bit writer of one thread over its own bit range of the slot's words: the first and the last
+// word may be shared with a neighbour (atomicOr), the words in between are its own (stores)
+struct BitOut {
+    uint32_t *words;
+    int64_t bit;       // next bit position
+    int64_t first_w;   // the range's first word (shared)
+    uint64_t acc;      // pending bits, LSB first, of word (bit >> 5) onwards
+    int nacc;          // bits in acc
+    int64_t accw;      // word index of acc's bit 0
+    __device__ void init(uint32_t *w, int64_t b) {
+        words = w;
+        bit = b;
+        first_w = b >> 5;
+        accw = b >> 5;
+        acc = 0;
+        nacc = (int)(b & 31);  // bits of the first word below our range: zeros
+    }
+    __device__ void flush_word(bool last) {
+        const uint32_t v = (uint32_t)acc;
+        if (accw == first_w || last) atomicOr(words + accw, v);
+        else words[accw] = v;
+        acc >>= 32;
+        nacc -= 32;
+        accw++;
+    }
+    __device__ void put(uint32_t v, int n) {  // n <= 16
+        if (n == 0) return;
+        acc |= (uint64_t)(v & ((1u << n) - 1u)) << nacc;
+        nacc += n;
+        bit += n;
+        if (nacc >= 32) flush_word(false);
+    }
+    __device__ void finish() {
+        if (nacc > 0) flush_word(true);
+    }
+};
+
+struct __attribute__((aligned(16))) Smem {
+    uint8_t in[kBlock + 64];
+    uint32_t table[1 << kHashBits];
+    uint32_t lf[286], df[30], cf[19];
+    uint8_t ll[286], dl[30], cl[19];
+    uint16_t lc[286], dc[30], cc[19];
+    uint8_t sym[320], ext[320];
+    uint32_t bits[kT];
+    int32_t hdr_bits, ns, hlit, hdist, hclen, too_big;
+    HuffScratch hs;
+};
+
+__device__ __forceinline__ uint32_t hash4(const uint8_t *p) {
+    const uint32_t v = (uint32_t)p[0] | (uint32_t)p[1] << 8 | (uint32_t)p[2] << 16 | (uint32_t)p[3] << 24;
+    return (v * 2654435761u) >> (32 - kHashBits);
+}
+
+// the code-length sequence run-length coded (bgzf_ref.c bgzf_rle_lengths)
+__device__ int rle_lengths(const uint8_t *ll, int hlit, const uint8_t *dl, int hdist, uint8_t *sym, uint8_t *ext) {
+    auto L = [&](int i) { return i < hlit ? ll[i] : dl[i - hlit]; };
+    const int n = hlit + hdist;
+    int k = 0;
+    for (int i = 0; i < n;) {
+        const int v = L(i);
+        int run = 1;
+        while (i + run < n && L(i + run) == v) run++;
+        if (v == 0) {
+            int r = run;
+            while (r >= 11) {
+                const int t = r > 138 ? 138 : r;
+                sym[k] = 18;
+                ext[k++] = (uint8_t)(t - 11);
+                r -= t;
+            }
+            if (r >= 3) {
+                sym[k] = 17;
+                ext[k++] = (uint8_t)(r - 3);
+                r = 0;
+            }
+            while (r-- > 0) {
+                sym[k] = 0;
+                ext[k++] = 0;
+            }
+        } else {
+            sym[k] = (uint8_t)v;
+            ext[k++] = 0;
+            int r = run - 1;
+            while (r >= 3) {
+                const int t = r > 6 ? 6 : r;
+                sym[k] = 16;
+                ext[k++] = (uint8_t)(t - 3);
+                r -= t;
+            }
+            while (r-- > 0) {
+                sym[k] = (uint8_t)v;
+                ext[k++] = 0;
+            }
+        }
+        i += run;
+    }
+    return k;
+}
+
+// blocks blk0 .. blk0 + gridDim.x - 1 of in[0, n_total); slot b of `slots` (65536 bytes) receives
+// block blk0 + b's header and deflate bytes, sizes[blk0 + b] its BGZF size (0: does not fit)
+__global__ __launch_bounds__(kT, 1) void k_bgzf(const uint8_t *__restrict__ in_all, int64_t n_total, int64_t blk0,
+                                                 uint8_t *__restrict__ slots, int32_t *__restrict__ sizes,
+                                                 uint16_t *__restrict__ dist_scr, uint32_t *__restrict__ tok_scr) {
+    __shared__ Smem S;
+    const int t = threadIdx.x;
+    const int64_t blk = blk0 + blockIdx.x;
+    const int64_t base = blk * kBlock;
+    if (base >= n_total) return;
+    const int n = (int)::min<int64_t>(kBlock, n_total - base);
+    uint8_t *slot = slots + (size_t)blockIdx.x * 65536;
+    uint32_t *words = reinterpret_cast<uint32_t *>(slot + 16);  // the deflate data starts at byte 18 = bit 16 of word 0
+    uint16_t *dist = dist_scr + (size_t)blockIdx.x * 65536;
+    uint32_t *tok = tok_scr + (size_t)blockIdx.x * kBlock;
+
+    // ---- load the block (dwords, then the tail), clear the table, the frequencies, the slot ----
+    const uint8_t *src = in_all + base;
+    for (int i = t; i < n; i += kT) S.in[i] = src[i];
+    for (int i = n + t; i < kBlock + 64; i += kT) S.in[i] = 0;
+    for (int i = t; i < (1 << kHashBits); i += kT) S.table[i] = 0;
+    for (int i = t; i < 286; i += kT) S.lf[i] = 0;
+    if (t < 30) S.df[t] = 0;
+    for (int i = t; i < 65536 / 4; i += kT) reinterpret_cast<uint32_t *>(slot)[i] = 0;
+    __syncthreads();
+
+    // ---- A. candidates ----
+    for (int r0 = 0; r0 < n; r0 += kT) {
+        const int p = r0 + t;
+        uint32_t h = 0;
+        if (p < n) {
+            int32_t c = -1;
+            if (p + 3 < n) {
+                h = hash4(S.in + p);
+                c = (int32_t)S.table[h] - 1;
+            }
+            dist[p] = (uint16_t)(c >= 0 ? p - c : 0);
+        }
+        __syncthreads();
+        if (p + 3 < n) atomicMax(&S.table[h], (uint32_t)p + 1);
+        __syncthreads();
+    }
+    __threadfence_block();
+
+    // ---- B. greedy parse of this thread's segment ----
+    const int s0 = t * kSeg, s1 = ::min(n, s0 + kSeg);
+    int nt = 0;
+    uint32_t *mytok = tok + s0;
+    for (int i = s0; i < s1;) {
+        const int maxl = ::min(s1 - i, 258);
+        int bestl = 0, bestd = 0;
+        const int cd[4] = {1, 2, 4, (int)dist[i]};
+        for (int c = 0; c < 4; c++) {
+            const int d = cd[c];
+            if (d <= 0 || d > i || d > kMaxDist) continue;
+            int l = 0;
+            while (l < maxl && S.in[i + l] == S.in[i - d + l]) l++;
+            if (l > bestl) {
+                bestl = l;
+                bestd = d;
+            }
+        }
+        if (bestl >= 3) {
+            mytok[nt++] = 0x80000000u | (uint32_t)bestl << 16 | (uint32_t)bestd;
+            atomicAdd(&S.lf[257 + len_code(bestl)], 1u);
+            atomicAdd(&S.df[dist_code(bestd)], 1u);
+            i += bestl;
+        } else {
+            mytok[nt++] = S.in[i];
+            atomicAdd(&S.lf[S.in[i]], 1u);
+            i++;
+        }
+    }
+    __syncthreads();
+
+    // ---- C. codes and the header (thread 0) ----
+    if (t == 0) {
+        S.lf[256]++;
+        huffman_lengths(S.lf, 286, 15, S.ll, S.hs);
+        huffman_lengths(S.df, 30, 15, S.dl, S.hs);
+        int used_d = 0;
+        for (int i = 0; i < 30; i++) used_d |= S.dl[i] != 0;
+        if (!used_d) S.dl[0] = 1;
+        int hlit = 286;
+        while (hlit > 257 && S.ll[hlit - 1] == 0) hlit--;
+        int hdist = 30;
+        while (hdist > 1 && S.dl[hdist - 1] == 0) hdist--;
+        const int ns = rle_lengths(S.ll, hlit, S.dl, hdist, S.sym, S.ext);
+        for (int i = 0; i < 19; i++) S.cf[i] = 0;
+        for (int i = 0; i < ns; i++) S.cf[S.sym[i]]++;
+        huffman_lengths(S.cf, 19, 7, S.cl, S.hs);
+        int hclen = 19;
+        while (hclen > 4 && S.cl[cClOrder[hclen - 1]] == 0) hclen--;
+        canonical_codes(S.ll, 286, S.lc);
+        canonical_codes(S.dl, 30, S.dc);
+        canonical_codes(S.cl, 19, S.cc);
+        int hb = 3 + 5 + 5 + 4 + 3 * hclen;
+        for (int i = 0; i < ns; i++) {
+            const int s = S.sym[i];
+            hb += S.cl[s] + (s == 16 ? 2 : s == 17 ? 3 : s == 18 ? 7 : 0);
+        }
+        S.hdr_bits = hb;
+        S.ns = ns;
+        S.hlit = hlit;
+        S.hdist = hdist;
+        S.hclen = hclen;
+    }
+    __syncthreads();
+
+    // ---- D. bits per thread, offsets ----
+    uint32_t mb = 0;
+    for (int k = 0; k < nt; k++) {
+        const uint32_t x = mytok[k];
+        if (!(x >> 31)) {
+            mb += S.ll[x];
+        } else {
+            const int l = (int)((x >> 16) & 0x1FF), d = (int)(x & 0xFFFF);
+            const int c = len_code(l), e = dist_code(d);
+            mb += S.ll[257 + c] + cLenExtra[c] + S.dl[e] + cDistExtra[e];
+        }
+    }
+    if (t == kT - 1) mb += S.ll[256];  // end of block
+    S.bits[t] = mb;
+    __syncthreads();
+    // exclusive scan over the 256 counts (one wave per 64, then the wave totals)
+    int64_t off = S.hdr_bits;
+    for (int j = 0; j < t; j++) off += S.bits[j];
+    int64_t total = S.hdr_bits;
+    for (int j = 0; j < kT; j++) total += S.bits[j];
+    const int64_t clen = (total + 7) >> 3;
+    if (clen > kOutCap) {  // does not fit: the host stores this block
+        if (t == 0) sizes[blk] = 0;
+        return;
+    }
+
+    // ---- E. the bits: header (thread 0, from bit 0), then every thread's tokens ----
+    // the slot's words start 16 bytes in, so deflate bit b is bit 16 + b of the word stream
+    BitOut o;
+    if (t == 0) {
+        o.init(words, 16);
+        o.put(1, 1);
+        o.put(2, 2);
+        o.put((uint32_t)(S.hlit - 257), 5);
+        o.put((uint32_t)(S.hdist - 1), 5);
+        o.put((uint32_t)(S.hclen - 4), 4);
+        for (int i = 0; i < S.hclen; i++) o.put(S.cl[cClOrder[i]], 3);
+        for (int i = 0; i < S.ns; i++) {
+            const int s = S.sym[i];
+            o.put(S.cc[s], S.cl[s]);
+            if (s == 16) o.put(S.ext[i], 2);
+            if (s == 17) o.put(S.ext[i], 3);
+            if (s == 18) o.put(S.ext[i], 7);
+        }
+    } else {
+        o.init(words, 16 + off);
+    }
+    for (int k = 0; k < nt; k++) {
+        const uint32_t x = mytok[k];
+        if (!(x >> 31)) {
+            o.put(S.lc[x], S.ll[x]);
+            continue;
+        }
+        const int l = (int)((x >> 16) & 0x1FF), d = (int)(x & 0xFFFF);
+        const int c = len_code(l), e = dist_code(d);
+        o.put(S.lc[257 + c], S.ll[257 + c]);
+        o.put((uint32_t)(l - cLenBase[c]), cLenExtra[c]);
+        o.put(S.dc[e], S.dl[e]);
+        o.put((uint32_t)(d - cDistBase[e]), cDistExtra[e]);
+    }
+    if (t == kT - 1) o.put(S.lc[256], S.ll[256]);
+    o.finish();
+    __syncthreads();
+    if (t == 0) {  // the gzip header with the BC extra field (bytes 16-17 = BSIZE - 1)
+        const int bsize = (int)(18 + clen + 8);
+        const uint8_t hdr[16] = {31, 139, 8, 4, 0, 0, 0, 0, 0, 255, 6, 0, 'B', 'C', 2, 0};
+        uint32_t w0 = 0, w1 = 0, w2 = 0, w3 = 0;
+        for (int i = 0; i < 4; i++) {
+            w0 |= (uint32_t)hdr[i] << (8 * i);
+            w1 |= (uint32_t)hdr[4 + i] << (8 * i);
+            w2 |= (uint32_t)hdr[8 + i] << (8 * i);
+            w3 |= (uint32_t)hdr[12 + i] << (8 * i);
+        }
+        uint32_t *sw = reinterpret_cast<uint32_t *>(slot);
+        sw[0] = w0;
+        sw[1] = w1;
+        sw[2] = w2;
+        sw[3] = w3;
+        // word 4 holds BSIZE - 1 in its low 16 bits and the first deflate bits above: OR it in
+        atomicOr(sw + 4, (uint32_t)(bsize - 1) & 0xFFFFu);
+        sizes[blk] = bsize;
+    }
+}
+
+// the blocks' bytes back to back: block b's first sizes[b] bytes to out + offs[b]
+__global__ void k_bgzf_pack(const uint8_t *__restrict__ slots, const int32_t *__restrict__ sizes,
+                            const int64_t *__restrict__ offs, uint8_t *__restrict__ out, int64_t blk0) {
+    const int64_t b = blockIdx.x;
+    const int n = sizes[blk0 + b];
+    const uint8_t *s = slots + (size_t)b * 65536;
+    uint8_t *d = out + offs[blk0 + b];
+    for (int i = threadIdx.x; i < n; i += blockDim.x) d[i] = s[i];
+}
+
+}  // namespace
+
+extern "C" {
+
+// BGZF compression of a device byte stream (include/bsdc.h): blocks of 65280 bytes, max_blocks
+// at a time.  bsdc_bgzf_deflate compresses blocks blk0 .. blk0 + nblk - 1 into the scratch's
+// slots and writes their sizes (BGZF block size with the 8 trailer bytes counted but not written;
+// 0 = the block does not fit and is stored by the host); bsdc_bgzf_pack then copies each slot's
+// bytes to out + offs[b] (offsets from the sizes, on the host).
+int64_t bsdc_bgzf_scratch_bytes(int64_t max_blocks) {
+    return max_blocks * (65536 + 65536 * 2 + (int64_t)kBlock * 4);
+}
+
+int32_t bsdc_bgzf_deflate(const uint8_t *d_in, int64_t n, int64_t blk0, int64_t nblk, uint8_t *d_scratch,
+                          int32_t *d_sizes, void *stream) {
+    if (nblk <= 0) return 0;
+    if (blk0 * kBlock >= n) return -22;
+    uint8_t *slots = d_scratch;
+    uint16_t *dist = reinterpret_cast<uint16_t *>(d_scratch + nblk * 65536);
+    uint32_t *tok = reinterpret_cast<uint32_t *>(d_scratch + nblk * (65536 + 65536 * 2));
+    hipLaunchKernelGGL(k_bgzf, dim3((unsigned)nblk), dim3(kT), 0, (hipStream_t)stream, d_in, n, blk0, slots, d_sizes,
+                       dist, tok);
+    return hipGetLastError() == hipSuccess ? 0 : -5;
+}
+
+int32_t bsdc_bgzf_pack(const uint8_t *d_scratch, const int32_t *d_sizes, const int64_t *d_offs, int64_t blk0,
+                       int64_t nblk, uint8_t *d_out, void *stream) {
+    if (nblk <= 0) return 0;
+    hipLaunchKernelGGL(k_bgzf_pack, dim3((unsigned)nblk), dim3(256), 0, (hipStream_t)stream, d_scratch, d_sizes, d_offs,
+                       d_out, blk0);
+    return hipGetLastError() == hipSuccess ? 0 : -5;
+}
+
+}  // extern "C"

@@ -1468,6 +1468,57 @@ extern "C" int32_t bsdc_bam_writer_add(bsdc_bam_writer *w, const bsdc_bam_record
     return 0;
 }
 
+// The GPU-compressed write path (bsdc_bgzf_deflate in libbsdc): encode, let the caller compress
+// the whole blocks on the GPU, then hand the compressed blocks back to be finished and written.
+extern "C" int64_t bsdc_bam_writer_encode(bsdc_bam_writer *w, const bsdc_bam_records *r, int32_t n_threads,
+                                          const uint8_t **data) {
+    set_threads(n_threads);
+    const int32_t rc = encode_records(r, w->tail);
+    if (rc != 0) return rc;
+    *data = w->tail.data();
+    return ((int64_t)w->tail.size() / kBlock) * kBlock;
+}
+
+// The first nblk whole blocks of the encoded tail, compressed elsewhere: block b's BGZF bytes are
+// packed[off_b .. off_b + sizes[b]) (off = running sum of sizes), complete but for CRC32 and ISIZE,
+// which are filled in here from the uncompressed bytes; a block of size 0 did not fit and is
+// deflated here (stored when incompressible).  Then the blocks are written in order and the
+// consumed bytes leave the tail.
+extern "C" int32_t bsdc_bam_writer_put_blocks(bsdc_bam_writer *w, int64_t nblk, uint8_t *packed, const int32_t *sizes,
+                                              int32_t n_threads) {
+    set_threads(n_threads);
+    if (nblk * kBlock > (int64_t)w->tail.size()) return fail(BSDC_IO_EFORMAT, "more blocks than encoded bytes");
+    std::vector<int64_t> off((size_t)nblk + 1, 0);
+    for (int64_t b = 0; b < nblk; b++) off[(size_t)b + 1] = off[(size_t)b] + std::max(sizes[b], 0);
+    const uint8_t *src0 = w->tail.data();
+    int bad = 0;
+#pragma omp parallel for schedule(static) reduction(| : bad)
+    for (int64_t b = 0; b < nblk; b++) {
+        const int32_t bs = sizes[b];
+        if (bs <= 0) continue;
+        if (bs < 26 || bs > 65536) {
+            bad |= 1;
+            continue;
+        }
+        uint8_t *h = packed + off[(size_t)b];
+        wr32(h + bs - 8, crc32_of(src0 + b * kBlock, kBlock));
+        wr32(h + bs - 4, (uint32_t)kBlock);
+    }
+    if (bad) return fail(BSDC_IO_EFORMAT, "bad compressed block size");
+    for (int64_t b = 0; b < nblk; b++) {
+        int32_t rc = 0;
+        if (sizes[b] > 0) {
+            if (fwrite(packed + off[(size_t)b], 1, (size_t)sizes[b], w->f) != (size_t)sizes[b])
+                rc = fail(BSDC_IO_EIO, "BGZF write failed");
+        } else {
+            rc = deflate_write(w->f, src0 + b * kBlock, kBlock, w->level);
+        }
+        if (rc != 0) return rc;
+    }
+    w->tail.erase(w->tail.begin(), w->tail.begin() + nblk * kBlock);
+    return 0;
+}
+
 extern "C" int32_t bsdc_bam_writer_close(bsdc_bam_writer *w, int32_t n_threads) {
     if (!w) return 0;
     set_threads(n_threads);

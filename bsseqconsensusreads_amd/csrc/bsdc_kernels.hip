@@ -236,8 +236,11 @@ __device__ __forceinline__ bool near_tie(T d0, T d1, T d2, T d3, int best, int n
 // is found by selection: each step takes the smallest (length desc, address) key above the last.
 // Desc::get(i, addr, len, rev): the set's i-th read; its column col is image byte addr + col
 // (forward) or addr - col (reverse); bases at bimg, quals at qimg, same offsets.
+#ifndef FP64_PICK_ATTR
+#define FP64_PICK_ATTR __attribute__((noinline))  // rare path: out of line, off the vote's registers
+#endif
 template <class Desc>
-__device__ int fp64_pick(const Desc &ds, int n, int col, const uint8_t *bimg, const uint8_t *qimg, const double *lnc,
+__device__ FP64_PICK_ATTR int fp64_pick(const Desc &ds, int n, int col, const uint8_t *bimg, const uint8_t *qimg, const double *lnc,
                          const double *lne3) {
     double L0 = 0.0, L1 = 0.0, L2 = 0.0, L3 = 0.0;
     uint64_t lo = 0;

@@ -171,6 +171,20 @@ void bsdc_agree_tables(double error_rate_pre_umi, double error_rate_post_umi, ui
    bucket of S ((float bits >> 21) - ((127 - 32) << 2), clamped to [0, 135]). */
 void bsdc_phred_buckets(double error_rate_pre_umi, double error_rate_post_umi, uint8_t *sq144);
 
+/* BGZF compression of the output BAM on the GPU (replaces the deflate of fgbio's / htsjdk's BAM
+   writer behind CallDuplexConsensusReads --output, main.snake.py:159-163; csrc/bsdc_bgzf.hip):
+   device bytes in[0, n) as blocks of 65280 bytes, one dynamic-Huffman DEFLATE block each.
+   bsdc_bgzf_deflate compresses blocks blk0 .. blk0 + nblk - 1 into the scratch
+   (bsdc_bgzf_scratch_bytes(nblk) bytes) and writes sizes[blk0 + b]: the BGZF block size, its
+   CRC32 / ISIZE trailer counted but left to the host (libbsdc_io bsdc_bam_writer_put_blocks), or
+   0 when the block does not fit (the host deflates it).  bsdc_bgzf_pack then copies block b's
+   bytes from the scratch to out + offs[blk0 + b].  Device pointers; stream = hipStream_t. */
+int64_t bsdc_bgzf_scratch_bytes(int64_t max_blocks);
+int32_t bsdc_bgzf_deflate(const uint8_t *in, int64_t n, int64_t blk0, int64_t nblk, uint8_t *scratch,
+                          int32_t *sizes, void *stream);
+int32_t bsdc_bgzf_pack(const uint8_t *scratch, const int32_t *sizes, const int64_t *offs, int64_t blk0,
+                       int64_t nblk, uint8_t *out, void *stream);
+
 #ifdef __cplusplus
 }
 #endif

@@ -81,6 +81,8 @@ def load():
         lib.orc_get_sources.argtypes = [C.c_void_p] + [C.c_void_p] * 4
         lib.orc_check_agree.restype = C.c_int64
         lib.orc_check_agree.argtypes = [C.c_void_p, C.c_void_p, C.c_void_p, C.c_int64]
+        lib.bgzf_ref_block.restype = C.c_int
+        lib.bgzf_ref_block.argtypes = [C.c_void_p, C.c_int, C.c_void_p]
         _lib = lib
     return _lib
 
@@ -327,3 +329,34 @@ def check_agree_tables(qlo, dthr, thr, dmax) -> int:
     dthr = np.ascontiguousarray(dthr, np.int32)
     thr = np.ascontiguousarray(thr, np.float32)
     return int(load().orc_check_agree(_ptr(qlo), _ptr(dthr), _ptr(thr), int(dmax)))
+
+
+def bgzf_block(data: bytes) -> bytes:
+    """One BGZF block of `data` (<= 65280 bytes) by the restatement of the GPU encoder
+    (bgzf_ref.c), CRC32 and ISIZE included; b"" when it would not fit (stored by the writer)."""
+    lib = load()
+    src = np.frombuffer(bytes(data) + b"\0" * 8, np.uint8)
+    out = np.zeros(65536, np.uint8)
+    n = lib.bgzf_ref_block(src.ctypes.data, len(data), out.ctypes.data)
+    return out[:n].tobytes()
+
+
+class BgzfStandIn:
+    """bam.GpuBgzf's interface on the CPU with bgzf_block: the BAM writer's GPU-compressed path
+    (encode, packed blocks, CRC / ISIZE filled by the writer) exercised without a GPU."""
+
+    def __init__(self):
+        self.blocks = 0
+
+    def compress(self, data_ptr: int, nbytes: int):
+        host = np.ctypeslib.as_array(C.cast(data_ptr, C.POINTER(C.c_uint8)), shape=(nbytes,))
+        parts, sizes = [], []
+        for b in range(nbytes // 65280):
+            blk = bgzf_block(host[b * 65280:(b + 1) * 65280].tobytes())
+            if len(blk) and b % 7 == 3:  # every 7th block as if it did not fit: the writer deflates it
+                blk = b""
+            parts.append(blk)
+            sizes.append(len(blk))
+        self.blocks += len(sizes)
+        packed = np.frombuffer(b"".join(parts) or b"\0", np.uint8).copy()
+        return packed, np.asarray(sizes, np.int32)

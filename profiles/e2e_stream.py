@@ -70,9 +70,9 @@ def child(args):
         info = bam.step5_stream(args.inp, args.fa, None, engine=eng, threads=args.threads, level=args.level,
                                 fastq=(args.out + ".1.fq.gz", args.out + ".2.fq.gz"),
                                 chunk_bytes=args.chunk_mb << 20, stats=stats)
-    else:
+    else:  # stream, or stream_gpubgzf: the BAM's blocks deflated on the GPU (bam.GpuBgzf)
         info = bam.step5_stream(args.inp, args.fa, args.out, engine=eng, threads=args.threads, level=args.level,
-                                chunk_bytes=args.chunk_mb << 20, stats=stats)
+                                chunk_bytes=args.chunk_mb << 20, stats=stats, gpu_bgzf=args.mode == "stream_gpubgzf")
     dt = time.perf_counter() - t0
     eng.close()
     ru = resource.getrusage(resource.RUSAGE_SELF)
@@ -128,8 +128,16 @@ def main():
         res[mode] = r
         outs[mode] = out
         print(mode, json.dumps(r), flush=True)
-    bams = [open(outs[m], "rb").read() for m in outs if m != "stream_fastq"]
+    bams = [open(outs[m], "rb").read() for m in outs if m not in ("stream_fastq", "stream_gpubgzf")]
     res["outputs_identical"] = all(b == bams[0] for b in bams)
+    if "stream_gpubgzf" in outs and "stream" in outs:  # other compressed bytes: compare the records
+        sys.path.insert(0, ROOT)
+        from bsseqconsensusreads_amd import bam as B
+        _, ra = B.read_bam(outs["stream"], a.threads)
+        _, rb = B.read_bam(outs["stream_gpubgzf"], a.threads)
+        res["gpubgzf_records_identical"] = bool(ra.n == rb.n and (ra.seq == rb.seq).all() and (ra.qual == rb.qual).all()
+                                                and (ra.aux.buf == rb.aux.buf).all())
+        res["gpubgzf_size_ratio"] = round(os.path.getsize(outs["stream_gpubgzf"]) / os.path.getsize(outs["stream"]), 3)
     print(json.dumps(res))
     return 0
 
