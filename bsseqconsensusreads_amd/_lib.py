@@ -8,7 +8,7 @@ HERE = os.path.dirname(os.path.abspath(__file__))
 # BSDC_LIB_PATH: an alternative build of the same library (profiling A/B runs only)
 LIB_PATH = os.environ.get("BSDC_LIB_PATH") or os.path.join(HERE, "libbsdc.so")
 
-BSDC_ABI_VERSION = 8
+BSDC_ABI_VERSION = 9
 SMALL_BUCKETS = 8  # BSDC_SMALL_BUCKETS
 LARGE_BUCKETS = 6  # BSDC_LARGE_BUCKETS
 MODE_CONVERT, MODE_EXTEND, MODE_VOTE, MODE_DUMP = 1, 2, 4, 8
@@ -90,7 +90,7 @@ def load(path: str = LIB_PATH):
     lib.bsdc_bgzf_scratch_bytes.restype = C.c_int64
     lib.bsdc_bgzf_deflate.argtypes = [C.c_void_p, C.c_int64, C.c_int64, C.c_int64, C.c_void_p, C.c_void_p, C.c_void_p]
     lib.bsdc_bgzf_deflate.restype = C.c_int32
-    lib.bsdc_bgzf_pack.argtypes = [C.c_void_p, C.c_void_p, C.c_void_p, C.c_int64, C.c_int64, C.c_void_p, C.c_void_p]
+    lib.bsdc_bgzf_pack.argtypes = [C.c_void_p, C.c_void_p, C.c_int64, C.c_int64, C.c_void_p, C.c_void_p]
     lib.bsdc_bgzf_pack.restype = C.c_int32
     lib.bsdc_phred_buckets.argtypes = [C.c_double, C.c_double, C.c_void_p]
     lib.bsdc_phred_buckets.restype = None

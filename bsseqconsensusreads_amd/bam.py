@@ -30,7 +30,7 @@ from . import records as R
 
 IO_LIB_PATH = os.environ.get("BSDC_IO_LIB_PATH") or os.path.join(os.path.dirname(os.path.abspath(__file__)),
                                                                  "libbsdc_io.so")
-BSDC_IO_ABI_VERSION = 5
+BSDC_IO_ABI_VERSION = 6
 _P = C.c_void_p
 
 
@@ -91,8 +91,10 @@ def _load():
     lib.bsdc_bam_writer_add.restype = C.c_int32
     lib.bsdc_bam_writer_encode.argtypes = [_P, C.POINTER(_Records), C.c_int32, C.POINTER(C.c_void_p)]
     lib.bsdc_bam_writer_encode.restype = C.c_int64
-    lib.bsdc_bam_writer_put_blocks.argtypes = [_P, C.c_int64, _P, _P, C.c_int32]
-    lib.bsdc_bam_writer_put_blocks.restype = C.c_int32
+    lib.bsdc_bam_writer_take.argtypes = [_P, C.c_int64, _P, _P, C.c_int32]
+    lib.bsdc_bam_writer_take.restype = C.c_int32
+    lib.bsdc_bam_writer_put.argtypes = [_P, C.c_int64, _P, _P, _P, _P, C.c_int32]
+    lib.bsdc_bam_writer_put.restype = C.c_int32
     lib.bsdc_bam_writer_close.argtypes = [_P, C.c_int32]
     lib.bsdc_bam_writer_close.restype = C.c_int32
     lib.bsdc_fastq_writer_open.argtypes = [C.c_char_p, C.c_char_p, C.c_int32, C.POINTER(_P)]
@@ -574,9 +576,10 @@ def write_bam(path: str, header: BamHeader, recs: OutRecordsBam, level: int = 6,
 
 class GpuBgzf:
     """BGZF compression of a BAM writer's whole blocks on one GPU (libbsdc bsdc_bgzf_*,
-    csrc/bsdc_bgzf.hip): the encoded bytes go to HBM, one workgroup deflates each 65280-byte block,
-    the blocks come back packed; the writer fills their CRC32 / ISIZE and writes them.  Its own HIP
-    stream, so it overlaps the consensus kernels of the next chunk."""
+    csrc/bsdc_bgzf.hip): the encoded bytes go to HBM from a pinned staging slot, one workgroup
+    deflates each 65280-byte block, the blocks come back packed; the writer fills their CRC32 /
+    ISIZE and writes them.  Its own HIP stream, so it overlaps the consensus kernels; submit()
+    returns at once, so the writer encodes the next records while the GPU compresses these."""
 
     MAX_BLOCKS = 1024  # blocks per kernel launch (the scratch: bsdc_bgzf_scratch_bytes of these)
 
@@ -590,51 +593,94 @@ class GpuBgzf:
         self.stream = torch.cuda.Stream(self.dev)
         self.scratch = torch.empty(int(self.lib.bsdc_bgzf_scratch_bytes(self.MAX_BLOCKS)), dtype=torch.uint8,
                                    device=self.dev)
+        self.buf = {}  # grown on demand: device din / out / sizes, pinned sizes_h / out_h / raw0 / raw1
+        self.slot = 0
+        self.job = None  # the submitted, unfinished (nblk, event)
         self.blocks = 0
         self.bytes_in = 0
         self.bytes_out = 0
 
-    def compress(self, data_ptr: int, nbytes: int):
-        """host bytes [data_ptr, +nbytes) (whole blocks) -> (packed blocks, sizes int32[nblk])."""
+    def _buf(self, name, n, dtype=None, pinned=False):
         torch = self.torch
-        nblk = nbytes // 65280
-        host = np.ctypeslib.as_array(C.cast(data_ptr, C.POINTER(C.c_uint8)), shape=(nbytes,))
-        sizes_h = np.zeros(nblk, np.int32)
+        t = self.buf.get(name)
+        if t is None or t.numel() < n:
+            n = max(int(n * 1.25), 1)
+            t = (torch.empty(n, dtype=dtype or torch.uint8, pin_memory=True) if pinned else
+                 torch.empty(n, dtype=dtype or torch.uint8, device=self.dev))
+            self.buf[name] = t
+        return t
+
+    def staging(self, nbytes: int):
+        """the next pinned staging slot (two alternate: one may still feed the last submit)."""
+        self.slot ^= 1
+        return self._buf("raw%d" % self.slot, nbytes, pinned=True)
+
+    def submit(self, raw, nblk: int):
+        """launch the compression of nblk blocks from the pinned slot `raw` (staging()); one job in
+        flight: finish() the last one first."""
+        torch = self.torch
+        if self.job is not None:
+            raise RuntimeError("GpuBgzf.submit with a job in flight")
+        n = nblk * 65280
+        din = self._buf("din", n)
+        out = self._buf("out", nblk * 65536)
+        sizes = self._buf("sizes", nblk, torch.int32)
+        sizes_h = self._buf("sizes_h", nblk, torch.int32, pinned=True)
+        st = self.stream.cuda_stream
         with torch.cuda.stream(self.stream):
-            din = torch.from_numpy(host).to(self.dev, non_blocking=False)
-            sizes = torch.empty(nblk, dtype=torch.int32, device=self.dev)
-            out = torch.empty(nblk * 65536, dtype=torch.uint8, device=self.dev)
-            offs_h = np.zeros(nblk + 1, np.int64)
-            st = self.stream.cuda_stream
+            din[:n].copy_(raw[:n], non_blocking=True)
             for b0 in range(0, nblk, self.MAX_BLOCKS):
                 nb = min(self.MAX_BLOCKS, nblk - b0)
-                if self.lib.bsdc_bgzf_deflate(din.data_ptr(), nbytes, b0, nb, self.scratch.data_ptr(), sizes.data_ptr(),
+                if self.lib.bsdc_bgzf_deflate(din.data_ptr(), n, b0, nb, self.scratch.data_ptr(), sizes.data_ptr(),
                                               st) != 0:
                     raise RuntimeError("bsdc_bgzf_deflate failed")
-                sz = sizes[b0:b0 + nb].cpu().numpy()  # (synchronizes the stream)
-                sizes_h[b0:b0 + nb] = sz
-                offs_h[b0 + 1:b0 + nb + 1] = offs_h[b0] + np.cumsum(np.maximum(sz, 0).astype(np.int64))
-                offs = torch.from_numpy(offs_h).to(self.dev)
-                if self.lib.bsdc_bgzf_pack(self.scratch.data_ptr(), sizes.data_ptr(), offs.data_ptr(), b0, nb,
-                                           out.data_ptr(), st) != 0:
+                if self.lib.bsdc_bgzf_pack(self.scratch.data_ptr(), sizes.data_ptr(), b0, nb, out.data_ptr(), st) != 0:
                     raise RuntimeError("bsdc_bgzf_pack failed")
-            total = int(offs_h[nblk])
-            packed = out[:total].cpu().numpy() if total else np.zeros(1, np.uint8)
+            sizes_h[:nblk].copy_(sizes[:nblk], non_blocking=True)
+            ev = torch.cuda.Event()
+            ev.record(self.stream)
+        self.job = (nblk, ev)
+
+    def finish(self):
+        """wait for the submitted job -> (packed blocks: a pinned view valid until the next finish,
+        sizes int32[nblk])."""
+        nblk, ev = self.job
+        self.job = None
+        ev.synchronize()
+        sizes_h = self.buf["sizes_h"][:nblk].numpy().copy()
+        total = int(np.maximum(sizes_h, 0).sum(dtype=np.int64))
+        out_h = self._buf("out_h", max(total, 1), pinned=True)
+        if total:
+            with self.torch.cuda.stream(self.stream):
+                out_h[:total].copy_(self.buf["out"][:total], non_blocking=True)
+            self.stream.synchronize()
         self.blocks += nblk
-        self.bytes_in += nbytes
+        self.bytes_in += nblk * 65280
         self.bytes_out += total
-        return packed, sizes_h
+        return out_h.numpy(), sizes_h
+
+    def compress(self, data_ptr: int, nbytes: int):
+        """host bytes [data_ptr, +nbytes) (whole blocks) -> (packed blocks, sizes int32[nblk])."""
+        nblk = nbytes // 65280
+        host = np.ctypeslib.as_array(C.cast(data_ptr, C.POINTER(C.c_uint8)), shape=(nbytes,))
+        raw = self.staging(nbytes)
+        raw.numpy()[:nbytes] = host
+        self.submit(raw, nblk)
+        packed, sizes = self.finish()
+        return packed[:int(np.maximum(sizes, 0).sum())].copy(), sizes
 
 
 class BamWriter:
     """Streaming BAM writer (bsdc_bam_writer): header at open, records added in order, the same
     bytes as write_bam of all the records at once -- or, with `gpu` (a GpuBgzf), every whole block
-    deflated on the GPU (valid BGZF, other compressed bytes)."""
+    deflated on the GPU (valid BGZF, other compressed bytes), one add's blocks compressing while
+    the next add encodes."""
 
     def __init__(self, path: str, header: BamHeader, level: int = 6, gpu: Optional["GpuBgzf"] = None):
         self.lib = _load()
         self.path = path
         self.gpu = gpu
+        self.pending = None  # (nblk, crc, raw) submitted to the GPU, not yet written
         rn = StringTable.from_list([x.encode() for x in header.ref_names])
         keep = []
 
@@ -652,28 +698,51 @@ class BamWriter:
         if rc != 0:
             raise OSError("%s: %s" % (path, self.lib.bsdc_io_last_error().decode()))
 
+    def _err(self):
+        return OSError("%s: %s" % (self.path, self.lib.bsdc_io_last_error().decode()))
+
+    def _drain(self, threads: int):
+        if self.pending is None:
+            return
+        nblk, crc, raw = self.pending
+        self.pending = None
+        packed, sizes = self.gpu.finish()
+        if self.lib.bsdc_bam_writer_put(self.h, nblk, _ptr(packed), _ptr(sizes), _ptr(crc), raw.data_ptr(),
+                                        int(threads)) != 0:
+            raise self._err()
+
     def add(self, recs: OutRecordsBam, threads: int = 0):
         keep = []
         r = _records_struct(recs, keep)
         if self.gpu is None:
             if self.lib.bsdc_bam_writer_add(self.h, C.byref(r), int(threads)) != 0:
-                raise OSError("%s: %s" % (self.path, self.lib.bsdc_io_last_error().decode()))
+                raise self._err()
             return
         data = C.c_void_p()
         nbytes = self.lib.bsdc_bam_writer_encode(self.h, C.byref(r), int(threads), C.byref(data))
         if nbytes < 0:
-            raise OSError("%s: %s" % (self.path, self.lib.bsdc_io_last_error().decode()))
-        if nbytes == 0:
-            return
-        packed, sizes = self.gpu.compress(data.value, int(nbytes))
-        if self.lib.bsdc_bam_writer_put_blocks(self.h, sizes.shape[0], _ptr(packed), _ptr(sizes), int(threads)) != 0:
-            raise OSError("%s: %s" % (self.path, self.lib.bsdc_io_last_error().decode()))
+            raise self._err()
+        nblk = int(nbytes) // 65280
+        job = None
+        if nblk:
+            raw = self.gpu.staging(int(nbytes))
+            crc = np.empty(nblk, np.uint32)
+            if self.lib.bsdc_bam_writer_take(self.h, nblk, raw.data_ptr(), _ptr(crc), int(threads)) != 0:
+                raise self._err()
+            job = (nblk, crc, raw)
+        self._drain(threads)
+        if job is not None:
+            self.gpu.submit(job[2], nblk)
+            self.pending = job
 
     def close(self, threads: int = 0):
         if self.h:
-            h, self.h = self.h, _P()
-            if self.lib.bsdc_bam_writer_close(h, int(threads)) != 0:
-                raise OSError("%s: %s" % (self.path, self.lib.bsdc_io_last_error().decode()))
+            try:
+                self._drain(threads)
+            finally:
+                h, self.h = self.h, _P()
+                if self.lib.bsdc_bam_writer_close(h, int(threads)) != 0:
+                    raise self._err()
 
 
 class FastqWriter:
@@ -895,11 +964,13 @@ def step5_stream(in_bam: str, fasta: str, out_bam: Optional[str], engine=None, p
                  threads: int = 0, level: int = 6, fastq: Optional[Tuple[str, str]] = None, tags: bool = True,
                  chunk_bytes: int = DEFAULT_CHUNK_BYTES, slack: int = DEFAULT_SLACK,
                  batch_bases: Optional[int] = None, stats: Optional[dict] = None, gpu_bgzf: bool = False) -> dict:
-    """step5 in bounded memory, pipelined: a decoder thread decodes the next chunk of the
-    coordinate-sorted input (stream_bam: cut where no template or MI family straddles), a reader
-    thread forms the previous chunk's families (C++ plan); this thread runs the chunk's family
-    batches on the GPU; a writer thread builds the output records of the chunk before and appends
-    them to the BAM (BamWriter).  Peak host memory is about five chunks, whatever the file size.  The output is
+    """step5 in bounded memory, pipelined: a decoder thread cuts the next chunk of the
+    coordinate-sorted input (stream_bam: inflate, split where no template or MI family straddles),
+    a reader thread parses the chunk before, a planner thread forms the families of the one before
+    that (C++ plan) and materializes its batches into pinned memory; this thread uploads a chunk's
+    batches and runs them on the GPU; a builder thread builds
+    the output records of the chunk before and a writer thread appends them to the BAM
+    (BamWriter).  Peak host memory is about six chunks, whatever the file size.  The output is
     byte-identical to step5's (tests/test_stream.py): every chunk's TemplateCoordinate keys sort
     before the next chunk's, so the chunks' families in order are the whole file's.  gpu_bgzf: the
     BAM's blocks are deflated on the engine's GPU (GpuBgzf; the same records, other compressed
@@ -909,15 +980,15 @@ def step5_stream(in_bam: str, fasta: str, out_bam: Optional[str], engine=None, p
     import time
 
     from . import pipeline
-    from .device import Engine
+    from .device import Engine, PinnedPool
     own = engine is None
     eng = Engine(0) if own else engine
     chunks: "queue.Queue" = queue.Queue(maxsize=1)
     outs: "queue.Queue" = queue.Queue(maxsize=1)
     err: list = []
     info = {"records_in": 0, "families": 0, "families_emitted": 0, "records_out": 0, "chunks": 0}
-    T = {"decode": 0.0, "parse": 0.0, "plan": 0.0, "gpu": 0.0, "records": 0.0, "encode": 0.0, "gpu_wait": 0.0,
-         "writer_wait": 0.0}
+    T = {"decode": 0.0, "parse": 0.0, "plan": 0.0, "materialize": 0.0, "gpu": 0.0, "records": 0.0, "encode": 0.0,
+         "gpu_wait": 0.0, "writer_wait": 0.0}
     G: dict = {}  # the GPU stage's host steps (pipeline.run_ranges timing)
     first = {}
     stop = threading.Event()  # set on any failure: the decoder and planner stop at their next chunk
@@ -925,7 +996,7 @@ def step5_stream(in_bam: str, fasta: str, out_bam: Optional[str], engine=None, p
     raws: "queue.Queue" = queue.Queue(maxsize=1)
 
     def decoder():  # cuts the next chunk (inflate, split, family-complete selection) while the
-        # reader thread decodes and plans the one before
+        # reader thread parses the one before
         it = None
         try:
             it = stream_chunks(in_bam, threads, chunk_bytes, slack)
@@ -944,7 +1015,9 @@ def step5_stream(in_bam: str, fasta: str, out_bam: Optional[str], engine=None, p
                 it.close()  # (the stream is freed once every chunk is back)
             raws.put(None)
 
-    def reader():
+    parsed: "queue.Queue" = queue.Queue(maxsize=1)
+
+    def reader():  # parses a chunk's records while the planner forms the families of the one before
         try:
             while True:
                 ch = raws.get()
@@ -952,14 +1025,11 @@ def step5_stream(in_bam: str, fasta: str, out_bam: Optional[str], engine=None, p
                     break
                 if stop.is_set():
                     ch.discard()
-                    continue  # drain to the decoder's None without planning
+                    continue  # drain to the decoder's None without parsing
                 t0 = time.perf_counter()
                 raw = ch.decode(threads)[1]
-                t1 = time.perf_counter()
-                plan = pipeline.plan_families(raw, "full", first["ref"])
-                T["parse"] += t1 - t0
-                T["plan"] += time.perf_counter() - t1
-                chunks.put((raw, plan))
+                T["parse"] += time.perf_counter() - t0
+                parsed.put(raw)
         except BaseException as e:  # noqa: BLE001 -- handed to the main thread
             err.append(e)
             stop.set()
@@ -968,6 +1038,39 @@ def step5_stream(in_bam: str, fasta: str, out_bam: Optional[str], engine=None, p
                 if ch is None:
                     break
                 ch.discard()
+        finally:
+            parsed.put(None)
+
+    # the planner materializes chunk k's batches into pool k % 3: chunk k - 3 is done on the GPU
+    # by then (the planner handed chunk k - 1 over only after the GPU stage took chunk k - 2)
+    pools = [PinnedPool() for _ in range(3)]
+
+    def planner():  # forms a chunk's families and materializes its batches ahead of the GPU stage
+        try:
+            k = 0
+            while True:
+                raw = parsed.get()
+                if raw is None:
+                    break
+                if stop.is_set():
+                    continue  # drain to the reader's None without planning
+                t0 = time.perf_counter()
+                plan = pipeline.plan_families(raw, "full", first["ref"])
+                t1 = time.perf_counter()
+                fbs = None
+                if not plan.split_ext:
+                    pool = pools[k % 3]
+                    k += 1
+                    pool.reset()
+                    fbs = pipeline.materialize_ranges(plan, pipeline.plan_ranges(plan, batch_bases), pool.images)
+                T["plan"] += t1 - t0
+                T["materialize"] += time.perf_counter() - t1
+                chunks.put((raw, plan, fbs))
+        except BaseException as e:  # noqa: BLE001 -- handed to the main thread
+            err.append(e)
+            stop.set()
+            while parsed.get() is not None:  # let the reader finish
+                pass
         finally:
             chunks.put(None)
 
@@ -1030,10 +1133,12 @@ def step5_stream(in_bam: str, fasta: str, out_bam: Optional[str], engine=None, p
         eng.load_reference(ref)
         td = threading.Thread(target=decoder, daemon=True)
         tr = threading.Thread(target=reader, daemon=True)
+        tp = threading.Thread(target=planner, daemon=True)
         tb = threading.Thread(target=builder, daemon=True)
         tw = threading.Thread(target=writer, daemon=True)
         td.start()
         tr.start()
+        tp.start()
         tb.start()
         tw.start()
         mode = pipeline.MODE_CONVERT | pipeline.MODE_EXTEND | pipeline.MODE_VOTE
@@ -1048,14 +1153,14 @@ def step5_stream(in_bam: str, fasta: str, out_bam: Optional[str], engine=None, p
                     break
                 if stop.is_set():  # another stage failed: stop working, drain below
                     break
-                raw, plan = item
+                raw, plan, fbs = item
                 t0 = time.perf_counter()
                 tg = tags and out_bam is not None  # the FASTQ pair carries no tags
-                if plan.split_ext:
+                if fbs is None:
                     cons = pipeline.run_step5(eng, raw, tags=tg, batch_bases=batch_bases)[0]
                 else:
-                    cons = pipeline.concat_consensus(
-                        pipeline.run_ranges(eng, plan, pipeline.plan_ranges(plan, batch_bases), mode, tg, G))
+                    cons = pipeline.concat_consensus(pipeline.run_batches(eng, fbs, mode, tg, G))
+                    del fbs
                 T["gpu"] += time.perf_counter() - t0
                 info["records_in"] += raw.n
                 info["families"] += int(cons.status.shape[0])
@@ -1066,13 +1171,14 @@ def step5_stream(in_bam: str, fasta: str, out_bam: Optional[str], engine=None, p
             stop.set()
             raise
         finally:
-            if not drained:  # let the reader finish (it stops planning once `stop` is set)
+            if not drained:  # let the planner finish (it stops planning once `stop` is set)
                 stop.set()
                 while chunks.get() is not None:
                     pass
             outs.put(None)
             tb.join()
             tw.join()
+            tp.join()
             tr.join()
             td.join()
     finally:

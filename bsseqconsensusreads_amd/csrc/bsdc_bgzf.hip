@@ -28,7 +28,7 @@ namespace {
 constexpr int kT = 256;          // threads per block = positions per candidate round
 constexpr int kSeg = 255;        // bytes per thread segment (kT * kSeg = 65280 = BGZF block)
 constexpr int kBlock = kT * kSeg;
-constexpr int kHashBits = 12;
+constexpr int kHashBits = 11;  // 2048 slots: the block, the table and the rest fit 80 KB of LDS (2 workgroups per CU)
 constexpr int kMaxDist = 32768;
 constexpr int kOutCap = 65536 - 26;  // deflate bytes that still fit a BGZF block
 
@@ -51,64 +51,78 @@ __device__ __forceinline__ int dist_code(int d) {
     return c;
 }
 
-// Huffman code lengths (bgzf_ref.c bgzf_huffman_lengths), one thread, scratch in LDS
+// Huffman code lengths (bgzf_ref.c bgzf_huffman_lengths) by the whole workgroup: the leaves'
+// order by (frequency, symbol) as a parallel rank count (every thread ranks its symbols against
+// all), then thread 0 builds the two-queue tree and the depths; the frequency halving retry is
+// workgroup-uniform.  Same lengths as the restatement's insertion sort + build.
 struct HuffScratch {
     uint32_t f[288];
     int16_t leaf[288];
     uint32_t w[576];
     int16_t parent[576];
+    int32_t nl, maxd;
 };
 __device__ void huffman_lengths(const uint32_t *freq_in, int n, int limit, uint8_t *len, HuffScratch &s) {
-    for (int i = 0; i < n; i++) s.f[i] = freq_in[i];
+    const int t = threadIdx.x;
+    for (int i = t; i < n; i += blockDim.x) s.f[i] = freq_in[i];
+    __syncthreads();
     for (;;) {
-        int nl = 0;
-        for (int i = 0; i < n; i++) {
+        for (int i = t; i < n; i += blockDim.x) {
             len[i] = 0;
-            if (s.f[i]) s.leaf[nl++] = (int16_t)i;
-        }
-        if (nl == 0) return;
-        if (nl == 1) {
-            len[s.leaf[0]] = 1;
-            return;
-        }
-        for (int i = 1; i < nl; i++) {
-            const int x = s.leaf[i];
-            int j = i - 1;
-            while (j >= 0 && (s.f[s.leaf[j]] > s.f[x] || (s.f[s.leaf[j]] == s.f[x] && s.leaf[j] > x))) {
-                s.leaf[j + 1] = s.leaf[j];
-                j--;
+            const uint32_t fi = s.f[i];
+            if (!fi) continue;
+            int r = 0;
+            for (int j = 0; j < n; j++) {
+                const uint32_t fj = s.f[j];
+                r += fj != 0 && (fj < fi || (fj == fi && j < i));
             }
-            s.leaf[j + 1] = (int16_t)x;
+            s.leaf[r] = (int16_t)i;
         }
-        for (int i = 0; i < nl; i++) {
-            s.w[i] = s.f[s.leaf[i]];
-            s.parent[i] = -1;
+        if (t == 0) {
+            int nl = 0;
+            for (int i = 0; i < n; i++) nl += s.f[i] != 0;
+            s.nl = nl;
         }
-        int qa = 0, qi = nl, ni = nl;
-        for (int k = 0; k < nl - 1; k++) {
-            int pick[2];
-            for (int q = 0; q < 2; q++) {
-                if (qa < nl && (qi >= ni || s.w[qa] <= s.w[qi])) pick[q] = qa++;
-                else pick[q] = qi++;
+        __syncthreads();
+        if (t == 0) {
+            const int nl = s.nl;
+            int maxd = 0;
+            if (nl == 1) {
+                len[s.leaf[0]] = 1;
+            } else if (nl > 1) {
+                for (int i = 0; i < nl; i++) {
+                    s.w[i] = s.f[s.leaf[i]];
+                    s.parent[i] = -1;
+                }
+                int qa = 0, qi = nl, ni = nl;
+                for (int k = 0; k < nl - 1; k++) {
+                    int pick[2];
+                    for (int q = 0; q < 2; q++) {
+                        if (qa < nl && (qi >= ni || s.w[qa] <= s.w[qi])) pick[q] = qa++;
+                        else pick[q] = qi++;
+                    }
+                    s.w[ni] = s.w[pick[0]] + s.w[pick[1]];
+                    s.parent[ni] = -1;
+                    s.parent[pick[0]] = s.parent[pick[1]] = (int16_t)ni;
+                    ni++;
+                }
+                // depths root-down: parents come after their children (the root is ni - 1); w reused
+                s.w[ni - 1] = 0;
+                for (int i = ni - 2; i >= 0; i--) {
+                    s.w[i] = s.w[s.parent[i]] + 1;
+                    if (i < nl) {
+                        len[s.leaf[i]] = (uint8_t)s.w[i];
+                        maxd = ::max(maxd, (int)s.w[i]);
+                    }
+                }
             }
-            s.w[ni] = s.w[pick[0]] + s.w[pick[1]];
-            s.parent[ni] = -1;
-            s.parent[pick[0]] = s.parent[pick[1]] = (int16_t)ni;
-            ni++;
+            s.maxd = maxd;
         }
-        // depths root-down: parents come after their children (the root is ni - 1); w reused
-        s.w[ni - 1] = 0;
-        int maxd = 0;
-        for (int i = ni - 2; i >= 0; i--) {
-            s.w[i] = s.w[s.parent[i]] + 1;
-            if (i < nl) {
-                len[s.leaf[i]] = (uint8_t)s.w[i];
-                maxd = ::max(maxd, (int)s.w[i]);
-            }
-        }
-        if (maxd <= limit) return;
-        for (int i = 0; i < n; i++)
+        __syncthreads();
+        if (s.maxd <= limit) return;
+        for (int i = t; i < n; i += blockDim.x)
             if (s.f[i]) s.f[i] = (s.f[i] >> 1) | 1u;
+        __syncthreads();
     }
 }
 __device__ void canonical_codes(const uint8_t *len, int n, uint16_t *code) {
@@ -167,17 +181,24 @@ struct BitOut {
     }
 };
 
+struct Late {  // phases C-D: in the hash table's place (dead after phase A)
+    HuffScratch hs;
+    uint8_t sym[320], ext[320];
+    uint32_t bits[kT];
+};
 struct __attribute__((aligned(16))) Smem {
-    uint8_t in[kBlock + 64];
-    uint32_t table[1 << kHashBits];
+    uint8_t in[kBlock];
+    union {
+        uint32_t table[1 << kHashBits];
+        Late late;
+    } u;
     uint32_t lf[286], df[30], cf[19];
     uint8_t ll[286], dl[30], cl[19];
     uint16_t lc[286], dc[30], cc[19];
-    uint8_t sym[320], ext[320];
-    uint32_t bits[kT];
-    int32_t hdr_bits, ns, hlit, hdist, hclen, too_big;
-    HuffScratch hs;
+    int32_t hdr_bits, ns, hlit, hdist, hclen;
 };
+static_assert(sizeof(Late) <= sizeof(uint32_t) << kHashBits, "phase C-D scratch fits the table");
+static_assert(sizeof(Smem) <= 80 * 1024, "two workgroups per CU");
 
 __device__ __forceinline__ uint32_t hash4(const uint8_t *p) {
     const uint32_t v = (uint32_t)p[0] | (uint32_t)p[1] << 8 | (uint32_t)p[2] << 16 | (uint32_t)p[3] << 24;
@@ -232,7 +253,7 @@ __device__ int rle_lengths(const uint8_t *ll, int hlit, const uint8_t *dl, int h
 
 // blocks blk0 .. blk0 + gridDim.x - 1 of in[0, n_total); slot b of `slots` (65536 bytes) receives
 // block blk0 + b's header and deflate bytes, sizes[blk0 + b] its BGZF size (0: does not fit)
-__global__ __launch_bounds__(kT, 1) void k_bgzf(const uint8_t *__restrict__ in_all, int64_t n_total, int64_t blk0,
+__global__ __launch_bounds__(kT, 2) void k_bgzf(const uint8_t *__restrict__ in_all, int64_t n_total, int64_t blk0,
                                                  uint8_t *__restrict__ slots, int32_t *__restrict__ sizes,
                                                  uint16_t *__restrict__ dist_scr, uint32_t *__restrict__ tok_scr) {
     __shared__ Smem S;
@@ -248,15 +269,16 @@ __global__ __launch_bounds__(kT, 1) void k_bgzf(const uint8_t *__restrict__ in_a
 
     // ---- load the block (dwords, then the tail), clear the table, the frequencies, the slot ----
     const uint8_t *src = in_all + base;
-    for (int i = t; i < n; i += kT) S.in[i] = src[i];
-    for (int i = n + t; i < kBlock + 64; i += kT) S.in[i] = 0;
-    for (int i = t; i < (1 << kHashBits); i += kT) S.table[i] = 0;
+    for (int i = t; i < n; i += kT) S.in[i] = src[i];  // (nothing reads past n)
+    for (int i = t; i < (1 << kHashBits); i += kT) S.u.table[i] = 0;
     for (int i = t; i < 286; i += kT) S.lf[i] = 0;
     if (t < 30) S.df[t] = 0;
     for (int i = t; i < 65536 / 4; i += kT) reinterpret_cast<uint32_t *>(slot)[i] = 0;
     __syncthreads();
 
-    // ---- A. candidates ----
+    // ---- A. candidates.  The round barriers only order the LDS table (s_waitcnt lgkmcnt(0) +
+    // s_barrier): a __syncthreads() would also wait for every round's HBM stores of `dist`, which
+    // only phase B reads, after the full barrier below ----
     for (int r0 = 0; r0 < n; r0 += kT) {
         const int p = r0 + t;
         uint32_t h = 0;
@@ -264,15 +286,19 @@ __global__ __launch_bounds__(kT, 1) void k_bgzf(const uint8_t *__restrict__ in_a
             int32_t c = -1;
             if (p + 3 < n) {
                 h = hash4(S.in + p);
-                c = (int32_t)S.table[h] - 1;
+                c = (int32_t)S.u.table[h] - 1;
             }
             dist[p] = (uint16_t)(c >= 0 ? p - c : 0);
         }
-        __syncthreads();
-        if (p + 3 < n) atomicMax(&S.table[h], (uint32_t)p + 1);
-        __syncthreads();
+        asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+        __builtin_amdgcn_s_barrier();
+        asm volatile("" ::: "memory");
+        if (p + 3 < n) atomicMax(&S.u.table[h], (uint32_t)p + 1);
+        asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+        __builtin_amdgcn_s_barrier();
+        asm volatile("" ::: "memory");
     }
-    __threadfence_block();
+    __syncthreads();  // (the dist stores, for phase B)
 
     // ---- B. greedy parse of this thread's segment ----
     const int s0 = t * kSeg, s1 = ::min(n, s0 + kSeg);
@@ -305,11 +331,12 @@ __global__ __launch_bounds__(kT, 1) void k_bgzf(const uint8_t *__restrict__ in_a
     }
     __syncthreads();
 
-    // ---- C. codes and the header (thread 0) ----
+    // ---- C. codes (the Huffman builds by the workgroup) and the header (thread 0) ----
+    if (t == 0) S.lf[256]++;
+    __syncthreads();
+    huffman_lengths(S.lf, 286, 15, S.ll, S.u.late.hs);
+    huffman_lengths(S.df, 30, 15, S.dl, S.u.late.hs);
     if (t == 0) {
-        S.lf[256]++;
-        huffman_lengths(S.lf, 286, 15, S.ll, S.hs);
-        huffman_lengths(S.df, 30, 15, S.dl, S.hs);
         int used_d = 0;
         for (int i = 0; i < 30; i++) used_d |= S.dl[i] != 0;
         if (!used_d) S.dl[0] = 1;
@@ -317,10 +344,17 @@ __global__ __launch_bounds__(kT, 1) void k_bgzf(const uint8_t *__restrict__ in_a
         while (hlit > 257 && S.ll[hlit - 1] == 0) hlit--;
         int hdist = 30;
         while (hdist > 1 && S.dl[hdist - 1] == 0) hdist--;
-        const int ns = rle_lengths(S.ll, hlit, S.dl, hdist, S.sym, S.ext);
+        const int ns = rle_lengths(S.ll, hlit, S.dl, hdist, S.u.late.sym, S.u.late.ext);
         for (int i = 0; i < 19; i++) S.cf[i] = 0;
-        for (int i = 0; i < ns; i++) S.cf[S.sym[i]]++;
-        huffman_lengths(S.cf, 19, 7, S.cl, S.hs);
+        for (int i = 0; i < ns; i++) S.cf[S.u.late.sym[i]]++;
+        S.ns = ns;
+        S.hlit = hlit;
+        S.hdist = hdist;
+    }
+    __syncthreads();
+    huffman_lengths(S.cf, 19, 7, S.cl, S.u.late.hs);
+    if (t == 0) {
+        const int ns = S.ns;
         int hclen = 19;
         while (hclen > 4 && S.cl[cClOrder[hclen - 1]] == 0) hclen--;
         canonical_codes(S.ll, 286, S.lc);
@@ -328,13 +362,10 @@ __global__ __launch_bounds__(kT, 1) void k_bgzf(const uint8_t *__restrict__ in_a
         canonical_codes(S.cl, 19, S.cc);
         int hb = 3 + 5 + 5 + 4 + 3 * hclen;
         for (int i = 0; i < ns; i++) {
-            const int s = S.sym[i];
+            const int s = S.u.late.sym[i];
             hb += S.cl[s] + (s == 16 ? 2 : s == 17 ? 3 : s == 18 ? 7 : 0);
         }
         S.hdr_bits = hb;
-        S.ns = ns;
-        S.hlit = hlit;
-        S.hdist = hdist;
         S.hclen = hclen;
     }
     __syncthreads();
@@ -352,13 +383,13 @@ __global__ __launch_bounds__(kT, 1) void k_bgzf(const uint8_t *__restrict__ in_a
         }
     }
     if (t == kT - 1) mb += S.ll[256];  // end of block
-    S.bits[t] = mb;
+    S.u.late.bits[t] = mb;
     __syncthreads();
     // exclusive scan over the 256 counts (one wave per 64, then the wave totals)
     int64_t off = S.hdr_bits;
-    for (int j = 0; j < t; j++) off += S.bits[j];
+    for (int j = 0; j < t; j++) off += S.u.late.bits[j];
     int64_t total = S.hdr_bits;
-    for (int j = 0; j < kT; j++) total += S.bits[j];
+    for (int j = 0; j < kT; j++) total += S.u.late.bits[j];
     const int64_t clen = (total + 7) >> 3;
     if (clen > kOutCap) {  // does not fit: the host stores this block
         if (t == 0) sizes[blk] = 0;
@@ -377,11 +408,11 @@ __global__ __launch_bounds__(kT, 1) void k_bgzf(const uint8_t *__restrict__ in_a
         o.put((uint32_t)(S.hclen - 4), 4);
         for (int i = 0; i < S.hclen; i++) o.put(S.cl[cClOrder[i]], 3);
         for (int i = 0; i < S.ns; i++) {
-            const int s = S.sym[i];
+            const int s = S.u.late.sym[i];
             o.put(S.cc[s], S.cl[s]);
-            if (s == 16) o.put(S.ext[i], 2);
-            if (s == 17) o.put(S.ext[i], 3);
-            if (s == 18) o.put(S.ext[i], 7);
+            if (s == 16) o.put(S.u.late.ext[i], 2);
+            if (s == 17) o.put(S.u.late.ext[i], 3);
+            if (s == 18) o.put(S.u.late.ext[i], 7);
         }
     } else {
         o.init(words, 16 + off);
@@ -423,13 +454,23 @@ __global__ __launch_bounds__(kT, 1) void k_bgzf(const uint8_t *__restrict__ in_a
     }
 }
 
-// the blocks' bytes back to back: block b's first sizes[b] bytes to out + offs[b]
+// the blocks' bytes back to back: block b's first sizes[b] bytes to out + the sum of the sizes
+// before it (this launch's and the earlier launches' blocks of the same stream: at most a few
+// thousand, summed by the workgroup, so the host need not wait for the sizes between launches)
 __global__ void k_bgzf_pack(const uint8_t *__restrict__ slots, const int32_t *__restrict__ sizes,
-                            const int64_t *__restrict__ offs, uint8_t *__restrict__ out, int64_t blk0) {
+                            uint8_t *__restrict__ out, int64_t blk0) {
+    __shared__ int64_t part[256 / 64];
     const int64_t b = blockIdx.x;
-    const int n = sizes[blk0 + b];
+    const int64_t upto = blk0 + b;
+    int64_t acc = 0;
+    for (int64_t j = threadIdx.x; j < upto; j += blockDim.x) acc += max(sizes[j], 0);
+    for (int o = 32; o > 0; o >>= 1) acc += __shfl_xor(acc, o);
+    if ((threadIdx.x & 63) == 0) part[threadIdx.x >> 6] = acc;
+    __syncthreads();
+    const int64_t off = part[0] + part[1] + part[2] + part[3];
+    const int n = sizes[upto];
     const uint8_t *s = slots + (size_t)b * 65536;
-    uint8_t *d = out + offs[blk0 + b];
+    uint8_t *d = out + off;
     for (int i = threadIdx.x; i < n; i += blockDim.x) d[i] = s[i];
 }
 
@@ -441,7 +482,7 @@ extern "C" {
 // at a time.  bsdc_bgzf_deflate compresses blocks blk0 .. blk0 + nblk - 1 into the scratch's
 // slots and writes their sizes (BGZF block size with the 8 trailer bytes counted but not written;
 // 0 = the block does not fit and is stored by the host); bsdc_bgzf_pack then copies each slot's
-// bytes to out + offs[b] (offsets from the sizes, on the host).
+// bytes to out + (the sum of sizes[0 .. b)), the blocks of every launch back to back.
 int64_t bsdc_bgzf_scratch_bytes(int64_t max_blocks) {
     return max_blocks * (65536 + 65536 * 2 + (int64_t)kBlock * 4);
 }
@@ -458,11 +499,11 @@ int32_t bsdc_bgzf_deflate(const uint8_t *d_in, int64_t n, int64_t blk0, int64_t 
     return hipGetLastError() == hipSuccess ? 0 : -5;
 }
 
-int32_t bsdc_bgzf_pack(const uint8_t *d_scratch, const int32_t *d_sizes, const int64_t *d_offs, int64_t blk0,
-                       int64_t nblk, uint8_t *d_out, void *stream) {
+int32_t bsdc_bgzf_pack(const uint8_t *d_scratch, const int32_t *d_sizes, int64_t blk0, int64_t nblk, uint8_t *d_out,
+                       void *stream) {
     if (nblk <= 0) return 0;
-    hipLaunchKernelGGL(k_bgzf_pack, dim3((unsigned)nblk), dim3(256), 0, (hipStream_t)stream, d_scratch, d_sizes, d_offs,
-                       d_out, blk0);
+    hipLaunchKernelGGL(k_bgzf_pack, dim3((unsigned)nblk), dim3(256), 0, (hipStream_t)stream, d_scratch, d_sizes, d_out,
+                       blk0);
     return hipGetLastError() == hipSuccess ? 0 : -5;
 }
 

@@ -1468,8 +1468,9 @@ extern "C" int32_t bsdc_bam_writer_add(bsdc_bam_writer *w, const bsdc_bam_record
     return 0;
 }
 
-// The GPU-compressed write path (bsdc_bgzf_deflate in libbsdc): encode, let the caller compress
-// the whole blocks on the GPU, then hand the compressed blocks back to be finished and written.
+// The GPU-compressed write path (bsdc_bgzf_deflate in libbsdc): encode, move the whole blocks out
+// to the caller's (pinned) buffer with their CRC32s, let the caller compress them on the GPU while
+// the next records encode, then hand the compressed blocks back to be finished and written.
 extern "C" int64_t bsdc_bam_writer_encode(bsdc_bam_writer *w, const bsdc_bam_records *r, int32_t n_threads,
                                           const uint8_t **data) {
     set_threads(n_threads);
@@ -1479,43 +1480,45 @@ extern "C" int64_t bsdc_bam_writer_encode(bsdc_bam_writer *w, const bsdc_bam_rec
     return ((int64_t)w->tail.size() / kBlock) * kBlock;
 }
 
-// The first nblk whole blocks of the encoded tail, compressed elsewhere: block b's BGZF bytes are
-// packed[off_b .. off_b + sizes[b]) (off = running sum of sizes), complete but for CRC32 and ISIZE,
-// which are filled in here from the uncompressed bytes; a block of size 0 did not fit and is
-// deflated here (stored when incompressible).  Then the blocks are written in order and the
-// consumed bytes leave the tail.
-extern "C" int32_t bsdc_bam_writer_put_blocks(bsdc_bam_writer *w, int64_t nblk, uint8_t *packed, const int32_t *sizes,
-                                              int32_t n_threads) {
+// The first nblk whole blocks of the encoded tail leave it: copied to dst (nblk * 65280 bytes) with
+// each block's CRC32 in crc[b] (one pass over the bytes, the blocks in parallel).
+extern "C" int32_t bsdc_bam_writer_take(bsdc_bam_writer *w, int64_t nblk, uint8_t *dst, uint32_t *crc,
+                                        int32_t n_threads) {
     set_threads(n_threads);
-    if (nblk * kBlock > (int64_t)w->tail.size()) return fail(BSDC_IO_EFORMAT, "more blocks than encoded bytes");
-    std::vector<int64_t> off((size_t)nblk + 1, 0);
-    for (int64_t b = 0; b < nblk; b++) off[(size_t)b + 1] = off[(size_t)b] + std::max(sizes[b], 0);
+    if (nblk < 0 || nblk * kBlock > (int64_t)w->tail.size()) return fail(BSDC_IO_EFORMAT, "more blocks than encoded bytes");
     const uint8_t *src0 = w->tail.data();
-    int bad = 0;
-#pragma omp parallel for schedule(static) reduction(| : bad)
+#pragma omp parallel for schedule(static)
+    for (int64_t b = 0; b < nblk; b++) {
+        memcpy(dst + b * kBlock, src0 + b * kBlock, (size_t)kBlock);
+        crc[b] = crc32_of(dst + b * kBlock, kBlock);
+    }
+    w->tail.erase(w->tail.begin(), w->tail.begin() + nblk * kBlock);
+    return 0;
+}
+
+// nblk taken blocks back compressed: block b's BGZF bytes are packed[off_b .. off_b + sizes[b])
+// (off = running sum of sizes), complete but for CRC32 and ISIZE, which are filled in here from
+// crc[b]; a block of size 0 did not fit and is deflated here from raw (the taken bytes; stored when
+// incompressible).  Then the blocks are written in order.
+extern "C" int32_t bsdc_bam_writer_put(bsdc_bam_writer *w, int64_t nblk, uint8_t *packed, const int32_t *sizes,
+                                       const uint32_t *crc, const uint8_t *raw, int32_t n_threads) {
+    set_threads(n_threads);
+    int64_t off = 0;
     for (int64_t b = 0; b < nblk; b++) {
         const int32_t bs = sizes[b];
-        if (bs <= 0) continue;
-        if (bs < 26 || bs > 65536) {
-            bad |= 1;
-            continue;
-        }
-        uint8_t *h = packed + off[(size_t)b];
-        wr32(h + bs - 8, crc32_of(src0 + b * kBlock, kBlock));
-        wr32(h + bs - 4, (uint32_t)kBlock);
-    }
-    if (bad) return fail(BSDC_IO_EFORMAT, "bad compressed block size");
-    for (int64_t b = 0; b < nblk; b++) {
         int32_t rc = 0;
-        if (sizes[b] > 0) {
-            if (fwrite(packed + off[(size_t)b], 1, (size_t)sizes[b], w->f) != (size_t)sizes[b])
-                rc = fail(BSDC_IO_EIO, "BGZF write failed");
+        if (bs > 0) {
+            if (bs < 26 || bs > 65536) return fail(BSDC_IO_EFORMAT, "bad compressed block size");
+            uint8_t *h = packed + off;
+            wr32(h + bs - 8, crc[b]);
+            wr32(h + bs - 4, (uint32_t)kBlock);
+            if (fwrite(h, 1, (size_t)bs, w->f) != (size_t)bs) rc = fail(BSDC_IO_EIO, "BGZF write failed");
+            off += bs;
         } else {
-            rc = deflate_write(w->f, src0 + b * kBlock, kBlock, w->level);
+            rc = deflate_write(w->f, raw + b * kBlock, kBlock, w->level);
         }
         if (rc != 0) return rc;
     }
-    w->tail.erase(w->tail.begin(), w->tail.begin() + nblk * kBlock);
     return 0;
 }
 

@@ -237,7 +237,7 @@ __device__ __forceinline__ bool near_tie(T d0, T d1, T d2, T d3, int best, int n
 // Desc::get(i, addr, len, rev): the set's i-th read; its column col is image byte addr + col
 // (forward) or addr - col (reverse); bases at bimg, quals at qimg, same offsets.
 #ifndef FP64_PICK_ATTR
-#define FP64_PICK_ATTR __attribute__((noinline))  // rare path: out of line, off the vote's registers
+#define FP64_PICK_ATTR  // (out of line, noinline: C2 k_small 3.065 -> 3.101 ms, profiles/r03/ab/README.md)
 #endif
 template <class Desc>
 __device__ FP64_PICK_ATTR int fp64_pick(const Desc &ds, int n, int col, const uint8_t *bimg, const uint8_t *qimg, const double *lnc,

@@ -153,6 +153,43 @@ class DeviceBatch:
         return out
 
 
+class PinnedPool:
+    """A pinned host arena for the family images of one chunk's batches (materialize's `images`,
+    bump-allocated): the streaming step materializes a whole chunk ahead of the GPU stage into
+    one pool, the batches upload asynchronously from it, and the pool is reset for a later chunk
+    once every upload from it is done (bam.step5_stream keeps three in rotation)."""
+
+    SEGMENT = 64 << 20
+
+    def __init__(self):
+        self.segs = []  # pinned uint8 tensors; the last one is being filled
+        self.used = 0  # bytes of the last segment handed out
+        self.total = 0  # bytes handed out since the reset
+
+    def images(self, n_slots: int):
+        nq = n_slots
+        ns = n_slots // 2 + 64
+        need = (ns + 255) // 256 * 256 + nq
+        if not self.segs or self.used + need > self.segs[-1].numel():
+            self.segs.append(torch.empty(max(need, self.SEGMENT), dtype=torch.uint8, pin_memory=True))
+            self.used = 0
+        seg = self.segs[-1]
+        a = self.used
+        b = a + (ns + 255) // 256 * 256
+        self.used = (b + nq + 255) // 256 * 256
+        self.total += need
+        return seg[a:a + ns].numpy(), seg[b:b + nq].numpy()
+
+    def reset(self):
+        """every batch materialized from the pool has been uploaded: hand its bytes out again
+        (a pool that spilled over several segments becomes one that holds the largest chunk)."""
+        if len(self.segs) > 1:
+            size = int(max(self.total, sum(t.numel() for t in self.segs)) * 1.25)
+            self.segs = [torch.empty(size, dtype=torch.uint8, pin_memory=True)]
+        self.used = 0
+        self.total = 0
+
+
 class Engine:
     """One libbsdc context on one GPU."""
 

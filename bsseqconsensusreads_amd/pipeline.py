@@ -274,6 +274,41 @@ def run_ranges(engine: Engine, plan: FamilyPlan, ranges, mode: int, tags: bool =
     return parts
 
 
+def materialize_ranges(plan: FamilyPlan, ranges, images=None) -> List[FamilyBatch]:
+    """The device batches of plan family ranges (batch.materialize each), for run_batches; `images`
+    e.g. a PinnedPool's, so that they upload asynchronously."""
+    return [materialize(plan, a, b, images=images) for a, b in ranges]
+
+
+def run_batches(engine: Engine, batches, mode: int, tags: bool = False,
+                timing: Optional[dict] = None) -> List[Consensus]:
+    """Materialized batches through the kernels, one launch each, output per batch in order; a
+    batch uploads and launches before the one before it is fetched.  `timing` as run_ranges."""
+    import time
+    T = timing if timing is not None else {}
+    parts: List[Consensus] = []
+    prev = None
+
+    def out(fb, db):
+        t0 = time.perf_counter()
+        o = db.fetch()
+        t1 = time.perf_counter()
+        parts.append(consensus_from_output(fb, o))
+        T["fetch"] = T.get("fetch", 0.0) + t1 - t0
+        T["unpack"] = T.get("unpack", 0.0) + time.perf_counter() - t1
+    for fb in batches:
+        t0 = time.perf_counter()
+        db = engine.upload(fb, tags=tags)
+        engine.run(db, mode | (MODE_TAGS if tags else 0))
+        T["upload"] = T.get("upload", 0.0) + time.perf_counter() - t0
+        if prev is not None:
+            out(*prev)
+        prev = (fb, db)
+    if prev is not None:
+        out(*prev)
+    return parts
+
+
 def concat_consensus(parts: List[Consensus]) -> Consensus:
     """Consensus of consecutive family ranges -> one Consensus in range order (strides padded to
     the widest)."""

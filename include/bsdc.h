@@ -26,7 +26,7 @@
 extern "C" {
 #endif
 
-#define BSDC_ABI_VERSION 8
+#define BSDC_ABI_VERSION 9
 #define BSDC_SMALL_BUCKETS 8
 #define BSDC_LARGE_BUCKETS 6
 #define BSDC_LARGE_LDS_MAX 158912 /* LDS arena bytes one large-family workgroup may use */ /* LDS arena size classes of the wavefront-per-family kernel */
@@ -176,14 +176,16 @@ void bsdc_phred_buckets(double error_rate_pre_umi, double error_rate_post_umi, u
    device bytes in[0, n) as blocks of 65280 bytes, one dynamic-Huffman DEFLATE block each.
    bsdc_bgzf_deflate compresses blocks blk0 .. blk0 + nblk - 1 into the scratch
    (bsdc_bgzf_scratch_bytes(nblk) bytes) and writes sizes[blk0 + b]: the BGZF block size, its
-   CRC32 / ISIZE trailer counted but left to the host (libbsdc_io bsdc_bam_writer_put_blocks), or
+   CRC32 / ISIZE trailer counted but left to the host (libbsdc_io bsdc_bam_writer_put), or
    0 when the block does not fit (the host deflates it).  bsdc_bgzf_pack then copies block b's
-   bytes from the scratch to out + offs[blk0 + b].  Device pointers; stream = hipStream_t. */
+   bytes from the scratch to out + (sizes[0] + .. + sizes[blk0 + b - 1]), so successive launches
+   over one stream's blocks pack them back to back with no host round trip.  Device pointers;
+   stream = hipStream_t. */
 int64_t bsdc_bgzf_scratch_bytes(int64_t max_blocks);
 int32_t bsdc_bgzf_deflate(const uint8_t *in, int64_t n, int64_t blk0, int64_t nblk, uint8_t *scratch,
                           int32_t *sizes, void *stream);
-int32_t bsdc_bgzf_pack(const uint8_t *scratch, const int32_t *sizes, const int64_t *offs, int64_t blk0,
-                       int64_t nblk, uint8_t *out, void *stream);
+int32_t bsdc_bgzf_pack(const uint8_t *scratch, const int32_t *sizes, int64_t blk0, int64_t nblk, uint8_t *out,
+                       void *stream);
 
 #ifdef __cplusplus
 }

@@ -17,7 +17,7 @@
 extern "C" {
 #endif
 
-#define BSDC_IO_ABI_VERSION 5
+#define BSDC_IO_ABI_VERSION 6
 #define BSDC_IO_EFORMAT (-10) /* not BGZF/BAM, truncated, bad CRC */
 #define BSDC_IO_EIO (-11)     /* open/read/write failed */
 
@@ -135,13 +135,15 @@ int32_t bsdc_bam_writer_open(const char *path, const char *header_text, int64_t 
                              int32_t level, bsdc_bam_writer **out);
 int32_t bsdc_bam_writer_add(bsdc_bam_writer *w, const bsdc_bam_records *r, int32_t n_threads);
 /* The same with the whole blocks compressed by the caller (on the GPU: bsdc_bgzf_deflate in
- * libbsdc): encode returns the bytes of whole 65280-byte blocks now at *data (valid until the next
- * call); put_blocks takes the first nblk of them back compressed -- block b's BGZF bytes packed
- * back to back, sizes[b] each with the CRC32 / ISIZE bytes still to fill, 0 = deflate it here --
- * and writes them in order. */
+ * libbsdc): encode returns the byte count of whole 65280-byte blocks now at the front of the tail
+ * (*data: valid until the next call); take moves the first nblk of them to dst with their CRC32s;
+ * put writes nblk taken blocks back compressed -- block b's BGZF bytes packed back to back,
+ * sizes[b] each with the CRC32 / ISIZE bytes still to fill (from crc[b]), 0 = deflate it here from
+ * raw (what take copied) -- in order.  Takes and puts come in the same order. */
 int64_t bsdc_bam_writer_encode(bsdc_bam_writer *w, const bsdc_bam_records *r, int32_t n_threads, const uint8_t **data);
-int32_t bsdc_bam_writer_put_blocks(bsdc_bam_writer *w, int64_t nblk, uint8_t *packed, const int32_t *sizes,
-                                   int32_t n_threads);
+int32_t bsdc_bam_writer_take(bsdc_bam_writer *w, int64_t nblk, uint8_t *dst, uint32_t *crc, int32_t n_threads);
+int32_t bsdc_bam_writer_put(bsdc_bam_writer *w, int64_t nblk, uint8_t *packed, const int32_t *sizes,
+                            const uint32_t *crc, const uint8_t *raw, int32_t n_threads);
 int32_t bsdc_bam_writer_close(bsdc_bam_writer *w, int32_t n_threads);
 
 /* Paired FASTQ of records, as picard SamToFastq F=path1 F2=path2 writes them (the step after the

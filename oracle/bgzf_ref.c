@@ -22,7 +22,7 @@
 
 #include "bgzf_ref.h"
 
-enum { kThreads = 256, kSeg = 255, kHashBits = 12, kMaxDist = 32768 };
+enum { kThreads = 256, kSeg = 255, kHashBits = 11, kMaxDist = 32768 };
 
 static const uint16_t kLenBase[29] = {3, 4, 5, 6, 7, 8, 9, 10, 11, 13, 15, 17, 19, 23, 27,
                                       31, 35, 43, 51, 59, 67, 83, 99, 115, 131, 163, 195, 227, 258};

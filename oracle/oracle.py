@@ -341,12 +341,40 @@ def bgzf_block(data: bytes) -> bytes:
     return out[:n].tobytes()
 
 
+class _HostSlot:
+    """a host byte buffer with the data_ptr() a pinned torch tensor has."""
+
+    def __init__(self, n: int):
+        self.a = np.zeros(max(n, 1), np.uint8)
+
+    def data_ptr(self) -> int:
+        return self.a.ctypes.data
+
+
 class BgzfStandIn:
     """bam.GpuBgzf's interface on the CPU with bgzf_block: the BAM writer's GPU-compressed path
-    (encode, packed blocks, CRC / ISIZE filled by the writer) exercised without a GPU."""
+    (encode, take into a staging slot, submit / finish, CRC / ISIZE filled by the writer)
+    exercised without a GPU."""
 
     def __init__(self):
         self.blocks = 0
+        self.slots = [None, None]
+        self.slot = 0
+        self.job = None
+
+    def staging(self, nbytes: int):
+        self.slot ^= 1
+        if self.slots[self.slot] is None or self.slots[self.slot].a.size < nbytes:
+            self.slots[self.slot] = _HostSlot(nbytes)
+        return self.slots[self.slot]
+
+    def submit(self, raw, nblk: int):
+        assert self.job is None
+        self.job = self.compress(raw.data_ptr(), nblk * 65280)
+
+    def finish(self):
+        job, self.job = self.job, None
+        return job
 
     def compress(self, data_ptr: int, nbytes: int):
         host = np.ctypeslib.as_array(C.cast(data_ptr, C.POINTER(C.c_uint8)), shape=(nbytes,))

@@ -14,7 +14,7 @@ ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 def test_codec_and_oracle_clean_under_asan_ubsan():
     p = subprocess.run([os.path.join(ROOT, "tests", "sanitize", "run.sh"), "-k",
                         "corrupt or truncated or malformed or round_trip or family_image or golden or numpy or "
-                        "forced_large or split_partner or empty_input"],
+                        "forced_large or split_partner or empty_input or restatement or stand_in"],
                        capture_output=True, text=True, timeout=900)
     assert p.returncode == 0, (p.stdout[-3000:], p.stderr[-3000:])
     assert "sanitizer builds loaded" in p.stdout and " passed" in p.stdout
