@@ -171,6 +171,16 @@ void set_threads(int n) {
 }
 
 const char kCigarOps[] = "MIDNSHP=X";
+inline double now_s() { return omp_get_wtime(); }
+
+// packed SEQ byte -> its two bases as one little-endian uint16 (high nibble first)
+struct NibblePairs {
+    uint16_t v[256];
+    NibblePairs() {
+        for (int b = 0; b < 256; b++) v[b] = (uint16_t)((b >> 4) | ((b & 15) << 8));
+    }
+};
+const NibblePairs kNibblePairs;
 
 // aux field size past the 3-byte tag+type header, or -1 if malformed
 int64_t aux_value_size(const uint8_t *p, const uint8_t *end) {
@@ -217,62 +227,103 @@ int64_t aux_int(const uint8_t *p) {
 }  // namespace
 
 // ids[k] = index of keys[k] among the distinct keys in first-seen order, appended to `uniq`; with
-// `present`, a record whose present[k] is empty gets -1.  Hash-sharded: the hashes and the shard
-// maps run in parallel, then the shards' first occurrences are merged by record index.
+// `present`, a record whose present[k] is empty gets -1.  Hash-sharded, every pass parallel: the
+// hashes, a stable counting scatter of the records by shard (per-thread histograms), one
+// open-addressing table per shard, and the global ids as a prefix sum over the records that are
+// their key's first occurrence.
 static void intern(const std::vector<std::string_view> &keys, const std::vector<std::string_view> *present,
             std::vector<int32_t> &ids, std::vector<std::string_view> &uniq) {
     const int64_t n = (int64_t)keys.size();
     constexpr int S = 256;
     std::vector<uint32_t> shard((size_t)n);
     std::vector<uint64_t> hv((size_t)n);
-#pragma omp parallel for schedule(static)
-    for (int64_t k = 0; k < n; k++) {
-        const bool ok = present == nullptr || !(*present)[(size_t)k].empty();
-        const uint64_t h = std::hash<std::string_view>{}(keys[(size_t)k]);
-        hv[(size_t)k] = h;
-        shard[(size_t)k] = ok ? (uint32_t)(h % S) : (uint32_t)S;
-    }
+    std::vector<int64_t> order((size_t)n);
+    std::vector<int32_t> local((size_t)n);
+    std::vector<uint8_t> is_first((size_t)n);
     std::vector<int64_t> start(S + 2, 0);
-    for (int64_t k = 0; k < n; k++) start[shard[(size_t)k] + 1]++;
-    for (int s = 0; s <= S; s++) start[s + 1] += start[s];
-    std::vector<int64_t> order((size_t)n), fill(start.begin(), start.end() - 1);
-    for (int64_t k = 0; k < n; k++) order[(size_t)fill[shard[(size_t)k]]++] = k;  // ascending k per shard
-    std::vector<int32_t> local((size_t)n, -1);
     std::vector<std::vector<int64_t>> first(S);
-    // per shard: an open-addressing table (linear probing) of the shard's distinct keys
-#pragma omp parallel for schedule(dynamic, 4)
-    for (int s = 0; s < S; s++) {
-        const int64_t cnt = start[s + 1] - start[s];
-        size_t cap = 16;
-        while ((int64_t)cap < 2 * cnt) cap <<= 1;
-        std::vector<int32_t> slot(cap, -1);
-        std::vector<int64_t> &fs = first[s];
-        for (int64_t i = start[s]; i < start[s + 1]; i++) {
-            const int64_t k = order[(size_t)i];
-            const std::string_view key = keys[(size_t)k];
-            size_t pos = (size_t)(hv[(size_t)k] / S) & (cap - 1);
-            while (slot[pos] >= 0 && keys[(size_t)fs[(size_t)slot[pos]]] != key) pos = (pos + 1) & (cap - 1);
-            if (slot[pos] < 0) {
-                slot[pos] = (int32_t)fs.size();
-                fs.push_back(k);
-            }
-            local[(size_t)k] = slot[pos];
+    const int T = omp_get_max_threads();
+    std::vector<int64_t> cnt((size_t)T * (S + 1), 0);  // per thread and shard (S = absent)
+    std::vector<int64_t> part((size_t)T + 1, 0);        // per thread: first occurrences in its block
+#pragma omp parallel
+    {
+        const int t = omp_get_thread_num(), nt = omp_get_num_threads();
+        const int64_t lo = n * t / nt, hi = n * (t + 1) / nt;
+        int64_t *c = cnt.data() + (size_t)t * (S + 1);
+        for (int64_t k = lo; k < hi; k++) {
+            const bool ok = present == nullptr || !(*present)[(size_t)k].empty();
+            const uint64_t h = std::hash<std::string_view>{}(keys[(size_t)k]);
+            hv[(size_t)k] = h;
+            const uint32_t sh = ok ? (uint32_t)(h % S) : (uint32_t)S;
+            shard[(size_t)k] = sh;
+            c[sh]++;
+            is_first[(size_t)k] = 0;
         }
-    }
-    std::vector<int64_t> firsts;
-    for (int s = 0; s < S; s++) firsts.insert(firsts.end(), first[s].begin(), first[s].end());
-    std::sort(firsts.begin(), firsts.end());
-    std::vector<int32_t> gid((size_t)n, -1);  // global id, stored at each key's first record
-    const int32_t base = (int32_t)uniq.size();
-    for (size_t i = 0; i < firsts.size(); i++) {
-        gid[(size_t)firsts[i]] = base + (int32_t)i;
-        uniq.push_back(keys[(size_t)firsts[i]]);
-    }
-    ids.resize((size_t)n);
-#pragma omp parallel for schedule(static)
-    for (int64_t k = 0; k < n; k++) {
-        const uint32_t s = shard[(size_t)k];
-        ids[(size_t)k] = s == (uint32_t)S ? -1 : gid[(size_t)first[s][(size_t)local[(size_t)k]]];
+#pragma omp barrier
+#pragma omp single
+        {
+            // shard s's records start after every smaller shard; within a shard, thread blocks
+            // in order, so the scatter keeps each shard's records in ascending k
+            int64_t run = 0;
+            for (int sh = 0; sh <= S; sh++) {
+                start[sh] = run;
+                for (int u = 0; u < nt; u++) {
+                    const int64_t v = cnt[(size_t)u * (S + 1) + sh];
+                    cnt[(size_t)u * (S + 1) + sh] = run;
+                    run += v;
+                }
+            }
+            start[S + 1] = run;
+        }
+        for (int64_t k = lo; k < hi; k++) order[(size_t)c[shard[(size_t)k]]++] = k;
+#pragma omp barrier
+        // per shard: an open-addressing table (linear probing) of the shard's distinct keys
+#pragma omp for schedule(dynamic, 4)
+        for (int sh = 0; sh < S; sh++) {
+            const int64_t m = start[sh + 1] - start[sh];
+            size_t cap = 16;
+            while ((int64_t)cap < 2 * m) cap <<= 1;
+            std::vector<int32_t> slot(cap, -1);
+            std::vector<int64_t> &fs = first[sh];
+            for (int64_t i = start[sh]; i < start[sh + 1]; i++) {
+                const int64_t k = order[(size_t)i];
+                const std::string_view key = keys[(size_t)k];
+                size_t pos = (size_t)(hv[(size_t)k] / S) & (cap - 1);
+                while (slot[pos] >= 0 && keys[(size_t)fs[(size_t)slot[pos]]] != key) pos = (pos + 1) & (cap - 1);
+                if (slot[pos] < 0) {
+                    slot[pos] = (int32_t)fs.size();
+                    fs.push_back(k);
+                    is_first[(size_t)k] = 1;
+                }
+                local[(size_t)k] = slot[pos];
+            }
+        }
+        // (implicit barrier) global ids: first occurrences ranked by record index
+        int64_t f = 0;
+        for (int64_t k = lo; k < hi; k++) f += is_first[(size_t)k];
+        part[(size_t)t + 1] = f;
+#pragma omp barrier
+#pragma omp single
+        {
+            for (int u = 0; u < nt; u++) part[(size_t)u + 1] += part[(size_t)u];
+            uniq.resize(uniq.size() + (size_t)part[(size_t)nt]);
+            ids.resize((size_t)n);
+        }
+        const int64_t base = (int64_t)uniq.size() - part[(size_t)nt];
+        int64_t g = base + part[(size_t)t];
+        for (int64_t k = lo; k < hi; k++)
+            if (is_first[(size_t)k]) {
+                uniq[(size_t)g] = keys[(size_t)k];
+                ids[(size_t)k] = (int32_t)g++;  // (a first occurrence's own id; the rest below)
+            }
+#pragma omp barrier
+        for (int64_t k = lo; k < hi; k++) {
+            const uint32_t sh = shard[(size_t)k];
+            if (sh == (uint32_t)S)
+                ids[(size_t)k] = -1;
+            else if (!is_first[(size_t)k])
+                ids[(size_t)k] = ids[(size_t)first[sh][(size_t)local[(size_t)k]]];
+        }
     }
 }
 
@@ -546,7 +597,6 @@ constexpr int64_t kBigTid = 0x7FFFFFFF;
 constexpr int64_t kKeyDelta = 4;  // |key position before tools 1 + 2 - after| <= 2, twice
 constexpr int kFamShards = 64;
 inline int fam_shard(uint64_t h) { return (int)(h >> 58); }
-inline double now_s() { return omp_get_wtime(); }
 struct StreamFam {
     int64_t lo = INT64_MAX, hi = INT64_MIN;  // min own position, max own or mate position (coord)
     TcKey klo{INT64_MAX, INT64_MAX}, khi{INT64_MIN, INT64_MIN};  // bounds of its records' keys
@@ -1218,7 +1268,8 @@ int32_t bsdc_bam_copy(const bsdc_bam *b, const bsdc_bam_arrays *a) {
         for (int i = 0; i < n_cig; i++) a->cigar[co[k] + i] = rd32(c + 4 * i);
         const uint8_t *sq = c + 4 * n_cig;
         uint8_t *dst = a->seq + so[k];
-        for (int32_t i = 0; i < l_seq; i++) dst[i] = (i & 1) ? (sq[i >> 1] & 0xF) : (sq[i >> 1] >> 4);
+        for (int32_t i = 0; i < l_seq >> 1; i++) memcpy(dst + 2 * i, &kNibblePairs.v[sq[i]], 2);
+        if (l_seq & 1) dst[l_seq - 1] = (uint8_t)(sq[l_seq >> 1] >> 4);
         memcpy(a->qual + so[k], sq + (l_seq + 1) / 2, (size_t)l_seq);
         const uint8_t *aux = sq + (l_seq + 1) / 2 + l_seq;
         memcpy(a->aux + ao[k], aux, (size_t)(ao[k + 1] - ao[k]));
