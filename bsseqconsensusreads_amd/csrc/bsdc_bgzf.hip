@@ -4,20 +4,22 @@
 // blocks out (it holds the uncompressed bytes), and stores a block whose deflate would not fit.
 //
 // The algorithm is oracle/bgzf_ref.c's, step for step, so the bytes are identical (tests):
-//  A. match candidates in rounds of 256 consecutive positions: every position of the round looks
-//     up its 4-byte hash in the LDS table, then the round inserts its positions (atomicMax: the
-//     largest wins a slot) -- a candidate is the most recent earlier position with the same hash
-//     outside the position's own round;
-//  B. thread t parses its 255-byte segment greedily (the longest of distances 1, 2, 4 and the
-//     candidate's, first on a tie, >= 3, not past the segment), tokens to HBM scratch, symbol
-//     frequencies by LDS atomics;
+//  A. match candidates in rounds of 256 consecutive positions: a position's candidate is the last
+//     earlier position of its round with the same 4 bytes (each thread scans the round's values in
+//     LDS back from its own), else what the LDS hash table holds; then the round inserts its
+//     positions (atomicMax: the largest wins a slot).  The candidates, as distances in HBM
+//     scratch, link every position to an earlier one: a hash chain;
+//  B. thread t parses its 255-byte segment: at each position the longest match (>= 3, not past the
+//     segment, first on a tie) of distances 1, 2, 4 and the first 8 positions down the chain;
+//     lazy: a match shorter than 32 yields a literal when the next position has a longer one;
+//     tokens to HBM scratch, symbol frequencies by LDS atomics;
 //  C. thread 0 builds the length-limited Huffman codes (the restatement's two-queue build), the
 //     run-length coded code lengths and their own code, and writes the block header bits;
 //  D. each thread's bit count, a block scan -> bit offsets;
 //  E. each thread writes its bits: whole 32-bit words as plain stores, its first and last
 //     (shared) words by atomicOr into the zeroed slot.
-// Bytes per block: 65280 in, ~11 KB out for the tagged step-5 output (ratio 5.8 against libdeflate
-// level 5's 7.26: the parse trades ratio for parallelism; profiles/deflate_levels.py).
+// Bytes per block: 65280 in, ~9.3 KB out for the tagged step-5 output (ratio 7.0 against libdeflate
+// level 5's 7.26, profiles/deflate_levels.py).
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 
@@ -30,6 +32,8 @@ constexpr int kSeg = 255;        // bytes per thread segment (kT * kSeg = 65280 
 constexpr int kBlock = kT * kSeg;
 constexpr int kHashBits = 11;  // 2048 slots: the block, the table and the rest fit 80 KB of LDS (2 workgroups per CU)
 constexpr int kMaxDist = 32768;
+constexpr int kChain = 8;        // chain positions tried per match search
+constexpr int kLazy = 32;        // matches shorter than this look one position ahead
 constexpr int kOutCap = 65536 - 26;  // deflate bytes that still fit a BGZF block
 
 __constant__ uint16_t cLenBase[29] = {3, 4, 5, 6, 7, 8, 9, 10, 11, 13, 15, 17, 19, 23, 27,
@@ -192,6 +196,7 @@ struct __attribute__((aligned(16))) Smem {
         uint32_t table[1 << kHashBits];
         Late late;
     } u;
+    uint32_t rv[kT];  // phase A: the round's 4-byte values
     uint32_t lf[286], df[30], cf[19];
     uint8_t ll[286], dl[30], cl[19];
     uint16_t lc[286], dc[30], cc[19];
@@ -199,11 +204,6 @@ struct __attribute__((aligned(16))) Smem {
 };
 static_assert(sizeof(Late) <= sizeof(uint32_t) << kHashBits, "phase C-D scratch fits the table");
 static_assert(sizeof(Smem) <= 80 * 1024, "two workgroups per CU");
-
-__device__ __forceinline__ uint32_t hash4(const uint8_t *p) {
-    const uint32_t v = (uint32_t)p[0] | (uint32_t)p[1] << 8 | (uint32_t)p[2] << 16 | (uint32_t)p[3] << 24;
-    return (v * 2654435761u) >> (32 - kHashBits);
-}
 
 // the code-length sequence run-length coded (bgzf_ref.c bgzf_rle_lengths)
 __device__ int rle_lengths(const uint8_t *ll, int hlit, const uint8_t *dl, int hdist, uint8_t *sym, uint8_t *ext) {
@@ -281,41 +281,79 @@ __global__ __launch_bounds__(kT, 2) void k_bgzf(const uint8_t *__restrict__ in_a
     // only phase B reads, after the full barrier below ----
     for (int r0 = 0; r0 < n; r0 += kT) {
         const int p = r0 + t;
-        uint32_t h = 0;
-        if (p < n) {
-            int32_t c = -1;
-            if (p + 3 < n) {
-                h = hash4(S.in + p);
-                c = (int32_t)S.u.table[h] - 1;
-            }
-            dist[p] = (uint16_t)(c >= 0 ? p - c : 0);
+        const bool has4 = p + 3 < n;
+        uint32_t h = 0, v = 0;
+        int32_t c = -1;
+        if (has4) {
+            v = (uint32_t)S.in[p] | (uint32_t)S.in[p + 1] << 8 | (uint32_t)S.in[p + 2] << 16 |
+                (uint32_t)S.in[p + 3] << 24;
+            h = (v * 2654435761u) >> (32 - kHashBits);
+            c = (int32_t)S.u.table[h] - 1;
         }
+        S.rv[t] = v;
         asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
         __builtin_amdgcn_s_barrier();
         asm volatile("" ::: "memory");
-        if (p + 3 < n) atomicMax(&S.u.table[h], (uint32_t)p + 1);
+        if (has4) {
+            for (int j = t - 1; j >= 0; j--)  // (every earlier position of the round has 4 bytes)
+                if (S.rv[j] == v) {
+                    c = r0 + j;
+                    break;
+                }
+            atomicMax(&S.u.table[h], (uint32_t)p + 1);
+        }
+        if (p < n) dist[p] = (uint16_t)(c >= 0 ? p - c : 0);
         asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
         __builtin_amdgcn_s_barrier();
         asm volatile("" ::: "memory");
     }
     __syncthreads();  // (the dist stores, for phase B)
 
-    // ---- B. greedy parse of this thread's segment ----
+    // ---- B. parse of this thread's segment ----
     const int s0 = t * kSeg, s1 = ::min(n, s0 + kSeg);
     int nt = 0;
     uint32_t *mytok = tok + s0;
-    for (int i = s0; i < s1;) {
+    // the longest match at i: distances 1, 2, 4, then down the chain (a candidate that does not
+    // match at the current best length cannot be longer, so it is not walked)
+    auto best_match = [&](int i, int &bl, int &bd) {
         const int maxl = ::min(s1 - i, 258);
-        int bestl = 0, bestd = 0;
-        const int cd[4] = {1, 2, 4, (int)dist[i]};
-        for (int c = 0; c < 4; c++) {
-            const int d = cd[c];
-            if (d <= 0 || d > i || d > kMaxDist) continue;
+        bl = 0;
+        bd = 0;
+        auto tryd = [&](int d) {
+            if (d > i || bl >= maxl || S.in[i + bl] != S.in[i - d + bl]) return;
             int l = 0;
             while (l < maxl && S.in[i + l] == S.in[i - d + l]) l++;
-            if (l > bestl) {
-                bestl = l;
-                bestd = d;
+            if (l > bl) {
+                bl = l;
+                bd = d;
+            }
+        };
+        tryd(1);
+        tryd(2);
+        tryd(4);
+        int c = dist[i] ? i - (int)dist[i] : -1;
+        for (int k = 0; k < kChain && c >= 0 && i - c <= kMaxDist; k++) {
+            tryd(i - c);
+            const int dc = dist[c];
+            c = dc ? c - dc : -1;
+        }
+    };
+    bool have_next = false;
+    int next_l = 0, next_d = 0;
+    for (int i = s0; i < s1;) {
+        int bestl, bestd;
+        if (have_next) {
+            bestl = next_l;
+            bestd = next_d;
+            have_next = false;
+        } else {
+            best_match(i, bestl, bestd);
+        }
+        if (bestl >= 3 && bestl < kLazy && i + 1 < s1) {
+            best_match(i + 1, next_l, next_d);
+            if (next_l > bestl) {  // a literal here, the longer match next
+                bestl = 0;
+                have_next = true;
             }
         }
         if (bestl >= 3) {

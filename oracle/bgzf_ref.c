@@ -5,13 +5,15 @@
  * Not a reference-tool algorithm: the reference writes BAM through htsjdk / pysam (zlib deflate).
  * This is this repository's own DEFLATE (RFC 1951) encoder, shaped for one 256-thread workgroup
  * per BGZF block (SAM/BAM spec section 4.1):
- *  1. match candidates, in rounds of kThreads consecutive positions: every position of a round
- *     looks up the 4-byte hash table, then the round's positions are inserted (the largest position
- *     wins a slot), so a candidate is the most recent earlier position with the same hash outside
- *     the position's own round;
- *  2. greedy parse of kSeg-byte segments (one per thread): at each position the longest of the
- *     distances 1, 2, 4 and the candidate's (first one on a tie), at least 3 long, never past the
- *     segment end;
+ *  1. match candidates, in rounds of kThreads consecutive positions: a position's candidate is
+ *     the last earlier position of its own round with the same 4 bytes, else what the 4-byte hash
+ *     table holds; then the round's positions are inserted (the largest position wins a slot), so
+ *     the table gives the most recent position with the same hash before the round.  The
+ *     candidates link every position to an earlier one: a hash chain;
+ *  2. parse of kSeg-byte segments (one per thread): at each position the longest match (at least
+ *     3, never past the segment end, first one on a tie) of the distances 1, 2, 4 and the first
+ *     kChain positions down the chain within kMaxDist; lazy: a match shorter than kLazy yields a
+ *     literal when the next position has a longer one;
  *  3. one dynamic-Huffman block (BFINAL=1, BTYPE=2): length-limited Huffman codes (frequencies
  *     halved until the longest code fits), canonical codes, code lengths run-length coded with
  *     16/17/18;
@@ -22,7 +24,7 @@
 
 #include "bgzf_ref.h"
 
-enum { kThreads = 256, kSeg = 255, kHashBits = 11, kMaxDist = 32768 };
+enum { kThreads = 256, kSeg = 255, kHashBits = 11, kMaxDist = 32768, kChain = 8, kLazy = 32 };
 
 static const uint16_t kLenBase[29] = {3, 4, 5, 6, 7, 8, 9, 10, 11, 13, 15, 17, 19, 23, 27,
                                       31, 35, 43, 51, 59, 67, 83, 99, 115, 131, 163, 195, 227, 258};
@@ -207,6 +209,27 @@ static uint32_t crc32_bytes(const uint8_t *p, int64_t n) {
     return c ^ 0xFFFFFFFFu;
 }
 
+/* the longest match at i (0 if none of length >= 1): distances 1, 2, 4, then down the chain */
+static void best_match(const uint8_t *in, const int32_t *cand, int i, int s1, int *pl, int *pd) {
+    const int maxl = s1 - i < 258 ? s1 - i : 258;
+    int cd[3 + kChain] = {1, 2, 4};
+    int nc = 3;
+    for (int c = cand[i]; c >= 0 && nc < 3 + kChain && i - c <= kMaxDist; c = cand[c]) cd[nc++] = i - c;
+    int bestl = 0, bestd = 0;
+    for (int k = 0; k < nc; k++) {
+        const int d = cd[k];
+        if (d > i) continue;
+        int l = 0;
+        while (l < maxl && in[i + l] == in[i - d + l]) l++;
+        if (l > bestl) {
+            bestl = l;
+            bestd = d;
+        }
+    }
+    *pl = bestl;
+    *pd = bestd;
+}
+
 /* One BGZF block of in[0, n) (1 <= n <= 65280) into out (65536 bytes): its size, or 0 when the
  * dynamic block does not fit (the caller then stores the block). */
 int bgzf_ref_block(const uint8_t *in, int n, uint8_t *out) {
@@ -215,7 +238,16 @@ int bgzf_ref_block(const uint8_t *in, int n, uint8_t *out) {
     memset(table, 0, sizeof table);
     for (int r0 = 0; r0 < n; r0 += kThreads) {
         const int r1 = r0 + kThreads < n ? r0 + kThreads : n;
-        for (int p = r0; p < r1; p++) cand[p] = p + 3 < n ? (int32_t)table[hash4(in + p)] - 1 : -1;
+        for (int p = r0; p < r1; p++) {
+            cand[p] = -1;
+            if (p + 3 >= n) continue;
+            cand[p] = (int32_t)table[hash4(in + p)] - 1;
+            for (int q = p - 1; q >= r0; q--)
+                if (memcmp(in + q, in + p, 4) == 0) {
+                    cand[p] = q;
+                    break;
+                }
+        }
         for (int p = r0; p < r1; p++)
             if (p + 3 < n) {
                 const uint32_t h = hash4(in + p);
@@ -229,18 +261,12 @@ int bgzf_ref_block(const uint8_t *in, int n, uint8_t *out) {
     for (int s0 = 0; s0 < n; s0 += kSeg) {
         const int s1 = s0 + kSeg < n ? s0 + kSeg : n;
         for (int i = s0; i < s1;) {
-            const int maxl = s1 - i < 258 ? s1 - i : 258;
-            int bestl = 0, bestd = 0;
-            const int cd[4] = {1, 2, 4, cand[i] >= 0 ? i - cand[i] : 0};
-            for (int c = 0; c < 4; c++) {
-                const int d = cd[c];
-                if (d <= 0 || d > i || d > kMaxDist) continue;
-                int l = 0;
-                while (l < maxl && in[i + l] == in[i - d + l]) l++;
-                if (l > bestl) {
-                    bestl = l;
-                    bestd = d;
-                }
+            int bestl, bestd;
+            best_match(in, cand, i, s1, &bestl, &bestd);
+            if (bestl >= 3 && bestl < kLazy && i + 1 < s1) {
+                int l2, d2;
+                best_match(in, cand, i + 1, s1, &l2, &d2);
+                if (l2 > bestl) bestl = 0;  /* a literal here, the longer match next */
             }
             if (bestl >= 3) {
                 tok[nt++] = 0x80000000u | (uint32_t)bestl << 16 | (uint32_t)bestd;
