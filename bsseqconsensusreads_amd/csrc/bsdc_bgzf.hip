@@ -10,7 +10,9 @@
 //     positions (atomicMax: the largest wins a slot).  The candidates, as distances in HBM
 //     scratch, link every position to an earlier one: a hash chain;
 //  B. thread t parses its 255-byte segment: at each position the longest match (>= 3, not past the
-//     segment, first on a tie) of distances 1, 2, 4 and the first 8 positions down the chain;
+//     segment, first on a tie) of distances 1, 2, 4 and the first 8 positions down the chain (from
+//     A2: each position's chain distances precomputed in parallel), the search ending at a match
+//     of 64;
 //     lazy: a match shorter than 32 yields a literal when the next position has a longer one;
 //     tokens to HBM scratch, symbol frequencies by LDS atomics;
 //  C. thread 0 builds the length-limited Huffman codes (the restatement's two-queue build), the
@@ -34,26 +36,28 @@ constexpr int kHashBits = 11;  // 2048 slots: the block, the table and the rest 
 constexpr int kMaxDist = 32768;
 constexpr int kChain = 8;        // chain positions tried per match search
 constexpr int kLazy = 32;        // matches shorter than this look one position ahead
+constexpr int kNice = 64;        // a match this long ends the search
 constexpr int kOutCap = 65536 - 26;  // deflate bytes that still fit a BGZF block
 
-__constant__ uint16_t cLenBase[29] = {3, 4, 5, 6, 7, 8, 9, 10, 11, 13, 15, 17, 19, 23, 27,
-                                      31, 35, 43, 51, 59, 67, 83, 99, 115, 131, 163, 195, 227, 258};
-__constant__ uint8_t cLenExtra[29] = {0, 0, 0, 0, 0, 0, 0, 0, 1, 1, 1, 1, 2, 2, 2, 2, 3, 3, 3, 3, 4, 4, 4, 4, 5, 5, 5, 5, 0};
-__constant__ uint16_t cDistBase[30] = {1, 2, 3, 4, 5, 7, 9, 13, 17, 25, 33, 49, 65, 97, 129, 193, 257, 385,
-                                       513, 769, 1025, 1537, 2049, 3073, 4097, 6145, 8193, 12289, 16385, 24577};
-__constant__ uint8_t cDistExtra[30] = {0, 0, 0, 0, 1, 1, 2, 2, 3, 3, 4, 4, 5, 5, 6, 6, 7, 7, 8, 8, 9, 9, 10, 10, 11, 11, 12, 12, 13, 13};
 __constant__ uint8_t cClOrder[19] = {16, 17, 18, 0, 8, 7, 9, 6, 10, 5, 11, 4, 12, 3, 13, 2, 14, 1, 15};
 
-__device__ __forceinline__ int len_code(int l) {
-    int c = 0;
-    while (c < 28 && cLenBase[c + 1] <= l) c++;
-    return c;
+// the RFC 1951 length / distance code tables as arithmetic (a divergent index into a __constant__
+// table is a vector memory load; these are on every token of phases B, D and E)
+__device__ __forceinline__ int len_code(int l) {  // 3 <= l <= 258
+    if (l < 11) return l - 3;
+    if (l == 258) return 28;
+    const int n = l - 3, e = 31 - __builtin_clz((unsigned)n);
+    return 4 * (e - 1) + ((n >> (e - 2)) & 3);
 }
-__device__ __forceinline__ int dist_code(int d) {
-    int c = 0;
-    while (c < 29 && cDistBase[c + 1] <= d) c++;
-    return c;
+__device__ __forceinline__ int len_base(int c) { return c < 8 ? c + 3 : c == 28 ? 258 : ((4 + (c & 3)) << ((c >> 2) - 1)) + 3; }
+__device__ __forceinline__ int len_extra(int c) { return c < 8 || c == 28 ? 0 : (c >> 2) - 1; }
+__device__ __forceinline__ int dist_code(int d) {  // 1 <= d <= 32768
+    if (d <= 4) return d - 1;
+    const int n = d - 1, e = 31 - __builtin_clz((unsigned)n);
+    return 2 * e + ((n >> (e - 1)) & 1);
 }
+__device__ __forceinline__ int dist_base(int e) { return e < 4 ? e + 1 : ((2 + (e & 1)) << ((e >> 1) - 1)) + 1; }
+__device__ __forceinline__ int dist_extra(int e) { return e < 4 ? 0 : (e >> 1) - 1; }
 
 // Huffman code lengths (bgzf_ref.c bgzf_huffman_lengths) by the whole workgroup: the leaves'
 // order by (frequency, symbol) as a parallel rank count (every thread ranks its symbols against
@@ -191,12 +195,12 @@ struct Late {  // phases C-D: in the hash table's place (dead after phase A)
     uint32_t bits[kT];
 };
 struct __attribute__((aligned(16))) Smem {
-    uint8_t in[kBlock];
+    uint8_t in[kBlock + 16];  // (+16: the match compare reads whole dwords; bytes past n are never counted)
     union {
         uint32_t table[1 << kHashBits];
         Late late;
     } u;
-    uint32_t rv[kT];  // phase A: the round's 4-byte values
+    alignas(16) uint32_t rv[kT];  // phase A: the round's 4-byte values
     uint32_t lf[286], df[30], cf[19];
     uint8_t ll[286], dl[30], cl[19];
     uint16_t lc[286], dc[30], cc[19];
@@ -204,6 +208,17 @@ struct __attribute__((aligned(16))) Smem {
 };
 static_assert(sizeof(Late) <= sizeof(uint32_t) << kHashBits, "phase C-D scratch fits the table");
 static_assert(sizeof(Smem) <= 80 * 1024, "two workgroups per CU");
+static_assert(kChain == 8, "a position's chain is one 16-byte word");
+
+// phase timing for profiles/bgzf_phases.sh (a build with -DBSDC_BGZF_PHASES; none in the product):
+// thread 0's wall clock (100 MHz) at the phase ends, per block of the last launch
+#ifdef BSDC_BGZF_PHASES
+__device__ uint64_t g_bgzf_phase[8192 * 8];
+#define BGZF_PHASE(k) \
+    if (threadIdx.x == 0 && blockIdx.x < 8192) g_bgzf_phase[blockIdx.x * 8 + (k)] = wall_clock64()
+#else
+#define BGZF_PHASE(k) (void)0
+#endif
 
 // the code-length sequence run-length coded (bgzf_ref.c bgzf_rle_lengths)
 __device__ int rle_lengths(const uint8_t *ll, int hlit, const uint8_t *dl, int hdist, uint8_t *sym, uint8_t *ext) {
@@ -255,9 +270,11 @@ __device__ int rle_lengths(const uint8_t *ll, int hlit, const uint8_t *dl, int h
 // block blk0 + b's header and deflate bytes, sizes[blk0 + b] its BGZF size (0: does not fit)
 __global__ __launch_bounds__(kT, 2) void k_bgzf(const uint8_t *__restrict__ in_all, int64_t n_total, int64_t blk0,
                                                  uint8_t *__restrict__ slots, int32_t *__restrict__ sizes,
-                                                 uint16_t *__restrict__ dist_scr, uint32_t *__restrict__ tok_scr) {
+                                                 uint16_t *__restrict__ dist_scr, uint32_t *__restrict__ tok_scr,
+                                                 uint16_t *__restrict__ chain_scr) {
     __shared__ Smem S;
     const int t = threadIdx.x;
+    BGZF_PHASE(0);
     const int64_t blk = blk0 + blockIdx.x;
     const int64_t base = blk * kBlock;
     if (base >= n_total) return;
@@ -266,6 +283,7 @@ __global__ __launch_bounds__(kT, 2) void k_bgzf(const uint8_t *__restrict__ in_a
     uint32_t *words = reinterpret_cast<uint32_t *>(slot + 16);  // the deflate data starts at byte 18 = bit 16 of word 0
     uint16_t *dist = dist_scr + (size_t)blockIdx.x * 65536;
     uint32_t *tok = tok_scr + (size_t)blockIdx.x * kBlock;
+    uint16_t *chain = chain_scr + (size_t)blockIdx.x * kBlock * kChain;
 
     // ---- load the block (dwords, then the tail), clear the table, the frequencies, the slot ----
     const uint8_t *src = in_all + base;
@@ -275,6 +293,7 @@ __global__ __launch_bounds__(kT, 2) void k_bgzf(const uint8_t *__restrict__ in_a
     if (t < 30) S.df[t] = 0;
     for (int i = t; i < 65536 / 4; i += kT) reinterpret_cast<uint32_t *>(slot)[i] = 0;
     __syncthreads();
+    BGZF_PHASE(1);
 
     // ---- A. candidates.  The round barriers only order the LDS table (s_waitcnt lgkmcnt(0) +
     // s_barrier): a __syncthreads() would also wait for every round's HBM stores of `dist`, which
@@ -295,11 +314,29 @@ __global__ __launch_bounds__(kT, 2) void k_bgzf(const uint8_t *__restrict__ in_a
         __builtin_amdgcn_s_barrier();
         asm volatile("" ::: "memory");
         if (has4) {
-            for (int j = t - 1; j >= 0; j--)  // (every earlier position of the round has 4 bytes)
-                if (S.rv[j] == v) {
-                    c = r0 + j;
-                    break;
-                }
+            // the last j < t with the same value (every earlier position of the round has 4
+            // bytes): a branch-free scan of the round's values up to this wave's end, 16-byte
+            // broadcast reads
+            const int w0 = t & ~63;  // the earlier waves' positions: all before t
+            int q = -1;
+#pragma unroll 4
+            for (int j = 0; j < w0; j += 4) {
+                const uint4 r = *reinterpret_cast<const uint4 *>(&S.rv[j]);
+                q = ::max(q, r.x == v ? j : -1);
+                q = ::max(q, r.y == v ? j + 1 : -1);
+                q = ::max(q, r.z == v ? j + 2 : -1);
+                q = ::max(q, r.w == v ? j + 3 : -1);
+            }
+            uint64_t m = 0;  // this wave's positions: a match mask, then the highest below t
+#pragma unroll
+            for (int j = 0; j < 64; j += 4) {
+                const uint4 r = *reinterpret_cast<const uint4 *>(&S.rv[w0 + j]);
+                m |= (uint64_t)(r.x == v) << j | (uint64_t)(r.y == v) << (j + 1) | (uint64_t)(r.z == v) << (j + 2) |
+                     (uint64_t)(r.w == v) << (j + 3);
+            }
+            m &= (1ull << (t & 63)) - 1;
+            if (m) q = w0 + 63 - __clzll((long long)m);
+            if (q >= 0) c = r0 + q;
             atomicMax(&S.u.table[h], (uint32_t)p + 1);
         }
         if (p < n) dist[p] = (uint16_t)(c >= 0 ? p - c : 0);
@@ -307,7 +344,50 @@ __global__ __launch_bounds__(kT, 2) void k_bgzf(const uint8_t *__restrict__ in_a
         __builtin_amdgcn_s_barrier();
         asm volatile("" ::: "memory");
     }
-    __syncthreads();  // (the dist stores, for phase B)
+    __syncthreads();  // (the dist stores)
+    BGZF_PHASE(2);
+
+    // ---- A2. every position's chain: the distances of its first kChain chain positions within
+    // kMaxDist (0 ends the list), 16 bytes a position.  Pointer chasing through `dist`, 16
+    // positions at a time per thread so their loads overlap ----
+    {
+        constexpr int kG = 16;
+        for (int p0 = t; p0 < n; p0 += kT * kG) {
+            int D[kG];
+            uint32_t w[kG][kChain / 2];
+#pragma unroll
+            for (int u = 0; u < kG; u++) {
+                const int p = p0 + u * kT;
+                D[u] = p < n ? dist[p] : 0;
+#pragma unroll
+                for (int k = 0; k < kChain / 2; k++) w[u][k] = 0;
+            }
+#pragma unroll
+            for (int k = 0; k < kChain; k++) {
+#pragma unroll
+                for (int u = 0; u < kG; u++) {
+                    if (D[u] > kMaxDist) D[u] = 0;
+                    w[u][k >> 1] |= (uint32_t)D[u] << (16 * (k & 1));
+                }
+                if (k + 1 < kChain) {
+#pragma unroll
+                    for (int u = 0; u < kG; u++)
+                        if (D[u]) {
+                            const int dc = dist[p0 + u * kT - D[u]];
+                            D[u] = dc ? D[u] + dc : 0;
+                        }
+                }
+            }
+#pragma unroll
+            for (int u = 0; u < kG; u++) {
+                const int p = p0 + u * kT;
+                if (p < n)
+                    *reinterpret_cast<uint4 *>(chain + (size_t)p * kChain) = make_uint4(w[u][0], w[u][1], w[u][2], w[u][3]);
+            }
+        }
+    }
+    __syncthreads();  // (the chain stores, for phase B)
+    BGZF_PHASE(3);
 
     // ---- B. parse of this thread's segment ----
     const int s0 = t * kSeg, s1 = ::min(n, s0 + kSeg);
@@ -320,22 +400,45 @@ __global__ __launch_bounds__(kT, 2) void k_bgzf(const uint8_t *__restrict__ in_a
         bl = 0;
         bd = 0;
         auto tryd = [&](int d) {
-            if (d > i || bl >= maxl || S.in[i + bl] != S.in[i - d + bl]) return;
+            if (d > i || bl >= ::min(maxl, kNice) || S.in[i + bl] != S.in[i - d + bl]) return;
+            // 4 bytes a compare (two aligned dwords per side, funnel-shifted; each dword read
+            // once), clamped to maxl
+            const uint32_t *w = reinterpret_cast<const uint32_t *>(S.in);
+            const int a = i, b = i - d;
+            const uint32_t sa = (uint32_t)(a & 3), sb = (uint32_t)(b & 3);
+            int wa = a >> 2, wb = b >> 2;
+            uint32_t alo = w[wa], blo = w[wb];
             int l = 0;
-            while (l < maxl && S.in[i + l] == S.in[i - d + l]) l++;
+            for (;;) {
+                const uint32_t ahi = w[wa + 1], bhi = w[wb + 1];
+                const uint32_t x = __builtin_amdgcn_alignbyte(ahi, alo, sa) ^ __builtin_amdgcn_alignbyte(bhi, blo, sb);
+                if (x) {
+                    l += __builtin_ctz(x) >> 3;
+                    break;
+                }
+                l += 4;
+                if (l >= maxl) break;
+                alo = ahi;
+                blo = bhi;
+                wa++;
+                wb++;
+            }
+            l = ::min(l, maxl);
             if (l > bl) {
                 bl = l;
                 bd = d;
             }
         };
+        const uint4 cw = *reinterpret_cast<const uint4 *>(chain + (size_t)i * kChain);
         tryd(1);
         tryd(2);
         tryd(4);
-        int c = dist[i] ? i - (int)dist[i] : -1;
-        for (int k = 0; k < kChain && c >= 0 && i - c <= kMaxDist; k++) {
-            tryd(i - c);
-            const int dc = dist[c];
-            c = dc ? c - dc : -1;
+        const uint32_t cws[4] = {cw.x, cw.y, cw.z, cw.w};
+#pragma unroll
+        for (int k = 0; k < kChain; k++) {
+            const int d = (int)((cws[k >> 1] >> (16 * (k & 1))) & 0xFFFFu);
+            if (!d) break;
+            tryd(d);
         }
     };
     bool have_next = false;
@@ -368,6 +471,7 @@ __global__ __launch_bounds__(kT, 2) void k_bgzf(const uint8_t *__restrict__ in_a
         }
     }
     __syncthreads();
+    BGZF_PHASE(4);
 
     // ---- C. codes (the Huffman builds by the workgroup) and the header (thread 0) ----
     if (t == 0) S.lf[256]++;
@@ -407,6 +511,7 @@ __global__ __launch_bounds__(kT, 2) void k_bgzf(const uint8_t *__restrict__ in_a
         S.hclen = hclen;
     }
     __syncthreads();
+    BGZF_PHASE(5);
 
     // ---- D. bits per thread, offsets ----
     uint32_t mb = 0;
@@ -417,12 +522,13 @@ __global__ __launch_bounds__(kT, 2) void k_bgzf(const uint8_t *__restrict__ in_a
         } else {
             const int l = (int)((x >> 16) & 0x1FF), d = (int)(x & 0xFFFF);
             const int c = len_code(l), e = dist_code(d);
-            mb += S.ll[257 + c] + cLenExtra[c] + S.dl[e] + cDistExtra[e];
+            mb += S.ll[257 + c] + len_extra(c) + S.dl[e] + dist_extra(e);
         }
     }
     if (t == kT - 1) mb += S.ll[256];  // end of block
     S.u.late.bits[t] = mb;
     __syncthreads();
+    BGZF_PHASE(6);
     // exclusive scan over the 256 counts (one wave per 64, then the wave totals)
     int64_t off = S.hdr_bits;
     for (int j = 0; j < t; j++) off += S.u.late.bits[j];
@@ -464,13 +570,14 @@ __global__ __launch_bounds__(kT, 2) void k_bgzf(const uint8_t *__restrict__ in_a
         const int l = (int)((x >> 16) & 0x1FF), d = (int)(x & 0xFFFF);
         const int c = len_code(l), e = dist_code(d);
         o.put(S.lc[257 + c], S.ll[257 + c]);
-        o.put((uint32_t)(l - cLenBase[c]), cLenExtra[c]);
+        o.put((uint32_t)(l - len_base(c)), len_extra(c));
         o.put(S.dc[e], S.dl[e]);
-        o.put((uint32_t)(d - cDistBase[e]), cDistExtra[e]);
+        o.put((uint32_t)(d - dist_base(e)), dist_extra(e));
     }
     if (t == kT - 1) o.put(S.lc[256], S.ll[256]);
     o.finish();
     __syncthreads();
+    BGZF_PHASE(7);
     if (t == 0) {  // the gzip header with the BC extra field (bytes 16-17 = BSIZE - 1)
         const int bsize = (int)(18 + clen + 8);
         const uint8_t hdr[16] = {31, 139, 8, 4, 0, 0, 0, 0, 0, 255, 6, 0, 'B', 'C', 2, 0};
@@ -522,7 +629,7 @@ extern "C" {
 // 0 = the block does not fit and is stored by the host); bsdc_bgzf_pack then copies each slot's
 // bytes to out + (the sum of sizes[0 .. b)), the blocks of every launch back to back.
 int64_t bsdc_bgzf_scratch_bytes(int64_t max_blocks) {
-    return max_blocks * (65536 + 65536 * 2 + (int64_t)kBlock * 4);
+    return max_blocks * (65536 + 65536 * 2 + (int64_t)kBlock * 4 + (int64_t)kBlock * 2 * kChain);
 }
 
 int32_t bsdc_bgzf_deflate(const uint8_t *d_in, int64_t n, int64_t blk0, int64_t nblk, uint8_t *d_scratch,
@@ -532,8 +639,9 @@ int32_t bsdc_bgzf_deflate(const uint8_t *d_in, int64_t n, int64_t blk0, int64_t 
     uint8_t *slots = d_scratch;
     uint16_t *dist = reinterpret_cast<uint16_t *>(d_scratch + nblk * 65536);
     uint32_t *tok = reinterpret_cast<uint32_t *>(d_scratch + nblk * (65536 + 65536 * 2));
+    uint16_t *chain = reinterpret_cast<uint16_t *>(d_scratch + nblk * (65536 + 65536 * 2 + (int64_t)kBlock * 4));
     hipLaunchKernelGGL(k_bgzf, dim3((unsigned)nblk), dim3(kT), 0, (hipStream_t)stream, d_in, n, blk0, slots, d_sizes,
-                       dist, tok);
+                       dist, tok, chain);
     return hipGetLastError() == hipSuccess ? 0 : -5;
 }
 
@@ -544,5 +652,11 @@ int32_t bsdc_bgzf_pack(const uint8_t *d_scratch, const int32_t *d_sizes, int64_t
                        blk0);
     return hipGetLastError() == hipSuccess ? 0 : -5;
 }
+
+#ifdef BSDC_BGZF_PHASES
+int32_t bsdc_bgzf_phases(uint64_t *host, int64_t n) {
+    return hipMemcpyFromSymbol(host, HIP_SYMBOL(g_bgzf_phase), (size_t)n * sizeof(uint64_t)) == hipSuccess ? 0 : -5;
+}
+#endif
 
 }  // extern "C"

@@ -12,7 +12,7 @@
  *     candidates link every position to an earlier one: a hash chain;
  *  2. parse of kSeg-byte segments (one per thread): at each position the longest match (at least
  *     3, never past the segment end, first one on a tie) of the distances 1, 2, 4 and the first
- *     kChain positions down the chain within kMaxDist; lazy: a match shorter than kLazy yields a
+ *     kChain positions down the chain within kMaxDist, the search ending at a kNice match; lazy: a match shorter than kLazy yields a
  *     literal when the next position has a longer one;
  *  3. one dynamic-Huffman block (BFINAL=1, BTYPE=2): length-limited Huffman codes (frequencies
  *     halved until the longest code fits), canonical codes, code lengths run-length coded with
@@ -24,7 +24,7 @@
 
 #include "bgzf_ref.h"
 
-enum { kThreads = 256, kSeg = 255, kHashBits = 11, kMaxDist = 32768, kChain = 8, kLazy = 32 };
+enum { kThreads = 256, kSeg = 255, kHashBits = 11, kMaxDist = 32768, kChain = 8, kLazy = 32, kNice = 64 };
 
 static const uint16_t kLenBase[29] = {3, 4, 5, 6, 7, 8, 9, 10, 11, 13, 15, 17, 19, 23, 27,
                                       31, 35, 43, 51, 59, 67, 83, 99, 115, 131, 163, 195, 227, 258};
@@ -209,7 +209,8 @@ static uint32_t crc32_bytes(const uint8_t *p, int64_t n) {
     return c ^ 0xFFFFFFFFu;
 }
 
-/* the longest match at i (0 if none of length >= 1): distances 1, 2, 4, then down the chain */
+/* the longest match at i (0 if none of length >= 1): distances 1, 2, 4, then down the chain,
+ * until one is kNice long */
 static void best_match(const uint8_t *in, const int32_t *cand, int i, int s1, int *pl, int *pd) {
     const int maxl = s1 - i < 258 ? s1 - i : 258;
     int cd[3 + kChain] = {1, 2, 4};
@@ -225,6 +226,7 @@ static void best_match(const uint8_t *in, const int32_t *cand, int i, int s1, in
             bestl = l;
             bestd = d;
         }
+        if (bestl >= kNice) break;
     }
     *pl = bestl;
     *pd = bestd;
