@@ -189,14 +189,46 @@ class BamHeader:
         return out
 
 
-def _decode(lib, h, what: str):
-    """A bsdc_bam handle (whole file or stream chunk) -> (BamHeader, RawRecords); frees nothing."""
+class BufferPool:
+    """Host byte buffers handed from one stream chunk's decoded records to a later chunk's
+    (bam.step5_stream): a fresh array of a few hundred MB costs its page faults and the kernel's
+    zeroing on every chunk.  take() the smallest free buffer that fits (or a new one), give() it
+    back once nothing refers to the arrays carved from it."""
+
+    def __init__(self, keep: int = 8):
+        import threading
+        self.free: list = []
+        self.keep = keep
+        self.lock = threading.Lock()
+
+    def take(self, nbytes: int) -> np.ndarray:
+        with self.lock:
+            fit = [i for i, b in enumerate(self.free) if b.size >= nbytes]
+            if fit:
+                return self.free.pop(min(fit, key=lambda i: self.free[i].size))
+        return np.empty(max(int(nbytes * 1.15), 1), np.uint8)
+
+    def give(self, buf: Optional[np.ndarray]):
+        if buf is None:
+            return
+        with self.lock:
+            self.free.append(buf)
+            if len(self.free) > self.keep:
+                self.free.remove(min(self.free, key=lambda b: b.size))
+
+
+def _decode(lib, h, what: str, pool: Optional[BufferPool] = None):
+    """A bsdc_bam handle (whole file or stream chunk) -> (BamHeader, RawRecords); frees nothing.
+    With `pool`, the record arrays are carved from one pooled buffer (bsdc_bam_copy writes every
+    element), kept as RawRecords._pool_buf for the caller to give back."""
     s = _Sizes()
     lib.bsdc_bam_sizes_of(h, C.byref(s))
     n = s.n_rec
+    specs = []
 
     def z(k, dt):
-        return np.zeros(max(int(k), 1), dt)
+        specs.append((max(int(k), 1), np.dtype(dt)))
+        return len(specs) - 1
     A = dict(flag=z(n, np.uint16), tid=z(n, np.int32), pos=z(n, np.int32), mapq=z(n, np.uint8),
              l_seq=z(n, np.int32), seq_off=z(n, np.int64), seq=z(s.n_bases, np.uint8), qual=z(s.n_bases, np.uint8),
              cig_off=z(n, np.int64), n_cig=z(n, np.int32), cigar=z(s.n_cigar, np.uint32),
@@ -207,6 +239,17 @@ def _decode(lib, h, what: str):
              rd=z(n, np.int32), aux_off=z(n + 1, np.int64), aux=z(s.aux_bytes, np.uint8),
              header=z(s.header_bytes, np.uint8), ref_len=z(s.n_ref, np.int64),
              ref_name_off=z(s.n_ref + 1, np.int64), ref_name_buf=z(s.ref_name_bytes, np.uint8))
+    buf = None
+    if pool is None:
+        arrs = [np.zeros(k, dt) for k, dt in specs]
+    else:
+        sizes = [(k * dt.itemsize + 63) & ~63 for k, dt in specs]
+        buf = pool.take(sum(sizes))
+        arrs, o = [], 0
+        for (k, dt), nb in zip(specs, sizes):
+            arrs.append(buf[o:o + k * dt.itemsize].view(dt))
+            o += nb
+    A = {key: arrs[i] for key, i in A.items()}
     a = _Arrays(**{k: _ptr(v) for k, v in A.items()})
     if lib.bsdc_bam_copy(h, C.byref(a)) != 0:
         raise OSError("%s: %s" % (what, lib.bsdc_io_last_error().decode()))
@@ -223,6 +266,7 @@ def _decode(lib, h, what: str):
         mi_names=StringTable(A["mi_buf"][:s.mi_bytes], A["mi_off"][:s.n_mi + 1], as_str=True),
         mc_off=A["mc_off"][:n], mc_n=A["mc_n"][:n], mc_cigar=A["mc_cigar"][:s.n_mc],
         aux=StringTable(A["aux"][:s.aux_bytes], A["aux_off"][:n + 1]), la_tag=A["la"][:n], rd_tag=A["rd"][:n])
+    raw._pool_buf = buf
     return header, raw
 
 
@@ -269,14 +313,22 @@ class StreamChunk:
     def __init__(self, lib, st, h, path: str):
         self._lib, self._st, self._h, self._path = lib, st, h, path
 
-    def decode(self, threads: int = 0):
-        """-> (BamHeader, RawRecords)"""
+    def decode(self, threads: int = 0, timing: Optional[dict] = None, pool: Optional[BufferPool] = None):
+        """-> (BamHeader, RawRecords); `timing`: seconds added under "parse" (records, tags,
+        interning) and "copy" (the arrays copied out); `pool`: see _decode."""
+        import time
         lib, h = self._lib, self._h
         self._h = None
         try:
+            t0 = time.perf_counter()
             if lib.bsdc_bam_parse(h, int(threads)) != 0:
                 raise OSError("%s: %s" % (self._path, lib.bsdc_io_last_error().decode()))
-            return _decode(lib, h, self._path)
+            t1 = time.perf_counter()
+            out = _decode(lib, h, self._path, pool)
+            if timing is not None:
+                timing["parse"] = timing.get("parse", 0.0) + t1 - t0
+                timing["copy"] = timing.get("copy", 0.0) + time.perf_counter() - t1
+            return out
         finally:
             lib.bsdc_bam_stream_recycle(self._st, h)
 
@@ -987,9 +1039,11 @@ def step5_stream(in_bam: str, fasta: str, out_bam: Optional[str], engine=None, p
     outs: "queue.Queue" = queue.Queue(maxsize=1)
     err: list = []
     info = {"records_in": 0, "families": 0, "families_emitted": 0, "records_out": 0, "chunks": 0}
-    T = {"decode": 0.0, "parse": 0.0, "plan": 0.0, "materialize": 0.0, "gpu": 0.0, "records": 0.0, "encode": 0.0,
+    T = {"decode": 0.0, "plan": 0.0, "materialize": 0.0, "gpu": 0.0, "records": 0.0, "encode": 0.0,
          "gpu_wait": 0.0, "writer_wait": 0.0}
-    G: dict = {}  # the GPU stage's host steps (pipeline.run_ranges timing)
+    G: dict = {}  # the GPU stage's host steps (pipeline.run_batches timing)
+    R_: dict = {}  # the reader's steps (StreamChunk.decode timing)
+    bufs = BufferPool()  # a chunk's record arrays, given back once its output is written
     first = {}
     stop = threading.Event()  # set on any failure: the decoder and planner stop at their next chunk
 
@@ -1026,9 +1080,7 @@ def step5_stream(in_bam: str, fasta: str, out_bam: Optional[str], engine=None, p
                 if stop.is_set():
                     ch.discard()
                     continue  # drain to the decoder's None without parsing
-                t0 = time.perf_counter()
-                raw = ch.decode(threads)[1]
-                T["parse"] += time.perf_counter() - t0
+                raw = ch.decode(threads, R_, bufs)[1]
                 parsed.put(raw)
         except BaseException as e:  # noqa: BLE001 -- handed to the main thread
             err.append(e)
@@ -1088,7 +1140,9 @@ def step5_stream(in_bam: str, fasta: str, out_bam: Optional[str], engine=None, p
                 t0 = time.perf_counter()
                 recs = duplex_records(cons, raw, first["prefix"], threads)
                 T["records"] += time.perf_counter() - t0
-                recq.put(recs)
+                buf = raw._pool_buf
+                del item, cons, raw
+                recq.put((recs, buf))
         except BaseException as e:  # noqa: BLE001
             err.append(e)
             stop.set()
@@ -1103,9 +1157,10 @@ def step5_stream(in_bam: str, fasta: str, out_bam: Optional[str], engine=None, p
             w = BamWriter(out_bam, output_header(first["header"]), level, gz) if out_bam is not None else None
             fq = FastqWriter(fastq[0], fastq[1], level) if fastq is not None else None
             while True:
-                recs = recq.get()
-                if recs is None:
+                item = recq.get()
+                if item is None:
                     break
+                recs, buf = item
                 t1 = time.perf_counter()
                 if w is not None:
                     w.add(recs, threads)
@@ -1113,6 +1168,8 @@ def step5_stream(in_bam: str, fasta: str, out_bam: Optional[str], engine=None, p
                     fq.add(recs, threads)
                 info["records_out"] += recs.n
                 T["encode"] += time.perf_counter() - t1
+                del item, recs
+                bufs.give(buf)  # (the chunk's records are written; nothing refers to its arrays)
             if w is not None:
                 w.close(threads)
             if fq is not None:
@@ -1189,6 +1246,7 @@ def step5_stream(in_bam: str, fasta: str, out_bam: Optional[str], engine=None, p
     if stats is not None:
         stats.update({k: round(v, 4) for k, v in T.items()})
         stats.update({"gpu_" + k: round(v, 4) for k, v in G.items()})
+        stats.update({"reader_" + k: round(v, 4) for k, v in R_.items()})
     return info
 
 
