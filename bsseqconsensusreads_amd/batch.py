@@ -797,6 +797,9 @@ def materialize_py(plan: FamilyPlan, f0: int, f1: int, small_cap: int = SMALL_AR
     for cap in LARGE_BUCKETS + (None,):
         sel = ~small & (need_l > lo) if cap is None else ~small & (need_l > lo) & (need_l <= cap)
         lf = np.nonzero(sel)[0]
+        # the largest images first: a class's dispatch lasts until its longest workgroup ends, so
+        # the longest start first and the short ones fill in around them
+        lf = lf[np.argsort(-img[lf], kind="stable")]
         e = np.zeros((lf.shape[0], 4), np.int64)
         e[:, 0] = lf
         e[:, 1] = fam_off[lf]

@@ -244,6 +244,7 @@ def materialize(plan, f0: int, f1: int, small_cap: int, n_threads: int = 0, imag
     lbuckets, larenas = [], []
     for q in range(LARGE_BUCKETS_N):
         lf = np.nonzero(cls == SMALL_BUCKETS_N + q)[0]
+        lf = lf[np.argsort(-img[lf], kind="stable")]  # largest image first (batch.py)
         e = np.zeros((lf.shape[0], 4), np.int64)
         e[:, 0] = lf
         e[:, 1] = fam_off[lf]
