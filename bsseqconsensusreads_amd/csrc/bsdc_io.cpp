@@ -1019,6 +1019,14 @@ int32_t bsdc_bam_stream_next_raw(bsdc_bam_stream *s, int64_t min_bytes, int64_t 
         t0 = now_s();
         const bool end = s->eof && s->comp.empty();
         if (end && s->tail < (int64_t)s->buf.size()) return fail(BSDC_IO_EFORMAT, "truncated BAM record");
+        if (!end && s->tail < min_bytes) {  // a chunk takes >= min_bytes of the buffered records:
+            s->prof[2] += now_s() - t0;     // not there yet, so no selection until the next fill
+            t0 = now_s();
+            rc = bsdc_bam_stream_fill(s);
+            if (rc != 0) return rc;
+            s->prof[0] += now_s() - t0;
+            continue;
+        }
         take.assign(s->fams.size(), 0);
         int64_t bytes = 0;
         if (end) {  // every family is complete and nothing is left to read
