@@ -195,7 +195,7 @@ class BufferPool:
     zeroing on every chunk.  take() the smallest free buffer that fits (or a new one), give() it
     back once nothing refers to the arrays carved from it."""
 
-    def __init__(self, keep: int = 8):
+    def __init__(self, keep: int = 4):
         import threading
         self.free: list = []
         self.keep = keep
@@ -213,8 +213,8 @@ class BufferPool:
             return
         with self.lock:
             self.free.append(buf)
-            if len(self.free) > self.keep:
-                self.free.remove(min(self.free, key=lambda b: b.size))
+            if len(self.free) > self.keep:  # drop the smallest (by position: arrays do not compare)
+                del self.free[min(range(len(self.free)), key=lambda i: self.free[i].size)]
 
 
 def _decode(lib, h, what: str, pool: Optional[BufferPool] = None):

@@ -148,3 +148,21 @@ def test_unsorted_input_fails_loudly(tmp_path):
     with pytest.raises(OSError, match="coordinate-sorted"):
         for _ in bam.stream_bam(p, threads=2, chunk_bytes=10_000):
             pass
+
+
+def test_buffer_pool_reuse_and_trim():
+    """bam.BufferPool (the stream reader's record arrays): the smallest free buffer that fits is
+    reused, a new one is made when none fits, and the free list keeps its `keep` largest."""
+    p = bam.BufferPool(keep=2)
+    a = p.take(1000)
+    assert a.size >= 1000
+    p.give(a)
+    assert p.take(500) is a  # reused
+    b, c, d = p.take(100), p.take(5000), p.take(300)
+    for x in (a, b, c, d):
+        p.give(x)
+    assert len(p.free) == 2 and sorted(x.size for x in p.free) == sorted([a.size, c.size])
+    p.give(None)
+    assert len(p.free) == 2
+    big = p.take(4000)
+    assert big is c
