@@ -79,3 +79,16 @@ def test_stream_writer_with_gpu_bgzf(tmp_path):
     for k in ("flag", "l_seq", "seq", "qual", "name_id"):
         assert np.array_equal(getattr(ra, k), getattr(rb, k)), k
     assert np.array_equal(ra.aux.buf, rb.aux.buf)
+
+
+def test_kernel_launches_in_pieces(monkeypatch):
+    """More blocks than one launch takes (GpuBgzf.MAX_BLOCKS, lowered here): the launches' blocks
+    are packed back to back by offsets summed on the device, each equal to the restatement's."""
+    monkeypatch.setattr(bam.GpuBgzf, "MAX_BLOCKS", 2)
+    rng = random.Random(3)
+    blocks = [bytes(rng.getrandbits(2) for _ in range(65280)) for _ in range(3)] + [b"ACGT" * 16320, b"\0" * 65280]
+    got = _kernel_blocks(b"".join(blocks))
+    assert len(got) == len(blocks)
+    for k, (g, d) in enumerate(zip(got, blocks)):
+        ref = oracle.bgzf_block(d)
+        assert g[:-8] == ref[:-8], k
