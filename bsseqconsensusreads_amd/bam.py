@@ -1019,10 +1019,10 @@ def step5_stream(in_bam: str, fasta: str, out_bam: Optional[str], engine=None, p
     """step5 in bounded memory, pipelined: a decoder thread cuts the next chunk of the
     coordinate-sorted input (stream_bam: inflate, split where no template or MI family straddles),
     a reader thread parses the chunk before, a planner thread forms the families of the one before
-    that (C++ plan), a materializer thread fills the batches of the one before that into pinned
-    memory; this thread uploads a chunk's batches and runs them on the GPU; a builder thread builds
+    that (C++ plan) and materializes its batches into pinned memory; this thread uploads a chunk's
+    batches and runs them on the GPU; a builder thread builds
     the output records of the chunk before and a writer thread appends them to the BAM
-    (BamWriter).  Peak host memory is about seven chunks, whatever the file size.  The output is
+    (BamWriter).  Peak host memory is about six chunks, whatever the file size.  The output is
     byte-identical to step5's (tests/test_stream.py): every chunk's TemplateCoordinate keys sort
     before the next chunk's, so the chunks' families in order are the whole file's.  gpu_bgzf: the
     BAM's blocks are deflated on the engine's GPU (GpuBgzf; the same records, other compressed
@@ -1093,10 +1093,13 @@ def step5_stream(in_bam: str, fasta: str, out_bam: Optional[str], engine=None, p
         finally:
             parsed.put(None)
 
-    planned: "queue.Queue" = queue.Queue(maxsize=1)
+    # the planner materializes chunk k's batches into pool k % 3: chunk k - 3 is done on the GPU
+    # by then (the planner handed chunk k - 1 over only after the GPU stage took chunk k - 2)
+    pools = [PinnedPool() for _ in range(3)]
 
-    def planner():  # forms a chunk's families while the materializer fills the batches of the one before
+    def planner():  # forms a chunk's families and materializes its batches ahead of the GPU stage
         try:
+            k = 0
             while True:
                 raw = parsed.get()
                 if raw is None:
@@ -1105,43 +1108,20 @@ def step5_stream(in_bam: str, fasta: str, out_bam: Optional[str], engine=None, p
                     continue  # drain to the reader's None without planning
                 t0 = time.perf_counter()
                 plan = pipeline.plan_families(raw, "full", first["ref"])
-                T["plan"] += time.perf_counter() - t0
-                planned.put((raw, plan))
-        except BaseException as e:  # noqa: BLE001 -- handed to the main thread
-            err.append(e)
-            stop.set()
-            while parsed.get() is not None:  # let the reader finish
-                pass
-        finally:
-            planned.put(None)
-
-    # the materializer fills chunk k's batches into pool k % 3: chunk k - 3 is done on the GPU by
-    # then (it handed chunk k - 1 over only after the GPU stage took chunk k - 2)
-    pools = [PinnedPool() for _ in range(3)]
-
-    def materializer():  # a chunk's batches into pinned memory, ahead of the GPU stage
-        try:
-            k = 0
-            while True:
-                item = planned.get()
-                if item is None:
-                    break
-                if stop.is_set():
-                    continue  # drain to the planner's None
-                raw, plan = item
+                t1 = time.perf_counter()
                 fbs = None
                 if not plan.split_ext:
-                    t0 = time.perf_counter()
                     pool = pools[k % 3]
                     k += 1
                     pool.reset()
                     fbs = pipeline.materialize_ranges(plan, pipeline.plan_ranges(plan, batch_bases), pool.images)
-                    T["materialize"] += time.perf_counter() - t0
+                T["plan"] += t1 - t0
+                T["materialize"] += time.perf_counter() - t1
                 chunks.put((raw, plan, fbs))
         except BaseException as e:  # noqa: BLE001 -- handed to the main thread
             err.append(e)
             stop.set()
-            while planned.get() is not None:  # let the planner finish
+            while parsed.get() is not None:  # let the reader finish
                 pass
         finally:
             chunks.put(None)
@@ -1211,13 +1191,11 @@ def step5_stream(in_bam: str, fasta: str, out_bam: Optional[str], engine=None, p
         td = threading.Thread(target=decoder, daemon=True)
         tr = threading.Thread(target=reader, daemon=True)
         tp = threading.Thread(target=planner, daemon=True)
-        tm = threading.Thread(target=materializer, daemon=True)
         tb = threading.Thread(target=builder, daemon=True)
         tw = threading.Thread(target=writer, daemon=True)
         td.start()
         tr.start()
         tp.start()
-        tm.start()
         tb.start()
         tw.start()
         mode = pipeline.MODE_CONVERT | pipeline.MODE_EXTEND | pipeline.MODE_VOTE
@@ -1250,14 +1228,13 @@ def step5_stream(in_bam: str, fasta: str, out_bam: Optional[str], engine=None, p
             stop.set()
             raise
         finally:
-            if not drained:  # let the materializer finish (it stops once `stop` is set)
+            if not drained:  # let the planner finish (it stops planning once `stop` is set)
                 stop.set()
                 while chunks.get() is not None:
                     pass
             outs.put(None)
             tb.join()
             tw.join()
-            tm.join()
             tp.join()
             tr.join()
             td.join()

@@ -20,7 +20,6 @@
 #include <string_view>
 #include <unordered_map>
 #include <mutex>
-#include <thread>
 #include <vector>
 #ifdef _OPENMP
 #include <omp.h>
@@ -636,16 +635,6 @@ struct bsdc_bam_stream {
     std::vector<Bytes> pool;  // returned chunk buffers (at most 2 kept)
     int64_t outstanding = 0;
     bool closed = false;
-    // read-ahead: the next fill's read and inflate run on a thread of their own (with its own
-    // OpenMP team) while this one splits records; its bytes wait in `ahead`.  Only that thread
-    // touches f / comp / eof while it runs; `drained` is this thread's view (eof, all inflated)
-    std::thread pf;
-    bool pf_run = false;
-    Bytes ahead;
-    int32_t pf_rc = 0;
-    std::string pf_err;
-    bool drained = false;
-    int32_t n_threads = 0;
 };
 
 int32_t bsdc_bam_stream_open(const char *path, int32_t n_threads, int64_t read_size, bsdc_bam_stream **out) {
@@ -655,7 +644,6 @@ int32_t bsdc_bam_stream_open(const char *path, int32_t n_threads, int64_t read_s
     if (!f) return fail(BSDC_IO_EIO, std::string("cannot open ") + path);
     auto *s = new bsdc_bam_stream();
     s->f = f;
-    s->n_threads = n_threads;
     s->read_size = read_size > 0 ? read_size : ((int64_t)64 << 20);
     if (const char *e = getenv("BSDC_STREAM_PAR_MIN")) s->par_min = atoll(e);  // (tests: 0 = always parallel)
     // inflate until the header is whole
@@ -672,7 +660,7 @@ int32_t bsdc_bam_stream_open(const char *path, int32_t n_threads, int64_t read_s
             s->tail = 0;
             break;
         }
-        if (s->drained) {
+        if (s->eof) {
             const int64_t dn = (int64_t)s->buf.size();
             const int32_t rc = parse_header(s->buf.data(), dn, &probe, &p);
             bsdc_bam_stream_close(s);
@@ -688,9 +676,8 @@ int32_t bsdc_bam_stream_open(const char *path, int32_t n_threads, int64_t read_s
     return 0;
 }
 
-namespace {
-// Reads read_size more compressed bytes and inflates the whole blocks onto the end of `out`.
-int32_t fill_into(bsdc_bam_stream *s, Bytes &out) {
+// Reads read_size more compressed bytes and inflates the whole blocks onto the end of buf.
+int32_t bsdc_bam_stream_fill(bsdc_bam_stream *s) {
     if (s->eof) return 0;
     const size_t have = s->comp.size();
     s->comp.resize(have + (size_t)s->read_size);
@@ -701,46 +688,9 @@ int32_t fill_into(bsdc_bam_stream *s, Bytes &out) {
         s->eof = true;
     }
     int64_t used = 0;
-    const int32_t rc = inflate_blocks(s->comp.data(), (int64_t)s->comp.size(), s->eof, out, &used);
+    const int32_t rc = inflate_blocks(s->comp.data(), (int64_t)s->comp.size(), s->eof, s->buf, &used);
     if (rc != 0) return rc;
     s->comp.erase(s->comp.begin(), s->comp.begin() + used);
-    return 0;
-}
-
-void prefetch_start(bsdc_bam_stream *s) {
-    s->pf_run = true;
-    s->pf = std::thread([s]() {
-        set_threads(s->n_threads);
-        s->ahead.clear();
-        s->pf_rc = fill_into(s, s->ahead);
-        if (s->pf_rc != 0) s->pf_err = g_err;
-    });
-}
-
-void prefetch_join(bsdc_bam_stream *s) {
-    if (s->pf_run) {
-        s->pf.join();
-        s->pf_run = false;
-    }
-}
-}  // namespace
-
-// The next read_size of compressed bytes inflated onto the end of buf: the read-ahead's (started
-// by the call before), then the one after is started.
-int32_t bsdc_bam_stream_fill(bsdc_bam_stream *s) {
-    if (s->drained) return 0;
-    if (!s->pf_run) prefetch_start(s);
-    prefetch_join(s);
-    if (s->pf_rc != 0) return fail(s->pf_rc, s->pf_err);
-    const int64_t n = (int64_t)s->ahead.size(), b0 = (int64_t)s->buf.size();
-    if (s->buf.capacity() < (size_t)(b0 + n + 8)) s->buf.reserve(std::max((size_t)(b0 + n + 8), 2 * s->buf.capacity()));
-    s->buf.resize((size_t)(b0 + n));
-    constexpr int64_t kPiece = 1 << 20;
-#pragma omp parallel for schedule(static)
-    for (int64_t o = 0; o < n; o += kPiece)
-        memcpy(s->buf.data() + b0 + o, s->ahead.data() + o, (size_t)std::min(kPiece, n - o));
-    s->drained = s->eof;  // (the last fill inflates every block: nothing is left in comp)
-    if (!s->drained) prefetch_start(s);
     return 0;
 }
 
@@ -1067,7 +1017,7 @@ int32_t bsdc_bam_stream_next_raw(bsdc_bam_stream *s, int64_t min_bytes, int64_t 
         if (rc != 0) return rc;
         s->prof[1] += now_s() - t0;
         t0 = now_s();
-        const bool end = s->drained;
+        const bool end = s->eof && s->comp.empty();
         if (end && s->tail < (int64_t)s->buf.size()) return fail(BSDC_IO_EFORMAT, "truncated BAM record");
         if (!end && s->tail < min_bytes) {  // a chunk takes >= min_bytes of the buffered records:
             s->prof[2] += now_s() - t0;     // not there yet, so no selection until the next fill
@@ -1256,7 +1206,6 @@ int32_t bsdc_bam_stream_header(const bsdc_bam_stream *s, bsdc_bam **out) {
 
 void bsdc_bam_stream_close(bsdc_bam_stream *s) {
     if (!s) return;
-    prefetch_join(s);
     if (s->f) fclose(s->f);
     s->f = nullptr;
     if (getenv("BSDC_STREAM_PROF"))
