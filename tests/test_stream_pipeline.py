@@ -1,5 +1,5 @@
-"""bam.step5_stream's thread pipeline on the CPU (decoder with read-ahead, reader with pooled
-record buffers, planner, materializer, GPU stage, builder, writer): the GPU stage's batches are
+"""bam.step5_stream's thread pipeline on the CPU (decoder, reader with pooled record buffers,
+planner + materialize, GPU stage, builder, writer): the GPU stage's batches are
 answered by oracle/ (tests/fleet_standin.OracleRunner, TEST INFRASTRUCTURE ONLY) and pinned pools
 by plain host arrays, so every hand-off, buffer rotation and drain runs without a GPU.  The BAM
 (with tags) and the FASTQ pair it writes are checked record by record against oracle/ on the
