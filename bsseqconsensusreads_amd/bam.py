@@ -195,7 +195,7 @@ class BufferPool:
     zeroing on every chunk.  take() the smallest free buffer that fits (or a new one), give() it
     back once nothing refers to the arrays carved from it."""
 
-    def __init__(self, keep: int = 4):
+    def __init__(self, keep: int = 6):
         import threading
         self.free: list = []
         self.keep = keep
@@ -861,11 +861,14 @@ def output_header(header: BamHeader) -> BamHeader:
     return BamHeader("\n".join(lines) + "\n", list(header.ref_names), np.asarray(header.ref_lens, np.int64))
 
 
-def consensus_tags(cons, em: np.ndarray, molecular: bool = False, threads: int = 0) -> StringTable:
+def consensus_tags(cons, em: np.ndarray, molecular: bool = False, threads: int = 0,
+                   pool: Optional["BufferPool"] = None) -> StringTable:
     """fgbio's consensus tags (aux bytes) of the output records R1, R2 of families `em`, from the
     single-strand reads in cons.ss (libbsdc_io bsdc_consensus_tags).  Duplex: a record's 'a'
     strand is its AB read (AB-R1 for R1, AB-R2 for R2), or the only strand present; 'b' its BA read
-    when both are present.  Molecular: set 0 for R1, set 1 for R2."""
+    when both are present.  Molecular: set 0 for R1, set 1 for R2.  With `pool`, the bytes land in
+    a pooled buffer (kept as the table's _pool_buf for the caller to give back): the tags are
+    ≈1.8 KB a record, and fresh pages for them cost as much as writing them."""
     lib = _load()
     ss = cons.ss
     F = em.shape[0]
@@ -891,15 +894,19 @@ def consensus_tags(cons, em: np.ndarray, molecular: bool = False, threads: int =
     args = (n, _ptr(row_a), _ptr(row_b), _ptr(out_len), 1 if molecular else 0, stride, _ptr(base), _ptr(qual),
             _ptr(depth), _ptr(err), _ptr(off))
     total = lib.bsdc_consensus_tags(*args, None, int(threads))
-    buf = np.empty(max(int(total), 1), np.uint8)
+    buf = pool.take(max(int(total), 1)) if pool is not None else np.empty(max(int(total), 1), np.uint8)
     lib.bsdc_consensus_tags(*args, _ptr(buf), int(threads))
-    return StringTable(buf[:int(total)], off)
+    tab = StringTable(buf[:int(total)], off)
+    tab._pool_buf = buf if pool is not None else None
+    return tab
 
 
-def duplex_records(cons, raw: R.RawRecords, prefix: str, threads: int = 0, molecular: bool = False) -> OutRecordsBam:
+def duplex_records(cons, raw: R.RawRecords, prefix: str, threads: int = 0, molecular: bool = False,
+                   pool: Optional["BufferPool"] = None) -> OutRecordsBam:
     """fgbio duplex output records for the emitted families of `cons`
     (pipeline.Consensus, family order): R1 then R2 per family; fgbio's consensus tags appended
-    when cons.ss holds the single-strand reads (``molecular``: CallMolecularConsensusReads' set)."""
+    when cons.ss holds the single-strand reads (``molecular``: CallMolecularConsensusReads' set).
+    `pool`: the tags' buffer comes from it (consensus_tags)."""
     lib = _load()
     em = np.nonzero((cons.status & 1) != 0)[0]
     F = em.shape[0]
@@ -941,7 +948,7 @@ def duplex_records(cons, raw: R.RawRecords, prefix: str, threads: int = 0, molec
     fam_names = _concat_fields([prefix.encode() + b":", mi], F)
     two = np.repeat(np.arange(F, dtype=np.int64), 2)
     names_t, auxs_t = _take_table(fam_names, two), _take_table(fam_aux, two)
-    tg = consensus_tags(cons, em, molecular, threads) if getattr(cons, "ss", None) is not None else None
+    tg = consensus_tags(cons, em, molecular, threads, pool) if getattr(cons, "ss", None) is not None else None
     L = np.ascontiguousarray(cons.length[em].reshape(-1), np.int32)  # R1, R2, R1, R2 ...
     seq_off = np.zeros(n + 1, np.int64)
     seq_off[1:] = np.cumsum(L)
@@ -1138,11 +1145,11 @@ def step5_stream(in_bam: str, fasta: str, out_bam: Optional[str], engine=None, p
                     break
                 cons, raw = item
                 t0 = time.perf_counter()
-                recs = duplex_records(cons, raw, first["prefix"], threads)
+                recs = duplex_records(cons, raw, first["prefix"], threads, pool=bufs)
                 T["records"] += time.perf_counter() - t0
-                buf = raw._pool_buf
+                back = [raw._pool_buf, getattr(recs.aux2, "_pool_buf", None)]
                 del item, cons, raw
-                recq.put((recs, buf))
+                recq.put((recs, back))
         except BaseException as e:  # noqa: BLE001
             err.append(e)
             stop.set()
@@ -1160,7 +1167,7 @@ def step5_stream(in_bam: str, fasta: str, out_bam: Optional[str], engine=None, p
                 item = recq.get()
                 if item is None:
                     break
-                recs, buf = item
+                recs, back = item
                 t1 = time.perf_counter()
                 if w is not None:
                     w.add(recs, threads)
@@ -1169,7 +1176,8 @@ def step5_stream(in_bam: str, fasta: str, out_bam: Optional[str], engine=None, p
                 info["records_out"] += recs.n
                 T["encode"] += time.perf_counter() - t1
                 del item, recs
-                bufs.give(buf)  # (the chunk's records are written; nothing refers to its arrays)
+                for buf in back:  # (the chunk's records are written; nothing refers to their arrays)
+                    bufs.give(buf)
             if w is not None:
                 w.close(threads)
             if fq is not None:

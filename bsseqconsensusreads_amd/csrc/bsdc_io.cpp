@@ -1747,18 +1747,29 @@ struct SsView {  // one single-strand consensus read, truncated to `len`
     int32_t len;
 };
 
-void per_read(AuxOut &o, const char *tD, const char *tM, const char *tE, const int32_t *depth, const int32_t *err,
-              int32_t len) {
+// D (max depth), M (min depth), E (errors / depth) of one read; depth(i), err(i) per column
+template <class Dep, class Err>
+void per_read(AuxOut &o, const char *tD, const char *tM, const char *tE, Dep depth, Err err, int32_t len) {
     int64_t mx = 0, mn = len ? INT64_MAX : 0, sd = 0, se = 0;
     for (int32_t i = 0; i < len; i++) {
-        mx = std::max<int64_t>(mx, depth[i]);
-        mn = std::min<int64_t>(mn, depth[i]);
-        sd += depth[i];
-        se += err[i];
+        const int64_t d = depth(i);
+        mx = std::max<int64_t>(mx, d);
+        mn = std::min<int64_t>(mn, d);
+        sd += d;
+        se += err(i);
     }
     o.integer(tD, mx);
     o.integer(tM, mn);
     o.real(tE, (float)se / (float)sd);
+}
+
+// a B:s array straight from the kernels' uint16 counts (the same 16 bits as the int16 value)
+void shorts16(AuxOut &o, const char *tag, const uint16_t *v, int32_t len) {
+    o.head(tag, 'B');
+    uint8_t b[5] = {'s'};
+    wr32(b + 1, (uint32_t)len);
+    o.bytes(b, 5);
+    o.bytes(v, 2 * (int64_t)len);  // (little-endian host)
 }
 }  // namespace
 
@@ -1777,50 +1788,43 @@ extern "C" int64_t bsdc_consensus_tags(int64_t n, const int64_t *row_a, const in
             const size_t at = (size_t)row * (size_t)stride;
             return SsView{ss_base + at, ss_qual + at, ss_depth + at, ss_err + at, L};
         };
-        std::vector<int32_t> td(L), te(L), ad(L), ae(L), bd(L), be(L);
         const SsView a = view(row_a[k]);
-        for (int32_t i = 0; i < L; i++) {
-            ad[i] = a.d[i];
-            ae[i] = a.e[i];
-        }
+        auto ad = [&](int32_t i) { return (int64_t)a.d[i]; };
+        auto ae = [&](int32_t i) { return (int64_t)a.e[i]; };
         if (kind == 1) {  // molecular: cD cM cE, cd ce
-            per_read(o, "cD", "cM", "cE", ad.data(), ae.data(), L);
-            o.shorts("cd", ad.data(), L);
-            o.shorts("ce", ae.data(), L);
+            per_read(o, "cD", "cM", "cE", ad, ae, L);
+            shorts16(o, "cd", a.d, L);
+            shorts16(o, "ce", a.e, L);
             return o.n;
         }
         const bool two = row_b[k] >= 0;
-        SsView b{};
+        const SsView b = two ? view(row_b[k]) : SsView{};
         if (two) {
-            b = view(row_b[k]);
-            for (int32_t i = 0; i < L; i++) {
-                bd[i] = b.d[i];
-                be[i] = b.e[i];
-            }
-        }
-        for (int32_t i = 0; i < L; i++) {
-            if (!two) {
-                td[i] = ad[i];
-                te[i] = ae[i];
-                continue;
-            }
             // the duplex call before its N mask; errors counted against it: a strand whose call
             // agrees contributes its errors, one that disagrees all of its reads
-            const uint8_t ab = a.b[i] & 15, bb = b.b[i] & 15;
-            const uint8_t raw = ab == bb ? ab : a.q[i] > b.q[i] ? ab : b.q[i] > a.q[i] ? bb : ab;
-            td[i] = ad[i] + bd[i];
-            te[i] = (ab == raw ? ae[i] : ad[i]) + (bb == raw ? be[i] : bd[i]);
+            auto td = [&](int32_t i) { return (int64_t)a.d[i] + b.d[i]; };
+            auto te = [&](int32_t i) {
+                const uint8_t ab = a.b[i] & 15, bb = b.b[i] & 15;
+                const uint8_t raw = ab == bb ? ab : a.q[i] > b.q[i] ? ab : b.q[i] > a.q[i] ? bb : ab;
+                return (int64_t)(ab == raw ? a.e[i] : a.d[i]) + (bb == raw ? b.e[i] : b.d[i]);
+            };
+            per_read(o, "cD", "cM", "cE", td, te, L);
+        } else {
+            per_read(o, "cD", "cM", "cE", ad, ae, L);
         }
-        per_read(o, "cD", "cM", "cE", td.data(), te.data(), L);
-        per_read(o, "aD", "aM", "aE", ad.data(), ae.data(), L);
-        if (two) per_read(o, "bD", "bM", "bE", bd.data(), be.data(), L);
-        o.shorts("ad", ad.data(), L);
-        o.shorts("ae", ae.data(), L);
+        per_read(o, "aD", "aM", "aE", ad, ae, L);
+        if (two) {
+            auto bdf = [&](int32_t i) { return (int64_t)b.d[i]; };
+            auto bef = [&](int32_t i) { return (int64_t)b.e[i]; };
+            per_read(o, "bD", "bM", "bE", bdf, bef, L);
+        }
+        shorts16(o, "ad", a.d, L);
+        shorts16(o, "ae", a.e, L);
         o.text("ac", a.b, L, kNt16, 0);
         o.text("aq", a.q, L, nullptr, 33);
         if (two) {
-            o.shorts("bd", bd.data(), L);
-            o.shorts("be", be.data(), L);
+            shorts16(o, "bd", b.d, L);
+            shorts16(o, "be", b.e, L);
             o.text("bc", b.b, L, kNt16, 0);
             o.text("bq", b.q, L, nullptr, 33);
         }
