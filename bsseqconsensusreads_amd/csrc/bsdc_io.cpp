@@ -1539,19 +1539,18 @@ extern "C" int64_t bsdc_bam_writer_encode(bsdc_bam_writer *w, const bsdc_bam_rec
     return ((int64_t)w->tail.size() / kBlock) * kBlock;
 }
 
-// The first nblk whole blocks of the encoded tail leave it: copied to dst (nblk * 65280 bytes) with
+namespace {
+// The first nblk whole blocks of an encoded tail leave it: copied to dst (nblk * 65280 bytes) with
 // each block's CRC32 in crc[b] (one pass over the bytes, the blocks in parallel).
-extern "C" int32_t bsdc_bam_writer_take(bsdc_bam_writer *w, int64_t nblk, uint8_t *dst, uint32_t *crc,
-                                        int32_t n_threads) {
-    set_threads(n_threads);
-    if (nblk < 0 || nblk * kBlock > (int64_t)w->tail.size()) return fail(BSDC_IO_EFORMAT, "more blocks than encoded bytes");
-    const uint8_t *src0 = w->tail.data();
+int32_t take_blocks(Bytes &tail, int64_t nblk, uint8_t *dst, uint32_t *crc) {
+    if (nblk < 0 || nblk * kBlock > (int64_t)tail.size()) return fail(BSDC_IO_EFORMAT, "more blocks than encoded bytes");
+    const uint8_t *src0 = tail.data();
 #pragma omp parallel for schedule(static)
     for (int64_t b = 0; b < nblk; b++) {
         memcpy(dst + b * kBlock, src0 + b * kBlock, (size_t)kBlock);
         crc[b] = crc32_of(dst + b * kBlock, kBlock);
     }
-    w->tail.erase(w->tail.begin(), w->tail.begin() + nblk * kBlock);
+    tail.erase(tail.begin(), tail.begin() + nblk * kBlock);
     return 0;
 }
 
@@ -1559,9 +1558,8 @@ extern "C" int32_t bsdc_bam_writer_take(bsdc_bam_writer *w, int64_t nblk, uint8_
 // (off = running sum of sizes), complete but for CRC32 and ISIZE, which are filled in here from
 // crc[b]; a block of size 0 did not fit and is deflated here from raw (the taken bytes; stored when
 // incompressible).  Then the blocks are written in order.
-extern "C" int32_t bsdc_bam_writer_put(bsdc_bam_writer *w, int64_t nblk, uint8_t *packed, const int32_t *sizes,
-                                       const uint32_t *crc, const uint8_t *raw, int32_t n_threads) {
-    set_threads(n_threads);
+int32_t put_blocks(FILE *f, int32_t level, int64_t nblk, uint8_t *packed, const int32_t *sizes, const uint32_t *crc,
+                   const uint8_t *raw) {
     int64_t off = 0;
     for (int64_t b = 0; b < nblk; b++) {
         const int32_t bs = sizes[b];
@@ -1571,14 +1569,27 @@ extern "C" int32_t bsdc_bam_writer_put(bsdc_bam_writer *w, int64_t nblk, uint8_t
             uint8_t *h = packed + off;
             wr32(h + bs - 8, crc[b]);
             wr32(h + bs - 4, (uint32_t)kBlock);
-            if (fwrite(h, 1, (size_t)bs, w->f) != (size_t)bs) rc = fail(BSDC_IO_EIO, "BGZF write failed");
+            if (fwrite(h, 1, (size_t)bs, f) != (size_t)bs) rc = fail(BSDC_IO_EIO, "BGZF write failed");
             off += bs;
         } else {
-            rc = deflate_write(w->f, raw + b * kBlock, kBlock, w->level);
+            rc = deflate_write(f, raw + b * kBlock, kBlock, level);
         }
         if (rc != 0) return rc;
     }
     return 0;
+}
+}  // namespace
+
+extern "C" int32_t bsdc_bam_writer_take(bsdc_bam_writer *w, int64_t nblk, uint8_t *dst, uint32_t *crc,
+                                        int32_t n_threads) {
+    set_threads(n_threads);
+    return take_blocks(w->tail, nblk, dst, crc);
+}
+
+extern "C" int32_t bsdc_bam_writer_put(bsdc_bam_writer *w, int64_t nblk, uint8_t *packed, const int32_t *sizes,
+                                       const uint32_t *crc, const uint8_t *raw, int32_t n_threads) {
+    set_threads(n_threads);
+    return put_blocks(w->f, w->level, nblk, packed, sizes, crc, raw);
 }
 
 extern "C" int32_t bsdc_bam_writer_close(bsdc_bam_writer *w, int32_t n_threads) {
@@ -1956,6 +1967,32 @@ extern "C" int32_t bsdc_fastq_writer_add(bsdc_fastq_writer *w, const bsdc_bam_re
         }
     }
     return 0;
+}
+
+// The same with the whole blocks compressed by the caller (bsdc_bam_writer_encode / take / put for
+// the two files): whole[d] = the bytes of whole blocks now at the front of file d's tail.
+extern "C" int32_t bsdc_fastq_writer_encode(bsdc_fastq_writer *w, const bsdc_bam_records *r, int32_t n_threads,
+                                            int64_t *whole) {
+    set_threads(n_threads);
+    const int32_t rc = format_fastq(r, w->tail);
+    if (rc != 0) return rc;
+    for (int d = 0; d < 2; d++) whole[d] = ((int64_t)w->tail[d].size() / kBlock) * kBlock;
+    return 0;
+}
+
+extern "C" int32_t bsdc_fastq_writer_take(bsdc_fastq_writer *w, int32_t which, int64_t nblk, uint8_t *dst, uint32_t *crc,
+                                          int32_t n_threads) {
+    set_threads(n_threads);
+    if (which != 0 && which != 1) return fail(BSDC_IO_EFORMAT, "no such FASTQ file");
+    return take_blocks(w->tail[which], nblk, dst, crc);
+}
+
+extern "C" int32_t bsdc_fastq_writer_put(bsdc_fastq_writer *w, int32_t which, int64_t nblk, uint8_t *packed,
+                                         const int32_t *sizes, const uint32_t *crc, const uint8_t *raw,
+                                         int32_t n_threads) {
+    set_threads(n_threads);
+    if (which != 0 && which != 1) return fail(BSDC_IO_EFORMAT, "no such FASTQ file");
+    return put_blocks(w->f[which], w->level, nblk, packed, sizes, crc, raw);
 }
 
 extern "C" int32_t bsdc_fastq_writer_close(bsdc_fastq_writer *w, int32_t n_threads) {

@@ -17,7 +17,7 @@
 extern "C" {
 #endif
 
-#define BSDC_IO_ABI_VERSION 6
+#define BSDC_IO_ABI_VERSION 7
 #define BSDC_IO_EFORMAT (-10) /* not BGZF/BAM, truncated, bad CRC */
 #define BSDC_IO_EIO (-11)     /* open/read/write failed */
 
@@ -159,6 +159,14 @@ int32_t bsdc_fastq_write(const char *path1, const char *path2, const bsdc_bam_re
 typedef struct bsdc_fastq_writer bsdc_fastq_writer;
 int32_t bsdc_fastq_writer_open(const char *path1, const char *path2, int32_t level, bsdc_fastq_writer **out);
 int32_t bsdc_fastq_writer_add(bsdc_fastq_writer *w, const bsdc_bam_records *r, int32_t n_threads);
+/* The FASTQ pair's whole blocks compressed by the caller, as for the BAM writer above: encode
+ * reports whole[d], the bytes of whole 65280-byte blocks at the front of file d's tail (d = 0, 1);
+ * take / put move and write file `which`'s blocks like bsdc_bam_writer_take / _put. */
+int32_t bsdc_fastq_writer_encode(bsdc_fastq_writer *w, const bsdc_bam_records *r, int32_t n_threads, int64_t *whole);
+int32_t bsdc_fastq_writer_take(bsdc_fastq_writer *w, int32_t which, int64_t nblk, uint8_t *dst, uint32_t *crc,
+                               int32_t n_threads);
+int32_t bsdc_fastq_writer_put(bsdc_fastq_writer *w, int32_t which, int64_t nblk, uint8_t *packed, const int32_t *sizes,
+                              const uint32_t *crc, const uint8_t *raw, int32_t n_threads);
 int32_t bsdc_fastq_writer_close(bsdc_fastq_writer *w, int32_t n_threads);
 
 /* Packed byte tables (entry r = buf[off[r], off[r + 1])), for the output records: per entry the

@@ -4,6 +4,7 @@ synthetic coordinate-sorted C2 BAM + FASTA on local disk, then, each in a fresh 
   whole   bam.step5: read the whole BAM, form every family, GPU batches, write the BAM
   stream  bam.step5_stream: bounded chunks, reader / GPU / writer threads overlapped
   stream_fastq  the same, writing the FASTQ pair of the next rule instead of the BAM
+  stream_gpubgzf, stream_fastq_gpubgzf  the same with the BGZF deflate on the GPU
   fleet   fleet.step5_stream_multi: this child reads and writes (it never touches the GPU), --workers
           spawned GPU worker processes (all on GPU 0 on a one-GPU box) run the batches
 The BAMs are compared byte for byte.  Usage:
@@ -66,10 +67,12 @@ def child(args):
     t0 = time.perf_counter()
     if args.mode == "whole":
         info = bam.step5(args.inp, args.fa, args.out, engine=eng, threads=args.threads, level=args.level)
-    elif args.mode == "stream_fastq":  # the fused FASTQ emission (main.snake.py:167-177), no BAM
+    elif args.mode in ("stream_fastq", "stream_fastq_gpubgzf"):  # the fused FASTQ emission
+        # (main.snake.py:167-177), no BAM; _gpubgzf: its blocks deflated on the GPU
         info = bam.step5_stream(args.inp, args.fa, None, engine=eng, threads=args.threads, level=args.level,
                                 fastq=(args.out + ".1.fq.gz", args.out + ".2.fq.gz"),
-                                chunk_bytes=args.chunk_mb << 20, stats=stats)
+                                chunk_bytes=args.chunk_mb << 20, stats=stats,
+                                gpu_bgzf=args.mode == "stream_fastq_gpubgzf")
     else:  # stream, or stream_gpubgzf: the BAM's blocks deflated on the GPU (bam.GpuBgzf)
         info = bam.step5_stream(args.inp, args.fa, args.out, engine=eng, threads=args.threads, level=args.level,
                                 chunk_bytes=args.chunk_mb << 20, stats=stats, gpu_bgzf=args.mode == "stream_gpubgzf")
@@ -128,7 +131,7 @@ def main():
         res[mode] = r
         outs[mode] = out
         print(mode, json.dumps(r), flush=True)
-    bams = [open(outs[m], "rb").read() for m in outs if m not in ("stream_fastq", "stream_gpubgzf")]
+    bams = [open(outs[m], "rb").read() for m in outs if m not in ("stream_fastq", "stream_gpubgzf", "stream_fastq_gpubgzf")]
     res["outputs_identical"] = all(b == bams[0] for b in bams)
     if "stream_gpubgzf" in outs and "stream" in outs:  # other compressed bytes: compare the records
         sys.path.insert(0, ROOT)
@@ -138,6 +141,11 @@ def main():
         res["gpubgzf_records_identical"] = bool(ra.n == rb.n and (ra.seq == rb.seq).all() and (ra.qual == rb.qual).all()
                                                 and (ra.aux.buf == rb.aux.buf).all())
         res["gpubgzf_size_ratio"] = round(os.path.getsize(outs["stream_gpubgzf"]) / os.path.getsize(outs["stream"]), 3)
+    if "stream_fastq_gpubgzf" in outs and "stream_fastq" in outs:  # the same FASTQ text
+        import gzip
+        res["fastq_gpubgzf_text_identical"] = all(
+            gzip.open(outs["stream_fastq"] + x).read() == gzip.open(outs["stream_fastq_gpubgzf"] + x).read()
+            for x in (".1.fq.gz", ".2.fq.gz"))
     print(json.dumps(res))
     return 0
 
