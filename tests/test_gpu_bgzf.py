@@ -92,3 +92,24 @@ def test_kernel_launches_in_pieces(monkeypatch):
     for k, (g, d) in enumerate(zip(got, blocks)):
         ref = oracle.bgzf_block(d)
         assert g[:-8] == ref[:-8], k
+
+
+def test_fastq_writer_with_gpu_bgzf(tmp_path):
+    """The paired-FASTQ writer with the GPU encoder: both files' blocks in one job, split back per
+    file; the FASTQ text equals the host-deflated writer's."""
+    import gzip
+    _, _, recs = _step5_bytes(3000, seed=13)
+    a = (str(tmp_path / "a1.fq.gz"), str(tmp_path / "a2.fq.gz"))
+    b = (str(tmp_path / "b1.fq.gz"), str(tmp_path / "b2.fq.gz"))
+    w = bam.FastqWriter(a[0], a[1], 5)
+    w.add(recs, 4)
+    w.close(4)
+    g = bam.GpuBgzf(0)
+    w = bam.FastqWriter(b[0], b[1], 5, gpu=g)
+    half = recs.n // 2 & ~1
+    w.add(bam.take_records(recs, np.arange(half)), 4)
+    w.add(bam.take_records(recs, np.arange(half, recs.n)), 4)
+    w.close(4)
+    assert g.blocks >= 2
+    for x, y in zip(a, b):
+        assert gzip.open(x).read() == gzip.open(y).read()
