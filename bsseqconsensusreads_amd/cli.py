@@ -47,7 +47,7 @@ def parse(argv):
         if name == "step5":
             p.add_argument("--gpus", type=int, default=1, help="one process per GPU, family batches dealt to them")
             p.add_argument("--gpu-bgzf", default="false", choices=("true", "false"),
-                           help="deflate the output BAM's blocks on the GPU (streaming, one GPU; larger file)")
+                           help="deflate the output BAM's and FASTQ pair's blocks on the GPU (streaming, one GPU; files ~4%% larger)")
             p.add_argument("--devices", default=None, help="comma-separated device id per rank (default 0..gpus-1)")
             p.add_argument("--batch-bases", type=int, default=None, help="device batch budget in bases")
             p.add_argument("--stream", default="auto", choices=["auto", "true", "false"],
