@@ -290,7 +290,7 @@ def read_bam(path: str, threads: int = 0):
         lib.bsdc_bam_free(h)
 
 
-DEFAULT_CHUNK_BYTES = 128 << 20  # uncompressed record bytes per stream chunk (about 0.45M records)
+DEFAULT_CHUNK_BYTES = 64 << 20  # uncompressed record bytes per stream chunk (about 0.23M records)
 DEFAULT_SLACK = 10_000           # positions: > any template's span (fragment + clips)
 
 

@@ -54,7 +54,7 @@ def parse(argv):
                            help="bounded-memory pipelined step (bam.step5_stream; coordinate-sorted input, one GPU); "
                                 "false = read the whole BAM first (bam.step5); auto = stream when the header "
                                 "says SO:coordinate")
-            p.add_argument("--chunk-mb", type=int, default=128, help="--stream: record MiB per chunk")
+            p.add_argument("--chunk-mb", type=int, default=64, help="--stream: record MiB per chunk")
         p.add_argument("--output-per-base-tags", default="true", choices=["true", "false"],
                        help="fgbio's consensus tags (per-read and per-base statistics); off = name/SEQ/QUAL/RG/MI/RX")
     a = ap.parse_args(argv)

@@ -90,7 +90,7 @@ def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--families", type=int, default=1_000_000)
     ap.add_argument("--threads", type=int, default=16)
-    ap.add_argument("--chunk-mb", type=int, default=128)
+    ap.add_argument("--chunk-mb", type=int, default=64)
     ap.add_argument("--level", type=int, default=5)
     ap.add_argument("--mode", default=None)
     ap.add_argument("--modes", default="stream,stream_fastq,whole")
