@@ -299,6 +299,8 @@ def step5_stream_multi(in_bam: str, fasta: str, out_bam: Optional[str], devices:
         with plock:
             plock.notify_all()
 
+    bufs = bam.BufferPool()  # a chunk's record and tag arrays, given back once it is written
+
     def decoder():  # cuts the next chunk while the planner decodes and plans the one before
         it = None
         try:
@@ -326,7 +328,7 @@ def step5_stream_multi(in_bam: str, fasta: str, out_bam: Optional[str], devices:
                     ch.discard()
                     continue  # drain to the decoder's None
                 t1 = time.perf_counter()
-                raw = ch.decode(threads)[1]
+                raw = ch.decode(threads, pool=bufs)[1]
                 t2 = time.perf_counter()
                 plan = pipeline.plan_families(raw, "full", ref)
                 T["plan"] += time.perf_counter() - t2
@@ -388,7 +390,7 @@ def step5_stream_multi(in_bam: str, fasta: str, out_bam: Optional[str], devices:
                 info["families"] += int(cons.status.shape[0])
                 info["families_emitted"] += int(((cons.status & 1) != 0).sum())
                 t0 = time.perf_counter()
-                recs = bam.duplex_records(cons, c["raw"], pre, threads)
+                recs = bam.duplex_records(cons, c["raw"], pre, threads, pool=bufs)
                 t1 = time.perf_counter()
                 if w is not None:
                     w.add(recs, threads)
@@ -397,6 +399,10 @@ def step5_stream_multi(in_bam: str, fasta: str, out_bam: Optional[str], devices:
                 info["records_out"] += recs.n
                 T["records"] += t1 - t0
                 T["encode"] += time.perf_counter() - t1
+                back = [getattr(c["raw"], "_pool_buf", None), getattr(recs.aux2, "_pool_buf", None)]
+                del c, cons, recs
+                for buf in back:  # (the chunk is written: nothing refers to its record arrays)
+                    bufs.give(buf)
             if not stop.is_set():
                 if w is not None:
                     w.close(threads)
