@@ -8,7 +8,7 @@ HERE = os.path.dirname(os.path.abspath(__file__))
 # BSDC_LIB_PATH: an alternative build of the same library (profiling A/B runs only)
 LIB_PATH = os.environ.get("BSDC_LIB_PATH") or os.path.join(HERE, "libbsdc.so")
 
-BSDC_ABI_VERSION = 9
+BSDC_ABI_VERSION = 10
 SMALL_BUCKETS = 8  # BSDC_SMALL_BUCKETS
 LARGE_BUCKETS = 6  # BSDC_LARGE_BUCKETS
 MODE_CONVERT, MODE_EXTEND, MODE_VOTE, MODE_DUMP = 1, 2, 4, 8
@@ -19,7 +19,7 @@ MODE_TAGS = 64  # single-strand reads + column statistics for the consensus tags
 class Params(C.Structure):
     _fields_ = [("error_rate_pre_umi", C.c_double), ("error_rate_post_umi", C.c_double),
                 ("min_input_base_quality", C.c_int32), ("consensus_call_overlapping_bases", C.c_int32),
-                ("min_reads", C.c_int32), ("reserved", C.c_int32)]
+                ("min_reads", C.c_int32), ("min_consensus_base_quality", C.c_int32)]
 
 
 class FamilyBatchC(C.Structure):
@@ -41,7 +41,7 @@ class ConsensusC(C.Structure):
                 ("ss_err", C.c_void_p)]
 
 
-EXPORTS = ("bsdc_abi_version", "bsdc_ctx_create", "bsdc_ctx_destroy", "bsdc_last_error",
+EXPORTS = ("bsdc_abi_version", "bsdc_ctx_create", "bsdc_ctx_set_params", "bsdc_ctx_destroy", "bsdc_last_error",
            "bsdc_load_reference", "bsdc_run", "bsdc_convert", "bsdc_extend", "bsdc_duplex_call",
            "bsdc_family_arena_bytes", "bsdc_small_arena_bytes", "bsdc_get_tables", "bsdc_model_tables",
            "bsdc_model_tables_fp64", "bsdc_agree_tables", "bsdc_phred_buckets", "bsdc_bgzf_scratch_bytes",
@@ -61,6 +61,8 @@ def load(path: str = LIB_PATH):
     lib.bsdc_abi_version.restype = C.c_int32
     lib.bsdc_ctx_create.argtypes = [C.c_int32, C.POINTER(Params), C.POINTER(C.c_void_p)]
     lib.bsdc_ctx_create.restype = C.c_int32
+    lib.bsdc_ctx_set_params.argtypes = [C.c_void_p, C.POINTER(Params)]
+    lib.bsdc_ctx_set_params.restype = C.c_int32
     lib.bsdc_ctx_destroy.argtypes = [C.c_void_p]
     lib.bsdc_ctx_destroy.restype = None
     lib.bsdc_last_error.argtypes = [C.c_void_p]

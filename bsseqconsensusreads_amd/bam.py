@@ -803,6 +803,19 @@ class BamWriter:
                     raise self._err()
 
 
+def close_quietly(*writers):
+    """Best-effort close of writers a failed step leaves open (BamWriter / FastqWriter / None):
+    finishes their in-flight GPU BGZF job and releases the C writer's FILE and buffers, swallowing
+    secondary errors (the step raises its first error anyway; the partial output is garbage)."""
+    for w in writers:
+        if w is None:
+            continue
+        try:
+            w.close()
+        except Exception:  # noqa: BLE001
+            pass
+
+
 class FastqWriter:
     """Streaming paired-FASTQ writer (bsdc_fastq_writer): the bytes write_fastq writes for all the
     records at once; every add holds whole pairs.  With `gpu` (a GpuBgzf), the whole blocks of
@@ -1210,6 +1223,7 @@ def step5_stream(in_bam: str, fasta: str, out_bam: Optional[str], engine=None, p
             recq.put(None)
 
     def writer():
+        w = fq = None
         try:
             gz = GpuBgzf(eng.device) if gpu_bgzf and out_bam is not None else None
             gzf = GpuBgzf(eng.device) if gpu_bgzf and fastq is not None else None  # (one job in flight each)
@@ -1237,6 +1251,7 @@ def step5_stream(in_bam: str, fasta: str, out_bam: Optional[str], engine=None, p
         except BaseException as e:  # noqa: BLE001
             err.append(e)
             stop.set()
+            close_quietly(w, fq)
             while recq.get() is not None:  # drain so the builder never blocks
                 pass
 
@@ -1311,7 +1326,8 @@ def step5_stream(in_bam: str, fasta: str, out_bam: Optional[str], engine=None, p
 
 
 def molecular(in_bam: str, out_bam: Optional[str], engine=None, prefix: Optional[str] = None, threads: int = 0,
-              level: int = 6, fastq: Optional[Tuple[str, str]] = None, tags: bool = True) -> dict:
+              level: int = 6, fastq: Optional[Tuple[str, str]] = None, tags: bool = True,
+              min_consensus_base_quality: int = 0) -> dict:
     """Rule call_consensus_reads_molecular (main.snake.py:46-55, fgbio CallMolecularConsensusReads)
     on files; with `fastq`, also consensus_to_fq_unfiltered (main.snake.py:58-67)."""
     from . import pipeline
@@ -1320,7 +1336,8 @@ def molecular(in_bam: str, out_bam: Optional[str], engine=None, prefix: Optional
     own = engine is None
     eng = Engine(0) if own else engine
     try:
-        cons, rm = pipeline.run_molecular(eng, raw, tags=tags and out_bam is not None)
+        cons, rm = pipeline.run_molecular(eng, raw, tags=tags and out_bam is not None,
+                                          min_consensus_base_quality=min_consensus_base_quality)
     finally:
         if own:
             eng.close()

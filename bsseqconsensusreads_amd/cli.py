@@ -55,6 +55,9 @@ def parse(argv):
                                 "false = read the whole BAM first (bam.step5); auto = stream when the header "
                                 "says SO:coordinate")
             p.add_argument("--chunk-mb", type=int, default=64, help="--stream: record MiB per chunk")
+        else:
+            p.add_argument("--min-consensus-base-quality", type=int, default=0,
+                           help="mask single-strand calls below this phred to N (main.snake.py:54 passes 0)")
         p.add_argument("--output-per-base-tags", default="true", choices=["true", "false"],
                        help="fgbio's consensus tags (per-read and per-base statistics); off = name/SEQ/QUAL/RG/MI/RX")
     a = ap.parse_args(argv)
@@ -132,7 +135,8 @@ def main(argv=None) -> int:
                                  tags=a.output_per_base_tags == "true", batch_bases=a.batch_bases, dist=dist)
             else:
                 info = bam.molecular(a.input, out, eng, a.read_name_prefix, a.threads, a.compression, fq,
-                                     tags=a.output_per_base_tags == "true")
+                                     tags=a.output_per_base_tags == "true",
+                                     min_consensus_base_quality=a.min_consensus_base_quality)
         finally:
             eng.close()
     except Exception as e:  # noqa: BLE001 -- the rule fails with the message, like the tools do

@@ -20,10 +20,16 @@
 #include <string_view>
 #include <unordered_map>
 #include <mutex>
+#include <chrono>
 #include <vector>
 #ifdef _OPENMP
 #include <omp.h>
 #include <parallel/algorithm>
+#else  // a build without -fopenmp runs every parallel region on one thread
+inline int omp_get_max_threads() { return 1; }
+inline int omp_get_thread_num() { return 0; }
+inline int omp_get_num_threads() { return 1; }
+#endif
 
 // Byte buffers that grow without zero-filling: every byte is written before it is read (inflate,
 // record encode, deflate slots), and value-initialising gigabytes per chunk was serial memset time
@@ -46,7 +52,6 @@ struct NoInit : std::allocator<T> {
     }
 };
 using Bytes = std::vector<uint8_t, NoInit<uint8_t>>;
-#endif
 
 namespace {
 
@@ -171,7 +176,9 @@ void set_threads(int n) {
 }
 
 const char kCigarOps[] = "MIDNSHP=X";
-inline double now_s() { return omp_get_wtime(); }
+inline double now_s() {
+    return std::chrono::duration<double>(std::chrono::steady_clock::now().time_since_epoch()).count();
+}
 
 // packed SEQ byte -> its two bases as one little-endian uint16 (high nibble first)
 struct NibblePairs {

@@ -182,7 +182,8 @@ __device__ __forceinline__ int phred_of(float S, const float *thr) {
 }
 
 // Per-column statistics of a single-strand consensus read (BSDC_MODE_TAGS), as fgbio
-// VanillaUmiConsensusCaller keeps them for the consensus tags: the call itself (N / 2 below Q2),
+// VanillaUmiConsensusCaller keeps them for the consensus tags: the call itself (N / 2 below the
+// caller's --min-consensus-base-quality, KParams::qmin, or without an A/C/G/T read),
 // depth = reads with an A/C/G/T at the column, errors = depth - reads showing the RAW best base
 // (before the Q2 mask; a column without reads has depth 0 and errors 0).  Both counts saturate at
 // 32767 (fgbio stores Shorts).  D: likelihood sums (2^-20 nats), n: reads per base.
@@ -254,7 +255,7 @@ __device__ FP64_PICK_ATTR int fp64_pick(const Desc &ds, int n, int col, const ui
             bool rv;
             ds.get(i, a, len, rv);
             if (len <= col) continue;
-            const uint64_t key = ((uint64_t)(0xFFFFu - (uint32_t)len) << 32) | a;
+            const uint64_t key = ((uint64_t)(0x7FFFFFFFu - (uint32_t)len) << 32) | a;  // (len < 2^31)
             if (key >= lo && key < kb) {
                 kb = key;
                 ab = a;
@@ -295,8 +296,8 @@ struct LargeDesc {  // k_large: uint2 {address, length | reverse << 31}
 };
 // the call of one single-strand column with its statistics; pick() gives fgbio's base on a near tie
 template <class Pick>
-__device__ __forceinline__ void ss_store(const SsAcc &a, const float *thr, int nset, Pick pick, uint8_t *b, uint8_t *q,
-                                         uint16_t *dp, uint16_t *er) {
+__device__ __forceinline__ void ss_store(const SsAcc &a, const float *thr, int nset, int qmin, Pick pick, uint8_t *b,
+                                         uint8_t *q, uint16_t *dp, uint16_t *er) {
     int best = first_max4(a.D[0], a.D[1], a.D[2], a.D[3]);
     if (near_tie(a.D[0], a.D[1], a.D[2], a.D[3], best, nset)) best = pick();
     const long long Db = a.D[best];
@@ -306,8 +307,9 @@ __device__ __forceinline__ void ss_store(const SsAcc &a, const float *thr, int n
         if (x != best) S += term(a.D[x] - Db);
     const int Q = phred_of(S, thr);
     const uint32_t depth = a.n[0] + a.n[1] + a.n[2] + a.n[3];
-    *b = Q < 2 ? (uint8_t)kN : (uint8_t)(1u << best);
-    *q = Q < 2 ? (uint8_t)2 : (uint8_t)Q;
+    const bool nocall = depth == 0 || Q < qmin;  // (NoCall, NoCallQual): no A/C/G/T read, or below the mask
+    *b = nocall ? (uint8_t)kN : (uint8_t)(1u << best);
+    *q = nocall ? (uint8_t)2 : (uint8_t)Q;
     *dp = (uint16_t)::min(depth, 32767u);
     *er = (uint16_t)::min(depth - a.n[best], 32767u);
 }
@@ -546,6 +548,7 @@ struct KParams {
     int32_t overlap;
     int32_t ref_chunks;       // 16-B chunks per reference window (ref_chunks(max_len))
     uint32_t ref_chunks_inv;  // ceil(2^32 / ref_chunks)
+    int32_t qmin;             // bsdc_params.min_consensus_base_quality: single-strand Q below it -> (N, 2)
 };
 
 // the first `bytes` of the Tables image (k_small: all of it; k_large: the kTabBytesL prefix)
@@ -831,12 +834,13 @@ __device__ __forceinline__ uint32_t bytes_nonzero(uint32_t x) {  // 0xFF where t
 }
 // Single-strand results of 4 columns -> duplex (fgbio DuplexConsensusCaller.duplexConsensus), in
 // bytes.  bmX: one-hot bases seen by side X (0 = none), QX: its phred from the likelihood sum.
-// Q < 2 -> (N, 2); one side absent -> the other side; both -> agree: sum, else the higher
+// Q < qmin -> (N, 2); one side absent -> the other side; both -> agree: sum, else the higher
 // quality's base with the difference, equal qualities -> 2; capped at 93; N or 2 -> (N, 2).
+// qadd = (128 - qmin) x 0x01010101: a byte Q (<= 93) + (128 - qmin) reaches bit 7 iff Q >= qmin.
 __device__ __forceinline__ void resolve4(bool ha, bool hb, uint32_t bmA, uint32_t QA, uint32_t bmB, uint32_t QB,
-                                         uint32_t &ob, uint32_t &oq, uint32_t *ss) {
-    const uint32_t okA = expand80((QA + 0x7E7E7E7Eu) & 0x80808080u);  // Q >= 2
-    const uint32_t okB = expand80((QB + 0x7E7E7E7Eu) & 0x80808080u);
+                                         uint32_t qadd, uint32_t &ob, uint32_t &oq, uint32_t *ss) {
+    const uint32_t okA = expand80((QA + qadd) & 0x80808080u);  // Q >= qmin
+    const uint32_t okB = expand80((QB + qadd) & 0x80808080u);
     const uint32_t bA = (bmA & okA) | (0x0F0F0F0Fu & ~okA), qA = (QA & okA) | (0x02020202u & ~okA);
     const uint32_t bB = (bmB & okB) | (0x0F0F0F0Fu & ~okB), qB = (QB & okB) | (0x02020202u & ~okB);
     ss[0] = bA;  // the single-strand results: side A bases, quals, side B bases, quals
@@ -1375,6 +1379,7 @@ __global__ __launch_bounds__(kWave *kSmallMaxWaves, kSmallMinWaves) __attribute_
     }
     if (emit && stop != 6) {
         const int ow = Lo.ow;
+        const uint32_t qadd = (uint32_t)(128 - P.qmin) * 0x01010101u;
         uint8_t *outb = A + Lo.outb;  // [2][ow] duplex bases
         uint8_t *outq = A + Lo.outq;  // [2][ow] duplex quals
         uint16_t *sq = reinterpret_cast<uint16_t *>(A + Lo.squeue);
@@ -1449,7 +1454,7 @@ __global__ __launch_bounds__(kWave *kSmallMaxWaves, kSmallMinWaves) __attribute_
                     }
                 }
                 uint32_t ob4, oq4, ss[4];
-                resolve4(hs[sa], hs[sb], bm[0], Qp[0], bm[1], Qp[1], ob4, oq4, ss);
+                resolve4(hs[sa], hs[sb], bm[0], Qp[0], bm[1], Qp[1], qadd, ob4, oq4, ss);
                 // slow columns: a side saw more than one base, or a negative sum.  The queued
                 // path recomputes only the slow side(s): the other side's single-strand result
                 // rides in the column's output bytes (base | 0x10 if it is side B; qual 0 = none).
@@ -1500,11 +1505,13 @@ __global__ __launch_bounds__(kWave *kSmallMaxWaves, kSmallMinWaves) __attribute_
                 vq = kq;
             } else if (have) {
                 int32_t D0 = 0, D1 = 0, D2 = 0, D3 = 0;
+                uint32_t seen = 0;  // bit 4 of a base byte: A/C/G/T
                 for (int i = 0; i < ns; i++) {
                     const uint32_t d = dlist[os + i];
                     if (c >= (int)((d >> 16) & 0x7FFF)) continue;
                     const uint32_t idx = (d & 0x80000000u) ? (d & 0xFFFF) - c : (d & 0xFFFF) + c;
                     const uint32_t braw = bimg[idx];
+                    seen |= braw;
                     const int32_t v = lr2[(braw >> 4) * 256u + qimg[idx]];
                     const uint32_t bb = (d & 0x80000000u) ? comp_nt16(braw) : (braw & 0x0F);
                     D0 += bb == kA ? v : 0;
@@ -1522,8 +1529,9 @@ __global__ __launch_bounds__(kWave *kSmallMaxWaves, kSmallMinWaves) __attribute_
                 if (best != 2) S += term32(D2 - Db);
                 if (best != 3) S += term32(D3 - Db);
                 const int Q = phred_of(S, thr);
-                vb = Q < 2 ? kN : (1u << best);
-                vq = Q < 2 ? 2u : (uint32_t)Q;
+                const bool nocall = !(seen & 0x10u) || Q < P.qmin;  // no A/C/G/T read, or below the mask
+                vb = nocall ? kN : (1u << best);
+                vq = nocall ? 2u : (uint32_t)Q;
             }
             const uint32_t pb = (uint32_t)__shfl_xor((int)vb, 1, kWave), pq = (uint32_t)__shfl_xor((int)vq, 1, kWave);
             if (act && side == 0) {
@@ -1580,7 +1588,7 @@ __global__ __launch_bounds__(kWave *kSmallMaxWaves, kSmallMinWaves) __attribute_
                     acc.add(bb, lr2[256 + qimg[idx]]);  // only one-hot codes count
                 }
                 auto pick = [&]() { return fp64_pick(SmallDesc{dlist + off[s]}, cnt[s], c, bimg, qimg, P.tab->lnc, P.tab->lne3); };
-                ss_store(acc, thr, cnt[s], pick, P.O.ss_base + row + c, P.O.ss_qual + row + c, P.O.ss_depth + row + c,
+                ss_store(acc, thr, cnt[s], P.qmin, pick, P.O.ss_base + row + c, P.O.ss_qual + row + c, P.O.ss_depth + row + c,
                          P.O.ss_err + row + c);
             }
             if (t == 0) P.O.ss_len[4 * fam + s] = (uint16_t)ls;
@@ -2161,8 +2169,10 @@ __device__ void process_large(const KParams &P, uint8_t *A, uint8_t *s_tab, cons
         if (best != 2) S += term(D2 - Db);
         if (best != 3) S += term(D3 - Db);
         const int Q = phred_of(S, thr);
-        ssb[s * ssw + col] = Q < 2 ? (uint8_t)kN : (uint8_t)(1u << best);
-        ssq[s * ssw + col] = Q < 2 ? (uint8_t)2 : (uint8_t)Q;
+        // pass A left the OR of the column's A/C/G/T codes in ssb: 0 = no A/C/G/T read
+        const bool nocall = ssb[s * ssw + col] == 0 || Q < P.qmin;
+        ssb[s * ssw + col] = nocall ? (uint8_t)kN : (uint8_t)(1u << best);
+        ssq[s * ssw + col] = nocall ? (uint8_t)2 : (uint8_t)Q;
     };
     // Wavefronts by set: wave w works on set w % 4; with 8 waves (512 threads) the two waves of a
     // set split its reads (PARTS = 2).
@@ -2269,9 +2279,10 @@ __device__ void process_large(const KParams &P, uint8_t *A, uint8_t *s_tab, cons
                         const float e = term(-Tj);
                         const float S = ((0.0f + e) + e) + e;
                         const int Q = phred_of(S, thr);
-                        ssb[ws * ssw + col] = Q < 2 ? (uint8_t)kN : (uint8_t)ob;
-                        ssq[ws * ssw + col] = Q < 2 ? (uint8_t)2 : (uint8_t)Q;
+                        ssb[ws * ssw + col] = Q < P.qmin ? (uint8_t)kN : (uint8_t)ob;
+                        ssq[ws * ssw + col] = Q < P.qmin ? (uint8_t)2 : (uint8_t)Q;
                     } else {
+                        ssb[ws * ssw + col] = (uint8_t)ob;  // (the OR: pass B's no-call test)
                         ssq[ws * ssw + col] = 0;
                     }
                 }
@@ -2456,7 +2467,7 @@ __device__ void process_large(const KParams &P, uint8_t *A, uint8_t *s_tab, cons
             }
             const int64_t at = (4 * (int64_t)fam + s) * stride + c;
             auto pick = [&]() { return fp64_pick(LargeDesc{dl}, cnt[s], c, slots, qimg, P.tab->lnc, P.tab->lne3); };
-            ss_store(acc, thr, cnt[s], pick, P.O.ss_base + at, P.O.ss_qual + at, P.O.ss_depth + at, P.O.ss_err + at);
+            ss_store(acc, thr, cnt[s], P.qmin, pick, P.O.ss_base + at, P.O.ss_qual + at, P.O.ss_depth + at, P.O.ss_err + at);
         }
         if (tt < 4) P.O.ss_len[4 * fam + tt] = (uint16_t)(hs[tt] ? lcv[tt] : 0);
     }
@@ -2650,6 +2661,30 @@ static void make_fp64(double post, double *lnc, double *lne3) {
 extern "C" {
 
 int32_t bsdc_abi_version(void) { return BSDC_ABI_VERSION; }
+
+static bool params_ok(const bsdc_params *p) {
+    return p->min_reads == 0 && p->min_input_base_quality >= 0 && p->min_consensus_base_quality >= 0 &&
+           p->min_consensus_base_quality <= 94;
+}
+
+int32_t bsdc_ctx_set_params(bsdc_ctx *c, const bsdc_params *params) {
+    if (!c || !params) return BSDC_EINVAL;
+    if (!params_ok(params)) {
+        c->err = "bad params";
+        return BSDC_EINVAL;
+    }
+    if (params->error_rate_pre_umi != c->params.error_rate_pre_umi ||
+        params->error_rate_post_umi != c->params.error_rate_post_umi) {
+        // new tables: no launch of this context may still read the old ones
+        HIP_OK(c, hipSetDevice(c->device));
+        HIP_OK(c, hipDeviceSynchronize());
+        make_tables(params->error_rate_pre_umi, params->error_rate_post_umi, c->host_tab.t);
+        make_fp64(params->error_rate_post_umi, c->host_tab.lnc, c->host_tab.lne3);
+        HIP_OK(c, hipMemcpy(c->dev_tab, &c->host_tab, sizeof(DevTables), hipMemcpyHostToDevice));
+    }
+    c->params = *params;  // the rest is read at launch time (bsdc_run)
+    return 0;
+}
 void bsdc_ctx_destroy(bsdc_ctx *c);
 
 int64_t bsdc_family_arena_bytes(int32_t n_rec, int64_t slot_bytes, int32_t max_len, int64_t complex_ops) {
@@ -2690,7 +2725,7 @@ void bsdc_phred_buckets(double pre, double post, uint8_t *sq144) {
 int32_t bsdc_ctx_create(int32_t device, const bsdc_params *params, bsdc_ctx **out) {
     if (!out || !params) return BSDC_EINVAL;
     *out = nullptr;
-    if (params->min_reads != 0 || params->min_input_base_quality < 0) return BSDC_EINVAL;
+    if (!params_ok(params)) return BSDC_EINVAL;
     int n = 0;
     if (hipGetDeviceCount(&n) != hipSuccess || device < 0 || device >= n) return BSDC_EDEVICE;
     bsdc_ctx *c = new bsdc_ctx();
@@ -2803,6 +2838,7 @@ int32_t bsdc_run(bsdc_ctx *c, const bsdc_family_batch *b, bsdc_consensus *o, int
     P.overlap = c->params.consensus_call_overlapping_bases;
     P.ref_chunks = ref_chunks(b->max_len);
     P.ref_chunks_inv = (uint32_t)((((uint64_t)1 << 32) + (uint64_t)P.ref_chunks - 1) / (uint64_t)P.ref_chunks);
+    P.qmin = c->params.min_consensus_base_quality;
     // the dispatches: on `s`, or (BSDC_FORK) spread over the side streams (created with the
     // context) after an event on `s`
     int nd = 0, used = 0;

@@ -6,8 +6,9 @@ The Engine owns one libbsdc context per GPU.  ``upload`` copies a FamilyBatch in
 """
 from __future__ import annotations
 
+import contextlib
 import ctypes as C
-from dataclasses import dataclass
+from dataclasses import dataclass, replace
 from typing import Dict, Optional
 
 import numpy as np
@@ -20,13 +21,30 @@ from .records import Reference
 
 @dataclass
 class ConsensusParams:
-    """fgbio CallDuplexConsensusReads options, defaults from main.snake.py:163."""
+    """fgbio CallDuplexConsensusReads options, defaults from main.snake.py:163.
+    min_consensus_base_quality: single-strand calls below it become (N, 2).  The duplex caller
+    passes no such flag; fgbio's single-strand caller inside it masks below PhredScore.MinValue = 2
+    (DESIGN.md 3.5).  Step 1 passes --min-consensus-base-quality=0 (main.snake.py:54):
+    MOLECULAR_PARAMS."""
 
     error_rate_pre_umi: float = 45.0
     error_rate_post_umi: float = 30.0
     min_input_base_quality: int = 0
     consensus_call_overlapping_bases: bool = True
     min_reads: int = 0
+    min_consensus_base_quality: int = 2
+
+    def c_struct(self):
+        return _lib.Params(self.error_rate_pre_umi, self.error_rate_post_umi, self.min_input_base_quality,
+                           int(self.consensus_call_overlapping_bases), self.min_reads,
+                           self.min_consensus_base_quality)
+
+
+# fgbio CallMolecularConsensusReads as rule call_consensus_reads_molecular runs it (main.snake.py:54):
+# --error-rate-pre-umi=45 --error-rate-post-umi=30 --min-input-base-quality=0
+# --min-consensus-base-quality=0 --consensus-call-overlapping-bases=true (--min-reads=1: a column
+# without an A/C/G/T read is a no-call, as in the duplex caller's single-strand caller)
+MOLECULAR_PARAMS = ConsensusParams(min_consensus_base_quality=0)
 
 
 def _dptr(t: torch.Tensor) -> int:
@@ -202,15 +220,33 @@ class Engine:
         self.params = params or ConsensusParams()
         self._stage = [None, None]  # pinned family-image staging buffers (stage_images)
         self._stage_i = 0
-        p = _lib.Params(self.params.error_rate_pre_umi, self.params.error_rate_post_umi,
-                        self.params.min_input_base_quality, int(self.params.consensus_call_overlapping_bases),
-                        self.params.min_reads, 0)
+        p = self.params.c_struct()
         h = C.c_void_p()
         rc = self.lib.bsdc_ctx_create(device_index, C.byref(p), C.byref(h))
         if rc != 0:
             raise RuntimeError("bsdc_ctx_create failed (%d)" % rc)
         self.ctx = h
         self.ref: Optional[Reference] = None
+
+    def set_params(self, params: ConsensusParams):
+        """Replace the context's flags (bsdc_ctx_set_params); later launches use them."""
+        p = params.c_struct()
+        self._check(self.lib.bsdc_ctx_set_params(self.ctx, C.byref(p)), "bsdc_ctx_set_params")
+        self.params = params
+
+    @contextlib.contextmanager
+    def flags(self, **changes):
+        """`with engine.flags(min_consensus_base_quality=0): ...` -- the engine runs with these
+        flags inside the block and its own afterwards (one context serving step 1 and step 5)."""
+        old = self.params
+        if all(getattr(old, k) == v for k, v in changes.items()):
+            yield self
+            return
+        self.set_params(replace(old, **changes))
+        try:
+            yield self
+        finally:
+            self.set_params(old)
 
     def stage_images(self, n_slots: int):
         """Pinned host arrays (seq, qual) for the next batch's family images (materialize's

@@ -183,7 +183,8 @@ class Fleet:
         for p in self.procs:
             p.start()
         self.n = len(devices)
-        self.load = [0] * self.n
+        self.load = [0] * self.n  # jobs in flight per worker (submit: dealer thread, done: collector)
+        self._load_lock = threading.Lock()
         self.slots = threading.Semaphore(max(1, inflight) * self.n)
         self.needs_raw = False
         try:
@@ -224,13 +225,15 @@ class Fleet:
         while not self.slots.acquire(timeout=0.5):
             if stop is not None and stop.is_set():
                 return -1
-        w = min(range(self.n), key=lambda i: self.load[i])
-        self.load[w] += 1
+        with self._load_lock:
+            w = min(range(self.n), key=lambda i: self.load[i])
+            self.load[w] += 1
         self.tqs[w].put(msg)
         return w
 
     def done(self, wid: int):
-        self.load[wid] -= 1
+        with self._load_lock:
+            self.load[wid] -= 1
         self.slots.release()
 
     def close(self, timeout: float = 60.0):
@@ -377,6 +380,7 @@ def step5_stream_multi(in_bam: str, fasta: str, out_bam: Optional[str], devices:
             outs.put(None)
 
     def writer():
+        w = fq = None
         try:
             w = bam.BamWriter(out_bam, bam.output_header(hdr0), level) if out_bam is not None else None
             fq = bam.FastqWriter(fastq[0], fastq[1], level) if fastq is not None else None
@@ -408,8 +412,11 @@ def step5_stream_multi(in_bam: str, fasta: str, out_bam: Optional[str], devices:
                     w.close(threads)
                 if fq is not None:
                     fq.close(threads)
+            else:
+                bam.close_quietly(w, fq)
         except BaseException as e:  # noqa: BLE001
             fail(e)
+            bam.close_quietly(w, fq)
             while outs.get() is not None:
                 pass
 

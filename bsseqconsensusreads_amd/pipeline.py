@@ -421,10 +421,13 @@ def molecular_records(raw: R.RawRecords) -> R.RawRecords:
     return dataclasses.replace(raw, mi_id=mi_id, mi_strand=mi_strand, mi_names=names)
 
 
-def run_molecular(engine: Engine, raw: R.RawRecords, tags: bool = False):
+def run_molecular(engine: Engine, raw: R.RawRecords, tags: bool = False,
+                  min_consensus_base_quality: int = 0):
     """fgbio CallMolecularConsensusReads with the step-1 flags (main.snake.py:54: pre 45, post 30,
-    min-reads 1, overlapping bases on) -> (Consensus over the runs, the run records).  Consensus
-    family f is MI run f; its R1 / R2 are the single-strand consensus of the run's R1s / R2s."""
+    min-reads 1, min-consensus-base-quality 0, overlapping bases on) -> (Consensus over the runs,
+    the run records).  Consensus family f is MI run f; its R1 / R2 are the single-strand consensus
+    of the run's R1s / R2s.  The engine runs with min_consensus_base_quality for this call only."""
     rm = molecular_records(raw)
     plan = plan_families(rm, "vote", family_order="mi-group")
-    return concat_consensus(run_ranges(engine, plan, plan_ranges(plan), MODE_VOTE, tags)), rm
+    with engine.flags(min_consensus_base_quality=min_consensus_base_quality):
+        return concat_consensus(run_ranges(engine, plan, plan_ranges(plan), MODE_VOTE, tags)), rm

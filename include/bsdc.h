@@ -26,7 +26,7 @@
 extern "C" {
 #endif
 
-#define BSDC_ABI_VERSION 9
+#define BSDC_ABI_VERSION 10
 #define BSDC_SMALL_BUCKETS 8
 #define BSDC_LARGE_BUCKETS 6
 #define BSDC_LARGE_LDS_MAX 158912 /* LDS arena bytes one large-family workgroup may use */ /* LDS arena size classes of the wavefront-per-family kernel */
@@ -42,7 +42,11 @@ typedef struct {
     int32_t min_input_base_quality;           /* --min-input-base-quality=0 */
     int32_t consensus_call_overlapping_bases; /* --consensus-call-overlapping-bases=true */
     int32_t min_reads;                        /* --min-reads=0 (only 0 is supported) */
-    int32_t reserved;
+    int32_t min_consensus_base_quality;       /* single-strand calls with Q below it -> (N, 2), 0..94:
+                                                 2 for step 5 (fgbio DuplexConsensusCaller's single-strand
+                                                 caller masks at PhredScore.MinValue; main.snake.py:163
+                                                 passes no such flag), 0 for step 1
+                                                 (--min-consensus-base-quality=0, main.snake.py:54) */
 } bsdc_params;
 
 /* Per-record `link` word (host-built) */
@@ -133,6 +137,9 @@ typedef struct bsdc_ctx bsdc_ctx;
 
 int32_t bsdc_abi_version(void);
 int32_t bsdc_ctx_create(int32_t device, const bsdc_params *params, bsdc_ctx **out);
+/* Replace a context's flags (e.g. one GPU context serving both callers: step 1's flags at
+ * main.snake.py:54, step 5's at :163).  New error rates rebuild the tables after a device sync. */
+int32_t bsdc_ctx_set_params(bsdc_ctx *ctx, const bsdc_params *params);
 void bsdc_ctx_destroy(bsdc_ctx *ctx);
 const char *bsdc_last_error(const bsdc_ctx *ctx);
 

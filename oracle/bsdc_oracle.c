@@ -618,7 +618,8 @@ typedef struct {
     double lnc[256], lne3[256];
 } fp64tab;
 
-static int ss_consensus(srcread **v, int n, const int64_t *lr, const fp64tab *f64, const float *thr, ssread *out) {
+static int ss_consensus(srcread **v, int n, const int64_t *lr, const fp64tab *f64, const float *thr, int min_cbq,
+                        ssread *out) {
     int32_t lc = 0;
     for (int i = 0; i < n; i++)
         if (v[i]->len > lc) lc = v[i]->len;
@@ -676,14 +677,16 @@ static int ss_consensus(srcread **v, int n, const int64_t *lr, const fp64tab *f6
             else
                 break;
         }
-        if (Q < 2) {
+        const int32_t depth = obs[0] + obs[1] + obs[2] + obs[3];
+        /* no A/C/G/T read (fgbio: fewer contributions than min-reads 1) or below
+         * --min-consensus-base-quality: (NoCall, NoCallQual = 2) */
+        if (depth == 0 || Q < min_cbq) {
             out->b[c] = 'N';
             out->q[c] = 2;
         } else {
             out->b[c] = "ACGT"[best];
             out->q[c] = (uint8_t)Q;
         }
-        const int32_t depth = obs[0] + obs[1] + obs[2] + obs[3];
         out->depth[c] = depth > 32767 ? 32767 : depth;
         out->err[c] = depth - obs[best] > 32767 ? 32767 : depth - obs[best];
     }
@@ -853,7 +856,7 @@ static void family_call(orec *recs, int n, const orc_records *in, const orc_para
     }
     ssread ss[4];
     int has[4];
-    for (int s = 0; s < 4; s++) has[s] = ss_consensus(sets[s], ns[s], lr, f64, thr, &ss[s]);
+    for (int s = 0; s < 4; s++) has[s] = ss_consensus(sets[s], ns[s], lr, f64, thr, p->min_consensus_base_quality, &ss[s]);
     int32_t nreads = 0;
     for (int s = 0; s < 4; s++) nreads += ns[s];
     res->fam_nreads[f] = nreads;

@@ -67,6 +67,8 @@ typedef struct {
     int32_t family_order;        /* 1: families = runs of one MI base in fgbio TemplateCoordinate order of the
                                     tool-2 records (SortBam at main.snake.py:152); 0: tool-2 MI groups */
     int32_t keep_sources;        /* 1: keep every family's source reads per set (orc_get_sources) */
+    int32_t min_consensus_base_quality; /* single-strand calls below this phred -> (N, 2): 2 for the duplex
+                                           caller's single-strand caller, 0 for main.snake.py:54 */
 } orc_params;
 
 typedef struct orc_result orc_result;

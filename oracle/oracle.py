@@ -42,7 +42,7 @@ class _Params(C.Structure):
     _fields_ = [("error_rate_pre_umi", C.c_double), ("error_rate_post_umi", C.c_double),
                 ("min_input_base_quality", C.c_int32), ("consensus_call_overlapping_bases", C.c_int32),
                 ("run_tools", C.c_int32), ("n_threads", C.c_int32), ("family_order", C.c_int32),
-                ("keep_sources", C.c_int32)]
+                ("keep_sources", C.c_int32), ("min_consensus_base_quality", C.c_int32)]
 
 
 _lib = None
@@ -160,10 +160,11 @@ def lex_ranks(strings, ids) -> np.ndarray:
 
 
 def run(raw, ref, pre=45.0, post=30.0, overlap=True, run_tools=True, threads=0,
-        family_order="template-coordinate", keep_sources=False) -> OracleResult:
+        family_order="template-coordinate", keep_sources=False, min_consensus_base_quality=2) -> OracleResult:
     """raw: bsseqconsensusreads_amd.records.RawRecords; ref: records.Reference.
     family_order: "template-coordinate" (fgbio SortBam + consecutive-MI grouping) or "mi-group"
-    (tool 2's first-seen MI groups)."""
+    (tool 2's first-seen MI groups).  min_consensus_base_quality: single-strand calls below it
+    become (N, 2) -- 2 for step 5's duplex caller, 0 for step 1 (main.snake.py:54)."""
     lib = load()
     keep = []
 
@@ -230,7 +231,7 @@ def run(raw, ref, pre=45.0, post=30.0, overlap=True, run_tools=True, threads=0,
     if family_order not in ("template-coordinate", "mi-group"):
         raise ValueError(family_order)
     p = _Params(pre, post, 0, int(overlap), int(run_tools), int(threads), int(family_order == "template-coordinate"),
-                int(keep_sources))
+                int(keep_sources), int(min_consensus_base_quality))
     t0 = time.perf_counter()
     h = lib.orc_run(C.byref(rr), C.byref(rf), C.byref(p))
     seconds = time.perf_counter() - t0

@@ -15,7 +15,8 @@ sharing no table and no code with either (main.snake.py:163 
       pErr  = not(L[b*] - or(L))                                        (or = logsumexp)
       pErr' = probabilityOfErrorTwoTrials(ln e_pre, pErr)
       Q     = min(93, floor(-10 pErr' / ln 10 + 0.001))                (PhredScore.fromLogProbability)
-      Q < 2 -> (N, 2)
+  VanillaUmiConsensusCaller: depth 0 (fewer contributions than min-reads 1) or
+      Q < min-consensus-base-quality -> (N, 2): 2 inside the duplex caller, 0 for step 1
   LogProbability: or(a, b) = max + log1p(exp(min - max)); and(a, b) = a + b;
       aOrNotB(a, b) = a + log1p(-exp(b - a)); not(x) = log(-expm1(x)) near 0, log1p(-exp(x)) else;
       probabilityOfErrorTwoTrials(x, y) = aOrNotB(or(x, y), ln(4/3) + x + y)   (x + y - 4/3 x y)
@@ -92,7 +93,7 @@ def phred_from_ln(ln_p):
     return np.minimum(q, 93).astype(np.int64)
 
 
-def ss_vote(count, lens, base, qual, stride, pre=45.0, post=30.0):
+def ss_vote(count, lens, base, qual, stride, pre=45.0, post=30.0, min_cbq=2):
     """Single-strand consensus of every (family, set) from its source reads.
 
     count [F, 4] reads per set, lens / flat base (nt16) / qual per read in family / set order.
@@ -138,8 +139,9 @@ def ss_vote(count, lens, base, qual, stride, pre=45.0, post=30.0):
     for k in range(4):
         tied |= np.where((L[k] == m) & (depth > 0), 1 << k, 0)
     live = np.arange(stride)[None, :] < lc[:, None]
-    callb = np.where(Q < 2, N_CODE, 1 << best).reshape(nrow, stride)
-    callq = np.where(Q < 2, 2, Q).reshape(nrow, stride)
+    nocall = (Q < min_cbq) | (depth == 0)
+    callb = np.where(nocall, N_CODE, 1 << best).reshape(nrow, stride)
+    callq = np.where(nocall, 2, Q).reshape(nrow, stride)
     return {"len": out_len,
             "base": np.where(live, callb, 0).astype(np.uint8).reshape(F, 4, stride),
             "qual": np.where(live, callq, 0).astype(np.uint8).reshape(F, 4, stride),

@@ -75,10 +75,10 @@ def trim_tails(raw, frac=0.3, seed=1, min_len=30):
     return b.finish()
 
 
-def near_tie_votes(raw, n_pos=6, seed=3, qlo=80, qhi=93, p_n=0.1):
+def near_tie_votes(raw, n_pos=6, seed=3, qlo=80, qhi=93, p_n=0.1, n_alleles=2):
     """Adversarial vote columns (a copy of `raw`): per family, `n_pos` reference positions inside
-    its forward reads' span get, in every record covering them, a random A/C/G/T base (two alleles
-    per position) at a random quality in [qlo, qhi] (an N at Q2 with probability p_n).  High
+    its forward reads' span get, in every record covering them, a random A/C/G/T base (`n_alleles`
+    alleles per position) at a random quality in [qlo, qhi] (an N at Q2 with probability p_n).  High
     qualities make the per-read likelihoods nearly equal (lr[q] saturates at the post-UMI error
     rate), so columns where the bases disagree are near ties -- fgbio's fp64 sums separate them,
     2^-20 fixed point does not."""
@@ -93,7 +93,7 @@ def near_tie_votes(raw, n_pos=6, seed=3, qlo=80, qhi=93, p_n=0.1):
     start = np.full(n_fam, np.iinfo(np.int64).max)
     np.minimum.at(start, fam[fwd], pos[fwd])
     P = start[:, None] + rng.integers(20, 130, size=(n_fam, n_pos))
-    alle = rng.choice(np.array([1, 2, 4, 8], np.uint8), size=(n_fam, n_pos, 2))
+    alle = rng.choice(np.array([1, 2, 4, 8], np.uint8), size=(n_fam, n_pos, n_alleles))
     for k in range(raw.n):
         f = int(fam[k])
         j = P[f] - pos[k]
@@ -103,7 +103,7 @@ def near_tie_votes(raw, n_pos=6, seed=3, qlo=80, qhi=93, p_n=0.1):
             if rng.random() < p_n:
                 seq[o], qual[o] = 15, 2
             else:
-                seq[o] = alle[f, i, int(rng.integers(0, 2))]
+                seq[o] = alle[f, i, int(rng.integers(0, n_alleles))]
                 qual[o] = int(rng.integers(qlo, qhi + 1))
     return dataclasses.replace(raw, seq=seq, qual=qual)
 

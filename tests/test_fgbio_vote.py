@@ -24,7 +24,8 @@ def fp64_check(raw, ref, run_tools=True, **kw):
     r = oracle.run(raw, ref, keep_sources=True, run_tools=run_tools, **kw)
     src = r.sources
     stride = r.ss["base"].shape[2]
-    ss = fv.ss_vote(src["count"], src["len"], src["base"], src["qual"], stride)
+    ss = fv.ss_vote(src["count"], src["len"], src["base"], src["qual"], stride,
+                    min_cbq=kw.get("min_consensus_base_quality", 2))
     return r, ss, fv.compare_ss(r.ss, ss)
 
 
@@ -112,3 +113,57 @@ def test_fp64_worked_values():
     count = np.array([[2, 0, 0, 0]], np.int32)
     ss = fv.ss_vote(count, np.ones(2, np.int64), np.array([1, 2], np.uint8), np.array([30, 30], np.uint8), 16)
     assert ss["gap"][0, 0, 0] == 0 and ss["tied"][0, 0, 0] == 0b11
+
+
+def low_quality_votes(raw, seed=5):
+    """Columns of four disagreeing low-quality reads: per family 16 positions, each record covering
+    one shows a random A/C/G/T (four alleles) at Q0-Q3, or N -- single-strand calls of Q1 (three
+    reads A, C, G at one quality: P(error) 2/3) and depth-0 columns (only Ns) among them."""
+    return near_tie_votes(raw, n_pos=16, qlo=0, qhi=3, p_n=0.15, n_alleles=4, seed=seed)
+
+
+def test_min_consensus_base_quality_worked_values():
+    """--min-consensus-base-quality: three reads A, C, G at Q30 in one set give
+    P(error) ~ 2/3 -> Q1.  Inside the duplex caller (mask 2) that column is (N, 2); step 1
+    (main.snake.py:54, mask 0) keeps fgbio's pick at Q1.  A column whose reads are all N is a
+    no-call under either mask."""
+    count = np.array([[3, 0, 0, 0]], np.int32)
+    b, q = np.array([1, 2, 4], np.uint8), np.array([30, 30, 30], np.uint8)
+    ss2 = fv.ss_vote(count, np.ones(3, np.int64), b, q, 16, min_cbq=2)
+    ss0 = fv.ss_vote(count, np.ones(3, np.int64), b, q, 16, min_cbq=0)
+    assert (ss2["base"][0, 0, 0], ss2["qual"][0, 0, 0]) == (15, 2)
+    assert ss0["qual"][0, 0, 0] == 1 and ss0["base"][0, 0, 0] in (1, 2, 4)
+    nn = fv.ss_vote(np.array([[2, 0, 0, 0]], np.int32), np.ones(2, np.int64), np.array([15, 15], np.uint8),
+                    np.array([30, 30], np.uint8), 16, min_cbq=0)
+    assert (nn["base"][0, 0, 0], nn["qual"][0, 0, 0]) == (15, 2)
+
+
+@pytest.mark.parametrize("min_cbq", [2, 0])
+def test_low_quality_columns_vs_fgbio_fp64(min_cbq):
+    """The restatement's mask against fgbio fp64 on Q0-Q3 disagreement columns, both thresholds:
+    Q1 calls exist and keep their base at 0, and are (N, 2) at 2."""
+    s = synth.generate("C1", 1500, seed=11, device="cpu", genome_len=400_000)
+    raw = low_quality_votes(s.raw)
+    r, ss, c = fp64_check(raw, s.ref, run_tools=False, min_consensus_base_quality=min_cbq)
+    assert_fp64_bar(c, "low-quality mask %d" % min_cbq)
+    assert c["n_boundary"] == 0  # the same threshold on both sides: no N flips at all
+    live = np.arange(r.ss["qual"].shape[2])[None, None, :] < r.ss["len"][:, :, None]
+    q1 = live & (r.ss["qual"] == 1)
+    nq2 = live & (r.ss["base"] == 15) & (r.ss["qual"] == 2)
+    if min_cbq == 0:
+        assert q1.sum() > 100 and np.isin(r.ss["base"][q1], [1, 2, 4, 8]).all()
+    else:
+        assert q1.sum() == 0 and nq2.sum() > 100
+
+
+def test_molecular_low_quality_vs_fgbio_fp64():
+    """Step 1's caller (mask 0, MI runs, no BA side) on the same columns."""
+    from bsseqconsensusreads_amd import pipeline
+    from bsseqconsensusreads_amd import records as R
+    s = synth.generate("C1", 800, seed=12, device="cpu", genome_len=400_000)
+    raw = low_quality_votes(s.raw, seed=6)
+    rm = pipeline.molecular_records(R.take(raw, np.lexsort((raw.mi_strand, raw.mi_id))))
+    r, ss, c = fp64_check(rm, s.ref, run_tools=False, family_order="mi-group", min_consensus_base_quality=0)
+    assert_fp64_bar(c, "molecular low-quality")
+    live = np.arange(r.cons_qual.shape[2])[None, None, :] < r.cons_len[:, :, None]
+    assert (live & (r.cons_qual == 1)).sum() > 50

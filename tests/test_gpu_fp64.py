@@ -14,24 +14,30 @@ import fgbio_vote as fv
 from bsseqconsensusreads_amd import batch, pipeline, synth
 from helpers import near_tie_votes
 from oracle import oracle
-from test_fgbio_vote import CASES, assert_fp64_bar
+from test_fgbio_vote import CASES, assert_fp64_bar, low_quality_votes
 from test_gpu_parity import assert_consensus_equal, assert_ss_equal
 
 pytestmark = pytest.mark.gpu
 
 
-def _gpu_vs_fp64(engine, raw, ref, run_tools, what):
+def _gpu_vs_fp64(engine, raw, ref, run_tools, what, molecular=False):
     engine.load_reference(ref)
-    if run_tools:
-        cons, _ = pipeline.run_step5(engine, raw, tags=True)
+    min_cbq = 0 if molecular else 2  # main.snake.py:54 vs the duplex caller's single-strand caller
+    if molecular:
+        cons, raw = pipeline.run_molecular(engine, raw, tags=True)
+        r = oracle.run(raw, ref, keep_sources=True, run_tools=False, family_order="mi-group",
+                       min_consensus_base_quality=0)
     else:
-        cons = pipeline.run_duplex(engine, raw, tags=True)
-    r = oracle.run(raw, ref, keep_sources=True, run_tools=run_tools)
+        if run_tools:
+            cons, _ = pipeline.run_step5(engine, raw, tags=True)
+        else:
+            cons = pipeline.run_duplex(engine, raw, tags=True)
+        r = oracle.run(raw, ref, keep_sources=True, run_tools=run_tools)
     assert_consensus_equal(cons, r, what)      # GPU == fixed-point restatement, bit for bit
     assert_ss_equal(cons, r, what)
     src = r.sources
     stride = cons.ss["base"].shape[2]
-    ss = fv.ss_vote(src["count"], src["len"], src["base"], src["qual"], stride)
+    ss = fv.ss_vote(src["count"], src["len"], src["base"], src["qual"], stride, min_cbq=min_cbq)
     c = fv.compare_ss({"len": cons.ss["len"], "base": cons.ss["base"], "qual": cons.ss["qual"]}, ss)
     assert_fp64_bar(c, what)
     # duplex consensus vs fgbio fp64 duplex of the fp64 single-strand reads
@@ -54,6 +60,7 @@ def _gpu_vs_fp64(engine, raw, ref, run_tools, what):
     assert not (live & (dq > 0) & same[:, :, :w]).any(), what + ": duplex qual differs from fgbio fp64"
     if c["qual_pm1"] == 0 and c["n_boundary"] == 0:
         assert int(db.sum()) == 0 and int((live & (dq > 0)).sum()) == 0
+    return cons
 
 
 @pytest.mark.parametrize("cfg,n,qlo", CASES)
@@ -72,3 +79,32 @@ def test_gpu_large_kernel_near_ties_vs_fgbio_fp64(engine, qlo, monkeypatch):
     monkeypatch.setattr(pipeline, "materialize",
                         lambda plan, f0, f1, small_cap=0, images=None: real(plan, f0, f1, small_cap=0, images=images))
     _gpu_vs_fp64(engine, raw, s.ref, False, "k_large q>=%d" % qlo)
+
+
+def _force_large(monkeypatch):
+    real = batch.materialize
+    monkeypatch.setattr(pipeline, "materialize",
+                        lambda plan, f0, f1, small_cap=0, images=None: real(plan, f0, f1, small_cap=0, images=images))
+
+
+@pytest.mark.parametrize("kernel", ["small", "large"])
+@pytest.mark.parametrize("caller", ["duplex", "molecular"])
+def test_gpu_min_consensus_base_quality(engine, kernel, caller, monkeypatch):
+    """Q0-Q3 disagreement columns (Q1 calls, all-N columns) in both kernels and both callers:
+    step 5's duplex caller masks single-strand Q < 2 to (N, 2), step 1 (main.snake.py:54,
+    --min-consensus-base-quality=0) keeps the call at Q1; GPU == oracle/ bit for bit, and both
+    within the fp64 bar of fgbio's arithmetic.  The engine's own flags are restored afterwards."""
+    from bsseqconsensusreads_amd import records as R
+    s = synth.generate("C1", 600, seed=17, device="cpu", genome_len=200_000)
+    raw = low_quality_votes(s.raw, seed=9)
+    if caller == "molecular":
+        raw = R.take(raw, np.lexsort((raw.mi_strand, raw.mi_id)))
+    if kernel == "large":
+        _force_large(monkeypatch)
+    cons = _gpu_vs_fp64(engine, raw, s.ref, False, "low-quality %s %s" % (caller, kernel),
+                        molecular=caller == "molecular")
+    w = cons.ss["qual"].shape[2]
+    live = np.arange(w)[None, None, :] < cons.ss["len"][:, :, None]
+    q1 = int((live & (cons.ss["qual"] == 1)).sum())
+    assert (q1 > 50) if caller == "molecular" else (q1 == 0)
+    assert engine.params.min_consensus_base_quality == 2

@@ -143,3 +143,33 @@ def test_c5_stream_beyond_one_batch(engine):
     ref = oracle.run(s.raw, s.ref, threads=THREADS)
     live = _compare_all(cons, ref, "C5 stream %d batches" % len(ranges))
     _invariants(cons, live, int(s.raw.l_seq.max()) + 1)
+
+
+@pytest.mark.timeout(900)
+def test_c5_full_share(engine, capsys):
+    """C5 (configs[4]) at its full per-GPU share for N = 8: 12.5M C2-shaped families, generated as
+    bench.py --config C5 builds rank 0's share (batches of 1.5M families, seed 42 + batch index, one
+    genome), each batch through pipeline.run_step5 and compared, every family, with oracle/ on that
+    batch's records.  Progress goes to the terminal per batch (the suite's runner watches for
+    silence)."""
+    total, per, first, done, emitted = 12_500_000, 1_500_000, None, 0, 0
+    i = 0
+    while done < total:
+        n = min(per, total - done)
+        s = synth.generate("C2", n, seed=42 + i, device="cuda", reuse=first)
+        if first is None:
+            engine.load_reference(s.ref)
+            first = s
+        cons, _ = pipeline.run_step5(engine, s.raw)
+        ref = oracle.run(s.raw, s.ref, threads=THREADS)
+        live = _compare_all(cons, ref, "C5 share batch %d" % i)
+        _invariants(cons, live, int(s.raw.l_seq.max()) + 1)
+        done += n
+        emitted += int(ref.status.sum())
+        with capsys.disabled():
+            print("\nC5 share: batch %d, %d / %d families bit-exact" % (i, done, total), flush=True)
+        del cons, ref, live
+        if s is not first:
+            del s
+        i += 1
+    assert done == total and emitted > 0.8 * total
