@@ -30,7 +30,7 @@ from . import records as R
 
 IO_LIB_PATH = os.environ.get("BSDC_IO_LIB_PATH") or os.path.join(os.path.dirname(os.path.abspath(__file__)),
                                                                  "libbsdc_io.so")
-BSDC_IO_ABI_VERSION = 7
+BSDC_IO_ABI_VERSION = 8
 _P = C.c_void_p
 
 
@@ -77,6 +77,8 @@ def _load():
     lib.bsdc_bam_stream_next.restype = C.c_int32
     lib.bsdc_bam_stream_next_raw.argtypes = [_P, C.c_int64, C.c_int64, C.POINTER(_P)]
     lib.bsdc_bam_stream_next_raw.restype = C.c_int32
+    lib.bsdc_bam_stream_next_runs.argtypes = [_P, C.c_int64, C.POINTER(_P)]
+    lib.bsdc_bam_stream_next_runs.restype = C.c_int32
     lib.bsdc_bam_parse.argtypes = [_P, C.c_int32]
     lib.bsdc_bam_parse.restype = C.c_int32
     lib.bsdc_bam_stream_close.argtypes = [_P]
@@ -345,10 +347,12 @@ class StreamChunk:
 
 
 def stream_chunks(path: str, threads: int = 0, chunk_bytes: int = DEFAULT_CHUNK_BYTES, slack: int = DEFAULT_SLACK,
-                  read_size: int = 8 << 20):
+                  read_size: int = 8 << 20, runs: bool = False):
     """The chunks of a coordinate-sorted BAM in bounded memory, undecoded (StreamChunk): cut where no
     template or MI family straddles two chunks (include/bsdc_io.h, bsdc_bam_stream_next_raw).  The
-    stream itself is freed once it is exhausted and every chunk has been decoded or discarded."""
+    stream itself is freed once it is exhausted and every chunk has been decoded or discarded.
+    runs: a GroupReadsByUmi-ordered BAM (step 1's input) cut between runs of one MI value instead
+    (bsdc_bam_stream_next_runs; any record order, no `slack`)."""
     lib = _load()
     st = _P()
     rc = lib.bsdc_bam_stream_open(path.encode(), int(threads), int(read_size), C.byref(st))
@@ -357,7 +361,10 @@ def stream_chunks(path: str, threads: int = 0, chunk_bytes: int = DEFAULT_CHUNK_
     try:
         while True:
             h = _P()
-            rc = lib.bsdc_bam_stream_next_raw(st, int(chunk_bytes), int(slack), C.byref(h))
+            if runs:
+                rc = lib.bsdc_bam_stream_next_runs(st, int(chunk_bytes), C.byref(h))
+            else:
+                rc = lib.bsdc_bam_stream_next_raw(st, int(chunk_bytes), int(slack), C.byref(h))
             if rc != 0:
                 raise OSError("%s: %s" % (path, lib.bsdc_io_last_error().decode()))
             if not h:
@@ -1087,7 +1094,31 @@ def step5_stream(in_bam: str, fasta: str, out_bam: Optional[str], engine=None, p
                  threads: int = 0, level: int = 6, fastq: Optional[Tuple[str, str]] = None, tags: bool = True,
                  chunk_bytes: int = DEFAULT_CHUNK_BYTES, slack: int = DEFAULT_SLACK,
                  batch_bases: Optional[int] = None, stats: Optional[dict] = None, gpu_bgzf: bool = False) -> dict:
-    """step5 in bounded memory, pipelined: a decoder thread cuts the next chunk of the
+    """step5 in bounded memory, pipelined (_stream_step)."""
+    return _stream_step(in_bam, fasta, out_bam, engine, prefix, threads, level, fastq, tags, chunk_bytes, slack,
+                        batch_bases, stats, gpu_bgzf, None)
+
+
+def molecular_stream(in_bam: str, out_bam: Optional[str], engine=None, prefix: Optional[str] = None, threads: int = 0,
+                     level: int = 6, fastq: Optional[Tuple[str, str]] = None, tags: bool = True,
+                     chunk_bytes: int = DEFAULT_CHUNK_BYTES, batch_bases: Optional[int] = None,
+                     stats: Optional[dict] = None, gpu_bgzf: bool = False, min_consensus_base_quality: int = 0) -> dict:
+    """Rule call_consensus_reads_molecular (main.snake.py:46-55) in bounded memory: the same
+    pipeline as step5_stream over a GroupReadsByUmi-ordered input cut between MI runs
+    (stream_chunks(runs=True)); each chunk's runs are its consensus families (pipeline.molecular_records,
+    the vote alone, --min-consensus-base-quality applied).  The output is byte-identical to
+    molecular()'s whole-file path: no run straddles two chunks.  The reference's rule needs -Xmx100g
+    (main.snake.py:54, README.md:83); this holds about six chunks."""
+    return _stream_step(in_bam, None, out_bam, engine, prefix, threads, level, fastq, tags, chunk_bytes, DEFAULT_SLACK,
+                        batch_bases, stats, gpu_bgzf, int(min_consensus_base_quality))
+
+
+def _stream_step(in_bam: str, fasta: Optional[str], out_bam: Optional[str], engine, prefix: Optional[str],
+                 threads: int, level: int, fastq: Optional[Tuple[str, str]], tags: bool, chunk_bytes: int, slack: int,
+                 batch_bases: Optional[int], stats: Optional[dict], gpu_bgzf: bool,
+                 molecular: Optional[int]) -> dict:
+    """step5 (molecular None) or step 1 (molecular = its --min-consensus-base-quality) in bounded
+    memory, pipelined: a decoder thread cuts the next chunk of the
     coordinate-sorted input (stream_bam: inflate, split where no template or MI family straddles),
     a reader thread parses the chunk before, a planner thread forms the families of the one before
     that (C++ plan) and materializes its batches into pinned memory; this thread uploads a chunk's
@@ -1124,7 +1155,7 @@ def step5_stream(in_bam: str, fasta: str, out_bam: Optional[str], engine=None, p
         # reader thread parses the one before
         it = None
         try:
-            it = stream_chunks(in_bam, threads, chunk_bytes, slack)
+            it = stream_chunks(in_bam, threads, chunk_bytes, slack, runs=molecular is not None)
             while not stop.is_set():
                 t0 = time.perf_counter()
                 nxt = next(it, None)
@@ -1178,7 +1209,13 @@ def step5_stream(in_bam: str, fasta: str, out_bam: Optional[str], engine=None, p
                 if stop.is_set():
                     continue  # drain to the reader's None without planning
                 t0 = time.perf_counter()
-                plan = pipeline.plan_families(raw, "full", first["ref"])
+                buf = raw._pool_buf
+                if molecular is None:
+                    plan = pipeline.plan_families(raw, "full", first["ref"])
+                else:  # step 1: the chunk's MI runs are the families, the vote alone
+                    raw = pipeline.molecular_records(raw)
+                    plan = pipeline.plan_families(raw, "vote", family_order="mi-group")
+                raw._pool_buf = buf
                 t1 = time.perf_counter()
                 fbs = None
                 if not plan.split_ext:
@@ -1209,7 +1246,7 @@ def step5_stream(in_bam: str, fasta: str, out_bam: Optional[str], engine=None, p
                     break
                 cons, raw = item
                 t0 = time.perf_counter()
-                recs = duplex_records(cons, raw, first["prefix"], threads, pool=bufs)
+                recs = duplex_records(cons, raw, first["prefix"], threads, molecular=molecular is not None, pool=bufs)
                 T["records"] += time.perf_counter() - t0
                 back = [raw._pool_buf, getattr(recs.aux2, "_pool_buf", None)]
                 del item, cons, raw
@@ -1258,11 +1295,20 @@ def step5_stream(in_bam: str, fasta: str, out_bam: Optional[str], engine=None, p
     # the header and the reference come first: the plan of a chunk needs the reference
     hdr0 = read_bam_header(in_bam)
     first["header"] = hdr0
-    ref = read_fasta(fasta, hdr0)
+    ref = read_fasta(fasta, hdr0) if molecular is None else None  # (step 1 converts nothing)
     first["ref"] = ref
     first["prefix"] = read_name_prefix(hdr0) if prefix is None else prefix
+    import contextlib
+    flags = contextlib.nullcontext() if molecular is None else eng.flags(min_consensus_base_quality=molecular)
     try:
-        eng.load_reference(ref)
+        flags.__enter__()
+    except BaseException:
+        if own:
+            eng.close()
+        raise
+    try:
+        if ref is not None:
+            eng.load_reference(ref)
         td = threading.Thread(target=decoder, daemon=True)
         tr = threading.Thread(target=reader, daemon=True)
         tp = threading.Thread(target=planner, daemon=True)
@@ -1273,7 +1319,7 @@ def step5_stream(in_bam: str, fasta: str, out_bam: Optional[str], engine=None, p
         tp.start()
         tb.start()
         tw.start()
-        mode = pipeline.MODE_CONVERT | pipeline.MODE_EXTEND | pipeline.MODE_VOTE
+        mode = pipeline.MODE_CONVERT | pipeline.MODE_EXTEND | pipeline.MODE_VOTE if molecular is None else pipeline.MODE_VOTE
         drained = False
         try:
             while True:
@@ -1314,6 +1360,7 @@ def step5_stream(in_bam: str, fasta: str, out_bam: Optional[str], engine=None, p
             tr.join()
             td.join()
     finally:
+        flags.__exit__(None, None, None)
         if own:
             eng.close()
     if err:

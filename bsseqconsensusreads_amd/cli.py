@@ -44,20 +44,23 @@ def parse(argv):
         p.add_argument("--threads", type=int, default=8)
         p.add_argument("--compression", type=int, default=6)
         p.add_argument("--device", type=int, default=0)
+        p.add_argument("--gpu-bgzf", default="false", choices=("true", "false"),
+                       help="deflate the output BAM's and FASTQ pair's blocks on the GPU (streaming; files ~4%% larger)")
+        p.add_argument("--batch-bases", type=int, default=None, help="device batch budget in bases")
+        p.add_argument("--chunk-mb", type=int, default=64, help="--stream: record MiB per chunk")
         if name == "step5":
             p.add_argument("--gpus", type=int, default=1, help="one process per GPU, family batches dealt to them")
-            p.add_argument("--gpu-bgzf", default="false", choices=("true", "false"),
-                           help="deflate the output BAM's and FASTQ pair's blocks on the GPU (streaming, one GPU; files ~4%% larger)")
             p.add_argument("--devices", default=None, help="comma-separated device id per rank (default 0..gpus-1)")
-            p.add_argument("--batch-bases", type=int, default=None, help="device batch budget in bases")
             p.add_argument("--stream", default="auto", choices=["auto", "true", "false"],
-                           help="bounded-memory pipelined step (bam.step5_stream; coordinate-sorted input, one GPU); "
+                           help="bounded-memory pipelined step (bam.step5_stream; coordinate-sorted input); "
                                 "false = read the whole BAM first (bam.step5); auto = stream when the header "
                                 "says SO:coordinate")
-            p.add_argument("--chunk-mb", type=int, default=64, help="--stream: record MiB per chunk")
         else:
             p.add_argument("--min-consensus-base-quality", type=int, default=0,
                            help="mask single-strand calls below this phred to N (main.snake.py:54 passes 0)")
+            p.add_argument("--stream", default="true", choices=["true", "false"],
+                           help="bounded-memory pipelined step cut between MI runs (bam.molecular_stream; the "
+                                "GroupReadsByUmi order of the input); false = read the whole BAM first")
         p.add_argument("--output-per-base-tags", default="true", choices=["true", "false"],
                        help="fgbio's consensus tags (per-read and per-base statistics); off = name/SEQ/QUAL/RG/MI/RX")
     a = ap.parse_args(argv)
@@ -65,6 +68,9 @@ def parse(argv):
         ap.error("--fastq1 and --fastq2 go together")
     if a.output == "-" and a.fastq1 is None:
         ap.error("nothing to write: give OUT.bam or --fastq1/--fastq2")
+    if a.gpu_bgzf == "true" and a.stream == "false":
+        print("warning: --gpu-bgzf applies to the streaming step only; --stream false deflates on the host",
+              file=sys.stderr)
     return a
 
 
@@ -133,6 +139,11 @@ def main(argv=None) -> int:
             elif a.cmd == "step5":
                 info = bam.step5(a.input, a.reference, out, eng, a.read_name_prefix, a.threads, a.compression, fq,
                                  tags=a.output_per_base_tags == "true", batch_bases=a.batch_bases, dist=dist)
+            elif a.stream == "true":
+                info = bam.molecular_stream(a.input, out, eng, a.read_name_prefix, a.threads, a.compression, fq,
+                                            tags=a.output_per_base_tags == "true", chunk_bytes=a.chunk_mb << 20,
+                                            batch_bases=a.batch_bases, gpu_bgzf=a.gpu_bgzf == "true",
+                                            min_consensus_base_quality=a.min_consensus_base_quality)
             else:
                 info = bam.molecular(a.input, out, eng, a.read_name_prefix, a.threads, a.compression, fq,
                                      tags=a.output_per_base_tags == "true",

@@ -642,6 +642,8 @@ struct bsdc_bam_stream {
     std::vector<Bytes> pool;  // returned chunk buffers (at most 2 kept)
     int64_t outstanding = 0;
     bool closed = false;
+    // MI-run chunks (bsdc_bam_stream_next_runs): the MI value of the last record scanned
+    std::string run_mi;
 };
 
 int32_t bsdc_bam_stream_open(const char *path, int32_t n_threads, int64_t read_size, bsdc_bam_stream **out) {
@@ -1150,6 +1152,94 @@ int32_t bsdc_bam_stream_next_raw(bsdc_bam_stream *s, int64_t min_bytes, int64_t 
             return 0;
         }
         rc = bsdc_bam_stream_fill(s);
+        if (rc != 0) return rc;
+        s->prof[0] += now_s() - t0;
+    }
+}
+
+// The next chunk of a GroupReadsByUmi-ordered stream (include/bsdc_io.h): a prefix of the
+// buffered records cut at the first record, at or past min_bytes, whose MI value differs from the
+// one before it, so no run of one MI tag (fgbio CallMolecularConsensusReads' unit) straddles two
+// chunks.  No family bookkeeping and no coordinate order: the records are listed by the parse.
+// s->tail = the bytes of whole records scanned (all of them in one run with s->run_mi, when the
+// scan did not find a cut).
+int32_t bsdc_bam_stream_next_runs(bsdc_bam_stream *s, int64_t min_bytes, bsdc_bam **out) {
+    *out = nullptr;
+    if (!s->recs.empty()) return fail(BSDC_IO_EINVAL, "stream already cut by families (bsdc_bam_stream_next_raw)");
+    const size_t want = (size_t)std::max<int64_t>(min_bytes, 0) * 5 / 4 + (size_t)s->read_size * 16;
+    if (s->buf.capacity() < want) s->buf.reserve(want);
+    if (s->spare.capacity() < want) {
+        std::lock_guard<std::mutex> lk(s->mu);
+        for (auto &v : s->pool)
+            if (v.capacity() >= want) {
+                s->spare.swap(v);
+                break;
+            }
+    }
+    if (s->spare.capacity() < want) s->spare.reserve(want);
+    for (;;) {
+        double t0 = now_s();
+        const uint8_t *d = s->buf.data();
+        const int64_t dn = (int64_t)s->buf.size();
+        int64_t p = s->tail, cut = -1;
+        while (p + 4 <= dn) {
+            const int64_t bs = rd32(d + p);
+            if (bs < 32) return fail(BSDC_IO_EFORMAT, "truncated BAM record");
+            if (p + 4 + bs > dn) break;
+            const uint8_t *r = d + p, *end = r + 4 + bs;
+            const int64_t body = 36 + (int64_t)r[12] + 4 * (int64_t)rd16(r + 16) + ((int64_t)rdi32(r + 20) + 1) / 2 +
+                                 (int64_t)rdi32(r + 20);
+            if (rdi32(r + 20) < 0 || r[12] < 1 || body > 4 + bs) return fail(BSDC_IO_EFORMAT, "malformed BAM record (lengths or aux)");
+            std::string_view mi;
+            for (const uint8_t *a = r + body; a + 3 <= end;) {
+                const int64_t vs = aux_value_size(a, end);
+                if (vs < 0 || vs > (end - a) - 3) return fail(BSDC_IO_EFORMAT, "malformed BAM record (lengths or aux)");
+                if (a[0] == 'M' && a[1] == 'I' && a[2] == 'Z') mi = std::string_view((const char *)a + 3, (size_t)vs - 1);
+                a += 3 + vs;
+            }
+            if (p > 0 && p >= min_bytes && mi != s->run_mi) {
+                cut = p;
+                break;
+            }
+            s->run_mi.assign(mi.data(), mi.size());
+            p += 4 + bs;
+        }
+        s->prof[1] += now_s() - t0;
+        const bool end = s->eof && s->comp.empty();
+        if (cut < 0) {
+            s->tail = p;
+            if (end) {
+                if (p < dn) return fail(BSDC_IO_EFORMAT, "truncated BAM record");
+                if (p == 0) return 0;  // the end of the stream
+                cut = p;
+            }
+        }
+        if (cut >= 0) {  // records [0, cut) go out in the buffer; the rest moves to `spare`
+            t0 = now_s();
+            auto *b = new bsdc_bam();
+            b->header = s->hdr.header;
+            b->ref_names = s->hdr.ref_names;
+            b->ref_len = s->hdr.ref_len;
+            const int64_t kept = dn - cut;
+            s->spare.resize((size_t)kept);
+            if (kept > 0) memcpy(s->spare.data(), d + cut, (size_t)kept);
+            b->data.swap(s->buf);
+            b->data.resize((size_t)cut + 8);
+            memset(b->data.data() + cut, 0, 8);
+            s->buf.swap(s->spare);
+            s->tail = 0;  // rescan the kept bytes (the first one opens a new run)
+            b->dn = cut;
+            b->parsed = false;
+            s->prof[3] += now_s() - t0;
+            {
+                std::lock_guard<std::mutex> lk(s->mu);
+                s->outstanding++;
+            }
+            *out = b;
+            return 0;
+        }
+        t0 = now_s();
+        const int32_t rc = bsdc_bam_stream_fill(s);
         if (rc != 0) return rc;
         s->prof[0] += now_s() - t0;
     }

@@ -17,9 +17,10 @@
 extern "C" {
 #endif
 
-#define BSDC_IO_ABI_VERSION 7
+#define BSDC_IO_ABI_VERSION 8
 #define BSDC_IO_EFORMAT (-10) /* not BGZF/BAM, truncated, bad CRC */
 #define BSDC_IO_EIO (-11)     /* open/read/write failed */
+#define BSDC_IO_EINVAL (-22)  /* bad argument */
 
 typedef struct bsdc_bam bsdc_bam; /* a decoded BAM held in host memory */
 
@@ -100,6 +101,14 @@ void bsdc_bam_stream_recycle(bsdc_bam_stream *s, bsdc_bam *b);
  * the next chunk while another decodes this one (bam.step5_stream). */
 int32_t bsdc_bam_stream_next_raw(bsdc_bam_stream *s, int64_t min_bytes, int64_t slack, bsdc_bam **out);
 int32_t bsdc_bam_parse(bsdc_bam *b, int32_t n_threads);
+/* Step 1's chunks (rule call_consensus_reads_molecular, main.snake.py:46-55): the input is in
+ * GroupReadsByUmi order, where fgbio CallMolecularConsensusReads' unit -- a run of consecutive
+ * records with one MI value -- is contiguous.  The next chunk unparsed: the buffered records up to
+ * the first record at or past min_bytes whose MI value differs from its predecessor's (the rest of
+ * the file at its end), so no run straddles two chunks and the chunks' runs concatenate to the
+ * whole file's.  No coordinate order is needed.  A stream is cut either this way or by
+ * bsdc_bam_stream_next_raw, not both.  *out = NULL at the end. */
+int32_t bsdc_bam_stream_next_runs(bsdc_bam_stream *s, int64_t min_bytes, bsdc_bam **out);
 
 /* Records to write (n_rec entries; every *_off array has n_rec + 1 entries). */
 typedef struct {
