@@ -183,30 +183,11 @@ __device__ __forceinline__ int phred_of(float S, const float *thr) {
 
 // Per-column statistics of a single-strand consensus read (BSDC_MODE_TAGS), as fgbio
 // VanillaUmiConsensusCaller keeps them for the consensus tags: the call itself (N / 2 below the
-// caller's --min-consensus-base-quality, KParams::qmin, or without an A/C/G/T read),
-// depth = reads with an A/C/G/T at the column, errors = depth - reads showing the RAW best base
-// (before the Q2 mask; a column without reads has depth 0 and errors 0).  Both counts saturate at
-// 32767 (fgbio stores Shorts).  D: likelihood sums (2^-20 nats), n: reads per base.
-struct SsAcc {
-    long long D[4];
-    uint32_t n[4];
-    __device__ __forceinline__ void clear() {
-#pragma unroll
-        for (int x = 0; x < 4; x++) {
-            D[x] = 0;
-            n[x] = 0;
-        }
-    }
-    // one read's base (plain nt16 code, sequencing orientation) and its lr value
-    __device__ __forceinline__ void add(uint32_t code, int32_t v) {
-#pragma unroll
-        for (int x = 0; x < 4; x++) {
-            const bool hit = code == (1u << x);
-            D[x] += hit ? v : 0;
-            n[x] += hit ? 1u : 0u;
-        }
-    }
-};
+// caller's --min-consensus-base-quality, KParams::qmin, or without an A/C/G/T read), depth = reads
+// with an A/C/G/T at the column, errors = depth - reads showing the RAW best base (before the
+// mask).  Both counts saturate at 32767 (fgbio stores Shorts).  They are fused into the vote: an
+// agreeing column's depth is its read count and its errors 0; a disagreeing one's come from the
+// per-base counts of the general call (k_small's queue, k_large's pass B).
 template <typename T>
 __device__ __forceinline__ int first_max4(T d0, T d1, T d2, T d3) {
     int best = 0;
@@ -294,26 +275,6 @@ struct LargeDesc {  // k_large: uint2 {address, length | reverse << 31}
         rv = (x.y >> 31) != 0;
     }
 };
-// the call of one single-strand column with its statistics; pick() gives fgbio's base on a near tie
-template <class Pick>
-__device__ __forceinline__ void ss_store(const SsAcc &a, const float *thr, int nset, int qmin, Pick pick, uint8_t *b,
-                                         uint8_t *q, uint16_t *dp, uint16_t *er) {
-    int best = first_max4(a.D[0], a.D[1], a.D[2], a.D[3]);
-    if (near_tie(a.D[0], a.D[1], a.D[2], a.D[3], best, nset)) best = pick();
-    const long long Db = a.D[best];
-    float S = 0.0f;
-#pragma unroll
-    for (int x = 0; x < 4; x++)
-        if (x != best) S += term(a.D[x] - Db);
-    const int Q = phred_of(S, thr);
-    const uint32_t depth = a.n[0] + a.n[1] + a.n[2] + a.n[3];
-    const bool nocall = depth == 0 || Q < qmin;  // (NoCall, NoCallQual): no A/C/G/T read, or below the mask
-    *b = nocall ? (uint8_t)kN : (uint8_t)(1u << best);
-    *q = nocall ? (uint8_t)2 : (uint8_t)Q;
-    *dp = (uint16_t)::min(depth, 32767u);
-    *er = (uint16_t)::min(depth - a.n[best], 32767u);
-}
-
 // tool 1 per-base rule (tools/1.convert_AG_to_CT.py:123-150), in its local form: the value at i
 // depends on m[i], m[i+1], ref[i], ref[i+1] only (the skip at :140 writes what the A rule would)
 __device__ __forceinline__ uint32_t convert_rule(uint32_t m0, uint32_t m1, bool has_next, uint32_t f0, uint32_t f1) {
@@ -1387,11 +1348,16 @@ __global__ __launch_bounds__(kWave *kSmallMaxWaves, kSmallMinWaves) __attribute_
         for (int e = 0; e < 2; e++) {
             const int ol = olen[e];
             const int sa = e == 0 ? 0 : 1, sb = e == 0 ? 3 : 2;
-            for (int c0 = 0; c0 < ol; c0 += 256) {
+            // TAGS: the single-strand reads run to their own lengths, which can pass the duplex's
+            // (min of the two); columns past a side's own length are not that side's
+            const int la = hs[sa] ? lcs[sa] : 0, lb = hs[sb] ? lcs[sb] : 0;
+            const int lv = TAGS ? ::max(la, lb) : ol;
+            for (int c0 = 0; c0 < lv; c0 += 256) {
                 const int c = c0 + 4 * t, c8 = 8 * c;
                 int32_t D[2][4] = {{0, 0, 0, 0}, {0, 0, 0, 0}};
                 uint32_t mf[2] = {0, 0}, mr[2] = {0, 0};  // one-hot ORs of forward / reverse reads
-                if (c < ol) {
+                uint32_t nf[2] = {0, 0}, nr[2] = {0, 0};  // TAGS: reads with an A/C/G/T, per column byte
+                if (c < lv) {
 #pragma unroll
                     for (int side = 0; side < 2; side++) {
                         const int s = side == 0 ? (e == 0 ? 0 : 1) : (e == 0 ? 3 : 2);
@@ -1404,14 +1370,18 @@ __global__ __launch_bounds__(kWave *kSmallMaxWaves, kSmallMinWaves) __attribute_
                             const int32_t a = (int32_t)(d & 0xFFFFu) + c;
                             const uint32_t b = lds_any32(bimg, a) & ~x, q = lds_any32(qimg, a);
                             mf[side] |= b;
-                            lookup4(lr2, b, q, D[side][0], D[side][1], D[side][2], D[side][3]);
+                            const uint32_t v = (b >> 4) & 0x01010101u;
+                            lookup4v(lr2, v, q, D[side][0], D[side][1], D[side][2], D[side][3]);
+                            if (TAGS) nf[side] += v;
                         };
                         auto rev = [&](uint32_t d) {  // bytes run backwards: byte 3 - j is column c + j
                             const uint32_t x = bytes_past(8 * (int)((d >> 16) & 0x7FFF) - c8, true);
                             const int32_t a = (int32_t)(d & 0xFFFFu) - c - 3;
                             const uint32_t b = lds_any32(bimg, a) & ~x, q = lds_any32(qimg, a);
                             mr[side] |= b;
-                            lookup4(lr2, b, q, D[side][3], D[side][2], D[side][1], D[side][0]);
+                            const uint32_t v = (b >> 4) & 0x01010101u;
+                            lookup4v(lr2, v, q, D[side][3], D[side][2], D[side][1], D[side][0]);
+                            if (TAGS) nr[side] += v;
                         };
                         // reads two at a time (both reads' loads in flight together), then an odd one
                         const int nf = nfw[s], na = cnt[s];
@@ -1455,11 +1425,15 @@ __global__ __launch_bounds__(kWave *kSmallMaxWaves, kSmallMinWaves) __attribute_
                 }
                 uint32_t ob4, oq4, ss[4];
                 resolve4(hs[sa], hs[sb], bm[0], Qp[0], bm[1], Qp[1], qadd, ob4, oq4, ss);
+                // (TAGS) the bytes of columns inside each side's own length; without TAGS every
+                // column below ol is inside both present sides
+                const uint32_t inA = TAGS ? ~bytes_past(8 * (la - c), false) : ~0u;
+                const uint32_t inB = TAGS ? ~bytes_past(8 * (lb - c), false) : ~0u;
                 // slow columns: a side saw more than one base, or a negative sum.  The queued
                 // path recomputes only the slow side(s): the other side's single-strand result
                 // rides in the column's output bytes (base | 0x10 if it is side B; qual 0 = none).
-                const uint32_t slowA = hs[sa] ? bytes_nonzero(multi[0] & 0x7F7F7F7Fu) | negm[0] : 0u;
-                const uint32_t slowB = hs[sb] ? bytes_nonzero(multi[1] & 0x7F7F7F7Fu) | negm[1] : 0u;
+                const uint32_t slowA = hs[sa] ? (bytes_nonzero(multi[0] & 0x7F7F7F7Fu) | negm[0]) & inA : 0u;
+                const uint32_t slowB = hs[sb] ? (bytes_nonzero(multi[1] & 0x7F7F7F7Fu) | negm[1]) & inB : 0u;
                 const uint32_t slow4 = slowA | slowB;
                 if (slow4) {
                     const uint32_t useA = hs[sa] ? ~slowA : 0u, useB = (hs[sb] ? ~slowB : 0u) & ~useA;
@@ -1470,14 +1444,46 @@ __global__ __launch_bounds__(kWave *kSmallMaxWaves, kSmallMinWaves) __attribute_
                 }
 #pragma unroll
                 for (int j = 0; j < 4; j++) {
-                    const bool qd = ((slow4 >> (8 * j)) & 0xFFu) != 0 && c + j < ol;
+                    const bool qd = ((slow4 >> (8 * j)) & 0xFFu) != 0 && c + j < lv;
                     const uint64_t ms = ballot(qd);
                     if (qd) sq[nq + mbcnt(ms)] = (uint16_t)((e << 15) | (c + j));
                     nq += __builtin_popcountll(ms);
                 }
-                if (c < ol) {
+                if (c < lv) {
                     st32(outb + e * ow + c, ob4);
                     st32(outq + e * ow + c, oq4);
+                }
+                // TAGS: the single-strand reads and their column statistics, fused into the vote
+                // (fgbio's per-read / per-base consensus tags).  A column whose side agrees (not
+                // slow) is that side's one base at its Q (or N / 2 below the mask), depth = its
+                // A/C/G/T reads, errors 0; a slow column's bytes are the queue's.
+                if (TAGS && c < lv) {
+#pragma unroll
+                    for (int side = 0; side < 2; side++) {
+                        const int s = side == 0 ? sa : sb;
+                        if (!hs[s]) continue;
+                        const uint32_t wr = (side == 0 ? inA & ~slowA : inB & ~slowB);
+                        const uint32_t bb = ss[2 * side], qq = ss[2 * side + 1];
+                        const uint32_t n4 = nf[side] + __builtin_bswap32(nr[side]);
+                        const uint32_t d01 = __builtin_amdgcn_perm(0u, n4, 0x0c010c00u);  // u16 of bytes 0, 1
+                        const uint32_t d23 = __builtin_amdgcn_perm(0u, n4, 0x0c030c02u);  // u16 of bytes 2, 3
+                        const int64_t at = (4 * (int64_t)fam + s) * stride + c;
+                        if (wr == 0xFFFFFFFFu) {
+                            *reinterpret_cast<uint32_t *>(P.O.ss_base + at) = bb;
+                            *reinterpret_cast<uint32_t *>(P.O.ss_qual + at) = qq;
+                            *reinterpret_cast<uint2 *>(P.O.ss_depth + at) = make_uint2(d01, d23);
+                            *reinterpret_cast<uint2 *>(P.O.ss_err + at) = make_uint2(0u, 0u);
+                        } else if (wr != 0u) {
+#pragma unroll
+                            for (int j = 0; j < 4; j++) {
+                                if (!((wr >> (8 * j)) & 0xFFu)) continue;
+                                P.O.ss_base[at + j] = (uint8_t)(bb >> (8 * j));
+                                P.O.ss_qual[at + j] = (uint8_t)(qq >> (8 * j));
+                                P.O.ss_depth[at + j] = (uint16_t)((n4 >> (8 * j)) & 0xFFu);
+                                P.O.ss_err[at + j] = 0;
+                            }
+                        }
+                    }
                 }
             }
         }
@@ -1505,6 +1511,7 @@ __global__ __launch_bounds__(kWave *kSmallMaxWaves, kSmallMinWaves) __attribute_
                 vq = kq;
             } else if (have) {
                 int32_t D0 = 0, D1 = 0, D2 = 0, D3 = 0;
+                uint32_t n0 = 0, n1 = 0, n2 = 0, n3 = 0;  // TAGS: reads per base
                 uint32_t seen = 0;  // bit 4 of a base byte: A/C/G/T
                 for (int i = 0; i < ns; i++) {
                     const uint32_t d = dlist[os + i];
@@ -1518,6 +1525,12 @@ __global__ __launch_bounds__(kWave *kSmallMaxWaves, kSmallMinWaves) __attribute_
                     D1 += bb == kC ? v : 0;
                     D2 += bb == kG ? v : 0;
                     D3 += bb == kT ? v : 0;
+                    if (TAGS) {
+                        n0 += bb == kA ? 1u : 0u;
+                        n1 += bb == kC ? 1u : 0u;
+                        n2 += bb == kG ? 1u : 0u;
+                        n3 += bb == kT ? 1u : 0u;
+                    }
                 }
                 int best = first_max4(D0, D1, D2, D3);
                 if (near_tie(D0, D1, D2, D3, best, ns))  // rare: fgbio's fp64 read-order pick
@@ -1532,6 +1545,15 @@ __global__ __launch_bounds__(kWave *kSmallMaxWaves, kSmallMinWaves) __attribute_
                 const bool nocall = !(seen & 0x10u) || Q < P.qmin;  // no A/C/G/T read, or below the mask
                 vb = nocall ? kN : (1u << best);
                 vq = nocall ? 2u : (uint32_t)Q;
+                if (TAGS) {  // this side's single-strand column (the fused tag statistics)
+                    const uint32_t depth = n0 + n1 + n2 + n3;
+                    const uint32_t nb = best == 0 ? n0 : best == 1 ? n1 : best == 2 ? n2 : n3;
+                    const int64_t at = (4 * (int64_t)fam + s) * stride + c;
+                    P.O.ss_base[at] = (uint8_t)vb;
+                    P.O.ss_qual[at] = (uint8_t)vq;
+                    P.O.ss_depth[at] = (uint16_t)::min(depth, 32767u);
+                    P.O.ss_err[at] = (uint16_t)::min(depth - nb, 32767u);
+                }
             }
             const uint32_t pb = (uint32_t)__shfl_xor((int)vb, 1, kWave), pq = (uint32_t)__shfl_xor((int)vq, 1, kWave);
             if (act && side == 0) {
@@ -1569,31 +1591,9 @@ __global__ __launch_bounds__(kWave *kSmallMaxWaves, kSmallMinWaves) __attribute_
             }
         }
     }
-    // single-strand reads and column statistics for the consensus tags: a lane per (set, column),
-    // walking the set's reads like the queued path (only with BSDC_MODE_TAGS)
-    if (TAGS && stop == 0) {
-#pragma unroll 1
-        for (int s = 0; s < 4; s++) {
-            const int ls = hs[s] ? lcs[s] : 0;
-            const int64_t row = (4 * (int64_t)fam + s) * stride;
-            for (int c = t; c < ls; c += kWave) {
-                SsAcc acc;
-                acc.clear();
-                for (int i = 0; i < cnt[s]; i++) {
-                    const uint32_t d = dlist[off[s] + i];
-                    if (c >= (int)((d >> 16) & 0x7FFF)) continue;
-                    const uint32_t idx = (d & 0x80000000u) ? (d & 0xFFFF) - c : (d & 0xFFFF) + c;
-                    const uint32_t braw = bimg[idx];
-                    const uint32_t bb = (d & 0x80000000u) ? comp_nt16(braw) : (braw & 0x0F);
-                    acc.add(bb, lr2[256 + qimg[idx]]);  // only one-hot codes count
-                }
-                auto pick = [&]() { return fp64_pick(SmallDesc{dlist + off[s]}, cnt[s], c, bimg, qimg, P.tab->lnc, P.tab->lne3); };
-                ss_store(acc, thr, cnt[s], P.qmin, pick, P.O.ss_base + row + c, P.O.ss_qual + row + c, P.O.ss_depth + row + c,
-                         P.O.ss_err + row + c);
-            }
-            if (t == 0) P.O.ss_len[4 * fam + s] = (uint16_t)ls;
-        }
-    }
+    // single-strand lengths of the consensus tags (their columns: the vote above, emitted families)
+    if (TAGS && t < 4) P.O.ss_len[4 * fam + t] = (uint16_t)(t == 0 ? (hs[0] ? lcs[0] : 0) : t == 1 ? (hs[1] ? lcs[1] : 0)
+                                                             : t == 2 ? (hs[2] ? lcs[2] : 0) : (hs[3] ? lcs[3] : 0));
     if (t == 0) {
         uint8_t st = emit ? 1 : 0;
         if (hs[0] || hs[1]) st |= 2;
@@ -1672,7 +1672,7 @@ __device__ __forceinline__ void block_sum_max(int a, int b, int *red, int &sum, 
     }
 }
 
-template <int G>
+template <int G, bool TAGS>
 __device__ void process_large(const KParams &P, uint8_t *A, uint8_t *s_tab, const int32_t *lr, const float *thr, uint4 ent,
                               int *red, int *s_cnt, int *s_lc, int *s_cur) {
     const int tt = threadIdx.x;
@@ -2158,7 +2158,8 @@ __device__ void process_large(const KParams &P, uint8_t *A, uint8_t *s_tab, cons
     // the read's end cleared, lr[q] added to the base's sum.  Sets of <= 128 reads: 4 columns per
     // thread, int32 sums (exact: |lr| < 2^24).  Deeper sets: 2 columns per thread, int32 sums
     // flushed to int64 every 128 reads.
-    auto resolve = [&](int s, int col, long long D0, long long D1, long long D2, long long D3) {
+    const int32_t stride_o = P.O.stride;
+    auto resolve = [&](int s, int col, long long D0, long long D1, long long D2, long long D3, uint32_t n01, uint32_t n23) {
         int best = first_max4(D0, D1, D2, D3);
         if (near_tie(D0, D1, D2, D3, best, cnt[s]))  // rare: fgbio's fp64 read-order pick
             best = fp64_pick(LargeDesc{desc + soff[s]}, cnt[s], col, slots, qimg, P.tab->lnc, P.tab->lne3);
@@ -2173,6 +2174,13 @@ __device__ void process_large(const KParams &P, uint8_t *A, uint8_t *s_tab, cons
         const bool nocall = ssb[s * ssw + col] == 0 || Q < P.qmin;
         ssb[s * ssw + col] = nocall ? (uint8_t)kN : (uint8_t)(1u << best);
         ssq[s * ssw + col] = nocall ? (uint8_t)2 : (uint8_t)Q;
+        if (TAGS) {  // the column's depth / errors (the raw best base's reads) for the consensus tags
+            const uint32_t depth = (n01 & 0xFFFFu) + (n01 >> 16) + (n23 & 0xFFFFu) + (n23 >> 16);
+            const uint32_t nb = ((best < 2 ? n01 : n23) >> (16 * (best & 1))) & 0xFFFFu;
+            const int64_t at = (4 * (int64_t)fam + s) * stride_o + col;
+            P.O.ss_depth[at] = (uint16_t)::min(depth, 32767u);
+            P.O.ss_err[at] = (uint16_t)::min(depth - nb, 32767u);
+        }
     };
     // Wavefronts by set: wave w works on set w % 4; with 8 waves (512 threads) the two waves of a
     // set split its reads (PARTS = 2).
@@ -2192,6 +2200,7 @@ __device__ void process_large(const KParams &P, uint8_t *A, uint8_t *s_tab, cons
     const int lane = tt & (kWave - 1), wv = tt >> 6, ws = wv & 3, wpart = wv >> 2;
     int64_t *psum = reinterpret_cast<int64_t *>(A + Lo.meta);        // [4][ssw] part-1 sums (RecMeta is dead)
     uint8_t *por = reinterpret_cast<uint8_t *>(psum + 4 * ssw);     // [4][ssw] part-1 ORs
+    uint16_t *pcn = reinterpret_cast<uint16_t *>(por + 4 * ssw);     // [4][ssw] part-1 A/C/G/T read counts (TAGS)
     {
         const int na = cnt[ws], lc = lcv[ws], nf = nfw[ws];
         const uint2 *dl = desc + soff[ws];
@@ -2201,8 +2210,10 @@ __device__ void process_large(const KParams &P, uint8_t *A, uint8_t *s_tab, cons
             const int c = cb + 4 * lane, c8 = 8 * c;
             long long T0 = 0, T1 = 0, T2 = 0, T3 = 0;
             uint32_t orm = 0;
+            uint32_t cn01 = 0, cn23 = 0;  // TAGS: A/C/G/T reads per column, u16 pairs
             if (cb < lc) {
                 int32_t t0 = 0, t1 = 0, t2 = 0, t3 = 0;
+                uint32_t c4 = 0;  // (bytes, <= 64 reads between flushes)
                 auto fwd = [&](uint32_t ex, uint32_t ey) {
                     const int sl = (int)ey;
                     const uint32_t keep = ~bytes_past(8 * sl - c8, false);
@@ -2211,6 +2222,7 @@ __device__ void process_large(const KParams &P, uint8_t *A, uint8_t *s_tab, cons
                     const uint32_t v = onehot01(b);
                     orm |= b & (v * 0xFFu);
                     lookup4v(lr2, v, q, t0, t1, t2, t3);
+                    if (TAGS) c4 += v;
                 };
                 auto rev = [&](uint32_t ex, uint32_t ey) {  // bytes run backwards from the read's last base
                     const int sl = (int)(ey & 0x7FFFFFFFu);
@@ -2221,6 +2233,7 @@ __device__ void process_large(const KParams &P, uint8_t *A, uint8_t *s_tab, cons
                     const uint32_t v = onehot01(b);
                     orm |= b & (v * 0xFFu);
                     lookup4v(lr2, v, q, t0, t1, t2, t3);
+                    if (TAGS) c4 += v;
                 };
                 auto flush = [&]() {  // int32 partials over <= 64 reads: exact
                     T0 += t0;
@@ -2228,6 +2241,11 @@ __device__ void process_large(const KParams &P, uint8_t *A, uint8_t *s_tab, cons
                     T2 += t2;
                     T3 += t3;
                     t0 = t1 = t2 = t3 = 0;
+                    if (TAGS) {
+                        cn01 += __builtin_amdgcn_perm(0u, c4, 0x0c010c00u);
+                        cn23 += __builtin_amdgcn_perm(0u, c4, 0x0c030c02u);
+                        c4 = 0;
+                    }
                 };
                 const int fe = ::min(re, nf);
                 for (int r0 = rb; r0 < fe; r0 += kWave) {
@@ -2260,6 +2278,7 @@ __device__ void process_large(const KParams &P, uint8_t *A, uint8_t *s_tab, cons
                         if (c + j < lc) {
                             psum[ws * ssw + c + j] = j == 0 ? T0 : j == 1 ? T1 : j == 2 ? T2 : T3;
                             por[ws * ssw + c + j] = (uint8_t)(orm >> (8 * j));
+                            if (TAGS) pcn[ws * ssw + c + j] = (uint16_t)((j < 2 ? cn01 : cn23) >> (16 * (j & 1)));
                         }
                 }
                 __syncthreads();
@@ -2271,9 +2290,11 @@ __device__ void process_large(const KParams &P, uint8_t *A, uint8_t *s_tab, cons
                     if (col >= lc) break;
                     uint32_t ob = (orm >> (8 * j)) & 0xFFu;
                     long long Tj = j == 0 ? T0 : j == 1 ? T1 : j == 2 ? T2 : T3;
+                    uint32_t nj = TAGS ? ((j < 2 ? cn01 : cn23) >> (16 * (j & 1))) & 0xFFFFu : 0u;
                     if (PARTS == 2) {
                         Tj += psum[ws * ssw + col];
                         ob |= por[ws * ssw + col];
+                        if (TAGS) nj += pcn[ws * ssw + col];
                     }
                     if (ob != 0 && (ob & (ob - 1)) == 0 && Tj > na) {
                         const float e = term(-Tj);
@@ -2281,6 +2302,11 @@ __device__ void process_large(const KParams &P, uint8_t *A, uint8_t *s_tab, cons
                         const int Q = phred_of(S, thr);
                         ssb[ws * ssw + col] = Q < P.qmin ? (uint8_t)kN : (uint8_t)ob;
                         ssq[ws * ssw + col] = Q < P.qmin ? (uint8_t)2 : (uint8_t)Q;
+                        if (TAGS) {  // one base seen: depth = its reads, errors 0
+                            const int64_t at = (4 * (int64_t)fam + ws) * stride_o + col;
+                            P.O.ss_depth[at] = (uint16_t)::min(nj, 32767u);
+                            P.O.ss_err[at] = 0;
+                        }
                     } else {
                         ssb[ws * ssw + col] = (uint8_t)ob;  // (the OR: pass B's no-call test)
                         ssq[ws * ssw + col] = 0;
@@ -2318,11 +2344,11 @@ __device__ void process_large(const KParams &P, uint8_t *A, uint8_t *s_tab, cons
         // reads a part, |lr| < 2^24), after mlist in the part-sum region.  Workgroup-uniform:
         // every set must fit, and every wave runs the same number of blocks (barriers inside).
         const int64_t region = ::max((int64_t)round16((int64_t)n * (int64_t)bsdc_layout::kRecMetaBytes) + round16(2 * (int64_t)n),
-                                     (int64_t)36 * ssw);
+                                     (int64_t)bsdc_layout::kVoteRegionPerCol * ssw);
         const int64_t pbo = round16(8 * (int64_t)ssw);
-        const bool split = PARTS == 2 && pbo + 4 * kWave * 16 <= region &&
+        const bool split = PARTS == 2 && pbo + 4 * kWave * 24 <= region &&
                            ::max(::max(cnt[0], cnt[1]), ::max(cnt[2], cnt[3])) <= 254;
-        int32_t *pb = reinterpret_cast<int32_t *>(reinterpret_cast<uint8_t *>(psum) + pbo);  // [4][64][4]
+        int32_t *pb = reinterpret_cast<int32_t *>(reinterpret_cast<uint8_t *>(psum) + pbo);  // [4][64][6]
         const int nmax = ::max(::max(s_lc[0], s_lc[1]), ::max(s_lc[2], s_lc[3]));
         const int rb = split ? (wpart == 0 ? 0 : na / 2) : 0, re = split ? (wpart == 0 ? na / 2 : na) : na;
         const int kstart = split ? 0 : kWave * wpart, kstep = split ? kWave : kWave * PARTS;
@@ -2337,6 +2363,7 @@ __device__ void process_large(const KParams &P, uint8_t *A, uint8_t *s_tab, cons
             const int col = k0 + cl < nm ? mlist[s * ssw + k0 + cl] : 0;
             long long D0 = 0, D1 = 0, D2 = 0, D3 = 0;
             int32_t d0 = 0, d1 = 0, d2 = 0, d3 = 0;
+            uint32_t n01 = 0, n23 = 0;  // TAGS: reads per base, u16 pairs (A | C << 16, G | T << 16)
             auto one = [&](uint32_t ex, uint32_t ey) {
                 const int sl = (int)(ey & 0x7FFFFFFFu);
                 const bool rv = ey >> 31, in = col < sl;
@@ -2347,6 +2374,10 @@ __device__ void process_large(const KParams &P, uint8_t *A, uint8_t *s_tab, cons
                 d1 += bb == kC ? v : 0;
                 d2 += bb == kG ? v : 0;
                 d3 += bb == kT ? v : 0;
+                if (TAGS && in) {
+                    n01 += bb == kA ? 1u : bb == kC ? 0x10000u : 0u;
+                    n23 += bb == kG ? 1u : bb == kT ? 0x10000u : 0u;
+                }
             };
             if (half) {
                 for (int r0 = 0; r0 < h; r0 += 32) {
@@ -2376,6 +2407,10 @@ __device__ void process_large(const KParams &P, uint8_t *A, uint8_t *s_tab, cons
                 add_up(D1);
                 add_up(D2);
                 add_up(D3);
+                if (TAGS) {
+                    n01 += (uint32_t)__shfl_xor((int)n01, 32, kWave);
+                    n23 += (uint32_t)__shfl_xor((int)n23, 32, kWave);
+                }
             }
             for (int r0 = rb; r0 < re && k0 < nm && !half; r0 += kWave) {
                 const uint2 dr = r0 + lane < re ? dl[r0 + lane] : make_uint2(0u, 0u);
@@ -2393,18 +2428,24 @@ __device__ void process_large(const KParams &P, uint8_t *A, uint8_t *s_tab, cons
                 d0 = d1 = d2 = d3 = 0;
             }
             if (split) {
-                int32_t *pw = pb + 4 * (s * kWave + lane);
+                int32_t *pw = pb + 6 * (s * kWave + lane);
                 if (wpart == 1 && act) {
                     pw[0] = (int32_t)D0;
                     pw[1] = (int32_t)D1;
                     pw[2] = (int32_t)D2;
                     pw[3] = (int32_t)D3;
+                    if (TAGS) {
+                        pw[4] = (int32_t)n01;
+                        pw[5] = (int32_t)n23;
+                    }
                 }
                 __syncthreads();
-                if (wpart == 0 && act) resolve(s, col, D0 + pw[0], D1 + pw[1], D2 + pw[2], D3 + pw[3]);
+                if (wpart == 0 && act)
+                    resolve(s, col, D0 + pw[0], D1 + pw[1], D2 + pw[2], D3 + pw[3], TAGS ? n01 + (uint32_t)pw[4] : 0u,
+                            TAGS ? n23 + (uint32_t)pw[5] : 0u);
                 __syncthreads();
             } else if (act) {
-                resolve(s, col, D0, D1, D2, D3);
+                resolve(s, col, D0, D1, D2, D3, n01, n23);
             }
         }
     }
@@ -2446,28 +2487,15 @@ __device__ void process_large(const KParams &P, uint8_t *A, uint8_t *s_tab, cons
             }
         }
     }
-    if ((P.mode & BSDC_MODE_TAGS) && stop == 0) {  // consensus-tag statistics, a thread per (set, column)
-        const int ntag = (hs[0] ? lcv[0] : 0) + (hs[1] ? lcv[1] : 0) + (hs[2] ? lcv[2] : 0) + (hs[3] ? lcv[3] : 0);
-        for (int k = tt; k < ntag; k += G) {
-            int s = 0, c = k;
-            while (c >= (hs[s] ? lcv[s] : 0)) {
-                c -= hs[s] ? lcv[s] : 0;
-                s++;
+    if (TAGS && stop == 0) {  // the single-strand reads of the consensus tags (the vote's rows; depth /
+        // errors went out with the calls)
+        for (int s = 0; s < 4; s++) {
+            const int ls = hs[s] ? lcv[s] : 0;
+            const int64_t row = (4 * (int64_t)fam + s) * stride;
+            for (int c = tt; c < ls; c += G) {
+                P.O.ss_base[row + c] = ssb[s * ssw + c];
+                P.O.ss_qual[row + c] = ssq[s * ssw + c];
             }
-            SsAcc acc;
-            acc.clear();
-            const uint2 *dl = desc + soff[s];
-            for (int i = 0; i < cnt[s]; i++) {
-                const uint2 e = dl[i];
-                if (c >= (int)(e.y & 0x7FFFFFFFu)) continue;
-                const bool rv = e.y >> 31;
-                const int32_t a = rv ? (int32_t)e.x - c : (int32_t)e.x + c;
-                const uint32_t braw = slots[a] & 0x0Fu;
-                acc.add(rv ? comp_nt16(braw) : braw, lr[qimg[a]]);
-            }
-            const int64_t at = (4 * (int64_t)fam + s) * stride + c;
-            auto pick = [&]() { return fp64_pick(LargeDesc{dl}, cnt[s], c, slots, qimg, P.tab->lnc, P.tab->lne3); };
-            ss_store(acc, thr, cnt[s], P.qmin, pick, P.O.ss_base + at, P.O.ss_qual + at, P.O.ss_depth + at, P.O.ss_err + at);
         }
         if (tt < 4) P.O.ss_len[4 * fam + tt] = (uint16_t)(hs[tt] ? lcv[tt] : 0);
     }
@@ -2491,7 +2519,7 @@ struct TablesL {  // k_large's LDS copy: the prefix of Tables it reads
 static_assert(sizeof(TablesL) == kTabBytesL, "TablesL image");
 // G = 256 threads for the buckets that fit 3 or more workgroups per CU, 512 for the LDS-heavy ones
 // (2 or 1 per CU, HBM scratch): twice the wavefronts in flight for the same LDS.
-template <bool IN_LDS, int G>
+template <bool IN_LDS, int G, bool TAGS>
 __global__ __launch_bounds__(G, G == 256 ? 5 : 2) void k_large(KParams P, const uint4 *fams, int64_t nfams, int32_t arena,
                                                                 int64_t scratch_off) {
     extern __shared__ __attribute__((aligned(16))) uint8_t smem[];  // the family's arena (IN_LDS)
@@ -2511,7 +2539,7 @@ __global__ __launch_bounds__(G, G == 256 ? 5 : 2) void k_large(KParams P, const 
     if (threadIdx.x == 0) s_cnt[0] = 0;  // the converted-record count (process_large's first phase)
     __syncthreads();
     uint8_t *A = IN_LDS ? smem : P.O.scratch + scratch_off + (size_t)i * (size_t)arena;
-    process_large<G>(P, A, reinterpret_cast<uint8_t *>(&s_tab), lr, thr, fams[i], red, s_cnt, s_lc, s_cur);
+    process_large<G, TAGS>(P, A, reinterpret_cast<uint8_t *>(&s_tab), lr, thr, fams[i], red, s_cnt, s_lc, s_cur);
 }
 
 }  // namespace
@@ -2906,15 +2934,28 @@ int32_t bsdc_run(bsdc_ctx *c, const bsdc_family_batch *b, bsdc_consensus *o, int
                 const bool big = q >= kLargeBigBucket;  // 2 or 1 workgroups per CU, or HBM scratch
                 const hipStream_t ls = next_stream();
                 if (rc) break;
-                if (a <= BSDC_LARGE_LDS_MAX && !big)
-                    hipLaunchKernelGGL((k_large<true, kLargeThreads>), dim3((unsigned)nf), dim3(kLargeThreads), (size_t)a, ls, P, f, nf, a,
-                                       (int64_t)0);
-                else if (a <= BSDC_LARGE_LDS_MAX)
-                    hipLaunchKernelGGL((k_large<true, kLargeThreadsBig>), dim3((unsigned)nf), dim3(kLargeThreadsBig), (size_t)a, ls, P, f,
-                                       nf, a, (int64_t)0);
-                else {
-                    hipLaunchKernelGGL((k_large<false, kLargeThreadsBig>), dim3((unsigned)nf), dim3(kLargeThreadsBig), 0, ls, P, f, nf, a,
-                                       soff);
+                const bool tg = (mode & BSDC_MODE_TAGS) != 0;
+                if (a <= BSDC_LARGE_LDS_MAX && !big) {
+                    if (tg)
+                        hipLaunchKernelGGL((k_large<true, kLargeThreads, true>), dim3((unsigned)nf), dim3(kLargeThreads), (size_t)a, ls, P, f,
+                                           nf, a, (int64_t)0);
+                    else
+                        hipLaunchKernelGGL((k_large<true, kLargeThreads, false>), dim3((unsigned)nf), dim3(kLargeThreads), (size_t)a, ls, P,
+                                           f, nf, a, (int64_t)0);
+                } else if (a <= BSDC_LARGE_LDS_MAX) {
+                    if (tg)
+                        hipLaunchKernelGGL((k_large<true, kLargeThreadsBig, true>), dim3((unsigned)nf), dim3(kLargeThreadsBig), (size_t)a, ls,
+                                           P, f, nf, a, (int64_t)0);
+                    else
+                        hipLaunchKernelGGL((k_large<true, kLargeThreadsBig, false>), dim3((unsigned)nf), dim3(kLargeThreadsBig), (size_t)a,
+                                           ls, P, f, nf, a, (int64_t)0);
+                } else {
+                    if (tg)
+                        hipLaunchKernelGGL((k_large<false, kLargeThreadsBig, true>), dim3((unsigned)nf), dim3(kLargeThreadsBig), 0, ls, P, f,
+                                           nf, a, soff);
+                    else
+                        hipLaunchKernelGGL((k_large<false, kLargeThreadsBig, false>), dim3((unsigned)nf), dim3(kLargeThreadsBig), 0, ls, P,
+                                           f, nf, a, soff);
                     soff += nf * (int64_t)a;
                 }
                 const hipError_t e = hipGetLastError();

@@ -17,6 +17,9 @@ BSDC_HD inline int64_t round16(int64_t x) { return (x + 15) & ~int64_t(15); }
 // 16-B chunks that cover one converted record's packed reference window
 BSDC_HD inline int ref_chunks(int max_len) { return (15 + (max_len + 4) / 2 + 15) / 16; }
 constexpr int kRecMetaBytes = 48;  // k_large's per-record metadata (RecMeta)
+// k_large's vote scratch per output column, in the region RecMeta leaves dead: the second wave
+// part's int64 sums (32), ORs (4) and A/C/G/T read counts (8, the tags)
+constexpr int kVoteRegionPerCol = 44;
 
 // Arena of one small family.  Regions live only as long as their phase and share space:
 //   bimg, qimg  the family image, bases / quals (whole kernel)
@@ -73,7 +76,8 @@ struct ArenaLayout {
         // wave part's sums
         meta = (uint32_t)o;
         clist = (uint32_t)(o + round16((int64_t)n * (int64_t)kRecMetaBytes));
-        const int64_t mb = round16((int64_t)n * (int64_t)kRecMetaBytes) + round16(2 * (int64_t)n), vb = 36 * (int64_t)ssw;
+        const int64_t mb = round16((int64_t)n * (int64_t)kRecMetaBytes) + round16(2 * (int64_t)n),
+                      vb = kVoteRegionPerCol * (int64_t)ssw;
         o += mb > vb ? mb : vb;
         lists = (uint32_t)o;
         o += round16((int64_t)n * 8);

@@ -7,6 +7,8 @@ synthetic coordinate-sorted C2 BAM + FASTA on local disk, then, each in a fresh 
   stream_gpubgzf, stream_fastq_gpubgzf  the same with the BGZF deflate on the GPU
   fleet   fleet.step5_stream_multi: this child reads and writes (it never touches the GPU), --workers
           spawned GPU worker processes (all on GPU 0 on a one-GPU box) run the batches
+  molecular_stream, molecular_whole  step 1 (bam.molecular_stream / bam.molecular) on the same
+          families in GroupReadsByUmi order (a second input, MI runs contiguous; BAM with tags, GPU BGZF)
 The BAMs are compared byte for byte.  Usage:
   python profiles/e2e_stream.py [--families N] [--threads T] [--chunk-mb M] [--level L]
                                 [--modes stream,stream_fastq,whole,fleet] [--workers W]"""
@@ -37,6 +39,9 @@ def prep(args):
     hdr = bam.BamHeader("@HD\tVN:1.6\tSO:coordinate\n@SQ\tSN:%s\tLN:%d\n@RG\tID:x\tSM:s\tLB:L1\n" % (
         s.ref.names[0], len(codes)), [s.ref.names[0]], np.asarray([len(codes)], np.int64))
     bam.write_bam(args.inp, hdr, bam.records_to_bam(raw), level=args.level, threads=args.threads)
+    if args.grouped:  # step 1's input: each MI's /A and /B molecules contiguous
+        g = R.take(s.raw, np.lexsort((s.raw.mi_strand, s.raw.mi_id)))
+        bam.write_bam(args.grouped, hdr, bam.records_to_bam(g), level=args.level, threads=args.threads)
     print(json.dumps({"records": int(raw.n)}))
 
 
@@ -65,7 +70,12 @@ def child(args):
     ru0 = resource.getrusage(resource.RUSAGE_SELF)
     cpu0 = ru0.ru_utime + ru0.ru_stime
     t0 = time.perf_counter()
-    if args.mode == "whole":
+    if args.mode == "molecular_stream":
+        info = bam.molecular_stream(args.grouped, args.out, engine=eng, threads=args.threads, level=args.level,
+                                    chunk_bytes=args.chunk_mb << 20, stats=stats, gpu_bgzf=True)
+    elif args.mode == "molecular_whole":
+        info = bam.molecular(args.grouped, args.out, engine=eng, threads=args.threads, level=args.level)
+    elif args.mode == "whole":
         info = bam.step5(args.inp, args.fa, args.out, engine=eng, threads=args.threads, level=args.level)
     elif args.mode in ("stream_fastq", "stream_fastq_gpubgzf"):  # the fused FASTQ emission
         # (main.snake.py:167-177), no BAM; _gpubgzf: its blocks deflated on the GPU
@@ -98,6 +108,7 @@ def main():
     ap.add_argument("--inp")
     ap.add_argument("--fa")
     ap.add_argument("--out")
+    ap.add_argument("--grouped", default="")
     a = ap.parse_args()
     if a.mode:
         return child(a)
@@ -105,8 +116,10 @@ def main():
     d = tempfile.mkdtemp(prefix="bsdc_e2es_")
     t0 = time.perf_counter()
     fa, inp = os.path.join(d, "g.fa"), os.path.join(d, "in.bam")
+    grouped = os.path.join(d, "grouped.bam") if "molecular" in a.modes else ""
     p = subprocess.run([sys.executable, os.path.abspath(__file__), "--mode", "prep", "--inp", inp, "--fa", fa,
-                        "--families", str(a.families), "--threads", str(a.threads), "--level", str(a.level)],
+                        "--families", str(a.families), "--threads", str(a.threads), "--level", str(a.level),
+                        "--grouped", grouped],
                        stdout=subprocess.PIPE, text=True, timeout=900)
     if p.returncode != 0:
         print(p.stdout[-2000:], file=sys.stderr)
@@ -121,7 +134,8 @@ def main():
         out = os.path.join(d, mode + ".bam")
         p = subprocess.run([sys.executable, os.path.abspath(__file__), "--mode", mode, "--inp", inp, "--fa", fa,
                             "--out", out, "--threads", str(a.threads), "--chunk-mb", str(a.chunk_mb),
-                            "--level", str(a.level), "--workers", str(a.workers)], stdout=subprocess.PIPE, text=True,
+                            "--level", str(a.level), "--workers", str(a.workers), "--grouped", grouped],
+                           stdout=subprocess.PIPE, text=True,
                            timeout=900)
         if p.returncode != 0:
             print(p.stdout[-2000:], file=sys.stderr)
@@ -131,7 +145,8 @@ def main():
         res[mode] = r
         outs[mode] = out
         print(mode, json.dumps(r), flush=True)
-    bams = [open(outs[m], "rb").read() for m in outs if m not in ("stream_fastq", "stream_gpubgzf", "stream_fastq_gpubgzf")]
+    bams = [open(outs[m], "rb").read() for m in outs if m not in ("stream_fastq", "stream_gpubgzf", "stream_fastq_gpubgzf")
+            and not m.startswith("molecular")]
     res["outputs_identical"] = all(b == bams[0] for b in bams)
     if "stream_gpubgzf" in outs and "stream" in outs:  # other compressed bytes: compare the records
         sys.path.insert(0, ROOT)
@@ -146,6 +161,12 @@ def main():
         res["fastq_gpubgzf_text_identical"] = all(
             gzip.open(outs["stream_fastq"] + x).read() == gzip.open(outs["stream_fastq_gpubgzf"] + x).read()
             for x in (".1.fq.gz", ".2.fq.gz"))
+    if "molecular_stream" in outs and "molecular_whole" in outs:  # GPU BGZF vs host deflate: the records
+        sys.path.insert(0, ROOT)
+        from bsseqconsensusreads_amd import bam as B
+        _, ra = B.read_bam(outs["molecular_whole"], a.threads)
+        _, rb = B.read_bam(outs["molecular_stream"], a.threads)
+        res["molecular_records_identical"] = bool(ra.n == rb.n and (ra.seq == rb.seq).all() and (ra.qual == rb.qual).all())
     print(json.dumps(res))
     return 0
 

@@ -38,7 +38,9 @@ def _gpu_vs_fp64(engine, raw, ref, run_tools, what, molecular=False):
     src = r.sources
     stride = cons.ss["base"].shape[2]
     ss = fv.ss_vote(src["count"], src["len"], src["base"], src["qual"], stride, min_cbq=min_cbq)
-    c = fv.compare_ss({"len": cons.ss["len"], "base": cons.ss["base"], "qual": cons.ss["qual"]}, ss)
+    em = np.nonzero((cons.status & 1) != 0)[0]  # (the kernels' single-strand reads: emitted families)
+    c = fv.compare_ss({"len": cons.ss["len"][em], "base": cons.ss["base"][em], "qual": cons.ss["qual"][em]},
+                      {k: v[em] for k, v in ss.items()})
     assert_fp64_bar(c, what)
     # duplex consensus vs fgbio fp64 duplex of the fp64 single-strand reads
     st, ln, b, q = fv.duplex(ss)
@@ -56,6 +58,7 @@ def _gpu_vs_fp64(engine, raw, ref, run_tools, what, molecular=False):
         for st_ in (sa, sb):
             same[:, e, :w] &= (cons.ss["base"][:, st_, :w] == ss["base"][:, st_, :w]) & \
                               (cons.ss["qual"][:, st_, :w] == ss["qual"][:, st_, :w])
+    same[(cons.status & 1) == 0] = True  # (no duplex read there: ln is 0)
     assert not (db & same[:, :, :w]).any(), what + ": duplex base differs from fgbio fp64"
     assert not (live & (dq > 0) & same[:, :, :w]).any(), what + ": duplex qual differs from fgbio fp64"
     if c["qual_pm1"] == 0 and c["n_boundary"] == 0:
@@ -104,7 +107,8 @@ def test_gpu_min_consensus_base_quality(engine, kernel, caller, monkeypatch):
     cons = _gpu_vs_fp64(engine, raw, s.ref, False, "low-quality %s %s" % (caller, kernel),
                         molecular=caller == "molecular")
     w = cons.ss["qual"].shape[2]
-    live = np.arange(w)[None, None, :] < cons.ss["len"][:, :, None]
+    em = (cons.status & 1) != 0
+    live = (np.arange(w)[None, None, :] < cons.ss["len"][:, :, None]) & em[:, None, None]
     q1 = int((live & (cons.ss["qual"] == 1)).sum())
     assert (q1 > 50) if caller == "molecular" else (q1 == 0)
     assert engine.params.min_consensus_base_quality == 2
