@@ -8,7 +8,7 @@ HERE = os.path.dirname(os.path.abspath(__file__))
 # BSDC_LIB_PATH: an alternative build of the same library (profiling A/B runs only)
 LIB_PATH = os.environ.get("BSDC_LIB_PATH") or os.path.join(HERE, "libbsdc.so")
 
-BSDC_ABI_VERSION = 10
+BSDC_ABI_VERSION = 11
 SMALL_BUCKETS = 8  # BSDC_SMALL_BUCKETS
 LARGE_BUCKETS = 6  # BSDC_LARGE_BUCKETS
 MODE_CONVERT, MODE_EXTEND, MODE_VOTE, MODE_DUMP = 1, 2, 4, 8
@@ -29,7 +29,10 @@ class FamilyBatchC(C.Structure):
                 ("rt", C.c_void_p), ("seq", C.c_void_p), ("qual", C.c_void_p),
                 ("small_fams", C.c_void_p), ("n_small", C.c_int64 * SMALL_BUCKETS), ("small_arena", C.c_int32 * SMALL_BUCKETS),
                 ("large_fams", C.c_void_p), ("n_large", C.c_int64 * LARGE_BUCKETS), ("large_arena", C.c_int32 * LARGE_BUCKETS),
-                ("max_len", C.c_int32)]
+                ("max_len", C.c_int32), ("split_part_arena", C.c_int32),
+                ("split_parts", C.c_void_p), ("n_split_parts", C.c_int64), ("split_part_recs", C.c_void_p),
+                ("split_fams", C.c_void_p),
+                ("n_split_fams", C.c_int64), ("split_partial_off", C.c_int64)]
 
 
 class ConsensusC(C.Structure):

@@ -16,7 +16,8 @@ so the kernel only ever sees records that reach the vote:
 """
 from __future__ import annotations
 
-from dataclasses import dataclass
+import os
+from dataclasses import dataclass, field
 from typing import List, Optional
 
 import numpy as np
@@ -47,6 +48,10 @@ LARGE_LDS_MAX = 158912  # BSDC_LARGE_LDS_MAX: 160 KB - the tables - the kernel's
 # the largest arena that still fits k = 5, 4, 3, 2, 1 workgroups per CU (5 is the VGPR limit)
 LARGE_BUCKETS = tuple((160 * 1024 // k - LDS_TABLES - 256) // 16 * 16 for k in (5, 4, 3, 2, 1))  # + 1 scratch bucket
 assert LARGE_BUCKETS[-1] == LARGE_LDS_MAX
+# k_large part mode (include/bsdc.h split_parts): the HBM-scratch bucket's families are cut into
+# parts whose arena fits this (3 workgroups of 256 threads per CU); BSDC_PART_CAP=0 turns it off
+PART_CAP = int(os.environ.get("BSDC_PART_CAP", str(LARGE_BUCKETS[2])))
+MAX_PART_REC = 254  # a part's per-set sums stay int32 and its read counts fit a byte
 
 
 def round16(x):
@@ -77,9 +82,9 @@ def large_arena_bytes(n, slot_bytes, max_len, complex_ops):
     """Mirror of ArenaLayout (csrc/bsdc_kernels.hip) / bsdc_family_arena_bytes."""
     n = np.asarray(n, dtype=np.int64)
     ssw = round16(np.asarray(max_len, dtype=np.int64) + 2)
-    # RecMeta per record + the converted-record list, or (vote) the second wave part's column sums
-    # and ORs: 36 B per column
-    total = np.maximum(round16(n * 48) + round16(2 * n), 36 * ssw) + round16(n * 8) + 8 * ssw
+    # RecMeta per record + the converted-record list, or (vote) the second wave part's column sums,
+    # ORs and read counts: 44 B per column (bsdc_layout::kVoteRegionPerCol)
+    total = np.maximum(round16(n * 48) + round16(2 * n), 44 * ssw) + round16(n * 8) + 8 * ssw
     cops = np.asarray(complex_ops, dtype=np.int64)
     total = total + np.where(cops > 0, round16(4 * (cops + 4 * n)), 0)
     total = total + round16(np.asarray(slot_bytes, dtype=np.int64))
@@ -119,6 +124,11 @@ class FamilyBatch:
     n_slots: int
     t2_rank: np.ndarray      # i64 [R] tool-2 output position of each batch record
     split_ext: bool          # a tool-2 extension partner sits in another family (see build_family_batch)
+    # ---- k_large part mode (split_hbm_bucket; include/bsdc.h) ----
+    split_parts: np.ndarray = field(default_factory=lambda: np.zeros((0, 4), np.uint32))  # u32 [P, 4]
+    split_part_recs: np.ndarray = field(default_factory=lambda: np.zeros((0, 4), np.uint32))  # u32 [PR, 4]
+    split_fams: np.ndarray = field(default_factory=lambda: np.zeros((0, 8), np.uint32))   # u32 [S, 8], arena offsets relative
+    split_part_arena: int = 16
 
     @property
     def n_rec(self) -> int:
@@ -141,6 +151,21 @@ class FamilyBatch:
         """u32 [n_large, 4] list entries of every large bucket, in order."""
         return np.concatenate(self.large_buckets).astype(np.uint32).reshape(-1, 4)
 
+    def scratch_layout(self):
+        """HBM scratch of the batch (bsdc_consensus.scratch): the arenas of the large buckets beyond
+        the LDS budget, the split families' fallback arenas, the parts' sums.  -> (total bytes, split
+        arena base, partial sums offset)."""
+        hbm = sum(int(b.shape[0]) * a for b, a in zip(self.large_buckets, self.large_arenas)
+                  if b.shape[0] and a > LARGE_LDS_MAX)
+        base = int(round16(hbm))
+        sf = self.split_fams
+        arenas = int(sf[:, 7].astype(np.int64).sum()) if sf.shape[0] else 0
+        poff = int(round16(base + arenas))
+        npart = int(self.split_parts.shape[0])
+        psz = int(round16(32 * npart)) + npart * 4 * self.stride * 20 if npart else 0
+        total = poff + psz
+        return (total + 256 if total else 0), base, poff
+
     def device_arrays(self):
         rec = np.stack([self.rec_off, self.rec_pos.view(np.uint32), self.rec_lenflag, self.rec_link], axis=1)
         d = {"fam_off": self.fam_off, "rec": np.ascontiguousarray(rec, dtype=np.uint32),
@@ -149,6 +174,12 @@ class FamilyBatch:
             d[k] = getattr(self, k)
         d["small_fams"] = np.ascontiguousarray(self.fam_entry[self.small_fams.astype(np.int64)]).reshape(-1) \
             if self.small_fams.shape[0] else np.zeros(4, np.uint32)
+        d["split_parts"] = np.ascontiguousarray(self.split_parts, np.uint32).reshape(-1)
+        d["split_part_recs"] = np.ascontiguousarray(self.split_part_recs, np.uint32).reshape(-1)
+        sf = np.array(self.split_fams, np.uint32).reshape(-1, 8)
+        if sf.shape[0]:  # fallback arena offsets: scratch-absolute, in 16-byte units
+            sf[:, 6] += np.uint32(self.scratch_layout()[1] // 16)
+        d["split_fams"] = sf.reshape(-1)
         return d
 
 
@@ -607,11 +638,62 @@ def plan_families_py(raw: R.RawRecords, mode: str = "full", ref: Optional[R.Refe
 
 def materialize(plan: FamilyPlan, f0: int, f1: int, small_cap: int = SMALL_ARENA_CAP, images=None) -> FamilyBatch:
     """The device batch of plan families [f0, f1) (family ids renumbered from 0): C++ (hostplan)
-    for the step-5 modes, materialize_py otherwise.  images: see hostplan.materialize."""
+    for the step-5 modes, materialize_py otherwise; then the HBM bucket's families cut into parts
+    (split_hbm_bucket).  images: see hostplan.materialize."""
     from . import hostplan
     if plan.mode in ("full", "vote") and hostplan.enabled():
-        return hostplan.materialize(plan, f0, f1, small_cap, images=images)
-    return materialize_py(plan, f0, f1, small_cap)
+        return split_hbm_bucket(hostplan.materialize(plan, f0, f1, small_cap, images=images))
+    return split_hbm_bucket(materialize_py(plan, f0, f1, small_cap))
+
+
+def split_hbm_bucket(fb: FamilyBatch, part_cap: Optional[int] = None, threads: int = 0) -> FamilyBatch:
+    """k_large's part mode (include/bsdc.h): the families of the HBM-scratch bucket that can be
+    cut between templates (no complex cigar, no tool-2 role) become parts of at most part_cap LDS
+    bytes, run in LDS, and one join workgroup per family; the rest stay in the bucket.  In place."""
+    from . import hostplan
+    cap = PART_CAP if part_cap is None else int(part_cap)
+    ents = np.ascontiguousarray(fb.large_buckets[-1], np.uint32).reshape(-1, 4)
+    if cap <= 0 or ents.shape[0] == 0:
+        return fb
+    cap = cap // 16 * 16
+    lib = hostplan._load()
+    rec = np.ascontiguousarray(np.stack([fb.rec_off, fb.rec_pos.view(np.uint32), fb.rec_lenflag, fb.rec_link], axis=1),
+                               np.uint32)
+    k = ents.shape[0]
+    nparts = np.zeros(k, np.int32)
+    nrecs = np.zeros(k, np.int64)
+    tot = int(lib.bsdc_split_count(rec.ctypes.data, ents.ctypes.data, k, cap, MAX_PART_REC, nparts.ctypes.data,
+                                   nrecs.ctypes.data, int(threads)))
+    if tot == 0:
+        return fb
+    first = np.zeros(k, np.int64)
+    first[1:] = np.cumsum(nparts[:-1], dtype=np.int64)
+    first_rec = np.zeros(k, np.int64)
+    first_rec[1:] = np.cumsum(nrecs[:-1])
+    parts = np.zeros((tot, 4), np.uint32)
+    part_recs = np.zeros((int(nrecs.sum()), 4), np.uint32)
+    lib.bsdc_split_fill(rec.ctypes.data, ents.ctypes.data, k, cap, MAX_PART_REC, first.ctypes.data, first_rec.ctypes.data,
+                        parts.ctypes.data, part_recs.ctypes.data, int(threads))
+    cut = nparts > 0
+    ce = ents[cut].astype(np.int64)
+    # the fallback arena of each cut family (ArenaLayout of the whole family, no complex cigars)
+    L = (fb.rec_lenflag & 0xFFFF).astype(np.int64)
+    mlf = np.asarray([int(L[a:a + m].max()) for a, m in zip(ce[:, 1], ce[:, 2])], np.int64)
+    need = round16(large_arena_bytes(ce[:, 2], 2 * ce[:, 3], mlf, np.zeros(ce.shape[0], np.int64)))
+    sf = np.zeros((ce.shape[0], 8), np.int64)
+    sf[:, :4] = ce
+    sf[:, 4] = first[cut]
+    sf[:, 5] = nparts[cut]
+    off = np.zeros(ce.shape[0], np.int64)
+    off[1:] = np.cumsum(need[:-1])
+    sf[:, 6] = off // 16
+    sf[:, 7] = need
+    fb.split_parts = parts
+    fb.split_part_recs = part_recs
+    fb.split_fams = sf.astype(np.uint32)
+    fb.split_part_arena = cap
+    fb.large_buckets = list(fb.large_buckets[:-1]) + [ents[~cut]]
+    return fb
 
 
 def materialize_py(plan: FamilyPlan, f0: int, f1: int, small_cap: int = SMALL_ARENA_CAP) -> FamilyBatch:

@@ -751,3 +751,128 @@ int32_t bsdc_materialize_fill(bsdc_batch *b, const bsdc_batch_arrays *o, int64_t
 void bsdc_batch_free(bsdc_batch *b) { delete b; }
 
 }  // extern "C"
+
+// ------------------------------------------------------------------------------------------
+// part mode: split families of the HBM-scratch bucket (include/bsdc_host.h)
+// ------------------------------------------------------------------------------------------
+namespace {
+struct SplitPart {
+    std::vector<int32_t> recs;   // family-local record indices
+    std::vector<int32_t> lmate;  // part-local mate index of each (0xFFFF: none)
+    int64_t img = 0;             // slot bytes, rounded to 32
+};
+// The parts of one bucket entry: whole templates (an R1 and the R2 its mate link names, or a
+// record no link joins) dealt in record order into parts grown while their arena fits; empty when
+// the family is not cut.  A record's slot holds round4(len + 2) entries (include/bsdc.h).
+std::vector<SplitPart> split_one(const uint32_t *rec, const uint32_t *e, int64_t part_cap, int32_t max_part_rec) {
+    std::vector<SplitPart> parts;
+    const int64_t r0 = e[1], n = e[2];
+    if (n < 2 || n >= 65536) return parts;
+    std::vector<int32_t> mate_of((size_t)n, -1);
+    std::vector<uint8_t> is_target((size_t)n, 0);
+    for (int64_t i = 0; i < n; i++) {
+        const uint32_t link = rec[4 * (r0 + i) + 3];
+        if (link & (BSDC_LINK_COMPLEX | BSDC_LINK_EXT_LEFT | BSDC_LINK_EXT_RIGHT)) return parts;
+        const uint32_t m = link & BSDC_LINK_MATE_MASK;
+        if (m == BSDC_LINK_MATE_MASK) continue;
+        if ((int64_t)m >= n || (int64_t)m == i || is_target[m]) return parts;
+        mate_of[(size_t)i] = (int32_t)m;
+        is_target[(size_t)m] = 1;
+    }
+    auto len_of = [&](int64_t i) { return (int32_t)(rec[4 * (r0 + i) + 2] & 0xFFFF); };
+    auto cap4 = [&](int64_t i) { return (int64_t)((len_of(i) + 2 + 3) & ~3); };
+    SplitPart cur;
+    int32_t ml = 0;
+    int64_t span = 0;
+    auto close = [&]() {
+        cur.img = (span + 31) & ~int64_t(31);
+        parts.push_back(std::move(cur));
+        cur = SplitPart();
+        ml = 0;
+        span = 0;
+    };
+    for (int64_t i = 0; i < n; i++) {
+        if (is_target[(size_t)i]) continue;  // (placed with its R1)
+        const int64_t m = mate_of[(size_t)i];
+        const int k = m >= 0 ? 2 : 1;
+        const int64_t add = cap4(i) + (m >= 0 ? cap4(m) : 0);
+        const int32_t ml2 = std::max(ml, std::max(len_of(i), m >= 0 ? len_of(m) : 0));
+        const int64_t n2 = (int64_t)cur.recs.size() + k;
+        const int64_t need = bsdc_layout::ArenaLayout((int)n2, 2 * ((span + add + 31) & ~int64_t(31)), ml2, 0).total;
+        if (!cur.recs.empty() && (need > part_cap || n2 > max_part_rec)) close();
+        {
+            const int64_t n1 = (int64_t)cur.recs.size() + k;
+            const int32_t ml1 = std::max(ml, std::max(len_of(i), m >= 0 ? len_of(m) : 0));
+            if (bsdc_layout::ArenaLayout((int)n1, 2 * ((span + add + 31) & ~int64_t(31)), ml1, 0).total > part_cap ||
+                n1 > max_part_rec) {  // one template alone does not fit
+                parts.clear();
+                return parts;
+            }
+        }
+        const int32_t li = (int32_t)cur.recs.size();
+        cur.recs.push_back((int32_t)i);
+        cur.lmate.push_back(m >= 0 ? li + 1 : 0xFFFF);
+        if (m >= 0) {
+            cur.recs.push_back((int32_t)m);
+            cur.lmate.push_back(0xFFFF);
+        }
+        span += add;
+        ml = std::max(ml, std::max(len_of(i), m >= 0 ? len_of(m) : 0));
+    }
+    if (!cur.recs.empty()) close();
+    if (parts.size() < 2) parts.clear();
+    return parts;
+}
+}  // namespace
+
+extern "C" {
+
+int64_t bsdc_split_count(const uint32_t *rec, const uint32_t *ents, int64_t n_ent, int64_t part_cap, int32_t max_part_rec,
+                         int32_t *nparts, int64_t *nrecs, int32_t n_threads) {
+#ifdef _OPENMP
+    if (n_threads > 0) omp_set_num_threads(n_threads);
+#endif
+    int64_t tot = 0;
+#pragma omp parallel for schedule(dynamic, 4) reduction(+ : tot)
+    for (int64_t e = 0; e < n_ent; e++) {
+        const auto pr = split_one(rec, ents + 4 * e, part_cap, max_part_rec);
+        nparts[e] = (int32_t)pr.size();
+        nrecs[e] = pr.empty() ? 0 : ents[4 * e + 2];
+        tot += nparts[e];
+    }
+    return tot;
+}
+
+void bsdc_split_fill(const uint32_t *rec, const uint32_t *ents, int64_t n_ent, int64_t part_cap, int32_t max_part_rec,
+                     const int64_t *first_part, const int64_t *first_rec, uint32_t *parts, uint32_t *part_recs,
+                     int32_t n_threads) {
+#ifdef _OPENMP
+    if (n_threads > 0) omp_set_num_threads(n_threads);
+#endif
+#pragma omp parallel for schedule(dynamic, 4)
+    for (int64_t e = 0; e < n_ent; e++) {
+        const uint32_t *en = ents + 4 * e;
+        const auto pr = split_one(rec, en, part_cap, max_part_rec);
+        const int64_t r0 = en[1];
+        int64_t pk = first_rec[e];
+        for (size_t j = 0; j < pr.size(); j++) {
+            uint32_t *o = parts + 4 * (first_part[e] + (int64_t)j);
+            o[0] = en[0];
+            o[1] = (uint32_t)pk;
+            o[2] = (uint32_t)pr[j].recs.size();
+            o[3] = (uint32_t)pr[j].img;
+            uint32_t dst = 0;
+            for (size_t q = 0; q < pr[j].recs.size(); q++, pk++) {
+                const int64_t gi = r0 + pr[j].recs[q];
+                uint32_t *w = part_recs + 4 * pk;
+                w[0] = (uint32_t)gi;
+                w[1] = dst;
+                w[2] = (uint32_t)pr[j].lmate[q];
+                w[3] = 0;
+                dst += (uint32_t)(((rec[4 * gi + 2] & 0xFFFF) + 2 + 3) & ~3u);
+            }
+        }
+    }
+}
+
+}  // extern "C"

@@ -1672,18 +1672,104 @@ __device__ __forceinline__ void block_sum_max(int a, int b, int *red, int &sum, 
     }
 }
 
+// Duplex combine and output of one family from its single-strand rows (LDS, [4][ssw] bases
+// ssb / quals ssq, lengths lcv, reads cnt): R1 = AB-R1 (+) BA-R2, R2 = AB-R2 (+) BA-R1, a strand
+// present on one side passing through; with TAGS the single-strand rows and lengths of the
+// consensus tags (their depth / errors went out with the calls); status and lengths.
 template <int G, bool TAGS>
+__device__ void large_emit(const KParams &P, uint32_t fam, const int *cnt, const int *lcv, const uint8_t *ssb,
+                           const uint8_t *ssq, int ssw, bool tag_rows) {
+    const int tt = threadIdx.x;
+    bool hs[4];
+    for (int s = 0; s < 4; s++) hs[s] = cnt[s] > 0 && lcv[s] > 0;
+    const bool emit = (hs[0] || hs[3]) && (hs[1] || hs[2]);
+    const int32_t stride = P.O.stride;
+    int olen[2];
+    for (int e = 0; e < 2; e++) {
+        const int sa = e == 0 ? 0 : 1, sb2 = e == 0 ? 3 : 2;
+        olen[e] = (hs[sa] && hs[sb2]) ? ::min(lcv[sa], lcv[sb2]) : hs[sa] ? lcv[sa] : hs[sb2] ? lcv[sb2] : 0;
+    }
+    if (emit) {
+        for (int e = 0; e < 2; e++) {
+            const int sa = e == 0 ? 0 : 1, sb2 = e == 0 ? 3 : 2;
+            const int64_t so = (2 * (int64_t)fam + e) * stride;
+            const int npair = (olen[e] + 1) >> 1;
+            for (int k = tt; k < npair; k += G) {
+                uint32_t ob[2] = {0, 0}, oq[2] = {0, 0};
+                for (int h = 0; h < 2; h++) {
+                    const int col = 2 * k + h;
+                    if (col >= olen[e]) break;
+                    if (hs[sa] && hs[sb2]) {
+                        duplex_col(ssb[sa * ssw + col], ssq[sa * ssw + col], ssb[sb2 * ssw + col], ssq[sb2 * ssw + col],
+                                   ob[h], oq[h]);
+                    } else {
+                        const int s1 = hs[sa] ? sa : sb2;
+                        ob[h] = ssb[s1 * ssw + col];
+                        oq[h] = ssq[s1 * ssw + col];
+                    }
+                }
+                P.O.seq[so / 2 + k] = (uint8_t)((ob[0] << 4) | ob[1]);
+                P.O.qual[so + 2 * k] = (uint8_t)oq[0];
+                if (2 * k + 1 < olen[e]) P.O.qual[so + 2 * k + 1] = (uint8_t)oq[1];
+            }
+        }
+    }
+    if (TAGS && tag_rows) {
+        for (int s = 0; s < 4; s++) {
+            const int ls = hs[s] ? lcv[s] : 0;
+            const int64_t row = (4 * (int64_t)fam + s) * stride;
+            for (int c = tt; c < ls; c += G) {
+                P.O.ss_base[row + c] = ssb[s * ssw + c];
+                P.O.ss_qual[row + c] = ssq[s * ssw + c];
+            }
+        }
+        if (tt < 4) P.O.ss_len[4 * fam + tt] = (uint16_t)(hs[tt] ? lcv[tt] : 0);
+    }
+    if (tt == 0) {
+        uint8_t st = emit ? 1 : 0;
+        if (hs[0] || hs[1]) st |= 2;
+        if (hs[2] || hs[3]) st |= 4;
+        P.O.status[fam] = st;
+        P.O.len[2 * fam] = (uint16_t)(emit ? olen[0] : 0);
+        P.O.len[2 * fam + 1] = (uint16_t)(emit ? olen[1] : 0);
+    }
+}
+
+// The parts' sums in scratch (include/bsdc.h split_partial_off): header [part][8] int32 (set
+// reads, set lengths), then int32x4 likelihood sums and u8x4 A/C/G/T read counts per (part, set,
+// column), the column pitch being the output stride.
+struct PartSums {
+    int32_t *head;
+    uint4 *sum;
+    uint32_t *cnt;
+    int32_t pitch;
+    __device__ __forceinline__ PartSums(const KParams &P) {
+        uint8_t *b = P.O.scratch + P.B.split_partial_off;
+        const int64_t np = P.B.n_split_parts;
+        pitch = P.O.stride;
+        head = reinterpret_cast<int32_t *>(b);
+        sum = reinterpret_cast<uint4 *>(b + round16(32 * np));
+        cnt = reinterpret_cast<uint32_t *>(b + round16(32 * np) + 16 * 4 * np * (int64_t)pitch);
+    }
+    __device__ __forceinline__ int64_t at(int64_t part, int s, int col) const { return (4 * part + s) * (int64_t)pitch + col; }
+};
+
+// PART: the entry is one part of a split family (include/bsdc.h split_parts): everything up to
+// the vote as for a family, then the part's per-column sums and counts go to scratch (PartSums)
+// instead of the calls; k_join adds the parts up.
+template <int G, bool TAGS, bool PART = false>
 __device__ void process_large(const KParams &P, uint8_t *A, uint8_t *s_tab, const int32_t *lr, const float *thr, uint4 ent,
                               int *red, int *s_cnt, int *s_lc, int *s_cur) {
     const int tt = threadIdx.x;
     const bsdc_family_batch &B = P.B;
-    const uint32_t fam = ent.x, r0 = ent.y, img = ent.w;  // list entry: family, first record, n, image bytes
+    // list entry: family, first record (a part: its first part record), n, image bytes
+    const uint32_t fam = ent.x, r0 = ent.y, img = ent.w;
     const int n = (int)ent.z;
     const bool do_convert = P.mode & BSDC_MODE_CONVERT;
     const bool do_extend = P.mode & BSDC_MODE_EXTEND;
     const bool do_vote = P.mode & BSDC_MODE_VOTE;
     const uint4 *REC = reinterpret_cast<const uint4 *>(B.rec);
-    const uint32_t off0 = n > 0 ? REC[r0].x : 0u;
+    const uint32_t off0 = n > 0 && !PART ? REC[r0].x : 0u;
     const int stop = (P.mode >> BSDC_MODE_STOP_SHIFT) & 15;  // profiling ablation (0 = full kernel)
 
     // ---- one round of global loads for everything the family needs first: the tables (s_cnt[0]
@@ -1698,7 +1784,9 @@ __device__ void process_large(const KParams &P, uint8_t *A, uint8_t *s_tab, cons
     RecMeta *M = reinterpret_cast<RecMeta *>(A + L0.meta);
     uint16_t *clist = reinterpret_cast<uint16_t *>(A + L0.clist);  // the converted records
     uint32_t qor = 0;  // OR of the family's quals: a byte >= 128 keeps the overlap off the SWAR path
-    const int nqc = (int)(img >> 4), nch = nqc + (int)(img >> 5);  // 16-B chunks: quals, then packed bases
+    // 16-B chunks: quals, then packed bases (a part copies its records' slots one by one instead)
+    const int nqc = PART ? 0 : (int)(img >> 4), nch = PART ? 0 : nqc + (int)(img >> 5);
+    const uint4 *PR = reinterpret_cast<const uint4 *>(B.split_part_recs);  // (PART) batch record, slot, mate
     auto load_chunk = [&](int k) {
         const uint8_t *src = k < nqc ? B.qual + off0 + 16 * (uint32_t)k : B.seq + (off0 >> 1) + 16 * (uint32_t)(k - nqc);
         return *reinterpret_cast<const uint4 *>(src);
@@ -1719,7 +1807,8 @@ __device__ void process_large(const KParams &P, uint8_t *A, uint8_t *s_tab, cons
     if (tt < kTabBytesL / 16) tv = reinterpret_cast<const uint4 *>(&P.tab->t)[tt];
     int c = 0, ml = 0;
     for (int r = tt; r < n; r += G) {
-        const uint32_t gi = r0 + r;
+        const uint4 pr = PART ? PR[r0 + r] : make_uint4(0, 0, 0, 0);
+        const uint32_t gi = PART ? pr.x : r0 + r;
         const uint4 rc = REC[gi];
         const uint32_t ci = B.cig_info[gi];
         const uint2 wn = reinterpret_cast<const uint2 *>(B.rec_win)[gi];
@@ -1729,9 +1818,9 @@ __device__ void process_large(const KParams &P, uint8_t *A, uint8_t *s_tab, cons
         m.pos = (int32_t)rc.y;
         m.len = m.in_len;
 
-        m.slot = rc.x - off0;
+        m.slot = PART ? pr.y : rc.x - off0;
         m.start = 1;
-        m.link = rc.w;
+        m.link = PART ? (rc.w & ~(uint32_t)BSDC_LINK_MATE_MASK) | pr.z : rc.w;  // (a part: its local mate)
         m.gidx = gi;
         const bool conv = do_convert && (m.link & BSDC_LINK_CONVERT);
         m.win = conv ? wn.x : 0u;
@@ -1750,6 +1839,34 @@ __device__ void process_large(const KParams &P, uint8_t *A, uint8_t *s_tab, cons
     for (int u = 0; u < kLStageU; u++)
         if (tt + u * G < nch) store_chunk(tt + u * G, v[u]);
     if (tt < kTabBytesL / 16) reinterpret_cast<uint4 *>(s_tab)[tt] = tv;
+    if (PART) {  // the part's records' slots, flattened over (record, 4 entries): U units per record
+        const int U = (B.max_len + 2 + 3) >> 2;
+        constexpr int PU = 4;  // units in flight per thread
+        for (int k0 = tt; k0 < n * U; k0 += PU * G) {
+            uint32_t q[PU], bb[PU], dst[PU];
+#pragma unroll
+            for (int u = 0; u < PU; u++) {
+                const int k = k0 + u * G;
+                dst[u] = 0xFFFFFFFFu;
+                if (k >= n * U) continue;
+                const int r = k / U, j = k - r * U;
+                const uint4 pr = PR[r0 + r];
+                const uint4 rc = REC[pr.x];
+                if (4 * j >= (int)(((rc.z & 0xFFFF) + 2 + 3) & ~3u)) continue;
+                q[u] = *reinterpret_cast<const uint32_t *>(B.qual + rc.x + 4 * j);
+                bb[u] = *reinterpret_cast<const uint16_t *>(B.seq + (rc.x >> 1) + 2 * j);
+                dst[u] = pr.y + 4 * (uint32_t)j;
+            }
+#pragma unroll
+            for (int u = 0; u < PU; u++) {
+                if (dst[u] == 0xFFFFFFFFu) continue;
+                st32(qimg + dst[u], q[u]);
+                qor |= q[u];
+                const uint32_t x = bb[u];  // two packed bytes, high nibble first -> four base bytes
+                st32(slots + dst[u], ((x >> 4) & 0xFu) | ((x & 0xFu) << 8) | ((x >> 12) << 16) | (((x >> 8) & 0xFu) << 24));
+            }
+        }
+    }
     for (int k0 = tt + kLStageU * G; k0 < nch; k0 += kLStageU * G) {  // families of more chunks
 #pragma unroll
         for (int u = 0; u < kLStageU; u++)
@@ -2182,6 +2299,13 @@ __device__ void process_large(const KParams &P, uint8_t *A, uint8_t *s_tab, cons
             P.O.ss_err[at] = (uint16_t)::min(depth - nb, 32767u);
         }
     };
+    // PART: a multi-base column's per-base sums (int32: a part holds < 255 reads a set) and counts
+    auto part_write = [&](int s, int col, long long D0, long long D1, long long D2, long long D3, uint32_t n01, uint32_t n23) {
+        const PartSums ps(P);
+        ps.sum[ps.at(blockIdx.x, s, col)] = make_uint4((uint32_t)(int32_t)D0, (uint32_t)(int32_t)D1, (uint32_t)(int32_t)D2,
+                                                       (uint32_t)(int32_t)D3);
+        ps.cnt[ps.at(blockIdx.x, s, col)] = (n01 & 0xFFu) | ((n01 >> 8) & 0xFF00u) | ((n23 & 0xFFu) << 16) | ((n23 >> 16) << 24);
+    };
     // Wavefronts by set: wave w works on set w % 4; with 8 waves (512 threads) the two waves of a
     // set split its reads (PARTS = 2).
     // Pass A: a lane owns 4 columns and walks the wave's reads, forward ones then reverse ones,
@@ -2222,7 +2346,7 @@ __device__ void process_large(const KParams &P, uint8_t *A, uint8_t *s_tab, cons
                     const uint32_t v = onehot01(b);
                     orm |= b & (v * 0xFFu);
                     lookup4v(lr2, v, q, t0, t1, t2, t3);
-                    if (TAGS) c4 += v;
+                    if (TAGS || PART) c4 += v;
                 };
                 auto rev = [&](uint32_t ex, uint32_t ey) {  // bytes run backwards from the read's last base
                     const int sl = (int)(ey & 0x7FFFFFFFu);
@@ -2233,7 +2357,7 @@ __device__ void process_large(const KParams &P, uint8_t *A, uint8_t *s_tab, cons
                     const uint32_t v = onehot01(b);
                     orm |= b & (v * 0xFFu);
                     lookup4v(lr2, v, q, t0, t1, t2, t3);
-                    if (TAGS) c4 += v;
+                    if (TAGS || PART) c4 += v;
                 };
                 auto flush = [&]() {  // int32 partials over <= 64 reads: exact
                     T0 += t0;
@@ -2241,7 +2365,7 @@ __device__ void process_large(const KParams &P, uint8_t *A, uint8_t *s_tab, cons
                     T2 += t2;
                     T3 += t3;
                     t0 = t1 = t2 = t3 = 0;
-                    if (TAGS) {
+                    if (TAGS || PART) {
                         cn01 += __builtin_amdgcn_perm(0u, c4, 0x0c010c00u);
                         cn23 += __builtin_amdgcn_perm(0u, c4, 0x0c030c02u);
                         c4 = 0;
@@ -2278,7 +2402,7 @@ __device__ void process_large(const KParams &P, uint8_t *A, uint8_t *s_tab, cons
                         if (c + j < lc) {
                             psum[ws * ssw + c + j] = j == 0 ? T0 : j == 1 ? T1 : j == 2 ? T2 : T3;
                             por[ws * ssw + c + j] = (uint8_t)(orm >> (8 * j));
-                            if (TAGS) pcn[ws * ssw + c + j] = (uint16_t)((j < 2 ? cn01 : cn23) >> (16 * (j & 1)));
+                            if (TAGS || PART) pcn[ws * ssw + c + j] = (uint16_t)((j < 2 ? cn01 : cn23) >> (16 * (j & 1)));
                         }
                 }
                 __syncthreads();
@@ -2290,13 +2414,25 @@ __device__ void process_large(const KParams &P, uint8_t *A, uint8_t *s_tab, cons
                     if (col >= lc) break;
                     uint32_t ob = (orm >> (8 * j)) & 0xFFu;
                     long long Tj = j == 0 ? T0 : j == 1 ? T1 : j == 2 ? T2 : T3;
-                    uint32_t nj = TAGS ? ((j < 2 ? cn01 : cn23) >> (16 * (j & 1))) & 0xFFFFu : 0u;
+                    uint32_t nj = (TAGS || PART) ? ((j < 2 ? cn01 : cn23) >> (16 * (j & 1))) & 0xFFFFu : 0u;
                     if (PARTS == 2) {
                         Tj += psum[ws * ssw + col];
                         ob |= por[ws * ssw + col];
-                        if (TAGS) nj += pcn[ws * ssw + col];
+                        if (TAGS || PART) nj += pcn[ws * ssw + col];
                     }
-                    if (ob != 0 && (ob & (ob - 1)) == 0 && Tj > na) {
+                    if (PART) {  // one base (or none) seen: the part's sums are that base's; else pass B
+                        if ((ob & (ob - 1)) == 0) {
+                            const PartSums ps(P);
+                            const int bi = ob ? __builtin_ctz(ob) : 0;
+                            const int32_t T = ob ? (int32_t)Tj : 0;
+                            ps.sum[ps.at(blockIdx.x, ws, col)] =
+                                make_uint4(bi == 0 ? T : 0, bi == 1 ? T : 0, bi == 2 ? T : 0, bi == 3 ? T : 0);
+                            ps.cnt[ps.at(blockIdx.x, ws, col)] = ob ? nj << (8 * bi) : 0u;
+                            ssq[ws * ssw + col] = 1;
+                        } else {
+                            ssq[ws * ssw + col] = 0;
+                        }
+                    } else if (ob != 0 && (ob & (ob - 1)) == 0 && Tj > na) {
                         const float e = term(-Tj);
                         const float S = ((0.0f + e) + e) + e;
                         const int Q = phred_of(S, thr);
@@ -2374,7 +2510,7 @@ __device__ void process_large(const KParams &P, uint8_t *A, uint8_t *s_tab, cons
                 d1 += bb == kC ? v : 0;
                 d2 += bb == kG ? v : 0;
                 d3 += bb == kT ? v : 0;
-                if (TAGS && in) {
+                if ((TAGS || PART) && in) {
                     n01 += bb == kA ? 1u : bb == kC ? 0x10000u : 0u;
                     n23 += bb == kG ? 1u : bb == kT ? 0x10000u : 0u;
                 }
@@ -2407,7 +2543,7 @@ __device__ void process_large(const KParams &P, uint8_t *A, uint8_t *s_tab, cons
                 add_up(D1);
                 add_up(D2);
                 add_up(D3);
-                if (TAGS) {
+                if (TAGS || PART) {
                     n01 += (uint32_t)__shfl_xor((int)n01, 32, kWave);
                     n23 += (uint32_t)__shfl_xor((int)n23, 32, kWave);
                 }
@@ -2434,79 +2570,37 @@ __device__ void process_large(const KParams &P, uint8_t *A, uint8_t *s_tab, cons
                     pw[1] = (int32_t)D1;
                     pw[2] = (int32_t)D2;
                     pw[3] = (int32_t)D3;
-                    if (TAGS) {
+                    if (TAGS || PART) {
                         pw[4] = (int32_t)n01;
                         pw[5] = (int32_t)n23;
                     }
                 }
                 __syncthreads();
-                if (wpart == 0 && act)
-                    resolve(s, col, D0 + pw[0], D1 + pw[1], D2 + pw[2], D3 + pw[3], TAGS ? n01 + (uint32_t)pw[4] : 0u,
-                            TAGS ? n23 + (uint32_t)pw[5] : 0u);
+                if (wpart == 0 && act) {
+                    if (PART)
+                        part_write(s, col, D0 + pw[0], D1 + pw[1], D2 + pw[2], D3 + pw[3], n01 + (uint32_t)pw[4], n23 + (uint32_t)pw[5]);
+                    else
+                        resolve(s, col, D0 + pw[0], D1 + pw[1], D2 + pw[2], D3 + pw[3], TAGS ? n01 + (uint32_t)pw[4] : 0u,
+                                TAGS ? n23 + (uint32_t)pw[5] : 0u);
+                }
                 __syncthreads();
             } else if (act) {
-                resolve(s, col, D0, D1, D2, D3, n01, n23);
+                if (PART)
+                    part_write(s, col, D0, D1, D2, D3, n01, n23);
+                else
+                    resolve(s, col, D0, D1, D2, D3, n01, n23);
             }
         }
     }
     __syncthreads();
     if (stop == 7) return;
+    if (PART) {  // the part's set sizes and lengths; k_join does the rest
+        if (tt < 8) PartSums(P).head[8 * (int64_t)blockIdx.x + tt] = tt < 4 ? cnt[tt] : lcv[tt - 4];
+        return;
+    }
 
     // ---- duplex combine and output ----
-    bool hs[4];
-    for (int s = 0; s < 4; s++) hs[s] = cnt[s] > 0 && lcv[s] > 0;
-    const bool emit = (hs[0] || hs[3]) && (hs[1] || hs[2]);
-    const int32_t stride = P.O.stride;
-    int olen[2];
-    for (int e = 0; e < 2; e++) {
-        const int sa = e == 0 ? 0 : 1, sb2 = e == 0 ? 3 : 2;
-        olen[e] = (hs[sa] && hs[sb2]) ? ::min(lcv[sa], lcv[sb2]) : hs[sa] ? lcv[sa] : hs[sb2] ? lcv[sb2] : 0;
-    }
-    if (emit) {
-        for (int e = 0; e < 2; e++) {
-            const int sa = e == 0 ? 0 : 1, sb2 = e == 0 ? 3 : 2;
-            const int64_t so = (2 * (int64_t)fam + e) * stride;
-            const int npair = (olen[e] + 1) >> 1;
-            for (int k = tt; k < npair; k += G) {
-                uint32_t ob[2] = {0, 0}, oq[2] = {0, 0};
-                for (int h = 0; h < 2; h++) {
-                    const int col = 2 * k + h;
-                    if (col >= olen[e]) break;
-                    if (hs[sa] && hs[sb2]) {
-                        duplex_col(ssb[sa * ssw + col], ssq[sa * ssw + col], ssb[sb2 * ssw + col], ssq[sb2 * ssw + col],
-                                   ob[h], oq[h]);
-                    } else {
-                        const int s1 = hs[sa] ? sa : sb2;
-                        ob[h] = ssb[s1 * ssw + col];
-                        oq[h] = ssq[s1 * ssw + col];
-                    }
-                }
-                P.O.seq[so / 2 + k] = (uint8_t)((ob[0] << 4) | ob[1]);
-                P.O.qual[so + 2 * k] = (uint8_t)oq[0];
-                if (2 * k + 1 < olen[e]) P.O.qual[so + 2 * k + 1] = (uint8_t)oq[1];
-            }
-        }
-    }
-    if (TAGS && stop == 0) {  // the single-strand reads of the consensus tags (the vote's rows; depth /
-        // errors went out with the calls)
-        for (int s = 0; s < 4; s++) {
-            const int ls = hs[s] ? lcv[s] : 0;
-            const int64_t row = (4 * (int64_t)fam + s) * stride;
-            for (int c = tt; c < ls; c += G) {
-                P.O.ss_base[row + c] = ssb[s * ssw + c];
-                P.O.ss_qual[row + c] = ssq[s * ssw + c];
-            }
-        }
-        if (tt < 4) P.O.ss_len[4 * fam + tt] = (uint16_t)(hs[tt] ? lcv[tt] : 0);
-    }
-    if (tt == 0) {
-        uint8_t st = emit ? 1 : 0;
-        if (hs[0] || hs[1]) st |= 2;
-        if (hs[2] || hs[3]) st |= 4;
-        P.O.status[fam] = st;
-        P.O.len[2 * fam] = (uint16_t)(emit ? olen[0] : 0);
-        P.O.len[2 * fam + 1] = (uint16_t)(emit ? olen[1] : 0);
-    }
+    large_emit<G, TAGS>(P, fam, cnt, lcv, ssb, ssq, ssw, stop == 0);
 }
 
 static_assert(BSDC_LARGE_LDS_MAX + kTabBytesL + 256 <= kLdsBytes, "large-family LDS budget");
@@ -2519,7 +2613,7 @@ struct TablesL {  // k_large's LDS copy: the prefix of Tables it reads
 static_assert(sizeof(TablesL) == kTabBytesL, "TablesL image");
 // G = 256 threads for the buckets that fit 3 or more workgroups per CU, 512 for the LDS-heavy ones
 // (2 or 1 per CU, HBM scratch): twice the wavefronts in flight for the same LDS.
-template <bool IN_LDS, int G, bool TAGS>
+template <bool IN_LDS, int G, bool TAGS, bool PART = false>
 __global__ __launch_bounds__(G, G == 256 ? 5 : 2) void k_large(KParams P, const uint4 *fams, int64_t nfams, int32_t arena,
                                                                 int64_t scratch_off) {
     extern __shared__ __attribute__((aligned(16))) uint8_t smem[];  // the family's arena (IN_LDS)
@@ -2539,7 +2633,102 @@ __global__ __launch_bounds__(G, G == 256 ? 5 : 2) void k_large(KParams P, const 
     if (threadIdx.x == 0) s_cnt[0] = 0;  // the converted-record count (process_large's first phase)
     __syncthreads();
     uint8_t *A = IN_LDS ? smem : P.O.scratch + scratch_off + (size_t)i * (size_t)arena;
-    process_large<G, TAGS>(P, A, reinterpret_cast<uint8_t *>(&s_tab), lr, thr, fams[i], red, s_cnt, s_lc, s_cur);
+    process_large<G, TAGS, PART>(P, A, reinterpret_cast<uint8_t *>(&s_tab), lr, thr, fams[i], red, s_cnt, s_lc, s_cur);
+}
+
+// One workgroup per split family (include/bsdc.h): the parts' sums and counts added up per
+// (set, column) -- exact integers, so the parts' order does not matter --, the single-strand call
+// of each column (as k_large's resolve), then duplex combine and output (large_emit).  A near-tie
+// column needs fgbio's read-order double sums over all the set's reads, which the parts did not
+// keep: then the family runs whole in its HBM fallback arena (process_large), as the HBM bucket does.
+template <bool TAGS>
+__global__ __launch_bounds__(kLargeThreadsBig, 2) void k_join(KParams P, const uint4 *sfams, int64_t nsf) {
+    constexpr int G = kLargeThreadsBig;
+    extern __shared__ __attribute__((aligned(16))) uint8_t smem[];  // single-strand rows: bases, quals [4][stride]
+    __shared__ __attribute__((aligned(16))) TablesL s_tab;
+    __shared__ int red[2 * G / kWave];
+    __shared__ int s_cnt[4], s_lc[4], s_cur[8];
+    __shared__ int s_tie;
+    const int tt = threadIdx.x;
+    const int64_t i = blockIdx.x;
+    if (i >= nsf) return;
+    const uint4 e0 = sfams[2 * i], e1 = sfams[2 * i + 1];  // the family's entry; first part, parts, fallback arena
+    load_tables<kTabBytesL>(&P.tab->t, reinterpret_cast<uint8_t *>(&s_tab));
+    const PartSums ps(P);
+    const int64_t p0 = e1.x;
+    const int np = (int)e1.y;
+    if (tt < 4) {
+        int c = 0, l = 0;
+        for (int p = 0; p < np; p++) {
+            c += ps.head[8 * (p0 + p) + tt];
+            l = ::max(l, ps.head[8 * (p0 + p) + 4 + tt]);
+        }
+        s_cnt[tt] = c;
+        s_lc[tt] = c > 0 ? l : 0;
+    }
+    if (tt == 0) s_tie = 0;
+    __syncthreads();
+    int cnt[4], lcv[4];
+    for (int s = 0; s < 4; s++) {
+        cnt[s] = s_cnt[s];
+        lcv[s] = s_lc[s];
+    }
+    const int pitch = P.O.stride;
+    uint8_t *ssb = smem, *ssq = smem + 4 * pitch;
+    const int ntot = lcv[0] + lcv[1] + lcv[2] + lcv[3];
+    for (int k = tt; k < ntot; k += G) {
+        int s = 0, c = k;
+        while (c >= lcv[s]) {
+            c -= lcv[s];
+            s++;
+        }
+        long long D0 = 0, D1 = 0, D2 = 0, D3 = 0;
+        uint32_t n0 = 0, n1 = 0, n2 = 0, n3 = 0;
+        for (int p = 0; p < np; p++) {
+            if (c >= ps.head[8 * (p0 + p) + 4 + s]) continue;  // (the part's set ends before c: nothing written)
+            const uint4 d = ps.sum[ps.at(p0 + p, s, c)];
+            const uint32_t m = ps.cnt[ps.at(p0 + p, s, c)];
+            D0 += (int32_t)d.x;
+            D1 += (int32_t)d.y;
+            D2 += (int32_t)d.z;
+            D3 += (int32_t)d.w;
+            n0 += m & 0xFFu;
+            n1 += (m >> 8) & 0xFFu;
+            n2 += (m >> 16) & 0xFFu;
+            n3 += m >> 24;
+        }
+        const int best = first_max4(D0, D1, D2, D3);
+        if (near_tie(D0, D1, D2, D3, best, cnt[s])) {
+            s_tie = 1;
+            continue;
+        }
+        const long long Db = best == 0 ? D0 : best == 1 ? D1 : best == 2 ? D2 : D3;
+        float S = 0.0f;
+        if (best != 0) S += term(D0 - Db);
+        if (best != 1) S += term(D1 - Db);
+        if (best != 2) S += term(D2 - Db);
+        if (best != 3) S += term(D3 - Db);
+        const int Q = phred_of(S, s_tab.thr);
+        const uint32_t depth = n0 + n1 + n2 + n3;
+        const bool nocall = depth == 0 || Q < P.qmin;
+        ssb[s * pitch + c] = nocall ? (uint8_t)kN : (uint8_t)(1u << best);
+        ssq[s * pitch + c] = nocall ? (uint8_t)2 : (uint8_t)Q;
+        if (TAGS) {
+            const uint32_t nb = best == 0 ? n0 : best == 1 ? n1 : best == 2 ? n2 : n3;
+            const int64_t at = (4 * (int64_t)e0.x + s) * pitch + c;
+            P.O.ss_depth[at] = (uint16_t)::min(depth, 32767u);
+            P.O.ss_err[at] = (uint16_t)::min(depth - nb, 32767u);
+        }
+    }
+    __syncthreads();
+    if (s_tie) {  // (rare) the whole family in its HBM arena, fgbio's pick on the near ties
+        if (tt == 0) s_cnt[0] = 0;
+        __syncthreads();
+        process_large<G, TAGS, false>(P, P.O.scratch + 16 * (int64_t)e1.z, reinterpret_cast<uint8_t *>(&s_tab), s_tab.lr,
+                                      s_tab.thr, e0, red, s_cnt, s_lc, s_cur);
+        return;
+    }
+    large_emit<G, TAGS>(P, e0.x, cnt, lcv, ssb, ssq, pitch, true);
 }
 
 }  // namespace
@@ -2825,6 +3014,11 @@ int32_t bsdc_run(bsdc_ctx *c, const bsdc_family_batch *b, bsdc_consensus *o, int
         c->err = "bad stride";
         return BSDC_EINVAL;
     }
+    if (b->n_split_parts > 0 && (b->split_part_arena % 16 || b->split_part_arena <= 0 ||
+                                 b->split_part_arena > BSDC_LARGE_LDS_MAX || !o->scratch || !b->split_parts || !b->split_fams)) {
+        c->err = "bad split families";
+        return BSDC_EINVAL;
+    }
     for (int q = 0; q < BSDC_LARGE_BUCKETS; q++) {
         if (b->n_large[q] > 0 && (b->large_arena[q] % 16 || b->large_arena[q] <= 0)) {
             c->err = "bad large arena size";
@@ -2962,6 +3156,31 @@ int32_t bsdc_run(bsdc_ctx *c, const bsdc_family_batch *b, bsdc_consensus *o, int
                 if (e != hipSuccess) fail(e, "k_large launch");
             }
             f += nf;
+        }
+        // split families: their parts (k_large part mode, LDS arenas, 256 threads), then one join
+        // workgroup per family, in order on one stream
+        if (rc == 0 && b->n_split_parts > 0 && b->n_split_fams > 0) {
+            const int32_t a = b->split_part_arena;
+            const bool tg = (mode & BSDC_MODE_TAGS) != 0;
+            const hipStream_t ls = next_stream();
+            if (rc == 0) {
+                const uint4 *pf = reinterpret_cast<const uint4 *>(b->split_parts);
+                const uint4 *sf = reinterpret_cast<const uint4 *>(b->split_fams);
+                const size_t jl = 8 * (size_t)o->stride;
+                if (tg) {
+                    hipLaunchKernelGGL((k_large<true, kLargeThreads, true, true>), dim3((unsigned)b->n_split_parts), dim3(kLargeThreads),
+                                       (size_t)a, ls, P, pf, b->n_split_parts, a, (int64_t)0);
+                    hipLaunchKernelGGL((k_join<true>), dim3((unsigned)b->n_split_fams), dim3(kLargeThreadsBig), jl, ls, P, sf,
+                                       b->n_split_fams);
+                } else {
+                    hipLaunchKernelGGL((k_large<true, kLargeThreads, false, true>), dim3((unsigned)b->n_split_parts),
+                                       dim3(kLargeThreads), (size_t)a, ls, P, pf, b->n_split_parts, a, (int64_t)0);
+                    hipLaunchKernelGGL((k_join<false>), dim3((unsigned)b->n_split_fams), dim3(kLargeThreadsBig), jl, ls, P, sf,
+                                       b->n_split_fams);
+                }
+                const hipError_t e = hipGetLastError();
+                if (e != hipSuccess) fail(e, "split launch");
+            }
         }
     }
     // join: `s` waits for every side stream used -- also after a failed launch, so that no work

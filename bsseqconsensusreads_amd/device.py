@@ -90,18 +90,21 @@ class DeviceBatch:
             self.ss_qual = torch.zeros(nss, dtype=torch.uint8, device=device)
             self.ss_depth = torch.zeros(nss, dtype=torch.int16, device=device)
             self.ss_err = torch.zeros(nss, dtype=torch.int16, device=device)
-        # HBM arenas of the large buckets beyond the LDS budget, one region per bucket (the bucket
-        # dispatches run concurrently on the library's side streams); + slack: dword reads may run
-        # a few bytes past the last arena (their bytes are masked)
-        need = sum(int(b.shape[0]) * a for b, a in zip(fb.large_buckets, fb.large_arenas)
-                   if b.shape[0] and a > LARGE_LDS_MAX)
-        self.scratch = torch.zeros(need + 256, dtype=torch.uint8, device=device) if need else None
+        # HBM scratch: arenas of the large buckets beyond the LDS budget, one region per bucket (the
+        # bucket dispatches run concurrently on the library's side streams), the split families'
+        # fallback arenas and their parts' sums (FamilyBatch.scratch_layout; + slack: dword reads
+        # may run a few bytes past the last arena, their bytes masked).  Every byte a kernel reads
+        # there it wrote first: no zero fill
+        need, _, poff = fb.scratch_layout()
+        self.scratch = torch.empty(need, dtype=torch.uint8, device=device) if need else None
         self._b = _lib.FamilyBatchC()
         b = self._b
         b.n_rec, b.n_fam = Rn, F
         for k in ("fam_off", "rec", "rec_win", "cig_off", "cig_info", "cigar", "rt", "seq", "qual",
-                  "small_fams", "large_fams"):
+                  "small_fams", "large_fams", "split_parts", "split_part_recs", "split_fams"):
             setattr(b, k, _dptr(self.t[k]))
+        b.n_split_parts, b.n_split_fams = int(fb.split_parts.shape[0]), int(fb.split_fams.shape[0])
+        b.split_part_arena, b.split_partial_off = int(fb.split_part_arena), int(poff)
         for q in range(_lib.SMALL_BUCKETS):
             b.n_small[q] = int(fb.small_buckets[q].shape[0])
             b.small_arena[q] = int(fb.small_arenas[q])

@@ -77,6 +77,12 @@ def _load():
     lib.bsdc_batch_free.argtypes = [_P]
     lib.bsdc_host_last_error.restype = C.c_char_p
     lib.bsdc_host_error_record.restype = C.c_int64
+    lib.bsdc_split_count.argtypes = [C.c_void_p, C.c_void_p, C.c_int64, C.c_int64, C.c_int32, C.c_void_p, C.c_void_p,
+                                     C.c_int32]
+    lib.bsdc_split_count.restype = C.c_int64
+    lib.bsdc_split_fill.argtypes = [C.c_void_p, C.c_void_p, C.c_int64, C.c_int64, C.c_int32, C.c_void_p, C.c_void_p,
+                                    C.c_void_p, C.c_void_p, C.c_int32]
+    lib.bsdc_split_fill.restype = None
     _lib = lib
     return lib
 

@@ -26,7 +26,7 @@
 extern "C" {
 #endif
 
-#define BSDC_ABI_VERSION 10
+#define BSDC_ABI_VERSION 11
 #define BSDC_SMALL_BUCKETS 8
 #define BSDC_LARGE_BUCKETS 6
 #define BSDC_LARGE_LDS_MAX 158912 /* LDS arena bytes one large-family workgroup may use */ /* LDS arena size classes of the wavefront-per-family kernel */
@@ -94,6 +94,21 @@ typedef struct {
     int32_t large_arena[BSDC_LARGE_BUCKETS];  /* bytes per workgroup of each bucket (multiple of 16); a
                                                  bucket beyond BSDC_LARGE_LDS_MAX keeps its arenas in `scratch` */
     int32_t max_len;             /* max record length */
+    int32_t split_part_arena;    /* LDS bytes per part workgroup (256 threads) */
+    /* Part mode (k_large): a family beyond the LDS buckets whose records hold no complex cigar and
+     * no tool-2 role is cut into parts of whole templates that each fit split_part_arena; a part
+     * runs everything up to the vote in LDS and leaves its per-column likelihood sums and read
+     * counts in `scratch`; one workgroup per family then adds the parts up, calls, combines and
+     * writes (a near-tie column -- rare -- makes that family run whole in its HBM arena instead). */
+    const uint32_t *split_parts; /* 4 words per part: family, first part record, n_rec, image bytes */
+    int64_t n_split_parts;
+    const uint32_t *split_part_recs; /* 4 words per part record: batch record, slot in the part's image,
+                                        part-local index of its mate (0xFFFF: none), 0 */
+    const uint32_t *split_fams;  /* 8 words per family: family, first record, n_rec, image bytes, first part,
+                                    parts, fallback arena offset in scratch / 16, fallback arena bytes */
+    int64_t n_split_fams;
+    int64_t split_partial_off;   /* scratch offset of the parts' sums: [part][8] int32 (set reads, set
+                                    lengths), then [part][4][stride] int32x4 sums, [part][4][stride] u8x4 counts */
 } bsdc_family_batch;
 
 /* Outputs (device pointers).  Consensus slot (f, end) holds `stride` bases. */
@@ -112,7 +127,9 @@ typedef struct {
     uint8_t *dump_qual;
     uint8_t *scratch;            /* arenas of the large buckets beyond BSDC_LARGE_LDS_MAX, one region per
                                     bucket (their dispatches may run concurrently): the sum of
-                                    n_large[q] * large_arena[q] over those buckets + 256 bytes */
+                                    n_large[q] * large_arena[q] over those buckets; then the split
+                                    families' fallback arenas and the parts' sums (bsdc_family_batch);
+                                    + 256 bytes */
     /* optional single-strand consensus reads and their per-column statistics (BSDC_MODE_TAGS),
      * the inputs of fgbio's per-read / per-base consensus tags (aD/aM/aE, ad/ae/ac/aq, ...;
      * cD/cM/cE, cd/ce for the molecular caller).  Row (f, s), s = 0 AB-R1, 1 AB-R2, 2 BA-R1,

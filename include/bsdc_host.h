@@ -110,6 +110,22 @@ int32_t bsdc_materialize_prepare(const bsdc_host_records *R, const bsdc_host_ref
 int32_t bsdc_materialize_fill(bsdc_batch *b, const bsdc_batch_arrays *o, int64_t *n_cigar_out);
 void bsdc_batch_free(bsdc_batch *b);
 
+/* k_large's part mode (include/bsdc.h split_parts): cuts families of a batch's HBM-scratch bucket
+ * into parts of whole templates (an R1 and the R2 its mate link names, or an unpaired record),
+ * dealt in record order, each part's ArenaLayout within part_cap and at most max_part_rec records.
+ * A family is cut only if none of its records has a complex cigar (the alignment filter needs the
+ * whole set) or a tool-2 role, it has < 65536 records, and it yields at least two parts.
+ * rec: the batch's [4 * n_rec] record words; ents: [n_ent][4] bucket entries (family, first
+ * record, n_rec, image bytes).  bsdc_split_count writes each entry's part count (0 = not cut) and
+ * record count in its parts, and returns the total parts; bsdc_split_fill writes the part entries
+ * (family, first part record, n_rec, image bytes) and part records (batch record, slot in the
+ * part image, part-local mate index or 0xFFFF, 0), entry e's from first_part[e] / first_rec[e]. */
+int64_t bsdc_split_count(const uint32_t *rec, const uint32_t *ents, int64_t n_ent, int64_t part_cap, int32_t max_part_rec,
+                         int32_t *nparts, int64_t *nrecs, int32_t n_threads);
+void bsdc_split_fill(const uint32_t *rec, const uint32_t *ents, int64_t n_ent, int64_t part_cap, int32_t max_part_rec,
+                     const int64_t *first_part, const int64_t *first_rec, uint32_t *parts, uint32_t *part_recs,
+                     int32_t n_threads);
+
 const char *bsdc_host_last_error(void);
 /* the input record of the last BSDC_PLAN_EMISSING_MI */
 int64_t bsdc_host_error_record(void);

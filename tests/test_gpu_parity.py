@@ -326,3 +326,49 @@ def test_cli_step5_and_molecular_files(engine, tmp_path):
         L = int(mref.cons_len[f, 1])
         assert lines[4 * i] == "@L1:%s/2" % rm.mi_names[int(mref.fam_mi[f])]
         assert lines[4 * i + 1] == R.NT16_TO_ASCII[mref.cons_seq[f, 1, :L]].tobytes().decode()
+
+
+def force_parts(monkeypatch, cap, seen):
+    """Route every family through k_large's part mode where it can be cut (include/bsdc.h
+    split_parts): all families large, all in the HBM bucket, then split_hbm_bucket with parts of at
+    most `cap` LDS bytes; families that cannot be cut (complex cigars, tool-2 roles, one part) stay
+    in the HBM bucket.  `seen` collects the batches."""
+    real = batch.materialize
+    monkeypatch.setattr(batch, "PART_CAP", 0)
+
+    def forced(plan, f0, f1, small_cap=0, images=None):
+        fb = real(plan, f0, f1, small_cap=0, images=images)
+        nb = len(fb.large_buckets)
+        fb.large_buckets = [np.zeros((0, 4), np.uint32)] * (nb - 1) + [fb.large_fams]
+        fb.large_arenas = [16] * (nb - 1) + [max(max(fb.large_arenas), batch.LARGE_LDS_MAX + 16)]
+        fb = batch.split_hbm_bucket(fb, part_cap=cap)
+        seen.append(fb)
+        return fb
+
+    monkeypatch.setattr(batch, "materialize", forced)
+    monkeypatch.setattr(pipeline, "materialize", forced)
+
+
+@pytest.mark.parametrize("cfg,n_fam,messy,qlo,cap", [("C3", 60, 0.0, None, 20000), ("C3", 50, 0.1, None, 24000),
+                                                    ("C1", 400, 0.0, 84, 10000), ("C4", 250, 0.05, None, 30000)])
+def test_split_families_vs_oracle(engine, monkeypatch, cfg, n_fam, messy, qlo, cap):
+    """k_large part mode: families cut into parts of whole templates (their sums in HBM, one join
+    workgroup per family), bit-exact against oracle/ -- consensus, the tags' single-strand reads and
+    statistics, and the tool-2 records the parts dump; with near-tie columns (q >= 84) the join
+    sends those families whole through their HBM fallback arena."""
+    from helpers import near_tie_votes
+    s = synth.generate(cfg, n_fam, seed=23, device="cpu", genome_len=300_000)
+    raw = synth.messify(s.raw, frac=messy, seed=3) if messy else s.raw
+    if qlo:
+        raw = near_tie_votes(raw, qlo=qlo, seed=8)
+    seen = []
+    force_parts(monkeypatch, cap, seen)
+    engine.load_reference(s.ref)
+    cons, t2 = pipeline.run_step5(engine, raw, dump=True, tags=True)
+    n_split = sum(fb.split_fams.shape[0] for fb in seen)
+    assert n_split > (0.8 * n_fam if cfg != "C4" and not messy else 0), n_split
+    ref = oracle.run(raw, s.ref)
+    assert_consensus_equal(cons, ref, "parts " + cfg)
+    assert_ss_equal(cons, ref, "parts " + cfg)
+    for k in ("src", "pos", "seq", "qual", "cigar"):
+        assert np.array_equal(getattr(t2, k), getattr(ref.tool2, k)), "parts %s tool-2 %s" % (cfg, k)
