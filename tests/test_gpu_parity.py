@@ -268,7 +268,7 @@ def test_molecular_vs_oracle(engine, cfg, n_fam, messy):
     (no BA side); equal to the restatement run as callduplex on the run records."""
     s, raw = _grouped(cfg, n_fam, seed=21, messy=messy)
     cons, rm = pipeline.run_molecular(engine, raw, tags=True)
-    ref = oracle.run(rm, s.ref, run_tools=False, family_order="mi-group")
+    ref = oracle.run(rm, s.ref, run_tools=False, family_order="mi-group", min_consensus_base_quality=0)
     assert_consensus_equal(cons, ref, "molecular " + cfg)
     assert_ss_equal(cons, ref, "molecular " + cfg)
     assert ((cons.status & 4) == 0).all()  # no BA side anywhere
@@ -317,7 +317,7 @@ def test_cli_step5_and_molecular_files(engine, tmp_path):
         assert lines[4 * i + 1] == R.NT16_TO_ASCII[ref.cons_seq[f, 0, :L]].tobytes().decode()
         assert lines[4 * i + 3] == (ref.cons_qual[f, 0, :L] + 33).tobytes().decode()
     rm = pipeline.molecular_records(raw)
-    mref = oracle.run(rm, s.ref, run_tools=False, family_order="mi-group")
+    mref = oracle.run(rm, s.ref, run_tools=False, family_order="mi-group", min_consensus_base_quality=0)
     mem = np.nonzero(mref.status == 1)[0]
     with gzip.open(p("m2.fq.gz"), "rt") as fh:
         lines = fh.read().split("\n")
