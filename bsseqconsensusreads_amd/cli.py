@@ -94,7 +94,7 @@ def _step5_fleet(a, gpus: int) -> int:
                                         a.read_name_prefix, a.threads, a.compression,
                                         (a.fastq1, a.fastq2) if a.fastq1 else None,
                                         tags=a.output_per_base_tags == "true", chunk_bytes=a.chunk_mb << 20,
-                                        batch_bases=a.batch_bases)
+                                        batch_bases=a.batch_bases, gpu_bgzf=a.gpu_bgzf == "true")
     except Exception as e:  # noqa: BLE001 -- the rule fails with the message
         print("%s: %s" % (type(e).__name__, e), file=sys.stderr)
         return 1

@@ -134,10 +134,11 @@ class DeviceBatch:
         return (self.status[:F].cpu().numpy(),
                 self.len[:2 * F].cpu().numpy().view(np.uint16).astype(np.int32).reshape(F, 2))
 
-    def fetch(self):
+    def fetch(self, alloc=None):
         """-> dict of numpy arrays (consensus and, if dumped, the post-tool records).  The copies
         are queued together on the current stream into pinned host memory (torch's caching host
-        allocator), then one synchronize."""
+        allocator), then one synchronize.  With alloc(nbytes) -> uint8 array (a fleet worker's
+        shared segment) the outputs land in that buffer instead, so they leave the worker by name."""
         F = self.n_fam
         t = {"status": self.status[:F], "len": self.len[:2 * F], "seq": self.seq[:F * self.stride],
              "qual": self.qual[:2 * F * self.stride]}
@@ -149,9 +150,21 @@ class DeviceBatch:
         if self.dump:
             t.update(dump_pos=self.dump_pos[:Rn], dump_len=self.dump_len[:Rn], dump_tags=self.dump_tags[:Rn],
                      dump_seq=self.dump_seq, dump_qual=self.dump_qual)
-        h = {k: v.to("cpu", non_blocking=True) for k, v in t.items()}
-        torch.cuda.current_stream(self.device).synchronize()
-        a = {k: v.numpy() for k, v in h.items()}
+        if alloc is None:
+            h = {k: v.to("cpu", non_blocking=True) for k, v in t.items()}
+            torch.cuda.current_stream(self.device).synchronize()
+            a = {k: v.numpy() for k, v in h.items()}
+        else:
+            sizes = {k: (v.numel() * v.element_size() + 255) // 256 * 256 for k, v in t.items()}
+            buf = alloc(max(1, sum(sizes.values())))
+            a, o = {}, 0
+            for k, v in t.items():
+                nb = v.numel() * v.element_size()
+                dst = torch.from_numpy(buf[o:o + nb]).view(v.dtype)
+                dst.copy_(v)
+                a[k] = dst.numpy()
+                o += sizes[k]
+            torch.cuda.current_stream(self.device).synchronize()
         out = {
             "status": a["status"],
             "len": a["len"].view(np.uint16).astype(np.int32).reshape(F, 2),

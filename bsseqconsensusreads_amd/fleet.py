@@ -7,9 +7,12 @@ once, in bounded chunks (bam.stream_bam), and a planner thread forms each chunk'
 (batch.plan_families, the fgbio TemplateCoordinate runs).  The coordinator cuts every chunk's
 families into device batches (pipeline.plan_ranges), builds each batch (C++ materialize) and hands
 it to the least-loaded worker through shared memory: arrays travel as torch.multiprocessing
-shared-memory tensors (one copy in, no pickled array data, no process-group traffic).  A worker
-uploads the batch to its GPU, runs the kernels (libbsdc, the same launch as one GPU) and hands
-the consensus arrays back the same way.  A collector thread puts the batches back in input order
+named shared-memory segments, pooled and reused on both sides (SegmentPool): materialize writes
+the family images straight into a coordinator segment, the rest of the batch is copied into
+another, and only names and offsets are pickled (no process-group traffic).  A worker uploads
+the batch to its GPU, runs the kernels (libbsdc, the same launch as one GPU) and fetches the
+consensus arrays into a segment of its own, which the coordinator reads in place and releases
+once the chunk is written.  A collector thread puts the batches back in input order
 and a writer thread turns each complete chunk into records and appends them to the BAM / FASTQ
 (bam.duplex_records, BamWriter, FastqWriter): the output is byte-identical to the one-GPU stream.
 
@@ -34,63 +37,211 @@ import queue
 import threading
 import time
 import traceback
+from multiprocessing import shared_memory
 from typing import Dict, List, Optional, Sequence, Tuple
 
 import numpy as np
-import torch
 import torch.multiprocessing as tmp
 
 from . import records as R
 
 _SMALL = 4096  # arrays below this many bytes travel pickled with the message
+_ALIGN = 64
 
 
 # ------------------------------------------------------------------------------------------
-# shared-memory packing of the batch / result objects
+# shared memory: named segments, reused
 # ------------------------------------------------------------------------------------------
-def _share_array(a: np.ndarray):
-    a = np.ascontiguousarray(a)
-    if a.nbytes < _SMALL:
-        return ("np", a)
-    t = torch.empty(a.nbytes, dtype=torch.uint8).share_memory_()
-    np.copyto(t.numpy(), a.reshape(-1).view(np.uint8))
-    return ("sh", t, a.dtype.str, a.shape)
+class SegmentPool:
+    """Named shared-memory segments (multiprocessing.shared_memory) owned by this process and
+    reused: take() the smallest free segment that fits (or a new one), give() it back once the
+    other side has let go of it.  A message's large arrays travel in one segment, so steady state
+    allocates nothing and faults no fresh pages (a fresh share_memory_() tensor per array cost as
+    much as the copy into it).  close() unlinks every segment."""
+
+    MIN = 16 << 20
+
+    def __init__(self, tag: str, keep: int = 8):
+        self.prefix = "bsdc%d_%s_%x" % (os.getpid(), tag, id(self) & 0xFFFFFF)
+        self.segs: Dict[str, "shared_memory.SharedMemory"] = {}
+        self.free: List[str] = []
+        self.keep = keep
+        self.n = 0
+        self.lock = threading.Lock()
+
+    def take(self, nbytes: int) -> str:
+        with self.lock:
+            fit = [x for x in self.free if self.segs[x].size >= nbytes]
+            if fit:
+                name = min(fit, key=lambda x: self.segs[x].size)
+                self.free.remove(name)
+                return name
+            name = "%s_%d" % (self.prefix, self.n)
+            self.n += 1
+        shm = shared_memory.SharedMemory(name=name, create=True, size=max(int(nbytes * 1.25) + _ALIGN, self.MIN))
+        with self.lock:
+            self.segs[name] = shm
+        return name
+
+    def give(self, name: Optional[str]):
+        if name is None:
+            return
+        with self.lock:
+            if name not in self.segs:
+                return
+            self.free.append(name)
+            while len(self.free) > self.keep:  # the smallest free ones go
+                x = min(self.free, key=lambda y: self.segs[y].size)
+                self.free.remove(x)
+                shm = self.segs.pop(x)
+                _close(shm, unlink=True)
+
+    def buf(self, name: str) -> memoryview:
+        return self.segs[name].buf
+
+    def owns(self, a: np.ndarray) -> Optional[Tuple[str, int]]:
+        """(segment, byte offset) of an array that lies in one of this pool's segments."""
+        if a.nbytes == 0:
+            return None
+        p = a.__array_interface__["data"][0]
+        with self.lock:
+            for name, shm in self.segs.items():
+                b = np.frombuffer(shm.buf, np.uint8).__array_interface__["data"][0]
+                if b <= p and p + a.nbytes <= b + shm.size:
+                    return name, p - b
+        return None
+
+    def close(self):
+        with self.lock:
+            segs, self.segs, self.free = self.segs, {}, []
+        for shm in segs.values():
+            _close(shm, unlink=True)
 
 
-def pack(obj):
-    """obj (dataclass / dict / list of numpy arrays, StringTables, scalars) -> a picklable tree whose
-    large arrays are shared-memory tensors."""
-    from .bam import StringTable
-    if isinstance(obj, np.ndarray):
-        return _share_array(obj)
-    if isinstance(obj, StringTable):
-        return ("st", pack(obj.buf), pack(obj.off), obj.as_str)
-    if dataclasses.is_dataclass(obj) and not isinstance(obj, type):
-        return ("dc", type(obj), {f.name: pack(getattr(obj, f.name)) for f in dataclasses.fields(obj)})
-    if isinstance(obj, dict):
-        return ("di", {k: pack(v) for k, v in obj.items()})
-    if isinstance(obj, (list, tuple)) and any(isinstance(x, np.ndarray) for x in obj):
-        return ("li", [pack(x) for x in obj])
-    return ("v", obj)
+_LINGER: list = []  # segments closed while numpy views still mapped them
 
 
-def unpack(tree):
-    """The inverse of pack: numpy views of the shared tensors (they stay alive with the views)."""
+def _close(shm, unlink: bool):
+    try:
+        shm.close()
+    except BufferError:  # numpy views still map it: the mapping goes with the views / the process
+        _LINGER.append(shm)
+    if unlink:
+        try:
+            shm.unlink()
+        except FileNotFoundError:
+            pass
+
+
+class SegmentViews:
+    """The other side's segments, opened once by name and kept (no remapping per message)."""
+
+    def __init__(self):
+        self.open: Dict[str, "shared_memory.SharedMemory"] = {}
+
+    def buf(self, name: str) -> memoryview:
+        shm = self.open.get(name)
+        if shm is None:
+            # (spawned workers share the coordinator's resource tracker, so attaching registers
+            # nothing new, and a segment left behind by a dead process is still unlinked at exit)
+            shm = shared_memory.SharedMemory(name=name)
+            self.open[name] = shm
+        return shm.buf
+
+    def close(self):
+        for shm in self.open.values():
+            _close(shm, unlink=False)
+        self.open = {}
+
+
+def pack(obj, pool: Optional[SegmentPool] = None):
+    """obj (dataclass / dict / list of numpy arrays, StringTables, scalars) -> (a picklable tree,
+    the segments it uses).  Arrays that already lie in one of `pool`'s segments (family images
+    materialized there, outputs fetched there) travel by reference; the others are copied into one
+    segment taken from `pool`.  The receiver reads them in place; the segments go back to `pool`
+    once it is done (the sender's bookkeeping)."""
+    big: List[np.ndarray] = []
+
+    def collect(o):
+        from .bam import StringTable
+        if isinstance(o, np.ndarray):
+            if o.nbytes >= _SMALL:
+                big.append(o)
+        elif isinstance(o, StringTable):
+            collect(o.buf)
+            collect(o.off)
+        elif dataclasses.is_dataclass(o) and not isinstance(o, type):
+            for f in dataclasses.fields(o):
+                collect(getattr(o, f.name))
+        elif isinstance(o, dict):
+            for v in o.values():
+                collect(v)
+        elif isinstance(o, (list, tuple)):
+            for v in o:
+                collect(v)
+    collect(obj)
+    place: Dict[int, Tuple[str, int]] = {}
+    need = 0
+    for a in big:
+        loc = pool.owns(a) if pool is not None and a.flags.c_contiguous else None
+        if loc is not None:
+            place[id(a)] = loc
+        else:
+            need += (a.nbytes + _ALIGN - 1) // _ALIGN * _ALIGN
+    seg = None
+    if need:
+        if pool is None:
+            raise ValueError("pack: large arrays need a segment pool")
+        seg = pool.take(need)
+        buf = np.frombuffer(pool.buf(seg), np.uint8)
+        o = 0
+        for a in big:
+            if id(a) in place:
+                continue
+            np.copyto(buf[o:o + a.nbytes], np.ascontiguousarray(a).reshape(-1).view(np.uint8))
+            place[id(a)] = (seg, o)
+            o += (a.nbytes + _ALIGN - 1) // _ALIGN * _ALIGN
+
+    def tree(o):
+        from .bam import StringTable
+        if isinstance(o, np.ndarray):
+            if o.nbytes < _SMALL:
+                return ("np", o)
+            name, off = place[id(o)]
+            return ("sm", name, off, o.dtype.str, o.shape)
+        if isinstance(o, StringTable):
+            return ("st", tree(o.buf), tree(o.off), o.as_str)
+        if dataclasses.is_dataclass(o) and not isinstance(o, type):
+            return ("dc", type(o), {f.name: tree(getattr(o, f.name)) for f in dataclasses.fields(o)})
+        if isinstance(o, dict):
+            return ("di", {k: tree(v) for k, v in o.items()})
+        if isinstance(o, (list, tuple)) and any(isinstance(x, np.ndarray) for x in o):
+            return ("li", [tree(x) for x in o])
+        return ("v", o)
+    return tree(obj), sorted({v[0] for v in place.values()})
+
+
+def unpack(tree, views: Optional[SegmentViews] = None, pool: Optional[SegmentPool] = None):
+    """The inverse of pack: numpy views of the named segments (opened through `views`, or this
+    process's own `pool`)."""
     from .bam import StringTable
     kind = tree[0]
     if kind == "np":
         return tree[1]
-    if kind == "sh":
-        _, t, dt, shape = tree
-        return t.numpy().view(np.dtype(dt)).reshape(shape)
+    if kind == "sm":
+        _, name, off, dt, shape = tree
+        buf = pool.buf(name) if pool is not None and name in pool.segs else views.buf(name)
+        dt = np.dtype(dt)
+        n = int(np.prod(shape, dtype=np.int64)) if len(shape) else 1
+        return np.frombuffer(buf, dt, count=n, offset=off).reshape(shape)
     if kind == "st":
-        return StringTable(unpack(tree[1]), unpack(tree[2]), tree[3])
+        return StringTable(unpack(tree[1], views, pool), unpack(tree[2], views, pool), tree[3])
     if kind == "dc":
-        return tree[1](**{k: unpack(v) for k, v in tree[2].items()})
+        return tree[1](**{k: unpack(v, views, pool) for k, v in tree[2].items()})
     if kind == "di":
-        return {k: unpack(v) for k, v in tree[1].items()}
+        return {k: unpack(v, views, pool) for k, v in tree[1].items()}
     if kind == "li":
-        return [unpack(x) for x in tree[1]]
+        return [unpack(x, views, pool) for x in tree[1]]
     return tree[1]
 
 
@@ -109,11 +260,12 @@ class GpuRunner:
     def load_reference(self, ref):
         self.eng.load_reference(ref)
 
-    def run_batch(self, fb, mode: int, tags: bool, raw_sub=None) -> dict:
+    def run_batch(self, fb, mode: int, tags: bool, raw_sub=None, alloc=None) -> dict:
+        """alloc(nbytes) -> a uint8 array the outputs are fetched into (a shared segment)."""
         from ._lib import MODE_TAGS
         db = self.eng.upload(fb, tags=tags)
         self.eng.run(db, mode | (MODE_TAGS if tags else 0))
-        return db.fetch()
+        return db.fetch(alloc)
 
     def run_chunk(self, raw, tags: bool, batch_bases):
         from . import pipeline
@@ -131,8 +283,16 @@ def _make_runner(spec: Optional[str], device: int):
 
 
 def _worker(wid: int, device: int, runner_spec: Optional[str], tq, rq):
-    """One GPU worker (a spawned process: it is the first thing here to touch the GPU)."""
+    """One GPU worker (a spawned process: it is the first thing here to touch the GPU).  Batches
+    arrive as views of the coordinator's segments; outputs are fetched into this worker's own
+    segments and travel back by name; the coordinator releases them once their chunk is written."""
     runner = None
+    pool = SegmentPool("w%d" % wid)
+    views = SegmentViews()
+
+    def alloc(nbytes: int):
+        name = pool.take(nbytes)
+        return np.frombuffer(pool.buf(name), np.uint8, count=nbytes)
     try:
         runner = _make_runner(runner_spec, device)
         rq.put(("ready", wid, bool(getattr(runner, "needs_raw", False))))
@@ -141,18 +301,29 @@ def _worker(wid: int, device: int, runner_spec: Optional[str], tq, rq):
             if msg is None:
                 break
             kind = msg[0]
-            if kind == "ref":
-                runner.load_reference(unpack(msg[1]))
+            if kind == "release":
+                pool.give(msg[1])
+            elif kind == "drop":  # the coordinator's run is over: unmap its segments
+                views.close()
+            elif kind == "ref":
+                runner.load_reference(unpack(msg[1], views))
             elif kind == "batch":
                 _, key, fb_t, mode, tags, raw_t = msg
-                out = runner.run_batch(unpack(fb_t), mode, tags, unpack(raw_t) if raw_t is not None else None)
-                del fb_t, raw_t
-                rq.put(("batch", wid, key, pack(out)))
+                fb = unpack(fb_t, views)
+                raw_sub = unpack(raw_t, views) if raw_t is not None else None
+                if isinstance(runner, GpuRunner):
+                    out = runner.run_batch(fb, mode, tags, raw_sub, alloc=alloc)
+                else:
+                    out = runner.run_batch(fb, mode, tags, raw_sub)
+                del fb, raw_sub, fb_t, raw_t
+                tree, segs = pack(out, pool)
+                rq.put(("batch", wid, key, tree, segs))
             elif kind == "chunk":
                 _, key, raw_t, tags, batch_bases = msg
-                cons = runner.run_chunk(unpack(raw_t), tags, batch_bases)
+                cons = runner.run_chunk(unpack(raw_t, views), tags, batch_bases)
                 del raw_t
-                rq.put(("chunk", wid, key, pack(cons)))
+                tree, segs = pack(cons, pool)
+                rq.put(("chunk", wid, key, tree, segs))
     except BaseException as e:  # noqa: BLE001 -- reported to the coordinator, which raises it
         rq.put(("error", wid, "%s: %s\n%s" % (type(e).__name__, e, traceback.format_exc())))
         # stay until the coordinator ends the fleet: results this worker sent earlier hold shared
@@ -168,6 +339,8 @@ def _worker(wid: int, device: int, runner_spec: Optional[str], tq, rq):
                 runner.close()
             except Exception:  # noqa: BLE001
                 pass
+        views.close()
+        pool.close()
 
 
 class Fleet:
@@ -270,9 +443,14 @@ def step5_stream_multi(in_bam: str, fasta: str, out_bam: Optional[str], devices:
                        prefix: Optional[str] = None, threads: int = 0, level: int = 6,
                        fastq: Optional[Tuple[str, str]] = None, tags: bool = True, chunk_bytes: Optional[int] = None,
                        slack: Optional[int] = None, batch_bases: Optional[int] = None, inflight: int = 2,
-                       runner: Optional[str] = None, stats: Optional[dict] = None) -> dict:
+                       runner: Optional[str] = None, stats: Optional[dict] = None, gpu_bgzf: bool = False,
+                       fleet: Optional["Fleet"] = None) -> dict:
     """bam.step5_stream over len(devices) GPU workers (see the module docstring).  Same file
-    contract and output bytes as bam.step5 / bam.step5_stream (main.snake.py:121-164)."""
+    contract and output bytes as bam.step5 / bam.step5_stream (main.snake.py:121-164).
+    gpu_bgzf: the writer deflates on devices[0] (bam.GpuBgzf; the coordinator touches that GPU
+    only after its workers are spawned).  fleet: an already started Fleet over `devices` (left
+    running; e.g. to time the stream without the workers' start-up), else one is started and
+    closed here."""
     from . import bam, pipeline
     chunk_bytes = bam.DEFAULT_CHUNK_BYTES if chunk_bytes is None else chunk_bytes
     slack = bam.DEFAULT_SLACK if slack is None else slack
@@ -284,14 +462,18 @@ def step5_stream_multi(in_bam: str, fasta: str, out_bam: Optional[str], devices:
     pre = bam.read_name_prefix(hdr0) if prefix is None else prefix
     tg = tags and out_bam is not None  # the FASTQ pair carries no tags
     mode = pipeline.MODE_CONVERT | pipeline.MODE_EXTEND | pipeline.MODE_VOTE
-    fleet = Fleet(devices, runner, inflight)
+    own_fleet = fleet is None
+    fleet = Fleet(devices, runner, inflight) if own_fleet else fleet
+    cpool = SegmentPool("c")  # batch images and messages; a batch's go back when its result arrives
+    views = SegmentViews()  # the workers' result segments
     stop = threading.Event()
     err: List[BaseException] = []
     raws: "queue.Queue" = queue.Queue(maxsize=1)
     chunks: "queue.Queue" = queue.Queue(maxsize=1)
     outs: "queue.Queue" = queue.Queue(maxsize=1)
     # chunk id -> {"raw", "n" (batches; None until the dealer has sent them all), "parts": {i:
-    # Consensus}, "index": {i: _FamilyIndex}}, filled by the dealer and the collector
+    # Consensus}, "index": {i: _FamilyIndex}, "in": {i: coordinator segments of batch i}, "out":
+    # [(worker, its result segments)]}, filled by the dealer and the collector
     pend: Dict[int, dict] = {}
     eof: List[Optional[int]] = [None]  # number of chunks, once the dealer has seen them all
     plock = threading.Condition()
@@ -368,11 +550,15 @@ def step5_stream_multi(in_bam: str, fasta: str, out_bam: Optional[str], devices:
                 m = fleet.get(timeout=0.5)
                 if m is None:
                     continue
-                kind, wid, (cid, i), res = m[0], m[1], m[2], unpack(m[3])
+                kind, wid, (cid, i), res = m[0], m[1], m[2], unpack(m[3], views)
                 with plock:
                     c = pend[cid]
                     c["parts"][i] = pipeline.consensus_from_output(c["index"].pop(i), res) if kind == "batch" else res
+                    c["out"].append((wid, m[4]))
+                    back = c["in"].pop(i, ())
                     plock.notify_all()
+                for name in back:  # (the worker has read the batch: its result is back)
+                    cpool.give(name)
                 fleet.done(wid)
         except BaseException as e:  # noqa: BLE001
             fail(e)
@@ -382,8 +568,10 @@ def step5_stream_multi(in_bam: str, fasta: str, out_bam: Optional[str], devices:
     def writer():
         w = fq = None
         try:
-            w = bam.BamWriter(out_bam, bam.output_header(hdr0), level) if out_bam is not None else None
-            fq = bam.FastqWriter(fastq[0], fastq[1], level) if fastq is not None else None
+            gz = bam.GpuBgzf(int(devices[0])) if gpu_bgzf and out_bam is not None else None
+            gzf = bam.GpuBgzf(int(devices[0])) if gpu_bgzf and fastq is not None else None
+            w = bam.BamWriter(out_bam, bam.output_header(hdr0), level, gz) if out_bam is not None else None
+            fq = bam.FastqWriter(fastq[0], fastq[1], level, gzf) if fastq is not None else None
             while True:
                 c = outs.get()
                 if c is None:
@@ -404,9 +592,13 @@ def step5_stream_multi(in_bam: str, fasta: str, out_bam: Optional[str], devices:
                 T["records"] += t1 - t0
                 T["encode"] += time.perf_counter() - t1
                 back = [getattr(c["raw"], "_pool_buf", None), getattr(recs.aux2, "_pool_buf", None)]
+                results = c["out"]
                 del c, cons, recs
                 for buf in back:  # (the chunk is written: nothing refers to its record arrays)
                     bufs.give(buf)
+                for wid, names in results:  # nor to the workers' result segments
+                    for name in names:
+                        fleet.tqs[wid].put(("release", name))
             if not stop.is_set():
                 if w is not None:
                     w.close(threads)
@@ -423,7 +615,7 @@ def step5_stream_multi(in_bam: str, fasta: str, out_bam: Optional[str], devices:
     workers = [threading.Thread(target=f, daemon=True) for f in (decoder, planner, collector, writer)]
     drained = False
     try:
-        fleet.broadcast(("ref", pack(dataclasses.replace(ref, letters={}))))
+        fleet.broadcast(("ref", pack(dataclasses.replace(ref, letters={}), cpool)[0]))
         for t in workers:
             t.start()
         cid = 0
@@ -438,27 +630,42 @@ def step5_stream_multi(in_bam: str, fasta: str, out_bam: Optional[str], devices:
             with plock:  # a bounded number of chunks between the dealer and the writer
                 while len(pend) >= 2 * fleet.n + 2 and not stop.is_set():
                     plock.wait(0.5)
-                pend[cid] = {"raw": raw, "n": None, "parts": {}, "index": {}}
+                pend[cid] = {"raw": raw, "n": None, "parts": {}, "index": {}, "in": {}, "out": []}
             n = 0
             if plan.split_ext:
-                if fleet.submit(("chunk", (cid, 0), pack(raw), tg, batch_bases), stop) >= 0:
+                t, segs = pack(raw, cpool)
+                with plock:
+                    pend[cid]["in"][0] = segs
+                if fleet.submit(("chunk", (cid, 0), t, tg, batch_bases), stop) >= 0:
                     n = 1
             else:
                 for a, b in pipeline.plan_ranges(plan, batch_bases):
                     t0 = time.perf_counter()
-                    fb = pipeline.materialize(plan, a, b)
+                    img = []
+
+                    def images(n_slots: int):  # the family images straight into a shared segment
+                        ns = (n_slots // 2 + 255) // 256 * 256
+                        img.append(cpool.take(ns + n_slots + 256))
+                        buf = np.frombuffer(cpool.buf(img[-1]), np.uint8)
+                        return buf[:ns], buf[ns:ns + n_slots]
+                    fb = pipeline.materialize(plan, a, b, images=images)
                     T["materialize"] += time.perf_counter() - t0
-                    with plock:
-                        pend[cid]["index"][n] = _FamilyIndex(fb.fam_mi.copy(), fb.fam_off.astype(np.int64),
-                                                             fb.src.astype(np.int64))
-                    raw_sub = pack(R.take(raw, fb.src.astype(np.int64))) if fleet.needs_raw else None
+                    raw_sub = R.take(raw, fb.src.astype(np.int64)) if fleet.needs_raw else None
                     # the worker needs the device arrays only (host bookkeeping stays here)
                     slim = dataclasses.replace(fb, src=np.zeros(0, np.int64), fam_mi=np.zeros(0, np.int32),
                                                t2_rank=np.zeros(0, np.int64), rec_tid=np.zeros(0, np.int32))
                     t0 = time.perf_counter()
-                    w = fleet.submit(("batch", (cid, n), pack(slim), mode, tg, raw_sub), stop)
+                    t, segs = pack(slim, cpool)
+                    rt, rsegs = pack(raw_sub, cpool) if raw_sub is not None else (None, [])
+                    T["pack"] = T.get("pack", 0.0) + time.perf_counter() - t0
+                    with plock:
+                        pend[cid]["index"][n] = _FamilyIndex(fb.fam_mi.copy(), fb.fam_off.astype(np.int64),
+                                                             fb.src.astype(np.int64))
+                        pend[cid]["in"][n] = sorted(set(segs) | set(rsegs) | set(img))
+                    t0 = time.perf_counter()
+                    w = fleet.submit(("batch", (cid, n), t, mode, tg, rt), stop)
                     T["submit_wait"] += time.perf_counter() - t0
-                    del fb, slim
+                    del fb, slim, raw_sub
                     if w < 0:
                         break
                     n += 1
@@ -479,7 +686,13 @@ def step5_stream_multi(in_bam: str, fasta: str, out_bam: Optional[str], devices:
                 pass
         for t in workers:
             t.join(timeout=600)
-        fleet.close()
+        if own_fleet:
+            fleet.close()
+        else:  # (a kept fleet's workers may still hold this run's result segments: let them go)
+            for wid in range(fleet.n):
+                fleet.tqs[wid].put(("drop",))
+        views.close()
+        cpool.close()
     if err:
         raise err[0]
     if stats is not None:

@@ -5,8 +5,9 @@ synthetic coordinate-sorted C2 BAM + FASTA on local disk, then, each in a fresh 
   stream  bam.step5_stream: bounded chunks, reader / GPU / writer threads overlapped
   stream_fastq  the same, writing the FASTQ pair of the next rule instead of the BAM
   stream_gpubgzf, stream_fastq_gpubgzf  the same with the BGZF deflate on the GPU
-  fleet   fleet.step5_stream_multi: this child reads and writes (it never touches the GPU), --workers
-          spawned GPU worker processes (all on GPU 0 on a one-GPU box) run the batches
+  fleet   fleet.step5_stream_multi: this child reads and writes, --workers spawned GPU worker
+          processes (all on GPU 0 on a one-GPU box; started before the clock) run the batches
+  fleet_gpubgzf  the same with the writer's deflate on GPU 0
   molecular_stream, molecular_whole  step 1 (bam.molecular_stream / bam.molecular) on the same
           families in GroupReadsByUmi order (a second input, MI runs contiguous; BAM with tags, GPU BGZF)
 The BAMs are compared byte for byte.  Usage:
@@ -53,12 +54,19 @@ def child(args):
 
     from bsseqconsensusreads_amd import bam
     stats = {}
-    if args.mode == "fleet":  # the coordinator never touches the GPU: its workers do
+    if args.mode in ("fleet", "fleet_gpubgzf"):  # the coordinator's workers hold the GPU
         from bsseqconsensusreads_amd import fleet
+        ts = time.perf_counter()
+        fl = fleet.Fleet([0] * args.workers)  # started (spawn, import, HIP init) outside the clock
         t0 = time.perf_counter()
-        info = fleet.step5_stream_multi(args.inp, args.fa, args.out, [0] * args.workers, threads=args.threads,
-                                        level=args.level, chunk_bytes=args.chunk_mb << 20, stats=stats)
-        dt = time.perf_counter() - t0
+        try:
+            info = fleet.step5_stream_multi(args.inp, args.fa, args.out, [0] * args.workers, threads=args.threads,
+                                            level=args.level, chunk_bytes=args.chunk_mb << 20, stats=stats,
+                                            gpu_bgzf=args.mode == "fleet_gpubgzf", fleet=fl)
+            dt = time.perf_counter() - t0
+        finally:
+            fl.close()
+        stats["fleet_start_s"] = round(t0 - ts, 3)
         rss = resource.getrusage(resource.RUSAGE_SELF).ru_maxrss / 1024
         crss = resource.getrusage(resource.RUSAGE_CHILDREN).ru_maxrss / 1024
         print(json.dumps({"mode": args.mode, "workers": args.workers, "seconds": round(dt, 3),
@@ -145,9 +153,12 @@ def main():
         res[mode] = r
         outs[mode] = out
         print(mode, json.dumps(r), flush=True)
-    bams = [open(outs[m], "rb").read() for m in outs if m not in ("stream_fastq", "stream_gpubgzf", "stream_fastq_gpubgzf")
+    bams = [open(outs[m], "rb").read() for m in outs if m != "stream_fastq" and "gpubgzf" not in m
             and not m.startswith("molecular")]
     res["outputs_identical"] = all(b == bams[0] for b in bams)
+    gz = [open(outs[m], "rb").read() for m in ("stream_gpubgzf", "fleet_gpubgzf") if m in outs]
+    if len(gz) == 2:  # the same GPU-deflated blocks from one GPU and from the fleet's writer
+        res["gpubgzf_fleet_identical"] = gz[0] == gz[1]
     if "stream_gpubgzf" in outs and "stream" in outs:  # other compressed bytes: compare the records
         sys.path.insert(0, ROOT)
         from bsseqconsensusreads_amd import bam as B

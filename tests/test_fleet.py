@@ -75,8 +75,25 @@ def test_worker_failure_mid_stream(sorted_input, tmp_path):
 
 
 def test_pack_roundtrip():
-    a = np.arange(100_000, dtype=np.int64).reshape(1000, 100)
-    t = {"a": a, "s": bam.StringTable.from_list([b"x", b"yz"]), "l": [a[:3], a[3:5]], "k": 7}
-    u = fleet.unpack(fleet.pack(t))
-    assert np.array_equal(u["a"], a) and u["k"] == 7 and u["s"][1] == b"yz"
-    assert np.array_equal(u["l"][1], a[3:5])
+    pool, views = fleet.SegmentPool("t"), fleet.SegmentViews()
+    try:
+        a = np.arange(100_000, dtype=np.int64).reshape(1000, 100)
+        t = {"a": a, "s": bam.StringTable.from_list([b"x", b"yz"]), "l": [a[:3], a[3:5]], "k": 7}
+        tree, segs = fleet.pack(t, pool)
+        assert len(segs) == 1
+        u = fleet.unpack(tree, views)
+        assert np.array_equal(u["a"], a) and u["k"] == 7 and u["s"][1] == b"yz"
+        assert np.array_equal(u["l"][1], a[3:5])
+        # an array already in one of the pool's segments travels by reference (no second segment)
+        name = pool.take(1 << 20)
+        img = np.frombuffer(pool.buf(name), np.uint8, count=1 << 20)
+        img[:] = 7
+        tree2, segs2 = fleet.pack({"img": img[4096:]}, pool)
+        assert segs2 == [name] and tree2[1]["img"][1:3] == (name, 4096)
+        assert (fleet.unpack(tree2, views)["img"] == 7).all()
+        pool.give(segs[0])
+        assert pool.take(100) == segs[0]  # reused
+        del u
+    finally:
+        views.close()
+        pool.close()

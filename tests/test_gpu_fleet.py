@@ -63,3 +63,13 @@ def test_cli_whole_file_ranks_equal_one_and_oracle(cli_input):
     two = _cli(tmp, inp, fa, "two_w", "--stream", "false", "--gpus", "2", "--devices", "0,0")
     assert one == two
     assert assert_bam_matches_oracle(str(tmp / "two_w.bam"), inp, fa, "cli --gpus 2 whole file") > 0
+
+
+def test_cli_fleet_gpu_bgzf_equals_one_gpu(cli_input):
+    """--gpus 2 --gpu-bgzf true: the coordinator's writer deflates on devices[0] (GpuBgzf), the
+    same blocks as the one-GPU stream with --gpu-bgzf true, so the files are byte-identical"""
+    tmp, inp, fa = cli_input
+    one = _cli(tmp, inp, fa, "one_gz", "--gpu-bgzf", "true")
+    two = _cli(tmp, inp, fa, "two_gz", "--gpus", "2", "--devices", "0,0", "--gpu-bgzf", "true")
+    assert one == two
+    assert assert_bam_matches_oracle(str(tmp / "two_gz.bam"), inp, fa, "cli --gpus 2 --gpu-bgzf") > 0
