@@ -88,7 +88,8 @@ class Resident:
         self.small = fb.small_fams.astype(np.int64)
         self.n_large = int(fb.large_fams.shape[0])
         self.n_disp = sum(1 for b in fb.small_buckets if b.shape[0])  # one k_small dispatch per LDS bucket
-        self.n_disp_large = sum(1 for b in fb.large_buckets if b.shape[0])  # one k_large dispatch per bucket
+        # one k_large dispatch per bucket, + the part dispatch and the k_join one of split families
+        self.n_disp_large = sum(1 for b in fb.large_buckets if b.shape[0]) + (2 if fb.split_fams.shape[0] else 0)
         self.molecules = int(np.unique(fb.fam_mi).shape[0])
         self.n_fam, self.n_rec, self.n_bases = fb.n_fam, fb.n_rec, fb.n_bases
         self.db.release_host()

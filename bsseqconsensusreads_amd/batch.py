@@ -52,6 +52,9 @@ assert LARGE_BUCKETS[-1] == LARGE_LDS_MAX
 # parts whose arena fits this (3 workgroups of 256 threads per CU); BSDC_PART_CAP=0 turns it off
 PART_CAP = int(os.environ.get("BSDC_PART_CAP", str(LARGE_BUCKETS[2])))
 MAX_PART_REC = 254  # a part's per-set sums stay int32 and its read counts fit a byte
+# the first large bucket whose families are cut into parts (default: the HBM-scratch bucket only;
+# BSDC_SPLIT_FROM=3 also cuts the 2- and 1-per-CU LDS classes -- profiling A/B)
+SPLIT_FROM = int(os.environ.get("BSDC_SPLIT_FROM", str(len(LARGE_BUCKETS))))
 
 
 def round16(x):
@@ -652,7 +655,10 @@ def split_hbm_bucket(fb: FamilyBatch, part_cap: Optional[int] = None, threads: i
     bytes, run in LDS, and one join workgroup per family; the rest stay in the bucket.  In place."""
     from . import hostplan
     cap = PART_CAP if part_cap is None else int(part_cap)
-    ents = np.ascontiguousarray(fb.large_buckets[-1], np.uint32).reshape(-1, 4)
+    lo = min(max(SPLIT_FROM, 0), len(fb.large_buckets) - 1)
+    sizes = [int(np.asarray(b).reshape(-1, 4).shape[0]) for b in fb.large_buckets[lo:]]
+    ents = np.concatenate([np.asarray(b, np.uint32).reshape(-1, 4) for b in fb.large_buckets[lo:]]) \
+        if sum(sizes) else np.zeros((0, 4), np.uint32)
     if cap <= 0 or ents.shape[0] == 0:
         return fb
     cap = cap // 16 * 16
@@ -692,7 +698,12 @@ def split_hbm_bucket(fb: FamilyBatch, part_cap: Optional[int] = None, threads: i
     fb.split_part_recs = part_recs
     fb.split_fams = sf.astype(np.uint32)
     fb.split_part_arena = cap
-    fb.large_buckets = list(fb.large_buckets[:-1]) + [ents[~cut]]
+    keep = ~cut
+    tail, o = [], 0
+    for k in sizes:  # the families left whole stay in their buckets
+        tail.append(ents[o:o + k][keep[o:o + k]])
+        o += k
+    fb.large_buckets = list(fb.large_buckets[:lo]) + tail
     return fb
 
 

@@ -18,8 +18,10 @@ for f in sorted(glob.glob(d + "/p*/**/*counter_collection.csv", recursive=True))
 # dispatch per bucket) under its name: mean per dispatch x dispatches per launch set = per set
 grouped = collections.defaultdict(dict)
 for k, disp in per.items():
-    m = re.search(r"(k_small|k_large)", k)
+    m = re.search(r"(k_small|k_large|k_join)", k)
     name = m.group(1) if m else k[:60]
+    if name == "k_join":  # the split families' join: one more dispatch of the k_large launch set
+        name = "k_large"
     if name == "k_small" and "<true>" in k:  # the consensus-tag instance (BSDC_MODE_TAGS) on its own
         name = "k_small_tags"
     grouped[name].update({(k,) + key: v for key, v in disp.items()})

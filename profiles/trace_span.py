@@ -24,7 +24,8 @@ def main():
     rows = []
     with open(trace, newline="") as f:
         for x in csv.DictReader(f):
-            if kern + "<" in x["Kernel_Name"]:
+            k = x["Kernel_Name"]
+            if kern + "<" in k or (kern == "k_large" and "k_join<" in k):  # (split families' join)
                 rows.append((int(x["Start_Timestamp"]), int(x["End_Timestamp"])))
     rows.sort()
     take = rows[-nsets * per:]
