@@ -30,6 +30,7 @@ on CPU.
 """
 from __future__ import annotations
 
+import ctypes
 import dataclasses
 import importlib
 import os
@@ -67,6 +68,8 @@ class SegmentPool:
         self.free: List[str] = []
         self.keep = keep
         self.n = 0
+        self.created_bytes = 0  # (stats: fresh segments fault their pages in on first touch)
+        self.closed = False
         self.lock = threading.Lock()
 
     def take(self, nbytes: int) -> str:
@@ -81,7 +84,32 @@ class SegmentPool:
         shm = shared_memory.SharedMemory(name=name, create=True, size=max(int(nbytes * 1.25) + _ALIGN, self.MIN))
         with self.lock:
             self.segs[name] = shm
+            self.created_bytes += shm.size
         return name
+
+    def prefill(self, count: int, size: int, threads: int = 4) -> threading.Thread:
+        """Create `count` free segments of `size` bytes and fault their pages in, on a background
+        thread (a fresh shared page costs a fault on first touch: ~1 GB/s, several times the copy
+        into it).  take() meanwhile creates what it needs itself."""
+        def run():
+            for _ in range(count):
+                with self.lock:
+                    if self.closed:
+                        return
+                    name = "%s_%d" % (self.prefix, self.n)
+                    self.n += 1
+                shm = shared_memory.SharedMemory(name=name, create=True, size=max(int(size), self.MIN))
+                _populate(shm, threads)
+                with self.lock:
+                    if not self.closed:
+                        self.segs[name] = shm
+                        self.created_bytes += shm.size
+                        self.free.append(name)
+                        continue
+                _close(shm, unlink=True)  # (the pool closed meanwhile)
+        t = threading.Thread(target=run, daemon=True)
+        t.start()
+        return t
 
     def give(self, name: Optional[str]):
         if name is None:
@@ -113,12 +141,42 @@ class SegmentPool:
 
     def close(self):
         with self.lock:
+            self.closed = True
             segs, self.segs, self.free = self.segs, {}, []
         for shm in segs.values():
             _close(shm, unlink=True)
 
 
 _LINGER: list = []  # segments closed while numpy views still mapped them
+_MADV_POPULATE_WRITE = 23  # Linux >= 5.14
+
+
+def _populate(shm, threads: int = 4):
+    """Fault a fresh segment's pages in (madvise MADV_POPULATE_WRITE over `threads` slices; one
+    write per page where the kernel lacks it)."""
+    a = np.frombuffer(shm.buf, np.uint8)
+    n = a.shape[0]
+    if n == 0:
+        return
+    try:
+        libc = ctypes.CDLL(None, use_errno=True)
+        libc.madvise.argtypes = [ctypes.c_void_p, ctypes.c_size_t, ctypes.c_int]
+        base = a.ctypes.data
+        step = -(-n // max(1, threads) // 4096) * 4096
+        rcs: List[int] = []
+
+        def one(o):
+            rcs.append(libc.madvise(base + o, min(step, n - o), _MADV_POPULATE_WRITE))
+        ts = [threading.Thread(target=one, args=(o,)) for o in range(0, n, step)]
+        for t in ts:
+            t.start()
+        for t in ts:
+            t.join()
+        if all(r == 0 for r in rcs):
+            return
+    except (OSError, AttributeError):
+        pass
+    a[::4096] = 0
 
 
 def _close(shm, unlink: bool):
@@ -291,6 +349,8 @@ def _worker(wid: int, device: int, runner_spec: Optional[str], tq, rq):
     views = SegmentViews()
 
     def alloc(nbytes: int):
+        if pool.n == 0:  # the first output: room for as many more, faulted in meanwhile
+            pool.prefill(4, int(1.25 * nbytes) + 4096)
         name = pool.take(nbytes)
         return np.frombuffer(pool.buf(name), np.uint8, count=nbytes)
     try:
@@ -358,7 +418,8 @@ class Fleet:
         self.n = len(devices)
         self.load = [0] * self.n  # jobs in flight per worker (submit: dealer thread, done: collector)
         self._load_lock = threading.Lock()
-        self.slots = threading.Semaphore(max(1, inflight) * self.n)
+        self.slots_total = max(1, inflight) * self.n
+        self.slots = threading.Semaphore(self.slots_total)
         self.needs_raw = False
         try:
             for _ in range(self.n):
@@ -465,6 +526,14 @@ def step5_stream_multi(in_bam: str, fasta: str, out_bam: Optional[str], devices:
     own_fleet = fleet is None
     fleet = Fleet(devices, runner, inflight) if own_fleet else fleet
     cpool = SegmentPool("c")  # batch images and messages; a batch's go back when its result arrives
+    # the segments the in-flight batches need, faulted in while the first chunk is read: a batch's
+    # images are about 0.75 x its record bytes (bounded by the batch base budget too)
+    est = int(0.75 * chunk_bytes)
+    if batch_bases:
+        est = min(est, int(1.7 * batch_bases))
+    nseg = fleet.slots_total + 2
+    cpool.prefill(nseg, int(1.25 * est) + 4096)
+    cpool.prefill(nseg, SegmentPool.MIN)
     views = SegmentViews()  # the workers' result segments
     stop = threading.Event()
     err: List[BaseException] = []
@@ -697,4 +766,6 @@ def step5_stream_multi(in_bam: str, fasta: str, out_bam: Optional[str], devices:
         raise err[0]
     if stats is not None:
         stats.update({k: round(v, 4) for k, v in T.items()})
+        stats["segments_created"] = cpool.n
+        stats["segments_created_MiB"] = round(cpool.created_bytes / 2**20, 1)
     return info
