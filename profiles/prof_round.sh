@@ -17,6 +17,8 @@ for c in ${CONFIGS:-C2 C3}; do
   find "$OUT/prof_$c" -name '*kernel_stats.csv' -exec cat {} \;
   # launch-set spans (the side streams overlap a set's dispatches: DESIGN.md 5.4)
   python profiles/trace_span.py "$(find "$OUT/prof_$c" -name '*kernel_trace.csv' | head -1)" "$OUT/prof_$c.log" "$OUT/span_$c.json" || exit 1
+  # the family kernels' rows of the trace (the whole trace is too large to keep)
+  python profiles/trace_filter.py "$(find "$OUT/prof_$c" -name '*kernel_trace.csv' | head -1)" "$OUT/trace_k_$c.csv" || exit 1
 done
 for c in ${CONFIGS:-C2 C3}; do
   [ -n "${SKIP_PMC:-}" ] && break
