@@ -867,8 +867,8 @@ void bsdc_split_fill(const uint32_t *rec, const uint32_t *ents, int64_t n_ent, i
                 uint32_t *w = part_recs + 4 * pk;
                 w[0] = (uint32_t)gi;
                 w[1] = dst;
-                w[2] = (uint32_t)pr[j].lmate[q];
-                w[3] = 0;
+                w[2] = (uint32_t)pr[j].lmate[q] | (rec[4 * gi + 2] & 0xFFFFu) << 16;  // | its length
+                w[3] = rec[4 * gi];  // its slot in the batch image (the staging copies it from there)
                 dst += (uint32_t)(((rec[4 * gi + 2] & 0xFFFF) + 2 + 3) & ~3u);
             }
         }

@@ -38,6 +38,9 @@
 namespace {
 
 constexpr int kWave = 64;
+#ifndef SPLIT_FIRST
+#define SPLIT_FIRST 0  // bsdc_run: launch the split families' part and join dispatches before the classes
+#endif
 #ifndef SMALL_PERSIST
 #define SMALL_PERSIST 0  // k_small: 1 = persistent waves taking families from a per-class counter
 #endif
@@ -1845,7 +1848,7 @@ __device__ void process_large(const KParams &P, uint8_t *A, uint8_t *s_tab, cons
 
         m.slot = PART ? pr.y : rc.x - off0;
         m.start = 1;
-        m.link = PART ? (rc.w & ~(uint32_t)BSDC_LINK_MATE_MASK) | pr.z : rc.w;  // (a part: its local mate)
+        m.link = PART ? (rc.w & ~(uint32_t)BSDC_LINK_MATE_MASK) | (pr.z & 0xFFFFu) : rc.w;  // (a part: its local mate)
         m.gidx = gi;
         const bool conv = do_convert && (m.link & BSDC_LINK_CONVERT);
         m.win = conv ? wn.x : 0u;
@@ -1865,22 +1868,24 @@ __device__ void process_large(const KParams &P, uint8_t *A, uint8_t *s_tab, cons
         if (tt + u * G < nch) store_chunk(tt + u * G, v[u]);
     if (tt < kTabBytesL / 16) reinterpret_cast<uint4 *>(s_tab)[tt] = tv;
     if (PART) {  // the part's records' slots, flattened over (record, 4 entries): U units per record
-        const int U = (B.max_len + 2 + 3) >> 2;
+        // (a part record's entry carries its batch slot and length: one load before the data)
+        const uint32_t U = (uint32_t)(B.max_len + 2 + 3) >> 2;
+        const uint32_t uinv = (uint32_t)((((uint64_t)1 << 32) + U - 1) / U);  // k / U = umulhi(k, uinv), k < 2^16
+        const bool fast_div = n * (int)U < 65536;
         constexpr int PU = 4;  // units in flight per thread
-        for (int k0 = tt; k0 < n * U; k0 += PU * G) {
+        for (int k0 = tt; k0 < n * (int)U; k0 += PU * G) {
             uint32_t q[PU], bb[PU], dst[PU];
 #pragma unroll
             for (int u = 0; u < PU; u++) {
                 const int k = k0 + u * G;
                 dst[u] = 0xFFFFFFFFu;
-                if (k >= n * U) continue;
-                const int r = k / U, j = k - r * U;
+                if (k >= n * (int)U) continue;
+                const uint32_t r = fast_div ? __umulhi((uint32_t)k, uinv) : (uint32_t)k / U, j = (uint32_t)k - r * U;
                 const uint4 pr = PR[r0 + r];
-                const uint4 rc = REC[pr.x];
-                if (4 * j >= (int)(((rc.z & 0xFFFF) + 2 + 3) & ~3u)) continue;
-                q[u] = *reinterpret_cast<const uint32_t *>(B.qual + rc.x + 4 * j);
-                bb[u] = *reinterpret_cast<const uint16_t *>(B.seq + (rc.x >> 1) + 2 * j);
-                dst[u] = pr.y + 4 * (uint32_t)j;
+                if (4 * j >= (((pr.z >> 16) + 2 + 3) & ~3u)) continue;
+                q[u] = *reinterpret_cast<const uint32_t *>(B.qual + pr.w + 4 * j);
+                bb[u] = *reinterpret_cast<const uint16_t *>(B.seq + (pr.w >> 1) + 2 * j);
+                dst[u] = pr.y + 4 * j;
             }
 #pragma unroll
             for (int u = 0; u < PU; u++) {
@@ -3116,6 +3121,33 @@ int32_t bsdc_run(bsdc_ctx *c, const bsdc_family_batch *b, bsdc_consensus *o, int
         }
         return c->side[i];
     };
+    // split families: their parts (k_large part mode, LDS arenas, 256 threads), then one join
+    // workgroup per family, in order on one stream
+    auto launch_split = [&]() {
+        if (rc != 0 || b->n_split_parts <= 0 || b->n_split_fams <= 0) return;
+        const int32_t a = b->split_part_arena;
+        const bool tg = (mode & BSDC_MODE_TAGS) != 0;
+        const hipStream_t ls = next_stream();
+        if (rc != 0) return;
+        const uint4 *pf = reinterpret_cast<const uint4 *>(b->split_parts);
+        const uint4 *sf = reinterpret_cast<const uint4 *>(b->split_fams);
+        const size_t jl = 8 * (size_t)o->stride;
+        if (tg) {
+            hipLaunchKernelGGL((k_large<true, kLargeThreads, true, true>), dim3((unsigned)b->n_split_parts), dim3(kLargeThreads),
+                               (size_t)a, ls, P, pf, b->n_split_parts, a, (int64_t)0);
+            hipLaunchKernelGGL((k_join<true>), dim3((unsigned)b->n_split_fams), dim3(kLargeThreadsBig), jl, ls, P, sf,
+                               b->n_split_fams);
+        } else {
+            hipLaunchKernelGGL((k_large<true, kLargeThreads, false, true>), dim3((unsigned)b->n_split_parts),
+                               dim3(kLargeThreads), (size_t)a, ls, P, pf, b->n_split_parts, a, (int64_t)0);
+            hipLaunchKernelGGL((k_join<false>), dim3((unsigned)b->n_split_fams), dim3(kLargeThreadsBig), jl, ls, P, sf,
+                               b->n_split_fams);
+        }
+        const hipError_t e = hipGetLastError();
+        if (e != hipSuccess) fail(e, "split launch");
+    };
+    // (SPLIT_FIRST: the part -> join chain, the longest dependency of the call, goes out first)
+    if (SPLIT_FIRST && !(mode & BSDC_MODE_SKIP_LARGE)) launch_split();
     if (SMALL_PERSIST && !(mode & BSDC_MODE_SKIP_SMALL)) {  // the class counters, before the fork
         const hipError_t e = hipMemsetAsync(c->ctr, 0, BSDC_SMALL_BUCKETS * sizeof(uint32_t), s);
         if (e != hipSuccess) fail(e, "hipMemsetAsync(counters)");
@@ -3194,31 +3226,7 @@ int32_t bsdc_run(bsdc_ctx *c, const bsdc_family_batch *b, bsdc_consensus *o, int
             }
             f += nf;
         }
-        // split families: their parts (k_large part mode, LDS arenas, 256 threads), then one join
-        // workgroup per family, in order on one stream
-        if (rc == 0 && b->n_split_parts > 0 && b->n_split_fams > 0) {
-            const int32_t a = b->split_part_arena;
-            const bool tg = (mode & BSDC_MODE_TAGS) != 0;
-            const hipStream_t ls = next_stream();
-            if (rc == 0) {
-                const uint4 *pf = reinterpret_cast<const uint4 *>(b->split_parts);
-                const uint4 *sf = reinterpret_cast<const uint4 *>(b->split_fams);
-                const size_t jl = 8 * (size_t)o->stride;
-                if (tg) {
-                    hipLaunchKernelGGL((k_large<true, kLargeThreads, true, true>), dim3((unsigned)b->n_split_parts), dim3(kLargeThreads),
-                                       (size_t)a, ls, P, pf, b->n_split_parts, a, (int64_t)0);
-                    hipLaunchKernelGGL((k_join<true>), dim3((unsigned)b->n_split_fams), dim3(kLargeThreadsBig), jl, ls, P, sf,
-                                       b->n_split_fams);
-                } else {
-                    hipLaunchKernelGGL((k_large<true, kLargeThreads, false, true>), dim3((unsigned)b->n_split_parts),
-                                       dim3(kLargeThreads), (size_t)a, ls, P, pf, b->n_split_parts, a, (int64_t)0);
-                    hipLaunchKernelGGL((k_join<false>), dim3((unsigned)b->n_split_fams), dim3(kLargeThreadsBig), jl, ls, P, sf,
-                                       b->n_split_fams);
-                }
-                const hipError_t e = hipGetLastError();
-                if (e != hipSuccess) fail(e, "split launch");
-            }
-        }
+        if (!SPLIT_FIRST) launch_split();
     }
     // join: `s` waits for every side stream used -- also after a failed launch, so that no work
     // already queued on a side stream outlives the caller's view of the batch's buffers

@@ -62,8 +62,9 @@ class SegmentPool:
 
     MIN = 16 << 20
 
-    def __init__(self, tag: str, keep: int = 8):
+    def __init__(self, tag: str, keep: int = 8, pinner: Optional["HostPinner"] = None):
         self.prefix = "bsdc%d_%s_%x" % (os.getpid(), tag, id(self) & 0xFFFFFF)
+        self.pinner = pinner  # (a GPU worker's: its segments are page-locked for DMA)
         self.segs: Dict[str, "shared_memory.SharedMemory"] = {}
         self.free: List[str] = []
         self.keep = keep
@@ -82,6 +83,8 @@ class SegmentPool:
             name = "%s_%d" % (self.prefix, self.n)
             self.n += 1
         shm = shared_memory.SharedMemory(name=name, create=True, size=max(int(nbytes * 1.25) + _ALIGN, self.MIN))
+        if self.pinner is not None:
+            self.pinner.pin(shm)
         with self.lock:
             self.segs[name] = shm
             self.created_bytes += shm.size
@@ -100,13 +103,15 @@ class SegmentPool:
                     self.n += 1
                 shm = shared_memory.SharedMemory(name=name, create=True, size=max(int(size), self.MIN))
                 _populate(shm, threads)
+                if self.pinner is not None:
+                    self.pinner.pin(shm)
                 with self.lock:
                     if not self.closed:
                         self.segs[name] = shm
                         self.created_bytes += shm.size
                         self.free.append(name)
                         continue
-                _close(shm, unlink=True)  # (the pool closed meanwhile)
+                self._drop(shm)  # (the pool closed meanwhile)
         t = threading.Thread(target=run, daemon=True)
         t.start()
         return t
@@ -121,8 +126,7 @@ class SegmentPool:
             while len(self.free) > self.keep:  # the smallest free ones go
                 x = min(self.free, key=lambda y: self.segs[y].size)
                 self.free.remove(x)
-                shm = self.segs.pop(x)
-                _close(shm, unlink=True)
+                self._drop(self.segs.pop(x))
 
     def buf(self, name: str) -> memoryview:
         return self.segs[name].buf
@@ -139,12 +143,17 @@ class SegmentPool:
                     return name, p - b
         return None
 
+    def _drop(self, shm):
+        if self.pinner is not None:
+            self.pinner.unpin(shm)
+        _close(shm, unlink=True)
+
     def close(self):
         with self.lock:
             self.closed = True
             segs, self.segs, self.free = self.segs, {}, []
         for shm in segs.values():
-            _close(shm, unlink=True)
+            self._drop(shm)
 
 
 _LINGER: list = []  # segments closed while numpy views still mapped them
@@ -194,8 +203,9 @@ def _close(shm, unlink: bool):
 class SegmentViews:
     """The other side's segments, opened once by name and kept (no remapping per message)."""
 
-    def __init__(self):
+    def __init__(self, pinner: Optional["HostPinner"] = None):
         self.open: Dict[str, "shared_memory.SharedMemory"] = {}
+        self.pinner = pinner
 
     def buf(self, name: str) -> memoryview:
         shm = self.open.get(name)
@@ -203,13 +213,51 @@ class SegmentViews:
             # (spawned workers share the coordinator's resource tracker, so attaching registers
             # nothing new, and a segment left behind by a dead process is still unlinked at exit)
             shm = shared_memory.SharedMemory(name=name)
+            if self.pinner is not None:
+                self.pinner.pin(shm)
             self.open[name] = shm
         return shm.buf
 
     def close(self):
         for shm in self.open.values():
+            if self.pinner is not None:
+                self.pinner.unpin(shm)
             _close(shm, unlink=False)
         self.open = {}
+
+
+class HostPinner:
+    """Page-locks a GPU worker's mappings of the shared segments (hipHostRegister through torch's
+    runtime binding), so a batch's arrays upload and its outputs come back by DMA straight from /
+    into the segments; a pageable copy goes through the runtime's staging buffers at a fraction of
+    the rate, on the worker's CPU.  Best effort: a mapping the runtime refuses stays pageable."""
+
+    def __init__(self, device: int):
+        self.device = device
+        self.done: Dict[int, int] = {}
+        self.lock = threading.Lock()
+
+    def pin(self, shm):
+        import torch
+        ptr = np.frombuffer(shm.buf, np.uint8).ctypes.data
+        with self.lock:
+            if ptr in self.done:
+                return
+            torch.cuda.set_device(self.device)  # (the calling thread's current device)
+            rc = torch._C._cudart.cudaHostRegister(ptr, shm.size, 0)
+            if int(rc) == 0:
+                self.done[ptr] = shm.size
+
+    def unpin(self, shm):
+        import torch
+        try:
+            ptr = np.frombuffer(shm.buf, np.uint8).ctypes.data
+        except (TypeError, ValueError):  # (already closed)
+            return
+        with self.lock:
+            if self.done.pop(ptr, None) is not None:
+                torch.cuda.set_device(self.device)
+                torch._C._cudart.cudaHostUnregister(ptr)
 
 
 def pack(obj, pool: Optional[SegmentPool] = None):
@@ -345,8 +393,9 @@ def _worker(wid: int, device: int, runner_spec: Optional[str], tq, rq):
     arrive as views of the coordinator's segments; outputs are fetched into this worker's own
     segments and travel back by name; the coordinator releases them once their chunk is written."""
     runner = None
-    pool = SegmentPool("w%d" % wid)
-    views = SegmentViews()
+    pinner = HostPinner(device) if runner_spec is None else None  # (the GPU runner only)
+    pool = SegmentPool("w%d" % wid, pinner=pinner)
+    views = SegmentViews(pinner)
 
     def alloc(nbytes: int):
         if pool.n == 0:  # the first output: room for as many more, faulted in meanwhile
@@ -369,6 +418,7 @@ def _worker(wid: int, device: int, runner_spec: Optional[str], tq, rq):
                 runner.load_reference(unpack(msg[1], views))
             elif kind == "batch":
                 _, key, fb_t, mode, tags, raw_t = msg
+                t0 = time.perf_counter()
                 fb = unpack(fb_t, views)
                 raw_sub = unpack(raw_t, views) if raw_t is not None else None
                 if isinstance(runner, GpuRunner):
@@ -376,18 +426,20 @@ def _worker(wid: int, device: int, runner_spec: Optional[str], tq, rq):
                 else:
                     out = runner.run_batch(fb, mode, tags, raw_sub)
                 del fb, raw_sub, fb_t, raw_t
+                t1 = time.perf_counter()
                 tree, segs = pack(out, pool)
-                rq.put(("batch", wid, key, tree, segs))
+                rq.put(("batch", wid, key, tree, segs,
+                        {"worker_run": t1 - t0, "worker_pack": time.perf_counter() - t1}))
             elif kind == "chunk":
                 _, key, raw_t, tags, batch_bases = msg
                 cons = runner.run_chunk(unpack(raw_t, views), tags, batch_bases)
                 del raw_t
                 tree, segs = pack(cons, pool)
-                rq.put(("chunk", wid, key, tree, segs))
+                rq.put(("chunk", wid, key, tree, segs, {}))
     except BaseException as e:  # noqa: BLE001 -- reported to the coordinator, which raises it
         rq.put(("error", wid, "%s: %s\n%s" % (type(e).__name__, e, traceback.format_exc())))
-        # stay until the coordinator ends the fleet: results this worker sent earlier hold shared
-        # memory whose descriptors the coordinator fetches from this process when it reads them
+        # stay until the coordinator ends the fleet: its segments unlinked now would leave the
+        # results it has not opened yet unreadable
         try:
             while tq.get(timeout=600) is not None:
                 pass
@@ -531,13 +583,14 @@ def step5_stream_multi(in_bam: str, fasta: str, out_bam: Optional[str], devices:
     est = int(0.75 * chunk_bytes)
     if batch_bases:
         est = min(est, int(1.7 * batch_bases))
-    nseg = fleet.slots_total + 2
+    nseg = fleet.slots_total + 3  # (+ the batches the planner has materialized ahead of the dealer)
     cpool.prefill(nseg, int(1.25 * est) + 4096)
     cpool.prefill(nseg, SegmentPool.MIN)
     views = SegmentViews()  # the workers' result segments
     stop = threading.Event()
     err: List[BaseException] = []
     raws: "queue.Queue" = queue.Queue(maxsize=1)
+    parsed: "queue.Queue" = queue.Queue(maxsize=1)
     chunks: "queue.Queue" = queue.Queue(maxsize=1)
     outs: "queue.Queue" = queue.Queue(maxsize=1)
     # chunk id -> {"raw", "n" (batches; None until the dealer has sent them all), "parts": {i:
@@ -554,6 +607,7 @@ def step5_stream_multi(in_bam: str, fasta: str, out_bam: Optional[str], devices:
             plock.notify_all()
 
     bufs = bam.BufferPool()  # a chunk's record and tag arrays, given back once it is written
+    R_: dict = {}  # the reader's steps (StreamChunk.decode timing)
 
     def decoder():  # cuts the next chunk while the planner decodes and plans the one before
         it = None
@@ -571,7 +625,7 @@ def step5_stream_multi(in_bam: str, fasta: str, out_bam: Optional[str], devices:
                 it.close()
             raws.put(None)
 
-    def planner():
+    def reader():  # parses a chunk's records while the planner forms the families of the one before
         try:
             while True:
                 t0 = time.perf_counter()
@@ -582,13 +636,10 @@ def step5_stream_multi(in_bam: str, fasta: str, out_bam: Optional[str], devices:
                     ch.discard()
                     continue  # drain to the decoder's None
                 t1 = time.perf_counter()
-                raw = ch.decode(threads, pool=bufs)[1]
-                t2 = time.perf_counter()
-                plan = pipeline.plan_families(raw, "full", ref)
-                T["plan"] += time.perf_counter() - t2
-                T["parse"] = T.get("parse", 0.0) + t2 - t1
+                raw = ch.decode(threads, R_, bufs)[1]
+                T["parse"] = T.get("parse", 0.0) + time.perf_counter() - t1
                 T["decode"] += t1 - t0  # the wait for the decoder
-                chunks.put((raw, plan))
+                parsed.put(raw)
         except BaseException as e:  # noqa: BLE001
             fail(e)
             while True:
@@ -596,6 +647,45 @@ def step5_stream_multi(in_bam: str, fasta: str, out_bam: Optional[str], devices:
                 if ch is None:
                     break
                 ch.discard()
+        finally:
+            parsed.put(None)
+
+    def materialize(plan, a: int, b: int):
+        """-> (the batch without its host bookkeeping, its _FamilyIndex, the segments it uses)."""
+        img = []
+
+        def images(n_slots: int):  # the family images straight into a shared segment
+            ns = (n_slots // 2 + 255) // 256 * 256
+            img.append(cpool.take(ns + n_slots + 256))
+            buf = np.frombuffer(cpool.buf(img[-1]), np.uint8)
+            return buf[:ns], buf[ns:ns + n_slots]
+        fb = pipeline.materialize(plan, a, b, images=images)
+        index = _FamilyIndex(fb.fam_mi.copy(), fb.fam_off.astype(np.int64), fb.src.astype(np.int64))
+        # the worker needs the device arrays only (host bookkeeping stays here)
+        slim = dataclasses.replace(fb, src=np.zeros(0, np.int64), fam_mi=np.zeros(0, np.int32),
+                                   t2_rank=np.zeros(0, np.int64), rec_tid=np.zeros(0, np.int32))
+        return slim, index, img
+
+    def planner():  # forms a chunk's families and materializes its batches ahead of the dealer
+        try:
+            while True:
+                raw = parsed.get()
+                if raw is None:
+                    break
+                if stop.is_set():
+                    continue  # drain to the reader's None
+                t0 = time.perf_counter()
+                plan = pipeline.plan_families(raw, "full", ref)
+                t1 = time.perf_counter()
+                T["plan"] += t1 - t0
+                batches = None if plan.split_ext else [materialize(plan, a, b)
+                                                       for a, b in pipeline.plan_ranges(plan, batch_bases)]
+                T["materialize"] += time.perf_counter() - t1
+                chunks.put((raw, plan, batches))
+        except BaseException as e:  # noqa: BLE001
+            fail(e)
+            while parsed.get() is not None:
+                pass
         finally:
             chunks.put(None)
 
@@ -620,6 +710,8 @@ def step5_stream_multi(in_bam: str, fasta: str, out_bam: Optional[str], devices:
                 if m is None:
                     continue
                 kind, wid, (cid, i), res = m[0], m[1], m[2], unpack(m[3], views)
+                for k, v in m[5].items():  # (the workers' busy time, summed)
+                    T[k] = T.get(k, 0.0) + v
                 with plock:
                     c = pend[cid]
                     c["parts"][i] = pipeline.consensus_from_output(c["index"].pop(i), res) if kind == "batch" else res
@@ -681,7 +773,7 @@ def step5_stream_multi(in_bam: str, fasta: str, out_bam: Optional[str], devices:
             while outs.get() is not None:
                 pass
 
-    workers = [threading.Thread(target=f, daemon=True) for f in (decoder, planner, collector, writer)]
+    workers = [threading.Thread(target=f, daemon=True) for f in (decoder, reader, planner, collector, writer)]
     drained = False
     try:
         fleet.broadcast(("ref", pack(dataclasses.replace(ref, letters={}), cpool)[0]))
@@ -693,7 +785,7 @@ def step5_stream_multi(in_bam: str, fasta: str, out_bam: Optional[str], devices:
             if item is None:
                 drained = True
                 break
-            raw, plan = item
+            raw, plan, batches = item
             info["records_in"] += raw.n
             info["chunks"] += 1
             with plock:  # a bounded number of chunks between the dealer and the writer
@@ -708,37 +800,24 @@ def step5_stream_multi(in_bam: str, fasta: str, out_bam: Optional[str], devices:
                 if fleet.submit(("chunk", (cid, 0), t, tg, batch_bases), stop) >= 0:
                     n = 1
             else:
-                for a, b in pipeline.plan_ranges(plan, batch_bases):
-                    t0 = time.perf_counter()
-                    img = []
-
-                    def images(n_slots: int):  # the family images straight into a shared segment
-                        ns = (n_slots // 2 + 255) // 256 * 256
-                        img.append(cpool.take(ns + n_slots + 256))
-                        buf = np.frombuffer(cpool.buf(img[-1]), np.uint8)
-                        return buf[:ns], buf[ns:ns + n_slots]
-                    fb = pipeline.materialize(plan, a, b, images=images)
-                    T["materialize"] += time.perf_counter() - t0
-                    raw_sub = R.take(raw, fb.src.astype(np.int64)) if fleet.needs_raw else None
-                    # the worker needs the device arrays only (host bookkeeping stays here)
-                    slim = dataclasses.replace(fb, src=np.zeros(0, np.int64), fam_mi=np.zeros(0, np.int32),
-                                               t2_rank=np.zeros(0, np.int64), rec_tid=np.zeros(0, np.int32))
+                for slim, index, img in batches:
+                    raw_sub = R.take(raw, index.src) if fleet.needs_raw else None
                     t0 = time.perf_counter()
                     t, segs = pack(slim, cpool)
                     rt, rsegs = pack(raw_sub, cpool) if raw_sub is not None else (None, [])
                     T["pack"] = T.get("pack", 0.0) + time.perf_counter() - t0
                     with plock:
-                        pend[cid]["index"][n] = _FamilyIndex(fb.fam_mi.copy(), fb.fam_off.astype(np.int64),
-                                                             fb.src.astype(np.int64))
+                        pend[cid]["index"][n] = index
                         pend[cid]["in"][n] = sorted(set(segs) | set(rsegs) | set(img))
                     t0 = time.perf_counter()
                     w = fleet.submit(("batch", (cid, n), t, mode, tg, rt), stop)
                     T["submit_wait"] += time.perf_counter() - t0
-                    del fb, slim, raw_sub
+                    del slim, raw_sub
                     if w < 0:
                         break
                     n += 1
                     info["batches"] += 1
+                del batches
             with plock:
                 pend[cid]["n"] = n
                 plock.notify_all()
@@ -766,6 +845,7 @@ def step5_stream_multi(in_bam: str, fasta: str, out_bam: Optional[str], devices:
         raise err[0]
     if stats is not None:
         stats.update({k: round(v, 4) for k, v in T.items()})
+        stats.update({"reader_" + k: round(v, 4) for k, v in R_.items()})
         stats["segments_created"] = cpool.n
         stats["segments_created_MiB"] = round(cpool.created_bytes / 2**20, 1)
     return info

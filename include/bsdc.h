@@ -103,7 +103,8 @@ typedef struct {
     const uint32_t *split_parts; /* 4 words per part: family, first part record, n_rec, image bytes */
     int64_t n_split_parts;
     const uint32_t *split_part_recs; /* 4 words per part record: batch record, slot in the part's image,
-                                        part-local index of its mate (0xFFFF: none), 0 */
+                                        part-local index of its mate (0xFFFF: none) | record length << 16,
+                                        slot in the batch image */
     const uint32_t *split_fams;  /* 8 words per family: family, first record, n_rec, image bytes, first part,
                                     parts, fallback arena offset in scratch / 16, fallback arena bytes */
     int64_t n_split_fams;

@@ -19,6 +19,7 @@ for c in ${CONFIGS:-C2 C3}; do
   python profiles/trace_span.py "$(find "$OUT/prof_$c" -name '*kernel_trace.csv' | head -1)" "$OUT/prof_$c.log" "$OUT/span_$c.json" || exit 1
   # the family kernels' rows of the trace (the whole trace is too large to keep)
   python profiles/trace_filter.py "$(find "$OUT/prof_$c" -name '*kernel_trace.csv' | head -1)" "$OUT/trace_k_$c.csv" || exit 1
+  find "$OUT/prof_$c" -type f -size +2M -delete
 done
 for c in ${CONFIGS:-C2 C3}; do
   [ -n "${SKIP_PMC:-}" ] && break

@@ -6,6 +6,7 @@ set -u -o pipefail
 mkdir -p gpurun_out/r4d
 BSDC_LIB_PATH=$(realpath ablibs/libbsdc_nofork.so) CONFIGS="C4 C3" SKIP_PMC=1 bash profiles/prof_round.sh r4d/nofork || exit 1
 BSDC_LIB_PATH=$(realpath ablibs/libbsdc_nofork.so) BSDC_PART_CAP=0 CONFIGS="C4" SKIP_PMC=1 bash profiles/prof_round.sh r4d/nofork_nopart || exit 1
+CFGS="C4" bash profiles/ab_r4.sh r4d base=- splitfirst=ablibs/libbsdc_splitfirst.so nopart=-:BSDC_PART_CAP=0 || exit 1
 bash profiles/collect_pmc.sh gpurun_out/r4d/pmc_C4 --config C4 || exit 1
 python profiles/pmc_bench_summary.py gpurun_out/r4d/pmc_C4 gpurun_out/r4d/pmc_C4.json > /dev/null || exit 1
 find gpurun_out/r4d -type f -size +2M -delete

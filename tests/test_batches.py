@@ -61,3 +61,37 @@ def test_split_partner_marks_both_families():
     plan = batch.plan_families(raw, "full", s.ref)
     assert plan.split_ext and 1 <= int(plan.fam_split.sum()) <= 2
     assert batch.build_family_batch(raw, "full", s.ref).split_ext
+
+
+def test_split_part_records_cover_each_family_once(monkeypatch):
+    """k_large part mode's host cut (bsdc_split_count / bsdc_split_fill via batch.split_hbm_bucket):
+    every record of a cut family sits in exactly one part, whole templates stay together (a part-
+    local mate points at the record's mate), the part images are the records' slots back to back,
+    and each part record carries its length and batch slot (what the part staging copies)."""
+    from bsseqconsensusreads_amd import batch as B, synth
+    s = synth.generate("C3", 300, seed=5, device="cpu", genome_len=200_000)
+    fb = B.build_family_batch(s.raw, "full", s.ref)
+    monkeypatch.setattr(B, "SPLIT_FROM", 0)  # every large bucket (C3 has no HBM-arena family)
+    fb = B.split_hbm_bucket(fb, part_cap=12_000)
+    sf = fb.split_fams.astype(np.int64)
+    assert sf.shape[0] > 0
+    parts, prec = fb.split_parts.astype(np.int64), fb.split_part_recs.astype(np.int64)
+    L = (fb.rec_lenflag & 0xFFFF).astype(np.int64)
+    for f in sf:
+        fam, r0, n, p0, npart = f[0], f[1], f[2], f[4], f[5]
+        seen = []
+        for p in parts[p0:p0 + npart]:
+            assert p[0] == fam
+            recs = prec[p[1]:p[1] + p[2]]
+            dst = 0
+            for li, w in enumerate(recs):
+                gi = int(w[0])
+                seen.append(gi)
+                assert w[1] == dst and (w[2] >> 16) == L[gi] and w[3] == fb.rec_off[gi]
+                dst += (L[gi] + 2 + 3) // 4 * 4
+                lm = int(w[2] & 0xFFFF)
+                gm = int(fb.rec_link[gi] & 0xFFFF)
+                if gm != 0xFFFF:  # the mate is in the same part, at its local index
+                    assert lm != 0xFFFF and recs[lm][0] == r0 + gm
+            assert p[3] == (dst + 31) // 32 * 32  # (images are whole 32-entry chunks)
+        assert sorted(seen) == list(range(r0, r0 + n))
