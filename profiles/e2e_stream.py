@@ -58,6 +58,10 @@ def child(args):
         from bsseqconsensusreads_amd import fleet
         ts = time.perf_counter()
         fl = fleet.Fleet([0] * args.workers)  # started (spawn, import, HIP init) outside the clock
+        if args.mode == "fleet_gpubgzf":  # (the writer's GPU runtime too, as the stream's engine is)
+            import torch
+            torch.zeros(1, device="cuda:0")
+            torch.cuda.synchronize()
         t0 = time.perf_counter()
         try:
             info = fleet.step5_stream_multi(args.inp, args.fa, args.out, [0] * args.workers, threads=args.threads,
