@@ -48,13 +48,15 @@ LARGE_LDS_MAX = 158912  # BSDC_LARGE_LDS_MAX: 160 KB - the tables - the kernel's
 # the largest arena that still fits k = 5, 4, 3, 2, 1 workgroups per CU (5 is the VGPR limit)
 LARGE_BUCKETS = tuple((160 * 1024 // k - LDS_TABLES - 256) // 16 * 16 for k in (5, 4, 3, 2, 1))  # + 1 scratch bucket
 assert LARGE_BUCKETS[-1] == LARGE_LDS_MAX
-# k_large part mode (include/bsdc.h split_parts): the HBM-scratch bucket's families are cut into
-# parts whose arena fits this (3 workgroups of 256 threads per CU); BSDC_PART_CAP=0 turns it off
-PART_CAP = int(os.environ.get("BSDC_PART_CAP", str(LARGE_BUCKETS[2])))
+# k_large part mode (include/bsdc.h split_parts): the families of the 1-per-CU class and of the
+# HBM-scratch bucket are cut into parts whose arena fits the 5-per-CU class (profiles/r04/ab_g,
+# ab_h: smaller parts keep more workgroups in flight; cutting the 2-per-CU class too loses);
+# BSDC_PART_CAP=0 turns it off
+PART_CAP = int(os.environ.get("BSDC_PART_CAP", str(LARGE_BUCKETS[0])))
 MAX_PART_REC = 254  # a part's per-set sums stay int32 and its read counts fit a byte
-# the first large bucket whose families are cut into parts (default: the HBM-scratch bucket only;
-# BSDC_SPLIT_FROM=3 also cuts the 2- and 1-per-CU LDS classes -- profiling A/B)
-SPLIT_FROM = int(os.environ.get("BSDC_SPLIT_FROM", str(len(LARGE_BUCKETS))))
+# the first large bucket whose families are cut into parts: 4 = the 1-per-CU class and the
+# HBM-scratch bucket (BSDC_SPLIT_FROM: profiling A/B)
+SPLIT_FROM = int(os.environ.get("BSDC_SPLIT_FROM", str(len(LARGE_BUCKETS) - 1)))
 
 
 def round16(x):
@@ -650,9 +652,10 @@ def materialize(plan: FamilyPlan, f0: int, f1: int, small_cap: int = SMALL_ARENA
 
 
 def split_hbm_bucket(fb: FamilyBatch, part_cap: Optional[int] = None, threads: int = 0) -> FamilyBatch:
-    """k_large's part mode (include/bsdc.h): the families of the HBM-scratch bucket that can be
-    cut between templates (no complex cigar, no tool-2 role) become parts of at most part_cap LDS
-    bytes, run in LDS, and one join workgroup per family; the rest stay in the bucket.  In place."""
+    """k_large's part mode (include/bsdc.h): the families of the large buckets from SPLIT_FROM on
+    (the 1-per-CU class and the HBM-scratch one) that can be cut between templates (no complex
+    cigar, no tool-2 role) become parts of at most part_cap LDS bytes, run in LDS, and one join
+    workgroup per family; the rest stay in their buckets.  In place."""
     from . import hostplan
     cap = PART_CAP if part_cap is None else int(part_cap)
     lo = min(max(SPLIT_FROM, 0), len(fb.large_buckets) - 1)
