@@ -167,7 +167,8 @@ class FamilyBatch:
         arenas = int(sf[:, 7].astype(np.int64).sum()) if sf.shape[0] else 0
         poff = int(round16(base + arenas))
         npart = int(self.split_parts.shape[0])
-        psz = int(round16(32 * npart)) + npart * 4 * self.stride * 20 if npart else 0
+        # + the per-family part counters of the fused join (u32 each)
+        psz = int(round16(32 * npart)) + npart * 4 * self.stride * 20 + int(round16(4 * sf.shape[0])) if npart else 0
         total = poff + psz
         return (total + 256 if total else 0), base, poff
 
@@ -697,6 +698,7 @@ def split_hbm_bucket(fb: FamilyBatch, part_cap: Optional[int] = None, threads: i
     off[1:] = np.cumsum(need[:-1])
     sf[:, 6] = off // 16
     sf[:, 7] = need
+    parts[:, 2] |= (np.repeat(np.arange(ce.shape[0], dtype=np.int64), nparts[cut]) << 8).astype(np.uint32)  # | split family
     fb.split_parts = parts
     fb.split_part_recs = part_recs
     fb.split_fams = sf.astype(np.uint32)

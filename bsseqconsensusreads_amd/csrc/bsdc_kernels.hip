@@ -38,6 +38,9 @@
 namespace {
 
 constexpr int kWave = 64;
+#ifndef JOIN_FUSED
+#define JOIN_FUSED 0  // part mode: the last part of a family to finish joins it (no k_join dispatch)
+#endif
 #ifndef SPLIT_FIRST
 #define SPLIT_FIRST 0  // bsdc_run: launch the split families' part and join dispatches before the classes
 #endif
@@ -1766,6 +1769,15 @@ __device__ void large_emit(const KParams &P, uint32_t fam, const int *cnt, const
 // The parts' sums in scratch (include/bsdc.h split_partial_off): header [part][8] int32 (set
 // reads, set lengths), then int32x4 likelihood sums and u8x4 A/C/G/T read counts per (part, set,
 // column), the column pitch being the output stride.
+#if JOIN_FUSED
+#define JOIN_ATTR __attribute__((noinline))  // (its own register allocation, not the part kernel's)
+#else
+#define JOIN_ATTR
+#endif
+template <int G, bool TAGS>
+__device__ JOIN_ATTR void join_family(const KParams &P, uint4 e0, uint4 e1, uint8_t *rows, uint8_t *tab, int *red,
+                                      int *s_cnt, int *s_lc, int *s_cur, int *s_tie);
+
 struct PartSums {
     int32_t *head;
     uint4 *sum;
@@ -1778,7 +1790,9 @@ struct PartSums {
         head = reinterpret_cast<int32_t *>(b);
         sum = reinterpret_cast<uint4 *>(b + round16(32 * np));
         cnt = reinterpret_cast<uint32_t *>(b + round16(32 * np) + 16 * 4 * np * (int64_t)pitch);
+        done = reinterpret_cast<uint32_t *>(b + round16(32 * np) + 20 * 4 * np * (int64_t)pitch);
     }
+    uint32_t *done;  // (JOIN_FUSED) parts finished, per split family; zeroed before the launch
     __device__ __forceinline__ int64_t at(int64_t part, int s, int col) const { return (4 * part + s) * (int64_t)pitch + col; }
 };
 
@@ -1792,7 +1806,7 @@ __device__ void process_large(const KParams &P, uint8_t *A, uint8_t *s_tab, cons
     const bsdc_family_batch &B = P.B;
     // list entry: family, first record (a part: its first part record), n, image bytes
     const uint32_t fam = ent.x, r0 = ent.y, img = ent.w;
-    const int n = (int)ent.z;
+    const int n = PART ? (int)(ent.z & 0xFFu) : (int)ent.z;  // (a part: | its split family << 8)
     const bool do_convert = P.mode & BSDC_MODE_CONVERT;
     const bool do_extend = P.mode & BSDC_MODE_EXTEND;
     const bool do_vote = P.mode & BSDC_MODE_VOTE;
@@ -2624,8 +2638,21 @@ __device__ void process_large(const KParams &P, uint8_t *A, uint8_t *s_tab, cons
     }
     __syncthreads();
     if (stop == 7) return;
-    if (PART) {  // the part's set sizes and lengths; k_join does the rest
+    if (PART) {  // the part's set sizes and lengths; k_join (or the family's last part) does the rest
         if (tt < 8) PartSums(P).head[8 * (int64_t)blockIdx.x + tt] = tt < 4 ? cnt[tt] : lcv[tt - 4];
+        if (JOIN_FUSED) {
+            __threadfence();  // (release: this part's sums and header, device-wide)
+            __syncthreads();
+            const uint32_t sfi = ent.z >> 8;
+            const uint4 *sf = reinterpret_cast<const uint4 *>(B.split_fams);
+            const uint4 e0 = sf[2 * (int64_t)sfi], e1 = sf[2 * (int64_t)sfi + 1];
+            if (tt == 0) s_cur[0] = atomicAdd(PartSums(P).done + sfi, 1u) + 1 == e1.y ? 1 : 0;
+            __syncthreads();
+            if (s_cur[0]) {
+                __threadfence();  // (acquire: the other parts' sums)
+                join_family<G, TAGS>(P, e0, e1, A, s_tab, red, s_cnt, s_lc, s_cur, s_cur + 7);
+            }
+        }
         return;
     }
 
@@ -2666,27 +2693,17 @@ __global__ __launch_bounds__(G, G == 256 ? 5 : 2) void k_large(KParams P, const 
     process_large<G, TAGS, PART>(P, A, reinterpret_cast<uint8_t *>(&s_tab), lr, thr, fams[i], red, s_cnt, s_lc, s_cur);
 }
 
-// One workgroup per split family (include/bsdc.h): the parts' sums and counts added up per
-// (set, column) -- exact integers, so the parts' order does not matter --, the single-strand call
-// of each column (as k_large's resolve), then duplex combine and output (large_emit).  A near-tie
-// column needs fgbio's read-order double sums over all the set's reads, which the parts did not
-// keep: then the family runs whole in its HBM fallback arena (process_large), as the HBM bucket does.
-template <bool TAGS>
-__global__ __launch_bounds__(kLargeThreadsBig, 2) void k_join(KParams P, const uint4 *sfams, int64_t nsf) {
-    constexpr int G = kLargeThreadsBig;
-    extern __shared__ __attribute__((aligned(16))) uint8_t smem[];  // single-strand rows: bases, quals [4][stride]
-    __shared__ __attribute__((aligned(16))) TablesL s_tab;
-    __shared__ int red[2 * G / kWave];
-    __shared__ int s_cnt[4], s_lc[4], s_cur[8];
-    __shared__ int s_tie;
+// A split family's join on one workgroup of G threads (k_join, or the family's last part with
+// JOIN_FUSED): rows = 8 x stride bytes of LDS for its single-strand rows, tab = the TablesL copy.
+template <int G, bool TAGS>
+__device__ JOIN_ATTR void join_family(const KParams &P, uint4 e0, uint4 e1, uint8_t *rows, uint8_t *tab, int *red,
+                                      int *s_cnt, int *s_lc, int *s_cur, int *s_tie) {
     const int tt = threadIdx.x;
-    const int64_t i = blockIdx.x;
-    if (i >= nsf) return;
-    const uint4 e0 = sfams[2 * i], e1 = sfams[2 * i + 1];  // the family's entry; first part, parts, fallback arena
-    load_tables<kTabBytesL>(&P.tab->t, reinterpret_cast<uint8_t *>(&s_tab));
+    const TablesL &T = *reinterpret_cast<const TablesL *>(tab);
     const PartSums ps(P);
     const int64_t p0 = e1.x;
     const int np = (int)e1.y;
+    __syncthreads();  // (s_cnt / s_lc / s_tie are the caller's too)
     if (tt < 4) {
         int c = 0, l = 0;
         for (int p = 0; p < np; p++) {
@@ -2696,7 +2713,7 @@ __global__ __launch_bounds__(kLargeThreadsBig, 2) void k_join(KParams P, const u
         s_cnt[tt] = c;
         s_lc[tt] = c > 0 ? l : 0;
     }
-    if (tt == 0) s_tie = 0;
+    if (tt == 0) *s_tie = 0;
     __syncthreads();
     int cnt[4], lcv[4];
     for (int s = 0; s < 4; s++) {
@@ -2704,7 +2721,7 @@ __global__ __launch_bounds__(kLargeThreadsBig, 2) void k_join(KParams P, const u
         lcv[s] = s_lc[s];
     }
     const int pitch = P.O.stride;
-    uint8_t *ssb = smem, *ssq = smem + 4 * pitch;
+    uint8_t *ssb = rows, *ssq = rows + 4 * pitch;
     const int ntot = lcv[0] + lcv[1] + lcv[2] + lcv[3];
     for (int k = tt; k < ntot; k += G) {
         int s = 0, c = k;
@@ -2729,7 +2746,7 @@ __global__ __launch_bounds__(kLargeThreadsBig, 2) void k_join(KParams P, const u
         }
         const int best = first_max4(D0, D1, D2, D3);
         if (near_tie(D0, D1, D2, D3, best, cnt[s])) {
-            s_tie = 1;
+            *s_tie = 1;
             continue;
         }
         const long long Db = best == 0 ? D0 : best == 1 ? D1 : best == 2 ? D2 : D3;
@@ -2738,7 +2755,7 @@ __global__ __launch_bounds__(kLargeThreadsBig, 2) void k_join(KParams P, const u
         if (best != 1) S += term(D1 - Db);
         if (best != 2) S += term(D2 - Db);
         if (best != 3) S += term(D3 - Db);
-        const int Q = phred_of(S, s_tab.thr);
+        const int Q = phred_of(S, T.thr);
         const uint32_t depth = n0 + n1 + n2 + n3;
         const bool nocall = depth == 0 || Q < P.qmin;
         ssb[s * pitch + c] = nocall ? (uint8_t)kN : (uint8_t)(1u << best);
@@ -2751,14 +2768,34 @@ __global__ __launch_bounds__(kLargeThreadsBig, 2) void k_join(KParams P, const u
         }
     }
     __syncthreads();
-    if (s_tie) {  // (rare) the whole family in its HBM arena, fgbio's pick on the near ties
+    if (*s_tie) {  // (rare) the whole family in its HBM arena, fgbio's pick on the near ties
         if (tt == 0) s_cnt[0] = 0;
         __syncthreads();
-        process_large<G, TAGS, false>(P, P.O.scratch + 16 * (int64_t)e1.z, reinterpret_cast<uint8_t *>(&s_tab), s_tab.lr,
-                                      s_tab.thr, e0, red, s_cnt, s_lc, s_cur);
+        process_large<G, TAGS, false>(P, P.O.scratch + 16 * (int64_t)e1.z, tab, T.lr, T.thr, e0, red, s_cnt, s_lc,
+                                      s_cur);
         return;
     }
     large_emit<G, TAGS>(P, e0.x, cnt, lcv, ssb, ssq, pitch, true);
+}
+
+// One workgroup per split family (include/bsdc.h): the parts' sums and counts added up per
+// (set, column) -- exact integers, so the parts' order does not matter --, the single-strand call
+// of each column (as k_large's resolve), then duplex combine and output (large_emit).  A near-tie
+// column needs fgbio's read-order double sums over all the set's reads, which the parts did not
+// keep: then the family runs whole in its HBM fallback arena (process_large), as the HBM bucket does.
+template <bool TAGS>
+__global__ __launch_bounds__(kLargeThreadsBig, 2) void k_join(KParams P, const uint4 *sfams, int64_t nsf) {
+    constexpr int G = kLargeThreadsBig;
+    extern __shared__ __attribute__((aligned(16))) uint8_t smem[];  // single-strand rows: bases, quals [4][stride]
+    __shared__ __attribute__((aligned(16))) TablesL s_tab;
+    __shared__ int red[2 * G / kWave];
+    __shared__ int s_cnt[4], s_lc[4], s_cur[8];
+    __shared__ int s_tie;
+    const int64_t i = blockIdx.x;
+    if (i >= nsf) return;
+    load_tables<kTabBytesL>(&P.tab->t, reinterpret_cast<uint8_t *>(&s_tab));
+    join_family<G, TAGS>(P, sfams[2 * i], sfams[2 * i + 1], smem, reinterpret_cast<uint8_t *>(&s_tab), red, s_cnt, s_lc,
+                         s_cur, &s_tie);
 }
 
 }  // namespace
@@ -3050,7 +3087,8 @@ int32_t bsdc_run(bsdc_ctx *c, const bsdc_family_batch *b, bsdc_consensus *o, int
         return BSDC_EINVAL;
     }
     if (b->n_split_parts > 0 && (b->split_part_arena % 16 || b->split_part_arena <= 0 ||
-                                 b->split_part_arena > BSDC_LARGE_LDS_MAX || !o->scratch || !b->split_parts || !b->split_fams)) {
+                                 b->split_part_arena > BSDC_LARGE_LDS_MAX || !o->scratch || !b->split_parts || !b->split_fams ||
+                                 (JOIN_FUSED && b->split_part_arena < 8 * o->stride))) {
         c->err = "bad split families";
         return BSDC_EINVAL;
     }
@@ -3132,16 +3170,27 @@ int32_t bsdc_run(bsdc_ctx *c, const bsdc_family_batch *b, bsdc_consensus *o, int
         const uint4 *pf = reinterpret_cast<const uint4 *>(b->split_parts);
         const uint4 *sf = reinterpret_cast<const uint4 *>(b->split_fams);
         const size_t jl = 8 * (size_t)o->stride;
+        if (JOIN_FUSED) {  // the per-family part counters (PartSums::done), zeroed on the parts' stream
+            const int64_t np = b->n_split_parts;
+            uint8_t *done = o->scratch + b->split_partial_off + round16(32 * np) + 80 * np * (int64_t)o->stride;
+            const hipError_t e = hipMemsetAsync(done, 0, 4 * (size_t)b->n_split_fams, ls);
+            if (e != hipSuccess) {
+                fail(e, "hipMemsetAsync(part counters)");
+                return;
+            }
+        }
         if (tg) {
             hipLaunchKernelGGL((k_large<true, kLargeThreads, true, true>), dim3((unsigned)b->n_split_parts), dim3(kLargeThreads),
                                (size_t)a, ls, P, pf, b->n_split_parts, a, (int64_t)0);
-            hipLaunchKernelGGL((k_join<true>), dim3((unsigned)b->n_split_fams), dim3(kLargeThreadsBig), jl, ls, P, sf,
-                               b->n_split_fams);
+            if (!JOIN_FUSED)
+                hipLaunchKernelGGL((k_join<true>), dim3((unsigned)b->n_split_fams), dim3(kLargeThreadsBig), jl, ls, P, sf,
+                                   b->n_split_fams);
         } else {
             hipLaunchKernelGGL((k_large<true, kLargeThreads, false, true>), dim3((unsigned)b->n_split_parts),
                                dim3(kLargeThreads), (size_t)a, ls, P, pf, b->n_split_parts, a, (int64_t)0);
-            hipLaunchKernelGGL((k_join<false>), dim3((unsigned)b->n_split_fams), dim3(kLargeThreadsBig), jl, ls, P, sf,
-                               b->n_split_fams);
+            if (!JOIN_FUSED)
+                hipLaunchKernelGGL((k_join<false>), dim3((unsigned)b->n_split_fams), dim3(kLargeThreadsBig), jl, ls, P, sf,
+                                   b->n_split_fams);
         }
         const hipError_t e = hipGetLastError();
         if (e != hipSuccess) fail(e, "split launch");

@@ -100,7 +100,8 @@ typedef struct {
      * runs everything up to the vote in LDS and leaves its per-column likelihood sums and read
      * counts in `scratch`; one workgroup per family then adds the parts up, calls, combines and
      * writes (a near-tie column -- rare -- makes that family run whole in its HBM arena instead). */
-    const uint32_t *split_parts; /* 4 words per part: family, first part record, n_rec, image bytes */
+    const uint32_t *split_parts; /* 4 words per part: family, first part record, n_rec (< 256) | its row in
+                                    split_fams << 8, image bytes */
     int64_t n_split_parts;
     const uint32_t *split_part_recs; /* 4 words per part record: batch record, slot in the part's image,
                                         part-local index of its mate (0xFFFF: none) | record length << 16,
@@ -109,7 +110,8 @@ typedef struct {
                                     parts, fallback arena offset in scratch / 16, fallback arena bytes */
     int64_t n_split_fams;
     int64_t split_partial_off;   /* scratch offset of the parts' sums: [part][8] int32 (set reads, set
-                                    lengths), then [part][4][stride] int32x4 sums, [part][4][stride] u8x4 counts */
+                                    lengths), then [part][4][stride] int32x4 sums, [part][4][stride] u8x4 counts,
+                                    then one u32 per split family (parts finished: the library's own) */
 } bsdc_family_batch;
 
 /* Outputs (device pointers).  Consensus slot (f, end) holds `stride` bases. */

@@ -77,12 +77,12 @@ def test_split_part_records_cover_each_family_once(monkeypatch):
     assert sf.shape[0] > 0
     parts, prec = fb.split_parts.astype(np.int64), fb.split_part_recs.astype(np.int64)
     L = (fb.rec_lenflag & 0xFFFF).astype(np.int64)
-    for f in sf:
+    for row, f in enumerate(sf):
         fam, r0, n, p0, npart = f[0], f[1], f[2], f[4], f[5]
         seen = []
         for p in parts[p0:p0 + npart]:
-            assert p[0] == fam
-            recs = prec[p[1]:p[1] + p[2]]
+            assert p[0] == fam and p[2] >> 8 == row  # (the part knows its split family's row)
+            recs = prec[p[1]:p[1] + (p[2] & 0xFF)]
             dst = 0
             for li, w in enumerate(recs):
                 gi = int(w[0])
