@@ -38,9 +38,6 @@
 namespace {
 
 constexpr int kWave = 64;
-#ifndef JOIN_FUSED
-#define JOIN_FUSED 0  // part mode: the last part of a family to finish joins it (no k_join dispatch)
-#endif
 #ifndef SPLIT_FIRST
 #define SPLIT_FIRST 0  // bsdc_run: launch the split families' part and join dispatches before the classes
 #endif
@@ -1769,14 +1766,9 @@ __device__ void large_emit(const KParams &P, uint32_t fam, const int *cnt, const
 // The parts' sums in scratch (include/bsdc.h split_partial_off): header [part][8] int32 (set
 // reads, set lengths), then int32x4 likelihood sums and u8x4 A/C/G/T read counts per (part, set,
 // column), the column pitch being the output stride.
-#if JOIN_FUSED
-#define JOIN_ATTR __attribute__((noinline))  // (its own register allocation, not the part kernel's)
-#else
-#define JOIN_ATTR
-#endif
 template <int G, bool TAGS>
-__device__ JOIN_ATTR void join_family(const KParams &P, uint4 e0, uint4 e1, uint8_t *rows, uint8_t *tab, int *red,
-                                      int *s_cnt, int *s_lc, int *s_cur, int *s_tie);
+__device__ void join_family(const KParams &P, uint4 e0, uint4 e1, uint8_t *rows, uint8_t *tab, int *red, int *s_cnt,
+                            int *s_lc, int *s_cur, int *s_tie);
 
 struct PartSums {
     int32_t *head;
@@ -1790,9 +1782,7 @@ struct PartSums {
         head = reinterpret_cast<int32_t *>(b);
         sum = reinterpret_cast<uint4 *>(b + round16(32 * np));
         cnt = reinterpret_cast<uint32_t *>(b + round16(32 * np) + 16 * 4 * np * (int64_t)pitch);
-        done = reinterpret_cast<uint32_t *>(b + round16(32 * np) + 20 * 4 * np * (int64_t)pitch);
     }
-    uint32_t *done;  // (JOIN_FUSED) parts finished, per split family; zeroed before the launch
     __device__ __forceinline__ int64_t at(int64_t part, int s, int col) const { return (4 * part + s) * (int64_t)pitch + col; }
 };
 
@@ -2638,21 +2628,8 @@ __device__ void process_large(const KParams &P, uint8_t *A, uint8_t *s_tab, cons
     }
     __syncthreads();
     if (stop == 7) return;
-    if (PART) {  // the part's set sizes and lengths; k_join (or the family's last part) does the rest
+    if (PART) {  // the part's set sizes and lengths; k_join does the rest
         if (tt < 8) PartSums(P).head[8 * (int64_t)blockIdx.x + tt] = tt < 4 ? cnt[tt] : lcv[tt - 4];
-        if (JOIN_FUSED) {
-            __threadfence();  // (release: this part's sums and header, device-wide)
-            __syncthreads();
-            const uint32_t sfi = ent.z >> 8;
-            const uint4 *sf = reinterpret_cast<const uint4 *>(B.split_fams);
-            const uint4 e0 = sf[2 * (int64_t)sfi], e1 = sf[2 * (int64_t)sfi + 1];
-            if (tt == 0) s_cur[0] = atomicAdd(PartSums(P).done + sfi, 1u) + 1 == e1.y ? 1 : 0;
-            __syncthreads();
-            if (s_cur[0]) {
-                __threadfence();  // (acquire: the other parts' sums)
-                join_family<G, TAGS>(P, e0, e1, A, s_tab, red, s_cnt, s_lc, s_cur, s_cur + 7);
-            }
-        }
         return;
     }
 
@@ -2693,11 +2670,11 @@ __global__ __launch_bounds__(G, G == 256 ? 5 : 2) void k_large(KParams P, const 
     process_large<G, TAGS, PART>(P, A, reinterpret_cast<uint8_t *>(&s_tab), lr, thr, fams[i], red, s_cnt, s_lc, s_cur);
 }
 
-// A split family's join on one workgroup of G threads (k_join, or the family's last part with
-// JOIN_FUSED): rows = 8 x stride bytes of LDS for its single-strand rows, tab = the TablesL copy.
+// A split family's join on one workgroup of G threads (k_join): rows = 8 x stride bytes of LDS for
+// its single-strand rows, tab = the TablesL copy.
 template <int G, bool TAGS>
-__device__ JOIN_ATTR void join_family(const KParams &P, uint4 e0, uint4 e1, uint8_t *rows, uint8_t *tab, int *red,
-                                      int *s_cnt, int *s_lc, int *s_cur, int *s_tie) {
+__device__ void join_family(const KParams &P, uint4 e0, uint4 e1, uint8_t *rows, uint8_t *tab, int *red, int *s_cnt,
+                            int *s_lc, int *s_cur, int *s_tie) {
     const int tt = threadIdx.x;
     const TablesL &T = *reinterpret_cast<const TablesL *>(tab);
     const PartSums ps(P);
@@ -3087,8 +3064,7 @@ int32_t bsdc_run(bsdc_ctx *c, const bsdc_family_batch *b, bsdc_consensus *o, int
         return BSDC_EINVAL;
     }
     if (b->n_split_parts > 0 && (b->split_part_arena % 16 || b->split_part_arena <= 0 ||
-                                 b->split_part_arena > BSDC_LARGE_LDS_MAX || !o->scratch || !b->split_parts || !b->split_fams ||
-                                 (JOIN_FUSED && b->split_part_arena < 8 * o->stride))) {
+                                 b->split_part_arena > BSDC_LARGE_LDS_MAX || !o->scratch || !b->split_parts || !b->split_fams)) {
         c->err = "bad split families";
         return BSDC_EINVAL;
     }
@@ -3170,27 +3146,16 @@ int32_t bsdc_run(bsdc_ctx *c, const bsdc_family_batch *b, bsdc_consensus *o, int
         const uint4 *pf = reinterpret_cast<const uint4 *>(b->split_parts);
         const uint4 *sf = reinterpret_cast<const uint4 *>(b->split_fams);
         const size_t jl = 8 * (size_t)o->stride;
-        if (JOIN_FUSED) {  // the per-family part counters (PartSums::done), zeroed on the parts' stream
-            const int64_t np = b->n_split_parts;
-            uint8_t *done = o->scratch + b->split_partial_off + round16(32 * np) + 80 * np * (int64_t)o->stride;
-            const hipError_t e = hipMemsetAsync(done, 0, 4 * (size_t)b->n_split_fams, ls);
-            if (e != hipSuccess) {
-                fail(e, "hipMemsetAsync(part counters)");
-                return;
-            }
-        }
         if (tg) {
             hipLaunchKernelGGL((k_large<true, kLargeThreads, true, true>), dim3((unsigned)b->n_split_parts), dim3(kLargeThreads),
                                (size_t)a, ls, P, pf, b->n_split_parts, a, (int64_t)0);
-            if (!JOIN_FUSED)
-                hipLaunchKernelGGL((k_join<true>), dim3((unsigned)b->n_split_fams), dim3(kLargeThreadsBig), jl, ls, P, sf,
-                                   b->n_split_fams);
+            hipLaunchKernelGGL((k_join<true>), dim3((unsigned)b->n_split_fams), dim3(kLargeThreadsBig), jl, ls, P, sf,
+                               b->n_split_fams);
         } else {
             hipLaunchKernelGGL((k_large<true, kLargeThreads, false, true>), dim3((unsigned)b->n_split_parts),
                                dim3(kLargeThreads), (size_t)a, ls, P, pf, b->n_split_parts, a, (int64_t)0);
-            if (!JOIN_FUSED)
-                hipLaunchKernelGGL((k_join<false>), dim3((unsigned)b->n_split_fams), dim3(kLargeThreadsBig), jl, ls, P, sf,
-                                   b->n_split_fams);
+            hipLaunchKernelGGL((k_join<false>), dim3((unsigned)b->n_split_fams), dim3(kLargeThreadsBig), jl, ls, P, sf,
+                               b->n_split_fams);
         }
         const hipError_t e = hipGetLastError();
         if (e != hipSuccess) fail(e, "split launch");
