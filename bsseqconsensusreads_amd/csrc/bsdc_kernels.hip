@@ -1770,6 +1770,13 @@ template <int G, bool TAGS>
 __device__ void join_family(const KParams &P, uint4 e0, uint4 e1, uint8_t *rows, uint8_t *tab, int *red, int *s_cnt,
                             int *s_lc, int *s_cur, int *s_tie);
 
+// more than one of the four per-base read counts (u8 each) is nonzero
+__device__ __forceinline__ bool multi_base(uint32_t m) {
+    return ((m & 0xFFu) != 0) + ((m & 0xFF00u) != 0) + ((m & 0xFF0000u) != 0) + ((m & 0xFF000000u) != 0) > 1;
+}
+// A part's column: its read counts per base (u8 x4), and the likelihood sum of its one base when
+// only one has reads (`one`, 4 B: most columns), else the four sums (`sum`, 16 B; k_join reads them
+// only then).
 struct PartSums {
     int32_t *head;
     uint4 *sum;
@@ -1782,7 +1789,9 @@ struct PartSums {
         head = reinterpret_cast<int32_t *>(b);
         sum = reinterpret_cast<uint4 *>(b + round16(32 * np));
         cnt = reinterpret_cast<uint32_t *>(b + round16(32 * np) + 16 * 4 * np * (int64_t)pitch);
+        one = reinterpret_cast<int32_t *>(b + round16(32 * np) + 20 * 4 * np * (int64_t)pitch);
     }
+    int32_t *one;  // the sum of a column whose reads show one base (its count byte the only one set)
     __device__ __forceinline__ int64_t at(int64_t part, int s, int col) const { return (4 * part + s) * (int64_t)pitch + col; }
 };
 
@@ -2336,9 +2345,13 @@ __device__ void process_large(const KParams &P, uint8_t *A, uint8_t *s_tab, cons
     // PART: a multi-base column's per-base sums (int32: a part holds < 255 reads a set) and counts
     auto part_write = [&](int s, int col, long long D0, long long D1, long long D2, long long D3, uint32_t n01, uint32_t n23) {
         const PartSums ps(P);
-        ps.sum[ps.at(blockIdx.x, s, col)] = make_uint4((uint32_t)(int32_t)D0, (uint32_t)(int32_t)D1, (uint32_t)(int32_t)D2,
-                                                       (uint32_t)(int32_t)D3);
-        ps.cnt[ps.at(blockIdx.x, s, col)] = (n01 & 0xFFu) | ((n01 >> 8) & 0xFF00u) | ((n23 & 0xFFu) << 16) | ((n23 >> 16) << 24);
+        const int64_t at = ps.at(blockIdx.x, s, col);
+        const uint32_t m = (n01 & 0xFFu) | ((n01 >> 8) & 0xFF00u) | ((n23 & 0xFFu) << 16) | ((n23 >> 16) << 24);
+        ps.cnt[at] = m;
+        if (multi_base(m))
+            ps.sum[at] = make_uint4((uint32_t)(int32_t)D0, (uint32_t)(int32_t)D1, (uint32_t)(int32_t)D2, (uint32_t)(int32_t)D3);
+        else  // (one base or none: the others' sums are 0)
+            ps.one[at] = (int32_t)(m & 0xFFu ? D0 : m & 0xFF00u ? D1 : m & 0xFF0000u ? D2 : D3);
     };
     // Wavefronts by set: wave w works on set w % 4; with 8 waves (512 threads) the two waves of a
     // set split its reads (PARTS = 2).
@@ -2459,8 +2472,7 @@ __device__ void process_large(const KParams &P, uint8_t *A, uint8_t *s_tab, cons
                             const PartSums ps(P);
                             const int bi = ob ? __builtin_ctz(ob) : 0;
                             const int32_t T = ob ? (int32_t)Tj : 0;
-                            ps.sum[ps.at(blockIdx.x, ws, col)] =
-                                make_uint4(bi == 0 ? T : 0, bi == 1 ? T : 0, bi == 2 ? T : 0, bi == 3 ? T : 0);
+                            ps.one[ps.at(blockIdx.x, ws, col)] = T;
                             ps.cnt[ps.at(blockIdx.x, ws, col)] = ob ? nj << (8 * bi) : 0u;
                             ssq[ws * ssw + col] = 1;
                         } else {
@@ -2671,7 +2683,8 @@ __global__ __launch_bounds__(G, G == 256 ? 5 : 2) void k_large(KParams P, const 
 }
 
 // A split family's join on one workgroup of G threads (k_join): rows = 8 x stride bytes of LDS for
-// its single-strand rows, tab = the TablesL copy.
+// its single-strand rows + kJoinParts x 8 bytes for the parts' set lengths, tab = the TablesL copy.
+constexpr int kJoinParts = 256;
 template <int G, bool TAGS>
 __device__ void join_family(const KParams &P, uint4 e0, uint4 e1, uint8_t *rows, uint8_t *tab, int *red, int *s_cnt,
                             int *s_lc, int *s_cur, int *s_tie) {
@@ -2680,7 +2693,13 @@ __device__ void join_family(const KParams &P, uint4 e0, uint4 e1, uint8_t *rows,
     const PartSums ps(P);
     const int64_t p0 = e1.x;
     const int np = (int)e1.y;
+    // the parts' set lengths, [set][part] in LDS after the rows (kJoinParts at most; more read them
+    // from HBM): a column's loop over the parts then issues only its sum and count loads
+    uint16_t *hl = reinterpret_cast<uint16_t *>(rows + 8 * P.O.stride);
+    const bool hl_lds = np <= kJoinParts;
     __syncthreads();  // (s_cnt / s_lc / s_tie are the caller's too)
+    if (hl_lds)
+        for (int k = tt; k < 4 * np; k += G) hl[(k & 3) * kJoinParts + (k >> 2)] = (uint16_t)ps.head[8 * (p0 + (k >> 2)) + 4 + (k & 3)];
     if (tt < 4) {
         int c = 0, l = 0;
         for (int p = 0; p < np; p++) {
@@ -2708,18 +2727,40 @@ __device__ void join_family(const KParams &P, uint4 e0, uint4 e1, uint8_t *rows,
         }
         long long D0 = 0, D1 = 0, D2 = 0, D3 = 0;
         uint32_t n0 = 0, n1 = 0, n2 = 0, n3 = 0;
-        for (int p = 0; p < np; p++) {
-            if (c >= ps.head[8 * (p0 + p) + 4 + s]) continue;  // (the part's set ends before c: nothing written)
-            const uint4 d = ps.sum[ps.at(p0 + p, s, c)];
-            const uint32_t m = ps.cnt[ps.at(p0 + p, s, c)];
-            D0 += (int32_t)d.x;
-            D1 += (int32_t)d.y;
-            D2 += (int32_t)d.z;
-            D3 += (int32_t)d.w;
-            n0 += m & 0xFFu;
-            n1 += (m >> 8) & 0xFFu;
-            n2 += (m >> 16) & 0xFFu;
-            n3 += m >> 24;
+        for (int pb = 0; pb < np; pb += 4) {  // four parts' loads in flight
+            uint4 d[4];
+            uint32_t m[4];
+            int32_t o[4];
+#pragma unroll
+            for (int u = 0; u < 4; u++) {
+                const int p = pb + u;
+                // (a part whose set ends before c wrote nothing there)
+                const bool in = p < np && c < (hl_lds ? (int)hl[s * kJoinParts + p] : ps.head[8 * (p0 + p) + 4 + s]);
+                m[u] = in ? ps.cnt[ps.at(p0 + p, s, c)] : 0u;
+                o[u] = in ? ps.one[ps.at(p0 + p, s, c)] : 0;
+            }
+#pragma unroll
+            for (int u = 0; u < 4; u++) {  // (the four sums only where more than one base has reads)
+                const uint32_t x = m[u];
+                if (multi_base(x)) {
+                    d[u] = ps.sum[ps.at(p0 + pb + u, s, c)];
+                } else {
+                    const uint32_t b = x & 0xFFu ? 0u : x & 0xFF00u ? 1u : x & 0xFF0000u ? 2u : 3u;
+                    d[u] = make_uint4(b == 0 ? (uint32_t)o[u] : 0u, b == 1 ? (uint32_t)o[u] : 0u, b == 2 ? (uint32_t)o[u] : 0u,
+                                      b == 3 ? (uint32_t)o[u] : 0u);
+                }
+            }
+#pragma unroll
+            for (int u = 0; u < 4; u++) {
+                D0 += (int32_t)d[u].x;
+                D1 += (int32_t)d[u].y;
+                D2 += (int32_t)d[u].z;
+                D3 += (int32_t)d[u].w;
+                n0 += m[u] & 0xFFu;
+                n1 += (m[u] >> 8) & 0xFFu;
+                n2 += (m[u] >> 16) & 0xFFu;
+                n3 += m[u] >> 24;
+            }
         }
         const int best = first_max4(D0, D1, D2, D3);
         if (near_tie(D0, D1, D2, D3, best, cnt[s])) {
@@ -3145,7 +3186,7 @@ int32_t bsdc_run(bsdc_ctx *c, const bsdc_family_batch *b, bsdc_consensus *o, int
         if (rc != 0) return;
         const uint4 *pf = reinterpret_cast<const uint4 *>(b->split_parts);
         const uint4 *sf = reinterpret_cast<const uint4 *>(b->split_fams);
-        const size_t jl = 8 * (size_t)o->stride;
+        const size_t jl = 8 * (size_t)o->stride + 8 * kJoinParts;
         if (tg) {
             hipLaunchKernelGGL((k_large<true, kLargeThreads, true, true>), dim3((unsigned)b->n_split_parts), dim3(kLargeThreads),
                                (size_t)a, ls, P, pf, b->n_split_parts, a, (int64_t)0);

@@ -110,7 +110,8 @@ typedef struct {
                                     parts, fallback arena offset in scratch / 16, fallback arena bytes */
     int64_t n_split_fams;
     int64_t split_partial_off;   /* scratch offset of the parts' sums: [part][8] int32 (set reads, set
-                                    lengths), then [part][4][stride] int32x4 sums, [part][4][stride] u8x4 counts */
+                                    lengths), then [part][4][stride] int32x4 sums, [part][4][stride] u8x4
+                                    counts, [part][4][stride] int32 one-base sums */
 } bsdc_family_batch;
 
 /* Outputs (device pointers).  Consensus slot (f, end) holds `stride` bases. */
