@@ -372,3 +372,29 @@ def test_split_families_vs_oracle(engine, monkeypatch, cfg, n_fam, messy, qlo, c
     assert_ss_equal(cons, ref, "parts " + cfg)
     for k in ("src", "pos", "seq", "qual", "cigar"):
         assert np.array_equal(getattr(t2, k), getattr(ref.tool2, k)), "parts %s tool-2 %s" % (cfg, k)
+
+
+@pytest.mark.parametrize("cfg,n_fam,cap", [("C3", 60, 20000), ("C4", 250, 30000)])
+def test_split_families_without_tags_vs_oracle(engine, monkeypatch, cfg, n_fam, cap):
+    """Part mode on the untagged launch (the FASTQ path: no single-strand outputs), bit-exact
+    against oracle/."""
+    s = synth.generate(cfg, n_fam, seed=29, device="cpu", genome_len=300_000)
+    seen = []
+    force_parts(monkeypatch, cap, seen)
+    engine.load_reference(s.ref)
+    cons, _ = pipeline.run_step5(engine, s.raw, tags=False)
+    assert sum(fb.split_fams.shape[0] for fb in seen) > 0
+    assert_consensus_equal(cons, oracle.run(s.raw, s.ref), "parts, no tags " + cfg)
+
+
+def test_split_families_molecular_vs_oracle(engine, monkeypatch):
+    """Part mode under step 1's caller (MI runs, no BA side, --min-consensus-base-quality=0): the
+    join masks with the context's own threshold, bit-exact against oracle/ at 0."""
+    s, raw = _grouped("C3", 40, seed=31)
+    seen = []
+    force_parts(monkeypatch, 16000, seen)
+    cons, rm = pipeline.run_molecular(engine, raw, tags=True)
+    assert sum(fb.split_fams.shape[0] for fb in seen) > 0
+    ref = oracle.run(rm, s.ref, run_tools=False, family_order="mi-group", min_consensus_base_quality=0)
+    assert_consensus_equal(cons, ref, "parts molecular")
+    assert_ss_equal(cons, ref, "parts molecular")
