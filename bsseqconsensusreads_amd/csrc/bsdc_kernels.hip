@@ -64,7 +64,8 @@ constexpr int kLargeThreads = LARGE_THREADS;
 #ifndef LARGE_THREADS_BIG
 #define LARGE_THREADS_BIG 512  // k_large workgroup size of the LDS-heavy buckets
 #endif
-constexpr int kLargeThreadsBig = LARGE_THREADS_BIG;
+constexpr int kLargeThreadsBig = LARGE_THREADS_BIG;  // 512 or 768
+constexpr int kJoinThreads = 512;
 constexpr int kLargeBigBucket = 3;
 #ifndef LARGE_VOTE_U
 #define LARGE_VOTE_U 4  // k_large vote pass A: reads in flight per lane
@@ -2365,8 +2366,8 @@ __device__ void process_large(const KParams &P, uint8_t *A, uint8_t *s_tab, cons
     // all, a small or negative sum) is marked (ssq = 0).
     // Pass B: the marked columns, 8 lanes each: the lanes split the reads, sum per base, reduce
     // by lane shuffles, and the first lane makes the general call (resolve).
-    constexpr int NW = G / kWave, PARTS = NW >= 8 ? 2 : 1;
-    static_assert(NW == 4 * PARTS, "k_large: 4 or 8 wavefronts");
+    constexpr int NW = G / kWave, PARTS = NW / 4;
+    static_assert(NW == 4 * PARTS && PARTS >= 1 && PARTS <= 3, "k_large: 4, 8 or 12 wavefronts");
     const int32_t *lr2 = lr - 256;  // TablesL: zero[256] then lr[256]
     const int lane = tt & (kWave - 1), wv = tt >> 6, ws = wv & 3, wpart = wv >> 2;
     int64_t *psum = reinterpret_cast<int64_t *>(A + Lo.meta);        // [4][ssw] part-1 sums (RecMeta is dead)
@@ -2375,7 +2376,7 @@ __device__ void process_large(const KParams &P, uint8_t *A, uint8_t *s_tab, cons
     {
         const int na = cnt[ws], lc = lcv[ws], nf = nfw[ws];
         const uint2 *dl = desc + soff[ws];
-        const int rb = wpart == 0 ? 0 : na / 2, re = PARTS == 1 || wpart == 1 ? na : na / 2;
+        const int rb = wpart * na / PARTS, re = (wpart + 1) * na / PARTS;  // this wave's share of the set's reads
         const int lmax = ::max(::max(lcv[0], lcv[1]), ::max(lcv[2], lcv[3]));
         for (int cb = 0; cb < lmax; cb += 4 * kWave) {  // the same trip count in every wave (barriers inside)
             const int c = cb + 4 * lane, c8 = 8 * c;
@@ -2442,14 +2443,26 @@ __device__ void process_large(const KParams &P, uint8_t *A, uint8_t *s_tab, cons
                     flush();
                 }
             }
-            if (PARTS == 2) {
-                if (wpart == 1 && cb < lc) {
+            // the other parts' partials meet in one region, the last part first, each later one
+            // adding its own, then part 0 reads them (one barrier per part)
+#pragma unroll
+            for (int pp = PARTS - 1; pp >= 1; pp--) {
+                if (wpart == pp && cb < lc) {
 #pragma unroll
                     for (int j = 0; j < 4; j++)
                         if (c + j < lc) {
-                            psum[ws * ssw + c + j] = j == 0 ? T0 : j == 1 ? T1 : j == 2 ? T2 : T3;
-                            por[ws * ssw + c + j] = (uint8_t)(orm >> (8 * j));
-                            if (TAGS || PART) pcn[ws * ssw + c + j] = (uint16_t)((j < 2 ? cn01 : cn23) >> (16 * (j & 1)));
+                            const long long tj = j == 0 ? T0 : j == 1 ? T1 : j == 2 ? T2 : T3;
+                            const uint8_t oj = (uint8_t)(orm >> (8 * j));
+                            const uint16_t nj = (uint16_t)((j < 2 ? cn01 : cn23) >> (16 * (j & 1)));
+                            if (pp == PARTS - 1) {
+                                psum[ws * ssw + c + j] = tj;
+                                por[ws * ssw + c + j] = oj;
+                                if (TAGS || PART) pcn[ws * ssw + c + j] = nj;
+                            } else {
+                                psum[ws * ssw + c + j] += tj;
+                                por[ws * ssw + c + j] |= oj;
+                                if (TAGS || PART) pcn[ws * ssw + c + j] += nj;
+                            }
                         }
                 }
                 __syncthreads();
@@ -2462,7 +2475,7 @@ __device__ void process_large(const KParams &P, uint8_t *A, uint8_t *s_tab, cons
                     uint32_t ob = (orm >> (8 * j)) & 0xFFu;
                     long long Tj = j == 0 ? T0 : j == 1 ? T1 : j == 2 ? T2 : T3;
                     uint32_t nj = (TAGS || PART) ? ((j < 2 ? cn01 : cn23) >> (16 * (j & 1))) & 0xFFFFu : 0u;
-                    if (PARTS == 2) {
+                    if (PARTS >= 2) {
                         Tj += psum[ws * ssw + col];
                         ob |= por[ws * ssw + col];
                         if (TAGS || PART) nj += pcn[ws * ssw + col];
@@ -2495,7 +2508,7 @@ __device__ void process_large(const KParams &P, uint8_t *A, uint8_t *s_tab, cons
                     }
                 }
             }
-            if (PARTS == 2) __syncthreads();
+            if (PARTS >= 2) __syncthreads();
         }
     }
     __syncthreads();
@@ -2528,11 +2541,11 @@ __device__ void process_large(const KParams &P, uint8_t *A, uint8_t *s_tab, cons
         const int64_t region = ::max((int64_t)round16((int64_t)n * (int64_t)bsdc_layout::kRecMetaBytes) + round16(2 * (int64_t)n),
                                      (int64_t)bsdc_layout::kVoteRegionPerCol * ssw);
         const int64_t pbo = round16(8 * (int64_t)ssw);
-        const bool split = PARTS == 2 && pbo + 4 * kWave * 24 <= region &&
-                           ::max(::max(cnt[0], cnt[1]), ::max(cnt[2], cnt[3])) <= 254;
+        const bool split = PARTS >= 2 && pbo + (PARTS - 1) * 4 * kWave * 24 <= region &&
+                           ::max(::max(cnt[0], cnt[1]), ::max(cnt[2], cnt[3])) <= 127 * PARTS;
         int32_t *pb = reinterpret_cast<int32_t *>(reinterpret_cast<uint8_t *>(psum) + pbo);  // [4][64][6]
         const int nmax = ::max(::max(s_lc[0], s_lc[1]), ::max(s_lc[2], s_lc[3]));
-        const int rb = split ? (wpart == 0 ? 0 : na / 2) : 0, re = split ? (wpart == 0 ? na / 2 : na) : na;
+        const int rb = split ? wpart * na / PARTS : 0, re = split ? (wpart + 1) * na / PARTS : na;
         const int kstart = split ? 0 : kWave * wpart, kstep = split ? kWave : kWave * PARTS;
         const int kend = split ? nmax : nm;
         // One wave on a set with <= 32 marked columns: its two halves take the same columns and
@@ -2609,9 +2622,9 @@ __device__ void process_large(const KParams &P, uint8_t *A, uint8_t *s_tab, cons
                 D3 += d3;
                 d0 = d1 = d2 = d3 = 0;
             }
-            if (split) {
-                int32_t *pw = pb + 6 * (s * kWave + lane);
-                if (wpart == 1 && act) {
+            if (split) {  // parts 1.. leave their sums in their own slots; part 0 adds them up
+                if (wpart >= 1 && act) {
+                    int32_t *pw = pb + 6 * (((wpart - 1) * 4 + s) * kWave + lane);
                     pw[0] = (int32_t)D0;
                     pw[1] = (int32_t)D1;
                     pw[2] = (int32_t)D2;
@@ -2623,11 +2636,22 @@ __device__ void process_large(const KParams &P, uint8_t *A, uint8_t *s_tab, cons
                 }
                 __syncthreads();
                 if (wpart == 0 && act) {
+#pragma unroll
+                    for (int pp = 1; pp < PARTS; pp++) {
+                        const int32_t *pw = pb + 6 * (((pp - 1) * 4 + s) * kWave + lane);
+                        D0 += pw[0];
+                        D1 += pw[1];
+                        D2 += pw[2];
+                        D3 += pw[3];
+                        if (TAGS || PART) {
+                            n01 += (uint32_t)pw[4];
+                            n23 += (uint32_t)pw[5];
+                        }
+                    }
                     if (PART)
-                        part_write(s, col, D0 + pw[0], D1 + pw[1], D2 + pw[2], D3 + pw[3], n01 + (uint32_t)pw[4], n23 + (uint32_t)pw[5]);
+                        part_write(s, col, D0, D1, D2, D3, n01, n23);
                     else
-                        resolve(s, col, D0 + pw[0], D1 + pw[1], D2 + pw[2], D3 + pw[3], TAGS ? n01 + (uint32_t)pw[4] : 0u,
-                                TAGS ? n23 + (uint32_t)pw[5] : 0u);
+                        resolve(s, col, D0, D1, D2, D3, TAGS ? n01 : 0u, TAGS ? n23 : 0u);
                 }
                 __syncthreads();
             } else if (act) {
@@ -2802,8 +2826,8 @@ __device__ void join_family(const KParams &P, uint4 e0, uint4 e1, uint8_t *rows,
 // column needs fgbio's read-order double sums over all the set's reads, which the parts did not
 // keep: then the family runs whole in its HBM fallback arena (process_large), as the HBM bucket does.
 template <bool TAGS>
-__global__ __launch_bounds__(kLargeThreadsBig, 2) void k_join(KParams P, const uint4 *sfams, int64_t nsf) {
-    constexpr int G = kLargeThreadsBig;
+__global__ __launch_bounds__(kJoinThreads, 2) void k_join(KParams P, const uint4 *sfams, int64_t nsf) {
+    constexpr int G = kJoinThreads;
     extern __shared__ __attribute__((aligned(16))) uint8_t smem[];  // single-strand rows: bases, quals [4][stride]
     __shared__ __attribute__((aligned(16))) TablesL s_tab;
     __shared__ int red[2 * G / kWave];
@@ -3190,12 +3214,12 @@ int32_t bsdc_run(bsdc_ctx *c, const bsdc_family_batch *b, bsdc_consensus *o, int
         if (tg) {
             hipLaunchKernelGGL((k_large<true, kLargeThreads, true, true>), dim3((unsigned)b->n_split_parts), dim3(kLargeThreads),
                                (size_t)a, ls, P, pf, b->n_split_parts, a, (int64_t)0);
-            hipLaunchKernelGGL((k_join<true>), dim3((unsigned)b->n_split_fams), dim3(kLargeThreadsBig), jl, ls, P, sf,
+            hipLaunchKernelGGL((k_join<true>), dim3((unsigned)b->n_split_fams), dim3(kJoinThreads), jl, ls, P, sf,
                                b->n_split_fams);
         } else {
             hipLaunchKernelGGL((k_large<true, kLargeThreads, false, true>), dim3((unsigned)b->n_split_parts),
                                dim3(kLargeThreads), (size_t)a, ls, P, pf, b->n_split_parts, a, (int64_t)0);
-            hipLaunchKernelGGL((k_join<false>), dim3((unsigned)b->n_split_fams), dim3(kLargeThreadsBig), jl, ls, P, sf,
+            hipLaunchKernelGGL((k_join<false>), dim3((unsigned)b->n_split_fams), dim3(kJoinThreads), jl, ls, P, sf,
                                b->n_split_fams);
         }
         const hipError_t e = hipGetLastError();
