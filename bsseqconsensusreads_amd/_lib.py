@@ -8,7 +8,7 @@ HERE = os.path.dirname(os.path.abspath(__file__))
 # BSDC_LIB_PATH: an alternative build of the same library (profiling A/B runs only)
 LIB_PATH = os.environ.get("BSDC_LIB_PATH") or os.path.join(HERE, "libbsdc.so")
 
-BSDC_ABI_VERSION = 11
+BSDC_ABI_VERSION = 12
 SMALL_BUCKETS = 8  # BSDC_SMALL_BUCKETS
 LARGE_BUCKETS = 6  # BSDC_LARGE_BUCKETS
 MODE_CONVERT, MODE_EXTEND, MODE_VOTE, MODE_DUMP = 1, 2, 4, 8
@@ -48,7 +48,7 @@ EXPORTS = ("bsdc_abi_version", "bsdc_ctx_create", "bsdc_ctx_set_params", "bsdc_c
            "bsdc_load_reference", "bsdc_run", "bsdc_convert", "bsdc_extend", "bsdc_duplex_call",
            "bsdc_family_arena_bytes", "bsdc_small_arena_bytes", "bsdc_get_tables", "bsdc_model_tables",
            "bsdc_model_tables_fp64", "bsdc_agree_tables", "bsdc_phred_buckets", "bsdc_bgzf_scratch_bytes",
-           "bsdc_bgzf_deflate", "bsdc_bgzf_pack")
+           "bsdc_bgzf_deflate", "bsdc_bgzf_pack", "bsdc_host_register", "bsdc_host_unregister")
 
 _lib = None
 
@@ -97,6 +97,10 @@ def load(path: str = LIB_PATH):
     lib.bsdc_bgzf_deflate.restype = C.c_int32
     lib.bsdc_bgzf_pack.argtypes = [C.c_void_p, C.c_void_p, C.c_int64, C.c_int64, C.c_void_p, C.c_void_p]
     lib.bsdc_bgzf_pack.restype = C.c_int32
+    lib.bsdc_host_register.argtypes = [C.c_int32, C.c_void_p, C.c_int64]
+    lib.bsdc_host_register.restype = C.c_int32
+    lib.bsdc_host_unregister.argtypes = [C.c_int32, C.c_void_p]
+    lib.bsdc_host_unregister.restype = C.c_int32
     lib.bsdc_phred_buckets.argtypes = [C.c_double, C.c_double, C.c_void_p]
     lib.bsdc_phred_buckets.restype = None
     if lib.bsdc_abi_version() != BSDC_ABI_VERSION:

@@ -2990,6 +2990,24 @@ extern "C" {
 
 int32_t bsdc_abi_version(void) { return BSDC_ABI_VERSION; }
 
+int32_t bsdc_host_register(int32_t device, void *ptr, int64_t nbytes) {
+    if (!ptr || nbytes <= 0) return BSDC_EINVAL;
+    if (hipSetDevice(device) != hipSuccess || hipHostRegister(ptr, (size_t)nbytes, hipHostRegisterDefault) != hipSuccess) {
+        (void)hipGetLastError();  // (not sticky: the next launch check must not see it)
+        return BSDC_EDEVICE;
+    }
+    return 0;
+}
+
+int32_t bsdc_host_unregister(int32_t device, void *ptr) {
+    if (!ptr) return BSDC_EINVAL;
+    if (hipSetDevice(device) != hipSuccess || hipHostUnregister(ptr) != hipSuccess) {
+        (void)hipGetLastError();
+        return BSDC_EDEVICE;
+    }
+    return 0;
+}
+
 static bool params_ok(const bsdc_params *p) {
     return p->min_reads == 0 && p->min_input_base_quality >= 0 && p->min_consensus_base_quality >= 0 &&
            p->min_consensus_base_quality <= 94;

@@ -227,37 +227,34 @@ class SegmentViews:
 
 
 class HostPinner:
-    """Page-locks a GPU worker's mappings of the shared segments (hipHostRegister through torch's
-    runtime binding), so a batch's arrays upload and its outputs come back by DMA straight from /
-    into the segments; a pageable copy goes through the runtime's staging buffers at a fraction of
-    the rate, on the worker's CPU.  Best effort: a mapping the runtime refuses stays pageable."""
+    """Page-locks a GPU worker's mappings of the shared segments (libbsdc bsdc_host_register), so a
+    batch's arrays upload and its outputs come back by DMA straight from / into the segments; a
+    pageable copy goes through the runtime's staging buffers at a fraction of the rate, on the
+    worker's CPU.  Best effort: a mapping the runtime refuses stays pageable."""
 
     def __init__(self, device: int):
+        from . import _lib
+        self.lib = _lib.load()
         self.device = device
         self.done: Dict[int, int] = {}
         self.lock = threading.Lock()
 
     def pin(self, shm):
-        import torch
         ptr = np.frombuffer(shm.buf, np.uint8).ctypes.data
         with self.lock:
             if ptr in self.done:
                 return
-            torch.cuda.set_device(self.device)  # (the calling thread's current device)
-            rc = torch._C._cudart.cudaHostRegister(ptr, shm.size, 0)
-            if int(rc) == 0:
+            if self.lib.bsdc_host_register(self.device, ptr, shm.size) == 0:
                 self.done[ptr] = shm.size
 
     def unpin(self, shm):
-        import torch
         try:
             ptr = np.frombuffer(shm.buf, np.uint8).ctypes.data
         except (TypeError, ValueError):  # (already closed)
             return
         with self.lock:
             if self.done.pop(ptr, None) is not None:
-                torch.cuda.set_device(self.device)
-                torch._C._cudart.cudaHostUnregister(ptr)
+                self.lib.bsdc_host_unregister(self.device, ptr)
 
 
 def pack(obj, pool: Optional[SegmentPool] = None):

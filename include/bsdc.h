@@ -26,7 +26,7 @@
 extern "C" {
 #endif
 
-#define BSDC_ABI_VERSION 11
+#define BSDC_ABI_VERSION 12
 #define BSDC_SMALL_BUCKETS 8
 #define BSDC_LARGE_BUCKETS 6
 #define BSDC_LARGE_LDS_MAX 158912 /* LDS arena bytes one large-family workgroup may use */ /* LDS arena size classes of the wavefront-per-family kernel */
@@ -209,6 +209,13 @@ void bsdc_phred_buckets(double error_rate_pre_umi, double error_rate_post_umi, u
    over one stream's blocks pack them back to back with no host round trip.  Device pointers;
    stream = hipStream_t. */
 int64_t bsdc_bgzf_scratch_bytes(int64_t max_blocks);
+
+/* Page-lock a caller's host range for DMA (hipHostRegister) / release it: a multi-GPU worker's
+ * mappings of the shared segments its batches and outputs travel in (fleet.py), so uploads and
+ * fetches run by DMA from / into them.  0, or BSDC_EDEVICE with the runtime's error cleared (a
+ * range that stays pageable still works, at the pageable copy rate). */
+int32_t bsdc_host_register(int32_t device, void *ptr, int64_t nbytes);
+int32_t bsdc_host_unregister(int32_t device, void *ptr);
 int32_t bsdc_bgzf_deflate(const uint8_t *in, int64_t n, int64_t blk0, int64_t nblk, uint8_t *scratch,
                           int32_t *sizes, void *stream);
 int32_t bsdc_bgzf_pack(const uint8_t *scratch, const int32_t *sizes, int64_t blk0, int64_t nblk, uint8_t *out,
