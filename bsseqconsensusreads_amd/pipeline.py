@@ -413,12 +413,43 @@ def molecular_records(raw: R.RawRecords) -> R.RawRecords:
         brk[1:] = key[1:] != key[:-1]
     run = np.cumsum(brk) - 1
     starts = np.nonzero(brk)[0]
-    suffix = {0: "/A", 1: "/B", -1: ""}
-    names = [raw.mi_names[int(raw.mi_id[k])] + suffix[int(raw.mi_strand[k])] if raw.mi_id[k] >= 0 else ""
-             for k in starts]
+    from .bam import StringTable
+    if isinstance(raw.mi_names, StringTable):  # a decoded BAM: the run names as one packed table
+        names = _run_names(raw.mi_names, raw.mi_id[starts], raw.mi_strand[starts])
+    else:
+        suffix = {0: "/A", 1: "/B", -1: ""}
+        names = [raw.mi_names[int(raw.mi_id[k])] + suffix[int(raw.mi_strand[k])] if raw.mi_id[k] >= 0 else ""
+                 for k in starts]
     mi_id = np.where(raw.mi_id >= 0, run, -1).astype(np.int32)
     mi_strand = np.where(raw.mi_id >= 0, 0, -1).astype(np.int8)
     return dataclasses.replace(raw, mi_id=mi_id, mi_strand=mi_strand, mi_names=names)
+
+
+def _run_names(tab, ids: np.ndarray, strands: np.ndarray):
+    """StringTable of tab[ids[k]] + "/A" (strand 0) / "/B" (strand 1) / "" (no strand), "" for
+    ids[k] < 0: molecular_records' run names, vectorised (one Python string per run cost as much as
+    planning the chunk)."""
+    from .bam import StringTable
+    ids = np.asarray(ids, np.int64)
+    strands = np.asarray(strands, np.int64)
+    n = int(ids.shape[0])
+    ok = ids >= 0
+    cid = np.where(ok, ids, 0)
+    src_len = np.where(ok, tab.off[cid + 1] - tab.off[cid], 0) if n else np.zeros(0, np.int64)
+    sfx = ok & (strands >= 0)
+    lens = src_len + 2 * sfx
+    off = np.zeros(n + 1, np.int64)
+    off[1:] = np.cumsum(lens)
+    buf = np.empty(int(off[-1]), np.uint8)
+    tot = int(src_len.sum())
+    if tot:
+        k = np.repeat(np.arange(n, dtype=np.int64), src_len)
+        j = np.arange(tot, dtype=np.int64) - np.repeat(np.cumsum(src_len) - src_len, src_len)
+        buf[off[k] + j] = tab.buf[tab.off[cid[k]] + j]
+    at = off[:-1][sfx] + src_len[sfx]
+    buf[at] = ord("/")
+    buf[at + 1] = np.where(strands[sfx] == 0, ord("A"), ord("B")).astype(np.uint8)
+    return StringTable(buf, off, as_str=True)
 
 
 def run_molecular(engine: Engine, raw: R.RawRecords, tags: bool = False,

@@ -187,3 +187,19 @@ def test_molecular_stream_pipeline_matches_oracle(standin, tmp_path):
     assert info["chunks"] > 4 and standin.flag_log == [0]
     n, q1 = assert_molecular_outputs_match_oracle(out, fq, p, min_cbq=0)
     assert n == info["records_out"] and q1 > 20
+
+
+def test_run_names_vectorised_equal_the_string_path():
+    """pipeline.molecular_records on a decoded BAM's packed MI table (the streaming path) names the
+    runs exactly as the per-run string path does: MI + "/A" or "/B", "" without an MI."""
+    from bsseqconsensusreads_amd import pipeline
+    from bsseqconsensusreads_amd.bam import StringTable
+    names = ["7", "12", "103", "x"]
+    tab = StringTable.from_list(names)
+    ids = np.array([0, 0, 1, -1, 2, 2, 3, 1], np.int32)
+    strands = np.array([0, 1, 1, -1, 0, -1, 1, 0], np.int8)
+    got = pipeline._run_names(tab, ids, strands)
+    sfx = {0: "/A", 1: "/B", -1: ""}
+    want = [names[i] + sfx[s] if i >= 0 else "" for i, s in zip(ids, strands)]
+    assert [got[k] for k in range(len(want))] == want
+    assert len(pipeline._run_names(tab, ids[:0], strands[:0])) == 0
