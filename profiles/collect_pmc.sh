@@ -7,7 +7,8 @@ OUT=$(realpath -m "$1"); shift
 R=$(pwd)
 mkdir -p "$OUT"
 cd /tmp && export TMPDIR=/tmp
-ARGS="--steps 3 --warmup 1 --cpu-sample 0 --no-tags-leg $*"
+# TAGS=1: keep bench's consensus-tag leg (the k_small<true> / k_large tag instances, summarised apart)
+if [ "${TAGS:-0}" = 1 ]; then ARGS="--steps 3 --warmup 1 --cpu-sample 0 $*"; else ARGS="--steps 3 --warmup 1 --cpu-sample 0 --no-tags-leg $*"; fi
 i=0
 for grp in \
   "SQ_WAVES SQ_BUSY_CYCLES SQ_WAVE_CYCLES SQ_INSTS_VALU SQ_INSTS_SALU SQ_INSTS_LDS SQ_INSTS_VMEM_RD SQ_INSTS_VMEM_WR" \

@@ -20,10 +20,12 @@ grouped = collections.defaultdict(dict)
 for k, disp in per.items():
     m = re.search(r"(k_small|k_large|k_join)", k)
     name = m.group(1) if m else k[:60]
-    if name == "k_join":  # the split families' join: one more dispatch of the k_large launch set
-        name = "k_large"
-    if name == "k_small" and "<true>" in k:  # the consensus-tag instance (BSDC_MODE_TAGS) on its own
+    if name == "k_small" and "k_small<true" in k:  # the consensus-tag instance (BSDC_MODE_TAGS) on its own
         name = "k_small_tags"
+    elif (name == "k_large" and re.search(r"k_large<(true|false), \d+, true", k)) or "k_join<true" in k:
+        name = "k_large_tags"  # (k_large<IN_LDS, G, TAGS, PART>, k_join<TAGS>)
+    elif name == "k_join":  # the split families' join: one more dispatch of the k_large launch set
+        name = "k_large"
     grouped[name].update({(k,) + key: v for key, v in disp.items()})
 out = {}
 for name, disp in grouped.items():
