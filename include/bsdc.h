@@ -213,7 +213,8 @@ int64_t bsdc_bgzf_scratch_bytes(int64_t max_blocks);
 /* Page-lock a caller's host range for DMA (hipHostRegister) / release it: a multi-GPU worker's
  * mappings of the shared segments its batches and outputs travel in (fleet.py), so uploads and
  * fetches run by DMA from / into them.  0, or BSDC_EDEVICE with the runtime's error cleared (a
- * range that stays pageable still works, at the pageable copy rate). */
+ * range that stays pageable still works, at the pageable copy rate).  No reference counterpart:
+ * the reference runs step 5 as one process per rule (main.snake.py:121-164, fgbio --threads). */
 int32_t bsdc_host_register(int32_t device, void *ptr, int64_t nbytes);
 int32_t bsdc_host_unregister(int32_t device, void *ptr);
 int32_t bsdc_bgzf_deflate(const uint8_t *in, int64_t n, int64_t blk0, int64_t nblk, uint8_t *scratch,
