@@ -38,12 +38,6 @@
 namespace {
 
 constexpr int kWave = 64;
-#ifndef SPLIT_FIRST
-#define SPLIT_FIRST 0  // bsdc_run: launch the split families' part and join dispatches before the classes
-#endif
-#ifndef SMALL_PERSIST
-#define SMALL_PERSIST 0  // k_small: 1 = persistent waves taking families from a per-class counter
-#endif
 #ifndef SMALL_WAVES
 #define SMALL_WAVES 7  // k_small waves per SIMD the register budget is cut for (7: <= 64 VGPRs, <= 96 SGPRs)
 #endif
@@ -1600,14 +1594,11 @@ __device__ __forceinline__ void small_family(const KParams &P, const Tables *T, 
     }
 }
 
-// One wavefront per family.  PERSIST = false: one family per wave, the grid covers the list.
-// PERSIST = true: the grid is what stays resident; a wave takes family blockIdx * waves + w first,
-// then the next unclaimed one from the class's counter (`ctr`, zeroed before the launch; one
-// vector atomic by lane 0 per family), so the tail is balanced and the tables are copied once per
-// resident workgroup.
-template <bool TAGS, bool PERSIST>
+// One wavefront per family, the grid covering the size class's list (persistent waves taking
+// families from a counter measured 4.4x slower: the loop costs registers).
+template <bool TAGS>
 __global__ __launch_bounds__(kWave *kSmallMaxWaves, kSmallMinWaves) __attribute__((amdgpu_num_sgpr(SMALL_SGPRS))) void k_small(
-    KParams P, const uint32_t *fams, int64_t nfams, int32_t arena, uint32_t *ctr) {
+    KParams P, const uint32_t *fams, int64_t nfams, int32_t arena) {
     extern __shared__ __attribute__((aligned(16))) uint8_t smem[];  // the wavefronts' arenas
     __shared__ __attribute__((aligned(16))) Tables s_tab;           // static: its address folds into offsets
     if (((P.mode >> BSDC_MODE_STOP_SHIFT) & 15) == 15) return;  // profiling: launch cost alone
@@ -1615,22 +1606,11 @@ __global__ __launch_bounds__(kWave *kSmallMaxWaves, kSmallMinWaves) __attribute_
     if (((P.mode >> BSDC_MODE_STOP_SHIFT) & 15) == 14) return;  // profiling: + the table copy
     const int w = threadIdx.x >> 6;
     const int t = threadIdx.x & 63;
-    int64_t fi = (int64_t)blockIdx.x * (blockDim.x >> 6) + w;
+    const int64_t fi = (int64_t)blockIdx.x * (blockDim.x >> 6) + w;
     // (the arenas start kArenaGuard bytes into smem: a dword load that straddles the start of a
     // family image -- its bytes before the image masked -- stays inside the allocation)
     uint8_t *A = smem + kArenaGuard + (size_t)w * (size_t)arena;
-    if (!PERSIST) {
-        if (fi < nfams) small_family<TAGS>(P, &s_tab, A, fams, fi, t);
-        return;
-    }
-    const int64_t first = (int64_t)gridDim.x * (blockDim.x >> 6);  // families handed out statically
-    while (fi < nfams) {  // every wave leaves once the counter passes the list's end
-        small_family<TAGS>(P, &s_tab, A, fams, fi, t);
-        uint32_t nx = 0;
-        if (t == 0) nx = atomicAdd(ctr, 1u);
-        fi = first + (int64_t)(uint32_t)__builtin_amdgcn_readfirstlane((int)nx);
-        wave_sync();  // (the arena is rewritten by the next family's staging)
-    }
+    if (fi < nfams) small_family<TAGS>(P, &s_tab, A, fams, fi, t);
 }
 
 // ==========================================================================================
@@ -2865,8 +2845,6 @@ struct bsdc_ctx {
     // caller's stream by events, so one dispatch's tail overlaps the next
     hipStream_t side[kForkStreams] = {};
     hipEvent_t ev_fork = nullptr, ev_join[kForkStreams] = {};
-    uint32_t *ctr = nullptr;  // (SMALL_PERSIST) one family counter per k_small size class
-    int n_cu = 0;
 };
 
 static float det_expf_host(float x) {
@@ -3080,9 +3058,7 @@ int32_t bsdc_ctx_create(int32_t device, const bsdc_params *params, bsdc_ctx **ou
     make_tables(params->error_rate_pre_umi, params->error_rate_post_umi, c->host_tab.t);
     make_fp64(params->error_rate_post_umi, c->host_tab.lnc, c->host_tab.lne3);
     if (hipSetDevice(device) != hipSuccess || hipMalloc(&c->dev_tab, sizeof(DevTables)) != hipSuccess ||
-        hipMemcpy(c->dev_tab, &c->host_tab, sizeof(DevTables), hipMemcpyHostToDevice) != hipSuccess ||
-        hipDeviceGetAttribute(&c->n_cu, hipDeviceAttributeMultiprocessorCount, device) != hipSuccess ||
-        (SMALL_PERSIST && hipMalloc(&c->ctr, 64 * sizeof(uint32_t)) != hipSuccess)) {
+        hipMemcpy(c->dev_tab, &c->host_tab, sizeof(DevTables), hipMemcpyHostToDevice) != hipSuccess) {
         bsdc_ctx_destroy(c);
         return BSDC_EDEVICE;
     }
@@ -3105,7 +3081,6 @@ void bsdc_ctx_destroy(bsdc_ctx *c) {
     (void)hipSetDevice(c->device);
     (void)hipFree(c->dev_tab);
     (void)hipFree(c->ref_seq);
-    (void)hipFree(c->ctr);
     for (int i = 0; i < kForkStreams; i++) {
         if (c->side[i]) (void)hipStreamDestroy(c->side[i]);
         if (c->ev_join[i]) (void)hipEventDestroy(c->ev_join[i]);
@@ -3243,12 +3218,6 @@ int32_t bsdc_run(bsdc_ctx *c, const bsdc_family_batch *b, bsdc_consensus *o, int
         const hipError_t e = hipGetLastError();
         if (e != hipSuccess) fail(e, "split launch");
     };
-    // (SPLIT_FIRST: the part -> join chain, the longest dependency of the call, goes out first)
-    if (SPLIT_FIRST && !(mode & BSDC_MODE_SKIP_LARGE)) launch_split();
-    if (SMALL_PERSIST && !(mode & BSDC_MODE_SKIP_SMALL)) {  // the class counters, before the fork
-        const hipError_t e = hipMemsetAsync(c->ctr, 0, BSDC_SMALL_BUCKETS * sizeof(uint32_t), s);
-        if (e != hipSuccess) fail(e, "hipMemsetAsync(counters)");
-    }
     if (!(mode & BSDC_MODE_SKIP_SMALL) && rc == 0) {
         const uint32_t *f = b->small_fams;
         for (int q = 0; q < BSDC_SMALL_BUCKETS && rc == 0; q++) {
@@ -3263,18 +3232,15 @@ int32_t bsdc_run(bsdc_ctx *c, const bsdc_family_batch *b, bsdc_consensus *o, int
                 const int64_t w8 = 8 * std::min<int64_t>(kSmallSimdWaves / 2, kLdsBytes / (kTabBytes + g2 + 8 * a));
                 const int nw = w8 > w4 ? 8 : 4;
                 const size_t lds = (size_t)nw * (size_t)b->small_arena[q] + (size_t)g2;  // + the static tables
-                int64_t blocks = (nf + nw - 1) / nw;
-                if (SMALL_PERSIST)  // the workgroups that stay resident (w4 / w8: waves per CU)
-                    blocks = std::min<int64_t>(blocks, (int64_t)c->n_cu * ((nw == 8 ? w8 : w4) / nw));
+                const int64_t blocks = (nf + nw - 1) / nw;
                 const hipStream_t ls = next_stream();
                 if (rc) break;
-                uint32_t *ctr = SMALL_PERSIST ? c->ctr + q : nullptr;
                 if (mode & BSDC_MODE_TAGS)
-                    hipLaunchKernelGGL((k_small<true, SMALL_PERSIST != 0>), dim3((unsigned)blocks), dim3(kWave * nw), lds, ls, P, f,
-                                       nf, b->small_arena[q], ctr);
+                    hipLaunchKernelGGL(k_small<true>, dim3((unsigned)blocks), dim3(kWave * nw), lds, ls, P, f, nf,
+                                       b->small_arena[q]);
                 else
-                    hipLaunchKernelGGL((k_small<false, SMALL_PERSIST != 0>), dim3((unsigned)blocks), dim3(kWave * nw), lds, ls, P, f,
-                                       nf, b->small_arena[q], ctr);
+                    hipLaunchKernelGGL(k_small<false>, dim3((unsigned)blocks), dim3(kWave * nw), lds, ls, P, f, nf,
+                                       b->small_arena[q]);
                 const hipError_t e = hipGetLastError();
                 if (e != hipSuccess) fail(e, "k_small launch");
             }
@@ -3323,7 +3289,7 @@ int32_t bsdc_run(bsdc_ctx *c, const bsdc_family_batch *b, bsdc_consensus *o, int
             }
             f += nf;
         }
-        if (!SPLIT_FIRST) launch_split();
+        launch_split();
     }
     // join: `s` waits for every side stream used -- also after a failed launch, so that no work
     // already queued on a side stream outlives the caller's view of the batch's buffers
