@@ -3204,16 +3204,22 @@ int32_t bsdc_run(bsdc_ctx *c, const bsdc_family_batch *b, bsdc_consensus *o, int
         const uint4 *pf = reinterpret_cast<const uint4 *>(b->split_parts);
         const uint4 *sf = reinterpret_cast<const uint4 *>(b->split_fams);
         const size_t jl = 8 * (size_t)o->stride + 8 * kJoinParts;
+        // k_join reads the sums header the parts write at the end of their vote: without
+        // BSDC_MODE_VOTE (the tools-only launches dump tool-2 records and stop before it) or with a
+        // profiling stop knob (the parts return early) that scratch is never written, so no join
+        const bool join = (mode & BSDC_MODE_VOTE) && ((mode >> BSDC_MODE_STOP_SHIFT) & 15) == 0;
         if (tg) {
             hipLaunchKernelGGL((k_large<true, kLargeThreads, true, true>), dim3((unsigned)b->n_split_parts), dim3(kLargeThreads),
                                (size_t)a, ls, P, pf, b->n_split_parts, a, (int64_t)0);
-            hipLaunchKernelGGL((k_join<true>), dim3((unsigned)b->n_split_fams), dim3(kJoinThreads), jl, ls, P, sf,
-                               b->n_split_fams);
+            if (join)
+                hipLaunchKernelGGL((k_join<true>), dim3((unsigned)b->n_split_fams), dim3(kJoinThreads), jl, ls, P, sf,
+                                   b->n_split_fams);
         } else {
             hipLaunchKernelGGL((k_large<true, kLargeThreads, false, true>), dim3((unsigned)b->n_split_parts),
                                dim3(kLargeThreads), (size_t)a, ls, P, pf, b->n_split_parts, a, (int64_t)0);
-            hipLaunchKernelGGL((k_join<false>), dim3((unsigned)b->n_split_fams), dim3(kJoinThreads), jl, ls, P, sf,
-                               b->n_split_fams);
+            if (join)
+                hipLaunchKernelGGL((k_join<false>), dim3((unsigned)b->n_split_fams), dim3(kJoinThreads), jl, ls, P, sf,
+                                   b->n_split_fams);
         }
         const hipError_t e = hipGetLastError();
         if (e != hipSuccess) fail(e, "split launch");

@@ -62,12 +62,16 @@ class SegmentPool:
 
     MIN = 16 << 20
 
-    def __init__(self, tag: str, keep: int = 8, pinner: Optional["HostPinner"] = None):
+    def __init__(self, tag: str, keep: int = 8, pinner: Optional["HostPinner"] = None,
+                 on_drop=None):
         self.prefix = "bsdc%d_%s_%x" % (os.getpid(), tag, id(self) & 0xFFFFFF)
         self.pinner = pinner  # (a GPU worker's: its segments are page-locked for DMA)
         self.segs: Dict[str, "shared_memory.SharedMemory"] = {}
         self.free: List[str] = []
         self.keep = keep
+        # on_drop(name): a segment was unlinked -- the other side unmaps (and unpins) its view of it
+        # (SegmentViews.forget), so neither side's mappings grow over a run
+        self.on_drop = on_drop
         self.n = 0
         self.created_bytes = 0  # (stats: fresh segments fault their pages in on first touch)
         self.closed = False
@@ -93,7 +97,12 @@ class SegmentPool:
     def prefill(self, count: int, size: int, threads: int = 4) -> threading.Thread:
         """Create `count` free segments of `size` bytes and fault their pages in, on a background
         thread (a fresh shared page costs a fault on first touch: ~1 GB/s, several times the copy
-        into it).  take() meanwhile creates what it needs itself."""
+        into it).  take() meanwhile creates what it needs itself.  The prefilled segments count
+        towards `keep`: give() trims the free list only beyond them, so steady state reuses them
+        instead of dropping and re-creating segments."""
+        with self.lock:
+            self.keep += count
+
         def run():
             for _ in range(count):
                 with self.lock:
@@ -127,6 +136,8 @@ class SegmentPool:
                 x = min(self.free, key=lambda y: self.segs[y].size)
                 self.free.remove(x)
                 self._drop(self.segs.pop(x))
+                if self.on_drop is not None:
+                    self.on_drop(x)
 
     def buf(self, name: str) -> memoryview:
         return self.segs[name].buf
@@ -218,6 +229,14 @@ class SegmentViews:
             self.open[name] = shm
         return shm.buf
 
+    def forget(self, name: str):
+        """The owner dropped segment `name`: unmap (and unpin) this side's view of it."""
+        shm = self.open.pop(name, None)
+        if shm is not None:
+            if self.pinner is not None:
+                self.pinner.unpin(shm)
+            _close(shm, unlink=False)
+
     def close(self):
         for shm in self.open.values():
             if self.pinner is not None:
@@ -308,8 +327,8 @@ def pack(obj, pool: Optional[SegmentPool] = None):
     def tree(o):
         from .bam import StringTable
         if isinstance(o, np.ndarray):
-            if o.nbytes < _SMALL:
-                return ("np", o)
+            if o.nbytes < _SMALL:  # (a copy: the queue pickles it later, and o may lie in a reused segment)
+                return ("np", np.array(o))
             name, off = place[id(o)]
             return ("sm", name, off, o.dtype.str, o.shape)
         if isinstance(o, StringTable):
@@ -391,14 +410,24 @@ def _worker(wid: int, device: int, runner_spec: Optional[str], tq, rq):
     segments and travel back by name; the coordinator releases them once their chunk is written."""
     runner = None
     pinner = HostPinner(device) if runner_spec is None else None  # (the GPU runner only)
-    pool = SegmentPool("w%d" % wid, pinner=pinner)
+    pool = SegmentPool("w%d" % wid, pinner=pinner, on_drop=lambda name: rq.put(("forget", wid, name)))
     views = SegmentViews(pinner)
+    taken: List[str] = []  # the segments alloc() handed out for the current batch
 
     def alloc(nbytes: int):
         if pool.n == 0:  # the first output: room for as many more, faulted in meanwhile
             pool.prefill(4, int(1.25 * nbytes) + 4096)
         name = pool.take(nbytes)
+        taken.append(name)
         return np.frombuffer(pool.buf(name), np.uint8, count=nbytes)
+
+    def unused(segs):
+        """Give back the alloc() segments the packed result does not refer to (a tiny
+        batch's outputs all travel pickled, so its fetch segment is never released otherwise)."""
+        for name in taken:
+            if name not in segs:
+                pool.give(name)
+        taken.clear()
     try:
         runner = _make_runner(runner_spec, device)
         rq.put(("ready", wid, bool(getattr(runner, "needs_raw", False))))
@@ -409,6 +438,8 @@ def _worker(wid: int, device: int, runner_spec: Optional[str], tq, rq):
             kind = msg[0]
             if kind == "release":
                 pool.give(msg[1])
+            elif kind == "forget":  # the coordinator dropped one of its segments
+                views.forget(msg[1])
             elif kind == "drop":  # the coordinator's run is over: unmap its segments
                 views.close()
             elif kind == "ref":
@@ -425,6 +456,7 @@ def _worker(wid: int, device: int, runner_spec: Optional[str], tq, rq):
                 del fb, raw_sub, fb_t, raw_t
                 t1 = time.perf_counter()
                 tree, segs = pack(out, pool)
+                unused(segs)
                 rq.put(("batch", wid, key, tree, segs,
                         {"worker_run": t1 - t0, "worker_pack": time.perf_counter() - t1}))
             elif kind == "chunk":
@@ -432,6 +464,7 @@ def _worker(wid: int, device: int, runner_spec: Optional[str], tq, rq):
                 cons = runner.run_chunk(unpack(raw_t, views), tags, batch_bases)
                 del raw_t
                 tree, segs = pack(cons, pool)
+                unused(segs)
                 rq.put(("chunk", wid, key, tree, segs, {}))
     except BaseException as e:  # noqa: BLE001 -- reported to the coordinator, which raises it
         rq.put(("error", wid, "%s: %s\n%s" % (type(e).__name__, e, traceback.format_exc())))
@@ -574,7 +607,9 @@ def step5_stream_multi(in_bam: str, fasta: str, out_bam: Optional[str], devices:
     mode = pipeline.MODE_CONVERT | pipeline.MODE_EXTEND | pipeline.MODE_VOTE
     own_fleet = fleet is None
     fleet = Fleet(devices, runner, inflight) if own_fleet else fleet
-    cpool = SegmentPool("c")  # batch images and messages; a batch's go back when its result arrives
+    # batch images and messages; a batch's go back when its result arrives; a dropped one is
+    # forgotten by every worker (fleet.broadcast is thread-safe: mp queues)
+    cpool = SegmentPool("c", on_drop=lambda name: fleet.broadcast(("forget", name)))
     # the segments the in-flight batches need, faulted in while the first chunk is read: a batch's
     # images are about 0.75 x its record bytes (bounded by the batch base budget too)
     est = int(0.75 * chunk_bytes)
@@ -705,6 +740,9 @@ def step5_stream_multi(in_bam: str, fasta: str, out_bam: Optional[str], devices:
                     break
                 m = fleet.get(timeout=0.5)
                 if m is None:
+                    continue
+                if m[0] == "forget":  # a worker dropped one of its result segments
+                    views.forget(m[2])
                     continue
                 kind, wid, (cid, i), res = m[0], m[1], m[2], unpack(m[3], views)
                 for k, v in m[5].items():  # (the workers' busy time, summed)

@@ -97,3 +97,40 @@ def test_pack_roundtrip():
     finally:
         views.close()
         pool.close()
+
+
+def test_segment_churn_and_forget():
+    """prefilled segments count towards `keep` (steady state reuses them, nothing is
+    dropped and re-created); a segment the pool does drop is reported through on_drop, and the
+    other side's SegmentViews.forget unmaps it; small arrays travel as copies (the queue pickles
+    them later, when their segment may already be reused)."""
+    dropped = []
+    pool = fleet.SegmentPool("c", keep=1, on_drop=dropped.append)
+    views = fleet.SegmentViews()
+    try:
+        pool.prefill(3, 1 << 20).join()
+        assert pool.keep == 4 and len(pool.free) == 3
+        names = [pool.take(1 << 10) for _ in range(3)]
+        for n in names:
+            pool.give(n)
+        assert dropped == [] and len(pool.free) == 3
+        names = [pool.take(1 << 10) for _ in range(3)]
+        extra = [pool.take(2 << 20) for _ in range(2)]  # two more than the prefilled ones
+        assert not set(extra) & set(names)
+        for n in extra + names:
+            views.buf(n)
+        for n in extra + names:
+            pool.give(n)
+        assert len(pool.free) == 4 and len(dropped) == 1
+        views.forget(dropped[0])
+        assert dropped[0] not in views.open and len(views.open) == 4 and dropped[0] not in pool.segs
+        views.forget("no-such-segment")
+        small = np.frombuffer(pool.buf(pool.free[0]), np.uint8, count=64)
+        small[:] = 3
+        tree, segs = fleet.pack({"q": small}, pool)
+        assert segs == [] and tree[1]["q"][1] is not small
+        small[:] = 5
+        assert (fleet.unpack(tree)["q"] == 3).all()
+    finally:
+        views.close()
+        pool.close()

@@ -387,6 +387,29 @@ def test_split_families_without_tags_vs_oracle(engine, monkeypatch, cfg, n_fam, 
     assert_consensus_equal(cons, oracle.run(s.raw, s.ref), "parts, no tags " + cfg)
 
 
+def test_split_families_tools_only_launch_vs_oracle(engine, monkeypatch):
+    """the split_ext fallback runs tools 1 + 2 as a launch of their own
+    (MODE_CONVERT | EXTEND | DUMP, no vote), and materialize cuts its large families into parts all
+    the same.  The parts dump their tool-2 records and stop before the vote, so no k_join may run
+    over their never-written sums; the records and the consensus of the vote launch after it equal
+    oracle/'s."""
+    s = synth.generate("C4", 250, seed=37, device="cpu", genome_len=300_000)
+    raw = s.raw  # (C4: singleton templates per strand, whose 4-record groups tool 2 extends, beside deep families)
+    for k in np.nonzero(raw.flag == 163)[0][3:400:7]:
+        raw.next_tid[int(k)] = 1
+    assert batch.plan_families(raw, "full", s.ref).split_ext
+    seen = []
+    force_parts(monkeypatch, 12000, seen)
+    engine.load_reference(s.ref)
+    cons, t2 = pipeline.run_step5(engine, raw, dump=True, tags=True)
+    assert sum(fb.split_fams.shape[0] for fb in seen) > 5
+    ref = oracle.run(raw, s.ref)
+    for k in ("src", "pos", "seq", "qual", "cigar"):
+        assert np.array_equal(getattr(t2, k), getattr(ref.tool2, k)), "split_ext parts tool-2 %s" % k
+    assert_consensus_equal(cons, ref, "split_ext parts")
+    assert_ss_equal(cons, ref, "split_ext parts")
+
+
 def test_split_families_molecular_vs_oracle(engine, monkeypatch):
     """Part mode under step 1's caller (MI runs, no BA side, --min-consensus-base-quality=0): the
     join masks with the context's own threshold, bit-exact against oracle/ at 0."""
