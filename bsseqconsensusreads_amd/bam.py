@@ -30,7 +30,7 @@ from . import records as R
 
 IO_LIB_PATH = os.environ.get("BSDC_IO_LIB_PATH") or os.path.join(os.path.dirname(os.path.abspath(__file__)),
                                                                  "libbsdc_io.so")
-BSDC_IO_ABI_VERSION = 8
+BSDC_IO_ABI_VERSION = 9
 _P = C.c_void_p
 
 
@@ -133,6 +133,20 @@ def _load():
     lib.bsdc_unpack_nibbles.restype = None
     lib.bsdc_rows_gather.argtypes = [C.c_int64, _P, _P, C.c_int64, _P, _P, _P, C.c_int32]
     lib.bsdc_rows_gather.restype = None
+    lib.bsdc_bam_find_cut.argtypes = [C.c_char_p, C.c_int32, C.c_int64, C.c_int64, C.c_int64, C.c_int64, C.c_int64,
+                                      _P]
+    lib.bsdc_bam_find_cut.restype = C.c_int32
+    lib.bsdc_bam_stream_open_range.argtypes = [C.c_char_p, C.c_int32, C.c_int64, C.c_int64, C.c_int64, C.c_int64,
+                                               C.c_int64, C.POINTER(_P)]
+    lib.bsdc_bam_stream_open_range.restype = C.c_int32
+    lib.bsdc_bam_stream_set_owner.argtypes = [_P, C.c_int32, _P, C.c_int32, C.c_int64, C.c_int32]
+    lib.bsdc_bam_stream_set_owner.restype = C.c_int32
+    lib.bsdc_bam_stream_range_stats.argtypes = [_P, _P]
+    lib.bsdc_bam_stream_range_stats.restype = None
+    lib.bsdc_bam_writer_fragment.argtypes = [_P, C.c_int32]
+    lib.bsdc_bam_writer_fragment.restype = C.c_int32
+    lib.bsdc_fastq_writer_fragment.argtypes = [_P]
+    lib.bsdc_fastq_writer_fragment.restype = C.c_int32
     if lib.bsdc_io_abi_version() != BSDC_IO_ABI_VERSION:
         raise RuntimeError("libbsdc_io ABI %d != %d" % (lib.bsdc_io_abi_version(), BSDC_IO_ABI_VERSION))
     _lib = lib
@@ -346,19 +360,58 @@ class StreamChunk:
             self._lib.bsdc_bam_stream_recycle(self._st, h)
 
 
+KEY_GUARD = 16  # positions of key gap on each side of a rank boundary (> 2 x kKeyDelta of the tools' jitter)
+
+
+def find_cut(path: str, start: int, threads: int = 0, min_span: Optional[int] = None, slack: int = DEFAULT_SLACK,
+             guard: int = KEY_GUARD, max_bytes: int = 256 << 20):
+    """A rank boundary of a coordinate-sorted BAM after file offset `start` (bsdc_bam_find_cut), or
+    None: a dict with `key` (the boundary X, 2 ints), `coord` (contig << 32 | x), `start` (block,
+    offset) of the first record at or past x - slack, `end` the same at or past x + slack, and
+    `slack`."""
+    lib = _load()
+    out = np.zeros(8, np.int64)
+    ms = 2 * slack if min_span is None else min_span
+    if lib.bsdc_bam_find_cut(path.encode(), int(threads), int(start), int(ms), int(slack), int(guard), int(max_bytes),
+                             _ptr(out)) != 0:
+        raise OSError("%s: %s" % (path, lib.bsdc_io_last_error().decode()))
+    if not out[7]:
+        return None
+    return {"start": (int(out[0]), int(out[1])), "end": (int(out[2]), int(out[3])), "key": (int(out[4]), int(out[5])),
+            "coord": int(out[6]), "slack": int(slack)}
+
+
 def stream_chunks(path: str, threads: int = 0, chunk_bytes: int = DEFAULT_CHUNK_BYTES, slack: int = DEFAULT_SLACK,
-                  read_size: int = 8 << 20, runs: bool = False):
+                  read_size: int = 8 << 20, runs: bool = False, rng=None, stats: Optional[dict] = None, owner=None):
     """The chunks of a coordinate-sorted BAM in bounded memory, undecoded (StreamChunk): cut where no
     template or MI family straddles two chunks (include/bsdc_io.h, bsdc_bam_stream_next_raw).  The
     stream itself is freed once it is exhausted and every chunk has been decoded or discarded.
     runs: a GroupReadsByUmi-ordered BAM (step 1's input) cut between runs of one MI value instead
-    (bsdc_bam_stream_next_runs; any record order, no `slack`)."""
+    (bsdc_bam_stream_next_runs; any record order, no `slack`).  rng: (start block, offset in it,
+    end block, offset in it) -- the records of that range only (start block -1: from the first
+    record, end block -1: to the end; bsdc_bam_stream_open_range); `stats` then receives the range
+    statistics (bsdc_bam_stream_range_stats: n, c0, dropped, foreign) once the stream is exhausted.
+    owner: (rank, boundaries[, stop]) -- keep the records whose key lies in the rank's interval
+    between the boundaries (find_cut dicts; bsdc_bam_stream_set_owner); stop: a foreign record
+    raises OSError("... foreign record ...")."""
     lib = _load()
     st = _P()
-    rc = lib.bsdc_bam_stream_open(path.encode(), int(threads), int(read_size), C.byref(st))
+    if rng is None:
+        rc = lib.bsdc_bam_stream_open(path.encode(), int(threads), int(read_size), C.byref(st))
+    else:
+        rc = lib.bsdc_bam_stream_open_range(path.encode(), int(threads), int(read_size), *[int(x) for x in rng],
+                                            C.byref(st))
     if rc != 0:
         raise OSError("%s: %s" % (path, lib.bsdc_io_last_error().decode()))
     try:
+        if owner is not None:
+            rank, cuts = owner[:2]
+            stop = len(owner) > 2 and bool(owner[2])
+            bd = np.array([[c["key"][0], c["key"][1], c["coord"]] for c in cuts], np.int64).reshape(-1)
+            wsl = min(c["slack"] for c in cuts) if cuts else 0  # (the windows' own margin)
+            if lib.bsdc_bam_stream_set_owner(st, int(rank), _ptr(bd) if len(bd) else None, len(cuts), int(wsl),
+                                             int(stop)) != 0:
+                raise OSError("%s: %s" % (path, lib.bsdc_io_last_error().decode()))
         while True:
             h = _P()
             if runs:
@@ -368,6 +421,10 @@ def stream_chunks(path: str, threads: int = 0, chunk_bytes: int = DEFAULT_CHUNK_
             if rc != 0:
                 raise OSError("%s: %s" % (path, lib.bsdc_io_last_error().decode()))
             if not h:
+                if stats is not None:
+                    v = np.zeros(4, np.int64)
+                    lib.bsdc_bam_stream_range_stats(st, _ptr(v))
+                    stats.update(n=int(v[0]), c0=int(v[1]), dropped=int(v[2]), foreign=int(v[3]))
                 return
             yield StreamChunk(lib, st, h, path)
     finally:
@@ -741,7 +798,10 @@ class BamWriter:
     deflated on the GPU (valid BGZF, other compressed bytes), one add's blocks compressing while
     the next add encodes."""
 
-    def __init__(self, path: str, header: BamHeader, level: int = 6, gpu: Optional["GpuBgzf"] = None):
+    def __init__(self, path: str, header: BamHeader, level: int = 6, gpu: Optional["GpuBgzf"] = None,
+                 fragment: Optional[str] = None):
+        """fragment: "first" (header, no EOF block) or "next" (neither) -- one rank's piece of a
+        BAM that ranks.assemble concatenates."""
         self.lib = _load()
         self.path = path
         self.gpu = gpu
@@ -762,6 +822,8 @@ class BamWriter:
                                            int(level), C.byref(self.h))
         if rc != 0:
             raise OSError("%s: %s" % (path, self.lib.bsdc_io_last_error().decode()))
+        if fragment is not None and self.lib.bsdc_bam_writer_fragment(self.h, int(fragment == "first")) != 0:
+            raise self._err()
 
     def _err(self):
         return OSError("%s: %s" % (self.path, self.lib.bsdc_io_last_error().decode()))
@@ -829,7 +891,8 @@ class FastqWriter:
     both files are deflated on the GPU in one job (valid BGZF-framed gzip, other compressed
     bytes), one add's blocks compressing while the next add encodes."""
 
-    def __init__(self, path1: str, path2: str, level: int = 6, gpu: Optional["GpuBgzf"] = None):
+    def __init__(self, path1: str, path2: str, level: int = 6, gpu: Optional["GpuBgzf"] = None,
+                 fragment: bool = False):
         self.lib = _load()
         self.path = path1
         self.gpu = gpu
@@ -837,6 +900,8 @@ class FastqWriter:
         self.h = _P()
         if self.lib.bsdc_fastq_writer_open(path1.encode(), path2.encode(), int(level), C.byref(self.h)) != 0:
             raise OSError("%s: %s" % (path1, self.lib.bsdc_io_last_error().decode()))
+        if fragment and self.lib.bsdc_fastq_writer_fragment(self.h) != 0:  # (no EOF blocks: ranks.assemble)
+            raise self._err()
 
     def _err(self):
         return OSError("%s: %s" % (self.path, self.lib.bsdc_io_last_error().decode()))
@@ -1116,7 +1181,8 @@ def molecular_stream(in_bam: str, out_bam: Optional[str], engine=None, prefix: O
 def _stream_step(in_bam: str, fasta: Optional[str], out_bam: Optional[str], engine, prefix: Optional[str],
                  threads: int, level: int, fastq: Optional[Tuple[str, str]], tags: bool, chunk_bytes: int, slack: int,
                  batch_bases: Optional[int], stats: Optional[dict], gpu_bgzf: bool,
-                 molecular: Optional[int]) -> dict:
+                 molecular: Optional[int], rng=None, fragment: Optional[str] = None, runner=None,
+                 range_stats: Optional[dict] = None, owner=None) -> dict:
     """step5 (molecular None) or step 1 (molecular = its --min-consensus-base-quality) in bounded
     memory, pipelined: a decoder thread cuts the next chunk of the
     coordinate-sorted input (stream_bam: inflate, split where no template or MI family straddles),
@@ -1128,15 +1194,24 @@ def _stream_step(in_bam: str, fasta: Optional[str], out_bam: Optional[str], engi
     byte-identical to step5's (tests/test_stream.py): every chunk's TemplateCoordinate keys sort
     before the next chunk's, so the chunks' families in order are the whole file's.  gpu_bgzf: the
     BAM's and the FASTQ pair's blocks are deflated on the engine's GPU (GpuBgzf; the same records,
-    other compressed bytes, files ≈4% larger)."""
+    other compressed bytes, files ≈4% larger).
+    rank-parallel use (ranks.py): rng = the record range of the input to run (stream_chunks),
+    range_stats its statistics once read, fragment = "first" / "next" (the output pieces a rank
+    writes: BamWriter, FastqWriter), runner = a fleet-style runner (run_batch / run_chunk; the CPU
+    stand-in of the tests) instead of an Engine."""
     import queue
     import threading
     import time
 
     from . import pipeline
-    from .device import Engine, PinnedPool
-    own = engine is None
-    eng = Engine(0) if own else engine
+    own = engine is None and runner is None
+    if runner is None:
+        from .device import Engine, PinnedPool
+        eng = Engine(0) if own else engine
+    else:
+        eng = None
+        if gpu_bgzf or molecular is not None:
+            raise ValueError("a runner stream: step 5 with host deflate only")
     chunks: "queue.Queue" = queue.Queue(maxsize=1)
     outs: "queue.Queue" = queue.Queue(maxsize=1)
     err: list = []
@@ -1155,7 +1230,8 @@ def _stream_step(in_bam: str, fasta: Optional[str], out_bam: Optional[str], engi
         # reader thread parses the one before
         it = None
         try:
-            it = stream_chunks(in_bam, threads, chunk_bytes, slack, runs=molecular is not None)
+            it = stream_chunks(in_bam, threads, chunk_bytes, slack, runs=molecular is not None, rng=rng,
+                               stats=range_stats, owner=owner)
             while not stop.is_set():
                 t0 = time.perf_counter()
                 nxt = next(it, None)
@@ -1197,7 +1273,7 @@ def _stream_step(in_bam: str, fasta: Optional[str], out_bam: Optional[str], engi
 
     # the planner materializes chunk k's batches into pool k % 3: chunk k - 3 is done on the GPU
     # by then (the planner handed chunk k - 1 over only after the GPU stage took chunk k - 2)
-    pools = [PinnedPool() for _ in range(3)]
+    pools = [PinnedPool() for _ in range(3)] if runner is None else None
 
     def planner():  # forms a chunk's families and materializes its batches ahead of the GPU stage
         try:
@@ -1219,10 +1295,13 @@ def _stream_step(in_bam: str, fasta: Optional[str], out_bam: Optional[str], engi
                 t1 = time.perf_counter()
                 fbs = None
                 if not plan.split_ext:
-                    pool = pools[k % 3]
-                    k += 1
-                    pool.reset()
-                    fbs = pipeline.materialize_ranges(plan, pipeline.plan_ranges(plan, batch_bases), pool.images)
+                    images = None
+                    if pools is not None:
+                        pool = pools[k % 3]
+                        k += 1
+                        pool.reset()
+                        images = pool.images
+                    fbs = pipeline.materialize_ranges(plan, pipeline.plan_ranges(plan, batch_bases), images)
                 T["plan"] += t1 - t0
                 T["materialize"] += time.perf_counter() - t1
                 chunks.put((raw, plan, fbs))
@@ -1264,8 +1343,8 @@ def _stream_step(in_bam: str, fasta: Optional[str], out_bam: Optional[str], engi
         try:
             gz = GpuBgzf(eng.device) if gpu_bgzf and out_bam is not None else None
             gzf = GpuBgzf(eng.device) if gpu_bgzf and fastq is not None else None  # (one job in flight each)
-            w = BamWriter(out_bam, output_header(first["header"]), level, gz) if out_bam is not None else None
-            fq = FastqWriter(fastq[0], fastq[1], level, gzf) if fastq is not None else None
+            w = BamWriter(out_bam, output_header(first["header"]), level, gz, fragment) if out_bam is not None else None
+            fq = FastqWriter(fastq[0], fastq[1], level, gzf, fragment is not None) if fastq is not None else None
             while True:
                 item = recq.get()
                 if item is None:
@@ -1308,7 +1387,7 @@ def _stream_step(in_bam: str, fasta: Optional[str], out_bam: Optional[str], engi
         raise
     try:
         if ref is not None:
-            eng.load_reference(ref)
+            (runner if runner is not None else eng).load_reference(ref)
         td = threading.Thread(target=decoder, daemon=True)
         tr = threading.Thread(target=reader, daemon=True)
         tp = threading.Thread(target=planner, daemon=True)
@@ -1334,7 +1413,17 @@ def _stream_step(in_bam: str, fasta: Optional[str], out_bam: Optional[str], engi
                 raw, plan, fbs = item
                 t0 = time.perf_counter()
                 tg = tags and out_bam is not None  # the FASTQ pair carries no tags
-                if fbs is None:
+                if runner is not None:
+                    if fbs is None:
+                        cons = runner.run_chunk(raw, tg, batch_bases)
+                    else:
+                        parts = []
+                        for fb in fbs:
+                            sub = R.take(raw, fb.src) if getattr(runner, "needs_raw", False) else None
+                            parts.append(pipeline.consensus_from_output(fb, runner.run_batch(fb, mode, tg, sub)))
+                        cons = pipeline.concat_consensus(parts)
+                        del fbs, parts
+                elif fbs is None:
                     cons = pipeline.run_step5(eng, raw, tags=tg, batch_bases=batch_bases)[0]
                 else:
                     cons = pipeline.concat_consensus(pipeline.run_batches(eng, fbs, mode, tg, G))

@@ -22,6 +22,7 @@ from typing import List, Optional
 
 import numpy as np
 
+from . import _lib
 from . import records as R
 
 LINK_MATE_NONE = 0xFFFF
@@ -74,12 +75,12 @@ def small_arena_bytes(n, img, nconv, complex_ops, max_len):
     n = np.asarray(n, dtype=np.int64)
     ws = 32 * ref_chunks(max_len)
     cops = np.asarray(complex_ops, dtype=np.int64)
-    ow = int(round16(int(max_len) + 2))
-    R = 2 * np.asarray(img, dtype=np.int64) + round16(4 * n) + 16 + round16(n)
-    e_ref = R + np.asarray(nconv, dtype=np.int64) * ws
+    rw = int(round16((int(max_len) + 2 + 19) // 20 * 20))  # k_pair's single-strand rows (>= the vote rows of k_small)
+    R = 2 * np.asarray(img, dtype=np.int64) + round16(4 * n) + 32 + round16(n)
+    e_ref = R + np.asarray(nconv, dtype=np.int64) * (ws + 16)  # (k_pair: + the converted records' info)
     simp = R + round16(16 * n) + round16(n) + 2 * round16(2 * n)
-    e_f = simp + np.where(cops > 0, round16(4 * (cops + 4 * n)), 0)
-    e_v = R + 8 * ow
+    e_f = simp + np.where(cops > 0, round16(4 * (cops + 4 * n)) + 256, 0)  # (+ filter_group's scratch)
+    e_v = R + 8 * rw
     return np.maximum(np.maximum(e_ref, e_f), e_v)
 
 
@@ -91,7 +92,7 @@ def large_arena_bytes(n, slot_bytes, max_len, complex_ops):
     # ORs and read counts: 44 B per column (bsdc_layout::kVoteRegionPerCol)
     total = np.maximum(round16(n * 48) + round16(2 * n), 44 * ssw) + round16(n * 8) + 8 * ssw
     cops = np.asarray(complex_ops, dtype=np.int64)
-    total = total + np.where(cops > 0, round16(4 * (cops + 4 * n)), 0)
+    total = total + np.where(cops > 0, round16(4 * (cops + 4 * n)) + 512, 0)  # (+ filter_group's scratch, X and Y)
     total = total + round16(np.asarray(slot_bytes, dtype=np.int64))
     return total
 
@@ -171,7 +172,22 @@ class FamilyBatch:
         total = poff + psz
         return (total + 256 if total else 0), base, poff
 
+    def pair_order(self) -> List[int]:
+        """Per small bucket, its families of more than 32 records (include/bsdc.h n_small_wide) moved
+        to the end of the bucket, in order: k_pair runs the others two per wavefront, k_small these
+        one per wavefront.  -> the wide count per bucket (idempotent)."""
+        sizes = np.diff(self.fam_off.astype(np.int64))
+        wide = []
+        for q, b in enumerate(self.small_buckets):
+            w = sizes[b.astype(np.int64)] > _lib.PAIR_MAX_REC if b.shape[0] else np.zeros(0, bool)
+            nw = int(w.sum())
+            if nw and not w[-nw:].all():
+                self.small_buckets[q] = np.concatenate([b[~w], b[w]]).astype(b.dtype)
+            wide.append(nw)
+        return wide
+
     def device_arrays(self):
+        self.pair_order()
         rec = np.stack([self.rec_off, self.rec_pos.view(np.uint32), self.rec_lenflag, self.rec_link], axis=1)
         d = {"fam_off": self.fam_off, "rec": np.ascontiguousarray(rec, dtype=np.uint32),
              "rec_win": np.ascontiguousarray(self.rec_win, dtype=np.uint32)}

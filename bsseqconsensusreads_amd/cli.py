@@ -14,10 +14,13 @@ step5 on one GPU streams a coordinate-sorted input (--stream auto, the default: 
 says SO:coordinate): bounded memory whatever the input size, decode / GPU / encode overlapped,
 output identical to the whole-file path (bam.step5_stream).  Other inputs are read whole
 (bam.step5); --stream true insists on streaming (an unsorted input is then an error).
-step5 --gpus N on a coordinate-sorted input streams too (fleet.step5_stream_multi): this process
-reads the BAM once and writes the outputs in order, N spawned worker processes (one per GPU) run
-the family batches it deals them through shared memory; bounded memory, output identical to
---gpus 1.  Other inputs (or a run under torch.distributed.run) take the whole-file path: one
+step5 --gpus N on a coordinate-sorted input streams too.  --multi ranks (the default;
+ranks.step5_ranks): N spawned rank processes (one per GPU) each decode, compute and encode their
+own key interval of the file, and this process concatenates their fragments -- no front end.
+When a record's owner could not read it (a mate on another contig or unmapped) the ranks stop
+and the file runs as --multi fleet (fleet.step5_stream_multi): this process reads the BAM once
+and writes the outputs in order, N spawned worker processes run the family batches it deals them
+through shared memory.  Both: bounded memory, output identical to --gpus 1.  Other inputs (or a run under torch.distributed.run) take the whole-file path: one
 process per GPU, every rank forms the plan, batches dealt to the ranks, rank 0 writes
 (bam.consensus_sharded).  --devices maps workers / ranks to device ids (default 0..N-1).
 """
@@ -51,6 +54,10 @@ def parse(argv):
         if name == "step5":
             p.add_argument("--gpus", type=int, default=1, help="one process per GPU, family batches dealt to them")
             p.add_argument("--devices", default=None, help="comma-separated device id per rank (default 0..gpus-1)")
+            p.add_argument("--multi", default="ranks", choices=["ranks", "fleet"],
+                           help="--gpus N on a coordinate-sorted input: ranks = each GPU's process reads, computes "
+                                "and writes its own part of the file (ranks.py; fleet when a record's owner could "
+                                "not read it); fleet = one process reads and writes, the GPUs' processes compute")
             p.add_argument("--stream", default="auto", choices=["auto", "true", "false"],
                            help="bounded-memory pipelined step (bam.step5_stream; coordinate-sorted input); "
                                 "false = read the whole BAM first (bam.step5); auto = stream when the header "
@@ -83,12 +90,27 @@ def _coordinate_sorted(bam, path: str) -> bool:
 
 
 def _step5_fleet(a, gpus: int) -> int:
-    """step5 --gpus N on a coordinate-sorted input: fleet.step5_stream_multi (module docstring)."""
-    from . import fleet
+    """step5 --gpus N on a coordinate-sorted input: ranks.step5_ranks, or fleet.step5_stream_multi
+    (module docstring)."""
+    from . import fleet, ranks
     devs = [int(x) for x in a.devices.split(",")] if a.devices else list(range(gpus))
     if len(devs) != gpus:
         print("--devices needs %d ids" % gpus, file=sys.stderr)
         return 2
+    if a.multi == "ranks":
+        try:
+            info = ranks.step5_ranks(a.input, a.reference, None if a.output == "-" else a.output, devs,
+                                     a.read_name_prefix, a.threads, a.compression,
+                                     (a.fastq1, a.fastq2) if a.fastq1 else None,
+                                     tags=a.output_per_base_tags == "true", chunk_bytes=a.chunk_mb << 20,
+                                     batch_bases=a.batch_bases, gpu_bgzf=a.gpu_bgzf == "true", on_foreign="raise")
+            print(json.dumps(info), file=sys.stderr)
+            return 0
+        except ranks.ForeignRecords as e:
+            print("ranks: %s; running --multi fleet" % e, file=sys.stderr)
+        except Exception as e:  # noqa: BLE001 -- the rule fails with the message
+            print("%s: %s" % (type(e).__name__, e), file=sys.stderr)
+            return 1
     try:
         info = fleet.step5_stream_multi(a.input, a.reference, None if a.output == "-" else a.output, devs,
                                         a.read_name_prefix, a.threads, a.compression,

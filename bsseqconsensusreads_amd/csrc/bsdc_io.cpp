@@ -604,6 +604,72 @@ constexpr int64_t kBigTid = 0x7FFFFFFF;
 constexpr int64_t kKeyDelta = 4;  // |key position before tools 1 + 2 - after| <= 2, twice
 constexpr int kFamShards = 64;
 inline int fam_shard(uint64_t h) { return (int)(h >> 58); }
+// A record's coordinate c, its reach e (max of its own and its mate's coordinate) and its coarse
+// TemplateCoordinate key: the template's lower end's contig, then the other end's (BIG for an
+// unpaired record or unmapped mate), then the lower end's unclipped 5' position -- from the
+// input's cigar and MC, so within kKeyDelta of the key of the records tools 1 and 2 make (a
+// prepended base, an appended one, the RD trim).  r: a whole record (block_size first); mc: its MC
+// value (empty if absent).
+struct RecKey {
+    int64_t c, e;
+    TcKey key;
+};
+inline RecKey rec_key(const uint8_t *r, std::string_view mc) {
+    const int l_name = r[12];
+    const int n_cig = rd16(r + 16);
+    const int32_t tid = rdi32(r + 4), pos = rdi32(r + 8), ntid = rdi32(r + 24), npos = rdi32(r + 28);
+    const int flag = rd16(r + 18);
+    const int64_t c = coord(tid, pos);
+    const uint8_t *cg = r + 36 + l_name;
+    int64_t lead = 0, trail = 0, reflen = 0;
+    {
+        int first_nc = -1, last_nc = -1;
+        for (int i = 0; i < n_cig; i++) {
+            const uint32_t op = rd32(cg + 4 * i) & 15;
+            if (op == 0 || op == 2 || op == 3 || op == 7 || op == 8) reflen += rd32(cg + 4 * i) >> 4;
+            if (op != 4 && op != 5) {
+                if (first_nc < 0) first_nc = i;
+                last_nc = i;
+            }
+        }
+        for (int i = 0; i < n_cig; i++) {
+            const uint32_t op = rd32(cg + 4 * i) & 15;
+            if (op != 4 && op != 5) continue;
+            if (first_nc < 0 || i < first_nc) lead += rd32(cg + 4 * i) >> 4;
+            else if (i > last_nc) trail += rd32(cg + 4 * i) >> 4;
+        }
+    }
+    const int64_t p_own = (flag & 16) ? pos + reflen - 1 + trail : pos - lead;
+    int64_t p_mate = npos;
+    if (!mc.empty() && !(mc.size() == 1 && mc[0] == '*')) {
+        int64_t mlead = 0, mref = 0, num = 0, clip_run = 0;  // clip_run: clips since the last non-clip op
+        bool seen_nc = false;
+        for (char ch : mc) {
+            if (ch >= '0' && ch <= '9') {
+                num = num * 10 + (ch - '0');
+                continue;
+            }
+            if (ch == 'M' || ch == 'D' || ch == 'N' || ch == '=' || ch == 'X') mref += num;
+            if (ch == 'S' || ch == 'H') {
+                if (!seen_nc) mlead += num;
+                else clip_run += num;
+            } else {
+                seen_nc = true;
+                clip_run = 0;
+            }
+            num = 0;
+        }
+        p_mate = (flag & 32) ? npos + mref - 1 + clip_run : npos - mlead;
+    }
+    const bool paired = (flag & 1) && !(flag & 8) && ntid >= 0;
+    const int64_t t1 = tid < 0 ? kBigTid : tid;
+    TcKey key;
+    if (!paired) key = {(t1 << 32) | kBigTid, p_own};
+    else if (tid == ntid) key = {(t1 << 32) | t1, std::min(p_own, p_mate)};
+    else if (tid >= 0 && tid < ntid) key = {(t1 << 32) | (int64_t)ntid, p_own};
+    else key = {((int64_t)ntid << 32) | t1, p_mate};
+    return RecKey{c, ntid >= 0 ? std::max(c, coord(ntid, npos)) : c, key};
+}
 struct StreamFam {
     int64_t lo = INT64_MAX, hi = INT64_MIN;  // min own position, max own or mate position (coord)
     TcKey klo{INT64_MAX, INT64_MAX}, khi{INT64_MIN, INT64_MIN};  // bounds of its records' keys
@@ -644,6 +710,20 @@ struct bsdc_bam_stream {
     bool closed = false;
     // MI-run chunks (bsdc_bam_stream_next_runs): the MI value of the last record scanned
     std::string run_mi;
+    // a record range of the file (bsdc_bam_stream_open_range): reading starts at a BGZF block and
+    // drops skip_head inflated bytes, and stops at file offset `limit` (-1: the end), dropping the
+    // last block's drop_tail bytes; fpos = the file offset read so far
+    int64_t fpos = 0, limit = -1, skip_head = 0, drop_tail = 0;
+    int64_t hdr_len = 0;  // the header's uncompressed bytes (the first record's offset)
+    // a rank's key interval (bsdc_bam_stream_set_owner): -1 = every record
+    int32_t own_rank = -1;
+    std::vector<TcKey> own_bounds;
+    std::vector<int64_t> own_coord;
+    int64_t own_slack = 0;
+    bool own_stop = false;
+    int64_t st_dropped = 0, st_foreign = 0;
+    // statistics of the records split so far: count, first coordinate, max reach, key bounds
+    int64_t st_n = 0, st_c0 = 0;
 };
 
 int32_t bsdc_bam_stream_open(const char *path, int32_t n_threads, int64_t read_size, bsdc_bam_stream **out) {
@@ -667,6 +747,7 @@ int32_t bsdc_bam_stream_open(const char *path, int32_t n_threads, int64_t read_s
             s->hdr.ref_len = probe.ref_len;
             s->buf.erase(s->buf.begin(), s->buf.begin() + p);
             s->tail = 0;
+            s->hdr_len = p;
             break;
         }
         if (s->eof) {
@@ -685,21 +766,372 @@ int32_t bsdc_bam_stream_open(const char *path, int32_t n_threads, int64_t read_s
     return 0;
 }
 
+namespace {
+// The BGZF block header at comp[0, n): its total size, or -1 if these bytes are no block header.
+int64_t bgzf_block_size(const uint8_t *h, int64_t n) {
+    if (n < 18 || h[0] != 31 || h[1] != 139 || h[2] != 8 || !(h[3] & 4)) return -1;
+    const int xlen = rd16(h + 10);
+    if (n < 12 + xlen) return -1;
+    for (int x = 0; x + 4 <= xlen;) {
+        const uint8_t *sf = h + 12 + x;
+        const int slen = rd16(sf + 2);
+        if (sf[0] == 'B' && sf[1] == 'C' && slen == 2) return (int64_t)rd16(sf + 4) + 1;
+        x += 4 + slen;
+    }
+    return -1;
+}
+}  // namespace
+
+// A record range of a coordinate-sorted BAM as a stream (see include/bsdc_io.h).
+int32_t bsdc_bam_stream_open_range(const char *path, int32_t n_threads, int64_t read_size, int64_t start_block,
+                                   int64_t start_off, int64_t end_block, int64_t end_off, bsdc_bam_stream **out) {
+    *out = nullptr;
+    bsdc_bam_stream *s = nullptr;
+    int32_t rc = bsdc_bam_stream_open(path, n_threads, read_size, &s);
+    if (rc != 0) return rc;
+    if (start_block < 0 && end_block >= 0) {  // the first range: from the file start, past the header
+        start_block = 0;
+        start_off = s->hdr_len;
+    }
+    if (start_block >= 0) {  // drop what the header read buffered; start at the block
+        if (fseeko(s->f, (off_t)start_block, SEEK_SET) != 0) {
+            bsdc_bam_stream_close(s);
+            return fail(BSDC_IO_EIO, "seek failed");
+        }
+        s->comp.clear();
+        s->buf.clear();
+        s->tail = 0;
+        s->eof = false;
+        s->fpos = start_block;
+        s->skip_head = start_off;
+    }
+    if (end_block >= 0) {
+        if (start_block >= 0 ? end_block < start_block : false) {
+            bsdc_bam_stream_close(s);
+            return fail(BSDC_IO_EFORMAT, "bad record range");
+        }
+        if (end_off == 0) {  // the range ends where that block starts
+            s->limit = end_block;
+        } else {
+            uint8_t h[64];
+            FILE *g = fopen(path, "rb");
+            const bool ok = g && fseeko(g, (off_t)end_block, SEEK_SET) == 0 && fread(h, 1, sizeof h, g) >= 18;
+            int64_t bs = ok ? bgzf_block_size(h, sizeof h) : -1;
+            uint8_t foot[4];
+            const bool ok2 = bs > 0 && fseeko(g, (off_t)(end_block + bs - 4), SEEK_SET) == 0 && fread(foot, 1, 4, g) == 4;
+            if (g) fclose(g);
+            if (!ok2 || end_off > (int64_t)rd32(foot)) {
+                bsdc_bam_stream_close(s);
+                return fail(BSDC_IO_EFORMAT, "bad record range end");
+            }
+            s->limit = end_block + bs;
+            s->drop_tail = (int64_t)rd32(foot) - end_off;
+        }
+        if (s->fpos >= s->limit) {  // (a header read that went past a range end inside the first block)
+            bsdc_bam_stream_close(s);
+            return fail(BSDC_IO_EFORMAT, "record range ends inside the header read; open it from a block");
+        }
+    }
+    *out = s;
+    return 0;
+}
+
+void bsdc_bam_stream_range_stats(const bsdc_bam_stream *s, int64_t *st) {
+    st[0] = s->st_n;
+    st[1] = s->st_c0;
+    st[2] = s->st_dropped;
+    st[3] = s->st_foreign;
+}
+
+namespace {
+// A record starts at d[p] (dn bytes follow the stream start d): its length fields, names and
+// cigar are consistent, and its bin is the one its position and cigar give (mapped records).
+bool plausible_record(const uint8_t *d, int64_t dn, int64_t p, int32_t n_ref, int64_t *next) {
+    if (p + 36 > dn) return false;
+    const uint8_t *r = d + p;
+    const int64_t bs = rd32(r);
+    if (bs < 32 || bs > (1 << 26) || p + 4 + bs > dn) return false;
+    const int32_t tid = rdi32(r + 4), pos = rdi32(r + 8), ntid = rdi32(r + 24), npos = rdi32(r + 28);
+    if (tid < -1 || tid >= n_ref || ntid < -1 || ntid >= n_ref || pos < -1 || npos < -1) return false;
+    const int l_name = r[12];
+    const int n_cig = rd16(r + 16);
+    const int32_t l_seq = rdi32(r + 20);
+    if (l_name < 1 || l_seq < 0) return false;
+    const int64_t body = 36 + (int64_t)l_name + 4 * (int64_t)n_cig + ((int64_t)l_seq + 1) / 2 + (int64_t)l_seq;
+    if (body > 4 + bs) return false;
+    if (r[36 + l_name - 1] != 0) return false;
+    for (int i = 0; i < l_name - 1; i++)
+        if (r[36 + i] < 33 || r[36 + i] > 126) return false;
+    const uint8_t *cg = r + 36 + l_name;
+    int64_t rl = 0;
+    for (int i = 0; i < n_cig; i++) {
+        const uint32_t op = rd32(cg + 4 * i) & 15;
+        if (op > 8) return false;
+        if (op == 0 || op == 2 || op == 3 || op == 7 || op == 8) rl += rd32(cg + 4 * i) >> 4;
+    }
+    if (tid >= 0 && pos >= 0) {  // SAMv1 reg2bin of [pos, end)
+        const int64_t beg = pos, end = (rl > 0 ? pos + rl : pos + 1) - 1;
+        int bin;
+        if (beg >> 14 == end >> 14) bin = (int)(((1 << 15) - 1) / 7 + (beg >> 14));
+        else if (beg >> 17 == end >> 17) bin = (int)(((1 << 12) - 1) / 7 + (beg >> 17));
+        else if (beg >> 20 == end >> 20) bin = (int)(((1 << 9) - 1) / 7 + (beg >> 20));
+        else if (beg >> 23 == end >> 23) bin = (int)(((1 << 6) - 1) / 7 + (beg >> 23));
+        else if (beg >> 26 == end >> 26) bin = (int)(((1 << 3) - 1) / 7 + (beg >> 26));
+        else bin = 0;
+        if (rd16(r + 14) != bin) return false;
+    }
+    *next = p + 4 + bs;
+    return true;
+}
+}  // namespace
+
+// A rank boundary of a coordinate-sorted BAM after a file offset (see include/bsdc_io.h).
+int32_t bsdc_bam_find_cut(const char *path, int32_t n_threads, int64_t from, int64_t min_span, int64_t slack,
+                          int64_t guard, int64_t max_bytes, int64_t *out) {
+    for (int i = 0; i < 7; i++) out[i] = -1;
+    out[7] = 0;
+    set_threads(n_threads);
+    int32_t n_ref = 0;
+    {
+        bsdc_bam_stream *hs = nullptr;
+        const int32_t rc = bsdc_bam_stream_open(path, 1, 1 << 20, &hs);
+        if (rc != 0) return rc;
+        n_ref = (int32_t)hs->hdr.ref_names.size();
+        bsdc_bam_stream_close(hs);
+    }
+    FILE *f = fopen(path, "rb");
+    if (!f) return fail(BSDC_IO_EIO, std::string("cannot open ") + path);
+    fseeko(f, 0, SEEK_END);
+    const int64_t fsize = (int64_t)ftello(f);
+    // the first BGZF block at or after `from`: a header whose chain of block sizes runs on (4
+    // blocks, or to the end of the file)
+    int64_t blk = -1;
+    {
+        const int64_t win = std::min<int64_t>(fsize - from, (int64_t)4 << 20);
+        Bytes w((size_t)std::max<int64_t>(win, 0));
+        fseeko(f, (off_t)from, SEEK_SET);
+        if (win > 0 && fread(w.data(), 1, w.size(), f) != w.size()) {
+            fclose(f);
+            return fail(BSDC_IO_EIO, "read error");
+        }
+        for (int64_t p = 0; p + 18 <= win && blk < 0; p++) {
+            int64_t q = p;
+            int okn = 0;
+            while (okn < 4 && q < win) {
+                const int64_t bs = bgzf_block_size(w.data() + q, win - q);
+                if (bs < 28) break;
+                q += bs;
+                okn++;
+            }
+            if (okn >= 4 || (okn >= 1 && from + q == fsize)) blk = from + p;
+        }
+    }
+    if (blk < 0) {  // no block starts in the window: the end of the file
+        fclose(f);
+        return 0;
+    }
+    // inflate from there, a few MB at a time, with a map of the blocks' uncompressed offsets
+    Bytes comp, data;
+    std::vector<int64_t> boff, uoff;  // per block inflated: file offset, offset in `data`
+    int64_t fo = blk;
+    bool feof_ = false;
+    auto more = [&]() -> int32_t {
+        if (feof_ || fo - blk >= max_bytes) return 1;
+        const int64_t want = std::min<int64_t>((int64_t)4 << 20, fsize - fo);
+        const size_t have = comp.size();
+        comp.resize(have + (size_t)std::max<int64_t>(want, 0));
+        fseeko(f, (off_t)fo, SEEK_SET);
+        const size_t got = want > 0 ? fread(comp.data() + have, 1, (size_t)want, f) : 0;
+        comp.resize(have + got);
+        const int64_t comp_base = fo - (int64_t)have;  // file offset of comp[0]
+        fo += (int64_t)got;
+        if (fo >= fsize) feof_ = true;
+        int64_t o = 0;  // the whole blocks of comp, listed, then inflated
+        std::vector<int64_t> nb_off, nb_u;
+        int64_t u = (int64_t)data.size();
+        while (o < (int64_t)comp.size()) {
+            const int64_t bs = bgzf_block_size(comp.data() + o, (int64_t)comp.size() - o);
+            if (bs < 0) {
+                if ((int64_t)comp.size() - o >= 18 + 256) return -1;
+                break;
+            }
+            if (o + bs > (int64_t)comp.size()) break;
+            nb_off.push_back(o);
+            nb_u.push_back(u);
+            u += rd32(comp.data() + o + bs - 4);
+            o += bs;
+        }
+        int64_t used = 0;
+        Bytes part;
+        const int32_t rc = inflate_blocks(comp.data(), o, true, part, &used);
+        if (rc != 0) return -1;
+        data.insert(data.end(), part.begin(), part.end());
+        for (size_t i = 0; i < nb_off.size(); i++) {
+            boff.push_back(comp_base + nb_off[i]);
+            uoff.push_back(nb_u[i]);
+        }
+        comp.erase(comp.begin(), comp.begin() + o);
+        return 0;
+    };
+    auto vofs = [&](int64_t p, int64_t *b_, int64_t *o_) {  // a record's block and offset in it
+        const size_t b = (size_t)(std::upper_bound(uoff.begin(), uoff.end(), p) - uoff.begin()) - 1;
+        *b_ = boff[b];
+        *o_ = p - uoff[b];
+    };
+    int32_t mr = more();
+    if (mr < 0) {
+        fclose(f);
+        return fail(BSDC_IO_EFORMAT, "corrupt BGZF data");
+    }
+    // the first record boundary: the smallest offset where 8 records (or all the data left) chain
+    int64_t sync = -1;
+    for (;;) {
+        const int64_t dn = (int64_t)data.size();
+        for (int64_t p0 = 0; p0 + 36 <= std::min<int64_t>(dn, (int64_t)1 << 20) && sync < 0; p0++) {
+            int64_t p = p0, nx = 0;
+            int k = 0;
+            while (k < 8 && plausible_record(data.data(), dn, p, n_ref, &nx)) {
+                p = nx;
+                k++;
+            }
+            if (k >= 8 || (k >= 1 && p == dn && feof_)) sync = p0;
+        }
+        if (sync >= 0) break;
+        mr = more();
+        if (mr != 0) break;
+    }
+    if (sync < 0) {  // no record starts in reach (the end of the file, or a record larger than max_bytes)
+        fclose(f);
+        return 0;
+    }
+    // records from the sync point: their offsets, coordinates and same-contig template keys
+    std::vector<int64_t> roff, rc_;
+    std::vector<int64_t> keys;  // key positions of the sync contig's same-contig templates
+    int64_t p = sync, ctid = -2, x = -1;
+    for (;;) {
+        int64_t nx = 0;
+        const int64_t dn = (int64_t)data.size();
+        if (p + 4 > dn || p + 4 + (int64_t)rd32(data.data() + p) > dn) {
+            mr = more();
+            if (mr < 0) {
+                fclose(f);
+                return fail(BSDC_IO_EFORMAT, "corrupt BGZF data");
+            }
+            if (mr > 0) break;  // the end of the file / of max_bytes: no boundary
+            continue;
+        }
+        if (!plausible_record(data.data(), dn, p, n_ref, &nx)) {
+            fclose(f);
+            return fail(BSDC_IO_EFORMAT, "malformed BAM record");
+        }
+        const uint8_t *r = data.data() + p;
+        std::string_view mc;
+        {
+            const int64_t bs = rd32(r);
+            const uint8_t *end = r + 4 + bs;
+            const int l_name = r[12];
+            const int n_cig = rd16(r + 16);
+            const int32_t l_seq = rdi32(r + 20);
+            const int64_t body = 36 + (int64_t)l_name + 4 * (int64_t)n_cig + ((int64_t)l_seq + 1) / 2 + (int64_t)l_seq;
+            for (const uint8_t *a = r + body; a + 3 <= end;) {
+                const int64_t vs = aux_value_size(a, end);
+                if (vs < 0 || vs > (end - a) - 3) break;
+                if (a[0] == 'M' && a[1] == 'C' && a[2] == 'Z') mc = std::string_view((const char *)a + 3, (size_t)vs - 1);
+                a += 3 + vs;
+            }
+        }
+        const RecKey rk = rec_key(r, mc);
+        if (ctid == -2) ctid = rk.c >= INT64_MAX / 4 ? -1 : (rk.c >> 32);
+        if (ctid < 0 || (rk.c >> 32) != ctid || rk.c >= INT64_MAX / 4) break;  // (a boundary stays inside a contig)
+        roff.push_back(p);
+        rc_.push_back(rk.c & 0xFFFFFFFFll);
+        if (rk.key.first == ((ctid << 32) | ctid)) keys.push_back(rk.key.second);
+        // a boundary x: at least min_span past the first record, no same-contig key within guard of
+        // it, and every record still unread at least slack past x + guard (an unread record's key
+        // is at least its position - slack)
+        const int64_t cur = rk.c & 0xFFFFFFFFll;
+        if (cur > rc_[0] + min_span + 2 * guard + slack && (int64_t)keys.size() > 1) {
+            std::vector<int64_t> ks(keys);
+            std::sort(ks.begin(), ks.end());
+            const int64_t lo = rc_[0] + min_span;
+            for (size_t i = 0; i + 1 < ks.size(); i++) {
+                const int64_t cand = std::max(ks[i] + guard + 1, lo);
+                if (cand + guard >= ks[i + 1]) continue;  // no room between these two keys
+                if (cand + guard + slack >= cur) break;   // too near the unread records
+                x = cand;
+                break;
+            }
+            if (x >= 0) break;
+        }
+        p = nx;
+    }
+    if (x < 0) {
+        fclose(f);
+        return 0;
+    }
+    // the next rank's window starts at the first record at or past x - slack; this one's ends at
+    // the first record at or past x + slack (windows overlap: a template's records near x are
+    // read by both ranks and kept by the owner of its key)
+    const int64_t ws = std::lower_bound(rc_.begin(), rc_.end(), x - slack) - rc_.begin();
+    const int64_t we = std::lower_bound(rc_.begin(), rc_.end(), x + slack) - rc_.begin();
+    if (ws >= (int64_t)roff.size() || we >= (int64_t)roff.size() || rc_[0] > x - slack) {
+        fclose(f);
+        return 0;
+    }
+    vofs(roff[(size_t)ws], &out[0], &out[1]);
+    vofs(roff[(size_t)we], &out[2], &out[3]);
+    out[4] = (ctid << 32) | ctid;
+    out[5] = x;
+    out[6] = (ctid << 32) + x;
+    out[7] = 1;
+    fclose(f);
+    return 0;
+}
+
+// A rank's share of its window (bsdc_bam_stream_set_owner): the records whose TemplateCoordinate
+// key lies in [bounds[rank - 1], bounds[rank]); a dropped record another rank cannot see (its
+// coordinate outside that rank's window) is counted as foreign.
+int32_t bsdc_bam_stream_set_owner(bsdc_bam_stream *s, int32_t rank, const int64_t *bounds, int32_t n_bounds,
+                                  int64_t slack, int32_t stop_on_foreign) {
+    if (!s || rank < 0 || rank > n_bounds || n_bounds < 0) return fail(BSDC_IO_EFORMAT, "bad rank");
+    s->own_rank = rank;
+    s->own_bounds.clear();
+    for (int32_t i = 0; i < n_bounds; i++) s->own_bounds.push_back(TcKey{bounds[3 * i], bounds[3 * i + 1]});
+    s->own_coord.clear();
+    for (int32_t i = 0; i < n_bounds; i++) s->own_coord.push_back(bounds[3 * i + 2]);
+    s->own_slack = slack;
+    s->own_stop = stop_on_foreign != 0;
+    return 0;
+}
+
 // Reads read_size more compressed bytes and inflates the whole blocks onto the end of buf.
 int32_t bsdc_bam_stream_fill(bsdc_bam_stream *s) {
     if (s->eof) return 0;
     const size_t have = s->comp.size();
-    s->comp.resize(have + (size_t)s->read_size);
-    const size_t got = fread(s->comp.data() + have, 1, (size_t)s->read_size, s->f);
+    const int64_t want = s->limit >= 0 ? std::min<int64_t>(s->read_size, std::max<int64_t>(s->limit - s->fpos, 0)) : s->read_size;
+    s->comp.resize(have + (size_t)want);
+    const size_t got = want > 0 ? fread(s->comp.data() + have, 1, (size_t)want, s->f) : 0;
     s->comp.resize(have + got);
-    if (got < (size_t)s->read_size) {
+    s->fpos += (int64_t)got;
+    if (got < (size_t)want || (s->limit >= 0 && s->fpos >= s->limit)) {
         if (ferror(s->f)) return fail(BSDC_IO_EIO, "read error");
         s->eof = true;
     }
+    const size_t before = s->buf.size();
     int64_t used = 0;
     const int32_t rc = inflate_blocks(s->comp.data(), (int64_t)s->comp.size(), s->eof, s->buf, &used);
     if (rc != 0) return rc;
     s->comp.erase(s->comp.begin(), s->comp.begin() + used);
+    if (s->skip_head > 0 && s->buf.size() > before) {  // a range's first block: the bytes before its first record
+        const int64_t k = std::min<int64_t>(s->skip_head, (int64_t)(s->buf.size() - before));
+        s->buf.erase(s->buf.begin() + (int64_t)before, s->buf.begin() + (int64_t)before + k);
+        s->skip_head -= k;
+    }
+    if (s->eof && s->drop_tail > 0) {  // a range's last block: the bytes past its end
+        if ((int64_t)s->buf.size() - s->tail < s->drop_tail) return fail(BSDC_IO_EFORMAT, "bad range end");
+        s->buf.resize(s->buf.size() - (size_t)s->drop_tail);
+        s->drop_tail = 0;
+    }
     return 0;
 }
 
@@ -708,7 +1140,7 @@ namespace {
 // is its MI base (the MI up to the first '/', as the reader interns it); a record without MI is a
 // family of its own.
 int32_t stream_split(bsdc_bam_stream *s) {
-    const uint8_t *d = s->buf.data() + s->tail;
+    uint8_t *d = s->buf.data() + s->tail;
     const int64_t dn = (int64_t)s->buf.size() - s->tail;
     // record boundaries (sequential), then each record's family key and positions (parallel)
     std::vector<int64_t> starts;
@@ -720,7 +1152,7 @@ int32_t stream_split(bsdc_bam_stream *s) {
         starts.push_back(p);
         p += 4 + bs;
     }
-    const int64_t nr = (int64_t)starts.size();
+    int64_t nr = (int64_t)starts.size();
     struct Parsed {
         std::string_view mi;
         uint64_t h;  // hash of mi
@@ -755,64 +1187,59 @@ int32_t stream_split(bsdc_bam_stream *s) {
         }
         const size_t slash = mi.find('/');
         if (slash != std::string_view::npos) mi = mi.substr(0, slash);
-        const int32_t tid = rdi32(r + 4), pos = rdi32(r + 8), ntid = rdi32(r + 24), npos = rdi32(r + 28);
-        const int flag = rd16(r + 18);
-        const int64_t c = coord(tid, pos);
-        // the template's key (batch.template_coordinate_order): the lower end's contig, then the
-        // other end's (BIG for an unpaired record or unmapped mate), then the lower end's unclipped
-        // 5' position -- from the input's cigar and MC, so within kKeyDelta of the key of the
-        // records tools 1 and 2 make (a prepended base, an appended one, the RD trim)
-        const uint8_t *cg = r + 36 + l_name;
-        int64_t lead = 0, trail = 0, reflen = 0;
-        {
-            int first_nc = -1, last_nc = -1;
-            for (int i = 0; i < n_cig; i++) {
-                const uint32_t op = rd32(cg + 4 * i) & 15;
-                if (op == 0 || op == 2 || op == 3 || op == 7 || op == 8) reflen += rd32(cg + 4 * i) >> 4;
-                if (op != 4 && op != 5) {
-                    if (first_nc < 0) first_nc = i;
-                    last_nc = i;
-                }
-            }
-            for (int i = 0; i < n_cig; i++) {
-                const uint32_t op = rd32(cg + 4 * i) & 15;
-                if (op != 4 && op != 5) continue;
-                if (first_nc < 0 || i < first_nc) lead += rd32(cg + 4 * i) >> 4;
-                else if (i > last_nc) trail += rd32(cg + 4 * i) >> 4;
-            }
-        }
-        const int64_t p_own = (flag & 16) ? pos + reflen - 1 + trail : pos - lead;
-        int64_t p_mate = npos;
-        if (!mc.empty() && !(mc.size() == 1 && mc[0] == '*')) {
-            int64_t mlead = 0, mref = 0, num = 0, clip_run = 0;  // clip_run: clips since the last non-clip op
-            bool seen_nc = false;
-            for (char ch : mc) {
-                if (ch >= '0' && ch <= '9') {
-                    num = num * 10 + (ch - '0');
-                    continue;
-                }
-                if (ch == 'M' || ch == 'D' || ch == 'N' || ch == '=' || ch == 'X') mref += num;
-                if (ch == 'S' || ch == 'H') {
-                    if (!seen_nc) mlead += num;
-                    else clip_run += num;
-                } else {
-                    seen_nc = true;
-                    clip_run = 0;
-                }
-                num = 0;
-            }
-            p_mate = (flag & 32) ? npos + mref - 1 + clip_run : npos - mlead;
-        }
-        const bool paired = (flag & 1) && !(flag & 8) && ntid >= 0;
-        const int64_t t1 = tid < 0 ? kBigTid : tid;
-        TcKey key;
-        if (!paired) key = {(t1 << 32) | kBigTid, p_own};
-        else if (tid == ntid) key = {(t1 << 32) | t1, std::min(p_own, p_mate)};
-        else if (tid >= 0 && tid < ntid) key = {(t1 << 32) | (int64_t)ntid, p_own};
-        else key = {((int64_t)ntid << 32) | t1, p_mate};
-        P[(size_t)k] = Parsed{mi, std::hash<std::string_view>{}(mi), c, ntid >= 0 ? std::max(c, coord(ntid, npos)) : c, key};
+        const RecKey rk = rec_key(r, mc);
+        P[(size_t)k] = Parsed{mi, std::hash<std::string_view>{}(mi), rk.c, rk.e, rk.key};
     }
     if (bad) return fail(BSDC_IO_EFORMAT, "malformed BAM record (lengths or aux)");
+    std::vector<uint8_t> drop;
+    if (s->own_rank >= 0 && nr > 0) {  // a rank: the records of its key interval only
+        drop.assign((size_t)nr, 0);
+        const auto &bd = s->own_bounds;
+        for (int64_t k = 0; k < nr; k++) {
+            const Parsed &q = P[(size_t)k];
+            const int owner = (int)(std::upper_bound(bd.begin(), bd.end(), q.key) - bd.begin());
+            if (owner == s->own_rank) continue;
+            drop[(size_t)k] = 1;
+            s->st_dropped++;
+            // the owner reads the coordinates [its lower bound - slack, its upper bound + slack)
+            const int64_t lo = owner == 0 ? INT64_MIN : s->own_coord[(size_t)owner - 1] - s->own_slack;
+            const int64_t hi = owner == (int)bd.size() ? INT64_MAX : s->own_coord[(size_t)owner] + s->own_slack;
+            if (q.c < lo || q.c >= hi) s->st_foreign++;
+        }
+        if (s->own_stop && s->st_foreign > 0)
+            return fail(BSDC_IO_EFORMAT, "foreign record: a record another rank owns but never reads (mate on "
+                                         "another contig or unmapped, or an insert longer than slack)");
+    }
+    int64_t call = INT64_MIN;  // (the cursor passes the dropped records too)
+    for (int64_t k = 0; k < nr; k++) call = std::max(call, P[(size_t)k].c);
+    if (nr > 0 && s->st_n == 0) s->st_c0 = P[0].c;  // (the range statistics: bsdc_bam_stream_range_stats)
+    s->st_n += nr;
+    if (!drop.empty()) {  // the kept records moved together (a record's MI view moves with it)
+        int64_t wp = 0, m = 0;
+        for (int64_t k = 0; k < nr; k++) {
+            if (drop[(size_t)k]) continue;
+            const int64_t st = starts[(size_t)k], len = 4 + (int64_t)rd32(d + st);
+            const int64_t mo = P[(size_t)k].mi.empty() ? 0 : (const uint8_t *)P[(size_t)k].mi.data() - (d + st);
+            if (wp != st) memmove(d + wp, d + st, (size_t)len);
+            P[(size_t)m] = P[(size_t)k];
+            if (!P[(size_t)m].mi.empty()) P[(size_t)m].mi = std::string_view((const char *)d + wp + mo, P[(size_t)m].mi.size());
+            starts[(size_t)m] = wp;
+            wp += len;
+            m++;
+        }
+        if (wp != p) {  // the partial record after them, and the buffer's end
+            memmove(d + wp, d + p, (size_t)(dn - p));
+            s->buf.resize((size_t)(s->tail + wp + (dn - p)));
+        }
+        nr = m;
+        P.resize((size_t)m);
+        starts.resize((size_t)m);
+        p = wp;
+        if (nr == 0) {
+            s->cursor = std::max(s->cursor, call);
+            return 0;
+        }
+    }
     // families (sequential: the MI map), then the records' bytes in one copy
     auto new_fam = [&]() {
         int32_t fam;
@@ -964,7 +1391,7 @@ int32_t stream_split(bsdc_bam_stream *s) {
             const int64_t len = (k + 1 < nr ? starts[(size_t)k + 1] : p) - starts[(size_t)k];
             s->recs[r0 + (size_t)k] = StreamRec{base + starts[(size_t)k], len, famv[(size_t)k]};
         }
-        s->cursor = std::max(s->cursor, P[(size_t)nr - 1].c);
+        s->cursor = std::max(s->cursor, std::max(P[(size_t)nr - 1].c, call));
         s->tail += p;
         return 0;
     }
@@ -989,6 +1416,7 @@ int32_t stream_split(bsdc_bam_stream *s) {
         const int64_t len = (k + 1 < nr ? starts[(size_t)k + 1] : p) - starts[(size_t)k];
         s->recs.push_back(StreamRec{base + starts[(size_t)k], len, fam});
     }
+    s->cursor = std::max(s->cursor, call);
     s->tail += p;
     return 0;
 }
@@ -1595,6 +2023,7 @@ struct bsdc_bam_writer {
     FILE *f = nullptr;
     int32_t level = 6;
     Bytes tail;
+    bool no_eof = false;  // a fragment (bsdc_bam_writer_fragment): no EOF block at the close
 };
 
 extern "C" int32_t bsdc_bam_writer_open(const char *path, const char *header_text, int64_t header_len, int32_t n_ref,
@@ -1693,10 +2122,19 @@ extern "C" int32_t bsdc_bam_writer_close(bsdc_bam_writer *w, int32_t n_threads) 
     if (!w) return 0;
     set_threads(n_threads);
     int32_t rc = deflate_write(w->f, w->tail.data(), (int64_t)w->tail.size(), w->level);
-    if (rc == 0 && fwrite(kBgzfEof, 1, 28, w->f) != 28) rc = fail(BSDC_IO_EIO, "BGZF write failed");
+    if (rc == 0 && !w->no_eof && fwrite(kBgzfEof, 1, 28, w->f) != 28) rc = fail(BSDC_IO_EIO, "BGZF write failed");
     if (fclose(w->f) != 0 && rc == 0) rc = fail(BSDC_IO_EIO, "BGZF close failed");
     delete w;
     return rc;
+}
+
+// A writer of one piece of a BAM whose pieces are concatenated later: header or not (keep_header:
+// the first piece), no EOF block at the close (the assembler appends one).
+extern "C" int32_t bsdc_bam_writer_fragment(bsdc_bam_writer *w, int32_t keep_header) {
+    if (!w) return fail(BSDC_IO_EFORMAT, "no writer");
+    if (!keep_header) w->tail.clear();  // (nothing but the header is encoded at the open)
+    w->no_eof = true;
+    return 0;
 }
 
 namespace {
@@ -2033,6 +2471,7 @@ struct bsdc_fastq_writer {
     FILE *f[2] = {nullptr, nullptr};
     int32_t level = 6;
     Bytes tail[2];
+    bool no_eof = false;  // a fragment: no EOF block at the close
 };
 
 extern "C" int32_t bsdc_fastq_writer_open(const char *path1, const char *path2, int32_t level, bsdc_fastq_writer **out) {
@@ -2098,11 +2537,17 @@ extern "C" int32_t bsdc_fastq_writer_close(bsdc_fastq_writer *w, int32_t n_threa
     int32_t rc = 0;
     for (int d = 0; d < 2; d++) {
         if (rc == 0) rc = deflate_write(w->f[d], w->tail[d].data(), (int64_t)w->tail[d].size(), w->level);
-        if (rc == 0 && fwrite(kBgzfEof, 1, 28, w->f[d]) != 28) rc = fail(BSDC_IO_EIO, "BGZF write failed");
+        if (rc == 0 && !w->no_eof && fwrite(kBgzfEof, 1, 28, w->f[d]) != 28) rc = fail(BSDC_IO_EIO, "BGZF write failed");
         if (fclose(w->f[d]) != 0 && rc == 0) rc = fail(BSDC_IO_EIO, "BGZF close failed");
     }
     delete w;
     return rc;
+}
+
+extern "C" int32_t bsdc_fastq_writer_fragment(bsdc_fastq_writer *w) {
+    if (!w) return fail(BSDC_IO_EFORMAT, "no writer");
+    w->no_eof = true;
+    return 0;
 }
 
 // Packed byte tables (entry r of a table = buf[off[r], off[r + 1])): per entry, the concatenation

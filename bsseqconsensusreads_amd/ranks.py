@@ -1,0 +1,228 @@
+"""Step 5 over N GPUs of one node with no single front end: N rank processes, each decoding,
+computing and encoding its own share of the BAM.
+
+The path is MI families, which are independent.  fleet.step5_stream_multi feeds N
+GPU workers from one coordinator that reads, plans and writes the whole file, so on one node its
+front end, not the GPUs, sets the pace.  Here the file itself is partitioned, by
+template key rather than by record range: in deep data every position is covered by templates,
+so no record boundary has all templates before it closed, but the keys (a template's lower
+unclipped 5' end, TemplateCoordinate order) leave gaps.
+
+1. The parent (which never touches a GPU) picks N - 1 boundaries X_1 < .. < X_N-1 in key gaps:
+   for each nominal split point r * size / N, bam.find_cut (include/bsdc_io.h bsdc_bam_find_cut)
+   syncs to the first BGZF block and record boundary after it and takes the first position x on
+   that contig, at least 2 * slack on, with no same-contig template key within KEY_GUARD positions
+   (a family's keys lie within the tools' jitter of each other, so none straddles x).  It also
+   returns where the records at x - slack and at x + slack start.  That reads a few MB per cut.
+2. Rank r owns the keys [X_r, X_r+1).  It runs the one-GPU streaming step (bam._stream_step:
+   decode, plan, GPU, records, BGZF) over the window from the record at X_r - slack to the one
+   at X_r+1 + slack (windows overlap by 2 * slack) and keeps only the records it owns
+   (bsdc_bam_stream_set_owner): a template's records near a boundary are read by both ranks and
+   kept by one.  It writes a fragment of each output: rank 0 the header and its records, the
+   others their records, none an EOF block.
+3. A rank that drops a record its owner cannot read (a mate on another contig or unmapped, whose
+   key sorts at its contig's end; an insert longer than slack) stops at once, and the parent
+   stops the others and reruns the file as one range, or raises ForeignRecords for its caller
+   to pick another path (cli.py: fleet.step5_stream_multi).  Such records would have to be sent
+   to their owner: not built.  Otherwise the parent concatenates the fragments and one BGZF EOF
+   block: ranks own disjoint key intervals in key order and no family straddles a boundary, so
+   the BAM and the FASTQ pair decompress to the one-process stream's bytes (tests/test_ranks.py);
+   only the BGZF block boundaries at the seams differ.
+
+Every rank's memory is bounded as the one-GPU stream's (about six chunks), and each rank decodes
+about 1/N of the records plus 2 * slack positions.  No collective: the ranks exchange nothing but
+their counts at the end.
+"""
+from __future__ import annotations
+
+import os
+import time
+import traceback
+from typing import List, Optional, Sequence, Tuple
+
+import torch.multiprocessing as tmp
+
+EOF_BLOCK = bytes.fromhex("1f8b08040000000000ff0600424302001b0003000000000000000000")
+
+
+def plan_cuts(path: str, n: int, threads: int = 0, slack: Optional[int] = None) -> List[dict]:
+    """The rank boundaries (bam.find_cut dicts) that split `path` into at most n key intervals of
+    about equal compressed size, in key order; fewer when boundaries coincide (a small file) or
+    none exists after a split point."""
+    from concurrent.futures import ThreadPoolExecutor
+
+    from . import bam
+    sl = bam.DEFAULT_SLACK if slack is None else slack
+    size = os.path.getsize(path)
+    starts = [size * r // n for r in range(1, n)]
+    with ThreadPoolExecutor(max_workers=max(1, min(8, n - 1))) as ex:  # (the C call drops the GIL)
+        found = list(ex.map(lambda s: bam.find_cut(path, s, threads, slack=sl), starts))
+    cuts = {}
+    for c in found:
+        if c is not None:
+            cuts.setdefault(c["key"], c)
+    return [cuts[k] for k in sorted(cuts)]
+
+
+def windows_of(cuts) -> List[Tuple[int, int, int, int]]:
+    """Rank r's record window (start block, offset, end block, offset): from the record at its
+    lower boundary - slack to the one at its upper boundary + slack (-1: the first record / the
+    end of the file)."""
+    lo = [(-1, 0)] + [c["start"] for c in cuts]
+    hi = [c["end"] for c in cuts] + [(-1, 0)]
+    return [(lo[r][0], lo[r][1], hi[r][0], hi[r][1]) for r in range(len(cuts) + 1)]
+
+
+def _rank(r: int, device: int, runner_spec: Optional[str], job: dict, rq):
+    """One rank (a spawned process: the first thing here to touch its GPU)."""
+    try:
+        from . import bam
+        runner = eng = None
+        if runner_spec is None:
+            from .device import Engine
+            eng = Engine(device)
+        else:
+            import importlib
+            mod, cls = runner_spec.split(":")
+            runner = getattr(importlib.import_module(mod), cls)(device)
+        st, rs = {}, {}
+        t0 = time.perf_counter()
+        try:
+            info = bam._stream_step(job["in_bam"], job["fasta"], job["out_bam"], eng, job["prefix"], job["threads"],
+                                    job["level"], job["fastq"], job["tags"], job["chunk_bytes"], job["slack"],
+                                    job["batch_bases"], st, job["gpu_bgzf"] and runner is None, None, rng=job["rng"],
+                                    fragment="first" if r == 0 else "next", runner=runner, range_stats=rs,
+                                    owner=(r, job["cuts"], True) if job["cuts"] else None)
+        finally:
+            if eng is not None:
+                eng.close()
+            if runner is not None and hasattr(runner, "close"):
+                runner.close()
+        info["seconds"] = round(time.perf_counter() - t0, 4)
+        rq.put(("done", r, info, st, rs))
+    except BaseException as e:  # noqa: BLE001 -- reported to the parent, which raises it
+        if isinstance(e, OSError) and "foreign record" in str(e):
+            rq.put(("foreign", r, str(e)))
+        else:
+            rq.put(("error", r, "%s: %s\n%s" % (type(e).__name__, e, traceback.format_exc())))
+
+
+class ForeignRecords(RuntimeError):
+    """A rank met a record whose owner never reads it (step5_ranks on_foreign="raise")."""
+
+
+def _concat(dst: str, parts: Sequence[str]):
+    """The fragments in rank order, then one BGZF EOF block."""
+    import shutil
+    with open(dst, "wb") as out:
+        for p in parts:
+            with open(p, "rb") as f:
+                shutil.copyfileobj(f, out, 1 << 24)
+        out.write(EOF_BLOCK)
+
+
+def step5_ranks(in_bam: str, fasta: str, out_bam: Optional[str], devices: Sequence[int], prefix: Optional[str] = None,
+                threads: int = 0, level: int = 6, fastq: Optional[Tuple[str, str]] = None, tags: bool = True,
+                chunk_bytes: Optional[int] = None, slack: Optional[int] = None, batch_bases: Optional[int] = None,
+                runner: Optional[str] = None, stats: Optional[dict] = None, gpu_bgzf: bool = False,
+                cuts: Optional[list] = None, on_foreign: str = "one") -> dict:
+    """Rules convert_Bstrain .. callduplex (main.snake.py:121-164) on a coordinate-sorted BAM by
+    len(devices) rank processes (see the module docstring); same file contract as bam.step5_stream.
+    runner: "module:Class" of a fleet-style runner (the CPU stand-in of the tests) instead of the
+    GPU; cuts: the rank boundaries to use (tests; default plan_cuts).  on_foreign: what a record
+    no rank can own does -- "one": rerun the file as one range (the default), "raise":
+    ForeignRecords (the caller picks another path: cli.py runs fleet.step5_stream_multi)."""
+    from . import bam
+    chunk_bytes = bam.DEFAULT_CHUNK_BYTES if chunk_bytes is None else chunk_bytes
+    slack = bam.DEFAULT_SLACK if slack is None else slack
+    t0 = time.perf_counter()
+    if cuts is None:
+        cuts = plan_cuts(in_bam, len(devices), threads, slack)
+    t_cut = time.perf_counter() - t0
+    hdr = bam.read_bam_header(in_bam)
+    pre = bam.read_name_prefix(hdr) if prefix is None else prefix
+
+    def run(cuts):
+        ranges = windows_of(cuts)
+        n = len(ranges)
+        tmpdir = os.path.dirname(os.path.abspath(out_bam if out_bam is not None else fastq[0]))
+        tag = "%s.rank%d" % (os.getpid(), id(ranges) & 0xFFFF)
+        frags = [(os.path.join(tmpdir, ".%s.%d.bam" % (tag, r)) if out_bam is not None else None,
+                  (os.path.join(tmpdir, ".%s.%d.r1.fq.gz" % (tag, r)), os.path.join(tmpdir, ".%s.%d.r2.fq.gz" % (tag, r)))
+                  if fastq is not None else None) for r in range(n)]
+        ctx = tmp.get_context("spawn")
+        rq = ctx.Queue()
+        procs = []
+        try:
+            for r in range(n):
+                job = dict(in_bam=in_bam, fasta=fasta, out_bam=frags[r][0], prefix=pre, threads=threads, level=level,
+                           fastq=frags[r][1], tags=tags, chunk_bytes=chunk_bytes, slack=slack, batch_bases=batch_bases,
+                           gpu_bgzf=gpu_bgzf, rng=ranges[r], cuts=cuts)
+                p = ctx.Process(target=_rank, args=(r, int(devices[r % len(devices)]), runner, job, rq), daemon=True)
+                p.start()
+                procs.append(p)
+            res = {}
+            while len(res) < n:
+                try:
+                    m = rq.get(timeout=1.0)
+                except Exception:  # noqa: BLE001 -- queue.Empty: check that the ranks are alive
+                    dead = [i for i, p in enumerate(procs) if not p.is_alive() and i not in res]
+                    if dead:
+                        raise RuntimeError("rank %d exited (code %s)" % (dead[0], procs[dead[0]].exitcode))
+                    continue
+                if m[0] == "error":
+                    raise RuntimeError("rank %d: %s" % (m[1], m[2]))
+                if m[0] == "foreign":
+                    raise ForeignRecords("rank %d: %s" % (m[1], m[2]))
+                res[m[1]] = m[2:]
+            for p in procs:
+                p.join(60)
+            return [res[r] for r in range(n)], frags, ranges
+        except BaseException:
+            for p in procs:  # (stopped before their fragments go: a live rank could still create one)
+                if p.is_alive():
+                    p.terminate()
+            for p in procs:
+                p.join(10)
+                if p.is_alive():
+                    p.kill()
+                    p.join(5)
+            for f in frags:
+                for path in ([f[0]] if f[0] else []) + (list(f[1]) if f[1] else []):
+                    if os.path.exists(path):
+                        os.unlink(path)
+            raise
+
+    t1 = time.perf_counter()
+    foreign = 0
+    try:
+        results, frags, ranges = run(cuts)
+    except ForeignRecords:  # (its ranks stopped at their first such record; no fragments are left)
+        if on_foreign == "raise" or not cuts:
+            raise
+        foreign = 1
+        results, frags, ranges = run([])
+    t2 = time.perf_counter()
+    try:
+        if out_bam is not None:
+            _concat(out_bam, [f[0] for f in frags])
+        if fastq is not None:
+            for d in range(2):
+                _concat(fastq[d], [f[1][d] for f in frags])
+    finally:
+        for f in frags:
+            for path in ([f[0]] if f[0] else []) + (list(f[1]) if f[1] else []):
+                if os.path.exists(path):
+                    os.unlink(path)
+    t3 = time.perf_counter()
+    info = {"ranks": len(ranges), "cuts_fallback": foreign > 0, "records_in": 0, "families": 0, "families_emitted": 0,
+            "records_out": 0}
+    for r, (inf, st, rs) in enumerate(results):
+        for k in ("records_in", "families", "families_emitted", "records_out"):
+            info[k] += int(inf.get(k, 0))
+    if stats is not None:
+        stats.update(cut_s=round(t_cut, 4), ranks_s=round(t2 - t1, 4), assemble_s=round(t3 - t2, 4),
+                     rank_records=[int(x[0].get("records_in", 0)) for x in results],
+                     rank_read=[int(x[2].get("n", 0)) for x in results],
+                     rank_seconds=[x[0].get("seconds") for x in results], ranges=ranges)
+    return info

@@ -26,7 +26,7 @@
 extern "C" {
 #endif
 
-#define BSDC_ABI_VERSION 12
+#define BSDC_ABI_VERSION 13
 #define BSDC_SMALL_BUCKETS 8
 #define BSDC_LARGE_BUCKETS 6
 #define BSDC_LARGE_LDS_MAX 158912 /* LDS arena bytes one large-family workgroup may use */ /* LDS arena size classes of the wavefront-per-family kernel */
@@ -112,6 +112,9 @@ typedef struct {
     int64_t split_partial_off;   /* scratch offset of the parts' sums: [part][8] int32 (set reads, set
                                     lengths), then [part][4][stride] int32x4 sums, [part][4][stride] u8x4
                                     counts, [part][4][stride] int32 one-base sums */
+    int64_t n_small_wide[BSDC_SMALL_BUCKETS]; /* (ABI 13) the LAST n_small_wide[q] entries of small bucket q
+                                    have more than 32 records: they run one per wavefront (k_small), the
+                                    others two per wavefront (k_pair, a half-wave each) */
 } bsdc_family_batch;
 
 /* Outputs (device pointers).  Consensus slot (f, end) holds `stride` bases. */

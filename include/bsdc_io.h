@@ -17,7 +17,7 @@
 extern "C" {
 #endif
 
-#define BSDC_IO_ABI_VERSION 8
+#define BSDC_IO_ABI_VERSION 9
 #define BSDC_IO_EFORMAT (-10) /* not BGZF/BAM, truncated, bad CRC */
 #define BSDC_IO_EIO (-11)     /* open/read/write failed */
 #define BSDC_IO_EINVAL (-22)  /* bad argument */
@@ -110,6 +110,37 @@ int32_t bsdc_bam_parse(bsdc_bam *b, int32_t n_threads);
  * bsdc_bam_stream_next_raw, not both.  *out = NULL at the end. */
 int32_t bsdc_bam_stream_next_runs(bsdc_bam_stream *s, int64_t min_bytes, bsdc_bam **out);
 
+/* Rank-parallel step 5 over one coordinate-sorted BAM (IO ABI 9; bsseqconsensusreads_amd/ranks.py).
+ * Rank r owns the templates whose TemplateCoordinate key lies in [X_r, X_r+1): it decodes the
+ * record window around that interval and keeps the records it owns, so the ranks' outputs, in
+ * rank order, are the one stream's.  A boundary X sits in a gap of the keys (no family straddles
+ * it), so it exists inside a contig even where every position is covered by templates.
+ * bsdc_bam_find_cut: from the first BGZF block at or after file offset `from`, the first record
+ * boundary (8 consecutive records that parse, bins included), then on that record's contig the
+ * first position x >= its coordinate + min_span with no same-contig template key within `guard`
+ * positions of x among the records read, and the records read reaching x + guard + slack (an
+ * unread record's key is at least its position - slack).  out[8] = {block file offset, offset in
+ * the block's uncompressed bytes} of the first record at or past x - slack (where the next rank's
+ * window starts), the same of the first record at or past x + slack (where this rank's window
+ * ends), then X = {contig << 32 | contig, x}, the coordinate contig << 32 | x, and 1 -- or -1s and
+ * 0: no boundary within max_bytes of compressed data on that contig.
+ * bsdc_bam_stream_open_range: a stream of the records from (start_block, start_off) -- start_block
+ * -1: the first record after the header -- up to (end_block, end_off) exclusive -- end_block -1:
+ * the end of the file.  bsdc_bam_stream_set_owner (before the first chunk): keep only the records
+ * whose key k has bounds[rank - 1] <= k < bounds[rank], bounds = n_bounds triples {key first,
+ * key second, coordinate} (find_cut's out[4..6]), and count as foreign the dropped records whose
+ * coordinate lies outside their owner's window [its lower coordinate - slack, its upper + slack)
+ * (a mate on another contig, or unmapped: the owner never reads them; ranks.py then falls back to
+ * one range); stop_on_foreign: the first one fails the stream (BSDC_IO_EFORMAT, "foreign
+ * record ...").  bsdc_bam_stream_range_stats: {records read, first coordinate, dropped, foreign}. */
+int32_t bsdc_bam_find_cut(const char *path, int32_t n_threads, int64_t from, int64_t min_span, int64_t slack,
+                          int64_t guard, int64_t max_bytes, int64_t *out);
+int32_t bsdc_bam_stream_open_range(const char *path, int32_t n_threads, int64_t read_size, int64_t start_block,
+                                   int64_t start_off, int64_t end_block, int64_t end_off, bsdc_bam_stream **out);
+int32_t bsdc_bam_stream_set_owner(bsdc_bam_stream *s, int32_t rank, const int64_t *bounds, int32_t n_bounds,
+                                  int64_t slack, int32_t stop_on_foreign);
+void bsdc_bam_stream_range_stats(const bsdc_bam_stream *s, int64_t *st);
+
 /* Records to write (n_rec entries; every *_off array has n_rec + 1 entries). */
 typedef struct {
     int64_t n_rec;
@@ -154,6 +185,9 @@ int32_t bsdc_bam_writer_take(bsdc_bam_writer *w, int64_t nblk, uint8_t *dst, uin
 int32_t bsdc_bam_writer_put(bsdc_bam_writer *w, int64_t nblk, uint8_t *packed, const int32_t *sizes,
                             const uint32_t *crc, const uint8_t *raw, int32_t n_threads);
 int32_t bsdc_bam_writer_close(bsdc_bam_writer *w, int32_t n_threads);
+/* A writer of one piece of a BAM assembled later (ranks.py): keep_header 0 drops the header
+ * encoded at the open; no EOF block at the close.  Call right after the open. */
+int32_t bsdc_bam_writer_fragment(bsdc_bam_writer *w, int32_t keep_header);
 
 /* Paired FASTQ of records, as picard SamToFastq F=path1 F2=path2 writes them (the step after the
  * duplex call, main.snake.py:167-177; parity unpinned): "@name/1" or "/2", SEQ, "+", QUAL+33,
@@ -177,6 +211,7 @@ int32_t bsdc_fastq_writer_take(bsdc_fastq_writer *w, int32_t which, int64_t nblk
 int32_t bsdc_fastq_writer_put(bsdc_fastq_writer *w, int32_t which, int64_t nblk, uint8_t *packed, const int32_t *sizes,
                               const uint32_t *crc, const uint8_t *raw, int32_t n_threads);
 int32_t bsdc_fastq_writer_close(bsdc_fastq_writer *w, int32_t n_threads);
+int32_t bsdc_fastq_writer_fragment(bsdc_fastq_writer *w); /* no EOF blocks at the close */
 
 /* Packed byte tables (entry r = buf[off[r], off[r + 1])), for the output records: per entry the
  * concatenation of k parts (a table, or a constant when offs[j] is NULL: bufs[j], const_len[j]

@@ -21,18 +21,27 @@ constexpr int kRecMetaBytes = 48;  // k_large's per-record metadata (RecMeta)
 // part's int64 sums (32), ORs (4) and A/C/G/T read counts (8, the tags)
 constexpr int kVoteRegionPerCol = 44;
 
-// Arena of one small family.  Regions live only as long as their phase and share space:
+// k_pair's single-strand rows: 20 columns per lane, 8 lanes per set, so a row is at least the
+// consensus length rounded up to 20 (and to 16, for the 8-column reads of the duplex pass)
+BSDC_HD inline int32_t pair_row(int max_len) { return (int32_t)round16((max_len + 2 + 19) / 20 * 20); }
+
+// Arena of one small family (k_small: one per wavefront; k_pair: two per wavefront, the same
+// layout).  Regions live only as long as their phase and share space:
 //   bimg, qimg  the family image, bases / quals (whole kernel)
 //   lists       reference-window starts (staging) -> read descriptors (vote), 4 B per record
-//   misc        consensus lengths lc[4], converted record -> lane
-//   R           reference windows (staging, convert) | alignment-filter scratch (source reads) |
-//               duplex rows + queued columns (vote)
+//   misc        consensus lengths lc[4] (u32); k_small: converted record -> lane (u8);
+//               k_pair: per-set read counts, offsets, forward counts (u8 x 4 each), then per
+//               converted record tool 1's RD (u8)
+//   R           k_pair's converted-record info (uint4 each), then reference windows (staging,
+//               convert) | alignment-filter scratch (source reads) | duplex rows + queued columns
+//               (k_small's vote) | the four single-strand rows, bases then quals (k_pair's vote)
 struct SmallLayout {
-    uint32_t bimg, qimg, lists, misc, ref, meta, setv, ordv, srcl, simp, outb, outq, squeue, total;
-    int32_t ws, ow;
+    uint32_t bimg, qimg, lists, misc, cinfo, ref, meta, setv, ordv, srcl, simp, grp, outb, outq, squeue, ssrow, total;
+    int32_t ws, ow, rw;
     BSDC_HD SmallLayout(int n, int64_t img, int nconv, int64_t cops, int max_len) {
         ws = 32 * ref_chunks(max_len);
         ow = (int32_t)round16(max_len + 2);
+        rw = pair_row(max_len);
         int64_t o = 0;
         bimg = (uint32_t)o;
         o += img;
@@ -40,21 +49,24 @@ struct SmallLayout {
         o += img;
         lists = (uint32_t)o;
         o += round16(4 * (int64_t)n);
-        misc = (uint32_t)o;  // lc[4] u32, then the lane of each converted record (u8)
-        o += 16 + round16(n);
+        misc = (uint32_t)o;  // lc[4] u32, then 16 B of set counts (k_pair), then a byte per record
+        o += 32 + round16(n);
         const int64_t R = o;
-        ref = (uint32_t)R;
-        const int64_t e_ref = R + (int64_t)nconv * ws;
+        cinfo = (uint32_t)R;
+        ref = (uint32_t)(R + 16 * (int64_t)nconv);
+        const int64_t e_ref = R + (int64_t)nconv * (ws + 16);
         meta = (uint32_t)R;  // SMeta per record
         setv = meta + (uint32_t)round16(16 * (int64_t)n);
         ordv = setv + (uint32_t)round16(n);
         srcl = ordv + (uint32_t)round16(2 * (int64_t)n);
         simp = srcl + (uint32_t)round16(2 * (int64_t)n);
-        const int64_t e_f = (int64_t)simp + (cops > 0 ? round16(4 * (cops + 4 * (int64_t)n)) : 0);
+        grp = (uint32_t)((int64_t)simp + (cops > 0 ? round16(4 * (cops + 4 * (int64_t)n)) : 0));
+        const int64_t e_f = (int64_t)grp + (cops > 0 ? 256 : 0);  // filter_group's 2 x 64 u16
         outb = (uint32_t)R;  // duplex bases, 2 ends
         outq = (uint32_t)(R + 2 * (int64_t)ow);
         squeue = (uint32_t)(R + 4 * (int64_t)ow);  // queued (end, column), u16
-        const int64_t e_v = R + 8 * (int64_t)ow;
+        ssrow = (uint32_t)R;  // k_pair: [4][rw] single-strand bases, then [4][rw] quals
+        const int64_t e_v = R + 8 * (int64_t)rw;  // (rw >= ow)
         int64_t e = e_ref > e_f ? e_ref : e_f;
         total = (uint32_t)(e > e_v ? e : e_v);
     }
@@ -65,7 +77,7 @@ struct SmallLayout {
 // the kernel stages the image and writes the metadata before it knows the family's longest read
 // and cigar size (which place the regions after them).
 struct ArenaLayout {
-    uint32_t meta, clist, lists, ssb, ssq, simp, slots, total;
+    uint32_t meta, clist, lists, ssb, ssq, simp, grp, slots, total;
     int32_t ssw;
     BSDC_HD ArenaLayout(int n, int64_t slot_bytes, int max_len, int64_t complex_ops) {
         ssw = (int32_t)round16(max_len + 2);
@@ -87,6 +99,8 @@ struct ArenaLayout {
         o += 4 * (int64_t)ssw;
         simp = (uint32_t)o;
         if (complex_ops > 0) o += round16(4 * (complex_ops + 4 * (int64_t)n));
+        grp = (uint32_t)o;  // filter_group's 2 x 64 u16, for X and for Y (complex families)
+        if (complex_ops > 0) o += 512;
         total = (uint32_t)o;
     }
 };

@@ -1,5 +1,5 @@
-"""The multi-GPU streaming step on the GPU (bsseqconsensusreads_amd/fleet.py): `cli step5 --gpus 2`
-on a coordinate-sorted BAM (one coordinator reading the file once, two spawned GPU workers, here
+"""The multi-GPU streaming step on the GPU (bsseqconsensusreads_amd/fleet.py): `cli step5 --gpus 2
+--multi fleet` on a coordinate-sorted BAM (one coordinator reading the file once, two spawned GPU workers, here
 both on GPU 0 via --devices 0,0) writes the bytes of `--gpus 1` (the one-GPU stream), and those
 records equal oracle/ on the whole file, record by record.  The whole-file distributed path
 (--stream false: every rank plans, rank 0 gathers and writes) is held to the same bar."""
@@ -50,7 +50,7 @@ def _cli(tmp, inp, fa, tag, *extra):
 def test_cli_fleet_two_gpus_equal_one_and_oracle(cli_input):
     tmp, inp, fa = cli_input
     one = _cli(tmp, inp, fa, "one")
-    two = _cli(tmp, inp, fa, "two", "--gpus", "2", "--devices", "0,0")
+    two = _cli(tmp, inp, fa, "two", "--gpus", "2", "--devices", "0,0", "--multi", "fleet")
     assert one == two
     assert assert_bam_matches_oracle(str(tmp / "two.bam"), inp, fa, "cli --gpus 2") > 0
 
@@ -70,6 +70,6 @@ def test_cli_fleet_gpu_bgzf_equals_one_gpu(cli_input):
     same blocks as the one-GPU stream with --gpu-bgzf true, so the files are byte-identical"""
     tmp, inp, fa = cli_input
     one = _cli(tmp, inp, fa, "one_gz", "--gpu-bgzf", "true")
-    two = _cli(tmp, inp, fa, "two_gz", "--gpus", "2", "--devices", "0,0", "--gpu-bgzf", "true")
+    two = _cli(tmp, inp, fa, "two_gz", "--gpus", "2", "--devices", "0,0", "--gpu-bgzf", "true", "--multi", "fleet")
     assert one == two
     assert assert_bam_matches_oracle(str(tmp / "two_gz.bam"), inp, fa, "cli --gpus 2 --gpu-bgzf") > 0

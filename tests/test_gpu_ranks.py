@@ -1,0 +1,40 @@
+"""Rank-parallel step 5 on the GPU (bsseqconsensusreads_amd/ranks.py): `cli step5 --gpus N` on a
+coordinate-sorted BAM (the default --multi ranks: N spawned rank processes, here all on GPU 0 via
+--devices, each decoding, computing and encoding its own key interval of the file) writes a BAM
+and FASTQ pair that decompress to the bytes of `--gpus 1`, whose records equal oracle/ on the
+whole file (tests/test_gpu_fleet.py).  Only the BGZF blocks at the ranks' seams differ."""
+import gzip
+import json
+
+import pytest
+
+from helpers import assert_bam_matches_oracle
+from test_gpu_fleet import _cli, cli_input  # noqa: F401 -- (the module fixture)
+
+pytestmark = pytest.mark.gpu
+
+
+@pytest.mark.parametrize("n", [2, 3])
+def test_cli_ranks_equal_one_gpu_and_oracle(cli_input, n):  # noqa: F811
+    tmp, inp, fa = cli_input
+    one = [gzip.decompress(b) for b in _cli(tmp, inp, fa, "r_one")]
+    got = _cli(tmp, inp, fa, "r%d" % n, "--gpus", str(n), "--devices", ",".join(["0"] * n))
+    assert [gzip.decompress(b) for b in got] == one
+    assert assert_bam_matches_oracle(str(tmp / ("r%d.bam" % n)), inp, fa, "cli --gpus %d ranks" % n) > 0
+
+
+def test_cli_ranks_report(cli_input):  # noqa: F811
+    """The ranks really split the file (no fallback): the info line names 2 ranks"""
+    import os
+    import subprocess
+    import sys
+    tmp, inp, fa = cli_input
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    env = {k: v for k, v in os.environ.items() if k not in ("WORLD_SIZE", "RANK", "LOCAL_RANK")}
+    env["PYTHONPATH"] = root + os.pathsep + env.get("PYTHONPATH", "")
+    p = subprocess.run([sys.executable, "-m", "bsseqconsensusreads_amd.cli", "step5", "--reference", fa, inp,
+                        str(tmp / "rep.bam"), "--threads", "4", "--gpus", "2", "--devices", "0,0"],
+                       env=env, capture_output=True, text=True, timeout=300)
+    assert p.returncode == 0, p.stderr[-3000:]
+    info = json.loads(p.stderr.strip().splitlines()[-1])
+    assert info["ranks"] == 2 and not info["cuts_fallback"]

@@ -1,0 +1,138 @@
+"""Rank-parallel step 5 (bsseqconsensusreads_amd/ranks.py) on CPU: the parent picks rank
+boundaries in the template keys' gaps (bsdc_bam_find_cut), spawned rank processes each decode the
+record window around their key interval and compute and encode the records they own (the one-GPU
+stream over a window, writing fragments), and the parent concatenates.  The ranks run tests/fleet_standin.py (oracle/ in the
+kernels' output layout) in place of the GPU; tests/test_gpu_ranks.py runs them on the GPU."""
+import gzip
+import os
+
+import numpy as np
+import pytest
+
+from bsseqconsensusreads_amd import bam, ranks
+from helpers import assert_bam_matches_oracle
+from test_fleet import STANDIN, sorted_input, write_fasta  # noqa: F401 -- (the module fixture)
+
+SLACK = 2000
+
+
+def _run(tmp, p, fa, tag, n, slack=SLACK, **kw):
+    out = str(tmp / ("%s.bam" % tag))
+    fq = (str(tmp / ("%s_1.fq.gz" % tag)), str(tmp / ("%s_2.fq.gz" % tag)))
+    st = {}
+    info = ranks.step5_ranks(p, fa, out, [0] * n, threads=2, fastq=fq, runner=STANDIN, chunk_bytes=80_000,
+                             slack=slack, batch_bases=40_000, stats=st, **kw)
+    return info, st, [gzip.decompress(open(x, "rb").read()) for x in (out,) + fq], out
+
+
+@pytest.fixture(scope="module")
+def one_range(sorted_input):  # noqa: F811
+    s, p, fa, tmp = sorted_input
+    return _run(tmp, p, fa, "one", 1)
+
+
+def test_cuts_partition_the_records(sorted_input):  # noqa: F811
+    """find_cut's boundaries are in key order, their windows overlap by about 2 x slack, and the
+    ranks' windows with ownership keep every record exactly once, none foreign"""
+    s, p, fa, tmp = sorted_input
+    cuts = ranks.plan_cuts(p, 4, threads=2, slack=SLACK)
+    assert len(cuts) == 3
+    assert [c["key"] for c in cuts] == sorted(set(c["key"] for c in cuts))
+    for c in cuts:
+        assert c["start"] < c["end"]
+        assert c["coord"] & 0xFFFFFFFF == c["key"][1]
+    kept, read = 0, 0
+    for r, rng in enumerate(ranks.windows_of(cuts)):
+        st = {}
+        for ch in bam.stream_chunks(p, 2, 80_000, SLACK, rng=rng, stats=st, owner=(r, cuts)):
+            ch.discard()
+        assert st["foreign"] == 0
+        kept += st["n"] - st["dropped"]
+        read += st["n"]
+    assert kept == s.raw.n
+    assert s.raw.n < read < 1.3 * s.raw.n
+
+
+def _same_contig_keys(raw):
+    """(contig, key position) of every record whose mate is mapped on its contig: the lower
+    unclipped 5' end of the template (include/bsdc_io.cpp rec_key, restated)."""
+    from test_families import _unclipped
+    out = []
+    for k in range(raw.n):
+        fl = int(raw.flag[k])
+        if not (fl & 1) or (fl & 8) or int(raw.next_tid[k]) != int(raw.tid[k]):
+            continue
+        us, ue = _unclipped(raw.record_cigar(k), int(raw.pos[k]))
+        own = ue if fl & 16 else us
+        if raw.mc_off[k] >= 0:
+            mc = raw.mc_cigar[raw.mc_off[k]:raw.mc_off[k] + raw.mc_n[k]]
+            mus, mue = _unclipped(mc, int(raw.next_pos[k]))
+            mate = mue if fl & 32 else mus
+        else:
+            mate = int(raw.next_pos[k])
+        out.append((int(raw.tid[k]), min(own, mate)))
+    return np.array(out, np.int64).reshape(-1, 2)
+
+
+def test_no_key_near_a_boundary(sorted_input):  # noqa: F811
+    """No template key lies within KEY_GUARD positions of a boundary on its contig (so no family,
+    whose keys lie within the tools' jitter of each other, straddles one)"""
+    s, p, fa, tmp = sorted_input
+    cuts = ranks.plan_cuts(p, 4, threads=2, slack=SLACK)
+    keys = _same_contig_keys(s.raw)
+    assert len(keys) > 0.5 * s.raw.n
+    for c in cuts:
+        tid = c["coord"] >> 32
+        near = (keys[:, 0] == tid) & (np.abs(keys[:, 1] - c["key"][1]) <= bam.KEY_GUARD)
+        assert not near.any()
+
+
+@pytest.mark.parametrize("n", [2, 3])
+def test_ranks_write_the_records_of_one(sorted_input, one_range, n):  # noqa: F811
+    """N ranks: the BAM and FASTQ pair decompress to the bytes of the one-range run, and every rank
+    keeps about 1/N of the records and reads its share plus 2 x slack positions"""
+    s, p, fa, tmp = sorted_input
+    info1, _, ref_bytes, _ = one_range
+    info, st, got, _ = _run(tmp, p, fa, "n%d" % n, n)
+    assert info["ranks"] == n and not info["cuts_fallback"]
+    for a, b in zip(got, ref_bytes):
+        assert a == b
+    assert info["records_in"] == info1["records_in"] == s.raw.n
+    total = s.raw.n
+    assert sum(st["rank_records"]) == total
+    assert max(st["rank_records"]) <= total / n + 0.15 * total, st["rank_records"]
+    assert max(st["rank_read"]) <= total / n + 0.2 * total, st["rank_read"]
+    assert min(st["rank_records"]) > 0
+
+
+def test_ranks_records_equal_whole_file_oracle(sorted_input, one_range):  # noqa: F811
+    s, p, fa, tmp = sorted_input
+    assert_bam_matches_oracle(one_range[3], p, fa, "ranks")
+
+
+def test_foreign_records_fall_back_to_one_range(sorted_input, one_range):  # noqa: F811
+    """A boundary whose owner cannot read some of its records (here: windows with no margin and
+    no key gap, so the mates past the boundary of templates owned before it are read only by the
+    next rank) is caught by the ranks' foreign counts and the file is rerun as one range: the
+    same bytes"""
+    s, p, fa, tmp = sorted_input
+    bad = bam.find_cut(p, os.path.getsize(p) // 2, 2, min_span=0, slack=0, guard=0)
+    assert bad is not None and bad["start"] == bad["end"]
+    info, st, got, _ = _run(tmp, p, fa, "bad", 2, cuts=[bad])
+    assert info["cuts_fallback"] and info["ranks"] == 1
+    for a, b in zip(got, one_range[2]):
+        assert a == b
+    with pytest.raises(ranks.ForeignRecords, match="foreign record"):
+        _run(tmp, p, fa, "bad2", 2, cuts=[bad], on_foreign="raise")
+    assert not [f for f in os.listdir(tmp) if f.startswith(".")], "fragments left behind"
+
+
+def test_rank_failure_reaches_the_caller(sorted_input, tmp_path):  # noqa: F811
+    s, p, fa, _ = sorted_input
+    with pytest.raises(RuntimeError, match="stand-in failure on batch 3"):
+        ranks.step5_ranks(p, fa, str(tmp_path / "x.bam"), [0, 0], threads=2, runner="fleet_standin:FailingRunner",
+                          chunk_bytes=80_000, slack=SLACK, batch_bases=40_000)
+    assert not [f for f in os.listdir(tmp_path) if f.startswith(".")], "fragments left behind"
+
+
+
