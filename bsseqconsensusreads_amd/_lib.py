@@ -8,7 +8,7 @@ HERE = os.path.dirname(os.path.abspath(__file__))
 # BSDC_LIB_PATH: an alternative build of the same library (profiling A/B runs only)
 LIB_PATH = os.environ.get("BSDC_LIB_PATH") or os.path.join(HERE, "libbsdc.so")
 
-BSDC_ABI_VERSION = 13
+BSDC_ABI_VERSION = 14
 SMALL_BUCKETS = 8  # BSDC_SMALL_BUCKETS
 PAIR_MAX_REC = 32  # families of more records run one per wavefront (bsdc_family_batch.n_small_wide)
 LARGE_BUCKETS = 6  # BSDC_LARGE_BUCKETS
@@ -43,7 +43,7 @@ class ConsensusC(C.Structure):
                 ("dump_pos", C.c_void_p), ("dump_len", C.c_void_p), ("dump_tags", C.c_void_p),
                 ("dump_seq", C.c_void_p), ("dump_qual", C.c_void_p), ("scratch", C.c_void_p),
                 ("ss_len", C.c_void_p), ("ss_base", C.c_void_p), ("ss_qual", C.c_void_p), ("ss_depth", C.c_void_p),
-                ("ss_err", C.c_void_p)]
+                ("ss_err", C.c_void_p), ("ss_wide", C.c_void_p), ("ss_wdepth", C.c_void_p), ("ss_werr", C.c_void_p)]
 
 
 EXPORTS = ("bsdc_abi_version", "bsdc_ctx_create", "bsdc_ctx_set_params", "bsdc_ctx_destroy", "bsdc_last_error",

@@ -30,7 +30,7 @@ from . import records as R
 
 IO_LIB_PATH = os.environ.get("BSDC_IO_LIB_PATH") or os.path.join(os.path.dirname(os.path.abspath(__file__)),
                                                                  "libbsdc_io.so")
-BSDC_IO_ABI_VERSION = 9
+BSDC_IO_ABI_VERSION = 10
 _P = C.c_void_p
 
 
@@ -120,8 +120,8 @@ def _load():
     lib.bsdc_fastq_write.restype = C.c_int32
     lib.bsdc_family_image.argtypes = [C.c_int64, _P, _P, _P, _P, _P, C.c_int64, _P, _P, C.c_int32]
     lib.bsdc_family_image.restype = C.c_int32
-    lib.bsdc_consensus_tags.argtypes = [C.c_int64, _P, _P, _P, C.c_int32, C.c_int32, _P, _P, _P, _P, _P, _P,
-                                        C.c_int32]
+    lib.bsdc_consensus_tags.argtypes = [C.c_int64, _P, _P, _P, C.c_int32, C.c_int32, _P, _P, _P, _P, _P, _P, _P,
+                                        _P, _P, C.c_int32]
     lib.bsdc_consensus_tags.restype = C.c_int64
     lib.bsdc_table_concat.argtypes = [C.c_int64, C.c_int32, C.POINTER(_P), C.POINTER(_P), _P, _P, _P, C.c_int32]
     lib.bsdc_table_concat.restype = C.c_int64
@@ -1024,11 +1024,25 @@ def consensus_tags(cons, em: np.ndarray, molecular: bool = False, threads: int =
     stride = int(ss["base"].shape[2])
     c = lambda a, dt: np.ascontiguousarray(a, dt).reshape(-1)
     base, qual = c(ss["base"], np.uint8), c(ss["qual"], np.uint8)
-    depth, err = c(ss["depth"], np.uint16), c(ss["err"], np.uint16)
+    wide, wdepth, werr = ss.get("wide"), ss.get("wdepth"), ss.get("werr")
+    if np.asarray(ss["depth"]).dtype != np.uint8:  # u16 statistics (oracle/): bytes + wide rows
+        d16, e16 = np.asarray(ss["depth"]), np.asarray(ss["err"])
+        big = (d16.reshape(d16.shape[0], -1).max(axis=1, initial=0) > 255) | \
+              (e16.reshape(e16.shape[0], -1).max(axis=1, initial=0) > 255)
+        wide = np.where(big, np.cumsum(big) - 1, -1).astype(np.int32)
+        wdepth, werr = d16[big].astype(np.uint16), e16[big].astype(np.uint16)
+        depth, err = c(np.minimum(d16, 255), np.uint8), c(np.minimum(e16, 255), np.uint8)
+    else:
+        depth, err = c(ss["depth"], np.uint8), c(ss["err"], np.uint8)
+    has_wide = wide is not None and wdepth is not None and wdepth.shape[0] > 0
+    if has_wide:
+        wide = np.ascontiguousarray(wide, np.int32)
+        wdepth, werr = c(wdepth[:, :, :stride], np.uint16), c(werr[:, :, :stride], np.uint16)
     row_a, row_b = np.ascontiguousarray(row_a), np.ascontiguousarray(row_b)
     off = np.zeros(n + 1, np.int64)
     args = (n, _ptr(row_a), _ptr(row_b), _ptr(out_len), 1 if molecular else 0, stride, _ptr(base), _ptr(qual),
-            _ptr(depth), _ptr(err), _ptr(off))
+            _ptr(depth), _ptr(err), _ptr(wide) if has_wide else None, _ptr(wdepth) if has_wide else None,
+            _ptr(werr) if has_wide else None, _ptr(off))
     total = lib.bsdc_consensus_tags(*args, None, int(threads))
     buf = pool.take(max(int(total), 1)) if pool is not None else np.empty(max(int(total), 1), np.uint8)
     lib.bsdc_consensus_tags(*args, _ptr(buf), int(threads))

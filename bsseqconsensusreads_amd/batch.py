@@ -939,3 +939,31 @@ def materialize_py(plan: FamilyPlan, f0: int, f1: int, small_cap: int = SMALL_AR
         small_buckets=buckets, small_arenas=arenas, large_buckets=lbuckets, large_arenas=larenas,
         max_len=max_len, src=order.astype(np.int64), fam_mi=fam_mi.astype(np.int32),
         n_bases=total, n_slots=n_slots, t2_rank=t2_rank, split_ext=split_ext)
+
+
+WIDE_MIN_RECORDS = 256  # a family of this many records may have a depth past a byte (include/bsdc.h ss_wide)
+
+
+def wide_rows(fam_off) -> "tuple[np.ndarray, int]":
+    """Per family its wide row (-1: none) -- the families of WIDE_MIN_RECORDS records or more,
+    numbered in order -- and their count."""
+    n = np.diff(np.asarray(fam_off, np.int64))
+    w = n >= WIDE_MIN_RECORDS
+    rows = np.where(w, np.cumsum(w) - 1, -1).astype(np.int32)
+    return rows, int(w.sum())
+
+
+def ss_stats16(ss: dict):
+    """(depth, err) [F, 4, stride] u16 of a consensus' single-strand reads: the bytes the kernels
+    write, with the exact values of the families that have wide rows (device.fetch's ss_wide)."""
+    d = np.asarray(ss["depth"]).astype(np.uint16)
+    e = np.asarray(ss["err"]).astype(np.uint16)
+    wide = ss.get("wide")
+    if wide is not None:
+        f = np.nonzero(np.asarray(wide) >= 0)[0]
+        if f.size:
+            w = np.asarray(wide)[f]
+            st = d.shape[2]
+            d[f] = ss["wdepth"][w][:, :, :st]
+            e[f] = ss["werr"][w][:, :, :st]
+    return d, e

@@ -2287,10 +2287,14 @@ struct AuxOut {
     }
 };
 
-struct SsView {  // one single-strand consensus read, truncated to `len`
+struct SsView {  // one single-strand consensus read, truncated to `len`: depths / errors as the
+                 // kernels' bytes, or a wide family's exact u16 values (w16 set)
     const uint8_t *b, *q;
-    const uint16_t *d, *e;
+    const uint8_t *d8, *e8;
+    const uint16_t *d16, *e16;
     int32_t len;
+    int64_t d(int32_t i) const { return d16 ? (int64_t)d16[i] : (int64_t)d8[i]; }
+    int64_t e(int32_t i) const { return e16 ? (int64_t)e16[i] : (int64_t)e8[i]; }
 };
 
 // D (max depth), M (min depth), E (errors / depth) of one read; depth(i), err(i) per column
@@ -2309,13 +2313,20 @@ void per_read(AuxOut &o, const char *tD, const char *tM, const char *tE, Dep dep
     o.real(tE, (float)se / (float)sd);
 }
 
-// a B:s array straight from the kernels' uint16 counts (the same 16 bits as the int16 value)
-void shorts16(AuxOut &o, const char *tag, const uint16_t *v, int32_t len) {
+// a B:s array of the kernels' counts: a wide family's u16 values as they are (the same 16 bits as
+// the int16 value), the bytes widened
+void shorts16(AuxOut &o, const char *tag, const uint8_t *v8, const uint16_t *v16, int32_t len) {
     o.head(tag, 'B');
     uint8_t b[5] = {'s'};
     wr32(b + 1, (uint32_t)len);
     o.bytes(b, 5);
-    o.bytes(v, 2 * (int64_t)len);  // (little-endian host)
+    if (v16) {
+        o.bytes(v16, 2 * (int64_t)len);  // (little-endian host)
+        return;
+    }
+    if (o.p)
+        for (int32_t i = 0; i < len; i++) wr16(o.p + o.n + 2 * i, (uint16_t)v8[i]);
+    o.n += 2 * (int64_t)len;
 }
 }  // namespace
 
@@ -2324,7 +2335,8 @@ void shorts16(AuxOut &o, const char *tag, const uint16_t *v, int32_t len) {
 // BSDC_MODE_TAGS.  See include/bsdc_io.h.
 extern "C" int64_t bsdc_consensus_tags(int64_t n, const int64_t *row_a, const int64_t *row_b, const int32_t *out_len,
                                        int32_t kind, int32_t stride, const uint8_t *ss_base, const uint8_t *ss_qual,
-                                       const uint16_t *ss_depth, const uint16_t *ss_err, int64_t *off, uint8_t *buf,
+                                       const uint8_t *ss_depth, const uint8_t *ss_err, const int32_t *ss_wide,
+                                       const uint16_t *ss_wdepth, const uint16_t *ss_werr, int64_t *off, uint8_t *buf,
                                        int32_t n_threads) {
     set_threads(n_threads);
     auto one = [&](int64_t k, uint8_t *p) -> int64_t {
@@ -2332,15 +2344,22 @@ extern "C" int64_t bsdc_consensus_tags(int64_t n, const int64_t *row_a, const in
         const int32_t L = out_len[k];
         auto view = [&](int64_t row) {
             const size_t at = (size_t)row * (size_t)stride;
-            return SsView{ss_base + at, ss_qual + at, ss_depth + at, ss_err + at, L};
+            SsView v{ss_base + at, ss_qual + at, ss_depth + at, ss_err + at, nullptr, nullptr, L};
+            const int32_t w = ss_wide ? ss_wide[row >> 2] : -1;
+            if (w >= 0) {
+                const size_t aw = (4 * (size_t)w + (size_t)(row & 3)) * (size_t)stride;
+                v.d16 = ss_wdepth + aw;
+                v.e16 = ss_werr + aw;
+            }
+            return v;
         };
         const SsView a = view(row_a[k]);
-        auto ad = [&](int32_t i) { return (int64_t)a.d[i]; };
-        auto ae = [&](int32_t i) { return (int64_t)a.e[i]; };
+        auto ad = [&](int32_t i) { return a.d(i); };
+        auto ae = [&](int32_t i) { return a.e(i); };
         if (kind == 1) {  // molecular: cD cM cE, cd ce
             per_read(o, "cD", "cM", "cE", ad, ae, L);
-            shorts16(o, "cd", a.d, L);
-            shorts16(o, "ce", a.e, L);
+            shorts16(o, "cd", a.d8, a.d16, L);
+            shorts16(o, "ce", a.e8, a.e16, L);
             return o.n;
         }
         const bool two = row_b[k] >= 0;
@@ -2348,11 +2367,11 @@ extern "C" int64_t bsdc_consensus_tags(int64_t n, const int64_t *row_a, const in
         if (two) {
             // the duplex call before its N mask; errors counted against it: a strand whose call
             // agrees contributes its errors, one that disagrees all of its reads
-            auto td = [&](int32_t i) { return (int64_t)a.d[i] + b.d[i]; };
+            auto td = [&](int32_t i) { return a.d(i) + b.d(i); };
             auto te = [&](int32_t i) {
                 const uint8_t ab = a.b[i] & 15, bb = b.b[i] & 15;
                 const uint8_t raw = ab == bb ? ab : a.q[i] > b.q[i] ? ab : b.q[i] > a.q[i] ? bb : ab;
-                return (int64_t)(ab == raw ? a.e[i] : a.d[i]) + (bb == raw ? b.e[i] : b.d[i]);
+                return (ab == raw ? a.e(i) : a.d(i)) + (bb == raw ? b.e(i) : b.d(i));
             };
             per_read(o, "cD", "cM", "cE", td, te, L);
         } else {
@@ -2360,17 +2379,17 @@ extern "C" int64_t bsdc_consensus_tags(int64_t n, const int64_t *row_a, const in
         }
         per_read(o, "aD", "aM", "aE", ad, ae, L);
         if (two) {
-            auto bdf = [&](int32_t i) { return (int64_t)b.d[i]; };
-            auto bef = [&](int32_t i) { return (int64_t)b.e[i]; };
+            auto bdf = [&](int32_t i) { return b.d(i); };
+            auto bef = [&](int32_t i) { return b.e(i); };
             per_read(o, "bD", "bM", "bE", bdf, bef, L);
         }
-        shorts16(o, "ad", a.d, L);
-        shorts16(o, "ae", a.e, L);
+        shorts16(o, "ad", a.d8, a.d16, L);
+        shorts16(o, "ae", a.e8, a.e16, L);
         o.text("ac", a.b, L, kNt16, 0);
         o.text("aq", a.q, L, nullptr, 33);
         if (two) {
-            shorts16(o, "bd", b.d, L);
-            shorts16(o, "be", b.e, L);
+            shorts16(o, "bd", b.d8, b.d16, L);
+            shorts16(o, "be", b.e8, b.e16, L);
             o.text("bc", b.b, L, kNt16, 0);
             o.text("bq", b.q, L, nullptr, 33);
         }

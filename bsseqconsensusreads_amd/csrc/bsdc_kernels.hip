@@ -521,6 +521,21 @@ struct KParams {
     int32_t qmin;             // bsdc_params.min_consensus_base_quality: single-strand Q below it -> (N, 2)
 };
 
+// (TAGS) a single-strand column's depth and errors: bytes (saturated) for every family, and the
+// exact u16 values in the family's wide row when it has one (include/bsdc.h ss_wide)
+__device__ __forceinline__ void put_ss_stats(const KParams &P, int64_t fam, int s, int64_t col, uint32_t depth,
+                                             uint32_t err) {
+    const int64_t at = (4 * fam + s) * P.O.stride + col;
+    P.O.ss_depth[at] = (uint8_t)::min(depth, 255u);
+    P.O.ss_err[at] = (uint8_t)::min(err, 255u);
+    const int32_t w = P.O.ss_wide ? P.O.ss_wide[fam] : -1;
+    if (w >= 0) {
+        const int64_t aw = (4 * (int64_t)w + s) * P.O.stride + col;
+        P.O.ss_wdepth[aw] = (uint16_t)::min(depth, 32767u);
+        P.O.ss_werr[aw] = (uint16_t)::min(err, 32767u);
+    }
+}
+
 // the first `bytes` of the Tables image (k_small: all of it; k_large: the kTabBytesL prefix)
 template <int BYTES>
 __device__ __forceinline__ void load_tables(const Tables *tab, uint8_t *dst) {
@@ -1463,22 +1478,20 @@ __device__ __forceinline__ void small_family(const KParams &P, const Tables *T, 
                         if (!hs[s]) continue;
                         const uint32_t wr = (side == 0 ? inA & ~slowA : inB & ~slowB);
                         const uint32_t bb = ss[2 * side], qq = ss[2 * side + 1];
-                        const uint32_t n4 = nf[side] + __builtin_bswap32(nr[side]);
-                        const uint32_t d01 = __builtin_amdgcn_perm(0u, n4, 0x0c010c00u);  // u16 of bytes 0, 1
-                        const uint32_t d23 = __builtin_amdgcn_perm(0u, n4, 0x0c030c02u);  // u16 of bytes 2, 3
+                        const uint32_t n4 = nf[side] + __builtin_bswap32(nr[side]);  // (<= 64 reads: bytes)
                         const int64_t at = (4 * (int64_t)fam + s) * stride + c;
                         if (wr == 0xFFFFFFFFu) {
                             *reinterpret_cast<uint32_t *>(P.O.ss_base + at) = bb;
                             *reinterpret_cast<uint32_t *>(P.O.ss_qual + at) = qq;
-                            *reinterpret_cast<uint2 *>(P.O.ss_depth + at) = make_uint2(d01, d23);
-                            *reinterpret_cast<uint2 *>(P.O.ss_err + at) = make_uint2(0u, 0u);
+                            *reinterpret_cast<uint32_t *>(P.O.ss_depth + at) = n4;
+                            *reinterpret_cast<uint32_t *>(P.O.ss_err + at) = 0u;
                         } else if (wr != 0u) {
 #pragma unroll
                             for (int j = 0; j < 4; j++) {
                                 if (!((wr >> (8 * j)) & 0xFFu)) continue;
                                 P.O.ss_base[at + j] = (uint8_t)(bb >> (8 * j));
                                 P.O.ss_qual[at + j] = (uint8_t)(qq >> (8 * j));
-                                P.O.ss_depth[at + j] = (uint16_t)((n4 >> (8 * j)) & 0xFFu);
+                                P.O.ss_depth[at + j] = (uint8_t)(n4 >> (8 * j));
                                 P.O.ss_err[at + j] = 0;
                             }
                         }
@@ -1550,8 +1563,8 @@ __device__ __forceinline__ void small_family(const KParams &P, const Tables *T, 
                     const int64_t at = (4 * (int64_t)fam + s) * stride + c;
                     P.O.ss_base[at] = (uint8_t)vb;
                     P.O.ss_qual[at] = (uint8_t)vq;
-                    P.O.ss_depth[at] = (uint16_t)::min(depth, 32767u);
-                    P.O.ss_err[at] = (uint16_t)::min(depth - nb, 32767u);
+                    P.O.ss_depth[at] = (uint8_t)depth;  // (<= 64 reads)
+                    P.O.ss_err[at] = (uint8_t)(depth - nb);
                 }
             }
             const uint32_t pb = (uint32_t)__shfl_xor((int)vb, 1, kWave), pq = (uint32_t)__shfl_xor((int)vq, 1, kWave);
@@ -2255,16 +2268,15 @@ __device__ __forceinline__ void pair_families(const KParams &P, const Tables *T,
                 if (wr == 0xFFFFFFFFu) {
                     *reinterpret_cast<uint32_t *>(P.O.ss_base + at) = bS;
                     *reinterpret_cast<uint32_t *>(P.O.ss_qual + at) = qS;
-                    *reinterpret_cast<uint2 *>(P.O.ss_depth + at) =
-                        make_uint2(__builtin_amdgcn_perm(0u, n4, 0x0c010c00u), __builtin_amdgcn_perm(0u, n4, 0x0c030c02u));
-                    *reinterpret_cast<uint2 *>(P.O.ss_err + at) = make_uint2(0u, 0u);
+                    *reinterpret_cast<uint32_t *>(P.O.ss_depth + at) = n4;
+                    *reinterpret_cast<uint32_t *>(P.O.ss_err + at) = 0u;
                 } else if (wr != 0u) {
 #pragma unroll
                     for (int k = 0; k < 4; k++) {
                         if (!((wr >> (8 * k)) & 0xFFu)) continue;
                         P.O.ss_base[at + k] = (uint8_t)(bS >> (8 * k));
                         P.O.ss_qual[at + k] = (uint8_t)(qS >> (8 * k));
-                        P.O.ss_depth[at + k] = (uint16_t)((n4 >> (8 * k)) & 0xFFu);
+                        P.O.ss_depth[at + k] = (uint8_t)(n4 >> (8 * k));
                         P.O.ss_err[at + k] = 0;
                     }
                 }
@@ -2351,8 +2363,8 @@ __device__ __forceinline__ void pair_families(const KParams &P, const Tables *T,
                     const int64_t at = (4 * (int64_t)fh + s) * stride + c;
                     P.O.ss_base[at] = (uint8_t)vb;
                     P.O.ss_qual[at] = (uint8_t)vq;
-                    P.O.ss_depth[at] = (uint16_t)::min(depth, 32767u);
-                    P.O.ss_err[at] = (uint16_t)::min(depth - nb, 32767u);
+                    P.O.ss_depth[at] = (uint8_t)depth;  // (<= 32 reads)
+                    P.O.ss_err[at] = (uint8_t)(depth - nb);
                 }
             }
             wave_sync();
@@ -3117,7 +3129,6 @@ __device__ void process_large(const KParams &P, uint8_t *A, uint8_t *s_tab, cons
     // the read's end cleared, lr[q] added to the base's sum.  Sets of <= 128 reads: 4 columns per
     // thread, int32 sums (exact: |lr| < 2^24).  Deeper sets: 2 columns per thread, int32 sums
     // flushed to int64 every 128 reads.
-    const int32_t stride_o = P.O.stride;
     auto resolve = [&](int s, int col, long long D0, long long D1, long long D2, long long D3, uint32_t n01, uint32_t n23) {
         int best = first_max4(D0, D1, D2, D3);
         if (near_tie(D0, D1, D2, D3, best, cnt[s]))  // rare: fgbio's fp64 read-order pick
@@ -3136,9 +3147,7 @@ __device__ void process_large(const KParams &P, uint8_t *A, uint8_t *s_tab, cons
         if (TAGS) {  // the column's depth / errors (the raw best base's reads) for the consensus tags
             const uint32_t depth = (n01 & 0xFFFFu) + (n01 >> 16) + (n23 & 0xFFFFu) + (n23 >> 16);
             const uint32_t nb = ((best < 2 ? n01 : n23) >> (16 * (best & 1))) & 0xFFFFu;
-            const int64_t at = (4 * (int64_t)fam + s) * stride_o + col;
-            P.O.ss_depth[at] = (uint16_t)::min(depth, 32767u);
-            P.O.ss_err[at] = (uint16_t)::min(depth - nb, 32767u);
+            put_ss_stats(P, fam, s, col, depth, depth - nb);
         }
     };
     // PART: a multi-base column's per-base sums (int32: a part holds < 255 reads a set) and counts
@@ -3296,9 +3305,7 @@ __device__ void process_large(const KParams &P, uint8_t *A, uint8_t *s_tab, cons
                         ssb[ws * ssw + col] = Q < P.qmin ? (uint8_t)kN : (uint8_t)ob;
                         ssq[ws * ssw + col] = Q < P.qmin ? (uint8_t)2 : (uint8_t)Q;
                         if (TAGS) {  // one base seen: depth = its reads, errors 0
-                            const int64_t at = (4 * (int64_t)fam + ws) * stride_o + col;
-                            P.O.ss_depth[at] = (uint16_t)::min(nj, 32767u);
-                            P.O.ss_err[at] = 0;
+                            put_ss_stats(P, fam, ws, col, nj, 0u);
                         }
                     } else {
                         ssb[ws * ssw + col] = (uint8_t)ob;  // (the OR: pass B's no-call test)
@@ -3602,9 +3609,7 @@ __device__ void join_family(const KParams &P, uint4 e0, uint4 e1, uint8_t *rows,
         ssq[s * pitch + c] = nocall ? (uint8_t)2 : (uint8_t)Q;
         if (TAGS) {
             const uint32_t nb = best == 0 ? n0 : best == 1 ? n1 : best == 2 ? n2 : n3;
-            const int64_t at = (4 * (int64_t)e0.x + s) * pitch + c;
-            P.O.ss_depth[at] = (uint16_t)::min(depth, 32767u);
-            P.O.ss_err[at] = (uint16_t)::min(depth - nb, 32767u);
+            put_ss_stats(P, e0.x, s, c, depth, depth - nb);
         }
     }
     __syncthreads();
@@ -3995,6 +4000,10 @@ int32_t bsdc_run(bsdc_ctx *c, const bsdc_family_batch *b, bsdc_consensus *o, int
     if ((mode & BSDC_MODE_TAGS) && (!(mode & BSDC_MODE_VOTE) || !o->ss_len || !o->ss_base || !o->ss_qual ||
                                     !o->ss_depth || !o->ss_err)) {
         c->err = "BSDC_MODE_TAGS needs BSDC_MODE_VOTE and the ss_* outputs";
+        return BSDC_EINVAL;
+    }
+    if ((mode & BSDC_MODE_TAGS) && o->ss_wide && (!o->ss_wdepth || !o->ss_werr)) {
+        c->err = "ss_wide needs ss_wdepth and ss_werr";
         return BSDC_EINVAL;
     }
     if ((mode & BSDC_MODE_DUMP) && (!o->dump_pos || !o->dump_len || !o->dump_tags || !o->dump_seq || !o->dump_qual)) {

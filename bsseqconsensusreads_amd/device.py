@@ -15,7 +15,7 @@ import numpy as np
 import torch
 
 from . import _lib
-from .batch import LARGE_LDS_MAX, FamilyBatch
+from .batch import LARGE_LDS_MAX, FamilyBatch, wide_rows
 from .records import Reference
 
 
@@ -88,8 +88,15 @@ class DeviceBatch:
             self.ss_len = torch.zeros(max(4 * F, 1), dtype=torch.int16, device=device)
             self.ss_base = torch.zeros(nss, dtype=torch.uint8, device=device)
             self.ss_qual = torch.zeros(nss, dtype=torch.uint8, device=device)
-            self.ss_depth = torch.zeros(nss, dtype=torch.int16, device=device)
-            self.ss_err = torch.zeros(nss, dtype=torch.int16, device=device)
+            self.ss_depth = torch.zeros(nss, dtype=torch.uint8, device=device)
+            self.ss_err = torch.zeros(nss, dtype=torch.uint8, device=device)
+            # families whose depths may pass a byte get exact u16 rows too (include/bsdc.h ss_wide)
+            self.ss_wide, self.n_wide = wide_rows(fb.fam_off)
+            if self.n_wide:
+                nw = 4 * self.n_wide * self.stride
+                self.t["ss_wide"] = torch.from_numpy(self.ss_wide.view(np.uint8)).to(device)
+                self.ss_wdepth = torch.zeros(nw, dtype=torch.int16, device=device)
+                self.ss_werr = torch.zeros(nw, dtype=torch.int16, device=device)
         # HBM scratch: arenas of the large buckets beyond the LDS budget, one region per bucket (the
         # bucket dispatches run concurrently on the library's side streams), the split families'
         # fallback arenas and their parts' sums (FamilyBatch.scratch_layout; + slack: dword reads
@@ -125,6 +132,9 @@ class DeviceBatch:
         if tags:
             o.ss_len, o.ss_base, o.ss_qual = _dptr(self.ss_len), _dptr(self.ss_base), _dptr(self.ss_qual)
             o.ss_depth, o.ss_err = _dptr(self.ss_depth), _dptr(self.ss_err)
+            if self.n_wide:
+                o.ss_wide = _dptr(self.t["ss_wide"])
+                o.ss_wdepth, o.ss_werr = _dptr(self.ss_wdepth), _dptr(self.ss_werr)
 
     def release_host(self):
         """Drop the host copy of the batch (the device copy stays resident)."""
@@ -148,6 +158,8 @@ class DeviceBatch:
         if self.tags:
             t.update(ss_len=self.ss_len[:4 * F], ss_base=self.ss_base[:n], ss_qual=self.ss_qual[:n],
                      ss_depth=self.ss_depth[:n], ss_err=self.ss_err[:n])
+            if self.n_wide:
+                t.update(ss_wdepth=self.ss_wdepth, ss_werr=self.ss_werr)
         Rn = self.n_rec
         if self.dump:
             t.update(dump_pos=self.dump_pos[:Rn], dump_len=self.dump_len[:Rn], dump_tags=self.dump_tags[:Rn],
@@ -178,8 +190,14 @@ class DeviceBatch:
             out["ss_len"] = a["ss_len"].view(np.uint16).astype(np.int32).reshape(F, 4)
             out["ss_base"] = a["ss_base"].reshape(F, 4, self.stride)
             out["ss_qual"] = a["ss_qual"].reshape(F, 4, self.stride)
-            out["ss_depth"] = a["ss_depth"].view(np.uint16).reshape(F, 4, self.stride)
-            out["ss_err"] = a["ss_err"].view(np.uint16).reshape(F, 4, self.stride)
+            out["ss_depth"] = a["ss_depth"].reshape(F, 4, self.stride)
+            out["ss_err"] = a["ss_err"].reshape(F, 4, self.stride)
+            out["ss_wide"] = self.ss_wide
+            W = self.n_wide
+            out["ss_wdepth"] = a["ss_wdepth"].view(np.uint16).reshape(W, 4, self.stride) if W else \
+                np.zeros((0, 4, self.stride), np.uint16)
+            out["ss_werr"] = a["ss_werr"].view(np.uint16).reshape(W, 4, self.stride) if W else \
+                np.zeros((0, 4, self.stride), np.uint16)
         if self.dump:
             out["dump_pos"] = a["dump_pos"]
             out["dump_len"] = a["dump_len"].view(np.uint16).astype(np.int32)

@@ -68,7 +68,9 @@ class Consensus:
     fam_src: np.ndarray = None      # input record index of each family record (family order)
     # with tags=True: the four single-strand consensus reads per family and their column
     # statistics (BSDC_MODE_TAGS), sets s = 0 AB-R1, 1 AB-R2, 2 BA-R1, 3 BA-R2: "len" [F, 4],
-    # "base" (nt16) / "qual" / "depth" / "err" [F, 4, stride]
+    # "base" (nt16) / "qual" / "depth" / "err" [F, 4, stride] (depth and err bytes, saturated; the
+    # exact u16 rows of the families of more than 255 records in "wdepth" / "werr" [W, 4, stride],
+    # row "wide"[f], -1 none; batch.ss_stats16 merges them)
     ss: Optional[dict] = None
 
 
@@ -225,7 +227,7 @@ def consensus_from_output(fb: FamilyBatch, out: dict) -> Consensus:
     ss = None
     if "ss_len" in out:
         ss = {"len": out["ss_len"], "base": out["ss_base"], "qual": out["ss_qual"], "depth": out["ss_depth"],
-              "err": out["ss_err"]}
+              "err": out["ss_err"], "wide": out["ss_wide"], "wdepth": out["ss_wdepth"], "werr": out["ss_werr"]}
     return Consensus(fb.fam_mi.copy(), out["status"], out["len"], seq, out["qual"], fb.fam_off.astype(np.int64),
                      fb.src.astype(np.int64), ss)
 
@@ -331,6 +333,17 @@ def concat_consensus(parts: List[Consensus]) -> Consensus:
         ss = {"len": np.concatenate([p.ss["len"] for p in parts])}
         for k in ("base", "qual", "depth", "err"):
             ss[k] = np.concatenate([pad(p.ss[k]) for p in parts])
+        if any(p.ss.get("wide") is not None for p in parts):  # wide rows renumbered part after part
+            wides, w0 = [], 0
+            for p in parts:
+                F = p.ss["len"].shape[0]
+                w = p.ss.get("wide")
+                w = np.full(F, -1, np.int32) if w is None else np.asarray(w, np.int32)
+                wides.append(np.where(w >= 0, w + w0, -1).astype(np.int32))
+                w0 += 0 if p.ss.get("wdepth") is None else int(p.ss["wdepth"].shape[0])
+            ss["wide"] = np.concatenate(wides)
+            for k in ("wdepth", "werr"):
+                ss[k] = np.concatenate([pad(p.ss[k]) for p in parts if p.ss.get(k) is not None])
     return Consensus(np.concatenate([p.fam_mi for p in parts]), np.concatenate([p.status for p in parts]),
                      np.concatenate([p.length for p in parts]), np.concatenate([pad(p.seq) for p in parts]),
                      np.concatenate([pad(p.qual) for p in parts]), fro.astype(np.int64),

@@ -26,7 +26,7 @@
 extern "C" {
 #endif
 
-#define BSDC_ABI_VERSION 13
+#define BSDC_ABI_VERSION 14
 #define BSDC_SMALL_BUCKETS 8
 #define BSDC_LARGE_BUCKETS 6
 #define BSDC_LARGE_LDS_MAX 158912 /* LDS arena bytes one large-family workgroup may use */ /* LDS arena size classes of the wavefront-per-family kernel */
@@ -143,8 +143,17 @@ typedef struct {
     uint16_t *ss_len;            /* [4*n_fam] single-strand consensus length (0 = set empty) */
     uint8_t *ss_base;            /* [4*n_fam*stride] nt16 code per byte (N when Q < 2) */
     uint8_t *ss_qual;            /* [4*n_fam*stride] */
-    uint16_t *ss_depth;          /* [4*n_fam*stride] reads with an A/C/G/T at the column */
-    uint16_t *ss_err;            /* [4*n_fam*stride] depth - reads showing the raw (pre-mask) best base */
+    uint8_t *ss_depth;           /* [4*n_fam*stride] reads with an A/C/G/T at the column (ABI 14: u8,
+                                    saturated at 255; exact in ss_wdepth for a family with a wide row) */
+    uint8_t *ss_err;             /* [4*n_fam*stride] depth - reads showing the raw (pre-mask) best base (u8,
+                                    saturated; exact in ss_werr) */
+    /* (ABI 14) families of more than 255 records, whose depths may not fit a byte: ss_wide[f] = the
+     * family's wide row w (-1: none; the host numbers them), and rows (w, s) of ss_wdepth / ss_werr
+     * hold its exact depths / errors, u16 saturated at 32767 as fgbio's tags.  NULL with no such
+     * family.  (A family routed to the small kernels has at most 64 records.) */
+    const int32_t *ss_wide;      /* [n_fam] */
+    uint16_t *ss_wdepth;         /* [4*n_wide*stride] */
+    uint16_t *ss_werr;           /* [4*n_wide*stride] */
 } bsdc_consensus;
 
 #define BSDC_MODE_CONVERT 1

@@ -17,7 +17,7 @@
 extern "C" {
 #endif
 
-#define BSDC_IO_ABI_VERSION 9
+#define BSDC_IO_ABI_VERSION 10
 #define BSDC_IO_EFORMAT (-10) /* not BGZF/BAM, truncated, bad CRC */
 #define BSDC_IO_EIO (-11)     /* open/read/write failed */
 #define BSDC_IO_EINVAL (-22)  /* bad argument */
@@ -251,14 +251,17 @@ int64_t bsdc_rx_consensus(int64_t n_fam, const int64_t *fam_rec_off, const int64
  * DuplexConsensusCaller.createSamRecord (kind 0) / VanillaUmiConsensusCaller.createSamRecord
  * (kind 1), main.snake.py:54,163; fgbio unvendored: PARITY UNPINNED).  Record k's consensus has
  * out_len[k] columns; row_a[k] / row_b[k] are its single-strand reads' rows of the ss_* arrays
- * libbsdc writes with BSDC_MODE_TAGS (row_b = -1: one strand; kind 1 uses row_a only).
+ * libbsdc writes with BSDC_MODE_TAGS (row_b = -1: one strand; kind 1 uses row_a only): depths and
+ * errors as bytes, a family f with ss_wide[f] = w >= 0 read from rows (w, s) of the exact u16
+ * ss_wdepth / ss_werr instead (include/bsdc.h; ss_wide NULL: none; IO ABI 10).
  *   kind 0: cD cM cE, aD aM aE, [bD bM bE], ad ae ac aq, [bd be bc bq]
  *   kind 1: cD cM cE, cd ce
  * Call with buf = NULL to fill off[0..n] (prefix sums of the sizes), then with buf. Returns the
  * total bytes. */
 int64_t bsdc_consensus_tags(int64_t n, const int64_t *row_a, const int64_t *row_b, const int32_t *out_len,
                             int32_t kind, int32_t stride, const uint8_t *ss_base, const uint8_t *ss_qual,
-                            const uint16_t *ss_depth, const uint16_t *ss_err, int64_t *off, uint8_t *buf,
+                            const uint8_t *ss_depth, const uint8_t *ss_err, const int32_t *ss_wide,
+                            const uint16_t *ss_wdepth, const uint16_t *ss_werr, int64_t *off, uint8_t *buf,
                             int32_t n_threads);
 
 #ifdef __cplusplus

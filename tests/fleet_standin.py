@@ -10,7 +10,7 @@ from __future__ import annotations
 
 import numpy as np
 
-from bsseqconsensusreads_amd.batch import round16
+from bsseqconsensusreads_amd.batch import round16, wide_rows
 from oracle import oracle
 
 
@@ -53,8 +53,13 @@ class OracleRunner:
             live4 = np.arange(stride)[None, None, :] < ss_len[:, :, None]
             out.update(ss_len=ss_len, ss_base=np.where(live4, pad(r.ss["base"]), 0).astype(np.uint8),
                        ss_qual=np.where(live4, pad(r.ss["qual"]), 0).astype(np.uint8),
-                       ss_depth=np.where(live4, pad(r.ss["depth"]), 0).astype(np.uint16),
-                       ss_err=np.where(live4, pad(r.ss["err"]), 0).astype(np.uint16))
+                       ss_depth=np.minimum(np.where(live4, pad(r.ss["depth"]), 0), 255).astype(np.uint8),
+                       ss_err=np.minimum(np.where(live4, pad(r.ss["err"]), 0), 255).astype(np.uint8))
+            wide, W = wide_rows(fb.fam_off)  # (the kernels' wide rows: families of 256+ records)
+            f = np.nonzero(wide >= 0)[0]
+            out.update(ss_wide=wide,
+                       ss_wdepth=np.where(live4[f], pad(r.ss["depth"])[f], 0).astype(np.uint16),
+                       ss_werr=np.where(live4[f], pad(r.ss["err"])[f], 0).astype(np.uint16))
         return out
 
     def run_chunk(self, raw, tags: bool, batch_bases):

@@ -394,6 +394,44 @@ def test_consensus_tags_of_the_oracle_consensus(tmp_path):
     assert one
 
 
+def test_consensus_tags_of_wide_families():
+    """Depths past a byte: the kernels' layout (u8 depth / err, exact u16 rows for the families of
+    256+ records, device.fetch ss_wide) encodes the same tags as the u16 statistics, which equal
+    the Python restatement"""
+    from bsseqconsensusreads_amd import batch
+    s, raw = _messy(120, seed=12)
+    res = oracle.run(raw, s.ref)
+    ss = dict(res.ss)
+    F = ss["len"].shape[0]
+    big = np.zeros(F, bool)
+    big[::3] = True  # every third family: depths in the hundreds / thousands
+    ss["depth"] = np.where(big[:, None, None], ss["depth"].astype(np.int64) * 137, ss["depth"]).astype(np.uint16)
+    ss["err"] = np.where(big[:, None, None], ss["err"].astype(np.int64) * 131, ss["err"]).astype(np.uint16)
+    assert ss["depth"].max() > 255
+    res.ss = ss
+    em = np.nonzero(res.status == 1)[0]
+    t16 = bam.consensus_tags(_cons_of(res), em)
+    wide = np.where(big, np.cumsum(big) - 1, -1).astype(np.int32)
+    ss8 = {"len": ss["len"], "base": ss["base"], "qual": ss["qual"],
+           "depth": np.minimum(ss["depth"], 255).astype(np.uint8), "err": np.minimum(ss["err"], 255).astype(np.uint8),
+           "wide": wide, "wdepth": ss["depth"][big], "werr": ss["err"][big]}
+    d16, e16 = batch.ss_stats16(ss8)
+    assert np.array_equal(d16, ss["depth"]) and np.array_equal(e16, ss["err"])
+    c8 = _cons_of(res)
+    c8.ss = ss8
+    t8 = bam.consensus_tags(c8, em)
+    assert np.array_equal(t8.off, t16.off) and np.array_equal(t8.buf, t16.buf)
+    for i, f in enumerate(em[:40]):
+        for e in range(2):
+            k = 2 * i + e
+            got = [(t, v) for t, _, v in R.parse_aux(bytes(t8.buf[t8.off[k]:t8.off[k + 1]]))]
+            exp = _expected_tags(ss, f, e, int(res.cons_len[f, e]), False)
+            assert [t for t, _ in got] == [t for t, _ in exp]
+            for (t, g), (_, x) in zip(got, exp):
+                if not t.endswith("E"):
+                    assert g == x, (f, e, t)
+
+
 def test_molecular_tags_of_the_oracle_consensus(tmp_path):
     from bsseqconsensusreads_amd import pipeline
     s, raw = _messy(200, seed=9)

@@ -42,11 +42,13 @@ def assert_ss_equal(cons, ref, what=""):
     the single-strand lengths of every family."""
     assert cons.ss is not None, what + ": no tag outputs"
     assert np.array_equal(cons.ss["len"], ref.ss["len"]), what + ": single-strand lengths"
+    d16, e16 = batch.ss_stats16(cons.ss)  # (the kernels' bytes + the wide families' exact rows)
+    got = {"base": cons.ss["base"], "qual": cons.ss["qual"], "depth": d16, "err": e16}
     for f in np.nonzero(ref.status == 1)[0]:
         for s in range(4):
             n = int(ref.ss["len"][f, s])
             for k in ("base", "qual", "depth", "err"):
-                g, r = cons.ss[k][f, s, :n].astype(np.int64), ref.ss[k][f, s, :n].astype(np.int64)
+                g, r = got[k][f, s, :n].astype(np.int64), ref.ss[k][f, s, :n].astype(np.int64)
                 if not np.array_equal(g, r):
                     d = np.nonzero(g != r)[0]
                     raise AssertionError("%s: family %d set %d %s differs at %s: gpu %s oracle %s" % (
