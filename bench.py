@@ -191,6 +191,15 @@ def run(args):
         torch.cuda.synchronize()
         tags_ms = e0.elapsed_time(e1) / ks
     n_disp = sum(r.n_disp for r in res)
+    # the tag leg's extra algorithmic bytes: the single-strand lengths (4 x u16 a family) and, for
+    # the emitted families, each set's read -- base, qual, depth, errors: 4 B a column
+    tag_extra = 0
+    if tags_ms is not None:
+        for r in res:
+            F = r.db.n_fam
+            ssl = r.db.ss_len[:4 * F].cpu().numpy().view(np.uint16).astype(np.int64).reshape(F, 4)
+            st = r.db.status[:F].cpu().numpy()
+            tag_extra += 8 * F + 4 * int(ssl[(st & 1) != 0].sum())
     bytes_small, bytes_all = 0, 0
     for r, (st, ln) in zip(res, outs):
         per = r.in_bytes + family_output_bytes(ln, st)
@@ -278,6 +287,13 @@ def run(args):
                          "issue": issue},
             "cpu_baseline": cpu,
             "tags_ms_per_step": round(tags_ms, 4) if tags_ms is not None else None,
+            "tags_roofline": {"bound": "hbm", "achieved": round((bytes_all + tag_extra) / (tags_ms / 1e3) / 1e9, 1),
+                              "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                              "frac": round((bytes_all + tag_extra) / (tags_ms / 1e3) / 1e9 / HBM_PEAK_GBS, 4),
+                              "algorithmic_bytes_per_step": int(bytes_all + tag_extra),
+                              "tag_bytes_per_step": int(tag_extra),
+                              "vs_headline_ms": round(tags_ms / (elapsed / args.steps * 1e3), 4)}
+            if tags_ms is not None else None,
             "tags_families_per_s": round(molecules / (tags_ms / 1e3), 1) if tags_ms else None,
             "families_emitted": int(emitted_total),
             "setup_s": round(setup_s, 1),

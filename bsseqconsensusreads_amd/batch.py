@@ -168,7 +168,8 @@ class FamilyBatch:
         arenas = int(sf[:, 7].astype(np.int64).sum()) if sf.shape[0] else 0
         poff = int(round16(base + arenas))
         npart = int(self.split_parts.shape[0])
-        psz = int(round16(32 * npart)) + npart * 4 * self.stride * 24 if npart else 0
+        # + the done count per split family (the last part joins; include/bsdc.h split_partial_off)
+        psz = int(round16(32 * npart)) + npart * 4 * self.stride * 24 + 4 * int(sf.shape[0]) if npart else 0
         total = poff + psz
         return (total + 256 if total else 0), base, poff
 

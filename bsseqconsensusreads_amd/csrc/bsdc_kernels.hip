@@ -519,6 +519,7 @@ struct KParams {
     int32_t ref_chunks;       // 16-B chunks per reference window (ref_chunks(max_len))
     uint32_t ref_chunks_inv;  // ceil(2^32 / ref_chunks)
     int32_t qmin;             // bsdc_params.min_consensus_base_quality: single-strand Q below it -> (N, 2)
+    int32_t part_join;        // split families: the last part of a family to finish joins it (no k_join)
 };
 
 // (TAGS) a single-strand column's depth and errors: bytes (saturated) for every family, and the
@@ -2576,9 +2577,10 @@ __device__ void large_emit(const KParams &P, uint32_t fam, const int *cnt, const
 // The parts' sums in scratch (include/bsdc.h split_partial_off): header [part][8] int32 (set
 // reads, set lengths), then int32x4 likelihood sums and u8x4 A/C/G/T read counts per (part, set,
 // column), the column pitch being the output stride.
-template <int G, bool TAGS>
+template <int G, bool TAGS, bool FALLBACK>
 __device__ void join_family(const KParams &P, uint4 e0, uint4 e1, uint8_t *rows, uint8_t *tab, int *red, int *s_cnt,
-                            int *s_lc, int *s_cur, int *s_tie);
+                            int *s_lc, int *s_cur, int *s_tie, int32_t *done);
+constexpr int32_t kJoinTie = 1 << 30;  // a split family's done count once its join met a near tie (part_join)
 
 // more than one of the four per-base read counts (u8 each) is nonzero
 __device__ __forceinline__ bool multi_base(uint32_t m) {
@@ -2600,8 +2602,10 @@ struct PartSums {
         sum = reinterpret_cast<uint4 *>(b + round16(32 * np));
         cnt = reinterpret_cast<uint32_t *>(b + round16(32 * np) + 16 * 4 * np * (int64_t)pitch);
         one = reinterpret_cast<int32_t *>(b + round16(32 * np) + 20 * 4 * np * (int64_t)pitch);
+        done = reinterpret_cast<int32_t *>(b + round16(32 * np) + 24 * 4 * np * (int64_t)pitch);
     }
-    int32_t *one;  // the sum of a column whose reads show one base (its count byte the only one set)
+    int32_t *one;   // the sum of a column whose reads show one base (its count byte the only one set)
+    int32_t *done;  // per split family: its parts finished (part_join; zeroed before the dispatch)
     __device__ __forceinline__ int64_t at(int64_t part, int s, int col) const { return (4 * part + s) * (int64_t)pitch + col; }
 };
 
@@ -3509,14 +3513,33 @@ __global__ __launch_bounds__(G, G == 256 ? 5 : 2) void k_large(KParams P, const 
     __syncthreads();
     uint8_t *A = IN_LDS ? smem : P.O.scratch + scratch_off + (size_t)i * (size_t)arena;
     process_large<G, TAGS, PART>(P, A, reinterpret_cast<uint8_t *>(&s_tab), lr, thr, fams[i], red, s_cnt, s_lc, s_cur);
+    if (PART && IN_LDS && P.part_join) {
+        // the family's parts count themselves done (agent scope: the parts run on every XCD, each
+        // with its own L2); the last one to finish adds them all up in its own arena (join_family)
+        __shared__ int s_last, s_tie;
+        __threadfence();  // this part's sums and header, released before the count
+        __syncthreads();
+        const uint32_t row = fams[i].z >> 8;
+        const uint4 *sf = reinterpret_cast<const uint4 *>(P.B.split_fams);
+        const uint4 e1 = sf[2 * row + 1];
+        if (threadIdx.x == 0) {
+            const int old = __hip_atomic_fetch_add(PartSums(P).done + row, 1, __ATOMIC_ACQ_REL, __HIP_MEMORY_SCOPE_AGENT);
+            s_last = old == (int)e1.y - 1;
+        }
+        __syncthreads();
+        if (!s_last) return;
+        __threadfence();  // the other parts' sums, acquired
+        join_family<G, TAGS, false>(P, sf[2 * row], e1, smem, reinterpret_cast<uint8_t *>(&s_tab), red, s_cnt, s_lc,
+                                    s_cur, &s_tie, PartSums(P).done + row);
+    }
 }
 
 // A split family's join on one workgroup of G threads (k_join): rows = 8 x stride bytes of LDS for
 // its single-strand rows + kJoinParts x 8 bytes for the parts' set lengths, tab = the TablesL copy.
 constexpr int kJoinParts = 256;
-template <int G, bool TAGS>
+template <int G, bool TAGS, bool FALLBACK>
 __device__ void join_family(const KParams &P, uint4 e0, uint4 e1, uint8_t *rows, uint8_t *tab, int *red, int *s_cnt,
-                            int *s_lc, int *s_cur, int *s_tie) {
+                            int *s_lc, int *s_cur, int *s_tie, int32_t *done) {
     const int tt = threadIdx.x;
     const TablesL &T = *reinterpret_cast<const TablesL *>(tab);
     const PartSums ps(P);
@@ -3614,10 +3637,14 @@ __device__ void join_family(const KParams &P, uint4 e0, uint4 e1, uint8_t *rows,
     }
     __syncthreads();
     if (*s_tie) {  // (rare) the whole family in its HBM arena, fgbio's pick on the near ties
-        if (tt == 0) s_cnt[0] = 0;
-        __syncthreads();
-        process_large<G, TAGS, false>(P, P.O.scratch + 16 * (int64_t)e1.z, tab, T.lr, T.thr, e0, red, s_cnt, s_lc,
-                                      s_cur);
+        if (FALLBACK) {
+            if (tt == 0) s_cnt[0] = 0;
+            __syncthreads();
+            process_large<G, TAGS, false>(P, P.O.scratch + 16 * (int64_t)e1.z, tab, T.lr, T.thr, e0, red, s_cnt, s_lc,
+                                          s_cur);
+        } else if (tt == 0) {  // (the part that joins: k_join runs it after the parts)
+            *done = kJoinTie;
+        }
         return;
     }
     large_emit<G, TAGS>(P, e0.x, cnt, lcv, ssb, ssq, pitch, true);
@@ -3639,8 +3666,26 @@ __global__ __launch_bounds__(kJoinThreads, 2) void k_join(KParams P, const uint4
     const int64_t i = blockIdx.x;
     if (i >= nsf) return;
     load_tables<kTabBytesL>(&P.tab->t, reinterpret_cast<uint8_t *>(&s_tab));
-    join_family<G, TAGS>(P, sfams[2 * i], sfams[2 * i + 1], smem, reinterpret_cast<uint8_t *>(&s_tab), red, s_cnt, s_lc,
-                         s_cur, &s_tie);
+    join_family<G, TAGS, true>(P, sfams[2 * i], sfams[2 * i + 1], smem, reinterpret_cast<uint8_t *>(&s_tab), red, s_cnt,
+                               s_lc, s_cur, &s_tie, nullptr);
+}
+
+// part_join: the split families whose join (in their last part) met a near tie run whole in their
+// HBM fallback arenas, fgbio's pick on the ties; every other workgroup exits at once
+template <bool TAGS>
+__global__ __launch_bounds__(kJoinThreads, 2) void k_tie(KParams P, const uint4 *sfams, int64_t nsf) {
+    constexpr int G = kJoinThreads;
+    __shared__ __attribute__((aligned(16))) TablesL s_tab;
+    __shared__ int red[2 * G / kWave];
+    __shared__ int s_cnt[4], s_lc[4], s_cur[8];
+    const int64_t i = blockIdx.x;
+    if (i >= nsf || PartSums(P).done[i] != kJoinTie) return;
+    load_tables<kTabBytesL>(&P.tab->t, reinterpret_cast<uint8_t *>(&s_tab));
+    if (threadIdx.x == 0) s_cnt[0] = 0;
+    __syncthreads();
+    const uint4 e0 = sfams[2 * i], e1 = sfams[2 * i + 1];
+    process_large<G, TAGS, false>(P, P.O.scratch + 16 * (int64_t)e1.z, reinterpret_cast<uint8_t *>(&s_tab), s_tab.lr,
+                                  s_tab.thr, e0, red, s_cnt, s_lc, s_cur);
 }
 
 }  // namespace
@@ -3672,6 +3717,9 @@ struct bsdc_ctx {
     // in the environment at context creation).  k_pair is parity-green but measured slower on C2
     // (3.52 vs 3.09 ms, profiles/r05/README.md): kept as the A/B arm
     bool pair = false;
+    // split families: the last part joins (default) or a k_join dispatch after all the parts
+    // (BSDC_SPLIT_JOIN=kernel: A/B)
+    bool part_join = true;
 };
 
 static float det_expf_host(float x) {
@@ -3902,6 +3950,8 @@ int32_t bsdc_ctx_create(int32_t device, const bsdc_params *params, bsdc_ctx **ou
     {
         const char *sk = getenv("BSDC_SMALL_KERNEL");
         c->pair = sk && std::string(sk) == "pair";
+        const char *sj = getenv("BSDC_SPLIT_JOIN");
+        c->part_join = !(sj && std::string(sj) == "kernel");
     }
     make_tables(params->error_rate_pre_umi, params->error_rate_post_umi, c->host_tab.t);
     make_fp64(params->error_rate_post_umi, c->host_tab.lnc, c->host_tab.lne3);
@@ -4022,6 +4072,7 @@ int32_t bsdc_run(bsdc_ctx *c, const bsdc_family_batch *b, bsdc_consensus *o, int
     P.ref_chunks = ref_chunks(b->max_len);
     P.ref_chunks_inv = (uint32_t)((((uint64_t)1 << 32) + (uint64_t)P.ref_chunks - 1) / (uint64_t)P.ref_chunks);
     P.qmin = c->params.min_consensus_base_quality;
+    P.part_join = 0;
     // the dispatches: on `s`, or (BSDC_FORK) spread over the side streams (created with the
     // context) after an event on `s`
     int nd = 0, used = 0;
@@ -4062,6 +4113,34 @@ int32_t bsdc_run(bsdc_ctx *c, const bsdc_family_batch *b, bsdc_consensus *o, int
         // BSDC_MODE_VOTE (the tools-only launches dump tool-2 records and stop before it) or with a
         // profiling stop knob (the parts return early) that scratch is never written, so no join
         const bool join = (mode & BSDC_MODE_VOTE) && ((mode >> BSDC_MODE_STOP_SHIFT) & 15) == 0;
+        // (default) the last part of each family joins it in its own arena, overlapping the other
+        // parts: no k_join dispatch waiting for every part.  Its done counters are zeroed first
+        if (join && c->part_join && (size_t)a >= jl) {
+            KParams Pj = P;
+            Pj.part_join = 1;
+            const int64_t np = b->n_split_parts;
+            uint8_t *done = o->scratch + b->split_partial_off + round16(32 * np) + 24 * 4 * np * (int64_t)o->stride;
+            hipError_t e = hipMemsetAsync(done, 0, 4 * (size_t)b->n_split_fams, ls);
+            if (e != hipSuccess) {
+                fail(e, "hipMemsetAsync(done)");
+                return;
+            }
+            // then k_tie for the families whose join met a near tie (the rest exit at once)
+            if (tg) {
+                hipLaunchKernelGGL((k_large<true, kLargeThreads, true, true>), dim3((unsigned)b->n_split_parts),
+                                   dim3(kLargeThreads), (size_t)a, ls, Pj, pf, b->n_split_parts, a, (int64_t)0);
+                hipLaunchKernelGGL((k_tie<true>), dim3((unsigned)b->n_split_fams), dim3(kJoinThreads), 0, ls, Pj, sf,
+                                   b->n_split_fams);
+            } else {
+                hipLaunchKernelGGL((k_large<true, kLargeThreads, false, true>), dim3((unsigned)b->n_split_parts),
+                                   dim3(kLargeThreads), (size_t)a, ls, Pj, pf, b->n_split_parts, a, (int64_t)0);
+                hipLaunchKernelGGL((k_tie<false>), dim3((unsigned)b->n_split_fams), dim3(kJoinThreads), 0, ls, Pj, sf,
+                                   b->n_split_fams);
+            }
+            e = hipGetLastError();
+            if (e != hipSuccess) fail(e, "split launch");
+            return;
+        }
         if (tg) {
             hipLaunchKernelGGL((k_large<true, kLargeThreads, true, true>), dim3((unsigned)b->n_split_parts), dim3(kLargeThreads),
                                (size_t)a, ls, P, pf, b->n_split_parts, a, (int64_t)0);

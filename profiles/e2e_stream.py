@@ -8,6 +8,9 @@ synthetic coordinate-sorted C2 BAM + FASTA on local disk, then, each in a fresh 
   fleet   fleet.step5_stream_multi: this child reads and writes, --workers spawned GPU worker
           processes (all on GPU 0 on a one-GPU box; started before the clock) run the batches
   fleet_gpubgzf  the same with the writer's deflate on GPU 0
+  ranks, ranks_gpubgzf  ranks.step5_ranks: --workers rank processes (all on GPU 0 here), each
+          decoding, computing and writing its own key interval with threads / workers host threads
+          (spawn and HIP init inside the clock)
   molecular_stream, molecular_whole  step 1 (bam.molecular_stream / bam.molecular) on the same
           families in GroupReadsByUmi order (a second input, MI runs contiguous; BAM with tags, GPU BGZF)
 The BAMs are compared byte for byte.  Usage:
@@ -76,6 +79,17 @@ def child(args):
         print(json.dumps({"mode": args.mode, "workers": args.workers, "seconds": round(dt, 3),
                           "peak_rss_MiB": round(rss, 1), "worker_peak_rss_MiB": round(crss, 1),
                           "stage_busy_s": stats, **info}))
+        return 0
+    if args.mode in ("ranks", "ranks_gpubgzf"):  # rank processes, each its own part of the file
+        from bsseqconsensusreads_amd import ranks
+        t0 = time.perf_counter()
+        info = ranks.step5_ranks(args.inp, args.fa, args.out, [0] * args.workers,
+                                 threads=max(1, args.threads // args.workers), level=args.level,
+                                 chunk_bytes=args.chunk_mb << 20, stats=stats, gpu_bgzf=args.mode == "ranks_gpubgzf")
+        dt = time.perf_counter() - t0
+        crss = resource.getrusage(resource.RUSAGE_CHILDREN).ru_maxrss / 1024
+        print(json.dumps({"mode": args.mode, "ranks": args.workers, "seconds": round(dt, 3),
+                          "rank_peak_rss_MiB": round(crss, 1), "stage_busy_s": stats, **info}))
         return 0
     from bsseqconsensusreads_amd.device import Engine
     eng = Engine(0)
@@ -158,7 +172,10 @@ def main():
         outs[mode] = out
         print(mode, json.dumps(r), flush=True)
     bams = [open(outs[m], "rb").read() for m in outs if m != "stream_fastq" and "gpubgzf" not in m
-            and not m.startswith("molecular")]
+            and not m.startswith("molecular") and not m.startswith("ranks")]
+    if "ranks" in outs and "stream" in outs:  # other BGZF blocks at the rank seams: the bytes inside
+        import gzip
+        res["ranks_bytes_identical"] = gzip.open(outs["ranks"]).read() == gzip.open(outs["stream"]).read()
     res["outputs_identical"] = all(b == bams[0] for b in bams)
     gz = [open(outs[m], "rb").read() for m in ("stream_gpubgzf", "fleet_gpubgzf") if m in outs]
     if len(gz) == 2:  # the same GPU-deflated blocks from one GPU and from the fleet's writer

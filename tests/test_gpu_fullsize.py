@@ -11,11 +11,12 @@
   cut into bounded batches that run back to back on one GPU and are gathered in order -- what each
   rank of a 2/4/8-GPU run does with its share of the 100M families.
 """
+import os
+from concurrent.futures import ThreadPoolExecutor
+
 import numpy as np
 import pytest
 import torch
-
-import os
 
 from bsseqconsensusreads_amd import batch, pipeline, synth
 from bsseqconsensusreads_amd._lib import MODE_CONVERT, MODE_EXTEND, MODE_VOTE
@@ -27,6 +28,15 @@ pytestmark = pytest.mark.gpu
 THREADS = int(os.environ.get("OMP_NUM_THREADS", "0") or 0) or min(os.cpu_count() or 1, 16)
 FULL = MODE_CONVERT | MODE_EXTEND | MODE_VOTE
 ACGTN = np.array([1, 2, 4, 8, 15])
+
+
+def _oracle_async(raw, ref):
+    """oracle/ on a thread (its C call drops the GIL), started before the GPU run so the two
+    overlap; .result() gives the restatement's result."""
+    ex = ThreadPoolExecutor(1)
+    fut = ex.submit(oracle.run, raw, ref, threads=THREADS)
+    ex.shutdown(wait=False)
+    return fut
 
 
 def _compare_all(cons, ref, what):
@@ -63,11 +73,12 @@ def test_bench_workload_c2_full_size(engine):
     fb = batch.build_family_batch(s.raw, "full", s.ref)
     assert fb.n_fam > 1_000_000 and not fb.split_ext
     engine.load_reference(s.ref)
+    fut = _oracle_async(s.raw, s.ref)
     a, b = _run_resident(engine, fb)
     for k in ("status", "len", "seq", "qual"):
         assert np.array_equal(a[k], b[k]), "second step over the resident batch differs in " + k
     cons = consensus_from_output(fb, a)
-    ref = oracle.run(s.raw, s.ref, threads=THREADS)
+    ref = fut.result()
     live = _compare_all(cons, ref, "C2 1M")
     # (a duplex disagreement keeps |qa - qb|, which can be 1: fgbio duplexConsensus)
     _invariants(cons, live, int((fb.rec_lenflag & 0xFFFF).max()))
@@ -91,12 +102,13 @@ def test_c3_full_size_every_family(engine):
     fb = batch.build_family_batch(s.raw, "full", s.ref)
     assert fb.n_fam >= 200_000 and not fb.split_ext and fb.large_fams.shape[0] > 100_000
     engine.load_reference(s.ref)
+    fut = _oracle_async(s.raw, s.ref)
     a, b = _run_resident(engine, fb)
     for k in ("status", "len", "seq", "qual"):
         assert np.array_equal(a[k], b[k]), "C3: second step differs in " + k
     cons = consensus_from_output(fb, a)
     del fb, a, b
-    ref = oracle.run(s.raw, s.ref, threads=THREADS)
+    ref = fut.result()
     live = _compare_all(cons, ref, "C3 200K")
     _invariants(cons, live, int(s.raw.l_seq.max()) + 1)
 
@@ -108,8 +120,9 @@ def test_c4_bench_batch_every_family(engine):
     straddles families), every family against oracle/."""
     s = synth.generate("C4", 1_000_000, seed=42, device="cuda")
     engine.load_reference(s.ref)
+    fut = _oracle_async(s.raw, s.ref)
     cons, _ = pipeline.run_step5(engine, s.raw)
-    ref = oracle.run(s.raw, s.ref, threads=THREADS)
+    ref = fut.result()
     live = _compare_all(cons, ref, "C4 1M")
     _invariants(cons, live, int(s.raw.l_seq.max()) + 1)
 
@@ -138,9 +151,10 @@ def test_c5_stream_beyond_one_batch(engine):
     ranges = pipeline.plan_ranges(plan, 1 << 30)
     slots = int(plan.fam_bases().sum())
     assert len(ranges) >= 3 and slots > (1 << 32), (len(ranges), slots)
+    fut = _oracle_async(s.raw, s.ref)
     cons, _ = pipeline.run_step5(engine, s.raw, batch_bases=1 << 30)
     assert cons.status.shape[0] == plan.n_fam
-    ref = oracle.run(s.raw, s.ref, threads=THREADS)
+    ref = fut.result()
     live = _compare_all(cons, ref, "C5 stream %d batches" % len(ranges))
     _invariants(cons, live, int(s.raw.l_seq.max()) + 1)
 
@@ -153,6 +167,19 @@ def test_c5_full_share(engine, capsys):
     batch's records.  Progress goes to the terminal per batch (the suite's runner watches for
     silence)."""
     total, per, first, done, emitted = 12_500_000, 1_500_000, None, 0, 0
+    # batch i's oracle runs on a thread while batch i + 1 is generated and run on the GPU
+    pending = None
+
+    def check(p):
+        nonlocal emitted
+        j, sj, cons, fut, upto = p
+        ref = fut.result()
+        live = _compare_all(cons, ref, "C5 share batch %d" % j)
+        _invariants(cons, live, int(sj.raw.l_seq.max()) + 1)
+        emitted += int(ref.status.sum())
+        with capsys.disabled():
+            print("\nC5 share: batch %d, %d / %d families bit-exact" % (j, upto, total), flush=True)
+
     i = 0
     while done < total:
         n = min(per, total - done)
@@ -161,15 +188,12 @@ def test_c5_full_share(engine, capsys):
             engine.load_reference(s.ref)
             first = s
         cons, _ = pipeline.run_step5(engine, s.raw)
-        ref = oracle.run(s.raw, s.ref, threads=THREADS)
-        live = _compare_all(cons, ref, "C5 share batch %d" % i)
-        _invariants(cons, live, int(s.raw.l_seq.max()) + 1)
+        fut = _oracle_async(s.raw, s.ref)
         done += n
-        emitted += int(ref.status.sum())
-        with capsys.disabled():
-            print("\nC5 share: batch %d, %d / %d families bit-exact" % (i, done, total), flush=True)
-        del cons, ref, live
-        if s is not first:
-            del s
+        if pending is not None:
+            check(pending)
+        pending = (i, s, cons, fut, done)
+        del s, cons
         i += 1
+    check(pending)
     assert done == total and emitted > 0.8 * total
