@@ -2582,6 +2582,17 @@ __device__ void join_family(const KParams &P, uint4 e0, uint4 e1, uint8_t *rows,
                             int *s_lc, int *s_cur, int *s_tie, int32_t *done);
 constexpr int32_t kJoinTie = 1 << 30;  // a split family's done count once its join met a near tie (part_join)
 
+// A part's sums and header: with part_join they leave by write-through (sc1) stores, so the
+// family's joiner -- the last part to finish, on any XCD -- needs only its own acquire (no release
+// fence per part); for k_join (a later dispatch) plain stores
+template <class T>
+__device__ __forceinline__ void st_part(const KParams &P, T *p, T v) {
+    if (P.part_join)
+        __hip_atomic_store(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    else
+        *p = v;
+}
+
 // more than one of the four per-base read counts (u8 each) is nonzero
 __device__ __forceinline__ bool multi_base(uint32_t m) {
     return ((m & 0xFFu) != 0) + ((m & 0xFF00u) != 0) + ((m & 0xFF0000u) != 0) + ((m & 0xFF000000u) != 0) > 1;
@@ -3159,11 +3170,20 @@ __device__ void process_large(const KParams &P, uint8_t *A, uint8_t *s_tab, cons
         const PartSums ps(P);
         const int64_t at = ps.at(blockIdx.x, s, col);
         const uint32_t m = (n01 & 0xFFu) | ((n01 >> 8) & 0xFF00u) | ((n23 & 0xFFu) << 16) | ((n23 >> 16) << 24);
-        ps.cnt[at] = m;
-        if (multi_base(m))
-            ps.sum[at] = make_uint4((uint32_t)(int32_t)D0, (uint32_t)(int32_t)D1, (uint32_t)(int32_t)D2, (uint32_t)(int32_t)D3);
-        else  // (one base or none: the others' sums are 0)
-            ps.one[at] = (int32_t)(m & 0xFFu ? D0 : m & 0xFF00u ? D1 : m & 0xFF0000u ? D2 : D3);
+        st_part(P, ps.cnt + at, m);
+        if (multi_base(m)) {
+            uint32_t *d = reinterpret_cast<uint32_t *>(ps.sum + at);
+            if (P.part_join) {
+                st_part(P, d, (uint32_t)(int32_t)D0);
+                st_part(P, d + 1, (uint32_t)(int32_t)D1);
+                st_part(P, d + 2, (uint32_t)(int32_t)D2);
+                st_part(P, d + 3, (uint32_t)(int32_t)D3);
+            } else {
+                ps.sum[at] = make_uint4((uint32_t)(int32_t)D0, (uint32_t)(int32_t)D1, (uint32_t)(int32_t)D2, (uint32_t)(int32_t)D3);
+            }
+        } else {  // (one base or none: the others' sums are 0)
+            st_part(P, ps.one + at, (int32_t)(m & 0xFFu ? D0 : m & 0xFF00u ? D1 : m & 0xFF0000u ? D2 : D3));
+        }
     };
     // Wavefronts by set: wave w works on set w % 4; with 8 waves (512 threads) the two waves of a
     // set split its reads (PARTS = 2).
@@ -3296,8 +3316,8 @@ __device__ void process_large(const KParams &P, uint8_t *A, uint8_t *s_tab, cons
                             const PartSums ps(P);
                             const int bi = ob ? __builtin_ctz(ob) : 0;
                             const int32_t T = ob ? (int32_t)Tj : 0;
-                            ps.one[ps.at(blockIdx.x, ws, col)] = T;
-                            ps.cnt[ps.at(blockIdx.x, ws, col)] = ob ? nj << (8 * bi) : 0u;
+                            st_part(P, ps.one + ps.at(blockIdx.x, ws, col), T);
+                            st_part(P, ps.cnt + ps.at(blockIdx.x, ws, col), ob ? nj << (8 * bi) : 0u);
                             ssq[ws * ssw + col] = 1;
                         } else {
                             ssq[ws * ssw + col] = 0;
@@ -3474,7 +3494,7 @@ __device__ void process_large(const KParams &P, uint8_t *A, uint8_t *s_tab, cons
     __syncthreads();
     if (stop == 7) return;
     if (PART) {  // the part's set sizes and lengths; k_join does the rest
-        if (tt < 8) PartSums(P).head[8 * (int64_t)blockIdx.x + tt] = tt < 4 ? cnt[tt] : lcv[tt - 4];
+        if (tt < 8) st_part(P, PartSums(P).head + 8 * (int64_t)blockIdx.x + tt, tt < 4 ? cnt[tt] : lcv[tt - 4]);
         return;
     }
 
@@ -3514,21 +3534,27 @@ __global__ __launch_bounds__(G, G == 256 ? 5 : 2) void k_large(KParams P, const 
     uint8_t *A = IN_LDS ? smem : P.O.scratch + scratch_off + (size_t)i * (size_t)arena;
     process_large<G, TAGS, PART>(P, A, reinterpret_cast<uint8_t *>(&s_tab), lr, thr, fams[i], red, s_cnt, s_lc, s_cur);
     if (PART && IN_LDS && P.part_join) {
-        // the family's parts count themselves done (agent scope: the parts run on every XCD, each
-        // with its own L2); the last one to finish adds them all up in its own arena (join_family)
+        // the family's parts count themselves done; the last one to finish adds them all up in its
+        // own arena (join_family).  The parts run on every XCD, each with its own L2: the hand-off
+        // is the agent-scope counter form of the guide's protocol with write-through (sc1) sums
+        // and header, which need no release fence -- every wave drains its stores, one lane counts
+        // after a barrier -- and one acquire by the joiner; correct for any placement of the parts
         __shared__ int s_last, s_tie;
-        __threadfence();  // this part's sums and header, released before the count
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // this wave's sums and header
         __syncthreads();
         const uint32_t row = fams[i].z >> 8;
         const uint4 *sf = reinterpret_cast<const uint4 *>(P.B.split_fams);
         const uint4 e1 = sf[2 * row + 1];
         if (threadIdx.x == 0) {
-            const int old = __hip_atomic_fetch_add(PartSums(P).done + row, 1, __ATOMIC_ACQ_REL, __HIP_MEMORY_SCOPE_AGENT);
+            const int old = __hip_atomic_fetch_add(PartSums(P).done + row, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
             s_last = old == (int)e1.y - 1;
+            if (s_last) {
+                __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+                asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+            }
         }
         __syncthreads();
         if (!s_last) return;
-        __threadfence();  // the other parts' sums, acquired
         join_family<G, TAGS, false>(P, sf[2 * row], e1, smem, reinterpret_cast<uint8_t *>(&s_tab), red, s_cnt, s_lc,
                                     s_cur, &s_tie, PartSums(P).done + row);
     }
@@ -3717,9 +3743,9 @@ struct bsdc_ctx {
     // in the environment at context creation).  k_pair is parity-green but measured slower on C2
     // (3.52 vs 3.09 ms, profiles/r05/README.md): kept as the A/B arm
     bool pair = false;
-    // split families: the last part joins (default) or a k_join dispatch after all the parts
-    // (BSDC_SPLIT_JOIN=kernel: A/B)
-    bool part_join = true;
+    // split families: a k_join dispatch after all the parts (default), or the last part of each
+    // family joins it (BSDC_SPLIT_JOIN=part: measured slower, profiles/r05/README.md)
+    bool part_join = false;
 };
 
 static float det_expf_host(float x) {
@@ -3951,7 +3977,7 @@ int32_t bsdc_ctx_create(int32_t device, const bsdc_params *params, bsdc_ctx **ou
         const char *sk = getenv("BSDC_SMALL_KERNEL");
         c->pair = sk && std::string(sk) == "pair";
         const char *sj = getenv("BSDC_SPLIT_JOIN");
-        c->part_join = !(sj && std::string(sj) == "kernel");
+        c->part_join = sj && std::string(sj) == "part";
     }
     make_tables(params->error_rate_pre_umi, params->error_rate_post_umi, c->host_tab.t);
     make_fp64(params->error_rate_post_umi, c->host_tab.lnc, c->host_tab.lne3);
@@ -4113,8 +4139,9 @@ int32_t bsdc_run(bsdc_ctx *c, const bsdc_family_batch *b, bsdc_consensus *o, int
         // BSDC_MODE_VOTE (the tools-only launches dump tool-2 records and stop before it) or with a
         // profiling stop knob (the parts return early) that scratch is never written, so no join
         const bool join = (mode & BSDC_MODE_VOTE) && ((mode >> BSDC_MODE_STOP_SHIFT) & 15) == 0;
-        // (default) the last part of each family joins it in its own arena, overlapping the other
-        // parts: no k_join dispatch waiting for every part.  Its done counters are zeroed first
+        // (BSDC_SPLIT_JOIN=part) the last part of each family joins it in its own arena, overlapping
+        // the other parts: no k_join dispatch waiting for every part.  Its done counters are zeroed
+        // first
         if (join && c->part_join && (size_t)a >= jl) {
             KParams Pj = P;
             Pj.part_join = 1;
@@ -4262,7 +4289,7 @@ int32_t bsdc_run(bsdc_ctx *c, const bsdc_family_batch *b, bsdc_consensus *o, int
             }
             f += nf;
         }
-        launch_split();
+        launch_split();  // (first instead: not faster, profiles/r05/README.md)
     }
     // join: `s` waits for every side stream used -- also after a failed launch, so that no work
     // already queued on a side stream outlives the caller's view of the batch's buffers

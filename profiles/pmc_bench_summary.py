@@ -18,13 +18,13 @@ for f in sorted(glob.glob(d + "/p*/**/*counter_collection.csv", recursive=True))
 # dispatch per bucket) under its name: mean per dispatch x dispatches per launch set = per set
 grouped = collections.defaultdict(dict)
 for k, disp in per.items():
-    m = re.search(r"(k_small|k_large|k_join)", k)
+    m = re.search(r"(k_small|k_pair|k_large|k_join|k_tie)", k)
     name = m.group(1) if m else k[:60]
     if name == "k_small" and "k_small<true" in k:  # the consensus-tag instance (BSDC_MODE_TAGS) on its own
         name = "k_small_tags"
-    elif (name == "k_large" and re.search(r"k_large<(true|false), \d+, true", k)) or "k_join<true" in k:
+    elif (name == "k_large" and re.search(r"k_large<(true|false), \d+, true", k)) or "k_join<true" in k or "k_tie<true" in k:
         name = "k_large_tags"  # (k_large<IN_LDS, G, TAGS, PART>, k_join<TAGS>)
-    elif name == "k_join":  # the split families' join: one more dispatch of the k_large launch set
+    elif name in ("k_join", "k_tie"):  # the split families' join: one more dispatch of the k_large launch set
         name = "k_large"
     grouped[name].update({(k,) + key: v for key, v in disp.items()})
 out = {}

@@ -17,7 +17,7 @@ def main():
         w = csv.writer(g)
         w.writerow(cols)
         for x in r:
-            if re.search(r"k_small|k_large|k_join", x["Kernel_Name"]):
+            if re.search(r"k_small|k_pair|k_large|k_join|k_tie", x["Kernel_Name"]):
                 w.writerow([x[c] for c in cols])
 
 

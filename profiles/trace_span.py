@@ -25,7 +25,7 @@ def main():
     with open(trace, newline="") as f:
         for x in csv.DictReader(f):
             k = x["Kernel_Name"]
-            if kern + "<" in k or (kern == "k_large" and "k_join<" in k):  # (split families' join)
+            if kern + "<" in k or (kern == "k_large" and ("k_join<" in k or "k_tie<" in k)):  # (split families' join)
                 rows.append((int(x["Start_Timestamp"]), int(x["End_Timestamp"])))
     rows.sort()
     take = rows[-nsets * per:]
