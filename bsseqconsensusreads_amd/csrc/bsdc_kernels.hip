@@ -59,7 +59,14 @@ constexpr int kLargeThreads = LARGE_THREADS;
 #define LARGE_THREADS_BIG 512  // k_large workgroup size of the LDS-heavy buckets
 #endif
 constexpr int kLargeThreadsBig = LARGE_THREADS_BIG;  // 512 or 768
-constexpr int kJoinThreads = 512;
+#ifndef JOIN_THREADS
+#define JOIN_THREADS 512
+#endif
+#ifndef JOIN_U
+#define JOIN_U 4
+#endif
+constexpr int kJoinThreads = JOIN_THREADS;  // k_join's workgroup (k_tie's too)
+constexpr int kJoinU = JOIN_U;              // parts' loads in flight per (set, column) in k_join
 constexpr int kLargeBigBucket = 3;
 #ifndef LARGE_VOTE_U
 #define LARGE_VOTE_U 4  // k_large vote pass A: reads in flight per lane
@@ -3605,39 +3612,55 @@ __device__ void join_family(const KParams &P, uint4 e0, uint4 e1, uint8_t *rows,
         }
         long long D0 = 0, D1 = 0, D2 = 0, D3 = 0;
         uint32_t n0 = 0, n1 = 0, n2 = 0, n3 = 0;
-        for (int pb = 0; pb < np; pb += 4) {  // four parts' loads in flight
-            uint4 d[4];
-            uint32_t m[4];
-            int32_t o[4];
+        auto add = [&](uint4 d, uint32_t m) {
+            D0 += (int32_t)d.x;
+            D1 += (int32_t)d.y;
+            D2 += (int32_t)d.z;
+            D3 += (int32_t)d.w;
+            n0 += m & 0xFFu;
+            n1 += (m >> 8) & 0xFFu;
+            n2 += (m >> 16) & 0xFFu;
+            n3 += m >> 24;
+        };
+        // one part's column as four sums: its one base's sum, or the four sums (multi-base)
+        auto four = [&](uint32_t x, int32_t o, uint4 sm) {
+            if (multi_base(x)) return sm;
+            const uint32_t b = x & 0xFFu ? 0u : x & 0xFF00u ? 1u : x & 0xFF0000u ? 2u : 3u;
+            return make_uint4(b == 0 ? (uint32_t)o : 0u, b == 1 ? (uint32_t)o : 0u, b == 2 ? (uint32_t)o : 0u,
+                              b == 3 ? (uint32_t)o : 0u);
+        };
+        if (hl_lds) {
+            // kJoinU parts' loads in flight, every load unconditional (a part past the set's end,
+            // or past the family's parts, reads an in-range slot and is masked after; a one-base
+            // column's sums load reads one shared line): no branch around a load, so no wait per part
+            for (int pb = 0; pb < np; pb += kJoinU) {
+                uint32_t m[kJoinU];
+                int32_t o[kJoinU];
+                bool in[kJoinU];
 #pragma unroll
-            for (int u = 0; u < 4; u++) {
-                const int p = pb + u;
-                // (a part whose set ends before c wrote nothing there)
-                const bool in = p < np && c < (hl_lds ? (int)hl[s * kJoinParts + p] : ps.head[8 * (p0 + p) + 4 + s]);
-                m[u] = in ? ps.cnt[ps.at(p0 + p, s, c)] : 0u;
-                o[u] = in ? ps.one[ps.at(p0 + p, s, c)] : 0;
-            }
-#pragma unroll
-            for (int u = 0; u < 4; u++) {  // (the four sums only where more than one base has reads)
-                const uint32_t x = m[u];
-                if (multi_base(x)) {
-                    d[u] = ps.sum[ps.at(p0 + pb + u, s, c)];
-                } else {
-                    const uint32_t b = x & 0xFFu ? 0u : x & 0xFF00u ? 1u : x & 0xFF0000u ? 2u : 3u;
-                    d[u] = make_uint4(b == 0 ? (uint32_t)o[u] : 0u, b == 1 ? (uint32_t)o[u] : 0u, b == 2 ? (uint32_t)o[u] : 0u,
-                                      b == 3 ? (uint32_t)o[u] : 0u);
+                for (int u = 0; u < kJoinU; u++) {
+                    const int pc = ::min(pb + u, np - 1);
+                    in[u] = pb + u < np && c < (int)hl[s * kJoinParts + pc];
+                    m[u] = ps.cnt[ps.at(p0 + pc, s, c)];
+                    o[u] = ps.one[ps.at(p0 + pc, s, c)];
                 }
-            }
+                uint4 sm[kJoinU];
 #pragma unroll
-            for (int u = 0; u < 4; u++) {
-                D0 += (int32_t)d[u].x;
-                D1 += (int32_t)d[u].y;
-                D2 += (int32_t)d[u].z;
-                D3 += (int32_t)d[u].w;
-                n0 += m[u] & 0xFFu;
-                n1 += (m[u] >> 8) & 0xFFu;
-                n2 += (m[u] >> 16) & 0xFFu;
-                n3 += m[u] >> 24;
+                for (int u = 0; u < kJoinU; u++) {
+                    m[u] = in[u] ? m[u] : 0u;
+                    o[u] = in[u] ? o[u] : 0;
+                    const int pc = ::min(pb + u, np - 1);
+                    sm[u] = ps.sum[multi_base(m[u]) ? ps.at(p0 + pc, s, c) : 0];
+                }
+#pragma unroll
+                for (int u = 0; u < kJoinU; u++) add(four(m[u], o[u], sm[u]), m[u]);
+            }
+        } else {  // (more than kJoinParts parts: their set lengths from HBM, part by part)
+            for (int p = 0; p < np; p++) {
+                if (c >= ps.head[8 * (p0 + p) + 4 + s]) continue;  // (a part whose set ends before c wrote nothing there)
+                const uint32_t x = ps.cnt[ps.at(p0 + p, s, c)];
+                const int32_t o = ps.one[ps.at(p0 + p, s, c)];
+                add(four(x, o, multi_base(x) ? ps.sum[ps.at(p0 + p, s, c)] : make_uint4(0u, 0u, 0u, 0u)), x);
             }
         }
         const int best = first_max4(D0, D1, D2, D3);
@@ -3682,7 +3705,7 @@ __device__ void join_family(const KParams &P, uint4 e0, uint4 e1, uint8_t *rows,
 // column needs fgbio's read-order double sums over all the set's reads, which the parts did not
 // keep: then the family runs whole in its HBM fallback arena (process_large), as the HBM bucket does.
 template <bool TAGS>
-__global__ __launch_bounds__(kJoinThreads, 2) void k_join(KParams P, const uint4 *sfams, int64_t nsf) {
+__global__ __launch_bounds__(kJoinThreads, 1024 / kJoinThreads) void k_join(KParams P, const uint4 *sfams, int64_t nsf) {
     constexpr int G = kJoinThreads;
     extern __shared__ __attribute__((aligned(16))) uint8_t smem[];  // single-strand rows: bases, quals [4][stride]
     __shared__ __attribute__((aligned(16))) TablesL s_tab;
@@ -3699,7 +3722,7 @@ __global__ __launch_bounds__(kJoinThreads, 2) void k_join(KParams P, const uint4
 // part_join: the split families whose join (in their last part) met a near tie run whole in their
 // HBM fallback arenas, fgbio's pick on the ties; every other workgroup exits at once
 template <bool TAGS>
-__global__ __launch_bounds__(kJoinThreads, 2) void k_tie(KParams P, const uint4 *sfams, int64_t nsf) {
+__global__ __launch_bounds__(kJoinThreads, 1024 / kJoinThreads) void k_tie(KParams P, const uint4 *sfams, int64_t nsf) {
     constexpr int G = kJoinThreads;
     __shared__ __attribute__((aligned(16))) TablesL s_tab;
     __shared__ int red[2 * G / kWave];
