@@ -719,6 +719,11 @@ def split_hbm_bucket(fb: FamilyBatch, part_cap: Optional[int] = None, threads: i
     fb.split_part_recs = part_recs
     fb.split_fams = sf.astype(np.uint32)
     fb.split_part_arena = cap
+    # each cut family's image re-laid out part after part (contiguous parts stage in 16-B chunks)
+    assert fb.rec_off.dtype == np.uint32 and fb.rec_off.flags.c_contiguous
+    assert fb.seq.flags.c_contiguous and fb.qual.flags.c_contiguous
+    lib.bsdc_split_move(fb.seq.ctypes.data, fb.qual.ctypes.data, fb.rec_off.ctypes.data, fb.split_fams.ctypes.data,
+                        int(fb.split_fams.shape[0]), parts.ctypes.data, part_recs.ctypes.data, int(threads))
     keep = ~cut
     tail, o = [], 0
     for k in sizes:  # the families left whole stay in their buckets

@@ -759,8 +759,14 @@ namespace {
 struct SplitPart {
     std::vector<int32_t> recs;   // family-local record indices
     std::vector<int32_t> lmate;  // part-local mate index of each (0xFFFF: none)
-    int64_t img = 0;             // slot bytes, rounded to 32
+    int64_t img = 0;             // slot entries
 };
+// A part's records lie back to back in the family image (bsdc_split_fill lays them out), from an
+// entry that need not be 32-aligned: the part stages the 32-entry chunks covering them, up to 31
+// entries before its first and after its last, so its arena has room for 32 entries more
+inline int64_t part_arena(int n, int64_t span, int32_t ml) {
+    return bsdc_layout::ArenaLayout(n, 2 * (((span + 31) & ~int64_t(31)) + 32), ml, 0).total;
+}
 // The parts of one bucket entry: whole templates (an R1 and the R2 its mate link names, or a
 // record no link joins) dealt in record order into parts grown while their arena fits; empty when
 // the family is not cut.  A record's slot holds round4(len + 2) entries (include/bsdc.h).
@@ -785,7 +791,7 @@ std::vector<SplitPart> split_one(const uint32_t *rec, const uint32_t *e, int64_t
     int32_t ml = 0;
     int64_t span = 0;
     auto close = [&]() {
-        cur.img = (span + 31) & ~int64_t(31);
+        cur.img = span;
         parts.push_back(std::move(cur));
         cur = SplitPart();
         ml = 0;
@@ -798,13 +804,12 @@ std::vector<SplitPart> split_one(const uint32_t *rec, const uint32_t *e, int64_t
         const int64_t add = cap4(i) + (m >= 0 ? cap4(m) : 0);
         const int32_t ml2 = std::max(ml, std::max(len_of(i), m >= 0 ? len_of(m) : 0));
         const int64_t n2 = (int64_t)cur.recs.size() + k;
-        const int64_t need = bsdc_layout::ArenaLayout((int)n2, 2 * ((span + add + 31) & ~int64_t(31)), ml2, 0).total;
+        const int64_t need = part_arena((int)n2, span + add, ml2);
         if (!cur.recs.empty() && (need > part_cap || n2 > max_part_rec)) close();
         {
             const int64_t n1 = (int64_t)cur.recs.size() + k;
             const int32_t ml1 = std::max(ml, std::max(len_of(i), m >= 0 ? len_of(m) : 0));
-            if (bsdc_layout::ArenaLayout((int)n1, 2 * ((span + add + 31) & ~int64_t(31)), ml1, 0).total > part_cap ||
-                n1 > max_part_rec) {  // one template alone does not fit
+            if (part_arena((int)n1, span + add, ml1) > part_cap || n1 > max_part_rec) {  // one template alone does not fit
                 parts.clear();
                 return parts;
             }
@@ -820,7 +825,35 @@ std::vector<SplitPart> split_one(const uint32_t *rec, const uint32_t *e, int64_t
         ml = std::max(ml, std::max(len_of(i), m >= 0 ? len_of(m) : 0));
     }
     if (!cur.recs.empty()) close();
-    if (parts.size() < 2) parts.clear();
+    if (parts.size() < 2) {
+        parts.clear();
+        return parts;
+    }
+    // the family's first record leads the family image (the whole-family fallback reads the image
+    // from its slot): its part goes first, its template first in the part, and the record first in
+    // its template (an R2 before its R1: the part-local mate links follow the order)
+    size_t j0 = 0, q0 = 0;
+    for (size_t j = 0; j < parts.size(); j++)
+        for (size_t q = 0; q < parts[j].recs.size(); q++)
+            if (parts[j].recs[q] == 0) j0 = j, q0 = q;
+    if (j0 != 0) std::rotate(parts.begin(), parts.begin() + (int64_t)j0, parts.begin() + (int64_t)j0 + 1);
+    SplitPart &P0 = parts[0];
+    const size_t t0 = (q0 > 0 && P0.lmate[q0 - 1] == (int32_t)q0) ? q0 - 1 : q0;  // its template's first record
+    const size_t tn = P0.lmate[t0] != 0xFFFF ? 2 : 1;
+    std::vector<int32_t> order;
+    order.push_back(0);
+    if (tn == 2) order.push_back(P0.recs[t0] == 0 ? P0.recs[t0 + 1] : P0.recs[t0]);
+    for (size_t q = 0; q < P0.recs.size(); q++)
+        if (q < t0 || q >= t0 + tn) order.push_back(P0.recs[q]);
+    std::vector<int32_t> pos((size_t)n, -1);
+    for (size_t q = 0; q < order.size(); q++) pos[(size_t)order[q]] = (int32_t)q;
+    std::vector<int32_t> lm(order.size(), 0xFFFF);
+    for (size_t q = 0; q < order.size(); q++) {
+        const int32_t m = mate_of[(size_t)order[q]];
+        if (m >= 0) lm[q] = pos[(size_t)m];
+    }
+    P0.recs = std::move(order);
+    P0.lmate = std::move(lm);
     return parts;
 }
 }  // namespace
@@ -855,21 +888,61 @@ void bsdc_split_fill(const uint32_t *rec, const uint32_t *ents, int64_t n_ent, i
         const auto pr = split_one(rec, en, part_cap, max_part_rec);
         const int64_t r0 = en[1];
         int64_t pk = first_rec[e];
+        // the family image re-laid out part after part (bsdc_split_move moves the bytes): a part's
+        // records back to back from `at`, staged as the 32-entry chunks from `at` rounded down
+        uint32_t at = rec[4 * r0];  // (the family's first slot: the image base)
         for (size_t j = 0; j < pr.size(); j++) {
             uint32_t *o = parts + 4 * (first_part[e] + (int64_t)j);
+            const uint32_t a0 = at & ~31u;
             o[0] = en[0];
             o[1] = (uint32_t)pk;
             o[2] = (uint32_t)pr[j].recs.size();
-            o[3] = (uint32_t)pr[j].img;
-            uint32_t dst = 0;
+            o[3] = ((at - a0) + (uint32_t)pr[j].img + 31u) & ~31u;  // staged entries
             for (size_t q = 0; q < pr[j].recs.size(); q++, pk++) {
                 const int64_t gi = r0 + pr[j].recs[q];
                 uint32_t *w = part_recs + 4 * pk;
                 w[0] = (uint32_t)gi;
-                w[1] = dst;
+                w[1] = at - a0;  // its slot in the part's staged image
                 w[2] = (uint32_t)pr[j].lmate[q] | (rec[4 * gi + 2] & 0xFFFFu) << 16;  // | its length
-                w[3] = rec[4 * gi];  // its slot in the batch image (the staging copies it from there)
-                dst += (uint32_t)(((rec[4 * gi + 2] & 0xFFFF) + 2 + 3) & ~3u);
+                w[3] = at;       // its new slot in the batch image
+                at += (uint32_t)(((rec[4 * gi + 2] & 0xFFFF) + 2 + 3) & ~3u);
+            }
+        }
+    }
+}
+
+
+// The cut families' images re-laid out as bsdc_split_fill placed their records (include/bsdc_host.h).
+void bsdc_split_move(uint8_t *seq, uint8_t *qual, uint32_t *rec_off, const uint32_t *split_fams, int64_t n_sf,
+                     const uint32_t *parts, const uint32_t *part_recs, int32_t n_threads) {
+#ifdef _OPENMP
+    if (n_threads > 0) omp_set_num_threads(n_threads);
+#endif
+#pragma omp parallel for schedule(dynamic, 4)
+    for (int64_t f = 0; f < n_sf; f++) {
+        const uint32_t *sf = split_fams + 8 * f;
+        const uint32_t r0 = sf[1], img = sf[3], p0 = sf[4], np = sf[5];
+        const uint32_t base = rec_off[r0];
+        std::vector<uint8_t> tq(img), ts(img / 2 + 1);
+        std::memcpy(tq.data(), qual + base, img);  // (entries no record holds keep their bytes)
+        std::memcpy(ts.data(), seq + base / 2, img / 2);
+        for (uint32_t p = p0; p < p0 + np; p++) {
+            const uint32_t *pt = parts + 4 * (int64_t)p;
+            for (uint32_t q = 0; q < (pt[2] & 0xFFu); q++) {
+                const uint32_t *w = part_recs + 4 * ((int64_t)pt[1] + q);
+                const uint32_t from = rec_off[w[0]], to = w[3];
+                const uint32_t cap = ((w[2] >> 16) + 2 + 3) & ~3u;  // (slots start at even entries: whole bytes)
+                std::memcpy(tq.data() + (to - base), qual + from, cap);
+                std::memcpy(ts.data() + (to - base) / 2, seq + from / 2, cap / 2);
+            }
+        }
+        std::memcpy(qual + base, tq.data(), img);
+        std::memcpy(seq + base / 2, ts.data(), img / 2);
+        for (uint32_t p = p0; p < p0 + np; p++) {
+            const uint32_t *pt = parts + 4 * (int64_t)p;
+            for (uint32_t q = 0; q < (pt[2] & 0xFFu); q++) {
+                const uint32_t *w = part_recs + 4 * ((int64_t)pt[1] + q);
+                rec_off[w[0]] = w[3];
             }
         }
     }

@@ -2642,7 +2642,10 @@ __device__ void process_large(const KParams &P, uint8_t *A, uint8_t *s_tab, cons
     const bool do_extend = P.mode & BSDC_MODE_EXTEND;
     const bool do_vote = P.mode & BSDC_MODE_VOTE;
     const uint4 *REC = reinterpret_cast<const uint4 *>(B.rec);
-    const uint32_t off0 = n > 0 && !PART ? REC[r0].x : 0u;
+    const uint4 *PR = reinterpret_cast<const uint4 *>(B.split_part_recs);  // (PART) batch record, slot, mate, batch slot
+    // the image's first entry in the batch: the family's first slot, or a part's staged chunks'
+    // first entry (its first record's batch slot less its slot in the staged image)
+    const uint32_t off0 = n > 0 ? (PART ? PR[r0].w - PR[r0].y : REC[r0].x) : 0u;
     const int stop = (P.mode >> BSDC_MODE_STOP_SHIFT) & 15;  // profiling ablation (0 = full kernel)
 
     // ---- one round of global loads for everything the family needs first: the tables (s_cnt[0]
@@ -2657,9 +2660,8 @@ __device__ void process_large(const KParams &P, uint8_t *A, uint8_t *s_tab, cons
     RecMeta *M = reinterpret_cast<RecMeta *>(A + L0.meta);
     uint16_t *clist = reinterpret_cast<uint16_t *>(A + L0.clist);  // the converted records
     uint32_t qor = 0;  // OR of the family's quals: a byte >= 128 keeps the overlap off the SWAR path
-    // 16-B chunks: quals, then packed bases (a part copies its records' slots one by one instead)
-    const int nqc = PART ? 0 : (int)(img >> 4), nch = PART ? 0 : nqc + (int)(img >> 5);
-    const uint4 *PR = reinterpret_cast<const uint4 *>(B.split_part_recs);  // (PART) batch record, slot, mate
+    // 16-B chunks: quals, then packed bases (a part's records lie back to back: its chunks too)
+    const int nqc = (int)(img >> 4), nch = nqc + (int)(img >> 5);
     auto load_chunk = [&](int k) {
         const uint8_t *src = k < nqc ? B.qual + off0 + 16 * (uint32_t)k : B.seq + (off0 >> 1) + 16 * (uint32_t)(k - nqc);
         return *reinterpret_cast<const uint4 *>(src);
@@ -2712,36 +2714,6 @@ __device__ void process_large(const KParams &P, uint8_t *A, uint8_t *s_tab, cons
     for (int u = 0; u < kLStageU; u++)
         if (tt + u * G < nch) store_chunk(tt + u * G, v[u]);
     if (tt < kTabBytesL / 16) reinterpret_cast<uint4 *>(s_tab)[tt] = tv;
-    if (PART) {  // the part's records' slots, flattened over (record, 4 entries): U units per record
-        // (a part record's entry carries its batch slot and length: one load before the data)
-        const uint32_t U = (uint32_t)(B.max_len + 2 + 3) >> 2;
-        const uint32_t uinv = (uint32_t)((((uint64_t)1 << 32) + U - 1) / U);  // k / U = umulhi(k, uinv), k < 2^16
-        const bool fast_div = n * (int)U < 65536;
-        constexpr int PU = 4;  // units in flight per thread
-        for (int k0 = tt; k0 < n * (int)U; k0 += PU * G) {
-            uint32_t q[PU], bb[PU], dst[PU];
-#pragma unroll
-            for (int u = 0; u < PU; u++) {
-                const int k = k0 + u * G;
-                dst[u] = 0xFFFFFFFFu;
-                if (k >= n * (int)U) continue;
-                const uint32_t r = fast_div ? __umulhi((uint32_t)k, uinv) : (uint32_t)k / U, j = (uint32_t)k - r * U;
-                const uint4 pr = PR[r0 + r];
-                if (4 * j >= (((pr.z >> 16) + 2 + 3) & ~3u)) continue;
-                q[u] = *reinterpret_cast<const uint32_t *>(B.qual + pr.w + 4 * j);
-                bb[u] = *reinterpret_cast<const uint16_t *>(B.seq + (pr.w >> 1) + 2 * j);
-                dst[u] = pr.y + 4 * j;
-            }
-#pragma unroll
-            for (int u = 0; u < PU; u++) {
-                if (dst[u] == 0xFFFFFFFFu) continue;
-                st32(qimg + dst[u], q[u]);
-                qor |= q[u];
-                const uint32_t x = bb[u];  // two packed bytes, high nibble first -> four base bytes
-                st32(slots + dst[u], ((x >> 4) & 0xFu) | ((x & 0xFu) << 8) | ((x >> 12) << 16) | (((x >> 8) & 0xFu) << 24));
-            }
-        }
-    }
     for (int k0 = tt + kLStageU * G; k0 < nch; k0 += kLStageU * G) {  // families of more chunks
 #pragma unroll
         for (int u = 0; u < kLStageU; u++)

@@ -83,6 +83,9 @@ def _load():
     lib.bsdc_split_fill.argtypes = [C.c_void_p, C.c_void_p, C.c_int64, C.c_int64, C.c_int32, C.c_void_p, C.c_void_p,
                                     C.c_void_p, C.c_void_p, C.c_int32]
     lib.bsdc_split_fill.restype = None
+    lib.bsdc_split_move.argtypes = [C.c_void_p, C.c_void_p, C.c_void_p, C.c_void_p, C.c_int64, C.c_void_p, C.c_void_p,
+                                    C.c_int32]
+    lib.bsdc_split_move.restype = None
     _lib = lib
     return lib
 

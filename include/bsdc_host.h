@@ -118,13 +118,21 @@ void bsdc_batch_free(bsdc_batch *b);
  * rec: the batch's [4 * n_rec] record words; ents: [n_ent][4] bucket entries (family, first
  * record, n_rec, image bytes).  bsdc_split_count writes each entry's part count (0 = not cut) and
  * record count in its parts, and returns the total parts; bsdc_split_fill writes the part entries
- * (family, first part record, n_rec, image bytes) and part records (batch record, slot in the
- * part image, part-local mate index or 0xFFFF, 0), entry e's from first_part[e] / first_rec[e]. */
+ * (family, first part record, n_rec, staged image entries) and part records (batch record, slot
+ * in the part's staged image, part-local mate index or 0xFFFF | length << 16, new batch slot),
+ * entry e's from first_part[e] / first_rec[e].  The new slots lay each cut family's image out part
+ * after part, each part's records back to back from its first record's slot (the family's first
+ * record first: the whole-family fallback reads the image from its slot); a part stages the
+ * 32-entry chunks that cover its records, from its first slot rounded down to 32 (the staged image
+ * entries).  bsdc_split_move then moves the bytes of seq (packed nt16) and qual and rewrites the
+ * batch records' slots (rec_off [n_rec]); split_fams: [n_sf][8] (include/bsdc.h). */
 int64_t bsdc_split_count(const uint32_t *rec, const uint32_t *ents, int64_t n_ent, int64_t part_cap, int32_t max_part_rec,
                          int32_t *nparts, int64_t *nrecs, int32_t n_threads);
 void bsdc_split_fill(const uint32_t *rec, const uint32_t *ents, int64_t n_ent, int64_t part_cap, int32_t max_part_rec,
                      const int64_t *first_part, const int64_t *first_rec, uint32_t *parts, uint32_t *part_recs,
                      int32_t n_threads);
+void bsdc_split_move(uint8_t *seq, uint8_t *qual, uint32_t *rec_off, const uint32_t *split_fams, int64_t n_sf,
+                     const uint32_t *parts, const uint32_t *part_recs, int32_t n_threads);
 
 const char *bsdc_host_last_error(void);
 /* the input record of the last BSDC_PLAN_EMISSING_MI */

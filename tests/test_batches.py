@@ -6,6 +6,7 @@ import numpy as np
 import pytest
 
 from bsseqconsensusreads_amd import batch, pipeline, shard, synth
+from bsseqconsensusreads_amd import records as R
 
 
 def _per_family_images(fb):
@@ -64,34 +65,46 @@ def test_split_partner_marks_both_families():
 
 
 def test_split_part_records_cover_each_family_once(monkeypatch):
-    """k_large part mode's host cut (bsdc_split_count / bsdc_split_fill via batch.split_hbm_bucket):
-    every record of a cut family sits in exactly one part, whole templates stay together (a part-
-    local mate points at the record's mate), the part images are the records' slots back to back,
-    and each part record carries its length and batch slot (what the part staging copies)."""
+    """k_large part mode's host cut (bsdc_split_count / bsdc_split_fill / bsdc_split_move via
+    batch.split_hbm_bucket): every record of a cut family sits in exactly one part, whole templates
+    stay together (a part-local mate points at the record's mate), each part's records lie back to
+    back in the re-laid-out family image (its staged chunks from its first slot rounded down to 32),
+    the family's first record leads its image, and every record's bases and quals moved with it."""
     from bsseqconsensusreads_amd import batch as B, synth
     s = synth.generate("C3", 300, seed=5, device="cpu", genome_len=200_000)
     fb = B.build_family_batch(s.raw, "full", s.ref)
+    L = (fb.rec_lenflag & 0xFFFF).astype(np.int64)
+    old_off = fb.rec_off.astype(np.int64).copy()
+    codes = R.unpack_nibbles(fb.seq, 2 * fb.seq.shape[0]).copy()
+    quals = fb.qual.copy()
     monkeypatch.setattr(B, "SPLIT_FROM", 0)  # every large bucket (C3 has no HBM-arena family)
     fb = B.split_hbm_bucket(fb, part_cap=12_000)
     sf = fb.split_fams.astype(np.int64)
     assert sf.shape[0] > 0
     parts, prec = fb.split_parts.astype(np.int64), fb.split_part_recs.astype(np.int64)
-    L = (fb.rec_lenflag & 0xFFFF).astype(np.int64)
+    codes2 = R.unpack_nibbles(fb.seq, 2 * fb.seq.shape[0])
+    new_off = fb.rec_off.astype(np.int64)
     for row, f in enumerate(sf):
         fam, r0, n, p0, npart = f[0], f[1], f[2], f[4], f[5]
-        seen = []
+        base = int(old_off[r0:r0 + n].min())
+        assert new_off[r0] == base  # (the whole-family fallback reads the image from there)
+        seen, at = [], base
         for p in parts[p0:p0 + npart]:
             assert p[0] == fam and p[2] >> 8 == row  # (the part knows its split family's row)
             recs = prec[p[1]:p[1] + (p[2] & 0xFF)]
-            dst = 0
+            a0 = int(recs[0][3] - recs[0][1])
+            assert a0 % 32 == 0 and 0 <= recs[0][1] < 32
             for li, w in enumerate(recs):
                 gi = int(w[0])
                 seen.append(gi)
-                assert w[1] == dst and (w[2] >> 16) == L[gi] and w[3] == fb.rec_off[gi]
-                dst += (L[gi] + 2 + 3) // 4 * 4
+                cap = (L[gi] + 2 + 3) // 4 * 4
+                assert w[3] == at == new_off[gi] and w[1] == at - a0 and (w[2] >> 16) == L[gi]
+                a, b = int(old_off[gi]), int(new_off[gi])
+                assert np.array_equal(codes2[b:b + cap], codes[a:a + cap]) and np.array_equal(fb.qual[b:b + cap], quals[a:a + cap])
+                at += cap
                 lm = int(w[2] & 0xFFFF)
                 gm = int(fb.rec_link[gi] & 0xFFFF)
                 if gm != 0xFFFF:  # the mate is in the same part, at its local index
                     assert lm != 0xFFFF and recs[lm][0] == r0 + gm
-            assert p[3] == (dst + 31) // 32 * 32  # (images are whole 32-entry chunks)
+            assert p[3] == (at - a0 + 31) // 32 * 32  # (the staged image: whole 32-entry chunks)
         assert sorted(seen) == list(range(r0, r0 + n))
