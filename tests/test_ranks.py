@@ -11,7 +11,7 @@ import pytest
 
 from bsseqconsensusreads_amd import bam, ranks
 from helpers import assert_bam_matches_oracle
-from test_fleet import STANDIN, sorted_input, write_fasta  # noqa: F401 -- (the module fixture)
+from test_fleet import STANDIN, _sorted_bam, sorted_input, write_fasta  # noqa: F401 -- (the module fixture)
 
 SLACK = 2000
 
@@ -136,3 +136,31 @@ def test_rank_failure_reaches_the_caller(sorted_input, tmp_path):  # noqa: F811
 
 
 
+
+
+def test_small_file_gets_fewer_ranks(tmp_path):
+    """A file too small for N key gaps 2 x slack apart runs on the ranks the cuts allow (here 1,
+    with a 300-position genome share per rank impossible), and still writes the one-range bytes"""
+    s, p = _sorted_bam(tmp_path, cfg="C2", n_fam=40, messy=0.0, seed=3, genome_len=6_000)
+    fa = str(tmp_path / "g.fa")
+    write_fasta(fa, s.ref)
+    assert len(ranks.plan_cuts(p, 4, threads=2, slack=SLACK)) == 0
+    info4, _, got4, _ = _run(tmp_path, p, fa, "four", 4)
+    info1, _, got1, _ = _run(tmp_path, p, fa, "one1", 1)
+    assert info4["ranks"] == 1 and not info4["cuts_fallback"]
+    assert got4 == got1 and info4["records_in"] == s.raw.n
+
+
+def test_empty_input(tmp_path):
+    """No records: one range, a header-only BAM and empty FASTQ files"""
+    from bsseqconsensusreads_amd import records as R
+    s, p = _sorted_bam(tmp_path, cfg="C2", n_fam=5, messy=0.0, seed=3, genome_len=6_000)
+    hdr, raw = bam.read_bam(p)
+    q = str(tmp_path / "empty.bam")
+    bam.write_bam(q, hdr, bam.records_to_bam(R.take(raw, np.zeros(0, np.int64))))
+    fa = str(tmp_path / "g.fa")
+    write_fasta(fa, s.ref)
+    info, _, got, _ = _run(tmp_path, q, fa, "empty", 3)
+    assert info["ranks"] == 1 and info["records_in"] == 0 and info["records_out"] == 0
+    assert got[1] == b"" and got[2] == b""
+    assert bam.read_bam(str(tmp_path / "empty.bam"))[1].n == 0
