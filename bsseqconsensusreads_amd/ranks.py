@@ -73,11 +73,30 @@ def windows_of(cuts) -> List[Tuple[int, int, int, int]]:
     return [(lo[r][0], lo[r][1], hi[r][0], hi[r][1]) for r in range(len(cuts) + 1)]
 
 
-def _rank(r: int, device: int, runner_spec: Optional[str], job: dict, rq):
-    """One rank (a spawned process: the first thing here to touch its GPU)."""
+def _run_job(r: int, eng, runner, job: dict) -> tuple:
+    """One rank's part of the file: the one-GPU stream over its window, its own keys only."""
+    from . import bam
+    st, rs = {}, {}
+    t0 = time.perf_counter()
     try:
-        from . import bam
-        runner = eng = None
+        info = bam._stream_step(job["in_bam"], job["fasta"], job["out_bam"], eng, job["prefix"], job["threads"],
+                                job["level"], job["fastq"], job["tags"], job["chunk_bytes"], job["slack"],
+                                job["batch_bases"], st, job["gpu_bgzf"] and runner is None, None, rng=job["rng"],
+                                fragment="first" if r == 0 else "next", runner=runner, range_stats=rs,
+                                owner=(r, job["cuts"], True) if job["cuts"] else None)
+    except OSError as e:
+        if "foreign record" in str(e):
+            return ("foreign", r, str(e))
+        raise
+    info["seconds"] = round(time.perf_counter() - t0, 4)
+    return ("done", r, info, st, rs)
+
+
+def _rank_server(i: int, device: int, runner_spec: Optional[str], tq, rq):
+    """A pool's rank process (spawned: the first thing here to touch its GPU): its engine or
+    runner once, then jobs until None."""
+    eng = runner = None
+    try:
         if runner_spec is None:
             from .device import Engine
             eng = Engine(device)
@@ -85,26 +104,94 @@ def _rank(r: int, device: int, runner_spec: Optional[str], job: dict, rq):
             import importlib
             mod, cls = runner_spec.split(":")
             runner = getattr(importlib.import_module(mod), cls)(device)
-        st, rs = {}, {}
-        t0 = time.perf_counter()
+        rq.put(("ready", i))
+        while True:
+            job = tq.get()
+            if job is None:
+                break
+            try:
+                rq.put(_run_job(job["rank"], eng, runner, job))
+            except BaseException as e:  # noqa: BLE001 -- reported to the parent, which raises it
+                rq.put(("error", job["rank"], "%s: %s\n%s" % (type(e).__name__, e, traceback.format_exc())))
+    except BaseException as e:  # noqa: BLE001
+        rq.put(("error", i, "%s: %s\n%s" % (type(e).__name__, e, traceback.format_exc())))
+    finally:
+        if eng is not None:
+            eng.close()
+        if runner is not None and hasattr(runner, "close"):
+            runner.close()
+
+
+class RankPool:
+    """N rank processes, one per device, spawned before this process touches any GPU (spawn
+    context), each holding its engine across calls of step5_ranks(pool=...): start it outside a
+    timed region, as fleet.Fleet's workers are."""
+
+    def __init__(self, devices: Sequence[int], runner: Optional[str] = None):
+        ctx = tmp.get_context("spawn")
+        self.rq = ctx.Queue()
+        self.tqs = [ctx.Queue() for _ in devices]
+        self.procs = [ctx.Process(target=_rank_server, args=(i, int(d), runner, self.tqs[i], self.rq), daemon=True)
+                      for i, d in enumerate(devices)]
+        for p in self.procs:
+            p.start()
+        self.n = len(devices)
         try:
-            info = bam._stream_step(job["in_bam"], job["fasta"], job["out_bam"], eng, job["prefix"], job["threads"],
-                                    job["level"], job["fastq"], job["tags"], job["chunk_bytes"], job["slack"],
-                                    job["batch_bases"], st, job["gpu_bgzf"] and runner is None, None, rng=job["rng"],
-                                    fragment="first" if r == 0 else "next", runner=runner, range_stats=rs,
-                                    owner=(r, job["cuts"], True) if job["cuts"] else None)
-        finally:
-            if eng is not None:
-                eng.close()
-            if runner is not None and hasattr(runner, "close"):
-                runner.close()
-        info["seconds"] = round(time.perf_counter() - t0, 4)
-        rq.put(("done", r, info, st, rs))
-    except BaseException as e:  # noqa: BLE001 -- reported to the parent, which raises it
-        if isinstance(e, OSError) and "foreign record" in str(e):
-            rq.put(("foreign", r, str(e)))
-        else:
-            rq.put(("error", r, "%s: %s\n%s" % (type(e).__name__, e, traceback.format_exc())))
+            for _ in range(self.n):
+                m = self.get()
+                if m[0] != "ready":
+                    raise RuntimeError("rank failed to start: %s" % (m,))
+        except BaseException:
+            self.close(terminate=True)
+            raise
+
+    def get(self):
+        """The next rank message; raises if a rank died."""
+        import queue
+        while True:
+            try:
+                return self.rq.get(timeout=1.0)
+            except queue.Empty:
+                dead = [i for i, p in enumerate(self.procs) if not p.is_alive()]
+                if dead:
+                    raise RuntimeError("rank %d exited (code %s)" % (dead[0], self.procs[dead[0]].exitcode))
+
+    def run(self, jobs: Sequence[dict]) -> list:
+        """Jobs 0..k-1 on ranks 0..k-1 (k <= n); their results in order.  A failing or foreign
+        rank raises after every rank has answered (the pool stays usable)."""
+        for r, job in enumerate(jobs):
+            self.tqs[r].put(dict(job, rank=r))
+        res, bad = {}, None
+        while len(res) < len(jobs):
+            m = self.get()
+            res[m[1]] = m
+            if m[0] in ("error", "foreign") and bad is None:
+                bad = m
+        if bad is not None:
+            if bad[0] == "foreign":
+                raise ForeignRecords("rank %d: %s" % (bad[1], bad[2]))
+            raise RuntimeError("rank %d: %s" % (bad[1], bad[2]))
+        return [res[r][2:] for r in range(len(jobs))]
+
+    def close(self, terminate: bool = False):
+        for q in self.tqs:
+            try:
+                q.put(None)
+            except Exception:  # noqa: BLE001
+                pass
+        for p in self.procs:
+            if terminate and p.is_alive():
+                p.terminate()
+            p.join(30)
+            if p.is_alive():
+                p.kill()
+                p.join(5)
+
+    def __enter__(self):
+        return self
+
+    def __exit__(self, *exc):
+        self.close(terminate=exc[0] is not None)
 
 
 class ForeignRecords(RuntimeError):
@@ -125,13 +212,15 @@ def step5_ranks(in_bam: str, fasta: str, out_bam: Optional[str], devices: Sequen
                 threads: int = 0, level: int = 6, fastq: Optional[Tuple[str, str]] = None, tags: bool = True,
                 chunk_bytes: Optional[int] = None, slack: Optional[int] = None, batch_bases: Optional[int] = None,
                 runner: Optional[str] = None, stats: Optional[dict] = None, gpu_bgzf: bool = False,
-                cuts: Optional[list] = None, on_foreign: str = "one") -> dict:
+                cuts: Optional[list] = None, on_foreign: str = "one", pool: Optional[RankPool] = None) -> dict:
     """Rules convert_Bstrain .. callduplex (main.snake.py:121-164) on a coordinate-sorted BAM by
     len(devices) rank processes (see the module docstring); same file contract as bam.step5_stream.
     runner: "module:Class" of a fleet-style runner (the CPU stand-in of the tests) instead of the
     GPU; cuts: the rank boundaries to use (tests; default plan_cuts).  on_foreign: what a record
     no rank can own does -- "one": rerun the file as one range (the default), "raise":
-    ForeignRecords (the caller picks another path: cli.py runs fleet.step5_stream_multi)."""
+    ForeignRecords (the caller picks another path: cli.py runs fleet.step5_stream_multi).  pool: a
+    started RankPool of at least len(devices) ranks to run on (its devices then; default: one is
+    spawned for this call and closed after)."""
     from . import bam
     chunk_bytes = bam.DEFAULT_CHUNK_BYTES if chunk_bytes is None else chunk_bytes
     slack = bam.DEFAULT_SLACK if slack is None else slack
@@ -142,7 +231,7 @@ def step5_ranks(in_bam: str, fasta: str, out_bam: Optional[str], devices: Sequen
     hdr = bam.read_bam_header(in_bam)
     pre = bam.read_name_prefix(hdr) if prefix is None else prefix
 
-    def run(cuts):
+    def run(cuts, pl: RankPool):
         ranges = windows_of(cuts)
         n = len(ranges)
         tmpdir = os.path.dirname(os.path.abspath(out_bam if out_bam is not None else fastq[0]))
@@ -150,59 +239,46 @@ def step5_ranks(in_bam: str, fasta: str, out_bam: Optional[str], devices: Sequen
         frags = [(os.path.join(tmpdir, ".%s.%d.bam" % (tag, r)) if out_bam is not None else None,
                   (os.path.join(tmpdir, ".%s.%d.r1.fq.gz" % (tag, r)), os.path.join(tmpdir, ".%s.%d.r2.fq.gz" % (tag, r)))
                   if fastq is not None else None) for r in range(n)]
-        ctx = tmp.get_context("spawn")
-        rq = ctx.Queue()
-        procs = []
+        jobs = [dict(in_bam=in_bam, fasta=fasta, out_bam=frags[r][0], prefix=pre, threads=threads, level=level,
+                     fastq=frags[r][1], tags=tags, chunk_bytes=chunk_bytes, slack=slack, batch_bases=batch_bases,
+                     gpu_bgzf=gpu_bgzf, rng=ranges[r], cuts=cuts) for r in range(n)]
         try:
-            for r in range(n):
-                job = dict(in_bam=in_bam, fasta=fasta, out_bam=frags[r][0], prefix=pre, threads=threads, level=level,
-                           fastq=frags[r][1], tags=tags, chunk_bytes=chunk_bytes, slack=slack, batch_bases=batch_bases,
-                           gpu_bgzf=gpu_bgzf, rng=ranges[r], cuts=cuts)
-                p = ctx.Process(target=_rank, args=(r, int(devices[r % len(devices)]), runner, job, rq), daemon=True)
-                p.start()
-                procs.append(p)
-            res = {}
-            while len(res) < n:
-                try:
-                    m = rq.get(timeout=1.0)
-                except Exception:  # noqa: BLE001 -- queue.Empty: check that the ranks are alive
-                    dead = [i for i, p in enumerate(procs) if not p.is_alive() and i not in res]
-                    if dead:
-                        raise RuntimeError("rank %d exited (code %s)" % (dead[0], procs[dead[0]].exitcode))
-                    continue
-                if m[0] == "error":
-                    raise RuntimeError("rank %d: %s" % (m[1], m[2]))
-                if m[0] == "foreign":
-                    raise ForeignRecords("rank %d: %s" % (m[1], m[2]))
-                res[m[1]] = m[2:]
-            for p in procs:
-                p.join(60)
-            return [res[r] for r in range(n)], frags, ranges
+            return pl.run(jobs), frags, ranges
         except BaseException:
-            for p in procs:  # (stopped before their fragments go: a live rank could still create one)
-                if p.is_alive():
-                    p.terminate()
-            for p in procs:
-                p.join(10)
-                if p.is_alive():
-                    p.kill()
-                    p.join(5)
-            for f in frags:
+            for f in frags:  # (every rank has answered: none still writes)
                 for path in ([f[0]] if f[0] else []) + (list(f[1]) if f[1] else []):
                     if os.path.exists(path):
                         os.unlink(path)
             raise
 
-    t1 = time.perf_counter()
-    foreign = 0
+    own = pool is None
+    if own:
+        t_p = time.perf_counter()
+        pool = RankPool(list(devices)[:len(cuts) + 1], runner)
+        t_pool = time.perf_counter() - t_p
+    else:
+        t_pool = 0.0
+        if pool.n < len(cuts) + 1:
+            raise ValueError("a pool of %d ranks for %d ranges" % (pool.n, len(cuts) + 1))
     try:
-        results, frags, ranges = run(cuts)
-    except ForeignRecords:  # (its ranks stopped at their first such record; no fragments are left)
-        if on_foreign == "raise" or not cuts:
-            raise
-        foreign = 1
-        results, frags, ranges = run([])
-    t2 = time.perf_counter()
+        t1 = time.perf_counter()
+        foreign = 0
+        try:
+            results, frags, ranges = run(cuts, pool)
+        except ForeignRecords:  # (no fragments are left)
+            if on_foreign == "raise" or not cuts:
+                raise
+            foreign = 1
+            results, frags, ranges = run([], pool)
+        t2 = time.perf_counter()
+    except BaseException:
+        if own:
+            pool.close(terminate=True)
+            own = False
+        raise
+    finally:
+        if own:
+            pool.close()
     try:
         if out_bam is not None:
             _concat(out_bam, [f[0] for f in frags])
@@ -221,7 +297,8 @@ def step5_ranks(in_bam: str, fasta: str, out_bam: Optional[str], devices: Sequen
         for k in ("records_in", "families", "families_emitted", "records_out"):
             info[k] += int(inf.get(k, 0))
     if stats is not None:
-        stats.update(cut_s=round(t_cut, 4), ranks_s=round(t2 - t1, 4), assemble_s=round(t3 - t2, 4),
+        stats.update(cut_s=round(t_cut, 4), pool_start_s=round(t_pool, 4), ranks_s=round(t2 - t1, 4),
+                     assemble_s=round(t3 - t2, 4),
                      rank_records=[int(x[0].get("records_in", 0)) for x in results],
                      rank_read=[int(x[2].get("n", 0)) for x in results],
                      rank_seconds=[x[0].get("seconds") for x in results], ranges=ranges)

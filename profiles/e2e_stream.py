@@ -8,9 +8,9 @@ synthetic coordinate-sorted C2 BAM + FASTA on local disk, then, each in a fresh 
   fleet   fleet.step5_stream_multi: this child reads and writes, --workers spawned GPU worker
           processes (all on GPU 0 on a one-GPU box; started before the clock) run the batches
   fleet_gpubgzf  the same with the writer's deflate on GPU 0
-  ranks, ranks_gpubgzf  ranks.step5_ranks: --workers rank processes (all on GPU 0 here), each
-          decoding, computing and writing its own key interval with threads / workers host threads
-          (spawn and HIP init inside the clock)
+  ranks, ranks_gpubgzf  ranks.step5_ranks: --workers rank processes (all on GPU 0 here; a
+          RankPool started before the clock), each decoding, computing and writing its own key
+          interval with threads / workers host threads
   molecular_stream, molecular_whole  step 1 (bam.molecular_stream / bam.molecular) on the same
           families in GroupReadsByUmi order (a second input, MI runs contiguous; BAM with tags, GPU BGZF)
 The BAMs are compared byte for byte.  Usage:
@@ -82,11 +82,18 @@ def child(args):
         return 0
     if args.mode in ("ranks", "ranks_gpubgzf"):  # rank processes, each its own part of the file
         from bsseqconsensusreads_amd import ranks
+        ts = time.perf_counter()
+        pool = ranks.RankPool([0] * args.workers)  # started (spawn, import, HIP init) outside the clock
         t0 = time.perf_counter()
-        info = ranks.step5_ranks(args.inp, args.fa, args.out, [0] * args.workers,
-                                 threads=max(1, args.threads // args.workers), level=args.level,
-                                 chunk_bytes=args.chunk_mb << 20, stats=stats, gpu_bgzf=args.mode == "ranks_gpubgzf")
-        dt = time.perf_counter() - t0
+        try:
+            info = ranks.step5_ranks(args.inp, args.fa, args.out, [0] * args.workers,
+                                     threads=max(1, args.threads // args.workers), level=args.level,
+                                     chunk_bytes=args.chunk_mb << 20, stats=stats,
+                                     gpu_bgzf=args.mode == "ranks_gpubgzf", pool=pool)
+            dt = time.perf_counter() - t0
+        finally:
+            pool.close()
+        stats["pool_start_s"] = round(t0 - ts, 3)
         crss = resource.getrusage(resource.RUSAGE_CHILDREN).ru_maxrss / 1024
         print(json.dumps({"mode": args.mode, "ranks": args.workers, "seconds": round(dt, 3),
                           "rank_peak_rss_MiB": round(crss, 1), "stage_busy_s": stats, **info}))

@@ -164,3 +164,19 @@ def test_empty_input(tmp_path):
     assert info["ranks"] == 1 and info["records_in"] == 0 and info["records_out"] == 0
     assert got[1] == b"" and got[2] == b""
     assert bam.read_bam(str(tmp_path / "empty.bam"))[1].n == 0
+
+
+def test_pool_runs_several_files(sorted_input, one_range):  # noqa: F811
+    """A RankPool started once runs several calls (its ranks keep their runners), each writing the
+    one-range bytes; a failing call leaves the pool usable"""
+    s, p, fa, tmp = sorted_input
+    with ranks.RankPool([0, 0], runner=STANDIN) as pool:
+        for k in range(2):
+            info, st, got, _ = _run(tmp, p, fa, "pool%d" % k, 2, pool=pool)
+            assert info["ranks"] == 2 and not info["cuts_fallback"] and st["pool_start_s"] == 0.0
+            assert got == one_range[2]
+        bad = bam.find_cut(p, os.path.getsize(p) // 2, 2, min_span=0, slack=0, guard=0)
+        with pytest.raises(ranks.ForeignRecords):
+            _run(tmp, p, fa, "poolbad", 2, cuts=[bad], on_foreign="raise", pool=pool)
+        info, _, got, _ = _run(tmp, p, fa, "pool2", 2, pool=pool)
+        assert got == one_range[2]
