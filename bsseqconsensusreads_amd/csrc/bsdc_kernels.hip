@@ -3741,6 +3741,7 @@ struct bsdc_ctx {
     // split families: a k_join dispatch after all the parts (default), or the last part of each
     // family joins it (BSDC_SPLIT_JOIN=part: measured slower, profiles/r05/README.md)
     bool part_join = false;
+    bool large_first = false;
 };
 
 static float det_expf_host(float x) {
@@ -3973,6 +3974,8 @@ int32_t bsdc_ctx_create(int32_t device, const bsdc_params *params, bsdc_ctx **ou
         c->pair = sk && std::string(sk) == "pair";
         const char *sj = getenv("BSDC_SPLIT_JOIN");
         c->part_join = sj && std::string(sj) == "part";
+        const char *lf = getenv("BSDC_LARGE_FIRST");
+        c->large_first = lf && std::string(lf) == "1";
     }
     make_tables(params->error_rate_pre_umi, params->error_rate_post_umi, c->host_tab.t);
     make_fp64(params->error_rate_post_umi, c->host_tab.lnc, c->host_tab.lne3);
@@ -4179,6 +4182,7 @@ int32_t bsdc_run(bsdc_ctx *c, const bsdc_family_batch *b, bsdc_consensus *o, int
         const hipError_t e = hipGetLastError();
         if (e != hipSuccess) fail(e, "split launch");
     };
+    auto launch_small_all = [&]() {
     if (!(mode & BSDC_MODE_SKIP_SMALL) && rc == 0) {
         const uint32_t *f = b->small_fams;
         for (int q = 0; q < BSDC_SMALL_BUCKETS && rc == 0; q++) {
@@ -4242,6 +4246,8 @@ int32_t bsdc_run(bsdc_ctx *c, const bsdc_family_batch *b, bsdc_consensus *o, int
             f += 4 * nf;
         }
     }
+    };
+    auto launch_large_all = [&]() {
     if (!(mode & BSDC_MODE_SKIP_LARGE) && rc == 0) {
         // one dispatch per non-empty bucket: its LDS arena size sets how many workgroups share a CU
         const uint4 *f = reinterpret_cast<const uint4 *>(b->large_fams);
@@ -4285,6 +4291,16 @@ int32_t bsdc_run(bsdc_ctx *c, const bsdc_family_batch *b, bsdc_consensus *o, int
             f += nf;
         }
         launch_split();  // (first instead: not faster, profiles/r05/README.md)
+    }
+    };
+    // (BSDC_LARGE_FIRST=1) the large families' dispatches first: their long per-family chains
+    // start at once and the small-family dispatches fill the CUs beside them
+    if (c->large_first) {
+        launch_large_all();
+        launch_small_all();
+    } else {
+        launch_small_all();
+        launch_large_all();
     }
     // join: `s` waits for every side stream used -- also after a failed launch, so that no work
     // already queued on a side stream outlives the caller's view of the batch's buffers
