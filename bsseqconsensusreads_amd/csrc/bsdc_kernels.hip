@@ -3741,7 +3741,6 @@ struct bsdc_ctx {
     // split families: a k_join dispatch after all the parts (default), or the last part of each
     // family joins it (BSDC_SPLIT_JOIN=part: measured slower, profiles/r05/README.md)
     bool part_join = false;
-    bool large_first = false;
 };
 
 static float det_expf_host(float x) {
@@ -3974,8 +3973,6 @@ int32_t bsdc_ctx_create(int32_t device, const bsdc_params *params, bsdc_ctx **ou
         c->pair = sk && std::string(sk) == "pair";
         const char *sj = getenv("BSDC_SPLIT_JOIN");
         c->part_join = sj && std::string(sj) == "part";
-        const char *lf = getenv("BSDC_LARGE_FIRST");
-        c->large_first = lf && std::string(lf) == "1";
     }
     make_tables(params->error_rate_pre_umi, params->error_rate_post_umi, c->host_tab.t);
     make_fp64(params->error_rate_post_umi, c->host_tab.lnc, c->host_tab.lne3);
@@ -4293,15 +4290,9 @@ int32_t bsdc_run(bsdc_ctx *c, const bsdc_family_batch *b, bsdc_consensus *o, int
         launch_split();  // (first instead: not faster, profiles/r05/README.md)
     }
     };
-    // (BSDC_LARGE_FIRST=1) the large families' dispatches first: their long per-family chains
-    // start at once and the small-family dispatches fill the CUs beside them
-    if (c->large_first) {
-        launch_large_all();
-        launch_small_all();
-    } else {
-        launch_small_all();
-        launch_large_all();
-    }
+    // small families first (the large families' dispatches first: not faster, profiles/r05/README.md)
+    launch_small_all();
+    launch_large_all();
     // join: `s` waits for every side stream used -- also after a failed launch, so that no work
     // already queued on a side stream outlives the caller's view of the batch's buffers
     for (int i = 0; i < kForkStreams; i++)
