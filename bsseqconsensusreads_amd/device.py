@@ -15,7 +15,7 @@ import numpy as np
 import torch
 
 from . import _lib
-from .batch import LARGE_LDS_MAX, FamilyBatch, wide_rows
+from .batch import FamilyBatch, wide_rows
 from .records import Reference
 
 

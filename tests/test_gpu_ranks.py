@@ -5,6 +5,9 @@ and FASTQ pair that decompress to the bytes of `--gpus 1`, whose records equal o
 whole file (tests/test_gpu_fleet.py).  Only the BGZF blocks at the ranks' seams differ."""
 import gzip
 import json
+import os
+import subprocess
+import sys
 
 import pytest
 
@@ -25,9 +28,6 @@ def test_cli_ranks_equal_one_gpu_and_oracle(cli_input, n):  # noqa: F811
 
 def test_cli_ranks_report(cli_input):  # noqa: F811
     """The ranks really split the file (no fallback): the info line names 2 ranks"""
-    import os
-    import subprocess
-    import sys
     tmp, inp, fa = cli_input
     root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
     env = {k: v for k, v in os.environ.items() if k not in ("WORLD_SIZE", "RANK", "LOCAL_RANK")}
