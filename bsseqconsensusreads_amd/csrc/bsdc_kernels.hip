@@ -67,11 +67,16 @@ constexpr int kLargeThreadsBig = LARGE_THREADS_BIG;  // 512 or 768
 #endif
 constexpr int kJoinThreads = JOIN_THREADS;  // k_join's workgroup (k_tie's too)
 constexpr int kJoinU = JOIN_U;              // parts' loads in flight per (set, column) in k_join
-constexpr int kLargeBigBucket = 3;
+#ifndef LARGE_BIG_BUCKET
+#define LARGE_BIG_BUCKET 2
+#endif
+// large buckets q >= this (3, 2, 1 workgroups per CU, scratch) use kLargeThreadsBig: 512-thread
+// workgroups from the 3-per-CU class on (24 waves per CU there; profiles/r05/README.md)
+constexpr int kLargeBigBucket = LARGE_BIG_BUCKET;
 #ifndef LARGE_VOTE_U
 #define LARGE_VOTE_U 4  // k_large vote pass A: reads in flight per lane
 #endif
-constexpr int kVoteU = LARGE_VOTE_U;  // large buckets q >= this (2, 1 workgroups per CU, scratch) use kLargeThreadsBig
+constexpr int kVoteU = LARGE_VOTE_U;
 #ifndef LARGE_OVL_CHUNKS
 #define LARGE_OVL_CHUNKS 2  // k_large overlap: SWAR dwords (4 positions each) per task
 #endif
@@ -4255,7 +4260,7 @@ int32_t bsdc_run(bsdc_ctx *c, const bsdc_family_batch *b, bsdc_consensus *o, int
             const int64_t nf = b->n_large[q];
             const int32_t a = b->large_arena[q];
             if (nf > 0) {
-                const bool big = q >= kLargeBigBucket;  // 2 or 1 workgroups per CU, or HBM scratch
+                const bool big = q >= kLargeBigBucket;  // 3, 2 or 1 workgroups per CU, or HBM scratch
                 const hipStream_t ls = next_stream();
                 if (rc) break;
                 const bool tg = (mode & BSDC_MODE_TAGS) != 0;
