@@ -41,7 +41,7 @@ MODE_CONVERT, MODE_EXTEND, MODE_VOTE, MODE_DUMP = 1, 2, 4, 8
 
 # small families run one per wavefront with their arena in LDS, in buckets of these arena sizes
 SMALL_BUCKETS = (3072, 4096, 5120, 6144, 8192, 12288, 16384, 24576)  # BSDC_SMALL_BUCKETS classes
-SMALL_ARENA_CAP = 24576
+SMALL_ARENA_CAP = int(os.environ.get("BSDC_SMALL_CAP", "24576"))  # (BSDC_SMALL_CAP: profiling A/B)
 LDS_TABLES = 1024 + 1024 + 384 + 2048 + 192  # kTabBytes (csrc/bsdc_kernels.hip)
 # large families run one per 256-thread workgroup, in buckets of these LDS arena sizes; the last
 # bucket (anything larger) keeps its arenas in HBM scratch
