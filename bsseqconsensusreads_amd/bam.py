@@ -30,7 +30,7 @@ from . import records as R
 
 IO_LIB_PATH = os.environ.get("BSDC_IO_LIB_PATH") or os.path.join(os.path.dirname(os.path.abspath(__file__)),
                                                                  "libbsdc_io.so")
-BSDC_IO_ABI_VERSION = 10
+BSDC_IO_ABI_VERSION = 11
 _P = C.c_void_p
 
 
@@ -141,6 +141,20 @@ def _load():
     lib.bsdc_bam_stream_open_range.restype = C.c_int32
     lib.bsdc_bam_stream_set_owner.argtypes = [_P, C.c_int32, _P, C.c_int32, C.c_int64, C.c_int32]
     lib.bsdc_bam_stream_set_owner.restype = C.c_int32
+    lib.bsdc_bam_stream_spill.argtypes = [_P, _P]
+    lib.bsdc_bam_stream_spill.restype = C.c_int64
+    lib.bsdc_bam_stream_chunk_contig.argtypes = [_P]
+    lib.bsdc_bam_stream_chunk_contig.restype = C.c_int64
+    lib.bsdc_bam_writer_flush.argtypes = [_P, C.c_int32]
+    lib.bsdc_bam_writer_flush.restype = C.c_int32
+    lib.bsdc_bam_writer_tell.argtypes = [_P]
+    lib.bsdc_bam_writer_tell.restype = C.c_int64
+    lib.bsdc_bam_writer_raw.argtypes = [_P, _P, C.c_int64, C.c_int32]
+    lib.bsdc_bam_writer_raw.restype = C.c_int32
+    lib.bsdc_fastq_writer_flush.argtypes = [_P, C.c_int32]
+    lib.bsdc_fastq_writer_flush.restype = C.c_int32
+    lib.bsdc_fastq_writer_tell.argtypes = [_P, _P]
+    lib.bsdc_fastq_writer_tell.restype = None
     lib.bsdc_bam_stream_range_stats.argtypes = [_P, _P]
     lib.bsdc_bam_stream_range_stats.restype = None
     lib.bsdc_bam_writer_fragment.argtypes = [_P, C.c_int32]
@@ -381,6 +395,19 @@ def find_cut(path: str, start: int, threads: int = 0, min_span: Optional[int] = 
             "coord": int(out[6]), "slack": int(slack)}
 
 
+OWN_STOP_FOREIGN, OWN_SPILL_CROSS, OWN_CONTIG_CHUNKS = 1, 2, 4  # include/bsdc_io.h BSDC_OWN_*
+
+
+def _stream_spill(lib, st) -> bytes:
+    """The stream's spilled raw records since the last call (bsdc_bam_stream_spill)."""
+    n = int(lib.bsdc_bam_stream_spill(st, None))
+    if n == 0:
+        return b""
+    buf = np.empty(n, np.uint8)
+    lib.bsdc_bam_stream_spill(st, _ptr(buf))
+    return buf.tobytes()
+
+
 def stream_chunks(path: str, threads: int = 0, chunk_bytes: int = DEFAULT_CHUNK_BYTES, slack: int = DEFAULT_SLACK,
                   read_size: int = 8 << 20, runs: bool = False, rng=None, stats: Optional[dict] = None, owner=None):
     """The chunks of a coordinate-sorted BAM in bounded memory, undecoded (StreamChunk): cut where no
@@ -391,9 +418,12 @@ def stream_chunks(path: str, threads: int = 0, chunk_bytes: int = DEFAULT_CHUNK_
     end block, offset in it) -- the records of that range only (start block -1: from the first
     record, end block -1: to the end; bsdc_bam_stream_open_range); `stats` then receives the range
     statistics (bsdc_bam_stream_range_stats: n, c0, dropped, foreign) once the stream is exhausted.
-    owner: (rank, boundaries[, stop]) -- keep the records whose key lies in the rank's interval
-    between the boundaries (find_cut dicts; bsdc_bam_stream_set_owner); stop: a foreign record
-    raises OSError("... foreign record ...")."""
+    owner: (rank, boundaries[, flags]) -- keep the records whose key lies in the rank's interval
+    between the boundaries (find_cut dicts; bsdc_bam_stream_set_owner); flags (OWN_*):
+    OWN_STOP_FOREIGN -- a foreign record raises OSError("... foreign record ..."); OWN_SPILL_CROSS
+    -- cross-key records of the core range are spilled: each chunk's `spill` bytes (raw records),
+    the rest in stats["spill_tail"]; OWN_CONTIG_CHUNKS -- each chunk's families share one key
+    contig, its `contig`."""
     lib = _load()
     st = _P()
     if rng is None:
@@ -406,11 +436,11 @@ def stream_chunks(path: str, threads: int = 0, chunk_bytes: int = DEFAULT_CHUNK_
     try:
         if owner is not None:
             rank, cuts = owner[:2]
-            stop = len(owner) > 2 and bool(owner[2])
+            flags = int(owner[2]) if len(owner) > 2 else 0  # OWN_* (True: OWN_STOP_FOREIGN)
             bd = np.array([[c["key"][0], c["key"][1], c["coord"]] for c in cuts], np.int64).reshape(-1)
             wsl = min(c["slack"] for c in cuts) if cuts else 0  # (the windows' own margin)
             if lib.bsdc_bam_stream_set_owner(st, int(rank), _ptr(bd) if len(bd) else None, len(cuts), int(wsl),
-                                             int(stop)) != 0:
+                                             flags) != 0:
                 raise OSError("%s: %s" % (path, lib.bsdc_io_last_error().decode()))
         while True:
             h = _P()
@@ -422,11 +452,15 @@ def stream_chunks(path: str, threads: int = 0, chunk_bytes: int = DEFAULT_CHUNK_
                 raise OSError("%s: %s" % (path, lib.bsdc_io_last_error().decode()))
             if not h:
                 if stats is not None:
-                    v = np.zeros(4, np.int64)
+                    v = np.zeros(5, np.int64)
                     lib.bsdc_bam_stream_range_stats(st, _ptr(v))
-                    stats.update(n=int(v[0]), c0=int(v[1]), dropped=int(v[2]), foreign=int(v[3]))
+                    stats.update(n=int(v[0]), c0=int(v[1]), dropped=int(v[2]), foreign=int(v[3]), spilled=int(v[4]),
+                                 spill_tail=_stream_spill(lib, st))
                 return
-            yield StreamChunk(lib, st, h, path)
+            ch = StreamChunk(lib, st, h, path)
+            ch.contig = int(lib.bsdc_bam_stream_chunk_contig(st))
+            ch.spill = _stream_spill(lib, st)
+            yield ch
     finally:
         lib.bsdc_bam_stream_close(st)
 
@@ -862,6 +896,21 @@ class BamWriter:
             self.gpu.submit(job[2], nblk)
             self.pending = job
 
+    def flush(self, threads: int = 0) -> int:
+        """Everything added so far written as whole BGZF blocks; -> the file's length, a point
+        where it may be cut (ranks.py splices other pieces in there)."""
+        self._drain(threads)
+        if self.lib.bsdc_bam_writer_flush(self.h, int(threads)) != 0:
+            raise self._err()
+        return int(self.lib.bsdc_bam_writer_tell(self.h))
+
+    def add_raw(self, data: bytes, threads: int = 0):
+        """Raw BAM records (block_size-prefixed), as a stream chunk holds them (host deflate)."""
+        if data:
+            buf = np.frombuffer(data, np.uint8)
+            if self.lib.bsdc_bam_writer_raw(self.h, _ptr(buf), buf.shape[0], int(threads)) != 0:
+                raise self._err()
+
     def close(self, threads: int = 0):
         if self.h:
             try:
@@ -946,6 +995,15 @@ class FastqWriter:
         if job is not None:
             self.gpu.submit(job[2], nb[0] + nb[1])
             self.pending = job
+
+    def flush(self, threads: int = 0):
+        """Everything added so far written as whole BGZF blocks; -> (length of file 1, of file 2)."""
+        self._drain(threads)
+        if self.lib.bsdc_fastq_writer_flush(self.h, int(threads)) != 0:
+            raise self._err()
+        out = np.zeros(2, np.int64)
+        self.lib.bsdc_fastq_writer_tell(self.h, _ptr(out))
+        return int(out[0]), int(out[1])
 
     def close(self, threads: int = 0):
         if self.h:
@@ -1196,7 +1254,8 @@ def _stream_step(in_bam: str, fasta: Optional[str], out_bam: Optional[str], engi
                  threads: int, level: int, fastq: Optional[Tuple[str, str]], tags: bool, chunk_bytes: int, slack: int,
                  batch_bases: Optional[int], stats: Optional[dict], gpu_bgzf: bool,
                  molecular: Optional[int], rng=None, fragment: Optional[str] = None, runner=None,
-                 range_stats: Optional[dict] = None, owner=None) -> dict:
+                 range_stats: Optional[dict] = None, owner=None, spill: Optional[str] = None,
+                 marks: Optional[list] = None) -> dict:
     """step5 (molecular None) or step 1 (molecular = its --min-consensus-base-quality) in bounded
     memory, pipelined: a decoder thread cuts the next chunk of the
     coordinate-sorted input (stream_bam: inflate, split where no template or MI family straddles),
@@ -1212,7 +1271,10 @@ def _stream_step(in_bam: str, fasta: Optional[str], out_bam: Optional[str], engi
     rank-parallel use (ranks.py): rng = the record range of the input to run (stream_chunks),
     range_stats its statistics once read, fragment = "first" / "next" (the output pieces a rank
     writes: BamWriter, FastqWriter), runner = a fleet-style runner (run_batch / run_chunk; the CPU
-    stand-in of the tests) instead of an Engine."""
+    stand-in of the tests) instead of an Engine, owner = the rank's key interval (stream_chunks),
+    spill = a file for the records the stream spills (raw, headerless BGZF), marks = a list that
+    receives, after each chunk's output is written and flushed, (BAM length, FASTQ lengths x 2,
+    the chunk's key contig): where ranks.py may splice other pieces in."""
     import queue
     import threading
     import time
@@ -1242,21 +1304,31 @@ def _stream_step(in_bam: str, fasta: Optional[str], out_bam: Optional[str], engi
 
     def decoder():  # cuts the next chunk (inflate, split, family-complete selection) while the
         # reader thread parses the one before
-        it = None
+        it = sw = None
+        rs = range_stats if range_stats is not None else ({} if spill is not None else None)
         try:
+            if spill is not None:  # (headerless: ranks.py prefixes the header)
+                sw = BamWriter(spill, first["header"], level, None, "next")
             it = stream_chunks(in_bam, threads, chunk_bytes, slack, runs=molecular is not None, rng=rng,
-                               stats=range_stats, owner=owner)
+                               stats=rs, owner=owner)
             while not stop.is_set():
                 t0 = time.perf_counter()
                 nxt = next(it, None)
                 T["decode"] += time.perf_counter() - t0
                 if nxt is None:
                     break
+                if sw is not None:
+                    sw.add_raw(nxt.spill, threads)
                 raws.put(nxt)
+            if sw is not None and not stop.is_set():
+                sw.add_raw(rs.pop("spill_tail", b""), threads)
+                sw.close(threads)
+                sw = None
         except BaseException as e:  # noqa: BLE001 -- handed to the main thread
             err.append(e)
             stop.set()
         finally:
+            close_quietly(sw)
             if it is not None:
                 it.close()  # (the stream is freed once every chunk is back)
             raws.put(None)
@@ -1273,6 +1345,7 @@ def _stream_step(in_bam: str, fasta: Optional[str], out_bam: Optional[str], engi
                     ch.discard()
                     continue  # drain to the decoder's None without parsing
                 raw = ch.decode(threads, R_, bufs)[1]
+                raw._chunk_contig = getattr(ch, "contig", -1)  # (marks: the writer's cut points)
                 parsed.put(raw)
         except BaseException as e:  # noqa: BLE001 -- handed to the main thread
             err.append(e)
@@ -1342,8 +1415,9 @@ def _stream_step(in_bam: str, fasta: Optional[str], out_bam: Optional[str], engi
                 recs = duplex_records(cons, raw, first["prefix"], threads, molecular=molecular is not None, pool=bufs)
                 T["records"] += time.perf_counter() - t0
                 back = [raw._pool_buf, getattr(recs.aux2, "_pool_buf", None)]
+                contig = getattr(raw, "_chunk_contig", -1)
                 del item, cons, raw
-                recq.put((recs, back))
+                recq.put((recs, back, contig))
         except BaseException as e:  # noqa: BLE001
             err.append(e)
             stop.set()
@@ -1359,16 +1433,22 @@ def _stream_step(in_bam: str, fasta: Optional[str], out_bam: Optional[str], engi
             gzf = GpuBgzf(eng.device) if gpu_bgzf and fastq is not None else None  # (one job in flight each)
             w = BamWriter(out_bam, output_header(first["header"]), level, gz, fragment) if out_bam is not None else None
             fq = FastqWriter(fastq[0], fastq[1], level, gzf, fragment is not None) if fastq is not None else None
+            if marks is not None:  # (the header, if any, is a piece of its own: key contig -1)
+                marks.append((w.flush(threads) if w is not None else 0, 0, 0, -1))
             while True:
                 item = recq.get()
                 if item is None:
                     break
-                recs, back = item
+                recs, back, contig = item
                 t1 = time.perf_counter()
                 if w is not None:
                     w.add(recs, threads)
                 if fq is not None:
                     fq.add(recs, threads)
+                if marks is not None:  # a cut point after each chunk (ranks.py)
+                    bo = w.flush(threads) if w is not None else 0
+                    fo = fq.flush(threads) if fq is not None else (0, 0)
+                    marks.append((bo, fo[0], fo[1], contig))
                 info["records_out"] += recs.n
                 T["encode"] += time.perf_counter() - t1
                 del item, recs

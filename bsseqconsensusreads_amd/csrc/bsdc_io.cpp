@@ -721,7 +721,11 @@ struct bsdc_bam_stream {
     std::vector<int64_t> own_coord;
     int64_t own_slack = 0;
     bool own_stop = false;
-    int64_t st_dropped = 0, st_foreign = 0;
+    bool own_spill = false;          // cross-key records of the core range go to `spill`, not the stream
+    bool own_contig_chunks = false;  // no chunk holds families of two key contigs
+    Bytes spill;                     // (bsdc_bam_stream_spill) raw records, file order
+    int64_t last_contig = -1;        // the key contig of the last chunk
+    int64_t st_dropped = 0, st_foreign = 0, st_spilled = 0;
     // statistics of the records split so far: count, first coordinate, max reach, key bounds
     int64_t st_n = 0, st_c0 = 0;
 };
@@ -841,7 +845,19 @@ void bsdc_bam_stream_range_stats(const bsdc_bam_stream *s, int64_t *st) {
     st[1] = s->st_c0;
     st[2] = s->st_dropped;
     st[3] = s->st_foreign;
+    st[4] = s->st_spilled;
 }
+
+int64_t bsdc_bam_stream_spill(bsdc_bam_stream *s, uint8_t *dst) {
+    const int64_t n = (int64_t)s->spill.size();
+    if (dst) {
+        if (n) memcpy(dst, s->spill.data(), (size_t)n);
+        s->spill.clear();
+    }
+    return n;
+}
+
+int64_t bsdc_bam_stream_chunk_contig(const bsdc_bam_stream *s) { return s->last_contig; }
 
 namespace {
 // A record starts at d[p] (dn bytes follow the stream start d): its length fields, names and
@@ -1092,7 +1108,7 @@ int32_t bsdc_bam_find_cut(const char *path, int32_t n_threads, int64_t from, int
 // key lies in [bounds[rank - 1], bounds[rank]); a dropped record another rank cannot see (its
 // coordinate outside that rank's window) is counted as foreign.
 int32_t bsdc_bam_stream_set_owner(bsdc_bam_stream *s, int32_t rank, const int64_t *bounds, int32_t n_bounds,
-                                  int64_t slack, int32_t stop_on_foreign) {
+                                  int64_t slack, int32_t flags) {
     if (!s || rank < 0 || rank > n_bounds || n_bounds < 0) return fail(BSDC_IO_EFORMAT, "bad rank");
     s->own_rank = rank;
     s->own_bounds.clear();
@@ -1100,7 +1116,9 @@ int32_t bsdc_bam_stream_set_owner(bsdc_bam_stream *s, int32_t rank, const int64_
     s->own_coord.clear();
     for (int32_t i = 0; i < n_bounds; i++) s->own_coord.push_back(bounds[3 * i + 2]);
     s->own_slack = slack;
-    s->own_stop = stop_on_foreign != 0;
+    s->own_stop = (flags & BSDC_OWN_STOP_FOREIGN) != 0;
+    s->own_spill = (flags & BSDC_OWN_SPILL_CROSS) != 0;
+    s->own_contig_chunks = (flags & BSDC_OWN_CONTIG_CHUNKS) != 0;
     return 0;
 }
 
@@ -1195,8 +1213,24 @@ int32_t stream_split(bsdc_bam_stream *s) {
     if (s->own_rank >= 0 && nr > 0) {  // a rank: the records of its key interval only
         drop.assign((size_t)nr, 0);
         const auto &bd = s->own_bounds;
+        // this rank's core coordinates (its own share of the file: cross-key records it spills)
+        const int64_t core_lo = s->own_rank == 0 ? INT64_MIN : s->own_coord[(size_t)s->own_rank - 1];
+        const int64_t core_hi = s->own_rank == (int)bd.size() ? INT64_MAX : s->own_coord[(size_t)s->own_rank];
         for (int64_t k = 0; k < nr; k++) {
             const Parsed &q = P[(size_t)k];
+            if (s->own_spill && (q.key.first >> 32) != (q.key.first & 0xFFFFFFFFll)) {
+                // a template with its mate on another contig or unmapped: its key sorts at its
+                // contig's end, its records lie anywhere; phase 2 forms its family (ranks.py)
+                drop[(size_t)k] = 1;
+                if (q.c >= core_lo && q.c < core_hi) {
+                    const uint8_t *r = d + starts[(size_t)k];
+                    s->spill.insert(s->spill.end(), r, r + 4 + rd32(r));
+                    s->st_spilled++;
+                } else {
+                    s->st_dropped++;
+                }
+                continue;
+            }
             const int owner = (int)(std::upper_bound(bd.begin(), bd.end(), q.key) - bd.begin());
             if (owner == s->own_rank) continue;
             drop[(size_t)k] = 1;
@@ -1465,7 +1499,8 @@ int32_t bsdc_bam_stream_next_raw(bsdc_bam_stream *s, int64_t min_bytes, int64_t 
             continue;
         }
         take.assign(s->fams.size(), 0);
-        int64_t bytes = 0;
+        int64_t bytes = 0, contig = -1;
+        bool forced = false;  // a rank's chunk cut at a key-contig change, whatever its size
         if (end) {  // every family is complete and nothing is left to read
             for (size_t m = 0; m < s->fams.size(); m++) take[m] = s->fams[m].n > 0;
         } else if (s->cursor != INT64_MIN) {
@@ -1507,18 +1542,25 @@ int32_t bsdc_bam_stream_next_raw(bsdc_bam_stream *s, int64_t min_bytes, int64_t 
             std::sort(ord.begin(), ord.end(), [&](int32_t a, int32_t b) { return s->fams[(size_t)a].klo < s->fams[(size_t)b].klo; });
             TcKey reach{INT64_MIN, INT64_MIN};
             size_t i = 0;
+            const int64_t kc0 = ord.empty() ? -1 : (s->fams[(size_t)ord[0]].klo.first >> 32);
             for (; i < ord.size(); i++) {
                 const StreamFam &F = s->fams[(size_t)ord[i]];
                 if (bytes > 0 && bytes >= min_bytes && reach < TcKey{F.klo.first, F.klo.second - 2 * kKeyDelta}) break;
+                if (s->own_contig_chunks && (F.klo.first >> 32) != kc0) {  // (a rank: one key contig a chunk)
+                    forced = bytes > 0;
+                    break;
+                }
                 bytes += fb[(size_t)ord[i]];
                 reach = std::max(reach, F.khi);
             }
             for (; i < ord.size(); i++) take[(size_t)ord[i]] = 0;
+            contig = kc0;
         }
         s->prof[2] += now_s() - t0;
         t0 = now_s();
-        if (end || (bytes > 0 && bytes >= min_bytes)) {
+        if (end || forced || (bytes > 0 && bytes >= min_bytes)) {
             if (bytes == 0) return 0;  // the end of the stream
+            s->last_contig = contig;
             auto *b = new bsdc_bam();
             b->header = s->hdr.header;
             b->ref_names = s->hdr.ref_names;
@@ -2128,6 +2170,29 @@ extern "C" int32_t bsdc_bam_writer_close(bsdc_bam_writer *w, int32_t n_threads) 
     return rc;
 }
 
+// Everything added so far leaves as BGZF blocks (the last one short), so the file can be cut here.
+extern "C" int32_t bsdc_bam_writer_flush(bsdc_bam_writer *w, int32_t n_threads) {
+    set_threads(n_threads);
+    const int32_t rc = deflate_write(w->f, w->tail.data(), (int64_t)w->tail.size(), w->level);
+    w->tail.clear();
+    return rc;
+}
+
+extern "C" int64_t bsdc_bam_writer_tell(bsdc_bam_writer *w) { return (int64_t)ftello(w->f); }
+
+// Raw BAM records (block_size-prefixed, as a stream chunk holds them) appended as they are.
+extern "C" int32_t bsdc_bam_writer_raw(bsdc_bam_writer *w, const uint8_t *data, int64_t n, int32_t n_threads) {
+    set_threads(n_threads);
+    w->tail.insert(w->tail.end(), data, data + n);
+    const int64_t whole = ((int64_t)w->tail.size() / kBlock) * kBlock;
+    if (whole > 0) {
+        const int32_t rc = deflate_write(w->f, w->tail.data(), whole, w->level);
+        if (rc != 0) return rc;
+        w->tail.erase(w->tail.begin(), w->tail.begin() + whole);
+    }
+    return 0;
+}
+
 // A writer of one piece of a BAM whose pieces are concatenated later: header or not (keep_header:
 // the first piece), no EOF block at the close (the assembler appends one).
 extern "C" int32_t bsdc_bam_writer_fragment(bsdc_bam_writer *w, int32_t keep_header) {
@@ -2567,6 +2632,20 @@ extern "C" int32_t bsdc_fastq_writer_fragment(bsdc_fastq_writer *w) {
     if (!w) return fail(BSDC_IO_EFORMAT, "no writer");
     w->no_eof = true;
     return 0;
+}
+
+extern "C" int32_t bsdc_fastq_writer_flush(bsdc_fastq_writer *w, int32_t n_threads) {
+    set_threads(n_threads);
+    for (int d = 0; d < 2; d++) {
+        const int32_t rc = deflate_write(w->f[d], w->tail[d].data(), (int64_t)w->tail[d].size(), w->level);
+        w->tail[d].clear();
+        if (rc != 0) return rc;
+    }
+    return 0;
+}
+
+extern "C" void bsdc_fastq_writer_tell(bsdc_fastq_writer *w, int64_t *out) {
+    for (int d = 0; d < 2; d++) out[d] = (int64_t)ftello(w->f[d]);
 }
 
 // Packed byte tables (entry r of a table = buf[off[r], off[r + 1])): per entry, the concatenation

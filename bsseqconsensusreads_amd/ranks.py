@@ -36,6 +36,7 @@ their counts at the end.
 from __future__ import annotations
 
 import os
+import shutil
 import time
 import traceback
 from typing import List, Optional, Sequence, Tuple
@@ -78,17 +79,20 @@ def _run_job(r: int, eng, runner, job: dict) -> tuple:
     from . import bam
     st, rs = {}, {}
     t0 = time.perf_counter()
+    marks = [] if job["cuts"] else None
     try:
         info = bam._stream_step(job["in_bam"], job["fasta"], job["out_bam"], eng, job["prefix"], job["threads"],
                                 job["level"], job["fastq"], job["tags"], job["chunk_bytes"], job["slack"],
                                 job["batch_bases"], st, job["gpu_bgzf"] and runner is None, None, rng=job["rng"],
-                                fragment="first" if r == 0 else "next", runner=runner, range_stats=rs,
-                                owner=(r, job["cuts"], True) if job["cuts"] else None)
+                                fragment=job["fragment"], runner=runner, range_stats=rs,
+                                owner=(r, job["cuts"], job["flags"]) if job["cuts"] else None, spill=job["spill"],
+                                marks=marks)
     except OSError as e:
         if "foreign record" in str(e):
             return ("foreign", r, str(e))
         raise
     info["seconds"] = round(time.perf_counter() - t0, 4)
+    info["marks"] = marks
     return ("done", r, info, st, rs)
 
 
@@ -208,6 +212,47 @@ def _concat(dst: str, parts: Sequence[str]):
         out.write(EOF_BLOCK)
 
 
+def _pieces(results, frags, phase2, fr2) -> list:
+    """Every rank output's pieces between its cut points (the marks _stream_step records after the
+    header and after each chunk), as (key contig, phase, rank, index, paths, starts, ends), in
+    output order: each contig's same-contig families (phase 1, ranks in key order), then its
+    cross-key families (phase 2, the owner of the contig's end)."""
+    out = []
+    for phase, (res, fr) in enumerate(((results, frags), (phase2, fr2))):
+        for r, (inf, _, _) in enumerate(res):
+            f = fr[r]
+            ps = [f["bam"], f["fq"][0] if f["fq"] else None, f["fq"][1] if f["fq"] else None]
+            prev = [0, 0, 0]
+            for i, m in enumerate(inf.get("marks") or []):
+                end = [m[0], m[1], m[2]]
+                out.append((m[3], phase, r, i, ps, list(prev), end))
+                prev = end
+            size = [os.path.getsize(p) if p else 0 for p in ps]
+            if any(size[k] > prev[k] for k in range(3)):  # (the last mark follows the last chunk)
+                raise RuntimeError("rank %d phase %d: bytes after its last cut point" % (r, phase + 1))
+    out.sort(key=lambda x: (x[0], x[1], x[2], x[3]))
+    return out
+
+
+def _assemble(dst: str, pieces, k: int):
+    """Output file k (0 the BAM, 1 / 2 the FASTQ pair) from its pieces in order, then one EOF block."""
+    with open(dst, "wb") as out:
+        for p in pieces:
+            path, a, b = p[4][k], p[5][k], p[6][k]
+            if path is None or b <= a:
+                continue
+            with open(path, "rb") as f:
+                f.seek(a)
+                left = b - a
+                while left > 0:
+                    buf = f.read(min(left, 1 << 24))
+                    if not buf:
+                        raise RuntimeError("%s: short piece" % path)
+                    out.write(buf)
+                    left -= len(buf)
+        out.write(EOF_BLOCK)
+
+
 def step5_ranks(in_bam: str, fasta: str, out_bam: Optional[str], devices: Sequence[int], prefix: Optional[str] = None,
                 threads: int = 0, level: int = 6, fastq: Optional[Tuple[str, str]] = None, tags: bool = True,
                 chunk_bytes: Optional[int] = None, slack: Optional[int] = None, batch_bases: Optional[int] = None,
@@ -231,24 +276,34 @@ def step5_ranks(in_bam: str, fasta: str, out_bam: Optional[str], devices: Sequen
     hdr = bam.read_bam_header(in_bam)
     pre = bam.read_name_prefix(hdr) if prefix is None else prefix
 
-    def run(cuts, pl: RankPool):
-        ranges = windows_of(cuts)
+    tmpdir = os.path.dirname(os.path.abspath(out_bam if out_bam is not None else fastq[0]))
+
+    def paths(tag, n, spill):
+        return [dict(bam=os.path.join(tmpdir, ".%s.%d.bam" % (tag, r)) if out_bam is not None else None,
+                     fq=(os.path.join(tmpdir, ".%s.%d.r1.fq.gz" % (tag, r)), os.path.join(tmpdir, ".%s.%d.r2.fq.gz" % (tag, r)))
+                     if fastq is not None else None,
+                     spill=os.path.join(tmpdir, ".%s.%d.spill" % (tag, r)) if spill else None) for r in range(n)]
+
+    def remove(fr):
+        for f in fr:
+            for path in ([f["bam"]] if f["bam"] else []) + (list(f["fq"]) if f["fq"] else []) + \
+                    ([f["spill"]] if f["spill"] else []):
+                if os.path.exists(path):
+                    os.unlink(path)
+
+    def run(cuts, pl: "RankPool", in_path: str, ranges, tag: str, phase: int):
         n = len(ranges)
-        tmpdir = os.path.dirname(os.path.abspath(out_bam if out_bam is not None else fastq[0]))
-        tag = "%s.rank%d" % (os.getpid(), id(ranges) & 0xFFFF)
-        frags = [(os.path.join(tmpdir, ".%s.%d.bam" % (tag, r)) if out_bam is not None else None,
-                  (os.path.join(tmpdir, ".%s.%d.r1.fq.gz" % (tag, r)), os.path.join(tmpdir, ".%s.%d.r2.fq.gz" % (tag, r)))
-                  if fastq is not None else None) for r in range(n)]
-        jobs = [dict(in_bam=in_bam, fasta=fasta, out_bam=frags[r][0], prefix=pre, threads=threads, level=level,
-                     fastq=frags[r][1], tags=tags, chunk_bytes=chunk_bytes, slack=slack, batch_bases=batch_bases,
-                     gpu_bgzf=gpu_bgzf, rng=ranges[r], cuts=cuts) for r in range(n)]
+        fr = paths(tag, n, phase == 0 and len(cuts) > 0)
+        flags = (bam.OWN_STOP_FOREIGN | bam.OWN_SPILL_CROSS | bam.OWN_CONTIG_CHUNKS) if phase == 0 else \
+            bam.OWN_CONTIG_CHUNKS
+        jobs = [dict(in_bam=in_path, fasta=fasta, out_bam=fr[r]["bam"], prefix=pre, threads=threads, level=level,
+                     fastq=fr[r]["fq"], tags=tags, chunk_bytes=chunk_bytes, slack=slack, batch_bases=batch_bases,
+                     gpu_bgzf=gpu_bgzf, rng=ranges[r], cuts=cuts, flags=flags, spill=fr[r]["spill"],
+                     fragment="first" if (r == 0 and phase == 0) else "next") for r in range(n)]
         try:
-            return pl.run(jobs), frags, ranges
+            return pl.run(jobs), fr
         except BaseException:
-            for f in frags:  # (every rank has answered: none still writes)
-                for path in ([f[0]] if f[0] else []) + (list(f[1]) if f[1] else []):
-                    if os.path.exists(path):
-                        os.unlink(path)
+            remove(fr)  # (every rank has answered: none still writes)
             raise
 
     own = pool is None
@@ -260,45 +315,71 @@ def step5_ranks(in_bam: str, fasta: str, out_bam: Optional[str], devices: Sequen
         t_pool = 0.0
         if pool.n < len(cuts) + 1:
             raise ValueError("a pool of %d ranks for %d ranges" % (pool.n, len(cuts) + 1))
+    tag = "%s.rank%d" % (os.getpid(), int(time.time() * 1000) & 0xFFFFFF)
+    frags, phase2, fr2, spill_bam = [], [], [], None
     try:
         t1 = time.perf_counter()
         foreign = 0
         try:
-            results, frags, ranges = run(cuts, pool)
+            ranges = windows_of(cuts)
+            results, frags = run(cuts, pool, in_bam, ranges, tag, 0)
         except ForeignRecords:  # (no fragments are left)
             if on_foreign == "raise" or not cuts:
                 raise
             foreign = 1
-            results, frags, ranges = run([], pool)
+            cuts, ranges = [], windows_of([])
+            results, frags = run(cuts, pool, in_bam, ranges, tag, 0)
         t2 = time.perf_counter()
+        # phase 2: the templates with a mate on another contig or unmapped, spilled by every rank
+        # from its core share, formed into families by the owners of their keys (the rank whose
+        # interval holds their contig's end), on one BAM of all the spills
+        n_cross = sum(int(x[2].get("spilled", 0)) for x in results)
+        if cuts and n_cross:
+            spill_bam = os.path.join(tmpdir, ".%s.spill.bam" % tag)
+            hw = bam.BamWriter(spill_bam + ".h", hdr, level, None, "first")
+            hw.close(threads)
+            with open(spill_bam, "wb") as out:
+                for part in [spill_bam + ".h"] + [f["spill"] for f in frags]:
+                    with open(part, "rb") as f:
+                        shutil.copyfileobj(f, out, 1 << 24)
+                out.write(EOF_BLOCK)
+            os.unlink(spill_bam + ".h")
+            phase2, fr2 = run(cuts, pool, spill_bam, [None] * len(ranges), tag + "x", 1)
+        t2b = time.perf_counter()
+        if not cuts:  # one range: its fragments as they are
+            if out_bam is not None:
+                _concat(out_bam, [frags[0]["bam"]])
+            if fastq is not None:
+                for d in range(2):
+                    _concat(fastq[d], [frags[0]["fq"][d]])
+        else:
+            pieces = _pieces(results, frags, phase2, fr2)
+            if out_bam is not None:
+                _assemble(out_bam, pieces, 0)
+            if fastq is not None:
+                for d in range(2):
+                    _assemble(fastq[d], pieces, 1 + d)
+        t3 = time.perf_counter()
     except BaseException:
         if own:
             pool.close(terminate=True)
             own = False
         raise
     finally:
+        remove(frags)
+        remove(fr2)
+        if spill_bam is not None and os.path.exists(spill_bam):
+            os.unlink(spill_bam)
         if own:
             pool.close()
-    try:
-        if out_bam is not None:
-            _concat(out_bam, [f[0] for f in frags])
-        if fastq is not None:
-            for d in range(2):
-                _concat(fastq[d], [f[1][d] for f in frags])
-    finally:
-        for f in frags:
-            for path in ([f[0]] if f[0] else []) + (list(f[1]) if f[1] else []):
-                if os.path.exists(path):
-                    os.unlink(path)
-    t3 = time.perf_counter()
-    info = {"ranks": len(ranges), "cuts_fallback": foreign > 0, "records_in": 0, "families": 0, "families_emitted": 0,
-            "records_out": 0}
-    for r, (inf, st, rs) in enumerate(results):
+    info = {"ranks": len(ranges), "cuts_fallback": foreign > 0, "cross_records": n_cross, "records_in": 0,
+            "families": 0, "families_emitted": 0, "records_out": 0}
+    for inf, st, rs in list(results) + list(phase2):
         for k in ("records_in", "families", "families_emitted", "records_out"):
             info[k] += int(inf.get(k, 0))
     if stats is not None:
         stats.update(cut_s=round(t_cut, 4), pool_start_s=round(t_pool, 4), ranks_s=round(t2 - t1, 4),
-                     assemble_s=round(t3 - t2, 4),
+                     cross_s=round(t2b - t2, 4), assemble_s=round(t3 - t2b, 4),
                      rank_records=[int(x[0].get("records_in", 0)) for x in results],
                      rank_read=[int(x[2].get("n", 0)) for x in results],
                      rank_seconds=[x[0].get("seconds") for x in results], ranges=ranges)

@@ -17,7 +17,7 @@
 extern "C" {
 #endif
 
-#define BSDC_IO_ABI_VERSION 10
+#define BSDC_IO_ABI_VERSION 11
 #define BSDC_IO_EFORMAT (-10) /* not BGZF/BAM, truncated, bad CRC */
 #define BSDC_IO_EIO (-11)     /* open/read/write failed */
 #define BSDC_IO_EINVAL (-22)  /* bad argument */
@@ -131,15 +131,28 @@ int32_t bsdc_bam_stream_next_runs(bsdc_bam_stream *s, int64_t min_bytes, bsdc_ba
  * key second, coordinate} (find_cut's out[4..6]), and count as foreign the dropped records whose
  * coordinate lies outside their owner's window [its lower coordinate - slack, its upper + slack)
  * (a mate on another contig, or unmapped: the owner never reads them; ranks.py then falls back to
- * one range); stop_on_foreign: the first one fails the stream (BSDC_IO_EFORMAT, "foreign
- * record ...").  bsdc_bam_stream_range_stats: {records read, first coordinate, dropped, foreign}. */
+ * one range); flags BSDC_OWN_STOP_FOREIGN: the first one fails the stream (BSDC_IO_EFORMAT,
+ * "foreign record ..."); BSDC_OWN_SPILL_CROSS: cross-key records (below) read in the rank's core
+ * coordinates [its lower bound, its upper bound) are spilled instead of streamed, the others
+ * dropped; BSDC_OWN_CONTIG_CHUNKS: every chunk's families share one key contig, so the output can
+ * be cut between contigs.  bsdc_bam_stream_range_stats: {records read, first coordinate, dropped,
+ * foreign, spilled}. */
 int32_t bsdc_bam_find_cut(const char *path, int32_t n_threads, int64_t from, int64_t min_span, int64_t slack,
                           int64_t guard, int64_t max_bytes, int64_t *out);
 int32_t bsdc_bam_stream_open_range(const char *path, int32_t n_threads, int64_t read_size, int64_t start_block,
                                    int64_t start_off, int64_t end_block, int64_t end_off, bsdc_bam_stream **out);
+#define BSDC_OWN_STOP_FOREIGN 1   /* set_owner flags: the first foreign record fails the stream */
+#define BSDC_OWN_SPILL_CROSS 2    /* cross-key records of the core range go to bsdc_bam_stream_spill */
+#define BSDC_OWN_CONTIG_CHUNKS 4  /* no chunk holds families of two key contigs */
 int32_t bsdc_bam_stream_set_owner(bsdc_bam_stream *s, int32_t rank, const int64_t *bounds, int32_t n_bounds,
-                                  int64_t slack, int32_t stop_on_foreign);
+                                  int64_t slack, int32_t flags);
 void bsdc_bam_stream_range_stats(const bsdc_bam_stream *s, int64_t *st);
+/* (IO ABI 11) The cross-key records spilled so far (raw, block_size-prefixed, file order): returns
+ * their bytes; with dst, copies them there and forgets them.  A cross key's contig halves differ:
+ * the template's mate is on another contig or unmapped, and its key sorts at its contig's end. */
+int64_t bsdc_bam_stream_spill(bsdc_bam_stream *s, uint8_t *dst);
+/* The key contig (key first component >> 32) of the families of the last chunk (-1: none yet). */
+int64_t bsdc_bam_stream_chunk_contig(const bsdc_bam_stream *s);
 
 /* Records to write (n_rec entries; every *_off array has n_rec + 1 entries). */
 typedef struct {
@@ -188,6 +201,12 @@ int32_t bsdc_bam_writer_close(bsdc_bam_writer *w, int32_t n_threads);
 /* A writer of one piece of a BAM assembled later (ranks.py): keep_header 0 drops the header
  * encoded at the open; no EOF block at the close.  Call right after the open. */
 int32_t bsdc_bam_writer_fragment(bsdc_bam_writer *w, int32_t keep_header);
+/* (IO ABI 11) flush: everything added so far leaves as BGZF blocks (the last one short), so the
+ * file may be cut at tell() (its bytes written); raw: block_size-prefixed BAM records appended as
+ * they are (a spill file). */
+int32_t bsdc_bam_writer_flush(bsdc_bam_writer *w, int32_t n_threads);
+int64_t bsdc_bam_writer_tell(bsdc_bam_writer *w);
+int32_t bsdc_bam_writer_raw(bsdc_bam_writer *w, const uint8_t *data, int64_t n, int32_t n_threads);
 
 /* Paired FASTQ of records, as picard SamToFastq F=path1 F2=path2 writes them (the step after the
  * duplex call, main.snake.py:167-177; parity unpinned): "@name/1" or "/2", SEQ, "+", QUAL+33,
@@ -211,7 +230,9 @@ int32_t bsdc_fastq_writer_take(bsdc_fastq_writer *w, int32_t which, int64_t nblk
 int32_t bsdc_fastq_writer_put(bsdc_fastq_writer *w, int32_t which, int64_t nblk, uint8_t *packed, const int32_t *sizes,
                               const uint32_t *crc, const uint8_t *raw, int32_t n_threads);
 int32_t bsdc_fastq_writer_close(bsdc_fastq_writer *w, int32_t n_threads);
-int32_t bsdc_fastq_writer_fragment(bsdc_fastq_writer *w); /* no EOF blocks at the close */
+int32_t bsdc_fastq_writer_fragment(bsdc_fastq_writer *w);
+int32_t bsdc_fastq_writer_flush(bsdc_fastq_writer *w, int32_t n_threads);
+void bsdc_fastq_writer_tell(bsdc_fastq_writer *w, int64_t *out);  /* out[2]: bytes written per file */ /* no EOF blocks at the close */
 
 /* Packed byte tables (entry r = buf[off[r], off[r + 1])), for the output records: per entry the
  * concatenation of k parts (a table, or a constant when offs[j] is NULL: bufs[j], const_len[j]

@@ -63,7 +63,21 @@ class OracleRunner:
         return out
 
     def run_chunk(self, raw, tags: bool, batch_bases):
-        raise NotImplementedError("the stand-in runs family batches only")
+        """A chunk whose tool-2 groups straddle its families (the streaming step's two-launch
+        case): oracle/ on the whole chunk, as pipeline.run_step5's Consensus."""
+        from bsseqconsensusreads_amd.pipeline import Consensus
+        r = self._result(raw)
+        F = int(r.status.shape[0])
+        status = (r.status & 1).astype(np.uint8)
+        ss = None
+        if tags:
+            ss_len = r.ss["len"].astype(np.int32)
+            status |= np.where((ss_len[:, 0] > 0) | (ss_len[:, 1] > 0), 2, 0).astype(np.uint8)
+            status |= np.where((ss_len[:, 2] > 0) | (ss_len[:, 3] > 0), 4, 0).astype(np.uint8)
+            ss = {"len": ss_len, "base": r.ss["base"], "qual": r.ss["qual"], "depth": r.ss["depth"], "err": r.ss["err"]}
+        return Consensus(np.asarray(r.fam_mi, np.int32), status, r.cons_len.astype(np.int32).reshape(F, 2),
+                         r.cons_seq, r.cons_qual, np.asarray(r.fam_rec_off, np.int64), np.asarray(r.fam_src, np.int64),
+                         ss)
 
     def close(self):
         pass

@@ -180,3 +180,65 @@ def test_pool_runs_several_files(sorted_input, one_range):  # noqa: F811
             _run(tmp, p, fa, "poolbad", 2, cuts=[bad], on_foreign="raise", pool=pool)
         info, _, got, _ = _run(tmp, p, fa, "pool2", 2, pool=pool)
         assert got == one_range[2]
+
+
+@pytest.fixture(scope="module")
+def cross_input(tmp_path_factory):
+    """Two contigs: templates of some families with their R2 moved onto the second contig (mate on
+    another contig), families whose mates are flagged unmapped, and the rest ordinary.  Their keys
+    sort at their contig's end, wherever the records lie: every rank spills its share of them and
+    the owners of the contigs' ends form their families (phase 2)."""
+    from bsseqconsensusreads_amd import records as R
+    from bsseqconsensusreads_amd import synth
+    from test_stream import _header
+    tmp = tmp_path_factory.mktemp("cross")
+    s = synth.generate("C2", 1500, seed=11, device="cpu", genome_len=300_000)
+    raw = s.raw
+    rng = np.random.default_rng(11)
+    codes = R.unpack_nibbles(s.ref.packed, s.ref.n_nibbles)
+    c0 = R.NT16_TO_ASCII[codes[int(s.ref.contig_off[0]):int(s.ref.contig_off[0]) + int(s.ref.contig_len[0])]].tobytes()
+    c1 = bytes(rng.choice(np.frombuffer(b"ACGT", np.uint8), 40_000).tobytes())
+    names = [s.ref.names[0], "chrX2"]
+    ref = R.Reference.from_contigs(names, {names[0]: c0, names[1]: c1}, keep_letters=False)
+    fam_x = rng.random(int(raw.mi_id.max()) + 1) < 0.06   # families with mates on contig 1
+    fam_u = (rng.random(int(raw.mi_id.max()) + 1) < 0.04) & ~fam_x  # mates unmapped
+    by_name = {}
+    for k in range(raw.n):
+        by_name.setdefault(int(raw.name_id[k]), []).append(k)
+    for ks in by_name.values():
+        if len(ks) != 2 or raw.mi_id[ks[0]] < 0:
+            continue
+        i, j = (ks[0], ks[1]) if raw.flag[ks[0]] & 64 else (ks[1], ks[0])  # R1, R2
+        m = int(raw.mi_id[i])
+        if fam_x[m]:
+            P = int(rng.integers(1000, 35_000))
+            raw.tid[j], raw.pos[j] = 1, P
+            raw.next_tid[i], raw.next_pos[i] = 1, P
+            raw.next_tid[j], raw.next_pos[j] = 0, raw.pos[i]
+            raw.tlen[i] = raw.tlen[j] = 0
+        elif fam_u[m]:
+            raw.flag[i] |= 8
+            raw.flag[j] |= 8
+    raw = R.take(raw, np.lexsort((raw.pos, raw.tid)))
+    p = str(tmp / "in.bam")
+    bam.write_bam(p, _header(ref), bam.records_to_bam(raw), level=1, threads=4)
+    fa = str(tmp / "g.fa")
+    write_fasta(fa, ref)
+    return raw, p, fa, tmp
+
+
+@pytest.mark.parametrize("n", [2, 3])
+def test_cross_contig_and_unmapped_mates(cross_input, n):  # noqa: F811
+    """Mates on another contig and unmapped mates: the ranks' output equals the one-range run's
+    bytes with no fallback, the cross-key templates going through phase 2"""
+    raw, p, fa, tmp = cross_input
+    info1, _, ref_bytes, _ = _run(tmp, p, fa, "x1", 1)
+    info, st, got, _ = _run(tmp, p, fa, "x%d" % n, n)
+    assert info["ranks"] == n and not info["cuts_fallback"]
+    assert info["cross_records"] > 100
+    assert info["records_in"] == info1["records_in"] == raw.n
+    for a, b in zip(got, ref_bytes):
+        assert a == b
+    assert not [f for f in os.listdir(tmp) if f.startswith(".")], "pieces left behind"
+    if n == 3:  # (and the records are the whole file's, against oracle/)
+        assert_bam_matches_oracle(str(tmp / "x3.bam"), p, fa, "ranks, cross-contig mates") > 0
