@@ -17,8 +17,9 @@ output identical to the whole-file path (bam.step5_stream).  Other inputs are re
 step5 --gpus N on a coordinate-sorted input streams too.  --multi ranks (the default;
 ranks.step5_ranks): N spawned rank processes (one per GPU) each decode, compute and encode their
 own key interval of the file, and this process concatenates their fragments -- no front end.
-When a record's owner could not read it (a mate on another contig or unmapped) the ranks stop
-and the file runs as --multi fleet (fleet.step5_stream_multi): this process reads the BAM once
+Mates on other contigs and unmapped mates are spilled and formed in a second phase.  When a
+record's owner could not read it (an insert longer than the window slack) the ranks stop and the
+file runs as --multi fleet (fleet.step5_stream_multi): this process reads the BAM once
 and writes the outputs in order, N spawned worker processes run the family batches it deals them
 through shared memory.  Both: bounded memory, output identical to --gpus 1.  Other inputs (or a run under torch.distributed.run) take the whole-file path: one
 process per GPU, every rank forms the plan, batches dealt to the ranks, rank 0 writes

@@ -20,18 +20,26 @@ unclipped 5' end, TemplateCoordinate order) leave gaps.
    (bsdc_bam_stream_set_owner): a template's records near a boundary are read by both ranks and
    kept by one.  It writes a fragment of each output: rank 0 the header and its records, the
    others their records, none an EOF block.
-3. A rank that drops a record its owner cannot read (a mate on another contig or unmapped, whose
-   key sorts at its contig's end; an insert longer than slack) stops at once, and the parent
-   stops the others and reruns the file as one range, or raises ForeignRecords for its caller
-   to pick another path (cli.py: fleet.step5_stream_multi).  Such records would have to be sent
-   to their owner: not built.  Otherwise the parent concatenates the fragments and one BGZF EOF
-   block: ranks own disjoint key intervals in key order and no family straddles a boundary, so
-   the BAM and the FASTQ pair decompress to the one-process stream's bytes (tests/test_ranks.py);
-   only the BGZF block boundaries at the seams differ.
+3. Templates whose mate is on another contig or unmapped have keys that sort at their contig's
+   end, whatever their records' positions: no window holds them.  Every rank spills those of its
+   core share (its own coordinates, between its boundaries) to a file instead of streaming them
+   (bsdc_bam_stream_spill), and cuts its chunks so that each holds families of one key contig,
+   recording a cut point after the header and after every chunk (BamWriter / FastqWriter
+   flush + tell).  Phase 2: the parent joins the spills into one BAM, and each rank runs the
+   stream over it, keeping the keys it owns, so the owner of a contig's end forms that contig's
+   cross-key families (recording its cut points too).
+4. The parent splices the pieces in key order: per contig, the ranks' same-contig pieces in rank
+   order, then the contig's cross-key pieces, then one BGZF EOF block.  The BAM and the FASTQ pair
+   decompress to the one-process stream's bytes (tests/test_ranks.py, with mates on a second
+   contig and unmapped mates too); only the BGZF block boundaries at the seams differ.
+5. What remains is a template whose insert is longer than slack, whose far record lies outside its
+   owner's window: a rank that drops such a record stops at once.  The parent then reruns the
+   file as one range, or raises ForeignRecords for its caller to pick another path (cli.py:
+   fleet.step5_stream_multi).
 
 Every rank's memory is bounded as the one-GPU stream's (about six chunks), and each rank decodes
 about 1/N of the records plus 2 * slack positions.  No collective: the ranks exchange nothing but
-their counts at the end.
+their spill files and their counts and cut points.
 """
 from __future__ import annotations
 
