@@ -48,6 +48,9 @@ constexpr int kWave = 64;
 #define SMALL_STAGE_U 4  // k_small staging: image chunk loads in flight per lane
 #endif
 constexpr int kStageU = SMALL_STAGE_U;
+#ifndef SMALL_QDMA
+#define SMALL_QDMA 0  // k_small: 1 stages the quals with LDS-DMA (global_load_lds_dwordx4; A/B arm)
+#endif
 #ifndef SMALL_PROBE
 #define SMALL_PROBE 0  // timing probes only (wrong results): 1 no window loads, 2 no base unpack
 #endif
@@ -622,6 +625,11 @@ __device__ __forceinline__ uint32_t ldsu32(const uint8_t *p) {
     return v;
 }
 __device__ __forceinline__ void stu32(uint8_t *p, uint32_t v) { __builtin_memcpy(p, &v, 4); }
+// 16 B per lane from global memory straight into LDS at lds + 16 * lane (lds wave-uniform)
+__device__ __forceinline__ void glds16(const uint8_t *g, uint8_t *lds) {
+    __builtin_amdgcn_global_load_lds((const __attribute__((address_space(1))) void *)g,
+                                     (__attribute__((address_space(3))) void *)lds, 16, 0, 0);
+}
 __device__ __forceinline__ void st16(uint8_t *p, uint16_t v) { *reinterpret_cast<uint16_t *>(p) = v; }  // 2-aligned p
 // The LDS dword at any byte offset p of `base` (16-aligned) from two aligned loads and a byte
 // align: gfx950 LDS stalls an unaligned dword access (SQ_LDS_UNALIGNED_STALL)
@@ -949,8 +957,16 @@ __device__ __forceinline__ void small_family(const KParams &P, const Tables *T, 
         return v;
     };
     uint32_t qor = 0;  // OR of every qual byte this lane stages (0x80 set: a qual >= 128)
+#if SMALL_QDMA
+    // quals straight into LDS: one 1 KiB wave-instruction per 64 chunks, no VGPR round trip (the
+    // image is as contiguous in LDS as in HBM); the qual >= 128 test then reads them back
+    for (int u = 0; u < ((nqc + 63) >> 6); u++) {
+        const int k = t + 64 * u;
+        if (k < nqc) glds16(B.qual + base_g + 16u * (uint32_t)k, qimg + 1024 * u);
+    }
+#endif
     auto store_img = [&](int k, uint4 v) {
-        if (k < nqc) {
+        if (k < nqc && !SMALL_QDMA) {
             *reinterpret_cast<uint4 *>(qimg + 16 * k) = v;
             qor |= v.x | v.y | v.z | v.w;
         } else if (k >= nqc && k < nch) {
@@ -963,7 +979,7 @@ __device__ __forceinline__ void small_family(const KParams &P, const Tables *T, 
     // lanes take qual chunks and packed-base chunks in separate rounds (the unpack runs once per
     // round of base chunks instead of in every round where some lane has one): chunk k of round u
     // is qual chunk t + 64 u for u < uq, packed-base chunk t + 64 (u - uq) after
-    const int uq = (nqc + 63) >> 6;
+    const int uq = SMALL_QDMA ? 0 : (nqc + 63) >> 6;
     auto kmap = [&](int u) {
         if (u < uq) return t + 64 * u < nqc ? t + 64 * u : nch;
         const int kb = t + 64 * (u - uq);
@@ -1038,6 +1054,14 @@ __device__ __forceinline__ void small_family(const KParams &P, const Tables *T, 
 #pragma unroll
         for (int u = 0; u < 2; u++) store_win(k0 + t + 64 * u, wv[u]);
     }
+#if SMALL_QDMA
+    __asm__ volatile("s_waitcnt vmcnt(0)" ::: "memory");  // the DMA'd quals have landed
+    wave_sync();
+    for (int k = t; k < nqc; k += 64) {
+        const uint4 q = *reinterpret_cast<const uint4 *>(qimg + 16 * k);
+        qor |= q.x | q.y | q.z | q.w;
+    }
+#endif
     wave_sync();
     if (stop == 1) return;
 

@@ -13,6 +13,7 @@ import pytest
 
 from helpers import assert_bam_matches_oracle
 from test_gpu_fleet import _cli, cli_input  # noqa: F401 -- (the module fixture)
+from test_ranks import cross_input  # noqa: F401 -- (the module fixture)
 
 pytestmark = pytest.mark.gpu
 
@@ -38,3 +39,24 @@ def test_cli_ranks_report(cli_input):  # noqa: F811
     assert p.returncode == 0, p.stderr[-3000:]
     info = json.loads(p.stderr.strip().splitlines()[-1])
     assert info["ranks"] == 2 and not info["cuts_fallback"]
+
+
+def test_cli_ranks_cross_contig_mates(cross_input):  # noqa: F811
+    """Mates on another contig and unmapped mates on the GPU: the two ranks spill them, form them
+    in phase 2 (no fallback), and the output decompresses to the bytes of --gpus 1 and equals
+    oracle/ on the whole file"""
+    raw, inp, fa, tmp = cross_input
+    one = [gzip.decompress(b) for b in _cli(tmp, inp, fa, "x_one")]
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    env = {k: v for k, v in os.environ.items() if k not in ("WORLD_SIZE", "RANK", "LOCAL_RANK")}
+    env["PYTHONPATH"] = root + os.pathsep + env.get("PYTHONPATH", "")
+    p = subprocess.run([sys.executable, "-m", "bsseqconsensusreads_amd.cli", "step5", "--reference", fa, inp,
+                        str(tmp / "x2.bam"), "--fastq1", str(tmp / "x21.fq.gz"), "--fastq2", str(tmp / "x22.fq.gz"),
+                        "--threads", "4", "--batch-bases", "20000", "--chunk-mb", "0",
+                        "--gpus", "2", "--devices", "0,0"], env=env, capture_output=True, text=True, timeout=300)
+    assert p.returncode == 0, p.stderr[-3000:]
+    info = json.loads(p.stderr.strip().splitlines()[-1])
+    assert info["ranks"] == 2 and not info["cuts_fallback"] and info["cross_records"] > 100
+    got = [gzip.decompress((tmp / ("x2%s" % x)).read_bytes()) for x in (".bam", "1.fq.gz", "2.fq.gz")]
+    assert got == one
+    assert assert_bam_matches_oracle(str(tmp / "x2.bam"), inp, fa, "cli --gpus 2 ranks, cross-contig") > 0
