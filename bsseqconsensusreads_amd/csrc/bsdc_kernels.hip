@@ -49,7 +49,7 @@ constexpr int kWave = 64;
 #endif
 constexpr int kStageU = SMALL_STAGE_U;
 #ifndef SMALL_QDMA
-#define SMALL_QDMA 0  // k_small: 1 stages the quals with LDS-DMA (global_load_lds_dwordx4; A/B arm)
+#define SMALL_QDMA 1  // k_small stages the quals with LDS-DMA (global_load_lds_dwordx4); 0: through VGPRs
 #endif
 #ifndef SMALL_PROBE
 #define SMALL_PROBE 0  // timing probes only (wrong results): 1 no window loads, 2 no base unpack
@@ -1399,9 +1399,15 @@ __device__ __forceinline__ void small_family(const KParams &P, const Tables *T, 
         for (int e = 0; e < 2; e++) {
             const int ol = olen[e];
             const int sa = e == 0 ? 0 : 1, sb = e == 0 ? 3 : 2;
+            // the two sets' figures as wave-uniform selects, not indexed by sa / sb: e is a loop
+            // variable, and a dynamically indexed array goes to scratch (the TAGS instance's did)
+            const int cA = e == 0 ? cnt[0] : cnt[1], cB = e == 0 ? cnt[3] : cnt[2];
+            const int fA = e == 0 ? nfw[0] : nfw[1], fB = e == 0 ? nfw[3] : nfw[2];
+            const int oA = e == 0 ? off[0] : off[1], oB = e == 0 ? off[3] : off[2];
+            const bool hA = cA > 0, hB = cB > 0;
             // TAGS: the single-strand reads run to their own lengths, which can pass the duplex's
             // (min of the two); columns past a side's own length are not that side's
-            const int la = hs[sa] ? lcs[sa] : 0, lb = hs[sb] ? lcs[sb] : 0;
+            const int la = hA ? (e == 0 ? lcs[0] : lcs[1]) : 0, lb = hB ? (e == 0 ? lcs[3] : lcs[2]) : 0;
             const int lv = TAGS ? ::max(la, lb) : ol;
             for (int c0 = 0; c0 < lv; c0 += 256) {
                 const int c = c0 + 4 * t, c8 = 8 * c;
@@ -1411,8 +1417,7 @@ __device__ __forceinline__ void small_family(const KParams &P, const Tables *T, 
                 if (c < lv) {
 #pragma unroll
                     for (int side = 0; side < 2; side++) {
-                        const int s = side == 0 ? (e == 0 ? 0 : 1) : (e == 0 ? 3 : 2);
-                        const int o = off[s];
+                        const int o = side == 0 ? oA : oB;
                         // one read: its 4 columns from c (descriptor d is wave-uniform; d = 0 is a
                         // read of length 0 and adds nothing, which pads the pairs below)
                         auto fwd = [&](uint32_t d) {
@@ -1435,7 +1440,7 @@ __device__ __forceinline__ void small_family(const KParams &P, const Tables *T, 
                             if (TAGS) nr[side] += v;
                         };
                         // reads two at a time (both reads' loads in flight together), then an odd one
-                        const int nf = nfw[s], na = cnt[s];
+                        const int nf = side == 0 ? fA : fB, na = side == 0 ? cA : cB;
                         int i = 0;
                         for (; i + 1 < nf; i += 2) {
                             const uint32_t d0 = rlu(dreg, o + i), d1 = rlu(dreg, o + i + 1);
@@ -1464,7 +1469,7 @@ __device__ __forceinline__ void small_family(const KParams &P, const Tables *T, 
                 uint32_t Qp[2] = {0, 0}, negm[2] = {0, 0};
 #pragma unroll
                 for (int side = 0; side < 2; side++) {
-                    const int32_t nset = side == 0 ? cnt[sa] : cnt[sb];
+                    const int32_t nset = side == 0 ? cA : cB;
 #pragma unroll
                     for (int j = 0; j < 4; j++) {
                         const int32_t dsum = D[side][j];
@@ -1475,7 +1480,7 @@ __device__ __forceinline__ void small_family(const KParams &P, const Tables *T, 
                     }
                 }
                 uint32_t ob4, oq4, ss[4];
-                resolve4(hs[sa], hs[sb], bm[0], Qp[0], bm[1], Qp[1], qadd, ob4, oq4, ss);
+                resolve4(hA, hB, bm[0], Qp[0], bm[1], Qp[1], qadd, ob4, oq4, ss);
                 // (TAGS) the bytes of columns inside each side's own length; without TAGS every
                 // column below ol is inside both present sides
                 const uint32_t inA = TAGS ? ~bytes_past(8 * (la - c), false) : ~0u;
@@ -1483,11 +1488,11 @@ __device__ __forceinline__ void small_family(const KParams &P, const Tables *T, 
                 // slow columns: a side saw more than one base, or a negative sum.  The queued
                 // path recomputes only the slow side(s): the other side's single-strand result
                 // rides in the column's output bytes (base | 0x10 if it is side B; qual 0 = none).
-                const uint32_t slowA = hs[sa] ? (bytes_nonzero(multi[0] & 0x7F7F7F7Fu) | negm[0]) & inA : 0u;
-                const uint32_t slowB = hs[sb] ? (bytes_nonzero(multi[1] & 0x7F7F7F7Fu) | negm[1]) & inB : 0u;
+                const uint32_t slowA = hA ? (bytes_nonzero(multi[0] & 0x7F7F7F7Fu) | negm[0]) & inA : 0u;
+                const uint32_t slowB = hB ? (bytes_nonzero(multi[1] & 0x7F7F7F7Fu) | negm[1]) & inB : 0u;
                 const uint32_t slow4 = slowA | slowB;
                 if (slow4) {
-                    const uint32_t useA = hs[sa] ? ~slowA : 0u, useB = (hs[sb] ? ~slowB : 0u) & ~useA;
+                    const uint32_t useA = hA ? ~slowA : 0u, useB = (hB ? ~slowB : 0u) & ~useA;
                     const uint32_t fb = (ss[0] & useA) | ((ss[2] | 0x10101010u) & useB);
                     const uint32_t fq = (ss[1] & useA) | (ss[3] & useB);
                     ob4 = (ob4 & ~slow4) | (fb & slow4);
@@ -1512,7 +1517,7 @@ __device__ __forceinline__ void small_family(const KParams &P, const Tables *T, 
 #pragma unroll
                     for (int side = 0; side < 2; side++) {
                         const int s = side == 0 ? sa : sb;
-                        if (!hs[s]) continue;
+                        if (!(side == 0 ? hA : hB)) continue;
                         const uint32_t wr = (side == 0 ? inA & ~slowA : inB & ~slowB);
                         const uint32_t bb = ss[2 * side], qq = ss[2 * side + 1];
                         const uint32_t n4 = nf[side] + __builtin_bswap32(nr[side]);  // (<= 64 reads: bytes)
