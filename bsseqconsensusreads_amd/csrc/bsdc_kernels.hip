@@ -2634,13 +2634,24 @@ __device__ __forceinline__ void st_part(const KParams &P, T *p, T v) {
         *p = v;
 }
 
+// a[s] for a lane-varying or loop-variable s, as selects: a dynamically indexed local array goes to
+// scratch (k_large's PART instances had 32-48 B of it)
+// Only the PART instances take the selects: in the whole-family instances the arrays stay in
+// registers anyway, and the selects cost C3's large set 1.4% (profiles/r05/README.md)
+template <bool SEL>
+__device__ __forceinline__ int pick4(const int (&a)[4], int s) {
+    if constexpr (SEL)
+        return s == 0 ? a[0] : s == 1 ? a[1] : s == 2 ? a[2] : a[3];
+    else
+        return a[s];
+}
 // more than one of the four per-base read counts (u8 each) is nonzero
 __device__ __forceinline__ bool multi_base(uint32_t m) {
     return ((m & 0xFFu) != 0) + ((m & 0xFF00u) != 0) + ((m & 0xFF0000u) != 0) + ((m & 0xFF000000u) != 0) > 1;
 }
-// A part's column: its read counts per base (u8 x4), and the likelihood sum of its one base when
-// only one has reads (`one`, 4 B: most columns), else the four sums (`sum`, 16 B; k_join reads them
-// only then).
+// A part's column: its read counts per base (u8 x4; without TAGS only the OR of its A/C/G/T codes,
+// u8), and the likelihood sum of its one base when only one has reads (`one`, 4 B: most columns),
+// else the four sums (`sum`, 16 B; k_join reads them only then).
 struct PartSums {
     int32_t *head;
     uint4 *sum;
@@ -2657,6 +2668,9 @@ struct PartSums {
         done = reinterpret_cast<int32_t *>(b + round16(32 * np) + 24 * 4 * np * (int64_t)pitch);
     }
     int32_t *one;   // the sum of a column whose reads show one base (its count byte the only one set)
+    // Without TAGS the parts keep no read counts: a column's OR of the A/C/G/T codes its reads show
+    // (u8, one-hot bits), in the count region, is all the join needs (PART_OR below)
+    __device__ __forceinline__ uint8_t *orb() const { return reinterpret_cast<uint8_t *>(cnt); }
     int32_t *done;  // per split family: its parts finished (part_join; zeroed before the dispatch)
     __device__ __forceinline__ int64_t at(int64_t part, int s, int col) const { return (4 * part + s) * (int64_t)pitch + col; }
 };
@@ -3142,8 +3156,8 @@ __device__ void process_large(const KParams &P, uint8_t *A, uint8_t *s_tab, cons
         const RecMeta &m = M[r];
         if (m.set == 0xFF) continue;
         const bool negr = m.flag & 16;
-        const int i = negr ? cnt[m.set] - 1 - atomicAdd(&s_cur[4 + m.set], 1) : atomicAdd(&s_cur[m.set], 1);
-        desc[soff[m.set] + i] = make_uint2(m.slot + (uint32_t)m.start + (negr ? (uint32_t)(m.len - 1) : 0u),
+        const int i = negr ? pick4<PART>(cnt, m.set) - 1 - atomicAdd(&s_cur[4 + m.set], 1) : atomicAdd(&s_cur[m.set], 1);
+        desc[pick4<PART>(soff, m.set) + i] = make_uint2(m.slot + (uint32_t)m.start + (negr ? (uint32_t)(m.len - 1) : 0u),
                                            (uint32_t)m.srclen | (negr ? 0x80000000u : 0u));
     }
     __syncthreads();
@@ -3159,8 +3173,8 @@ __device__ void process_large(const KParams &P, uint8_t *A, uint8_t *s_tab, cons
     // flushed to int64 every 128 reads.
     auto resolve = [&](int s, int col, long long D0, long long D1, long long D2, long long D3, uint32_t n01, uint32_t n23) {
         int best = first_max4(D0, D1, D2, D3);
-        if (near_tie(D0, D1, D2, D3, best, cnt[s]))  // rare: fgbio's fp64 read-order pick
-            best = fp64_pick(LargeDesc{desc + soff[s]}, cnt[s], col, slots, qimg, P.tab->lnc, P.tab->lne3);
+        if (near_tie(D0, D1, D2, D3, best, pick4<PART>(cnt, s)))  // rare: fgbio's fp64 read-order pick
+            best = fp64_pick(LargeDesc{desc + pick4<PART>(soff, s)}, pick4<PART>(cnt, s), col, slots, qimg, P.tab->lnc, P.tab->lne3);
         const long long Db = best == 0 ? D0 : best == 1 ? D1 : best == 2 ? D2 : D3;
         float S = 0.0f;
         if (best != 0) S += term(D0 - Db);
@@ -3183,8 +3197,8 @@ __device__ void process_large(const KParams &P, uint8_t *A, uint8_t *s_tab, cons
         const PartSums ps(P);
         const int64_t at = ps.at(blockIdx.x, s, col);
         const uint32_t m = (n01 & 0xFFu) | ((n01 >> 8) & 0xFF00u) | ((n23 & 0xFFu) << 16) | ((n23 >> 16) << 24);
-        st_part(P, ps.cnt + at, m);
-        if (multi_base(m)) {
+        if (TAGS) st_part(P, ps.cnt + at, m);
+        if (!TAGS || multi_base(m)) {  // (without TAGS pass B sees only multi-base columns; pass A wrote their OR)
             uint32_t *d = reinterpret_cast<uint32_t *>(ps.sum + at);
             if (P.part_join) {
                 st_part(P, d, (uint32_t)(int32_t)D0);
@@ -3218,8 +3232,8 @@ __device__ void process_large(const KParams &P, uint8_t *A, uint8_t *s_tab, cons
     uint8_t *por = reinterpret_cast<uint8_t *>(psum + 4 * ssw);     // [4][ssw] part-1 ORs
     uint16_t *pcn = reinterpret_cast<uint16_t *>(por + 4 * ssw);     // [4][ssw] part-1 A/C/G/T read counts (TAGS)
     {
-        const int na = cnt[ws], lc = lcv[ws], nf = nfw[ws];
-        const uint2 *dl = desc + soff[ws];
+        const int na = pick4<PART>(cnt, ws), lc = pick4<PART>(lcv, ws), nf = pick4<PART>(nfw, ws);
+        const uint2 *dl = desc + pick4<PART>(soff, ws);
         const int rb = wpart * na / PARTS, re = (wpart + 1) * na / PARTS;  // this wave's share of the set's reads
         const int lmax = ::max(::max(lcv[0], lcv[1]), ::max(lcv[2], lcv[3]));
         for (int cb = 0; cb < lmax; cb += 4 * kWave) {  // the same trip count in every wave (barriers inside)
@@ -3238,7 +3252,7 @@ __device__ void process_large(const KParams &P, uint8_t *A, uint8_t *s_tab, cons
                     const uint32_t v = onehot01(b);
                     orm |= b & (v * 0xFFu);
                     lookup4v(lr2, v, q, t0, t1, t2, t3);
-                    if (TAGS || PART) c4 += v;
+                    if (TAGS) c4 += v;
                 };
                 auto rev = [&](uint32_t ex, uint32_t ey) {  // bytes run backwards from the read's last base
                     const int sl = (int)(ey & 0x7FFFFFFFu);
@@ -3249,7 +3263,7 @@ __device__ void process_large(const KParams &P, uint8_t *A, uint8_t *s_tab, cons
                     const uint32_t v = onehot01(b);
                     orm |= b & (v * 0xFFu);
                     lookup4v(lr2, v, q, t0, t1, t2, t3);
-                    if (TAGS || PART) c4 += v;
+                    if (TAGS) c4 += v;
                 };
                 auto flush = [&]() {  // int32 partials over <= 64 reads: exact
                     T0 += t0;
@@ -3257,7 +3271,7 @@ __device__ void process_large(const KParams &P, uint8_t *A, uint8_t *s_tab, cons
                     T2 += t2;
                     T3 += t3;
                     t0 = t1 = t2 = t3 = 0;
-                    if (TAGS || PART) {
+                    if (TAGS) {
                         cn01 += __builtin_amdgcn_perm(0u, c4, 0x0c010c00u);
                         cn23 += __builtin_amdgcn_perm(0u, c4, 0x0c030c02u);
                         c4 = 0;
@@ -3301,40 +3315,46 @@ __device__ void process_large(const KParams &P, uint8_t *A, uint8_t *s_tab, cons
                             if (pp == PARTS - 1) {
                                 psum[ws * ssw + c + j] = tj;
                                 por[ws * ssw + c + j] = oj;
-                                if (TAGS || PART) pcn[ws * ssw + c + j] = nj;
+                                if (TAGS) pcn[ws * ssw + c + j] = nj;
                             } else {
                                 psum[ws * ssw + c + j] += tj;
                                 por[ws * ssw + c + j] |= oj;
-                                if (TAGS || PART) pcn[ws * ssw + c + j] += nj;
+                                if (TAGS) pcn[ws * ssw + c + j] += nj;
                             }
                         }
                 }
                 __syncthreads();
             }
             if (wpart == 0 && cb < lc) {
+                uint32_t or4 = 0;  // PART without TAGS: the lane's 4 columns' ORs and one-base sums,
+                int32_t one4[4] = {0, 0, 0, 0};  // stored as one dword and one 16-B vector after the loop
 #pragma unroll
                 for (int j = 0; j < 4; j++) {
                     const int col = c + j;
                     if (col >= lc) break;
                     uint32_t ob = (orm >> (8 * j)) & 0xFFu;
                     long long Tj = j == 0 ? T0 : j == 1 ? T1 : j == 2 ? T2 : T3;
-                    uint32_t nj = (TAGS || PART) ? ((j < 2 ? cn01 : cn23) >> (16 * (j & 1))) & 0xFFFFu : 0u;
+                    uint32_t nj = TAGS ? ((j < 2 ? cn01 : cn23) >> (16 * (j & 1))) & 0xFFFFu : 0u;
                     if (PARTS >= 2) {
                         Tj += psum[ws * ssw + col];
                         ob |= por[ws * ssw + col];
-                        if (TAGS || PART) nj += pcn[ws * ssw + col];
+                        if (TAGS) nj += pcn[ws * ssw + col];
                     }
                     if (PART) {  // one base (or none) seen: the part's sums are that base's; else pass B
                         if ((ob & (ob - 1)) == 0) {
-                            const PartSums ps(P);
                             const int bi = ob ? __builtin_ctz(ob) : 0;
                             const int32_t T = ob ? (int32_t)Tj : 0;
-                            st_part(P, ps.one + ps.at(blockIdx.x, ws, col), T);
-                            st_part(P, ps.cnt + ps.at(blockIdx.x, ws, col), ob ? nj << (8 * bi) : 0u);
+                            if (TAGS) {
+                                const PartSums ps(P);
+                                st_part(P, ps.one + ps.at(blockIdx.x, ws, col), T);
+                                st_part(P, ps.cnt + ps.at(blockIdx.x, ws, col), ob ? nj << (8 * bi) : 0u);
+                            }
+                            one4[j] = T;
                             ssq[ws * ssw + col] = 1;
                         } else {
                             ssq[ws * ssw + col] = 0;
                         }
+                        or4 |= ob << (8 * j);
                     } else if (ob != 0 && (ob & (ob - 1)) == 0 && Tj > na) {
                         const float e = term(-Tj);
                         const float S = ((0.0f + e) + e) + e;
@@ -3349,6 +3369,18 @@ __device__ void process_large(const KParams &P, uint8_t *A, uint8_t *s_tab, cons
                         ssq[ws * ssw + col] = 0;
                     }
                 }
+                if (PART && !TAGS) {  // (c + 3 < stride: c is a multiple of 4 below lc, stride of 16)
+                    const PartSums ps(P);
+                    const int64_t at = ps.at(blockIdx.x, ws, c);
+                    if (P.part_join) {
+                        st_part(P, reinterpret_cast<uint32_t *>(ps.orb() + at), or4);
+#pragma unroll
+                        for (int j = 0; j < 4; j++) st_part(P, ps.one + at + j, one4[j]);
+                    } else {
+                        *reinterpret_cast<uint32_t *>(ps.orb() + at) = or4;
+                        *reinterpret_cast<int4 *>(ps.one + at) = make_int4(one4[0], one4[1], one4[2], one4[3]);
+                    }
+                }
             }
             if (PARTS >= 2) __syncthreads();
         }
@@ -3361,7 +3393,7 @@ __device__ void process_large(const KParams &P, uint8_t *A, uint8_t *s_tab, cons
     // the descriptors broadcast as in pass A: four per-base sums, then the general call (resolve).
     uint16_t *mlist = reinterpret_cast<uint16_t *>(psum);  // [4][ssw]
     if (wpart == 0) {
-        const int lc = lcv[ws];
+        const int lc = pick4<PART>(lcv, ws);
         int nm = 0;
         for (int cb = 0; cb < lc; cb += kWave) {
             const int col = cb + lane;
@@ -3374,8 +3406,8 @@ __device__ void process_large(const KParams &P, uint8_t *A, uint8_t *s_tab, cons
     }
     __syncthreads();
     {
-        const int s = ws, na = cnt[s], nm = s_lc[s];
-        const uint2 *dl = desc + soff[s];
+        const int s = ws, na = pick4<PART>(cnt, s), nm = s_lc[s];
+        const uint2 *dl = desc + pick4<PART>(soff, s);
         // With two waves per set (PARTS = 2) both take the same 64 marked columns and split the
         // set's reads; part 1's four sums meet part 0's through LDS (int32: exact for <= 127
         // reads a part, |lr| < 2^24), after mlist in the part-sum region.  Workgroup-uniform:
@@ -3411,7 +3443,7 @@ __device__ void process_large(const KParams &P, uint8_t *A, uint8_t *s_tab, cons
                 d1 += bb == kC ? v : 0;
                 d2 += bb == kG ? v : 0;
                 d3 += bb == kT ? v : 0;
-                if ((TAGS || PART) && in) {
+                if (TAGS && in) {
                     n01 += bb == kA ? 1u : bb == kC ? 0x10000u : 0u;
                     n23 += bb == kG ? 1u : bb == kT ? 0x10000u : 0u;
                 }
@@ -3444,7 +3476,7 @@ __device__ void process_large(const KParams &P, uint8_t *A, uint8_t *s_tab, cons
                 add_up(D1);
                 add_up(D2);
                 add_up(D3);
-                if (TAGS || PART) {
+                if (TAGS) {
                     n01 += (uint32_t)__shfl_xor((int)n01, 32, kWave);
                     n23 += (uint32_t)__shfl_xor((int)n23, 32, kWave);
                 }
@@ -3471,7 +3503,7 @@ __device__ void process_large(const KParams &P, uint8_t *A, uint8_t *s_tab, cons
                     pw[1] = (int32_t)D1;
                     pw[2] = (int32_t)D2;
                     pw[3] = (int32_t)D3;
-                    if (TAGS || PART) {
+                    if (TAGS) {
                         pw[4] = (int32_t)n01;
                         pw[5] = (int32_t)n23;
                     }
@@ -3485,7 +3517,7 @@ __device__ void process_large(const KParams &P, uint8_t *A, uint8_t *s_tab, cons
                         D1 += pw[1];
                         D2 += pw[2];
                         D3 += pw[3];
-                        if (TAGS || PART) {
+                        if (TAGS) {
                             n01 += (uint32_t)pw[4];
                             n23 += (uint32_t)pw[5];
                         }
@@ -3507,7 +3539,7 @@ __device__ void process_large(const KParams &P, uint8_t *A, uint8_t *s_tab, cons
     __syncthreads();
     if (stop == 7) return;
     if (PART) {  // the part's set sizes and lengths; k_join does the rest
-        if (tt < 8) st_part(P, PartSums(P).head + 8 * (int64_t)blockIdx.x + tt, tt < 4 ? cnt[tt] : lcv[tt - 4]);
+        if (tt < 8) st_part(P, PartSums(P).head + 8 * (int64_t)blockIdx.x + tt, tt < 4 ? pick4<PART>(cnt, tt) : pick4<PART>(lcv, tt - 4));
         return;
     }
 
@@ -3617,24 +3649,32 @@ __device__ void join_family(const KParams &P, uint4 e0, uint4 e1, uint8_t *rows,
             s++;
         }
         long long D0 = 0, D1 = 0, D2 = 0, D3 = 0;
-        uint32_t n0 = 0, n1 = 0, n2 = 0, n3 = 0;
+        uint32_t n0 = 0, n1 = 0, n2 = 0, n3 = 0;  // (without TAGS: n0 = the OR of the parts' ORs)
         auto add = [&](uint4 d, uint32_t m) {
             D0 += (int32_t)d.x;
             D1 += (int32_t)d.y;
             D2 += (int32_t)d.z;
             D3 += (int32_t)d.w;
-            n0 += m & 0xFFu;
-            n1 += (m >> 8) & 0xFFu;
-            n2 += (m >> 16) & 0xFFu;
-            n3 += m >> 24;
+            if (TAGS) {
+                n0 += m & 0xFFu;
+                n1 += (m >> 8) & 0xFFu;
+                n2 += (m >> 16) & 0xFFu;
+                n3 += m >> 24;
+            } else {
+                n0 |= m;
+            }
         };
+        // a part's column record -- counts (TAGS) or OR (one-hot bits) -- shows more than one base
+        auto multi = [&](uint32_t x) { return TAGS ? multi_base(x) : (x & (x - 1)) != 0; };
         // one part's column as four sums: its one base's sum, or the four sums (multi-base)
         auto four = [&](uint32_t x, int32_t o, uint4 sm) {
-            if (multi_base(x)) return sm;
-            const uint32_t b = x & 0xFFu ? 0u : x & 0xFF00u ? 1u : x & 0xFF0000u ? 2u : 3u;
+            if (multi(x)) return sm;
+            const uint32_t b = TAGS ? (x & 0xFFu ? 0u : x & 0xFF00u ? 1u : x & 0xFF0000u ? 2u : 3u)
+                                    : (x & 1u ? 0u : x & 2u ? 1u : x & 4u ? 2u : 3u);
             return make_uint4(b == 0 ? (uint32_t)o : 0u, b == 1 ? (uint32_t)o : 0u, b == 2 ? (uint32_t)o : 0u,
                               b == 3 ? (uint32_t)o : 0u);
         };
+        auto rec = [&](int64_t at) { return TAGS ? ps.cnt[at] : (uint32_t)ps.orb()[at]; };
         if (hl_lds) {
             // kJoinU parts' loads in flight, every load unconditional (a part past the set's end,
             // or past the family's parts, reads an in-range slot and is masked after; a one-base
@@ -3647,7 +3687,7 @@ __device__ void join_family(const KParams &P, uint4 e0, uint4 e1, uint8_t *rows,
                 for (int u = 0; u < kJoinU; u++) {
                     const int pc = ::min(pb + u, np - 1);
                     in[u] = pb + u < np && c < (int)hl[s * kJoinParts + pc];
-                    m[u] = ps.cnt[ps.at(p0 + pc, s, c)];
+                    m[u] = rec(ps.at(p0 + pc, s, c));
                     o[u] = ps.one[ps.at(p0 + pc, s, c)];
                 }
                 uint4 sm[kJoinU];
@@ -3656,7 +3696,7 @@ __device__ void join_family(const KParams &P, uint4 e0, uint4 e1, uint8_t *rows,
                     m[u] = in[u] ? m[u] : 0u;
                     o[u] = in[u] ? o[u] : 0;
                     const int pc = ::min(pb + u, np - 1);
-                    sm[u] = ps.sum[multi_base(m[u]) ? ps.at(p0 + pc, s, c) : 0];
+                    sm[u] = ps.sum[multi(m[u]) ? ps.at(p0 + pc, s, c) : 0];
                 }
 #pragma unroll
                 for (int u = 0; u < kJoinU; u++) add(four(m[u], o[u], sm[u]), m[u]);
@@ -3664,9 +3704,9 @@ __device__ void join_family(const KParams &P, uint4 e0, uint4 e1, uint8_t *rows,
         } else {  // (more than kJoinParts parts: their set lengths from HBM, part by part)
             for (int p = 0; p < np; p++) {
                 if (c >= ps.head[8 * (p0 + p) + 4 + s]) continue;  // (a part whose set ends before c wrote nothing there)
-                const uint32_t x = ps.cnt[ps.at(p0 + p, s, c)];
+                const uint32_t x = rec(ps.at(p0 + p, s, c));
                 const int32_t o = ps.one[ps.at(p0 + p, s, c)];
-                add(four(x, o, multi_base(x) ? ps.sum[ps.at(p0 + p, s, c)] : make_uint4(0u, 0u, 0u, 0u)), x);
+                add(four(x, o, multi(x) ? ps.sum[ps.at(p0 + p, s, c)] : make_uint4(0u, 0u, 0u, 0u)), x);
             }
         }
         const int best = first_max4(D0, D1, D2, D3);
@@ -3681,7 +3721,7 @@ __device__ void join_family(const KParams &P, uint4 e0, uint4 e1, uint8_t *rows,
         if (best != 2) S += term(D2 - Db);
         if (best != 3) S += term(D3 - Db);
         const int Q = phred_of(S, T.thr);
-        const uint32_t depth = n0 + n1 + n2 + n3;
+        const uint32_t depth = n0 + n1 + n2 + n3;  // (without TAGS: nonzero iff a read shows an A/C/G/T)
         const bool nocall = depth == 0 || Q < P.qmin;
         ssb[s * pitch + c] = nocall ? (uint8_t)kN : (uint8_t)(1u << best);
         ssq[s * pitch + c] = nocall ? (uint8_t)2 : (uint8_t)Q;
