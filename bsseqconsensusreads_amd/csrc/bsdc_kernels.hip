@@ -2669,8 +2669,13 @@ struct PartSums {
     }
     int32_t *one;   // the sum of a column whose reads show one base (its count byte the only one set)
     // Without TAGS the parts keep no read counts: a column's OR of the A/C/G/T codes its reads show
-    // (u8, one-hot bits), in the count region, is all the join needs (PART_OR below)
-    __device__ __forceinline__ uint8_t *orb() const { return reinterpret_cast<uint8_t *>(cnt); }
+    // (u8, one-hot bits) is all the join needs.  It lives at the start of the column's count row
+    // (rows keep the counts' 4 x stride spacing: a part's row shares its cache lines with no more
+    // of the other parts' rows than the count rows did -- the fused join's joiner, on another XCD,
+    // must not find another part's bytes in a line its own L2 holds)
+    __device__ __forceinline__ uint8_t *orb(int64_t at, int col) const {
+        return reinterpret_cast<uint8_t *>(cnt) + 4 * at - 3 * (int64_t)col;
+    }
     int32_t *done;  // per split family: its parts finished (part_join; zeroed before the dispatch)
     __device__ __forceinline__ int64_t at(int64_t part, int s, int col) const { return (4 * part + s) * (int64_t)pitch + col; }
 };
@@ -3326,8 +3331,12 @@ __device__ void process_large(const KParams &P, uint8_t *A, uint8_t *s_tab, cons
                 __syncthreads();
             }
             if (wpart == 0 && cb < lc) {
-                uint32_t or4 = 0;  // PART without TAGS: the lane's 4 columns' ORs and one-base sums,
-                int32_t one4[4] = {0, 0, 0, 0};  // stored as one dword and one 16-B vector after the loop
+                // PART: the lane's 4 columns' records -- ORs (one dword) or, with TAGS, counts (one
+                // 16-B vector; a multi-base column's are pass B's) -- and one-base sums (one vector),
+                // stored after the loop: per-column 4-B stores at a 16-B lane stride wrote each line
+                // several times (C4 part dispatch: 1034 -> 263 MB written, profiles/r05/README.md)
+                uint32_t or4 = 0, cnt4[4] = {0u, 0u, 0u, 0u};
+                int32_t one4[4] = {0, 0, 0, 0};
 #pragma unroll
                 for (int j = 0; j < 4; j++) {
                     const int col = c + j;
@@ -3343,13 +3352,8 @@ __device__ void process_large(const KParams &P, uint8_t *A, uint8_t *s_tab, cons
                     if (PART) {  // one base (or none) seen: the part's sums are that base's; else pass B
                         if ((ob & (ob - 1)) == 0) {
                             const int bi = ob ? __builtin_ctz(ob) : 0;
-                            const int32_t T = ob ? (int32_t)Tj : 0;
-                            if (TAGS) {
-                                const PartSums ps(P);
-                                st_part(P, ps.one + ps.at(blockIdx.x, ws, col), T);
-                                st_part(P, ps.cnt + ps.at(blockIdx.x, ws, col), ob ? nj << (8 * bi) : 0u);
-                            }
-                            one4[j] = T;
+                            one4[j] = ob ? (int32_t)Tj : 0;
+                            cnt4[j] = ob ? nj << (8 * bi) : 0u;
                             ssq[ws * ssw + col] = 1;
                         } else {
                             ssq[ws * ssw + col] = 0;
@@ -3369,15 +3373,23 @@ __device__ void process_large(const KParams &P, uint8_t *A, uint8_t *s_tab, cons
                         ssq[ws * ssw + col] = 0;
                     }
                 }
-                if (PART && !TAGS) {  // (c + 3 < stride: c is a multiple of 4 below lc, stride of 16)
+                // (only lanes with columns: a lane past lc would write into the next row; c < lc
+                // gives c + 3 < stride, c being a multiple of 4 and stride of 16)
+                if (PART && c < lc) {
                     const PartSums ps(P);
                     const int64_t at = ps.at(blockIdx.x, ws, c);
                     if (P.part_join) {
-                        st_part(P, reinterpret_cast<uint32_t *>(ps.orb() + at), or4);
 #pragma unroll
-                        for (int j = 0; j < 4; j++) st_part(P, ps.one + at + j, one4[j]);
+                        for (int j = 0; j < 4; j++) {
+                            if (TAGS) st_part(P, ps.cnt + at + j, cnt4[j]);
+                            st_part(P, ps.one + at + j, one4[j]);
+                        }
+                        if (!TAGS) st_part(P, reinterpret_cast<uint32_t *>(ps.orb(at, c)), or4);
                     } else {
-                        *reinterpret_cast<uint32_t *>(ps.orb() + at) = or4;
+                        if (TAGS)
+                            *reinterpret_cast<uint4 *>(ps.cnt + at) = make_uint4(cnt4[0], cnt4[1], cnt4[2], cnt4[3]);
+                        else
+                            *reinterpret_cast<uint32_t *>(ps.orb(at, c)) = or4;
                         *reinterpret_cast<int4 *>(ps.one + at) = make_int4(one4[0], one4[1], one4[2], one4[3]);
                     }
                 }
@@ -3674,7 +3686,7 @@ __device__ void join_family(const KParams &P, uint4 e0, uint4 e1, uint8_t *rows,
             return make_uint4(b == 0 ? (uint32_t)o : 0u, b == 1 ? (uint32_t)o : 0u, b == 2 ? (uint32_t)o : 0u,
                               b == 3 ? (uint32_t)o : 0u);
         };
-        auto rec = [&](int64_t at) { return TAGS ? ps.cnt[at] : (uint32_t)ps.orb()[at]; };
+        auto rec = [&](int64_t at) { return TAGS ? ps.cnt[at] : (uint32_t)*ps.orb(at, c); };
         if (hl_lds) {
             // kJoinU parts' loads in flight, every load unconditional (a part past the set's end,
             // or past the family's parts, reads an in-range slot and is masked after; a one-base

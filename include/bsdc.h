@@ -111,8 +111,8 @@ typedef struct {
     int64_t n_split_fams;
     int64_t split_partial_off;   /* scratch offset of the parts' sums: [part][8] int32 (set reads, set
                                     lengths), then [part][4][stride] int32x4 sums, [part][4][stride] u8x4
-                                    counts (without BSDC_MODE_TAGS: the first [part][4][stride] bytes
-                                    hold each column's OR of one-hot A/C/G/T codes instead), [part][4]
+                                    counts (without BSDC_MODE_TAGS: byte 0..stride-1 of each count row
+                                    holds the column's OR of one-hot A/C/G/T codes instead), [part][4]
                                     [stride] int32 one-base sums, then (ABI 14)
                                     [n_split_fams] int32 parts done: the last part of a family joins it */
     int64_t n_small_wide[BSDC_SMALL_BUCKETS]; /* (ABI 13) the LAST n_small_wide[q] entries of small bucket q

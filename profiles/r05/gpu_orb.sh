@@ -10,9 +10,12 @@ B="$(pwd)/profiles/_build"
 timeout -k 10 300 python -u -m pytest tests/test_gpu_parity.py tests/test_gpu_fp64.py -x -q --timeout 300 --timeout-method thread > "$OUT/pytest.log" 2>&1 \
   || { echo "gpu tests failed"; grep -E "PASS|FAIL|Error|error" "$OUT/pytest.log" | tail -30; exit 1; }
 tail -1 "$OUT/pytest.log"
-BSDC_SPLIT_JOIN=part timeout -k 10 300 python -u -m pytest tests/test_gpu_parity.py -k split -x -q --timeout 300 --timeout-method thread > "$OUT/pytest_partjoin.log" 2>&1 \
-  || { echo "part-join tests failed"; grep -E "PASS|FAIL|Error|error" "$OUT/pytest_partjoin.log" | tail -30; exit 1; }
-tail -1 "$OUT/pytest_partjoin.log"
+# the opt-in fused-join arm, HEAD's library and this one (reported, not fatal)
+for v in head new; do
+  case $v in head) LP="$B/libbsdc_head.so";; *) LP="";; esac
+  BSDC_LIB_PATH="$LP" BSDC_SPLIT_JOIN=part timeout -k 10 300 python -u -m pytest tests/test_gpu_parity.py -k split -q --timeout 300 --timeout-method thread > "$OUT/pytest_partjoin_$v.log" 2>&1
+  echo "part-join $v rc=$?"; grep -E "^FAILED|passed|failed" "$OUT/pytest_partjoin_$v.log" | tail -8
+done
 timeout -k 10 400 python -u -m pytest tests/test_gpu_fullsize.py -k "c4" -x -q --timeout 380 --timeout-method thread > "$OUT/pytest_c4.log" 2>&1 \
   || { echo "c4 tests failed"; grep -E "PASS|FAIL|Error|error" "$OUT/pytest_c4.log" | tail -30; exit 1; }
 tail -1 "$OUT/pytest_c4.log"
