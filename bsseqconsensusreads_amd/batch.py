@@ -42,6 +42,10 @@ MODE_CONVERT, MODE_EXTEND, MODE_VOTE, MODE_DUMP = 1, 2, 4, 8
 # small families run one per wavefront with their arena in LDS, in buckets of these arena sizes
 SMALL_BUCKETS = (3072, 4096, 5120, 6144, 8192, 12288, 16384, 24576)  # BSDC_SMALL_BUCKETS classes
 SMALL_ARENA_CAP = int(os.environ.get("BSDC_SMALL_CAP", "24576"))  # (BSDC_SMALL_CAP: profiling A/B)
+# route_small_cap: a batch whose small families are mostly ones with arenas above MID_ARENA_CAP
+# sends those to k_large (BSDC_SMALL_ROUTE=0 or an explicit BSDC_SMALL_CAP: never)
+MID_ARENA_CAP = 16384
+SMALL_ROUTE = os.environ.get("BSDC_SMALL_ROUTE", "1") != "0" and "BSDC_SMALL_CAP" not in os.environ
 LDS_TABLES = 1024 + 1024 + 384 + 2048 + 192  # kTabBytes (csrc/bsdc_kernels.hip)
 # large families run one per 256-thread workgroup, in buckets of these LDS arena sizes; the last
 # bucket (anything larger) keeps its arenas in HBM scratch
@@ -451,7 +455,7 @@ class FamilyPlan:
 
 
 def build_family_batch(raw: R.RawRecords, mode: str = "full", ref: Optional[R.Reference] = None,
-                       small_cap: int = SMALL_ARENA_CAP, family_order: str = "template-coordinate") -> FamilyBatch:
+                       small_cap: Optional[int] = None, family_order: str = "template-coordinate") -> FamilyBatch:
     """mode: 'full' (raw step-5 input: tools 1+2 then the vote), 'convert' (tool 1 alone: one
     family per converted record), 'extend' (tool-1 output: tool 2 alone), 'vote' (tool-2 output).
     family_order ('full' / 'vote'): 'template-coordinate' -- the vote's families are the runs of one
@@ -658,11 +662,42 @@ def plan_families_py(raw: R.RawRecords, mode: str = "full", ref: Optional[R.Refe
                       kfirst=kfirst, kn=kn, fam_split=fam_split)
 
 
-def materialize(plan: FamilyPlan, f0: int, f1: int, small_cap: int = SMALL_ARENA_CAP, images=None) -> FamilyBatch:
+def route_small_cap(plan: FamilyPlan, f0: int, f1: int, cap: int = SMALL_ARENA_CAP, mid: int = MID_ARENA_CAP,
+                    sample: int = 2048) -> int:
+    """The small-arena cap for plan families [f0, f1): `mid` when more than half of the records of
+    the small families (<= 64 records, arena <= cap) are in families whose arena exceeds `mid`,
+    else `cap`.  k_small runs such families 6 waves per CU at most (LDS), k_large's 5-per-CU class
+    at half their cost: C3 (deep families) 9.00 -> 8.54 ms per step; where they are a minority (C4)
+    moving them lengthens the large leg more than it shortens the small one (profiles/r05/README.md).
+    Estimated on up to `sample` evenly spaced families, with the arena of SmallLayout for no complex
+    cigar (small_arena_bytes; the exact one is the C++ plan's)."""
+    nf = f1 - f0
+    if not SMALL_ROUTE or cap <= mid or nf <= 0:
+        return cap
+    pick = np.unique(np.linspace(f0, f1 - 1, min(nf, sample)).astype(np.int64))
+    a, b = plan.fam_off[pick].astype(np.int64), plan.fam_off[pick + 1].astype(np.int64)
+    sizes = b - a
+    if not sizes.sum():
+        return cap
+    fam_of = np.repeat(np.arange(pick.shape[0]), sizes)
+    recs = plan.order[np.repeat(a - np.cumsum(sizes) + sizes, sizes) + np.arange(int(sizes.sum()))]
+    L = plan.L[recs].astype(np.int64)
+    cap4 = (L + 2 + 3) & ~np.int64(3)
+    img = (np.bincount(fam_of, weights=cap4, minlength=pick.shape[0]).astype(np.int64) + 31) & ~np.int64(31)
+    nconv = np.bincount(fam_of, weights=plan.conv[recs].astype(np.int64), minlength=pick.shape[0]).astype(np.int64)
+    need = small_arena_bytes(sizes, img, nconv, np.zeros_like(sizes), int(L.max()))
+    small = (sizes <= 64) & (need <= cap)
+    return mid if 2 * int(sizes[small & (need > mid)].sum()) > int(sizes[small].sum()) else cap
+
+
+def materialize(plan: FamilyPlan, f0: int, f1: int, small_cap: Optional[int] = None, images=None) -> FamilyBatch:
     """The device batch of plan families [f0, f1) (family ids renumbered from 0): C++ (hostplan)
     for the step-5 modes, materialize_py otherwise; then the HBM bucket's families cut into parts
-    (split_hbm_bucket).  images: see hostplan.materialize."""
+    (split_hbm_bucket).  small_cap: the largest small-family arena (None: route_small_cap).
+    images: see hostplan.materialize."""
     from . import hostplan
+    if small_cap is None:
+        small_cap = route_small_cap(plan, f0, f1)
     if plan.mode in ("full", "vote") and hostplan.enabled():
         return split_hbm_bucket(hostplan.materialize(plan, f0, f1, small_cap, images=images))
     return split_hbm_bucket(materialize_py(plan, f0, f1, small_cap))

@@ -108,3 +108,22 @@ def test_split_part_records_cover_each_family_once(monkeypatch):
                     assert lm != 0xFFFF and recs[lm][0] == r0 + gm
             assert p[3] == (at - a0 + 31) // 32 * 32  # (the staged image: whole 32-entry chunks)
         assert sorted(seen) == list(range(r0, r0 + n))
+
+
+def test_route_small_cap_by_family_mix(monkeypatch):
+    """route_small_cap: deep families (C3: most small-family records in arenas above 16 KB) go to
+    k_large from 16 KB on; shallow and skewed mixes (C2, C4) keep the 24 KB cap; explicit caps and
+    BSDC_SMALL_ROUTE=0 turn it off"""
+    from bsseqconsensusreads_amd import synth
+    got = {}
+    for cfg, n in (("C2", 20000), ("C3", 3000), ("C4", 20000)):
+        s = synth.generate(cfg, n, seed=3, device="cpu")
+        plan = batch.plan_families(s.raw, "full", s.ref)
+        got[cfg] = batch.route_small_cap(plan, 0, plan.n_fam)
+        if cfg == "C3":
+            fb = batch.materialize(plan, 0, plan.n_fam)  # (the routed cap reaches the plan)
+            assert max(a for a, b in zip(fb.small_arenas, fb.small_buckets) if b.shape[0]) <= batch.MID_ARENA_CAP
+            monkeypatch.setattr(batch, "SMALL_ROUTE", False)
+            assert batch.route_small_cap(plan, 0, plan.n_fam) == batch.SMALL_ARENA_CAP
+            monkeypatch.setattr(batch, "SMALL_ROUTE", True)
+    assert got == {"C2": batch.SMALL_ARENA_CAP, "C3": batch.MID_ARENA_CAP, "C4": batch.SMALL_ARENA_CAP}
