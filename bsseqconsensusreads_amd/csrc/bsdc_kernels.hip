@@ -48,6 +48,9 @@ constexpr int kWave = 64;
 #define SMALL_STAGE_U 4  // k_small staging: image chunk loads in flight per lane
 #endif
 constexpr int kStageU = SMALL_STAGE_U;
+#ifndef LARGE_QDMA
+#define LARGE_QDMA 0  // k_large: 1 stages the quals with LDS-DMA (global_load_lds_dwordx4; A/B arm)
+#endif
 #ifndef SMALL_QDMA
 #define SMALL_QDMA 1  // k_small stages the quals with LDS-DMA (global_load_lds_dwordx4); 0: through VGPRs
 #endif
@@ -2727,10 +2730,22 @@ __device__ void process_large(const KParams &P, uint8_t *A, uint8_t *s_tab, cons
             unpack32<false>(v, slots + 32 * (k - nqc));
         }
     };
+    // LARGE_QDMA, arena in LDS (not the HBM-scratch arenas): the quals straight into LDS, wave w's
+    // lanes taking chunks j * G + 64 w + lane, lane-linear in LDS as the DMA writes them; the
+    // packed bases go through VGPRs (unpacked)
+    const bool dma = LARGE_QDMA && __builtin_amdgcn_is_shared((const __attribute__((address_space(0))) void *)A);
+    if (dma) {
+        for (int j = 0; j * G < nqc; j++) {
+            const int kb = j * G + (tt & ~(kWave - 1));
+            if (kb + (tt & (kWave - 1)) < nqc) glds16(B.qual + off0 + 16u * (uint32_t)(kb + (tt & (kWave - 1))), qimg + 16 * kb);
+        }
+    }
+    auto chunk_of = [&](int i) { return dma ? nqc + i : i; };  // (with dma the register rounds: packed bases only)
+    const int nreg = dma ? nch - nqc : nch;
     uint4 v[kLStageU];
 #pragma unroll
     for (int u = 0; u < kLStageU; u++)
-        if (tt + u * G < nch) v[u] = load_chunk(tt + u * G);
+        if (tt + u * G < nreg) v[u] = load_chunk(chunk_of(tt + u * G));
     uint4 tv = make_uint4(0, 0, 0, 0);
     if (tt < kTabBytesL / 16) tv = reinterpret_cast<const uint4 *>(&P.tab->t)[tt];
     int c = 0, ml = 0;
@@ -2765,15 +2780,23 @@ __device__ void process_large(const KParams &P, uint8_t *A, uint8_t *s_tab, cons
     }
 #pragma unroll
     for (int u = 0; u < kLStageU; u++)
-        if (tt + u * G < nch) store_chunk(tt + u * G, v[u]);
+        if (tt + u * G < nreg) store_chunk(chunk_of(tt + u * G), v[u]);
     if (tt < kTabBytesL / 16) reinterpret_cast<uint4 *>(s_tab)[tt] = tv;
-    for (int k0 = tt + kLStageU * G; k0 < nch; k0 += kLStageU * G) {  // families of more chunks
+    for (int k0 = tt + kLStageU * G; k0 < nreg; k0 += kLStageU * G) {  // families of more chunks
 #pragma unroll
         for (int u = 0; u < kLStageU; u++)
-            if (k0 + u * G < nch) v[u] = load_chunk(k0 + u * G);
+            if (k0 + u * G < nreg) v[u] = load_chunk(chunk_of(k0 + u * G));
 #pragma unroll
         for (int u = 0; u < kLStageU; u++)
-            if (k0 + u * G < nch) store_chunk(k0 + u * G, v[u]);
+            if (k0 + u * G < nreg) store_chunk(chunk_of(k0 + u * G), v[u]);
+    }
+    if (dma) {
+        __asm__ volatile("s_waitcnt vmcnt(0)" ::: "memory");  // this thread's DMA'd quals have landed
+        __syncthreads();
+        for (int k = tt; k < nqc; k += G) {
+            const uint4 q = *reinterpret_cast<const uint4 *>(qimg + 16 * k);
+            qor |= q.x | q.y | q.z | q.w;
+        }
     }
     int cops, maxlen_f;
     block_sum_max<G>(c, ml, red, cops, maxlen_f);  // (its barrier publishes the arena and the tables)
