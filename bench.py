@@ -236,6 +236,19 @@ def run(args):
                      "valu_issue_frac": round(v_launch * 2 / (1024 * 2.4e9) / t_dom, 4),
                      "pmc_source": os.path.relpath(pmc, ROOT)}
 
+    # the tag leg's HBM bytes per step, from the TAGS=1 PMC passes (profiles/pmc_<config>_tags.json:
+    # its k_small<true> and k_large / k_join tag instances), when committed for this workload
+    tags_traffic = None
+    pmt = os.path.join(ROOT, "profiles", "pmc_%s_tags.json" % args.config)
+    if tags_ms is not None and os.path.exists(pmt) and args.families == DEFAULT_FAMILIES.get(args.config, 1_000_000) \
+            and args.seed == 42:
+        with open(pmt) as fh:
+            kt = json.load(fh)
+        parts = [(kt.get("k_small_tags", {}).get("hbm_bytes_per_dispatch"), n_disp),
+                 (kt.get("k_large_tags", {}).get("hbm_bytes_per_dispatch"), sum(r.n_disp_large for r in res))]
+        if all(b is not None or nd == 0 for b, nd in parts):
+            tags_traffic = int(sum(b * nd for b, nd in parts if nd))
+
     cpu = None
     if rank == 0 and world == 1 and args.cpu_sample > 0:
         # the host's CPU share: OMP_NUM_THREADS / nproc (16 on the GPU box, whose os.cpu_count()
@@ -292,6 +305,7 @@ def run(args):
                               "frac": round((bytes_all + tag_extra) / (tags_ms / 1e3) / 1e9 / HBM_PEAK_GBS, 4),
                               "algorithmic_bytes_per_step": int(bytes_all + tag_extra),
                               "tag_bytes_per_step": int(tag_extra),
+                              "traffic": tags_traffic,
                               "vs_headline_ms": round(tags_ms / (elapsed / args.steps * 1e3), 4)}
             if tags_ms is not None else None,
             "tags_families_per_s": round(molecules / (tags_ms / 1e3), 1) if tags_ms else None,
