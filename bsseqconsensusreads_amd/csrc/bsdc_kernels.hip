@@ -3847,6 +3847,9 @@ struct bsdc_ctx {
     // in the environment at context creation).  k_pair is parity-green but measured slower on C2
     // (3.52 vs 3.09 ms, profiles/r05/README.md): kept as the A/B arm
     bool pair = false;
+    // (BSDC_SMALL_ORDER=work) the small buckets' dispatches in descending families x arena, the
+    // longest first, instead of by arena size (A/B knob)
+    bool small_by_work = false;
     // split families: a k_join dispatch after all the parts (default), or the last part of each
     // family joins it (BSDC_SPLIT_JOIN=part: measured slower, profiles/r05/README.md)
     bool part_join = false;
@@ -4080,6 +4083,8 @@ int32_t bsdc_ctx_create(int32_t device, const bsdc_params *params, bsdc_ctx **ou
     {
         const char *sk = getenv("BSDC_SMALL_KERNEL");
         c->pair = sk && std::string(sk) == "pair";
+        const char *so = getenv("BSDC_SMALL_ORDER");
+        c->small_by_work = so && std::string(so) == "work";
         const char *sj = getenv("BSDC_SPLIT_JOIN");
         c->part_join = sj && std::string(sj) == "part";
     }
@@ -4290,8 +4295,23 @@ int32_t bsdc_run(bsdc_ctx *c, const bsdc_family_batch *b, bsdc_consensus *o, int
     };
     auto launch_small_all = [&]() {
     if (!(mode & BSDC_MODE_SKIP_SMALL) && rc == 0) {
-        const uint32_t *f = b->small_fams;
-        for (int q = 0; q < BSDC_SMALL_BUCKETS && rc == 0; q++) {
+        int64_t fstart[BSDC_SMALL_BUCKETS];
+        int order[BSDC_SMALL_BUCKETS];
+        {
+            int64_t o = 0;
+            for (int q = 0; q < BSDC_SMALL_BUCKETS; q++) {
+                fstart[q] = o;
+                o += 4 * b->n_small[q];
+                order[q] = q;
+            }
+        }
+        if (c->small_by_work)
+            std::stable_sort(order, order + BSDC_SMALL_BUCKETS, [&](int x, int y) {
+                return b->n_small[x] * b->small_arena[x] > b->n_small[y] * b->small_arena[y];
+            });
+        for (int i = 0; i < BSDC_SMALL_BUCKETS && rc == 0; i++) {
+            const int q = order[i];
+            const uint32_t *f = b->small_fams + fstart[q];
             const int64_t nall = b->n_small[q];
             const int64_t nwide = c->pair ? std::min<int64_t>(std::max<int64_t>(b->n_small_wide[q], 0), nall) : 0;
             int64_t nf = nall - nwide;  // k_pair: the first nall - nwide entries (all of them without c->pair: k_small)
@@ -4349,7 +4369,6 @@ int32_t bsdc_run(bsdc_ctx *c, const bsdc_family_batch *b, bsdc_consensus *o, int
                 const hipError_t e = hipGetLastError();
                 if (e != hipSuccess) fail(e, "k_small launch");
             }
-            f += 4 * nf;
         }
     }
     };
