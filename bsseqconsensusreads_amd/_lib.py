@@ -8,9 +8,8 @@ HERE = os.path.dirname(os.path.abspath(__file__))
 # BSDC_LIB_PATH: an alternative build of the same library (profiling A/B runs only)
 LIB_PATH = os.environ.get("BSDC_LIB_PATH") or os.path.join(HERE, "libbsdc.so")
 
-BSDC_ABI_VERSION = 14
+BSDC_ABI_VERSION = 15
 SMALL_BUCKETS = 8  # BSDC_SMALL_BUCKETS
-PAIR_MAX_REC = 32  # families of more records run one per wavefront (bsdc_family_batch.n_small_wide)
 LARGE_BUCKETS = 6  # BSDC_LARGE_BUCKETS
 MODE_CONVERT, MODE_EXTEND, MODE_VOTE, MODE_DUMP = 1, 2, 4, 8
 MODE_SKIP_SMALL, MODE_SKIP_LARGE = 16, 32
@@ -33,8 +32,7 @@ class FamilyBatchC(C.Structure):
                 ("max_len", C.c_int32), ("split_part_arena", C.c_int32),
                 ("split_parts", C.c_void_p), ("n_split_parts", C.c_int64), ("split_part_recs", C.c_void_p),
                 ("split_fams", C.c_void_p),
-                ("n_split_fams", C.c_int64), ("split_partial_off", C.c_int64),
-                ("n_small_wide", C.c_int64 * SMALL_BUCKETS)]
+                ("n_split_fams", C.c_int64), ("split_partial_off", C.c_int64)]
 
 
 class ConsensusC(C.Structure):

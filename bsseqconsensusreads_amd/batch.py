@@ -16,7 +16,6 @@ so the kernel only ever sees records that reach the vote:
 """
 from __future__ import annotations
 
-import os
 from dataclasses import dataclass, field
 from typing import List, Optional
 
@@ -41,11 +40,11 @@ MODE_CONVERT, MODE_EXTEND, MODE_VOTE, MODE_DUMP = 1, 2, 4, 8
 
 # small families run one per wavefront with their arena in LDS, in buckets of these arena sizes
 SMALL_BUCKETS = (3072, 4096, 5120, 6144, 8192, 12288, 16384, 24576)  # BSDC_SMALL_BUCKETS classes
-SMALL_ARENA_CAP = int(os.environ.get("BSDC_SMALL_CAP", "24576"))  # (BSDC_SMALL_CAP: profiling A/B)
+SMALL_ARENA_CAP = 24576  # the largest small-family arena (profiles/r05/README.md: small-arena cap A/B)
 # route_small_cap: a batch whose small families are mostly ones with arenas above MID_ARENA_CAP
-# sends those to k_large (BSDC_SMALL_ROUTE=0 or an explicit BSDC_SMALL_CAP: never)
+# sends those to k_large (SMALL_ROUTE = False: never)
 MID_ARENA_CAP = 16384
-SMALL_ROUTE = os.environ.get("BSDC_SMALL_ROUTE", "1") != "0" and "BSDC_SMALL_CAP" not in os.environ
+SMALL_ROUTE = True
 LDS_TABLES = 1024 + 1024 + 384 + 2048 + 192  # kTabBytes (csrc/bsdc_kernels.hip)
 # large families run one per 256-thread workgroup, in buckets of these LDS arena sizes; the last
 # bucket (anything larger) keeps its arenas in HBM scratch
@@ -56,12 +55,12 @@ assert LARGE_BUCKETS[-1] == LARGE_LDS_MAX
 # k_large part mode (include/bsdc.h split_parts): the families of the 1-per-CU class and of the
 # HBM-scratch bucket are cut into parts whose arena fits the 5-per-CU class (profiles/r04/ab_g,
 # ab_h: smaller parts keep more workgroups in flight; cutting the 2-per-CU class too loses);
-# BSDC_PART_CAP=0 turns it off
-PART_CAP = int(os.environ.get("BSDC_PART_CAP", str(LARGE_BUCKETS[0])))
+# PART_CAP = 0 turns it off
+PART_CAP = LARGE_BUCKETS[0]
 MAX_PART_REC = 254  # a part's per-set sums stay int32 and its read counts fit a byte
 # the first large bucket whose families are cut into parts: 4 = the 1-per-CU class and the
-# HBM-scratch bucket (BSDC_SPLIT_FROM: profiling A/B)
-SPLIT_FROM = int(os.environ.get("BSDC_SPLIT_FROM", str(len(LARGE_BUCKETS) - 1)))
+# HBM-scratch bucket (profiles/r05/README.md: split-from A/B)
+SPLIT_FROM = len(LARGE_BUCKETS) - 1
 
 
 def round16(x):
@@ -79,12 +78,12 @@ def small_arena_bytes(n, img, nconv, complex_ops, max_len):
     n = np.asarray(n, dtype=np.int64)
     ws = 32 * ref_chunks(max_len)
     cops = np.asarray(complex_ops, dtype=np.int64)
-    rw = int(round16((int(max_len) + 2 + 19) // 20 * 20))  # k_pair's single-strand rows (>= the vote rows of k_small)
-    R = 2 * np.asarray(img, dtype=np.int64) + round16(4 * n) + 32 + round16(n)
-    e_ref = R + np.asarray(nconv, dtype=np.int64) * (ws + 16)  # (k_pair: + the converted records' info)
+    ow = int(round16(int(max_len) + 2))
+    R = 2 * np.asarray(img, dtype=np.int64) + round16(4 * n) + 16 + round16(n)
+    e_ref = R + np.asarray(nconv, dtype=np.int64) * ws
     simp = R + round16(16 * n) + round16(n) + 2 * round16(2 * n)
     e_f = simp + np.where(cops > 0, round16(4 * (cops + 4 * n)) + 256, 0)  # (+ filter_group's scratch)
-    e_v = R + 8 * rw
+    e_v = R + 8 * ow
     return np.maximum(np.maximum(e_ref, e_f), e_v)
 
 
@@ -172,27 +171,11 @@ class FamilyBatch:
         arenas = int(sf[:, 7].astype(np.int64).sum()) if sf.shape[0] else 0
         poff = int(round16(base + arenas))
         npart = int(self.split_parts.shape[0])
-        # + the done count per split family (the last part joins; include/bsdc.h split_partial_off)
-        psz = int(round16(32 * npart)) + npart * 4 * self.stride * 24 + 4 * int(sf.shape[0]) if npart else 0
+        psz = int(round16(32 * npart)) + npart * 4 * self.stride * 24 if npart else 0
         total = poff + psz
         return (total + 256 if total else 0), base, poff
 
-    def pair_order(self) -> List[int]:
-        """Per small bucket, its families of more than 32 records (include/bsdc.h n_small_wide) moved
-        to the end of the bucket, in order: k_pair runs the others two per wavefront, k_small these
-        one per wavefront.  -> the wide count per bucket (idempotent)."""
-        sizes = np.diff(self.fam_off.astype(np.int64))
-        wide = []
-        for q, b in enumerate(self.small_buckets):
-            w = sizes[b.astype(np.int64)] > _lib.PAIR_MAX_REC if b.shape[0] else np.zeros(0, bool)
-            nw = int(w.sum())
-            if nw and not w[-nw:].all():
-                self.small_buckets[q] = np.concatenate([b[~w], b[w]]).astype(b.dtype)
-            wide.append(nw)
-        return wide
-
     def device_arrays(self):
-        self.pair_order()
         rec = np.stack([self.rec_off, self.rec_pos.view(np.uint32), self.rec_lenflag, self.rec_link], axis=1)
         d = {"fam_off": self.fam_off, "rec": np.ascontiguousarray(rec, dtype=np.uint32),
              "rec_win": np.ascontiguousarray(self.rec_win, dtype=np.uint32)}

@@ -48,14 +48,8 @@ constexpr int kWave = 64;
 #define SMALL_STAGE_U 4  // k_small staging: image chunk loads in flight per lane
 #endif
 constexpr int kStageU = SMALL_STAGE_U;
-#ifndef LARGE_QDMA
-#define LARGE_QDMA 0  // k_large: 1 stages the quals with LDS-DMA (global_load_lds_dwordx4; A/B arm)
-#endif
 #ifndef SMALL_QDMA
 #define SMALL_QDMA 1  // k_small stages the quals with LDS-DMA (global_load_lds_dwordx4); 0: through VGPRs
-#endif
-#ifndef SMALL_PROBE
-#define SMALL_PROBE 0  // timing probes only (wrong results): 1 no window loads, 2 no base unpack
 #endif
 #ifndef LARGE_THREADS
 #define LARGE_THREADS 256  // k_large workgroup size (a multiple of 64)
@@ -137,18 +131,10 @@ struct Tables {
 // The device copy: the LDS image above plus fgbio's per-read terms in double precision, read from
 // HBM on the rare near-tie path only: lnc[q] = ln P(correct), lne3[q] = ln P(error) / 3 of a Q base
 // after the post-UMI step, computed the way fgbio's LogProbability computes them (make_fp64).
-// k_pair's keep masks of a lane's 20-column vote window by the k columns (0..20) a read still
-// covers there: dwords [0, 5) 0xFF and [6, 11) 0x01 in each kept byte; forward windows keep bytes
-// < k, reverse ones (bytes run backwards) bytes >= 20 - k (built on the host: make_pair_masks)
-struct PairMasks {
-    uint32_t fwd[21][12];
-    uint32_t rev[21][12];
-};
 struct DevTables {
     Tables t;
     double lnc[256];
     double lne3[256];
-    PairMasks pm;
 };
 
 using bsdc_layout::ArenaLayout;
@@ -537,7 +523,6 @@ struct KParams {
     int32_t ref_chunks;       // 16-B chunks per reference window (ref_chunks(max_len))
     uint32_t ref_chunks_inv;  // ceil(2^32 / ref_chunks)
     int32_t qmin;             // bsdc_params.min_consensus_base_quality: single-strand Q below it -> (N, 2)
-    int32_t part_join;        // split families: the last part of a family to finish joins it (no k_join)
 };
 
 // (TAGS) a single-strand column's depth and errors: bytes (saturated) for every family, and the
@@ -973,10 +958,7 @@ __device__ __forceinline__ void small_family(const KParams &P, const Tables *T, 
             *reinterpret_cast<uint4 *>(qimg + 16 * k) = v;
             qor |= v.x | v.y | v.z | v.w;
         } else if (k >= nqc && k < nch) {
-            if (SMALL_PROBE == 2)
-                *reinterpret_cast<uint4 *>(bimg + 32 * (k - nqc)) = v;
-            else
-                unpack32<true>(v, bimg + 32 * (k - nqc));
+            unpack32<true>(v, bimg + 32 * (k - nqc));
         }
     };
     // lanes take qual chunks and packed-base chunks in separate rounds (the unpack runs once per
@@ -1022,7 +1004,7 @@ __device__ __forceinline__ void small_family(const KParams &P, const Tables *T, 
     // window chunk k -> (converted record k / rcn, part k % rcn); rcn and its 2^32 reciprocal are
     // launch constants (floor(k * rinv / 2^32) is exact for k, rcn < 2^16)
     const uint32_t rcn = (uint32_t)P.ref_chunks, rinv = P.ref_chunks_inv;
-    const int wtot = SMALL_PROBE == 1 ? 0 : nconv * (int)rcn;
+    const int wtot = nconv * (int)rcn;
     auto load_win = [&](int k) {
         uint4 x = make_uint4(0, 0, 0, 0);
         if (k < wtot) {
@@ -1681,813 +1663,6 @@ __global__ __launch_bounds__(kWave *kSmallMaxWaves, kSmallMinWaves) __attribute_
 }
 
 // ==========================================================================================
-// k_pair: two families per wavefront, one per 32-lane half
-// ==========================================================================================
-// k_small gives a family the whole wavefront, so its per-record phases (extend, overlap set-up,
-// source reads, descriptors) run on 8 of 64 lanes at C2 and the slow-column queue on a few; its
-// vote puts both strands of an end in one lane (4 columns per lane: a 151-column end fills 38 of
-// 64 lanes).  Here each half-wave owns one family, every per-record phase runs both families in
-// one instruction stream, and the vote gives each of the four single-strand sets (AB-R1, AB-R2,
-// BA-R1, BA-R2: independent until the duplex combine) 8 lanes of 20 columns (160 per pass, 151 of
-// 160 busy at 2x150), all four sets at once.  The single strands go to LDS rows; a queue over the
-// whole wavefront recomputes the columns that need the general call; one pass combines the ends
-// and packs.  Same arithmetic as k_small (and oracle/): fixed-point sums, the agreement tables,
-// the general call, fgbio's near-tie pick.
-constexpr int kPairCols = 20;                            // vote columns per lane
-constexpr int kPairSetLanes = 8;                         // lanes per single-strand set
-constexpr int kPairBlock = kPairCols * kPairSetLanes;    // columns per set per vote pass
-constexpr int kPairScratch = 512;                        // per-wave LDS: overlap templates | queued columns
-constexpr int kPairMaxRec = 32;                          // records of a family a half-wave holds
-#ifndef PAIR_SIMD_WAVES
-#define PAIR_SIMD_WAVES 4  // k_pair waves per SIMD its register budget is cut for (<= 128 VGPRs)
-#endif
-
-// the bits of a wave ballot that belong to this lane's half, and its rank among them
-__device__ __forceinline__ uint32_t half_bits(uint64_t m, int h) { return h ? (uint32_t)(m >> 32) : (uint32_t)m; }
-__device__ __forceinline__ int half_rank(uint64_t m, int h) {
-    const uint32_t lo = h ? 0u : (uint32_t)m, hi = h ? (uint32_t)(m >> 32) : 0u;
-    return (int)__builtin_amdgcn_mbcnt_hi(hi, __builtin_amdgcn_mbcnt_lo(lo, 0u));
-}
-// fgbio duplex combine of 4 columns whose single-strand calls (already masked to N / 2 below the
-// caller's threshold) both exist: agree -> sum, else the higher quality's base with the
-// difference, equal -> 2; capped at 93; an N or a 2 -> (N, 2) (the second half of resolve4)
-__device__ __forceinline__ void duplex4(uint32_t bA, uint32_t qA, uint32_t bB, uint32_t qB, uint32_t &ob, uint32_t &oq) {
-    const uint32_t same = ~bytes_nonzero(bA ^ bB);
-    const uint32_t dAB = (qA | 0x80808080u) - qB;
-    const uint32_t geA = expand80(dAB & 0x80808080u);
-    const uint32_t dBA = (qB | 0x80808080u) - qA;
-    const uint32_t ad = ((dAB & geA) | (dBA & ~geA)) & 0x7F7F7F7Fu;
-    const uint32_t sum = qA + qB;
-    const uint32_t over = expand80((sum + 0x22222222u) & 0x80808080u);
-    const uint32_t sum93 = (sum & ~over) | (0x5D5D5D5Du & over);
-    const uint32_t ad2 = ad | (0x02020202u & ~bytes_nonzero(ad));
-    const uint32_t rb = (bA & (same | geA)) | (bB & ~(same | geA));
-    const uint32_t rq = (sum93 & same) | (ad2 & ~same);
-    const uint32_t isN = ((bA + 0x01010101u) | (bB + 0x01010101u)) & 0x10101010u;
-    const uint32_t is2 = ~bytes_nonzero(rq ^ 0x02020202u);
-    const uint32_t nm = expand80(isN << 3) | is2;
-    ob = (rb & ~nm) | (0x0F0F0F0Fu & nm);
-    oq = (rq & ~nm) | (0x02020202u & nm);
-}
-
-// Two families on one wavefront: half h = t >> 5 runs list entry fi0 + h in arena A0 + h * arena
-// (at most 32 records each).  scr: this wavefront's kPairScratch bytes.
-template <bool TAGS>
-__device__ __forceinline__ void pair_families(const KParams &P, const Tables *T, const PairMasks *PM, uint8_t *A0,
-                                              int32_t arena, uint32_t *scr, const uint32_t *fams, int64_t fi0,
-                                              int64_t nfams, int t) {
-    const int32_t *lr2 = T->zero;  // [2][256]: row (base byte >> 4) = 1 for A/C/G/T
-    const float *thr = T->thr;
-    const uint8_t *qlo = T->qlo;
-    const int32_t *dthr = T->dthr;
-    const bsdc_family_batch &B = P.B;
-    const bool do_convert = P.mode & BSDC_MODE_CONVERT;
-    const bool do_extend = P.mode & BSDC_MODE_EXTEND;
-    const bool do_vote = P.mode & BSDC_MODE_VOTE;
-    const int max_len = B.max_len;
-    const int stop = (P.mode >> BSDC_MODE_STOP_SHIFT) & 15;  // profiling ablation (0 = full kernel)
-    const int h = t >> 5, l = t & 31;
-    const int64_t fi = fi0 + h;
-    const bool live = fi < nfams;
-    uint4 ent = make_uint4(0, 0, 0, 0);
-    if (live) ent = reinterpret_cast<const uint4 *>(fams)[fi];
-    const uint32_t fam = ent.x, r0 = ent.y;
-    const int n = (int)(ent.z & 0xFF);
-    const uint32_t img = (ent.z >> 8) * 32u;
-    const uint32_t base_g = ent.w;
-    // (the host puts a bucket's families of more than 32 records after the ones k_pair runs:
-    // bsdc_family_batch.n_small_wide; such a family here would be a host bug, and is left unwritten)
-    if (ballot(n > kPairMaxRec)) return;
-    uint8_t *A = A0 + h * arena;
-    uint8_t *bimg = A, *qimg = A + img;
-
-    // ---- staging: each half its family's record metadata, image chunks (32 per round) and the
-    // converted records' reference windows, as k_small ----
-    const bool has = l < n;
-    uint4 rc = make_uint4(0, 0, 0, 0);
-    uint2 win = make_uint2(0, 0);
-    uint32_t cinfo = 0;
-    if (has) {
-        rc = reinterpret_cast<const uint4 *>(B.rec)[r0 + l];
-        win = reinterpret_cast<const uint2 *>(B.rec_win)[r0 + l];
-        cinfo = B.cig_info[r0 + l];
-    }
-    const int nqc = (int)(img >> 4), nch = nqc + (int)(img >> 5);
-    const int rounds = (::max(rl(nch, 0), rl(nch, 32)) + 31) >> 5;
-    auto load_img = [&](int k) {
-        uint4 v = make_uint4(0, 0, 0, 0);
-        if (k < nqc)
-            v = *reinterpret_cast<const uint4 *>(B.qual + base_g + 16 * (uint32_t)k);
-        else if (k < nch)
-            v = *reinterpret_cast<const uint4 *>(B.seq + (base_g >> 1) + 16 * (uint32_t)(k - nqc));
-        return v;
-    };
-    uint32_t qor = 0;
-    auto store_img = [&](int k, uint4 v) {
-        if (k < nqc) {
-            *reinterpret_cast<uint4 *>(qimg + 16 * k) = v;
-            qor |= v.x | v.y | v.z | v.w;
-        } else if (k < nch) {
-            unpack32<true>(v, bimg + 32 * (k - nqc));
-        }
-    };
-    uint4 v[kStageU];
-#pragma unroll
-    for (int u = 0; u < kStageU; u++) v[u] = load_img(l + 32 * u);
-
-    const uint32_t gslot = rc.x;
-    int32_t pos = (int32_t)rc.y;
-    const int32_t L = (int32_t)(rc.z & 0xFFFF);
-    const uint32_t flag = rc.z >> 16;
-    uint32_t link = rc.w;
-    const bool conv = has && do_convert && (link & BSDC_LINK_CONVERT);
-    const bool cplx = has && (link & BSDC_LINK_COMPLEX);
-    if (!cplx) cinfo = 0;
-    const uint64_t conv_mask = ballot(conv);
-    const int nconv = __builtin_popcount(half_bits(conv_mask, h));
-    const int ci = half_rank(conv_mask, h);
-    int cops = (int)(cinfo & 0xFFFF);
-#pragma unroll
-    for (int o = 16; o >= 1; o >>= 1) cops += __shfl_xor(cops, o, kWave);  // (within the half)
-    const SmallLayout Lo(n, img, nconv, cops, max_len);
-    uint4 *cinf = reinterpret_cast<uint4 *>(A + Lo.cinfo);  // converted record -> {slot, L, window, valid nibbles}
-    uint8_t *refw = A + Lo.ref;
-    const int ws = Lo.ws;
-    const int rw = Lo.rw;
-    uint32_t *lc = reinterpret_cast<uint32_t *>(A + Lo.misc);
-    uint8_t *convrd = A + Lo.misc + 32;  // converted record -> tool 1's RD
-    const uint32_t slot = gslot - base_g;
-    if (conv) cinf[ci] = make_uint4(slot, (uint32_t)L, win.x, win.y);
-    if (l < 4) lc[l] = 0;
-    wave_sync();
-    const uint32_t rcn = (uint32_t)P.ref_chunks, rinv = P.ref_chunks_inv;
-    const int wtot = nconv * (int)rcn;
-    const int wrounds = (::max(rl(wtot, 0), rl(wtot, 32)) + 31) >> 5;
-    auto load_win = [&](int k) {
-        uint4 x = make_uint4(0, 0, 0, 0);
-        if (k < wtot) {
-            const uint32_t cr = __umulhi((uint32_t)k, rinv), part = (uint32_t)k - cr * rcn;
-            x = *reinterpret_cast<const uint4 *>(P.ref + ((cinf[cr].z >> 1) & ~15u) + 16 * part);
-        }
-        return x;
-    };
-    auto store_win = [&](int k, uint4 x) {
-        if (k < wtot) {
-            const uint32_t cr = __umulhi((uint32_t)k, rinv), part = (uint32_t)k - cr * rcn;
-            unpack32<false>(x, refw + cr * ws + 32 * part);
-        }
-    };
-    uint4 wv[2];
-#pragma unroll
-    for (int u = 0; u < 2; u++) wv[u] = load_win(l + 32 * u);
-#pragma unroll
-    for (int u = 0; u < kStageU; u++) store_img(l + 32 * u, v[u]);
-    for (int u0 = kStageU; u0 < rounds; u0 += kStageU) {
-#pragma unroll
-        for (int u = 0; u < kStageU; u++) v[u] = load_img(l + 32 * (u0 + u));
-#pragma unroll
-        for (int u = 0; u < kStageU; u++) store_img(l + 32 * (u0 + u), v[u]);
-    }
-#pragma unroll
-    for (int u = 0; u < 2; u++) store_win(l + 32 * u, wv[u]);
-    for (int u0 = 2; u0 < wrounds; u0 += 2) {
-#pragma unroll
-        for (int u = 0; u < 2; u++) wv[u] = load_win(l + 32 * (u0 + u));
-#pragma unroll
-        for (int u = 0; u < 2; u++) store_win(l + 32 * (u0 + u), wv[u]);
-    }
-    wave_sync();
-    if (stop == 1) return;
-
-    // ---- tool 1 (tools/1.convert_AG_to_CT.py:84-183): flattened over (converted record, 8
-    // positions), both families' records at once.  A task loads its two dwords and the next one
-    // (the original bases) before it stores: a round's loads all precede its stores, and a later
-    // round never reads a dword an earlier one wrote ----
-    int32_t start = 1, len = L;
-    bool rd = false;
-    {
-        const int T8 = (max_len + 8) >> 3;  // tasks per converted record: ceil((max_len + 1) / 8)
-        const uint32_t t8inv = (uint32_t)((((uint64_t)1 << 32) + (uint64_t)T8 - 1) / (uint64_t)T8);
-        const int ntask = nconv * T8;
-        const int crounds = (::max(rl(ntask, 0), rl(ntask, 32)) + 31) >> 5;
-        for (int u = 0; u < crounds; u++) {
-            const int k = l + 32 * u;
-            if (k >= ntask) continue;
-            const uint32_t cr = __umulhi((uint32_t)k, t8inv), j8 = (uint32_t)k - cr * (uint32_t)T8;
-            const uint4 info = cinf[cr];
-            const uint32_t s_slot = info.x;
-            const int32_t Lm = (int32_t)info.y + 1, s_avail = (int32_t)info.w;
-            const int32_t j4 = 8 * (int32_t)j8;
-            if (j4 >= Lm) continue;
-            const uint32_t m0 = lds32(bimg + s_slot + j4), m1 = lds32(bimg + s_slot + j4 + 4),
-                           m2 = lds32(bimg + s_slot + j4 + 8);
-            const uint32_t a = cr * (uint32_t)ws + (info.z & 31u) + (uint32_t)j4;
-            const uint32_t d0 = lds32(refw + (a & ~3u)), d1 = lds32(refw + (a & ~3u) + 4), d2 = lds32(refw + (a & ~3u) + 8);
-            const uint32_t sh = a & 3u;
-            uint32_t f0a = alignbyte(d1, d0, sh), f1a = sh == 3 ? d1 : alignbyte(d1, d0, sh + 1);
-            uint32_t f0b = alignbyte(d2, d1, sh), f1b = sh == 3 ? d2 : alignbyte(d2, d1, sh + 1);
-            if (j4 + 9 > s_avail) {  // past the contig end / absent contig: N (bytes at or past s_avail)
-                const int v8 = 8 * (s_avail - j4);
-                const uint32_t p0a = bytes_past(v8, false), p1a = bytes_past(v8 - 8, false);
-                const uint32_t p0b = bytes_past(v8 - 32, false), p1b = bytes_past(v8 - 40, false);
-                f0a = (f0a & ~p0a) | (0x0F0F0F0Fu & p0a);
-                f1a = (f1a & ~p1a) | (0x0F0F0F0Fu & p1a);
-                f0b = (f0b & ~p0b) | (0x0F0F0F0Fu & p0b);
-                f1b = (f1b & ~p1b) | (0x0F0F0F0Fu & p1b);
-            }
-            uint32_t ma = m0;
-            if (j4 == 0) {  // :121 seed, m[0] = ref[0] (flagged when A/C/G/T)
-                const uint32_t r0b = f0a & 0xFFu;
-                ma = (ma & ~0xFFu) | r0b | ((r0b != 0 && (r0b & (r0b - 1)) == 0) ? 0x10u : 0u);
-                qimg[s_slot] = 40;  // :174-177 'I' + quals
-            }
-            const int lastA = Lm - 1 - j4, lastB = lastA - 4;  // the record's last position has no next base
-            uint32_t nxa = 0x80808080u, nxb = 0x80808080u;
-            if (lastA >= 0 && lastA < 4) nxa &= ~(0xFFu << (8 * lastA));
-            if (lastB >= 0 && lastB < 4) nxb &= ~(0xFFu << (8 * lastB));
-            const uint32_t oa = convert4f(ma, alignbyte(m1, m0, 1), f0a, f1a, nxa);
-            const uint32_t ob = convert4f(m1, alignbyte(m2, m1, 1), f0b, f1b, nxb);
-            st32(bimg + s_slot + j4, oa);
-            if (lastB >= 0) st32(bimg + s_slot + j4 + 4, ob);
-            // :157-170 a final C before a reference G is trimmed (one task holds the last position)
-            if (lastA >= 0 && lastA < 4)
-                convrd[cr] = ((oa >> (8 * lastA)) & 0x0F) == kC && ((f1a >> (8 * lastA)) & 0x0F) == kG;
-            else if (lastB >= 0 && lastB < 4)
-                convrd[cr] = ((ob >> (8 * lastB)) & 0x0F) == kC && ((f1b >> (8 * lastB)) & 0x0F) == kG;
-        }
-    }
-    wave_sync();
-    if (conv) {
-        rd = convrd[ci] != 0;
-        start = 0;
-        len = L + 1 - (rd ? 1 : 0);
-        pos = pos - 1 > 0 ? pos - 1 : 0;
-    }
-    if (!do_convert && has && (link & BSDC_LINK_RD_IN)) rd = true;
-    if (rd) link |= kLinkRdDev;
-    if (stop == 2) return;
-
-    // ---- tool 2: gap extension of 4-record groups (tools/2.extend_gap.py:58-110) ----
-    if (do_extend) {
-        const int p = (h << 5) | (int)((link >> BSDC_LINK_PARTNER_SHIFT) & 3u);
-        const uint32_t p_slot = (uint32_t)__shfl((int)slot, p, kWave);
-        const int32_t p_start = __shfl(start, p, kWave);
-        const int32_t p_len = __shfl(len, p, kWave);
-        const bool er = has && (link & BSDC_LINK_EXT_RIGHT);
-        const bool el = has && (link & BSDC_LINK_EXT_LEFT) && rd;
-        uint32_t b0 = 0, q0 = 0, bl = 0, ql = 0;
-        if (er) {  // :70-80 the converted partner's first base / qual
-            b0 = bimg[p_slot + p_start];
-            q0 = qimg[p_slot + p_start];
-        }
-        if (el) {  // :92-101 the partner's last base / qual, after its own prepend
-            if (p_len > 0) {
-                bl = bimg[p_slot + p_start + p_len - 1];
-                ql = qimg[p_slot + p_start + p_len - 1];
-            } else {
-                bl = bimg[slot + start];
-                ql = qimg[slot + start];
-            }
-        }
-        wave_sync();  // (the partner's bytes are read before any record's are written)
-        if (er) {
-            bimg[slot + start - 1] = (uint8_t)b0;
-            qimg[slot + start - 1] = (uint8_t)q0;
-            start -= 1;
-            len += 1;
-            pos -= 1;
-        }
-        if (el) {
-            bimg[slot + start + len] = (uint8_t)bl;
-            qimg[slot + start + len] = (uint8_t)ql;
-            len += 1;
-        }
-        wave_sync();
-    }
-    int32_t reflen = len;
-    if (cplx) {
-        reflen = (int32_t)(cinfo >> 16) + (conv ? 1 : 0) - ((conv && rd) ? 1 : 0) +
-                 ((do_extend && (link & BSDC_LINK_EXT_RIGHT)) ? 1 : 0) +
-                 ((do_extend && (link & BSDC_LINK_EXT_LEFT) && rd) ? 1 : 0);
-    }
-
-    // ---- stage dump ----
-    if (P.mode & BSDC_MODE_DUMP) {
-        const int nmax = ::max(rl(n, 0), rl(n, 32));
-        for (int r = 0; r < nmax; r++) {
-            const int src = (h << 5) | r;
-            const uint32_t s_slot = (uint32_t)__shfl((int)slot, src, kWave), s_g = (uint32_t)__shfl((int)gslot, src, kWave);
-            const int32_t s_start = __shfl(start, src, kWave), s_len = __shfl(len, src, kWave);
-            if (r < n)
-                for (int j = l; j < s_len; j += 32) {
-                    P.O.dump_seq[s_g + j] = bimg[s_slot + s_start + j] & 0x0F;
-                    P.O.dump_qual[s_g + j] = qimg[s_slot + s_start + j];
-                }
-        }
-        if (has) {
-            const uint32_t gi = r0 + l;
-            P.O.dump_pos[gi] = pos;
-            P.O.dump_len[gi] = (uint16_t)len;
-            uint8_t tg = 0;
-            if (rd) tg |= 1;
-            if (conv) tg |= 2 | 4;
-            if (do_extend && (link & BSDC_LINK_EXT_RIGHT)) tg |= 4;
-            if (do_extend && (link & BSDC_LINK_EXT_LEFT) && rd) tg |= 8;
-            P.O.dump_tags[gi] = tg;
-        }
-    }
-    if (!do_vote || stop == 3) return;
-
-    // ---- overlapping-bases consensus: both families' simple templates on one list (16 lanes per
-    // template, 4 positions per lane, as k_small), complex ones (or a family with a quality byte >=
-    // 128) one template at a time on the whole wavefront ----
-    const uint32_t mate = link & BSDC_LINK_MATE_MASK;
-    const bool usable = has && (link & BSDC_LINK_USABLE);
-    const uint32_t img0 = (uint32_t)rl((int32_t)img, 0), img1 = (uint32_t)rl((int32_t)img, 32);
-    if (P.overlap) {
-        const bool mate_ok = usable && mate != BSDC_LINK_MATE_MASK && !(flag & 4);
-        const int ml = mate_ok ? ((h << 5) | (int)mate) : t;
-        const uint32_t b_link = (uint32_t)__shfl((int)link, ml, kWave), b_flag = (uint32_t)__shfl((int)flag, ml, kWave);
-        const int32_t b_pos = __shfl(pos, ml, kWave), b_reflen = __shfl(reflen, ml, kWave);
-        const uint32_t b_base = (uint32_t)__shfl((int)(slot + (uint32_t)start), ml, kWave);
-        const int32_t s0 = ::max(pos, b_pos), e0 = ::min(pos + reflen - 1, b_pos + b_reflen - 1);
-        const bool ok = mate_ok && (b_link & BSDC_LINK_USABLE) && !(b_flag & 4) && reflen > 0 && b_reflen > 0 &&
-                        s0 <= e0;
-        const bool wild = half_bits(ballot((qor & 0x80808080u) != 0), h) != 0;
-        const bool fast = ok && !((link | b_link) & BSDC_LINK_COMPLEX) && !wild;
-        uint64_t tm = ballot(ok && !fast);
-        while (tm) {
-            const int a = __builtin_ctzll(tm);
-            tm &= tm - 1;
-            const int ha = a >> 5;
-            uint8_t *ba = A0 + ha * arena;
-            uint8_t *qa_ = ba + (ha ? img1 : img0);
-            const int b = (ha << 5) | (int)rlu(mate, a);
-            const uint32_t la_ = rlu(link, a), lb_ = rlu(link, b);
-            const int32_t pa = rl(pos, a), pb = rl(pos, b), la = rl(len, a), lb = rl(len, b);
-            const int32_t ps0 = rl(s0, a), pe0 = rl(e0, a);
-            const uint32_t sa = rlu(slot, a) + (uint32_t)rl(start, a), sb = rlu(slot, b) + (uint32_t)rl(start, b);
-            const uint32_t r0a = rlu(r0, a);
-            const bool ca = la_ & BSDC_LINK_COMPLEX, cb = lb_ & BSDC_LINK_COMPLEX;
-            CigView va, vb;
-            if (ca) va = make_cigview(B, r0a + (a & 31), la_, do_convert && (la_ & BSDC_LINK_CONVERT), (la_ & kLinkRdDev) != 0, do_extend);
-            if (cb) vb = make_cigview(B, r0a + (b & 31), lb_, do_convert && (lb_ & BSDC_LINK_CONVERT), (lb_ & kLinkRdDev) != 0, do_extend);
-            for (int32_t p = ps0 + t; p <= pe0; p += 64) {
-                const int ia = ca ? read_at_ref(va, pa, la, p) : (p - pa < la ? p - pa : -1);
-                const int ib = cb ? read_at_ref(vb, pb, lb, p) : (p - pb < lb ? p - pb : -1);
-                if (ia < 0 || ib < 0) continue;
-                const uint32_t x = ba[sa + ia], y = ba[sb + ib];
-                if (x == kN || y == kN) continue;
-                const int qa = qa_[sa + ia], qb = qa_[sb + ib];
-                if (x == y) {
-                    const uint8_t q = (uint8_t)::min(qa + qb, 93);
-                    qa_[sa + ia] = q;
-                    qa_[sb + ib] = q;
-                } else if (qa > qb) {
-                    ba[sb + ib] = (uint8_t)x;
-                    qa_[sa + ia] = qa_[sb + ib] = (uint8_t)(qa - qb);
-                } else if (qb > qa) {
-                    ba[sa + ia] = (uint8_t)y;
-                    qa_[sa + ia] = qa_[sb + ib] = (uint8_t)(qb - qa);
-                } else {
-                    ba[sa + ia] = ba[sb + ib] = (uint8_t)kN;
-                    qa_[sa + ia] = qa_[sb + ib] = 2;
-                }
-            }
-        }
-        const uint64_t fm = ballot(fast);
-        const int nt = __builtin_popcountll(fm);
-        if (nt > 0) {
-            if (fast) {  // (<= 16 templates per family: 384 B of the wave's scratch)
-                const int i = mbcnt(fm);
-                scr[3 * i] = (slot + (uint32_t)start + (uint32_t)(s0 - pos)) | ((uint32_t)h << 31);
-                scr[3 * i + 1] = b_base + (uint32_t)(s0 - b_pos);
-                scr[3 * i + 2] = (uint32_t)(e0 - s0 + 1);
-            }
-            wave_sync();
-            for (int g0 = 0; g0 < nt; g0 += 4) {
-                const int g = g0 + (t >> 4);
-                if (g < nt) {
-                    const uint32_t xr = scr[3 * g], xb = scr[3 * g + 1];
-                    const int ovl = (int)scr[3 * g + 2];
-                    const uint32_t hh = xr >> 31, xa = xr & 0x7FFFFFFFu;
-                    uint8_t *bh = A0 + hh * arena;
-                    const int nd = ((int)(xa & 3u) + ovl + 3) >> 2;
-                    for (int d = t & 15; d < nd; d += 16) overlap_dw(bh, bh + (hh ? img1 : img0), xa, xb, ovl, d);
-                }
-            }
-        }
-        wave_sync();
-    }
-    if (stop == 4) return;
-
-    // ---- source reads: read-through trim, trailing-N trim, strand/end set ----
-    const bool neg = flag & 16;
-    int32_t srclen = 0;
-    uint32_t set = 0xFF;
-    if (usable) {
-        int32_t keep = len;
-        CigView cv;
-        if (cplx) cv = make_cigview(B, r0 + l, link, conv, rd, do_extend);
-        if (link & BSDC_LINK_RT) keep = readthrough_keep(B, r0 + l, flag, pos, len, reflen, cplx, &cv);
-        const uint8_t *sbp = bimg + slot + start;
-        while (keep > 0) {
-            const uint32_t bb = neg ? sbp[len - keep] : sbp[keep - 1];
-            if (bb != kN) break;
-            keep--;
-        }
-        srclen = keep;
-        if (keep > 0) {
-            const bool r1 = flag & 0x40;
-            set = (link & BSDC_LINK_AB) ? (r1 ? 0u : 1u) : (r1 ? 2u : 3u);
-        }
-    }
-
-    // ---- most-common-alignment filter (families with a non-M-only cigar; one lane per family) ----
-    const uint64_t fneed = ballot(cplx && set != 0xFF);
-    if (fneed) {
-        SMeta *meta = reinterpret_cast<SMeta *>(A + Lo.meta);
-        uint8_t *setv = A + Lo.setv;
-        uint16_t *ordv = reinterpret_cast<uint16_t *>(A + Lo.ordv);
-        uint16_t *srcl = reinterpret_cast<uint16_t *>(A + Lo.srcl);
-        if (has) {
-            meta[l].gidx = r0 + l;
-            meta[l].pos = pos;
-            meta[l].link = link;
-            meta[l].len = (uint16_t)len;
-            meta[l].flag = (uint16_t)flag;
-            srcl[l] = (uint16_t)srclen;
-            setv[l] = (uint8_t)set;
-        }
-        wave_sync();
-        if (l == 0 && half_bits(fneed, h)) {
-            uint32_t *so = reinterpret_cast<uint32_t *>(A + Lo.simp);
-            uint16_t *grp = reinterpret_cast<uint16_t *>(A + Lo.grp);
-            uint32_t *sofs = so + cops + 2 * n;
-            uint32_t fill = 0;
-            for (int r = 0; r < n; r++) {
-                sofs[r] = 0;
-                if (setv[r] == 0xFF) continue;
-                const SMeta m = meta[r];
-                const bool mc = m.link & BSDC_LINK_COMPLEX;
-                const bool mconv = do_convert && (m.link & BSDC_LINK_CONVERT);
-                CigView cv2;
-                if (mc) cv2 = make_cigview(B, m.gidx, m.link, mconv, (m.link & kLinkRdDev) != 0, do_extend);
-                const int c = simplified_cigar(&cv2, mc, m.flag & 16, srcl[r], so + fill);
-                sofs[r] = fill | ((uint32_t)c << 16);
-                fill += (uint32_t)c;
-            }
-            for (int xy = 0; xy < 2; xy++) {
-                const int s1 = xy == 0 ? 0 : 1, s2 = xy == 0 ? 3 : 2;
-                int cnt = 0;
-                for (int r = 0; r < n; r++)
-                    if (setv[r] == s1) ordv[cnt++] = (uint16_t)r;
-                for (int r = 0; r < n; r++)
-                    if (setv[r] == s2) ordv[cnt++] = (uint16_t)r;
-                filter_group(ordv, cnt, srcl, sofs, so, setv, grp, grp + 64);
-            }
-        }
-        wave_sync();
-        if (has) set = setv[l];
-        wave_sync();
-    }
-
-    // ---- read descriptors by set (forward reads first), set counts, single-strand lengths ----
-    // descriptor: column c of the source read is image byte sbase + c (forward) / sbase - c
-    // (reverse); srclen < 2^15
-    const uint32_t sbase = slot + start + (neg ? (uint32_t)(len - 1) : 0u);
-    const uint32_t desc = sbase | ((uint32_t)srclen << 16) | (neg ? 0x80000000u : 0u);
-    uint32_t *dlist = reinterpret_cast<uint32_t *>(A + Lo.lists);
-    uint32_t cnt4 = 0, nfw4 = 0, off4 = 0;  // per set, a byte each (<= 32 reads)
-    {
-        int o = 0;
-#pragma unroll
-        for (int s = 0; s < 4; s++) {
-            const uint64_t mf = ballot(set == (uint32_t)s && !neg), mr = ballot(set == (uint32_t)s && neg);
-            const int nf = __builtin_popcount(half_bits(mf, h));
-            const int nc = nf + __builtin_popcount(half_bits(mr, h));
-            if (set == (uint32_t)s) dlist[o + (neg ? nf + half_rank(mr, h) : half_rank(mf, h))] = desc;
-            cnt4 |= (uint32_t)nc << (8 * s);
-            nfw4 |= (uint32_t)nf << (8 * s);
-            off4 |= (uint32_t)o << (8 * s);
-            o += nc;
-        }
-    }
-    if (set != 0xFF) atomicMax(&lc[set], (uint32_t)srclen);
-    if (l == 0) {  // (the queue reads another half's set counts from here)
-        lc[4] = cnt4;
-        lc[5] = off4;
-    }
-    wave_sync();
-    int lcs[4];
-    bool hs[4];
-#pragma unroll
-    for (int s = 0; s < 4; s++) {
-        lcs[s] = (int)lc[s];
-        hs[s] = ((cnt4 >> (8 * s)) & 0xFFu) != 0;
-    }
-    const bool emit = live && (hs[0] || hs[3]) && (hs[1] || hs[2]);
-    int olen[2];
-#pragma unroll
-    for (int e = 0; e < 2; e++) {
-        const int sa = e == 0 ? 0 : 1, sb = e == 0 ? 3 : 2;
-        olen[e] = (hs[sa] && hs[sb]) ? ::min(lcs[sa], lcs[sb]) : hs[sa] ? lcs[sa] : hs[sb] ? lcs[sb] : 0;
-    }
-    if (stop == 5) return;
-
-    // ---- single-strand vote: lane (set sv, block bk) owns columns 20 bk .. + 19 (+ 160 per pass)
-    // of its set and walks the set's reads, forward ones then reverse ones: per read one 20-byte
-    // window of bases and of quals (6 aligned dwords each + byte align), the bytes past the read
-    // masked by PairMasks, the one-hot bases ORed, lr2[valid][q] added per column ----
-    const int32_t stride = P.O.stride;
-    uint8_t *ssb = A + Lo.ssrow;       // [4][rw] single-strand bases (plain nt16)
-    uint8_t *ssq = ssb + 4 * rw;       // [4][rw] single-strand quals
-    const uint32_t qadd = (uint32_t)(128 - P.qmin) * 0x01010101u;
-    const int sv = (l >> 3) & 3, bk = l & 7;
-    const int cntv = emit ? (int)((cnt4 >> (8 * sv)) & 0xFFu) : 0;
-    const int nfwv = emit ? (int)((nfw4 >> (8 * sv)) & 0xFFu) : 0;
-    const int offv = (int)((off4 >> (8 * sv)) & 0xFFu);
-    const int lcv = sv == 0 ? lcs[0] : sv == 1 ? lcs[1] : sv == 2 ? lcs[2] : lcs[3];
-    // columns this lane's set must produce: its own length for the tags, else the duplex length
-    const int lim = cntv == 0 ? 0 : TAGS ? lcv : (sv == 0 || sv == 3) ? olen[0] : olen[1];
-    int tfw = 0, trv = 0, lmax = 0;  // wave maxima (the per-(half, set) values sit in lanes 0, 8, .., 56)
-#pragma unroll
-    for (int q = 0; q < 8; q++) {
-        tfw = ::max(tfw, rl(nfwv, 8 * q));
-        trv = ::max(trv, rl(cntv - nfwv, 8 * q));
-        lmax = ::max(lmax, rl(lim, 8 * q));
-    }
-    const uint32_t *dl = dlist + offv;
-    if (stop != 6)
-    for (int cb = 0; cb * kPairBlock < lmax; cb++) {
-        const int c0 = kPairCols * bk + kPairBlock * cb;
-        const bool act = c0 < lim;
-        const int nfa = act ? nfwv : 0, nra = act ? cntv - nfwv : 0;
-        int32_t D[kPairCols];
-        uint32_t mf[5], mr[5], nfc[5], nrc[5];
-#pragma unroll
-        for (int j = 0; j < kPairCols; j++) D[j] = 0;
-#pragma unroll
-        for (int j = 0; j < 5; j++) mf[j] = mr[j] = nfc[j] = nrc[j] = 0;
-        for (int i = 0; i < tfw; i++) {
-            if (i < nfa) {
-                const uint32_t d = dl[i];
-                const int32_t a = (int32_t)(d & 0xFFFFu) + c0;
-                const int k = ::min(::max((int)((d >> 16) & 0x7FFFu) - c0, 0), kPairCols);
-                const uint32_t *km = PM->fwd[k];
-                const int32_t a4 = a & ~3;
-                const uint32_t sh = (uint32_t)a & 3u;
-                uint32_t W[6], Q[6];
-#pragma unroll
-                for (int j = 0; j < 6; j++) {
-                    W[j] = lds32(bimg + a4 + 4 * j);
-                    Q[j] = lds32(qimg + a4 + 4 * j);
-                }
-#pragma unroll
-                for (int j = 0; j < 5; j++) {
-                    const uint32_t b = alignbyte(W[j + 1], W[j], sh), q = alignbyte(Q[j + 1], Q[j], sh);
-                    mf[j] |= b & km[j];
-                    const uint32_t vv = (b >> 4) & km[6 + j];
-                    lookup4v(lr2, vv, q, D[4 * j], D[4 * j + 1], D[4 * j + 2], D[4 * j + 3]);
-                    if (TAGS) nfc[j] += vv;
-                }
-            }
-        }
-        for (int i = 0; i < trv; i++) {
-            if (i < nra) {
-                const uint32_t d = dl[nfa + i];
-                // the window's lowest byte; a window wholly before the image (all of it past the
-                // read) is clamped to read inside the workgroup's tables, masked
-                const int32_t a = ::max((int32_t)(d & 0xFFFFu) - c0 - (kPairCols - 1), -4096);
-                const int k = ::min(::max((int)((d >> 16) & 0x7FFFu) - c0, 0), kPairCols);
-                const uint32_t *km = PM->rev[k];
-                const int32_t a4 = a & ~3;
-                const uint32_t sh = (uint32_t)a & 3u;
-                uint32_t W[6], Q[6];
-#pragma unroll
-                for (int j = 0; j < 6; j++) {
-                    W[j] = lds32(bimg + a4 + 4 * j);
-                    Q[j] = lds32(qimg + a4 + 4 * j);
-                }
-#pragma unroll
-                for (int i2 = 0; i2 < 5; i2++) {  // memory dword i2 holds columns 4j+3 .. 4j, j = 4 - i2
-                    const int j = 4 - i2;
-                    const uint32_t b = alignbyte(W[i2 + 1], W[i2], sh), q = alignbyte(Q[i2 + 1], Q[i2], sh);
-                    mr[i2] |= b & km[i2];
-                    const uint32_t vv = (b >> 4) & km[6 + i2];
-                    lookup4v(lr2, vv, q, D[4 * j + 3], D[4 * j + 2], D[4 * j + 1], D[4 * j]);
-                    if (TAGS) nrc[i2] += vv;
-                }
-            }
-        }
-        // per column: Q from the sum alone (agreement), else slow: the general call below
-        uint32_t slow20 = 0;
-#pragma unroll
-        for (int j = 0; j < 5; j++) {
-            const int c = c0 + 4 * j;
-            const uint32_t bm = (mf[j] & 0x0F0F0F0Fu) | comp4(__builtin_bswap32(mr[4 - j] & 0x0F0F0F0Fu));
-            const uint32_t multi = bm & ((bm | 0x10101010u) - 0x01010101u);  // per byte: more than one base seen
-            uint32_t Qp = 0, negm = 0;
-#pragma unroll
-            for (int k = 0; k < 4; k++) {
-                const int32_t dsum = D[4 * j + k];
-                negm |= dsum <= cntv ? 0xFFu << (8 * k) : 0u;
-                const int32_t dd = ::min(::max(dsum, 0), (int32_t)((1 << 27) - 1));
-                const uint32_t q0 = qlo[dd >> 16];
-                Qp |= (q0 + (dd >= dthr[q0 + 1] ? 1u : 0u)) << (8 * k);
-            }
-            const uint32_t inl = ~bytes_past(8 * (lim - c), false);
-            const uint32_t slow = (bytes_nonzero(multi & 0x7F7F7F7Fu) | negm) & inl;
-            const uint32_t okq = expand80((Qp + qadd) & 0x80808080u);  // Q >= qmin
-            const uint32_t bS = (bm & okq) | (0x0F0F0F0Fu & ~okq), qS = (Qp & okq) | (0x02020202u & ~okq);
-            if (act) {
-                st32(ssb + sv * rw + c, bS);
-                st32(ssq + sv * rw + c, qS);
-            }
-            // TAGS: the single-strand read and its column statistics (fgbio's consensus tags) of
-            // the agreeing columns; a slow column's come from the queue
-            if (TAGS && act) {
-                const uint32_t wr = ~slow & ~bytes_past(8 * (lcv - c), false);
-                const uint32_t n4 = nfc[j] + __builtin_bswap32(nrc[4 - j]);
-                const int64_t at = (4 * (int64_t)fam + sv) * stride + c;
-                if (wr == 0xFFFFFFFFu) {
-                    *reinterpret_cast<uint32_t *>(P.O.ss_base + at) = bS;
-                    *reinterpret_cast<uint32_t *>(P.O.ss_qual + at) = qS;
-                    *reinterpret_cast<uint32_t *>(P.O.ss_depth + at) = n4;
-                    *reinterpret_cast<uint32_t *>(P.O.ss_err + at) = 0u;
-                } else if (wr != 0u) {
-#pragma unroll
-                    for (int k = 0; k < 4; k++) {
-                        if (!((wr >> (8 * k)) & 0xFFu)) continue;
-                        P.O.ss_base[at + k] = (uint8_t)(bS >> (8 * k));
-                        P.O.ss_qual[at + k] = (uint8_t)(qS >> (8 * k));
-                        P.O.ss_depth[at + k] = (uint8_t)(n4 >> (8 * k));
-                        P.O.ss_err[at + k] = 0;
-                    }
-                }
-            }
-            slow20 |= ((((slow >> 7) & 0x01010101u) * 0x01020408u) >> 24) << (4 * j);
-        }
-        if (stop == 7) continue;
-        // ---- queue: the slow (set, column) cells of both families, compacted over the wavefront
-        // in passes of 64; a lane per cell runs the general call (four likelihoods, up to three
-        // exp terms, fgbio's pick on a near tie) and overwrites the cell's single-strand row ----
-        const int nsl = __builtin_popcount(slow20);
-        int incl = nsl;
-#pragma unroll
-        for (int o = 1; o < 64; o <<= 1) {
-            const int y = __shfl_up(incl, (unsigned)o, kWave);
-            if (t >= o) incl += y;
-        }
-        const int total = rl(incl, 63);
-        const int excl = incl - nsl;
-        for (int p0 = 0; p0 < total; p0 += 64) {
-            {
-                uint32_t m = slow20;
-                int idx = excl;
-                while (m) {
-                    const int bit = __builtin_ctz(m);
-                    m &= m - 1;
-                    if (idx >= p0 && idx < p0 + 64) scr[idx - p0] = ((uint32_t)h << 31) | ((uint32_t)sv << 29) | (uint32_t)(c0 + bit);
-                    idx++;
-                }
-            }
-            wave_sync();
-            if (p0 + t < total) {
-                const uint32_t e = scr[t];
-                const int hh = (int)(e >> 31), s = (int)((e >> 29) & 3u), c = (int)(e & 0x1FFFFFFFu);
-                uint8_t *Ah = A0 + hh * arena;
-                const uint32_t ih = hh ? img1 : img0;
-                const int nh = hh ? rl(n, 32) : rl(n, 0);
-                const uint32_t lists_h = 2 * ih, misc_h = lists_h + (uint32_t)round16(4 * nh);
-                const uint32_t *lch = reinterpret_cast<const uint32_t *>(Ah + misc_h);
-                const int ns = (int)((lch[4] >> (8 * s)) & 0xFFu), os = (int)((lch[5] >> (8 * s)) & 0xFFu);
-                const uint32_t *dh = reinterpret_cast<const uint32_t *>(Ah + lists_h) + os;
-                const uint8_t *bh = Ah, *qh = Ah + ih;
-                int32_t D0 = 0, D1 = 0, D2 = 0, D3 = 0;
-                uint32_t n0 = 0, n1 = 0, n2 = 0, n3 = 0;  // TAGS: reads per base
-                uint32_t seen = 0;                          // bit 4 of a base byte: A/C/G/T
-                for (int i = 0; i < ns; i++) {
-                    const uint32_t d = dh[i];
-                    if (c >= (int)((d >> 16) & 0x7FFF)) continue;
-                    const uint32_t idx = (d & 0x80000000u) ? (d & 0xFFFF) - c : (d & 0xFFFF) + c;
-                    const uint32_t braw = bh[idx];
-                    seen |= braw;
-                    const int32_t vv = lr2[(braw >> 4) * 256u + qh[idx]];
-                    const uint32_t bb = (d & 0x80000000u) ? comp_nt16(braw) : (braw & 0x0F);
-                    D0 += bb == kA ? vv : 0;
-                    D1 += bb == kC ? vv : 0;
-                    D2 += bb == kG ? vv : 0;
-                    D3 += bb == kT ? vv : 0;
-                    if (TAGS) {
-                        n0 += bb == kA ? 1u : 0u;
-                        n1 += bb == kC ? 1u : 0u;
-                        n2 += bb == kG ? 1u : 0u;
-                        n3 += bb == kT ? 1u : 0u;
-                    }
-                }
-                int best = first_max4(D0, D1, D2, D3);
-                if (near_tie(D0, D1, D2, D3, best, ns))  // rare: fgbio's fp64 read-order pick
-                    best = fp64_pick(SmallDesc{dh}, ns, c, bh, qh, P.tab->lnc, P.tab->lne3);
-                const int32_t Db = best == 0 ? D0 : best == 1 ? D1 : best == 2 ? D2 : D3;
-                float S = 0.0f;  // |D| < 2^30 here (<= 32 reads)
-                if (best != 0) S += term32(D0 - Db);
-                if (best != 1) S += term32(D1 - Db);
-                if (best != 2) S += term32(D2 - Db);
-                if (best != 3) S += term32(D3 - Db);
-                const int Q = phred_of(S, thr);
-                const bool nocall = !(seen & 0x10u) || Q < P.qmin;  // no A/C/G/T read, or below the mask
-                const uint32_t vb = nocall ? kN : (1u << best), vq = nocall ? 2u : (uint32_t)Q;
-                const uint32_t R_h = misc_h + 32 + (uint32_t)round16(nh);
-                Ah[R_h + s * rw + c] = (uint8_t)vb;
-                Ah[R_h + 4 * rw + s * rw + c] = (uint8_t)vq;
-                if (TAGS) {
-                    const uint32_t depth = n0 + n1 + n2 + n3;
-                    const uint32_t nb = best == 0 ? n0 : best == 1 ? n1 : best == 2 ? n2 : n3;
-                    const uint32_t fh = (uint32_t)(hh ? rl((int32_t)fam, 32) : rl((int32_t)fam, 0));
-                    const int64_t at = (4 * (int64_t)fh + s) * stride + c;
-                    P.O.ss_base[at] = (uint8_t)vb;
-                    P.O.ss_qual[at] = (uint8_t)vq;
-                    P.O.ss_depth[at] = (uint8_t)depth;  // (<= 32 reads)
-                    P.O.ss_err[at] = (uint8_t)(depth - nb);
-                }
-            }
-            wave_sync();
-        }
-    }
-    wave_sync();
-
-    // ---- duplex combine and pack: per half, lanes 0-15 end 0 (AB-R1 + BA-R2), 16-31 end 1
-    // (AB-R2 + BA-R1), 8 columns per lane ----
-    if (emit && stop != 6 && stop != 7 && stop != 8) {
-        const int e = (l >> 4) & 1, kk = l & 15;
-        const int sa = e ? 1 : 0, sb = e ? 2 : 3;
-        const int ol = e ? olen[1] : olen[0];
-        const bool ha = hs[sa], hb = hs[sb];
-        for (int cp = 8 * kk; cp < ol; cp += 128) {
-            const uint2 bA = *reinterpret_cast<const uint2 *>(ssb + sa * rw + cp);
-            const uint2 qA = *reinterpret_cast<const uint2 *>(ssq + sa * rw + cp);
-            const uint2 bB = *reinterpret_cast<const uint2 *>(ssb + sb * rw + cp);
-            const uint2 qB = *reinterpret_cast<const uint2 *>(ssq + sb * rw + cp);
-            uint32_t ob0, oq0, ob1, oq1;
-            if (ha && hb) {
-                duplex4(bA.x, qA.x, bB.x, qB.x, ob0, oq0);
-                duplex4(bA.y, qA.y, bB.y, qB.y, ob1, oq1);
-            } else {
-                ob0 = ha ? bA.x : bB.x;
-                oq0 = ha ? qA.x : qB.x;
-                ob1 = ha ? bA.y : bB.y;
-                oq1 = ha ? qA.y : qB.y;
-            }
-            const int k8 = 8 * (ol - cp);  // columns of the 8 inside the consensus, x 8
-            const uint32_t keep0 = ~bytes_past(k8, false), keep1 = ~bytes_past(k8 - 32, false);
-            ob0 &= keep0;
-            ob1 &= keep1;
-            // bytes b0..b7 -> nibbles b0 b1 | b2 b3 | ... (BAM order, high nibble first)
-            const uint32_t t0 = (ob0 << 4) | (ob0 >> 8), t1 = (ob1 << 4) | (ob1 >> 8);
-            const uint32_t pk = __builtin_amdgcn_perm(t1, t0, 0x06040200u);
-            const int64_t so = (2 * (int64_t)fam + e) * stride;
-            *reinterpret_cast<uint32_t *>(P.O.seq + so / 2 + cp / 2) = pk;
-            *reinterpret_cast<uint2 *>(P.O.qual + so + cp) = make_uint2(oq0 & keep0, oq1 & keep1);
-        }
-    }
-    if (!live) return;
-    // single-strand lengths of the consensus tags (their columns: the vote above, emitted families)
-    if (TAGS && l < 4) P.O.ss_len[4 * fam + l] = (uint16_t)(hs[l & 3] ? lcs[l & 3] : 0);
-    if (l == 0) {
-        uint8_t st = emit ? 1 : 0;
-        if (hs[0] || hs[1]) st |= 2;
-        if (hs[2] || hs[3]) st |= 4;
-        P.O.status[fam] = st;
-        P.O.len[2 * fam] = (uint16_t)(emit ? olen[0] : 0);
-        P.O.len[2 * fam + 1] = (uint16_t)(emit ? olen[1] : 0);
-    }
-}
-
-// Two families per wavefront (k_small's size classes; the launcher's LDS holds two arenas and
-// kPairScratch bytes per wavefront after the workgroup's tables and masks).
-template <bool TAGS>
-__global__ __launch_bounds__(kWave *kSmallMaxWaves, PAIR_SIMD_WAVES) void k_pair(KParams P, const uint32_t *fams,
-                                                                              int64_t nfams, int32_t arena) {
-    extern __shared__ __attribute__((aligned(16))) uint8_t smem[];  // the wavefronts' arenas, then their scratch
-    __shared__ __attribute__((aligned(16))) Tables s_tab;
-    __shared__ __attribute__((aligned(16))) PairMasks s_pm;
-    if (((P.mode >> BSDC_MODE_STOP_SHIFT) & 15) == 15) return;  // profiling: launch cost alone
-    for (int i = threadIdx.x; i < (int)(sizeof(PairMasks) / 16); i += blockDim.x)
-        reinterpret_cast<uint4 *>(&s_pm)[i] = reinterpret_cast<const uint4 *>(&P.tab->pm)[i];
-    load_tables<kTabBytes>(&P.tab->t, reinterpret_cast<uint8_t *>(&s_tab));  // (its barrier covers the masks)
-    if (((P.mode >> BSDC_MODE_STOP_SHIFT) & 15) == 14) return;  // profiling: + the table copy
-    const int nw = blockDim.x >> 6;
-    const int w = threadIdx.x >> 6;
-    const int t = threadIdx.x & 63;
-    const int64_t fi0 = 2 * ((int64_t)blockIdx.x * nw + w);
-    uint8_t *A0 = smem + kArenaGuard + (size_t)(2 * w) * (size_t)arena;
-    uint32_t *scr = reinterpret_cast<uint32_t *>(smem + 2 * kArenaGuard + (size_t)(2 * nw) * (size_t)arena +
-                                                 (size_t)w * kPairScratch);
-    if (fi0 < nfams) pair_families<TAGS>(P, &s_tab, &s_pm, A0, arena, scr, fams, fi0, nfams, t);
-}
-
-// ==========================================================================================
 // k_large: one 256-thread workgroup per family (arena in LDS or in HBM scratch)
 // ==========================================================================================
 struct RecMeta {  // 48 B, one per record of the family, in the arena
@@ -2621,21 +1796,6 @@ __device__ void large_emit(const KParams &P, uint32_t fam, const int *cnt, const
 // The parts' sums in scratch (include/bsdc.h split_partial_off): header [part][8] int32 (set
 // reads, set lengths), then int32x4 likelihood sums and u8x4 A/C/G/T read counts per (part, set,
 // column), the column pitch being the output stride.
-template <int G, bool TAGS, bool FALLBACK>
-__device__ void join_family(const KParams &P, uint4 e0, uint4 e1, uint8_t *rows, uint8_t *tab, int *red, int *s_cnt,
-                            int *s_lc, int *s_cur, int *s_tie, int32_t *done);
-constexpr int32_t kJoinTie = 1 << 30;  // a split family's done count once its join met a near tie (part_join)
-
-// A part's sums and header: with part_join they leave by write-through (sc1) stores, so the
-// family's joiner -- the last part to finish, on any XCD -- needs only its own acquire (no release
-// fence per part); for k_join (a later dispatch) plain stores
-template <class T>
-__device__ __forceinline__ void st_part(const KParams &P, T *p, T v) {
-    if (P.part_join)
-        __hip_atomic_store(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    else
-        *p = v;
-}
 
 // a[s] for a lane-varying or loop-variable s, as selects: a dynamically indexed local array goes to
 // scratch (k_large's PART instances had 32-48 B of it)
@@ -2668,18 +1828,14 @@ struct PartSums {
         sum = reinterpret_cast<uint4 *>(b + round16(32 * np));
         cnt = reinterpret_cast<uint32_t *>(b + round16(32 * np) + 16 * 4 * np * (int64_t)pitch);
         one = reinterpret_cast<int32_t *>(b + round16(32 * np) + 20 * 4 * np * (int64_t)pitch);
-        done = reinterpret_cast<int32_t *>(b + round16(32 * np) + 24 * 4 * np * (int64_t)pitch);
     }
     int32_t *one;   // the sum of a column whose reads show one base (its count byte the only one set)
     // Without TAGS the parts keep no read counts: a column's OR of the A/C/G/T codes its reads show
     // (u8, one-hot bits) is all the join needs.  It lives at the start of the column's count row
-    // (rows keep the counts' 4 x stride spacing: a part's row shares its cache lines with no more
-    // of the other parts' rows than the count rows did -- the fused join's joiner, on another XCD,
-    // must not find another part's bytes in a line its own L2 holds)
+    // (rows keep the counts' 4 x stride spacing)
     __device__ __forceinline__ uint8_t *orb(int64_t at, int col) const {
         return reinterpret_cast<uint8_t *>(cnt) + 4 * at - 3 * (int64_t)col;
     }
-    int32_t *done;  // per split family: its parts finished (part_join; zeroed before the dispatch)
     __device__ __forceinline__ int64_t at(int64_t part, int s, int col) const { return (4 * part + s) * (int64_t)pitch + col; }
 };
 
@@ -2730,18 +1886,9 @@ __device__ void process_large(const KParams &P, uint8_t *A, uint8_t *s_tab, cons
             unpack32<false>(v, slots + 32 * (k - nqc));
         }
     };
-    // LARGE_QDMA, arena in LDS (not the HBM-scratch arenas): the quals straight into LDS, wave w's
-    // lanes taking chunks j * G + 64 w + lane, lane-linear in LDS as the DMA writes them; the
-    // packed bases go through VGPRs (unpacked)
-    const bool dma = LARGE_QDMA && __builtin_amdgcn_is_shared((const __attribute__((address_space(0))) void *)A);
-    if (dma) {
-        for (int j = 0; j * G < nqc; j++) {
-            const int kb = j * G + (tt & ~(kWave - 1));
-            if (kb + (tt & (kWave - 1)) < nqc) glds16(B.qual + off0 + 16u * (uint32_t)(kb + (tt & (kWave - 1))), qimg + 16 * kb);
-        }
-    }
-    auto chunk_of = [&](int i) { return dma ? nqc + i : i; };  // (with dma the register rounds: packed bases only)
-    const int nreg = dma ? nch - nqc : nch;
+    // (quals by LDS-DMA here measured slower: profiles/r05/README.md)
+    auto chunk_of = [&](int i) { return i; };
+    const int nreg = nch;
     uint4 v[kLStageU];
 #pragma unroll
     for (int u = 0; u < kLStageU; u++)
@@ -2789,14 +1936,6 @@ __device__ void process_large(const KParams &P, uint8_t *A, uint8_t *s_tab, cons
 #pragma unroll
         for (int u = 0; u < kLStageU; u++)
             if (k0 + u * G < nreg) store_chunk(chunk_of(k0 + u * G), v[u]);
-    }
-    if (dma) {
-        __asm__ volatile("s_waitcnt vmcnt(0)" ::: "memory");  // this thread's DMA'd quals have landed
-        __syncthreads();
-        for (int k = tt; k < nqc; k += G) {
-            const uint4 q = *reinterpret_cast<const uint4 *>(qimg + 16 * k);
-            qor |= q.x | q.y | q.z | q.w;
-        }
     }
     int cops, maxlen_f;
     block_sum_max<G>(c, ml, red, cops, maxlen_f);  // (its barrier publishes the arena and the tables)
@@ -3225,19 +2364,11 @@ __device__ void process_large(const KParams &P, uint8_t *A, uint8_t *s_tab, cons
         const PartSums ps(P);
         const int64_t at = ps.at(blockIdx.x, s, col);
         const uint32_t m = (n01 & 0xFFu) | ((n01 >> 8) & 0xFF00u) | ((n23 & 0xFFu) << 16) | ((n23 >> 16) << 24);
-        if (TAGS) st_part(P, ps.cnt + at, m);
+        if (TAGS) ps.cnt[at] = m;
         if (!TAGS || multi_base(m)) {  // (without TAGS pass B sees only multi-base columns; pass A wrote their OR)
-            uint32_t *d = reinterpret_cast<uint32_t *>(ps.sum + at);
-            if (P.part_join) {
-                st_part(P, d, (uint32_t)(int32_t)D0);
-                st_part(P, d + 1, (uint32_t)(int32_t)D1);
-                st_part(P, d + 2, (uint32_t)(int32_t)D2);
-                st_part(P, d + 3, (uint32_t)(int32_t)D3);
-            } else {
-                ps.sum[at] = make_uint4((uint32_t)(int32_t)D0, (uint32_t)(int32_t)D1, (uint32_t)(int32_t)D2, (uint32_t)(int32_t)D3);
-            }
+            ps.sum[at] = make_uint4((uint32_t)(int32_t)D0, (uint32_t)(int32_t)D1, (uint32_t)(int32_t)D2, (uint32_t)(int32_t)D3);
         } else {  // (one base or none: the others' sums are 0)
-            st_part(P, ps.one + at, (int32_t)(m & 0xFFu ? D0 : m & 0xFF00u ? D1 : m & 0xFF0000u ? D2 : D3));
+            ps.one[at] = (int32_t)(m & 0xFFu ? D0 : m & 0xFF00u ? D1 : m & 0xFF0000u ? D2 : D3);
         }
     };
     // Wavefronts by set: wave w works on set w % 4; with 8 waves (512 threads) the two waves of a
@@ -3401,20 +2532,11 @@ __device__ void process_large(const KParams &P, uint8_t *A, uint8_t *s_tab, cons
                 if (PART && c < lc) {
                     const PartSums ps(P);
                     const int64_t at = ps.at(blockIdx.x, ws, c);
-                    if (P.part_join) {
-#pragma unroll
-                        for (int j = 0; j < 4; j++) {
-                            if (TAGS) st_part(P, ps.cnt + at + j, cnt4[j]);
-                            st_part(P, ps.one + at + j, one4[j]);
-                        }
-                        if (!TAGS) st_part(P, reinterpret_cast<uint32_t *>(ps.orb(at, c)), or4);
-                    } else {
-                        if (TAGS)
-                            *reinterpret_cast<uint4 *>(ps.cnt + at) = make_uint4(cnt4[0], cnt4[1], cnt4[2], cnt4[3]);
-                        else
-                            *reinterpret_cast<uint32_t *>(ps.orb(at, c)) = or4;
-                        *reinterpret_cast<int4 *>(ps.one + at) = make_int4(one4[0], one4[1], one4[2], one4[3]);
-                    }
+                    if (TAGS)
+                        *reinterpret_cast<uint4 *>(ps.cnt + at) = make_uint4(cnt4[0], cnt4[1], cnt4[2], cnt4[3]);
+                    else
+                        *reinterpret_cast<uint32_t *>(ps.orb(at, c)) = or4;
+                    *reinterpret_cast<int4 *>(ps.one + at) = make_int4(one4[0], one4[1], one4[2], one4[3]);
                 }
             }
             if (PARTS >= 2) __syncthreads();
@@ -3574,7 +2696,7 @@ __device__ void process_large(const KParams &P, uint8_t *A, uint8_t *s_tab, cons
     __syncthreads();
     if (stop == 7) return;
     if (PART) {  // the part's set sizes and lengths; k_join does the rest
-        if (tt < 8) st_part(P, PartSums(P).head + 8 * (int64_t)blockIdx.x + tt, tt < 4 ? pick4<PART>(cnt, tt) : pick4<PART>(lcv, tt - 4));
+        if (tt < 8) PartSums(P).head[8 * (int64_t)blockIdx.x + tt] = tt < 4 ? pick4<PART>(cnt, tt) : pick4<PART>(lcv, tt - 4);
         return;
     }
 
@@ -3613,39 +2735,14 @@ __global__ __launch_bounds__(G, G == 256 ? 5 : 2) void k_large(KParams P, const 
     __syncthreads();
     uint8_t *A = IN_LDS ? smem : P.O.scratch + scratch_off + (size_t)i * (size_t)arena;
     process_large<G, TAGS, PART>(P, A, reinterpret_cast<uint8_t *>(&s_tab), lr, thr, fams[i], red, s_cnt, s_lc, s_cur);
-    if (PART && IN_LDS && P.part_join) {
-        // the family's parts count themselves done; the last one to finish adds them all up in its
-        // own arena (join_family).  The parts run on every XCD, each with its own L2: the hand-off
-        // is the agent-scope counter form of the guide's protocol with write-through (sc1) sums
-        // and header, which need no release fence -- every wave drains its stores, one lane counts
-        // after a barrier -- and one acquire by the joiner; correct for any placement of the parts
-        __shared__ int s_last, s_tie;
-        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // this wave's sums and header
-        __syncthreads();
-        const uint32_t row = fams[i].z >> 8;
-        const uint4 *sf = reinterpret_cast<const uint4 *>(P.B.split_fams);
-        const uint4 e1 = sf[2 * row + 1];
-        if (threadIdx.x == 0) {
-            const int old = __hip_atomic_fetch_add(PartSums(P).done + row, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-            s_last = old == (int)e1.y - 1;
-            if (s_last) {
-                __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
-                asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-            }
-        }
-        __syncthreads();
-        if (!s_last) return;
-        join_family<G, TAGS, false>(P, sf[2 * row], e1, smem, reinterpret_cast<uint8_t *>(&s_tab), red, s_cnt, s_lc,
-                                    s_cur, &s_tie, PartSums(P).done + row);
-    }
 }
 
 // A split family's join on one workgroup of G threads (k_join): rows = 8 x stride bytes of LDS for
 // its single-strand rows + kJoinParts x 8 bytes for the parts' set lengths, tab = the TablesL copy.
 constexpr int kJoinParts = 256;
-template <int G, bool TAGS, bool FALLBACK>
+template <int G, bool TAGS>
 __device__ void join_family(const KParams &P, uint4 e0, uint4 e1, uint8_t *rows, uint8_t *tab, int *red, int *s_cnt,
-                            int *s_lc, int *s_cur, int *s_tie, int32_t *done) {
+                            int *s_lc, int *s_cur, int *s_tie) {
     const int tt = threadIdx.x;
     const TablesL &T = *reinterpret_cast<const TablesL *>(tab);
     const PartSums ps(P);
@@ -3767,14 +2864,9 @@ __device__ void join_family(const KParams &P, uint4 e0, uint4 e1, uint8_t *rows,
     }
     __syncthreads();
     if (*s_tie) {  // (rare) the whole family in its HBM arena, fgbio's pick on the near ties
-        if (FALLBACK) {
-            if (tt == 0) s_cnt[0] = 0;
-            __syncthreads();
-            process_large<G, TAGS, false>(P, P.O.scratch + 16 * (int64_t)e1.z, tab, T.lr, T.thr, e0, red, s_cnt, s_lc,
-                                          s_cur);
-        } else if (tt == 0) {  // (the part that joins: k_join runs it after the parts)
-            *done = kJoinTie;
-        }
+        if (tt == 0) s_cnt[0] = 0;
+        __syncthreads();
+        process_large<G, TAGS, false>(P, P.O.scratch + 16 * (int64_t)e1.z, tab, T.lr, T.thr, e0, red, s_cnt, s_lc, s_cur);
         return;
     }
     large_emit<G, TAGS>(P, e0.x, cnt, lcv, ssb, ssq, pitch, true);
@@ -3796,26 +2888,8 @@ __global__ __launch_bounds__(kJoinThreads, 1024 / kJoinThreads) void k_join(KPar
     const int64_t i = blockIdx.x;
     if (i >= nsf) return;
     load_tables<kTabBytesL>(&P.tab->t, reinterpret_cast<uint8_t *>(&s_tab));
-    join_family<G, TAGS, true>(P, sfams[2 * i], sfams[2 * i + 1], smem, reinterpret_cast<uint8_t *>(&s_tab), red, s_cnt,
-                               s_lc, s_cur, &s_tie, nullptr);
-}
-
-// part_join: the split families whose join (in their last part) met a near tie run whole in their
-// HBM fallback arenas, fgbio's pick on the ties; every other workgroup exits at once
-template <bool TAGS>
-__global__ __launch_bounds__(kJoinThreads, 1024 / kJoinThreads) void k_tie(KParams P, const uint4 *sfams, int64_t nsf) {
-    constexpr int G = kJoinThreads;
-    __shared__ __attribute__((aligned(16))) TablesL s_tab;
-    __shared__ int red[2 * G / kWave];
-    __shared__ int s_cnt[4], s_lc[4], s_cur[8];
-    const int64_t i = blockIdx.x;
-    if (i >= nsf || PartSums(P).done[i] != kJoinTie) return;
-    load_tables<kTabBytesL>(&P.tab->t, reinterpret_cast<uint8_t *>(&s_tab));
-    if (threadIdx.x == 0) s_cnt[0] = 0;
-    __syncthreads();
-    const uint4 e0 = sfams[2 * i], e1 = sfams[2 * i + 1];
-    process_large<G, TAGS, false>(P, P.O.scratch + 16 * (int64_t)e1.z, reinterpret_cast<uint8_t *>(&s_tab), s_tab.lr,
-                                  s_tab.thr, e0, red, s_cnt, s_lc, s_cur);
+    join_family<G, TAGS>(P, sfams[2 * i], sfams[2 * i + 1], smem, reinterpret_cast<uint8_t *>(&s_tab), red, s_cnt,
+                         s_lc, s_cur, &s_tie);
 }
 
 }  // namespace
@@ -3843,16 +2917,6 @@ struct bsdc_ctx {
     // caller's stream by events, so one dispatch's tail overlaps the next
     hipStream_t side[kForkStreams] = {};
     hipEvent_t ev_fork = nullptr, ev_join[kForkStreams] = {};
-    // small families: one per wavefront (k_small, the default) or two (k_pair; BSDC_SMALL_KERNEL=pair
-    // in the environment at context creation).  k_pair is parity-green but measured slower on C2
-    // (3.52 vs 3.09 ms, profiles/r05/README.md): kept as the A/B arm
-    bool pair = false;
-    // (BSDC_SMALL_ORDER=work) the small buckets' dispatches in descending families x arena, the
-    // longest first, instead of by arena size (A/B knob)
-    bool small_by_work = false;
-    // split families: a k_join dispatch after all the parts (default), or the last part of each
-    // family joins it (BSDC_SPLIT_JOIN=part: measured slower, profiles/r05/README.md)
-    bool part_join = false;
 };
 
 static float det_expf_host(float x) {
@@ -3963,23 +3027,6 @@ static void make_fp64(double post, double *lnc, double *lne3) {
     }
 }
 
-static void make_pair_masks(PairMasks &pm) {
-    for (int dir = 0; dir < 2; dir++)
-        for (int k = 0; k <= kPairCols; k++)
-            for (int w = 0; w < 12; w++) {
-                uint32_t v = 0;
-                if (w < 5 || (w >= 6 && w < 11)) {
-                    const int j = w < 5 ? w : w - 6;
-                    const uint32_t byte = w < 5 ? 0xFFu : 0x01u;
-                    for (int b = 0; b < 4; b++) {
-                        const int p = 4 * j + b;
-                        if (dir == 0 ? p < k : p >= kPairCols - k) v |= byte << (8 * b);
-                    }
-                }
-                (dir == 0 ? pm.fwd : pm.rev)[k][w] = v;
-            }
-}
-
 #define HIP_OK(ctx, call)                                                                     \
     do {                                                                                      \
         hipError_t e_ = (call);                                                               \
@@ -4080,17 +3127,8 @@ int32_t bsdc_ctx_create(int32_t device, const bsdc_params *params, bsdc_ctx **ou
     bsdc_ctx *c = new bsdc_ctx();
     c->device = device;
     c->params = *params;
-    {
-        const char *sk = getenv("BSDC_SMALL_KERNEL");
-        c->pair = sk && std::string(sk) == "pair";
-        const char *so = getenv("BSDC_SMALL_ORDER");
-        c->small_by_work = so && std::string(so) == "work";
-        const char *sj = getenv("BSDC_SPLIT_JOIN");
-        c->part_join = sj && std::string(sj) == "part";
-    }
     make_tables(params->error_rate_pre_umi, params->error_rate_post_umi, c->host_tab.t);
     make_fp64(params->error_rate_post_umi, c->host_tab.lnc, c->host_tab.lne3);
-    make_pair_masks(c->host_tab.pm);
     if (hipSetDevice(device) != hipSuccess || hipMalloc(&c->dev_tab, sizeof(DevTables)) != hipSuccess ||
         hipMemcpy(c->dev_tab, &c->host_tab, sizeof(DevTables), hipMemcpyHostToDevice) != hipSuccess) {
         bsdc_ctx_destroy(c);
@@ -4173,7 +3211,7 @@ int32_t bsdc_run(bsdc_ctx *c, const bsdc_family_batch *b, bsdc_consensus *o, int
     for (int q = 0; q < BSDC_SMALL_BUCKETS; q++) {
         if (b->n_small[q] > 0 &&
             (b->small_arena[q] % 16 || b->small_arena[q] <= 0 ||
-             (size_t)kTabBytes + sizeof(PairMasks) + 2 * (size_t)kArenaGuard + 2 * (size_t)b->small_arena[q] + kPairScratch > kLdsBytes)) {
+             (size_t)kTabBytes + 2 * (size_t)kArenaGuard + 4 * (size_t)b->small_arena[q] > kLdsBytes)) {
             c->err = "bad small arena size";
             return BSDC_EINVAL;
         }
@@ -4207,7 +3245,6 @@ int32_t bsdc_run(bsdc_ctx *c, const bsdc_family_batch *b, bsdc_consensus *o, int
     P.ref_chunks = ref_chunks(b->max_len);
     P.ref_chunks_inv = (uint32_t)((((uint64_t)1 << 32) + (uint64_t)P.ref_chunks - 1) / (uint64_t)P.ref_chunks);
     P.qmin = c->params.min_consensus_base_quality;
-    P.part_join = 0;
     // the dispatches: on `s`, or (BSDC_FORK) spread over the side streams (created with the
     // context) after an event on `s`
     int nd = 0, used = 0;
@@ -4248,35 +3285,6 @@ int32_t bsdc_run(bsdc_ctx *c, const bsdc_family_batch *b, bsdc_consensus *o, int
         // BSDC_MODE_VOTE (the tools-only launches dump tool-2 records and stop before it) or with a
         // profiling stop knob (the parts return early) that scratch is never written, so no join
         const bool join = (mode & BSDC_MODE_VOTE) && ((mode >> BSDC_MODE_STOP_SHIFT) & 15) == 0;
-        // (BSDC_SPLIT_JOIN=part) the last part of each family joins it in its own arena, overlapping
-        // the other parts: no k_join dispatch waiting for every part.  Its done counters are zeroed
-        // first
-        if (join && c->part_join && (size_t)a >= jl) {
-            KParams Pj = P;
-            Pj.part_join = 1;
-            const int64_t np = b->n_split_parts;
-            uint8_t *done = o->scratch + b->split_partial_off + round16(32 * np) + 24 * 4 * np * (int64_t)o->stride;
-            hipError_t e = hipMemsetAsync(done, 0, 4 * (size_t)b->n_split_fams, ls);
-            if (e != hipSuccess) {
-                fail(e, "hipMemsetAsync(done)");
-                return;
-            }
-            // then k_tie for the families whose join met a near tie (the rest exit at once)
-            if (tg) {
-                hipLaunchKernelGGL((k_large<true, kLargeThreads, true, true>), dim3((unsigned)b->n_split_parts),
-                                   dim3(kLargeThreads), (size_t)a, ls, Pj, pf, b->n_split_parts, a, (int64_t)0);
-                hipLaunchKernelGGL((k_tie<true>), dim3((unsigned)b->n_split_fams), dim3(kJoinThreads), 0, ls, Pj, sf,
-                                   b->n_split_fams);
-            } else {
-                hipLaunchKernelGGL((k_large<true, kLargeThreads, false, true>), dim3((unsigned)b->n_split_parts),
-                                   dim3(kLargeThreads), (size_t)a, ls, Pj, pf, b->n_split_parts, a, (int64_t)0);
-                hipLaunchKernelGGL((k_tie<false>), dim3((unsigned)b->n_split_fams), dim3(kJoinThreads), 0, ls, Pj, sf,
-                                   b->n_split_fams);
-            }
-            e = hipGetLastError();
-            if (e != hipSuccess) fail(e, "split launch");
-            return;
-        }
         if (tg) {
             hipLaunchKernelGGL((k_large<true, kLargeThreads, true, true>), dim3((unsigned)b->n_split_parts), dim3(kLargeThreads),
                                (size_t)a, ls, P, pf, b->n_split_parts, a, (int64_t)0);
@@ -4295,59 +3303,10 @@ int32_t bsdc_run(bsdc_ctx *c, const bsdc_family_batch *b, bsdc_consensus *o, int
     };
     auto launch_small_all = [&]() {
     if (!(mode & BSDC_MODE_SKIP_SMALL) && rc == 0) {
-        int64_t fstart[BSDC_SMALL_BUCKETS];
-        int order[BSDC_SMALL_BUCKETS];
-        {
-            int64_t o = 0;
-            for (int q = 0; q < BSDC_SMALL_BUCKETS; q++) {
-                fstart[q] = o;
-                o += 4 * b->n_small[q];
-                order[q] = q;
-            }
-        }
-        if (c->small_by_work)
-            std::stable_sort(order, order + BSDC_SMALL_BUCKETS, [&](int x, int y) {
-                return b->n_small[x] * b->small_arena[x] > b->n_small[y] * b->small_arena[y];
-            });
-        for (int i = 0; i < BSDC_SMALL_BUCKETS && rc == 0; i++) {
-            const int q = order[i];
-            const uint32_t *f = b->small_fams + fstart[q];
-            const int64_t nall = b->n_small[q];
-            const int64_t nwide = c->pair ? std::min<int64_t>(std::max<int64_t>(b->n_small_wide[q], 0), nall) : 0;
-            int64_t nf = nall - nwide;  // k_pair: the first nall - nwide entries (all of them without c->pair: k_small)
-            if (nf > 0 && c->pair) {
-                // two families per wavefront; 1, 2, 4 or 8 wavefronts per workgroup (they share the
-                // tables and masks), whichever keeps more families resident per CU (LDS, and the
-                // register budget's PAIR_SIMD_WAVES per SIMD); the smaller on a tie
-                const int64_t a = b->small_arena[q];
-                const int64_t per = 2 * a + kPairScratch, stat = kTabBytes + (int64_t)sizeof(PairMasks) + 2 * kArenaGuard;
-                int nw = 1;
-                int64_t best = 0;
-                for (int cand = 1; cand <= 8; cand *= 2) {
-                    const int64_t res = cand * std::min<int64_t>(4 * PAIR_SIMD_WAVES / cand, kLdsBytes / (stat + cand * per));
-                    if (res > best) {
-                        best = res;
-                        nw = cand;
-                    }
-                }
-                const size_t lds = (size_t)nw * (size_t)per + 2 * (size_t)kArenaGuard;  // + the static tables / masks
-                const int64_t blocks = (nf + 2 * nw - 1) / (2 * nw);
-                const hipStream_t ls = next_stream();
-                if (rc) break;
-                if (mode & BSDC_MODE_TAGS)
-                    hipLaunchKernelGGL(k_pair<true>, dim3((unsigned)blocks), dim3(kWave * nw), lds, ls, P, f, nf,
-                                       b->small_arena[q]);
-                else
-                    hipLaunchKernelGGL(k_pair<false>, dim3((unsigned)blocks), dim3(kWave * nw), lds, ls, P, f, nf,
-                                       b->small_arena[q]);
-                const hipError_t e = hipGetLastError();
-                if (e != hipSuccess) fail(e, "k_pair launch");
-            }
-            if (c->pair) {  // then the wide tail, one family per wavefront
-                f += 4 * nf;
-                nf = nwide;
-            }
-            if (nf > 0 && rc == 0) {
+        const uint32_t *f = b->small_fams;
+        for (int q = 0; q < BSDC_SMALL_BUCKETS && rc == 0; q++) {
+            const int64_t nf = b->n_small[q];
+            if (nf > 0) {
                 // wavefronts per workgroup (they share one copy of the tables): 4 or 8, whichever
                 // keeps more wavefronts resident per CU; the smaller on a tie
                 // (a workgroup's wavefronts spread over the 4 SIMDs: at most kSmallSimdWaves each)
@@ -4356,19 +3315,18 @@ int32_t bsdc_run(bsdc_ctx *c, const bsdc_family_batch *b, bsdc_consensus *o, int
                 const int64_t w4 = 4 * std::min<int64_t>(kSmallSimdWaves, kLdsBytes / (kTabBytes + g2 + 4 * a));
                 const int64_t w8 = 8 * std::min<int64_t>(kSmallSimdWaves / 2, kLdsBytes / (kTabBytes + g2 + 8 * a));
                 const int nw = w8 > w4 ? 8 : 4;
-                const size_t lds = (size_t)nw * (size_t)b->small_arena[q] + (size_t)g2;  // + the static tables
+                const size_t lds = (size_t)nw * (size_t)a + (size_t)g2;  // + the static tables
                 const int64_t blocks = (nf + nw - 1) / nw;
                 const hipStream_t ls = next_stream();
                 if (rc) break;
                 if (mode & BSDC_MODE_TAGS)
-                    hipLaunchKernelGGL(k_small<true>, dim3((unsigned)blocks), dim3(kWave * nw), lds, ls, P, f, nf,
-                                       b->small_arena[q]);
+                    hipLaunchKernelGGL(k_small<true>, dim3((unsigned)blocks), dim3(kWave * nw), lds, ls, P, f, nf, b->small_arena[q]);
                 else
-                    hipLaunchKernelGGL(k_small<false>, dim3((unsigned)blocks), dim3(kWave * nw), lds, ls, P, f, nf,
-                                       b->small_arena[q]);
+                    hipLaunchKernelGGL(k_small<false>, dim3((unsigned)blocks), dim3(kWave * nw), lds, ls, P, f, nf, b->small_arena[q]);
                 const hipError_t e = hipGetLastError();
                 if (e != hipSuccess) fail(e, "k_small launch");
             }
+            f += 4 * nf;
         }
     }
     };

@@ -112,10 +112,8 @@ class DeviceBatch:
             setattr(b, k, _dptr(self.t[k]))
         b.n_split_parts, b.n_split_fams = int(fb.split_parts.shape[0]), int(fb.split_fams.shape[0])
         b.split_part_arena, b.split_partial_off = int(fb.split_part_arena), int(poff)
-        wide = fb.pair_order()  # (device_arrays above already put them last)
         for q in range(_lib.SMALL_BUCKETS):
             b.n_small[q] = int(fb.small_buckets[q].shape[0])
-            b.n_small_wide[q] = int(wide[q])
             b.small_arena[q] = int(fb.small_arenas[q])
         for q in range(_lib.LARGE_BUCKETS):
             b.n_large[q] = int(fb.large_buckets[q].shape[0])

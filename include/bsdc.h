@@ -26,7 +26,7 @@
 extern "C" {
 #endif
 
-#define BSDC_ABI_VERSION 14
+#define BSDC_ABI_VERSION 15
 #define BSDC_SMALL_BUCKETS 8
 #define BSDC_LARGE_BUCKETS 6
 #define BSDC_LARGE_LDS_MAX 158912 /* LDS arena bytes one large-family workgroup may use */ /* LDS arena size classes of the wavefront-per-family kernel */
@@ -113,11 +113,7 @@ typedef struct {
                                     lengths), then [part][4][stride] int32x4 sums, [part][4][stride] u8x4
                                     counts (without BSDC_MODE_TAGS: byte 0..stride-1 of each count row
                                     holds the column's OR of one-hot A/C/G/T codes instead), [part][4]
-                                    [stride] int32 one-base sums, then (ABI 14)
-                                    [n_split_fams] int32 parts done: the last part of a family joins it */
-    int64_t n_small_wide[BSDC_SMALL_BUCKETS]; /* (ABI 13) the LAST n_small_wide[q] entries of small bucket q
-                                    have more than 32 records: they run one per wavefront (k_small), the
-                                    others two per wavefront (k_pair, a half-wave each) */
+                                    [stride] int32 one-base sums */
 } bsdc_family_batch;
 
 /* Outputs (device pointers).  Consensus slot (f, end) holds `stride` bases. */

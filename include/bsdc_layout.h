@@ -21,27 +21,19 @@ constexpr int kRecMetaBytes = 48;  // k_large's per-record metadata (RecMeta)
 // part's int64 sums (32), ORs (4) and A/C/G/T read counts (8, the tags)
 constexpr int kVoteRegionPerCol = 44;
 
-// k_pair's single-strand rows: 20 columns per lane, 8 lanes per set, so a row is at least the
-// consensus length rounded up to 20 (and to 16, for the 8-column reads of the duplex pass)
-BSDC_HD inline int32_t pair_row(int max_len) { return (int32_t)round16((max_len + 2 + 19) / 20 * 20); }
-
-// Arena of one small family (k_small: one per wavefront; k_pair: two per wavefront, the same
-// layout).  Regions live only as long as their phase and share space:
+// Arena of one small family (k_small: one per wavefront).  Regions live only as long as their
+// phase and share space:
 //   bimg, qimg  the family image, bases / quals (whole kernel)
 //   lists       reference-window starts (staging) -> read descriptors (vote), 4 B per record
-//   misc        consensus lengths lc[4] (u32); k_small: converted record -> lane (u8);
-//               k_pair: per-set read counts, offsets, forward counts (u8 x 4 each), then per
-//               converted record tool 1's RD (u8)
-//   R           k_pair's converted-record info (uint4 each), then reference windows (staging,
-//               convert) | alignment-filter scratch (source reads) | duplex rows + queued columns
-//               (k_small's vote) | the four single-strand rows, bases then quals (k_pair's vote)
+//   misc        consensus lengths lc[4] (u32), then converted record -> lane (u8)
+//   R           reference windows (staging, convert) | alignment-filter scratch (source reads) |
+//               duplex rows + queued columns (vote)
 struct SmallLayout {
-    uint32_t bimg, qimg, lists, misc, cinfo, ref, meta, setv, ordv, srcl, simp, grp, outb, outq, squeue, ssrow, total;
-    int32_t ws, ow, rw;
+    uint32_t bimg, qimg, lists, misc, ref, meta, setv, ordv, srcl, simp, grp, outb, outq, squeue, total;
+    int32_t ws, ow;
     BSDC_HD SmallLayout(int n, int64_t img, int nconv, int64_t cops, int max_len) {
         ws = 32 * ref_chunks(max_len);
         ow = (int32_t)round16(max_len + 2);
-        rw = pair_row(max_len);
         int64_t o = 0;
         bimg = (uint32_t)o;
         o += img;
@@ -49,12 +41,11 @@ struct SmallLayout {
         o += img;
         lists = (uint32_t)o;
         o += round16(4 * (int64_t)n);
-        misc = (uint32_t)o;  // lc[4] u32, then 16 B of set counts (k_pair), then a byte per record
-        o += 32 + round16(n);
+        misc = (uint32_t)o;  // lc[4] u32, then a byte per record
+        o += 16 + round16(n);
         const int64_t R = o;
-        cinfo = (uint32_t)R;
-        ref = (uint32_t)(R + 16 * (int64_t)nconv);
-        const int64_t e_ref = R + (int64_t)nconv * (ws + 16);
+        ref = (uint32_t)R;
+        const int64_t e_ref = R + (int64_t)nconv * ws;
         meta = (uint32_t)R;  // SMeta per record
         setv = meta + (uint32_t)round16(16 * (int64_t)n);
         ordv = setv + (uint32_t)round16(n);
@@ -64,9 +55,8 @@ struct SmallLayout {
         const int64_t e_f = (int64_t)grp + (cops > 0 ? 256 : 0);  // filter_group's 2 x 64 u16
         outb = (uint32_t)R;  // duplex bases, 2 ends
         outq = (uint32_t)(R + 2 * (int64_t)ow);
-        squeue = (uint32_t)(R + 4 * (int64_t)ow);  // queued (end, column), u16
-        ssrow = (uint32_t)R;  // k_pair: [4][rw] single-strand bases, then [4][rw] quals
-        const int64_t e_v = R + 8 * (int64_t)rw;  // (rw >= ow)
+        squeue = (uint32_t)(R + 4 * (int64_t)ow);  // queued (end, column), u16: at most 2 ow of them
+        const int64_t e_v = R + 8 * (int64_t)ow;
         int64_t e = e_ref > e_f ? e_ref : e_f;
         total = (uint32_t)(e > e_v ? e : e_v);
     }

@@ -112,8 +112,8 @@ def test_split_part_records_cover_each_family_once(monkeypatch):
 
 def test_route_small_cap_by_family_mix(monkeypatch):
     """route_small_cap: deep families (C3: most small-family records in arenas above 16 KB) go to
-    k_large from 16 KB on; shallow and skewed mixes (C2, C4) keep the 24 KB cap; explicit caps and
-    BSDC_SMALL_ROUTE=0 turn it off"""
+    k_large from 16 KB on; shallow and skewed mixes (C2, C4) keep the 24 KB cap; SMALL_ROUTE = False
+    turns it off"""
     from bsseqconsensusreads_amd import synth
     got = {}
     for cfg, n in (("C2", 20000), ("C3", 3000), ("C4", 20000)):

@@ -137,26 +137,6 @@ def test_messy_records_vs_oracle(engine):
     assert_ss_equal(cons, ref, "messy")
 
 
-@pytest.mark.parametrize("tags", [True, False])
-def test_pair_small_kernel_vs_oracle(monkeypatch, tags):
-    """k_pair (two small families per wavefront; BSDC_SMALL_KERNEL=pair, the A/B arm of k_small)
-    on clean and messy C2 families, with and without the tag outputs"""
-    from bsseqconsensusreads_amd.device import Engine
-    monkeypatch.setenv("BSDC_SMALL_KERNEL", "pair")
-    eng = Engine(0)
-    try:
-        s = synth.generate("C2", 2000, seed=13, device="cpu", genome_len=300_000)
-        for what, raw in (("clean", s.raw), ("messy", synth.messify(s.raw, frac=0.25, seed=4))):
-            eng.load_reference(s.ref)
-            cons, _ = pipeline.run_step5(eng, raw, tags=tags)
-            ref = oracle.run(raw, s.ref, threads=8)
-            assert_consensus_equal(cons, ref, "pair " + what)
-            if tags:
-                assert_ss_equal(cons, ref, "pair " + what)
-    finally:
-        eng.close()
-
-
 @pytest.mark.parametrize("read_len,trim", [(100, 0.0), (250, 0.0), (150, 0.4), (300, 0.2)])
 def test_read_lengths_vs_oracle(engine, read_len, trim):
     """2x100 / 2x250 / 2x300 runs and adapter-trimmed reads of mixed lengths (columns past a read's
