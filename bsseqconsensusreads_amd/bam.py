@@ -22,7 +22,7 @@ from __future__ import annotations
 import ctypes as C
 import os
 from dataclasses import dataclass
-from typing import List, Optional, Tuple
+from typing import List, Optional, Sequence, Tuple
 
 import numpy as np
 
@@ -30,7 +30,7 @@ from . import records as R
 
 IO_LIB_PATH = os.environ.get("BSDC_IO_LIB_PATH") or os.path.join(os.path.dirname(os.path.abspath(__file__)),
                                                                  "libbsdc_io.so")
-BSDC_IO_ABI_VERSION = 11
+BSDC_IO_ABI_VERSION = 12
 _P = C.c_void_p
 
 
@@ -143,8 +143,12 @@ def _load():
     lib.bsdc_bam_stream_set_owner.restype = C.c_int32
     lib.bsdc_bam_stream_spill.argtypes = [_P, _P]
     lib.bsdc_bam_stream_spill.restype = C.c_int64
-    lib.bsdc_bam_stream_chunk_contig.argtypes = [_P]
-    lib.bsdc_bam_stream_chunk_contig.restype = C.c_int64
+    lib.bsdc_bam_stream_set_defer.argtypes = [_P, C.c_int64]
+    lib.bsdc_bam_stream_set_defer.restype = C.c_int32
+    lib.bsdc_bam_stream_splices.argtypes = [_P, _P]
+    lib.bsdc_bam_stream_splices.restype = C.c_int64
+    lib.bsdc_bam_rec_keys.argtypes = [_P, _P]
+    lib.bsdc_bam_rec_keys.restype = C.c_int32
     lib.bsdc_bam_writer_flush.argtypes = [_P, C.c_int32]
     lib.bsdc_bam_writer_flush.restype = C.c_int32
     lib.bsdc_bam_writer_tell.argtypes = [_P]
@@ -322,6 +326,11 @@ def read_bam(path: str, threads: int = 0):
 
 DEFAULT_CHUNK_BYTES = 64 << 20  # uncompressed record bytes per stream chunk (about 0.23M records)
 DEFAULT_SLACK = 10_000           # positions: > any template's span (fragment + clips)
+# a template whose mate lies further than this (or on another contig, unmapped or absent) is
+# deferred: it leaves the stream for the spill, whose families are spliced in at their keys
+# (bsdc_bam_stream_set_defer); half the slack, so that no rank window misses a near template's end
+DEFAULT_DEFER_SPAN = DEFAULT_SLACK // 2
+DEFER_MARGIN = 12  # kDeferMargin (csrc/bsdc_io.cpp): 3 x kKeyDelta
 
 
 def read_bam_header(path: str) -> BamHeader:
@@ -348,6 +357,9 @@ class StreamChunk:
 
     def __init__(self, lib, st, h, path: str):
         self._lib, self._st, self._h, self._path = lib, st, h, path
+        self.keys = False      # decode() also fills RawRecords.tc_key (bsdc_bam_rec_keys)
+        self.splices = None    # int64 [k, 2]: deferred keys to cut this chunk's output before
+        self.spill = b""       # spill entries (bsdc_bam_stream_spill) since the chunk before
 
     def decode(self, threads: int = 0, timing: Optional[dict] = None, pool: Optional[BufferPool] = None):
         """-> (BamHeader, RawRecords); `timing`: seconds added under "parse" (records, tags,
@@ -361,6 +373,11 @@ class StreamChunk:
                 raise OSError("%s: %s" % (self._path, lib.bsdc_io_last_error().decode()))
             t1 = time.perf_counter()
             out = _decode(lib, h, self._path, pool)
+            if self.keys:  # the records' coarse TemplateCoordinate keys (splicing deferred families)
+                kk = np.zeros(2 * max(out[1].n, 1), np.int64)
+                if lib.bsdc_bam_rec_keys(h, _ptr(kk)) != 0:
+                    raise OSError("%s: %s" % (self._path, lib.bsdc_io_last_error().decode()))
+                out[1].tc_key = kk[:2 * out[1].n].reshape(-1, 2)
             if timing is not None:
                 timing["parse"] = timing.get("parse", 0.0) + t1 - t0
                 timing["copy"] = timing.get("copy", 0.0) + time.perf_counter() - t1
@@ -395,11 +412,12 @@ def find_cut(path: str, start: int, threads: int = 0, min_span: Optional[int] = 
             "coord": int(out[6]), "slack": int(slack)}
 
 
-OWN_STOP_FOREIGN, OWN_SPILL_CROSS, OWN_CONTIG_CHUNKS = 1, 2, 4  # include/bsdc_io.h BSDC_OWN_*
+OWN_STOP_FOREIGN = 1  # include/bsdc_io.h BSDC_OWN_*
 
 
 def _stream_spill(lib, st) -> bytes:
-    """The stream's spilled raw records since the last call (bsdc_bam_stream_spill)."""
+    """The stream's spill entries since the last call (bsdc_bam_stream_spill: per record an int64
+    coordinate, an int64 file sequence number, the block_size-prefixed record)."""
     n = int(lib.bsdc_bam_stream_spill(st, None))
     if n == 0:
         return b""
@@ -408,8 +426,40 @@ def _stream_spill(lib, st) -> bytes:
     return buf.tobytes()
 
 
+def _stream_splices(lib, st) -> np.ndarray:
+    """The deferred keys the last chunk reported (bsdc_bam_stream_splices) -> int64 [k, 2]."""
+    n = int(lib.bsdc_bam_stream_splices(st, None))
+    out = np.zeros((max(n, 1), 2), np.int64)
+    if n:
+        lib.bsdc_bam_stream_splices(st, _ptr(out))
+    return out[:n]
+
+
+def spill_sorted_records(data: bytes) -> bytes:
+    """Spill entries (_stream_spill, possibly several streams' concatenated) -> their records in
+    file order: sorted by (coordinate, sequence), the stable order of the input for equal pairs."""
+    if not data:
+        return b""
+    a = np.frombuffer(data, np.uint8)
+    offs, p = [], 0
+    n = a.shape[0]
+    while p < n:  # (entries: 16-byte key, 4-byte block_size, the rest of the record)
+        offs.append(p)
+        p += 20 + int(a[p + 16:p + 20].view(np.uint32)[0])
+    if p != n:
+        raise ValueError("truncated spill")
+    offs = np.array(offs, np.int64)
+    c = np.array([int(a[o:o + 8].view(np.int64)[0]) for o in offs], np.int64) if offs.shape[0] < 64 else \
+        a[(offs[:, None] + np.arange(8)).reshape(-1)].view(np.int64)
+    q = a[(offs[:, None] + 8 + np.arange(8)).reshape(-1)].view(np.int64)
+    order = np.lexsort((np.arange(offs.shape[0]), q, c))
+    ends = np.append(offs[1:], n)
+    return b"".join(data[int(offs[i]) + 16:int(ends[i])] for i in order)
+
+
 def stream_chunks(path: str, threads: int = 0, chunk_bytes: int = DEFAULT_CHUNK_BYTES, slack: int = DEFAULT_SLACK,
-                  read_size: int = 8 << 20, runs: bool = False, rng=None, stats: Optional[dict] = None, owner=None):
+                  read_size: int = 8 << 20, runs: bool = False, rng=None, stats: Optional[dict] = None, owner=None,
+                  defer: int = 0, keys: bool = False):
     """The chunks of a coordinate-sorted BAM in bounded memory, undecoded (StreamChunk): cut where no
     template or MI family straddles two chunks (include/bsdc_io.h, bsdc_bam_stream_next_raw).  The
     stream itself is freed once it is exhausted and every chunk has been decoded or discarded.
@@ -420,10 +470,12 @@ def stream_chunks(path: str, threads: int = 0, chunk_bytes: int = DEFAULT_CHUNK_
     statistics (bsdc_bam_stream_range_stats: n, c0, dropped, foreign) once the stream is exhausted.
     owner: (rank, boundaries[, flags]) -- keep the records whose key lies in the rank's interval
     between the boundaries (find_cut dicts; bsdc_bam_stream_set_owner); flags (OWN_*):
-    OWN_STOP_FOREIGN -- a foreign record raises OSError("... foreign record ..."); OWN_SPILL_CROSS
-    -- cross-key records of the core range are spilled: each chunk's `spill` bytes (raw records),
-    the rest in stats["spill_tail"]; OWN_CONTIG_CHUNKS -- each chunk's families share one key
-    contig, its `contig`."""
+    OWN_STOP_FOREIGN -- a foreign record raises OSError("... foreign record ...").
+    defer: the span past which a template is deferred (bsdc_bam_stream_set_defer; 0 = off): each
+    chunk then carries its `spill` entries and its `splices` (the deferred keys its output is cut
+    before), and its records decode with their keys (RawRecords.tc_key); once exhausted, `stats`
+    receives the rest as "spill_tail" and "splices_tail".  keys: the records decode with their keys
+    in any case."""
     lib = _load()
     st = _P()
     if rng is None:
@@ -442,6 +494,8 @@ def stream_chunks(path: str, threads: int = 0, chunk_bytes: int = DEFAULT_CHUNK_
             if lib.bsdc_bam_stream_set_owner(st, int(rank), _ptr(bd) if len(bd) else None, len(cuts), int(wsl),
                                              flags) != 0:
                 raise OSError("%s: %s" % (path, lib.bsdc_io_last_error().decode()))
+        if defer and lib.bsdc_bam_stream_set_defer(st, int(defer)) != 0:
+            raise OSError("%s: %s" % (path, lib.bsdc_io_last_error().decode()))
         while True:
             h = _P()
             if runs:
@@ -452,14 +506,17 @@ def stream_chunks(path: str, threads: int = 0, chunk_bytes: int = DEFAULT_CHUNK_
                 raise OSError("%s: %s" % (path, lib.bsdc_io_last_error().decode()))
             if not h:
                 if stats is not None:
-                    v = np.zeros(5, np.int64)
+                    v = np.zeros(7, np.int64)
                     lib.bsdc_bam_stream_range_stats(st, _ptr(v))
                     stats.update(n=int(v[0]), c0=int(v[1]), dropped=int(v[2]), foreign=int(v[3]), spilled=int(v[4]),
-                                 spill_tail=_stream_spill(lib, st))
+                                 deferred=int(v[5]), peak_buffered=int(v[6]), spill_tail=_stream_spill(lib, st),
+                                 splices_tail=_stream_splices(lib, st))
                 return
             ch = StreamChunk(lib, st, h, path)
-            ch.contig = int(lib.bsdc_bam_stream_chunk_contig(st))
-            ch.spill = _stream_spill(lib, st)
+            ch.keys = bool(defer) or keys
+            if defer:
+                ch.spill = _stream_spill(lib, st)
+                ch.splices = _stream_splices(lib, st)
             yield ch
     finally:
         lib.bsdc_bam_stream_close(st)
@@ -1230,10 +1287,12 @@ def step5(in_bam: str, fasta: str, out_bam: Optional[str], engine=None, prefix: 
 def step5_stream(in_bam: str, fasta: str, out_bam: Optional[str], engine=None, prefix: Optional[str] = None,
                  threads: int = 0, level: int = 6, fastq: Optional[Tuple[str, str]] = None, tags: bool = True,
                  chunk_bytes: int = DEFAULT_CHUNK_BYTES, slack: int = DEFAULT_SLACK,
-                 batch_bases: Optional[int] = None, stats: Optional[dict] = None, gpu_bgzf: bool = False) -> dict:
-    """step5 in bounded memory, pipelined (_stream_step)."""
+                 batch_bases: Optional[int] = None, stats: Optional[dict] = None, gpu_bgzf: bool = False,
+                 defer: Optional[int] = None, read_size: int = 8 << 20) -> dict:
+    """step5 in bounded memory, pipelined (_stream_step); defer: the span past which a template is
+    deferred (default DEFAULT_DEFER_SPAN; 0 = off); read_size: compressed bytes per refill."""
     return _stream_step(in_bam, fasta, out_bam, engine, prefix, threads, level, fastq, tags, chunk_bytes, slack,
-                        batch_bases, stats, gpu_bgzf, None)
+                        batch_bases, stats, gpu_bgzf, None, defer=defer, read_size=read_size)
 
 
 def molecular_stream(in_bam: str, out_bam: Optional[str], engine=None, prefix: Optional[str] = None, threads: int = 0,
@@ -1250,12 +1309,111 @@ def molecular_stream(in_bam: str, out_bam: Optional[str], engine=None, prefix: O
                         batch_bases, stats, gpu_bgzf, int(min_consensus_base_quality))
 
 
+MINKEY = -(1 << 62)  # sort key of the pieces before every family (the header, a first range's start)
+
+
+def _family_cuts(cons, raw, plan, splices, strict: bool, start: int = 0):
+    """Output record indices where a chunk's BAM / FASTQ output is cut before each splice key, in
+    order: (record index, key) per key used.  A family's key is its first record's coarse key
+    (RawRecords.tc_key).  strict (the main stream): before the first family whose key exceeds the
+    splice (no family lies within kDeferMargin of one); else (the spill's pass): before the first
+    family whose key reaches the splice minus kDeferMargin (a deferred template's two records may
+    estimate its key a few positions apart).  splices[start:] are tried; a key no family of the
+    chunk reaches is left (-> cuts, the index of the first key left)."""
+    F = int(cons.status.shape[0])
+    if F == 0 or splices.shape[0] <= start:
+        return [], start
+    first = plan.order[plan.fam_off[:-1]]
+    k0, k1 = raw.tc_key[first, 0], raw.tc_key[first, 1]
+    em = np.zeros(F + 1, np.int64)
+    em[1:] = np.cumsum((cons.status & 1) != 0)
+    out, lo, j = [], 0, start
+    while j < splices.shape[0]:
+        s0, s1 = int(splices[j, 0]), int(splices[j, 1]) - (0 if strict else DEFER_MARGIN)
+        hit = (k0 > s0) | ((k0 == s0) & ((k1 > s1) if strict else (k1 >= s1)))
+        hit[:lo] = False
+        if not hit.any():
+            if not strict:  # (the pass's later chunks take it)
+                break
+            f = F
+        else:
+            f = int(np.argmax(hit))
+        lo = max(lo, f)
+        out.append((2 * int(em[lo]), (int(splices[j, 0]), int(splices[j, 1]))))
+        j += 1
+    return out, j
+
+
+def _slice_records(recs: "OutRecordsBam", a: int, b: int) -> "OutRecordsBam":
+    """Records a..b-1 as views (the encoders index the ragged fields by absolute offsets)."""
+    return OutRecordsBam(flag=recs.flag[a:b], tid=recs.tid[a:b], pos=recs.pos[a:b], mapq=recs.mapq[a:b],
+                         next_tid=recs.next_tid[a:b], next_pos=recs.next_pos[a:b], tlen=recs.tlen[a:b],
+                         names=StringTable(recs.names.buf, recs.names.off[a:b + 1]), cig_off=recs.cig_off[a:b + 1],
+                         cigar=recs.cigar, seq_off=recs.seq_off[a:b + 1], seq=recs.seq, qual=recs.qual,
+                         aux=StringTable(recs.aux.buf, recs.aux.off[a:b + 1]),
+                         aux2=StringTable(recs.aux2.buf, recs.aux2.off[a:b + 1]) if recs.aux2 is not None else None)
+
+
+def pieces_of(marks, paths, phase: int, rank: int) -> list:
+    """One output's pieces between its marks (_stream_step): (sort key, phase, rank, index, paths,
+    starts, ends), ends of the last piece = the files' sizes."""
+    out = []
+    size = [os.path.getsize(x) if x else 0 for x in paths]
+    for i, (offs, key) in enumerate(marks):
+        end = list(marks[i + 1][0]) if i + 1 < len(marks) else size
+        out.append((tuple(key), phase, rank, i, list(paths), list(offs), end))
+    return out
+
+
+def assemble(dst: str, pieces, k: int):
+    """Output file k (0 the BAM, 1 / 2 the FASTQ pair) from the pieces in sort-key order, then one
+    BGZF EOF block; written aside and renamed over dst."""
+    tmp = dst + ".asm"
+    with open(tmp, "wb") as out:
+        for p in sorted(pieces, key=lambda x: (x[0], x[1], x[2], x[3])):
+            path, a, b = p[4][k], p[5][k], p[6][k]
+            if path is None or b <= a:
+                continue
+            with open(path, "rb") as f:
+                f.seek(a)
+                left = b - a
+                while left > 0:
+                    buf = f.read(min(left, 1 << 24))
+                    if not buf:
+                        raise RuntimeError("%s: short piece" % path)
+                    out.write(buf)
+                    left -= len(buf)
+        out.write(EOF_BLOCK)
+    os.replace(tmp, dst)
+
+
+EOF_BLOCK = bytes.fromhex("1f8b08040000000000ff0600424302001b0003000000000000000000")
+
+
+def write_spill_bam(dst: str, header: "BamHeader", spills: Sequence[str], level: int = 1, threads: int = 0) -> int:
+    """The spill files' records (bsdc_bam_stream_spill entries) in file order as a BAM -> records."""
+    data = b"".join(open(x, "rb").read() for x in spills if x and os.path.exists(x))
+    recs = spill_sorted_records(data)
+    w = BamWriter(dst, header, level)
+    try:
+        w.add_raw(recs, threads)
+    finally:
+        w.close(threads)
+    n, p = 0, 0
+    mv = memoryview(recs)
+    while p < len(recs):
+        p += 4 + int.from_bytes(mv[p:p + 4], "little")
+        n += 1
+    return n
+
+
 def _stream_step(in_bam: str, fasta: Optional[str], out_bam: Optional[str], engine, prefix: Optional[str],
                  threads: int, level: int, fastq: Optional[Tuple[str, str]], tags: bool, chunk_bytes: int, slack: int,
                  batch_bases: Optional[int], stats: Optional[dict], gpu_bgzf: bool,
                  molecular: Optional[int], rng=None, fragment: Optional[str] = None, runner=None,
                  range_stats: Optional[dict] = None, owner=None, spill: Optional[str] = None,
-                 marks: Optional[list] = None) -> dict:
+                 marks: Optional[list] = None, defer: Optional[int] = None, late_splices=None,
+                 first_key=None, read_size: int = 8 << 20) -> dict:
     """step5 (molecular None) or step 1 (molecular = its --min-consensus-base-quality) in bounded
     memory, pipelined: a decoder thread cuts the next chunk of the
     coordinate-sorted input (stream_bam: inflate, split where no template or MI family straddles),
@@ -1268,21 +1426,33 @@ def _stream_step(in_bam: str, fasta: Optional[str], out_bam: Optional[str], engi
     before the next chunk's, so the chunks' families in order are the whole file's.  gpu_bgzf: the
     BAM's and the FASTQ pair's blocks are deflated on the engine's GPU (GpuBgzf; the same records,
     other compressed bytes, files ≈4% larger).
+    Deferred templates (step 5; defer = the span, default DEFAULT_DEFER_SPAN, 0 = off): a template
+    whose other end lies far away or on another contig (bsdc_bam_stream_set_defer) would hold every
+    family after its key in memory until the stream reaches that end.  Its records go to a spill
+    file instead (with every family that may interleave with it), and the output is cut, at every
+    deferred key, into pieces (marks).  At the end a second pass runs the spill's records (in file
+    order, their own BAM; memory as their count) with the same keys (late_splices: each cut before
+    the first family that reaches the key), and the pieces of both are assembled in key order: the
+    same records as the whole file's.  Without deferred templates the output is written in place,
+    as it always was.
     rank-parallel use (ranks.py): rng = the record range of the input to run (stream_chunks),
     range_stats its statistics once read, fragment = "first" / "next" (the output pieces a rank
     writes: BamWriter, FastqWriter), runner = a fleet-style runner (run_batch / run_chunk; the CPU
     stand-in of the tests) instead of an Engine, owner = the rank's key interval (stream_chunks),
-    spill = a file for the records the stream spills (raw, headerless BGZF), marks = a list that
-    receives, after each chunk's output is written and flushed, (BAM length, FASTQ lengths x 2,
-    the chunk's key contig): where ranks.py may splice other pieces in."""
+    spill = the file the deferred records go to, marks = a list that receives the output's cut
+    points ((BAM offset, FASTQ offsets x 2), sort key of the piece that starts there): ranks.py
+    runs the second pass and the assembly; first_key = the sort key of the rank's first piece."""
     import queue
     import threading
     import time
 
     from . import pipeline
     own = engine is None and runner is None
+    # (a rank's engine may still be loading: ranks._LazyEngine; torch is imported with it)
+    lazy = bool(getattr(engine, "lazy", False))
     if runner is None:
-        from .device import Engine, PinnedPool
+        if own:
+            from .device import Engine
         eng = Engine(0) if own else engine
     else:
         eng = None
@@ -1291,7 +1461,23 @@ def _stream_step(in_bam: str, fasta: Optional[str], out_bam: Optional[str], engi
     chunks: "queue.Queue" = queue.Queue(maxsize=1)
     outs: "queue.Queue" = queue.Queue(maxsize=1)
     err: list = []
-    info = {"records_in": 0, "families": 0, "families_emitted": 0, "records_out": 0, "chunks": 0}
+    info = {"records_in": 0, "families": 0, "families_emitted": 0, "records_out": 0, "chunks": 0,
+            "spilled_bytes": 0, "deferred_families": 0, "splices": []}
+    # deferral (step 5): the spill file and the output's pieces
+    dspan = 0 if molecular is not None else (DEFAULT_DEFER_SPAN if defer is None else int(defer))
+    late = None if late_splices is None else np.asarray(late_splices, np.int64).reshape(-1, 2)
+    lj = [0]  # (the spill's pass: the first deferred key not yet cut at)
+    tie = 0 if late is not None else 1  # (a spill piece sorts before the stream's piece of its key)
+    solo = marks is None and late is None  # this call runs the spill's pass and the assembly itself
+    mk = [] if marks is None else marks
+    frag = "first" if (solo and dspan) else fragment
+    # (the spill pass's first piece, before its first key, is empty: after the header in any case)
+    k_first = tuple(first_key) if first_key is not None else (MINKEY, 0, 2 if late is not None else 1)
+    out0 = out_bam if out_bam is not None else fastq[0]
+    spill_path = spill if spill is not None else \
+        (os.path.join(os.path.dirname(os.path.abspath(out0)), ".%s.%d.%x.spill" % (os.path.basename(out0), os.getpid(),
+                                                                                  id(info))) if dspan else None)
+    splices_tail: list = []
     T = {"decode": 0.0, "plan": 0.0, "materialize": 0.0, "gpu": 0.0, "records": 0.0, "encode": 0.0,
          "gpu_wait": 0.0, "writer_wait": 0.0}
     G: dict = {}  # the GPU stage's host steps (pipeline.run_batches timing)
@@ -1305,30 +1491,36 @@ def _stream_step(in_bam: str, fasta: Optional[str], out_bam: Optional[str], engi
     def decoder():  # cuts the next chunk (inflate, split, family-complete selection) while the
         # reader thread parses the one before
         it = sw = None
-        rs = range_stats if range_stats is not None else ({} if spill is not None else None)
+        rs = range_stats if range_stats is not None else {}
         try:
-            if spill is not None:  # (headerless: ranks.py prefixes the header)
-                sw = BamWriter(spill, first["header"], level, None, "next")
-            it = stream_chunks(in_bam, threads, chunk_bytes, slack, runs=molecular is not None, rng=rng,
-                               stats=rs, owner=owner)
+            if dspan:
+                sw = open(spill_path, "wb")
+            it = stream_chunks(in_bam, threads, chunk_bytes, slack, read_size, runs=molecular is not None, rng=rng,
+                               stats=rs, owner=owner, defer=dspan, keys=late is not None)
             while not stop.is_set():
                 t0 = time.perf_counter()
                 nxt = next(it, None)
                 T["decode"] += time.perf_counter() - t0
                 if nxt is None:
                     break
-                if sw is not None:
-                    sw.add_raw(nxt.spill, threads)
+                if sw is not None and nxt.spill:
+                    sw.write(nxt.spill)
+                    info["spilled_bytes"] += len(nxt.spill)
                 raws.put(nxt)
+            if not stop.is_set():
+                info["deferred_families"] = int(rs.get("deferred", 0))
+                info["peak_buffered"] = int(rs.get("peak_buffered", 0))
             if sw is not None and not stop.is_set():
-                sw.add_raw(rs.pop("spill_tail", b""), threads)
-                sw.close(threads)
-                sw = None
+                tail = rs.pop("spill_tail", b"")
+                sw.write(tail)
+                info["spilled_bytes"] += len(tail)
+                splices_tail.append(rs.pop("splices_tail", np.zeros((0, 2), np.int64)))
         except BaseException as e:  # noqa: BLE001 -- handed to the main thread
             err.append(e)
             stop.set()
         finally:
-            close_quietly(sw)
+            if sw is not None:
+                sw.close()
             if it is not None:
                 it.close()  # (the stream is freed once every chunk is back)
             raws.put(None)
@@ -1345,7 +1537,7 @@ def _stream_step(in_bam: str, fasta: Optional[str], out_bam: Optional[str], engi
                     ch.discard()
                     continue  # drain to the decoder's None without parsing
                 raw = ch.decode(threads, R_, bufs)[1]
-                raw._chunk_contig = getattr(ch, "contig", -1)  # (marks: the writer's cut points)
+                raw._splices = ch.splices  # (the deferred keys this chunk's output is cut before)
                 parsed.put(raw)
         except BaseException as e:  # noqa: BLE001 -- handed to the main thread
             err.append(e)
@@ -1359,8 +1551,12 @@ def _stream_step(in_bam: str, fasta: Optional[str], out_bam: Optional[str], engi
             parsed.put(None)
 
     # the planner materializes chunk k's batches into pool k % 3: chunk k - 3 is done on the GPU
-    # by then (the planner handed chunk k - 1 over only after the GPU stage took chunk k - 2)
-    pools = [PinnedPool() for _ in range(3)] if runner is None else None
+    # by then (the planner handed chunk k - 1 over only after the GPU stage took chunk k - 2).  A
+    # loading engine's first chunks materialize into plain host arrays, the pools come with it
+    def new_pools():
+        from .device import PinnedPool
+        return [PinnedPool() for _ in range(3)]
+    pools = None if runner is not None else ([] if lazy else new_pools())
 
     def planner():  # forms a chunk's families and materializes its batches ahead of the GPU stage
         try:
@@ -1383,7 +1579,9 @@ def _stream_step(in_bam: str, fasta: Optional[str], out_bam: Optional[str], engi
                 fbs = None
                 if not plan.split_ext:
                     images = None
-                    if pools is not None:
+                    if pools is not None and not pools and eng.ready():
+                        pools.extend(new_pools())
+                    if pools:
                         pool = pools[k % 3]
                         k += 1
                         pool.reset()
@@ -1410,14 +1608,13 @@ def _stream_step(in_bam: str, fasta: Optional[str], out_bam: Optional[str], engi
                 T["writer_wait"] += time.perf_counter() - t0
                 if item is None:
                     break
-                cons, raw = item
+                cons, raw, cuts = item
                 t0 = time.perf_counter()
                 recs = duplex_records(cons, raw, first["prefix"], threads, molecular=molecular is not None, pool=bufs)
                 T["records"] += time.perf_counter() - t0
                 back = [raw._pool_buf, getattr(recs.aux2, "_pool_buf", None)]
-                contig = getattr(raw, "_chunk_contig", -1)
                 del item, cons, raw
-                recq.put((recs, back, contig))
+                recq.put((recs, back, cuts))
         except BaseException as e:  # noqa: BLE001
             err.append(e)
             stop.set()
@@ -1431,24 +1628,31 @@ def _stream_step(in_bam: str, fasta: Optional[str], out_bam: Optional[str], engi
         try:
             gz = GpuBgzf(eng.device) if gpu_bgzf and out_bam is not None else None
             gzf = GpuBgzf(eng.device) if gpu_bgzf and fastq is not None else None  # (one job in flight each)
-            w = BamWriter(out_bam, output_header(first["header"]), level, gz, fragment) if out_bam is not None else None
-            fq = FastqWriter(fastq[0], fastq[1], level, gzf, fragment is not None) if fastq is not None else None
-            if marks is not None:  # (the header, if any, is a piece of its own: key contig -1)
-                marks.append((w.flush(threads) if w is not None else 0, 0, 0, -1))
+            w = BamWriter(out_bam, output_header(first["header"]), level, gz, frag) if out_bam is not None else None
+            fq = FastqWriter(fastq[0], fastq[1], level, gzf, frag is not None) if fastq is not None else None
+
+            def cut(key):  # everything so far leaves as whole blocks; a piece with this key starts here
+                bo = w.flush(threads) if w is not None else 0
+                fo = fq.flush(threads) if fq is not None else (0, 0)
+                mk.append(((bo, fo[0], fo[1]), key))
+            mk.append(((0, 0, 0), k_first))  # (a first piece holds the header, if any)
             while True:
                 item = recq.get()
                 if item is None:
                     break
-                recs, back, contig = item
+                recs, back, cuts = item
                 t1 = time.perf_counter()
-                if w is not None:
-                    w.add(recs, threads)
-                if fq is not None:
-                    fq.add(recs, threads)
-                if marks is not None:  # a cut point after each chunk (ranks.py)
-                    bo = w.flush(threads) if w is not None else 0
-                    fo = fq.flush(threads) if fq is not None else (0, 0)
-                    marks.append((bo, fo[0], fo[1], contig))
+                a = 0
+                for idx, key in cuts + [(recs.n, None)]:
+                    part = recs if (a == 0 and idx == recs.n) else _slice_records(recs, a, idx)
+                    if idx > a:
+                        if w is not None:
+                            w.add(part, threads)
+                        if fq is not None:
+                            fq.add(part, threads)
+                    if key is not None:
+                        cut((key[0], key[1], tie))
+                    a = idx
                 info["records_out"] += recs.n
                 T["encode"] += time.perf_counter() - t1
                 del item, recs
@@ -1527,7 +1731,13 @@ def _stream_step(in_bam: str, fasta: Optional[str], out_bam: Optional[str], engi
                 info["families"] += int(cons.status.shape[0])
                 info["families_emitted"] += int(((cons.status & 1) != 0).sum())
                 info["chunks"] += 1
-                outs.put((cons, raw))
+                cuts = []
+                if late is not None:  # the spill's pass: cut before the families of each deferred key
+                    cuts, lj[0] = _family_cuts(cons, raw, plan, late, False, lj[0])
+                elif getattr(raw, "_splices", None) is not None and raw._splices.shape[0]:
+                    cuts, _ = _family_cuts(cons, raw, plan, raw._splices, True)
+                    info["splices"].append(raw._splices)
+                outs.put((cons, raw, cuts))
         except BaseException:
             stop.set()
             raise
@@ -1542,10 +1752,18 @@ def _stream_step(in_bam: str, fasta: Optional[str], out_bam: Optional[str], engi
             tp.join()
             tr.join()
             td.join()
+        if not err:
+            info["splices"] = np.concatenate(info["splices"] + splices_tail + [np.zeros((0, 2), np.int64)]) \
+                if dspan else np.zeros((0, 2), np.int64)
+            if solo and dspan:  # the deferred templates' pass and the assembly (or just the EOF blocks)
+                _finish_deferred(in_bam, fasta, out_bam, fastq, eng if runner is None else None, runner, first["prefix"],
+                                 threads, level, tags, chunk_bytes, slack, batch_bases, gpu_bgzf, mk, spill_path, info)
     finally:
         flags.__exit__(None, None, None)
         if own:
             eng.close()
+        if solo and spill_path is not None and os.path.exists(spill_path):
+            os.unlink(spill_path)
     if err:
         raise err[0]
     if stats is not None:
@@ -1553,6 +1771,40 @@ def _stream_step(in_bam: str, fasta: Optional[str], out_bam: Optional[str], engi
         stats.update({"gpu_" + k: round(v, 4) for k, v in G.items()})
         stats.update({"reader_" + k: round(v, 4) for k, v in R_.items()})
     return info
+
+
+def _finish_deferred(in_bam, fasta, out_bam, fastq, eng, runner, prefix, threads, level, tags, chunk_bytes, slack,
+                     batch_bases, gpu_bgzf, marks, spill_path, info):
+    """One process's deferred templates: with none, the EOF blocks the fragment-mode writers left
+    out; else the spill's records as their own BAM through the stream (no deferral; cut at every
+    deferred key), then the pieces of both outputs assembled in key order."""
+    paths = [out_bam, fastq[0] if fastq else None, fastq[1] if fastq else None]
+    if info["splices"].shape[0] == 0 and info["spilled_bytes"] == 0:
+        for x in paths:
+            if x is not None:
+                with open(x, "ab") as f:
+                    f.write(EOF_BLOCK)
+        return
+    base = spill_path + ".p2"
+    sb = base + ".bam"
+    p2 = [base + ".out.bam" if out_bam is not None else None,
+          base + ".1.fq.gz" if fastq else None, base + ".2.fq.gz" if fastq else None]
+    try:
+        info["deferred_records"] = write_spill_bam(sb, read_bam_header(in_bam), [spill_path], 1, threads)
+        mk2: list = []
+        inf2 = _stream_step(sb, fasta, p2[0], eng, prefix, threads, level, (p2[1], p2[2]) if fastq else None, tags,
+                            chunk_bytes, slack, batch_bases, None, gpu_bgzf, None, fragment="next",
+                            runner=runner, marks=mk2, defer=0, late_splices=info["splices"])
+        for k in ("records_in", "families", "families_emitted", "records_out"):
+            info[k] += inf2[k]
+        pieces = pieces_of(marks, paths, 0, 0) + pieces_of(mk2, p2, 1, 0)
+        for k in range(3):
+            if paths[k] is not None:
+                assemble(paths[k], pieces, k)
+    finally:
+        for x in [sb] + p2:
+            if x is not None and os.path.exists(x):
+                os.unlink(x)
 
 
 def molecular(in_bam: str, out_bam: Optional[str], engine=None, prefix: Optional[str] = None, threads: int = 0,

@@ -93,7 +93,7 @@ def _coordinate_sorted(bam, path: str) -> bool:
 def _step5_fleet(a, gpus: int) -> int:
     """step5 --gpus N on a coordinate-sorted input: ranks.step5_ranks, or fleet.step5_stream_multi
     (module docstring)."""
-    from . import fleet, ranks
+    from . import ranks  # (fleet, with torch, only if it runs)
     devs = [int(x) for x in a.devices.split(",")] if a.devices else list(range(gpus))
     if len(devs) != gpus:
         print("--devices needs %d ids" % gpus, file=sys.stderr)
@@ -112,6 +112,7 @@ def _step5_fleet(a, gpus: int) -> int:
         except Exception as e:  # noqa: BLE001 -- the rule fails with the message
             print("%s: %s" % (type(e).__name__, e), file=sys.stderr)
             return 1
+    from . import fleet
     try:
         info = fleet.step5_stream_multi(a.input, a.reference, None if a.output == "-" else a.output, devs,
                                         a.read_name_prefix, a.threads, a.compression,

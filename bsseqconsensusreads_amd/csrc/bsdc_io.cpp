@@ -20,6 +20,7 @@
 #include <string_view>
 #include <unordered_map>
 #include <mutex>
+#include <set>
 #include <chrono>
 #include <vector>
 #ifdef _OPENMP
@@ -595,13 +596,18 @@ inline int64_t coord(int32_t tid, int32_t pos) {
 }
 struct StreamRec {
     int64_t off, len;  // the record's bytes in bsdc_bam_stream::buf
-    int32_t fam;       // its MI family (stream-wide index)
+    int32_t fam;       // its MI family (stream-wide index); -1: deferred (left for bsdc_bam_stream_spill)
+    int64_t c, seq;    // its coordinate and its place in the file (the spill's sort key)
 };
 // a TemplateCoordinate key, coarsely: (lower end's contig << 32 | other end's contig, lower end's
 // position); BIG (0x7FFFFFFF) for an unmapped or absent mate, as the key's mate contig
 using TcKey = std::pair<int64_t, int64_t>;
 constexpr int64_t kBigTid = 0x7FFFFFFF;
 constexpr int64_t kKeyDelta = 4;  // |key position before tools 1 + 2 - after| <= 2, twice
+// a family whose coarse keys come this close to a deferred key may interleave with it in the exact
+// TemplateCoordinate order (both sides' keys move by up to kKeyDelta; a deferred template's two
+// records may estimate its key kKeyDelta apart): it is deferred too
+constexpr int64_t kDeferMargin = 3 * kKeyDelta;
 constexpr int kFamShards = 64;
 inline int fam_shard(uint64_t h) { return (int)(h >> 58); }
 // A record's coordinate c, its reach e (max of its own and its mate's coordinate) and its coarse
@@ -613,6 +619,8 @@ inline int fam_shard(uint64_t h) { return (int)(h >> 58); }
 struct RecKey {
     int64_t c, e;
     TcKey key;
+    int64_t m;  // the mate's coordinate (c when the mate is unmapped or absent)
+    bool own;   // the key is this record's own end (the template's lower end), not its mate's
 };
 inline RecKey rec_key(const uint8_t *r, std::string_view mc) {
     const int l_name = r[12];
@@ -664,16 +672,27 @@ inline RecKey rec_key(const uint8_t *r, std::string_view mc) {
     const bool paired = (flag & 1) && !(flag & 8) && ntid >= 0;
     const int64_t t1 = tid < 0 ? kBigTid : tid;
     TcKey key;
+    bool own = true;
     if (!paired) key = {(t1 << 32) | kBigTid, p_own};
-    else if (tid == ntid) key = {(t1 << 32) | t1, std::min(p_own, p_mate)};
+    else if (tid == ntid) key = {(t1 << 32) | t1, std::min(p_own, p_mate)}, own = p_own <= p_mate;
     else if (tid >= 0 && tid < ntid) key = {(t1 << 32) | (int64_t)ntid, p_own};
-    else key = {((int64_t)ntid << 32) | t1, p_mate};
-    return RecKey{c, ntid >= 0 ? std::max(c, coord(ntid, npos)) : c, key};
+    else key = {((int64_t)ntid << 32) | t1, p_mate}, own = false;
+    const int64_t m = ntid >= 0 ? coord(ntid, npos) : c;
+    return RecKey{c, std::max(c, m), key, m, own};
+}
+// A far record (bsdc_bam_stream_set_defer): its template's key is a cross key (the mate on another
+// contig, unmapped or absent: the key sorts at its contig's end) or its mate lies more than `span`
+// positions away on the same contig.
+inline bool far_record(const RecKey &k, int64_t span) {
+    if ((k.key.first >> 32) != (k.key.first & 0xFFFFFFFFll)) return true;
+    return (k.m > k.c ? k.m - k.c : k.c - k.m) > span;
 }
 struct StreamFam {
     int64_t lo = INT64_MAX, hi = INT64_MIN;  // min own position, max own or mate position (coord)
     TcKey klo{INT64_MAX, INT64_MAX}, khi{INT64_MIN, INT64_MIN};  // bounds of its records' keys
     int64_t n = 0;                           // buffered records
+    bool def = false;  // deferred by adjacency (set_defer): its records go to the spill
+    bool live() const { return n > 0; }
 };
 }  // namespace
 
@@ -721,11 +740,17 @@ struct bsdc_bam_stream {
     std::vector<int64_t> own_coord;
     int64_t own_slack = 0;
     bool own_stop = false;
-    bool own_spill = false;          // cross-key records of the core range go to `spill`, not the stream
-    bool own_contig_chunks = false;  // no chunk holds families of two key contigs
-    Bytes spill;                     // (bsdc_bam_stream_spill) raw records, file order
-    int64_t last_contig = -1;        // the key contig of the last chunk
-    int64_t st_dropped = 0, st_foreign = 0, st_spilled = 0;
+    // deferred templates (bsdc_bam_stream_set_defer): span 0 = off
+    int64_t defer_span = 0;
+    Bytes spill;                     // (bsdc_bam_stream_spill) {coordinate, seq, record} entries
+    std::set<TcKey> dset;            // deferred keys near the emitted output (adjacency test)
+    std::set<TcKey> dreg;            // every far template key registered (its far record's check)
+    std::vector<TcKey> pend;         // deferred keys not yet reported (bsdc_bam_stream_splices)
+    std::vector<TcKey> splices;      // the keys reported with the last chunk
+    TcKey reach{INT64_MIN, INT64_MIN};  // the largest key emitted so far
+    int64_t seq = 0;                 // records split so far (file order)
+    int64_t st_dropped = 0, st_foreign = 0, st_spilled = 0, st_deferred = 0;
+    int64_t st_peak = 0;  // the most record bytes buffered at a chunk selection (the memory bound)
     // statistics of the records split so far: count, first coordinate, max reach, key bounds
     int64_t st_n = 0, st_c0 = 0;
 };
@@ -846,6 +871,14 @@ void bsdc_bam_stream_range_stats(const bsdc_bam_stream *s, int64_t *st) {
     st[2] = s->st_dropped;
     st[3] = s->st_foreign;
     st[4] = s->st_spilled;
+    st[5] = s->st_deferred;
+    st[6] = s->st_peak;
+}
+
+int32_t bsdc_bam_stream_set_defer(bsdc_bam_stream *s, int64_t span) {
+    if (!s || span < 0) return fail(BSDC_IO_EINVAL, "bad defer span");
+    s->defer_span = span;
+    return 0;
 }
 
 int64_t bsdc_bam_stream_spill(bsdc_bam_stream *s, uint8_t *dst) {
@@ -857,7 +890,17 @@ int64_t bsdc_bam_stream_spill(bsdc_bam_stream *s, uint8_t *dst) {
     return n;
 }
 
-int64_t bsdc_bam_stream_chunk_contig(const bsdc_bam_stream *s) { return s->last_contig; }
+int64_t bsdc_bam_stream_splices(bsdc_bam_stream *s, int64_t *dst) {
+    const int64_t n = (int64_t)s->splices.size();
+    if (dst) {
+        for (int64_t i = 0; i < n; i++) {
+            dst[2 * i] = s->splices[(size_t)i].first;
+            dst[2 * i + 1] = s->splices[(size_t)i].second;
+        }
+        s->splices.clear();
+    }
+    return n;
+}
 
 namespace {
 // A record starts at d[p] (dn bytes follow the stream start d): its length fields, names and
@@ -1117,8 +1160,6 @@ int32_t bsdc_bam_stream_set_owner(bsdc_bam_stream *s, int32_t rank, const int64_
     for (int32_t i = 0; i < n_bounds; i++) s->own_coord.push_back(bounds[3 * i + 2]);
     s->own_slack = slack;
     s->own_stop = (flags & BSDC_OWN_STOP_FOREIGN) != 0;
-    s->own_spill = (flags & BSDC_OWN_SPILL_CROSS) != 0;
-    s->own_contig_chunks = (flags & BSDC_OWN_CONTIG_CHUNKS) != 0;
     return 0;
 }
 
@@ -1154,9 +1195,64 @@ int32_t bsdc_bam_stream_fill(bsdc_bam_stream *s) {
 }
 
 namespace {
+// The live family of an MI base, or -1 (no family is created)
+int32_t find_fam(bsdc_bam_stream *s, std::string_view mi, uint64_t h) {
+    if (!s->fam_exact.empty()) {
+        auto ie = s->fam_exact.find(std::string(mi));
+        if (ie != s->fam_exact.end() && s->fams[(size_t)ie->second].live()) return ie->second;
+    }
+    const auto &fm = s->fam_of[(size_t)fam_shard(h)];
+    auto it = fm.find(h);
+    if (it != fm.end() && s->fams[(size_t)it->second].live() && s->fam_key[(size_t)it->second] == mi) return it->second;
+    return -1;
+}
+// A deferred key (bsdc_bam_stream_set_defer): kept for the adjacency test and reported as a splice
+// point with the chunk whose keys reach past it.  A key at or behind what was already emitted (a far
+// record whose template's lower record was never read) cannot be spliced: an error.
+int32_t defer_key(bsdc_bam_stream *s, const TcKey &k) {
+    if (k.first < s->reach.first || (k.first == s->reach.first && k.second <= s->reach.second + 2 * kKeyDelta))
+        return fail(BSDC_IO_EFORMAT, "a template whose other end lies far away has its lower record missing or "
+                                     "behind the output already written; read the file whole instead");
+    if (s->dset.insert(k).second) s->pend.push_back(k);
+    return 0;
+}
+// a spill entry: {coordinate, file sequence} (the pass-2 sort key), then the record
+void spill_record(bsdc_bam_stream *s, const uint8_t *r, int64_t c, int64_t seq) {
+    const int64_t len = 4 + (int64_t)rd32(r);
+    const size_t at = s->spill.size();
+    s->spill.resize(at + 16 + (size_t)len);
+    memcpy(s->spill.data() + at, &c, 8);
+    memcpy(s->spill.data() + at + 8, &seq, 8);
+    memcpy(s->spill.data() + at + 16, r, (size_t)len);
+    s->st_spilled++;
+}
+// Family m (buffered, complete, owned) turns deferred: its key range is registered; its records
+// follow with spill_deferred.
+int32_t defer_family(bsdc_bam_stream *s, int32_t m) {
+    StreamFam &F = s->fams[(size_t)m];
+    F.def = true;
+    s->st_deferred++;
+    const int32_t rc = defer_key(s, F.klo);
+    if (rc == 0) s->dset.insert(F.khi);  // (the range's upper end: adjacency only, not a splice point)
+    return rc;
+}
+// The buffered records s->recs[0, upto) of deferred families to the spill (they are owned: a rank
+// drops the others before family assignment); they leave their families' counts.
+void spill_deferred(bsdc_bam_stream *s, size_t upto) {
+    for (size_t i = 0; i < upto; i++) {
+        StreamRec &r = s->recs[i];
+        if (r.fam < 0 || !s->fams[(size_t)r.fam].def) continue;
+        spill_record(s, s->buf.data() + r.off, r.c, r.seq);
+        s->fams[(size_t)r.fam].n--;
+        r.fam = -1;
+    }
+}
+
 // The whole records of buf's unsplit tail added to the buffered records, each with its MI family.  A record's family
 // is its MI base (the MI up to the first '/', as the reader interns it); a record without MI is a
-// family of its own.
+// family of its own.  With set_defer, a far record (far_record) -- and every record of its MI family,
+// buffered or to come -- goes to the spill instead (a rank: the far records of its core coordinates,
+// and the near ones it owns), and its keys are registered (defer_key).
 int32_t stream_split(bsdc_bam_stream *s) {
     uint8_t *d = s->buf.data() + s->tail;
     const int64_t dn = (int64_t)s->buf.size() - s->tail;
@@ -1171,11 +1267,15 @@ int32_t stream_split(bsdc_bam_stream *s) {
         p += 4 + bs;
     }
     int64_t nr = (int64_t)starts.size();
+    const bool defer = s->defer_span > 0;
     struct Parsed {
         std::string_view mi;
         uint64_t h;  // hash of mi
         int64_t c, e;
         TcKey key;
+        int64_t seq;   // the record's place in the file (split order)
+        uint8_t far;   // far_record (set_defer)
+        uint8_t own;   // the key is the record's own end
     };
     std::vector<Parsed> P((size_t)nr);
     int bad = 0;
@@ -1206,34 +1306,31 @@ int32_t stream_split(bsdc_bam_stream *s) {
         const size_t slash = mi.find('/');
         if (slash != std::string_view::npos) mi = mi.substr(0, slash);
         const RecKey rk = rec_key(r, mc);
-        P[(size_t)k] = Parsed{mi, std::hash<std::string_view>{}(mi), rk.c, rk.e, rk.key};
+        P[(size_t)k] = Parsed{mi, std::hash<std::string_view>{}(mi), rk.c, rk.e, rk.key, s->seq + k,
+                              (uint8_t)(defer && far_record(rk, s->defer_span)), (uint8_t)rk.own};
     }
     if (bad) return fail(BSDC_IO_EFORMAT, "malformed BAM record (lengths or aux)");
-    std::vector<uint8_t> drop;
+    s->seq += nr;
+    // per record: 0 buffered, 1 dropped (another rank's), 2 far (family marking; spilled if `core`)
+    std::vector<uint8_t> cls((size_t)nr, 0), core((size_t)nr, 1), owned((size_t)nr, 1);
     if (s->own_rank >= 0 && nr > 0) {  // a rank: the records of its key interval only
-        drop.assign((size_t)nr, 0);
         const auto &bd = s->own_bounds;
-        // this rank's core coordinates (its own share of the file: cross-key records it spills)
+        // this rank's core coordinates (its own share of the file: the far records it spills)
         const int64_t core_lo = s->own_rank == 0 ? INT64_MIN : s->own_coord[(size_t)s->own_rank - 1];
         const int64_t core_hi = s->own_rank == (int)bd.size() ? INT64_MAX : s->own_coord[(size_t)s->own_rank];
         for (int64_t k = 0; k < nr; k++) {
             const Parsed &q = P[(size_t)k];
-            if (s->own_spill && (q.key.first >> 32) != (q.key.first & 0xFFFFFFFFll)) {
-                // a template with its mate on another contig or unmapped: its key sorts at its
-                // contig's end, its records lie anywhere; phase 2 forms its family (ranks.py)
-                drop[(size_t)k] = 1;
-                if (q.c >= core_lo && q.c < core_hi) {
-                    const uint8_t *r = d + starts[(size_t)k];
-                    s->spill.insert(s->spill.end(), r, r + 4 + rd32(r));
-                    s->st_spilled++;
-                } else {
-                    s->st_dropped++;
-                }
+            const int owner = (int)(std::upper_bound(bd.begin(), bd.end(), q.key) - bd.begin());
+            owned[(size_t)k] = owner == s->own_rank;
+            if (q.far) {
+                // a template reaching past the windows: every rank marks its MI family, the rank
+                // whose core holds the record spills it, the key's owner registers the key
+                cls[(size_t)k] = 2;
+                core[(size_t)k] = q.c >= core_lo && q.c < core_hi;
                 continue;
             }
-            const int owner = (int)(std::upper_bound(bd.begin(), bd.end(), q.key) - bd.begin());
-            if (owner == s->own_rank) continue;
-            drop[(size_t)k] = 1;
+            if (owned[(size_t)k]) continue;
+            cls[(size_t)k] = 1;
             s->st_dropped++;
             // the owner reads the coordinates [its lower bound - slack, its upper bound + slack)
             const int64_t lo = owner == 0 ? INT64_MIN : s->own_coord[(size_t)owner - 1] - s->own_slack;
@@ -1241,21 +1338,29 @@ int32_t stream_split(bsdc_bam_stream *s) {
             if (q.c < lo || q.c >= hi) s->st_foreign++;
         }
         if (s->own_stop && s->st_foreign > 0)
-            return fail(BSDC_IO_EFORMAT, "foreign record: a record another rank owns but never reads (mate on "
-                                         "another contig or unmapped, or an insert longer than slack)");
+            return fail(BSDC_IO_EFORMAT, "foreign record: a record another rank owns but never reads (its template "
+                                         "reaches past the windows and deferral is off)");
+    } else if (defer) {
+        for (int64_t k = 0; k < nr; k++)
+            if (P[(size_t)k].far) cls[(size_t)k] = 2;
     }
     int64_t call = INT64_MIN;  // (the cursor passes the dropped records too)
     for (int64_t k = 0; k < nr; k++) call = std::max(call, P[(size_t)k].c);
     if (nr > 0 && s->st_n == 0) s->st_c0 = P[0].c;  // (the range statistics: bsdc_bam_stream_range_stats)
     s->st_n += nr;
-    if (!drop.empty()) {  // the kept records moved together (a record's MI view moves with it)
+    bool any_drop = false;
+    for (int64_t k = 0; k < nr && !any_drop; k++) any_drop = cls[(size_t)k] == 1;
+    if (any_drop) {  // the other records moved together (a record's MI view moves with it)
         int64_t wp = 0, m = 0;
         for (int64_t k = 0; k < nr; k++) {
-            if (drop[(size_t)k]) continue;
+            if (cls[(size_t)k] == 1) continue;
             const int64_t st = starts[(size_t)k], len = 4 + (int64_t)rd32(d + st);
             const int64_t mo = P[(size_t)k].mi.empty() ? 0 : (const uint8_t *)P[(size_t)k].mi.data() - (d + st);
             if (wp != st) memmove(d + wp, d + st, (size_t)len);
             P[(size_t)m] = P[(size_t)k];
+            cls[(size_t)m] = cls[(size_t)k];
+            core[(size_t)m] = core[(size_t)k];
+            owned[(size_t)m] = owned[(size_t)k];
             if (!P[(size_t)m].mi.empty()) P[(size_t)m].mi = std::string_view((const char *)d + wp + mo, P[(size_t)m].mi.size());
             starts[(size_t)m] = wp;
             wp += len;
@@ -1293,20 +1398,21 @@ int32_t stream_split(bsdc_bam_stream *s) {
     auto fam_of_mi = [&](std::string_view mi, uint64_t h) {
         if (!s->fam_exact.empty()) {
             auto ie = s->fam_exact.find(std::string(mi));
-            if (ie != s->fam_exact.end() && s->fams[(size_t)ie->second].n > 0) return ie->second;
+            if (ie != s->fam_exact.end() && s->fams[(size_t)ie->second].live()) return ie->second;
         }
         auto &fm = s->fam_of[(size_t)fam_shard(h)];
         auto it = fm.find(h);
-        if (it != fm.end() && s->fams[(size_t)it->second].n > 0 && s->fam_key[(size_t)it->second] == mi)
+        if (it != fm.end() && s->fams[(size_t)it->second].live() && s->fam_key[(size_t)it->second] == mi)
             return it->second;
         const int32_t fam = new_fam();
         s->fam_key[(size_t)fam].assign(mi.data(), mi.size());
         if (it == fm.end()) fm.emplace(h, fam);
-        else if (s->fams[(size_t)it->second].n == 0) it->second = fam;
+        else if (!s->fams[(size_t)it->second].live()) it->second = fam;
         else s->fam_exact[std::string(mi)] = fam;  // collision with a live family
         return fam;
     };
     const int64_t base = s->tail;
+    std::vector<int32_t> famv((size_t)nr);
     if (nr > 0 && nr >= s->par_min && s->fam_exact.empty()) {
         // ---- the same in parallel: families by hash shard (a family's records all fall in one
         // shard), new families numbered in shard order, 64-bit collisions resolved serially ----
@@ -1317,19 +1423,19 @@ int32_t stream_split(bsdc_bam_stream *s) {
         if (unsorted)
             return fail(BSDC_IO_EFORMAT, "input is not coordinate-sorted (the streaming step needs the "
                                          "coordinate order of the step-5 input; read it whole instead)");
-        constexpr int S = kFamShards;  // + bucket S: records without MI
-        std::vector<int64_t> sstart(S + 2, 0);
+        constexpr int S = kFamShards;  // + bucket S: records without MI; S + 1: far records (none)
+        std::vector<int64_t> sstart(S + 3, 0);
         std::vector<uint8_t> shard_of((size_t)nr);
         for (int64_t k = 0; k < nr; k++) {
-            const int sh = P[(size_t)k].mi.empty() ? S : fam_shard(P[(size_t)k].h);
+            const int sh = cls[(size_t)k] == 2 ? S + 1 : P[(size_t)k].mi.empty() ? S : fam_shard(P[(size_t)k].h);
             shard_of[(size_t)k] = (uint8_t)sh;
             sstart[(size_t)sh + 1]++;
+            if (sh == S + 1) famv[(size_t)k] = -9;
         }
-        for (int sh = 0; sh <= S; sh++) sstart[(size_t)sh + 1] += sstart[(size_t)sh];
+        for (int sh = 0; sh <= S + 1; sh++) sstart[(size_t)sh + 1] += sstart[(size_t)sh];
         std::vector<int64_t> sorder((size_t)nr), sfill(sstart.begin(), sstart.end() - 1);
         for (int64_t k = 0; k < nr; k++) sorder[(size_t)sfill[shard_of[(size_t)k]]++] = k;
         // fam[k]: >= 0 an existing family; -1 no MI; -2 a collision; <= -3 new family -3 - i of the shard
-        std::vector<int32_t> famv((size_t)nr);
         std::vector<std::vector<int64_t>> newfirst(S + 1);
 #pragma omp parallel for schedule(dynamic, 1)
         for (int sh = 0; sh <= S; sh++) {
@@ -1344,7 +1450,7 @@ int32_t stream_split(bsdc_bam_stream *s) {
                 const int64_t k = sorder[(size_t)i];
                 const Parsed &q = P[(size_t)k];
                 auto it = fm.find(q.h);
-                if (it != fm.end() && s->fams[(size_t)it->second].n > 0) {
+                if (it != fm.end() && s->fams[(size_t)it->second].live()) {
                     famv[(size_t)k] = s->fam_key[(size_t)it->second] == q.mi ? it->second : -2;
                     continue;
                 }
@@ -1391,7 +1497,7 @@ int32_t stream_split(bsdc_bam_stream *s) {
                 const std::string key(P[(size_t)k].mi);
                 auto ie = s->fam_exact.find(key);
                 if (ie != s->fam_exact.end() &&
-                    (s->fams[(size_t)ie->second].n > 0 || ((size_t)ie->second < fresh.size() && fresh[(size_t)ie->second]))) {
+                    (s->fams[(size_t)ie->second].live() || ((size_t)ie->second < fresh.size() && fresh[(size_t)ie->second]))) {
                     famv[(size_t)k] = ie->second;
                 } else {
                     const int32_t f = new_fam();
@@ -1402,7 +1508,7 @@ int32_t stream_split(bsdc_bam_stream *s) {
                 }
             }
         }
-        // ids and per-family bounds, shard by shard (disjoint families), then the records
+        // ids and per-family bounds, shard by shard (disjoint families)
 #pragma omp parallel for schedule(dynamic, 1)
         for (int sh = 0; sh <= S; sh++) {
             for (int64_t i = sstart[(size_t)sh]; i < sstart[(size_t)sh + 1]; i++) {
@@ -1418,37 +1524,56 @@ int32_t stream_split(bsdc_bam_stream *s) {
                 F.n++;
             }
         }
-        const size_t r0 = s->recs.size();
-        s->recs.resize(r0 + (size_t)nr);
-#pragma omp parallel for schedule(static)
+    } else {
         for (int64_t k = 0; k < nr; k++) {
-            const int64_t len = (k + 1 < nr ? starts[(size_t)k + 1] : p) - starts[(size_t)k];
-            s->recs[r0 + (size_t)k] = StreamRec{base + starts[(size_t)k], len, famv[(size_t)k]};
+            const Parsed &q = P[(size_t)k];
+            if (q.c < s->cursor)
+                return fail(BSDC_IO_EFORMAT, "input is not coordinate-sorted (the streaming step needs the "
+                                             "coordinate order of the step-5 input; read it whole instead)");
+            s->cursor = std::max(s->cursor, q.c);
+            if (cls[(size_t)k] == 2) continue;  // (a far record: its family, if any, below)
+            const int32_t fam = !q.mi.empty() ? fam_of_mi(q.mi, q.h) : new_fam();  // (no MI: a family of its own)
+            StreamFam &F = s->fams[(size_t)fam];
+            F.lo = std::min(F.lo, q.c);
+            F.hi = std::max(F.hi, q.e);
+            F.klo = std::min(F.klo, q.key);
+            F.khi = std::max(F.khi, q.key);
+            F.n++;
+            s->cursor = std::max(s->cursor, q.c);
+            famv[(size_t)k] = fam;
         }
-        s->cursor = std::max(s->cursor, std::max(P[(size_t)nr - 1].c, call));
-        s->tail += p;
-        return 0;
     }
+    // the records, in file order: buffered with their family, or (a far record) deferred -- unless
+    // its MI family is buffered (a molecule whose other templates are near): it joins that family,
+    // so one MI never straddles the stream and the spill over a key gap it would not straddle in the
+    // whole file's order
     for (int64_t k = 0; k < nr; k++) {
         const Parsed &q = P[(size_t)k];
-        if (q.c < s->cursor)
-            return fail(BSDC_IO_EFORMAT, "input is not coordinate-sorted (the streaming step needs the "
-                                         "coordinate order of the step-5 input; read it whole instead)");
-        int32_t fam;
-        if (!q.mi.empty()) {
-            fam = fam_of_mi(q.mi, q.h);
-        } else {
-            fam = new_fam();  // a record without MI: a family of its own
+        int32_t f = famv[(size_t)k];
+        if (cls[(size_t)k] == 2) {
+            f = q.mi.empty() ? -1 : find_fam(s, q.mi, q.h);
+            if (f < 0) {
+                // the template's key comes with its lower record (the other one finds it registered);
+                // a record whose lower record never came registers it if still ahead of the output
+                if (owned[(size_t)k] && (q.own || !s->dreg.count(q.key))) {
+                    const int32_t rc = defer_key(s, q.key);
+                    if (rc != 0) return rc;
+                    s->dreg.insert(q.key);
+                }
+                if (core[(size_t)k]) spill_record(s, d + starts[(size_t)k], q.c, q.seq);
+                continue;
+            }
+            if (!owned[(size_t)k])  // (another rank's template whose MI this rank buffers: not a rank's to join)
+                return fail(BSDC_IO_EFORMAT, "a far record of an MI family another rank owns");
+            StreamFam &F = s->fams[(size_t)f];
+            F.lo = std::min(F.lo, q.c);
+            F.hi = std::max(F.hi, q.e);
+            F.klo = std::min(F.klo, q.key);
+            F.khi = std::max(F.khi, q.key);
+            F.n++;
         }
-        StreamFam &F = s->fams[(size_t)fam];
-        F.lo = std::min(F.lo, q.c);
-        F.hi = std::max(F.hi, q.e);
-        F.klo = std::min(F.klo, q.key);
-        F.khi = std::max(F.khi, q.key);
-        F.n++;
-        s->cursor = std::max(s->cursor, q.c);
         const int64_t len = (k + 1 < nr ? starts[(size_t)k + 1] : p) - starts[(size_t)k];
-        s->recs.push_back(StreamRec{base + starts[(size_t)k], len, fam});
+        s->recs.push_back(StreamRec{base + starts[(size_t)k], len, f, q.c, q.seq});
     }
     s->cursor = std::max(s->cursor, call);
     s->tail += p;
@@ -1498,9 +1623,14 @@ int32_t bsdc_bam_stream_next_raw(bsdc_bam_stream *s, int64_t min_bytes, int64_t 
             s->prof[0] += now_s() - t0;
             continue;
         }
+        {
+            int64_t held = 0;
+            for (const auto &r : s->recs) held += r.fam >= 0 ? r.len : 0;
+            s->st_peak = std::max(s->st_peak, held);
+        }
         take.assign(s->fams.size(), 0);
-        int64_t bytes = 0, contig = -1;
-        bool forced = false;  // a rank's chunk cut at a key-contig change, whatever its size
+        int64_t bytes = 0;
+        TcKey chunk_reach{INT64_MIN, INT64_MIN};
         if (end) {  // every family is complete and nothing is left to read
             for (size_t m = 0; m < s->fams.size(); m++) take[m] = s->fams[m].n > 0;
         } else if (s->cursor != INT64_MIN) {
@@ -1530,37 +1660,72 @@ int32_t bsdc_bam_stream_next_raw(bsdc_bam_stream *s, int64_t min_bytes, int64_t 
                 take[m] = F.n > 0 && F.hi + slack < s->cursor && hi_of(F) < T;
             }
         }
+        if (s->defer_span > 0 && !s->dset.empty()) {
+            // a family whose keys come within kDeferMargin of a deferred key may interleave with it
+            // in TemplateCoordinate order: it is deferred too (and its keys then defer its own
+            // neighbours), so that the stream's and the spill's families are each whole
+            std::vector<int32_t> nd;
+            for (bool more = true; more;) {
+                more = false;
+                for (size_t m = 0; m < s->fams.size(); m++) {
+                    if (!take[m]) continue;
+                    const StreamFam &F = s->fams[m];
+                    auto it = s->dset.lower_bound(TcKey{F.klo.first, F.klo.second - kDeferMargin});
+                    if (it == s->dset.end() || TcKey{F.khi.first, F.khi.second + kDeferMargin} < *it) continue;
+                    take[m] = 0;
+                    const int32_t rc = defer_family(s, (int32_t)m);
+                    if (rc != 0) return rc;
+                    nd.push_back((int32_t)m);
+                    more = true;
+                }
+            }
+            if (!nd.empty()) {
+                spill_deferred(s, s->recs.size());
+                for (int32_t m : nd) {  // (their records are in the spill: the families are done)
+                    s->fams[(size_t)m].def = false;
+                    s->free_fams.push_back(m);
+                }
+            }
+        }
         {
             // bounded chunks: of the families that may go, only a key prefix of about min_bytes,
             // cut between two families whose key ranges do not meet (the rest stays for the next
             // call, where it may go again)
             std::vector<int64_t> fb(s->fams.size(), 0);
-            for (auto &r : s->recs) fb[(size_t)r.fam] += take[(size_t)r.fam] ? r.len : 0;
+            for (auto &r : s->recs)
+                if (r.fam >= 0) fb[(size_t)r.fam] += take[(size_t)r.fam] ? r.len : 0;
             std::vector<int32_t> ord;
             for (size_t m = 0; m < s->fams.size(); m++)
                 if (take[m]) ord.push_back((int32_t)m);
             std::sort(ord.begin(), ord.end(), [&](int32_t a, int32_t b) { return s->fams[(size_t)a].klo < s->fams[(size_t)b].klo; });
             TcKey reach{INT64_MIN, INT64_MIN};
             size_t i = 0;
-            const int64_t kc0 = ord.empty() ? -1 : (s->fams[(size_t)ord[0]].klo.first >> 32);
             for (; i < ord.size(); i++) {
                 const StreamFam &F = s->fams[(size_t)ord[i]];
                 if (bytes > 0 && bytes >= min_bytes && reach < TcKey{F.klo.first, F.klo.second - 2 * kKeyDelta}) break;
-                if (s->own_contig_chunks && (F.klo.first >> 32) != kc0) {  // (a rank: one key contig a chunk)
-                    forced = bytes > 0;
-                    break;
-                }
                 bytes += fb[(size_t)ord[i]];
                 reach = std::max(reach, F.khi);
             }
             for (; i < ord.size(); i++) take[(size_t)ord[i]] = 0;
-            contig = kc0;
+            chunk_reach = reach;
         }
         s->prof[2] += now_s() - t0;
         t0 = now_s();
-        if (end || forced || (bytes > 0 && bytes >= min_bytes)) {
-            if (bytes == 0) return 0;  // the end of the stream
-            s->last_contig = contig;
+        if (end || (bytes > 0 && bytes >= min_bytes)) {
+            if (bytes == 0) {  // the end of the stream: every deferred key left is a splice after the last chunk
+                std::sort(s->pend.begin(), s->pend.end());
+                s->splices = s->pend;
+                s->pend.clear();
+                return 0;
+            }
+            // the deferred keys this chunk's families reach past: its output is cut before each
+            if (chunk_reach > s->reach) s->reach = chunk_reach;
+            std::sort(s->pend.begin(), s->pend.end());
+            const size_t np = (size_t)(std::upper_bound(s->pend.begin(), s->pend.end(), s->reach) - s->pend.begin());
+            s->splices.assign(s->pend.begin(), s->pend.begin() + (ptrdiff_t)np);
+            s->pend.erase(s->pend.begin(), s->pend.begin() + (ptrdiff_t)np);
+            // keys far enough behind the output cannot meet a family still to come
+            s->dset.erase(s->dset.begin(), s->dset.lower_bound(TcKey{s->reach.first, s->reach.second - 4 * kDeferMargin}));
             auto *b = new bsdc_bam();
             b->header = s->hdr.header;
             b->ref_names = s->hdr.ref_names;
@@ -1576,11 +1741,12 @@ int32_t bsdc_bam_stream_next_raw(bsdc_bam_stream *s, int64_t min_bytes, int64_t 
             int64_t ok = 0;
             for (int64_t i = 0; i < nrec; i++) {
                 const StreamRec &r = s->recs[(size_t)i];
+                if (r.fam < 0) continue;  // (deferred: in the spill)
                 if (take[(size_t)r.fam]) {
                     b->rec_start.push_back(r.off);
                 } else {
                     src_k.push_back(r.off);
-                    krecs.push_back(StreamRec{ok, r.len, r.fam});
+                    krecs.push_back(StreamRec{ok, r.len, r.fam, r.c, r.seq});
                     ok += r.len;
                 }
             }
@@ -1604,10 +1770,10 @@ int32_t bsdc_bam_stream_next_raw(bsdc_bam_stream *s, int64_t min_bytes, int64_t 
             for (int sh = 0; sh < kFamShards; sh++) {  // forget the emitted MI bases
                 auto &fm = s->fam_of[(size_t)sh];
                 for (auto it = fm.begin(); it != fm.end();)
-                    it = s->fams[(size_t)it->second].n == 0 ? fm.erase(it) : std::next(it);
+                    it = !s->fams[(size_t)it->second].live() ? fm.erase(it) : std::next(it);
             }
             for (auto it = s->fam_exact.begin(); it != s->fam_exact.end();)
-                it = s->fams[(size_t)it->second].n == 0 ? s->fam_exact.erase(it) : std::next(it);
+                it = !s->fams[(size_t)it->second].live() ? s->fam_exact.erase(it) : std::next(it);
             s->buf.swap(s->spare);  // (spare is now the chunk's old, empty vector: reserved on the next call)
             s->tail = ok;
             s->recs.swap(krecs);
@@ -1713,6 +1879,34 @@ int32_t bsdc_bam_stream_next_runs(bsdc_bam_stream *s, int64_t min_bytes, bsdc_ba
         if (rc != 0) return rc;
         s->prof[0] += now_s() - t0;
     }
+}
+
+// The coarse TemplateCoordinate key of every record of b, in record order (see include/bsdc_io.h).
+int32_t bsdc_bam_rec_keys(const bsdc_bam *b, int64_t *out) {
+    const int64_t n = (int64_t)b->rec_start.size();
+    int bad = 0;
+#pragma omp parallel for schedule(static) reduction(| : bad)
+    for (int64_t k = 0; k < n; k++) {
+        const uint8_t *r = b->data.data() + b->rec_start[(size_t)k];
+        const int64_t bs = rd32(r);
+        const uint8_t *end = r + 4 + bs;
+        const int64_t body = 36 + (int64_t)r[12] + 4 * (int64_t)rd16(r + 16) + ((int64_t)rdi32(r + 20) + 1) / 2 +
+                             (int64_t)rdi32(r + 20);
+        std::string_view mc;
+        for (const uint8_t *a = r + body; a + 3 <= end;) {
+            const int64_t vs = aux_value_size(a, end);
+            if (vs < 0 || vs > (end - a) - 3) {
+                bad |= 1;
+                break;
+            }
+            if (a[0] == 'M' && a[1] == 'C' && a[2] == 'Z') mc = std::string_view((const char *)a + 3, (size_t)vs - 1);
+            a += 3 + vs;
+        }
+        const RecKey rk = rec_key(r, mc);
+        out[2 * k] = rk.key.first;
+        out[2 * k + 1] = rk.key.second;
+    }
+    return bad ? fail(BSDC_IO_EFORMAT, "malformed BAM record (aux)") : 0;
 }
 
 // Parses a raw chunk (records, tags, interned names and MI bases); a no-op for a parsed one.

@@ -19,15 +19,17 @@ from __future__ import annotations
 
 import dataclasses
 from dataclasses import dataclass
-from typing import List, Optional
+from typing import TYPE_CHECKING, List, Optional
 
 import numpy as np
 
 from . import records as R
 from . import shard
 from .batch import FamilyBatch, FamilyPlan, build_family_batch, materialize, plan_families
-from .device import Engine
 from ._lib import MODE_CONVERT, MODE_DUMP, MODE_EXTEND, MODE_TAGS, MODE_VOTE
+
+if TYPE_CHECKING:  # (torch loads with the engine, not with the host planning: ranks.py overlaps the two)
+    from .device import Engine
 
 
 @dataclass

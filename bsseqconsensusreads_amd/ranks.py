@@ -20,39 +20,40 @@ unclipped 5' end, TemplateCoordinate order) leave gaps.
    (bsdc_bam_stream_set_owner): a template's records near a boundary are read by both ranks and
    kept by one.  It writes a fragment of each output: rank 0 the header and its records, the
    others their records, none an EOF block.
-3. Templates whose mate is on another contig or unmapped have keys that sort at their contig's
-   end, whatever their records' positions: no window holds them.  Every rank spills those of its
-   core share (its own coordinates, between its boundaries) to a file instead of streaming them
-   (bsdc_bam_stream_spill), and cuts its chunks so that each holds families of one key contig,
-   recording a cut point after the header and after every chunk (BamWriter / FastqWriter
-   flush + tell).  Phase 2: the parent joins the spills into one BAM, and each rank runs the
-   stream over it, keeping the keys it owns, so the owner of a contig's end forms that contig's
-   cross-key families (recording its cut points too).
-4. The parent splices the pieces in key order: per contig, the ranks' same-contig pieces in rank
-   order, then the contig's cross-key pieces, then one BGZF EOF block.  The BAM and the FASTQ pair
-   decompress to the one-process stream's bytes (tests/test_ranks.py, with mates on a second
-   contig and unmapped mates too); only the BGZF block boundaries at the seams differ.
-5. What remains is a template whose insert is longer than slack, whose far record lies outside its
-   owner's window: a rank that drops such a record stops at once.  The parent then reruns the
-   file as one range, or raises ForeignRecords for its caller to pick another path (cli.py:
-   fleet.step5_stream_multi).
+3. A template whose other end lies far away -- a same-contig insert longer than the defer span
+   (bam.DEFAULT_DEFER_SPAN, half the slack), a mate on another contig, unmapped or absent, whose
+   key sorts at its contig's end -- is deferred, as in the one-process stream
+   (include/bsdc_io.h bsdc_bam_stream_set_defer): its records go to the spill of the rank whose
+   core coordinates (between its boundaries) hold them, its key is registered by the key's owner,
+   and the owner cuts its output into pieces at every deferred key (and defers the families that
+   may interleave with one).  No record is then foreign to every window.  Phase 2: the parent joins
+   the spills into one BAM in file order, and one rank runs the stream over it, cut at the union
+   of the deferred keys (bam._stream_step late_splices).
+4. The parent assembles the pieces of every rank and of phase 2 in key order, then one BGZF EOF
+   block (bam.assemble).  The BAM and the FASTQ pair decompress to the one-process stream's bytes
+   (tests/test_ranks.py, with mates on a second contig, unmapped mates and long inserts); only the
+   BGZF block boundaries at the seams differ.
+5. With deferral off (defer=0) a template whose insert is longer than slack would have its far
+   record outside its owner's window: a rank that drops such a record stops at once, and the
+   parent reruns the file as one range or raises ForeignRecords (on_foreign).
 
 Every rank's memory is bounded as the one-GPU stream's (about six chunks), and each rank decodes
 about 1/N of the records plus 2 * slack positions.  No collective: the ranks exchange nothing but
 their spill files and their counts and cut points.
+
+Start-up: neither the parent nor a rank's host stages import torch (the rank processes are plain
+multiprocessing spawns).  A rank reports ready at once and creates its engine -- torch, HIP, the
+tables -- on a thread of its own (_LazyEngine), while its first job's decoder, reader and planner
+already run; the GPU stage takes the engine when it has its first batches.
 """
 from __future__ import annotations
 
+import multiprocessing as mp
 import os
-import shutil
+import threading
 import time
 import traceback
 from typing import List, Optional, Sequence, Tuple
-
-import torch.multiprocessing as tmp
-
-EOF_BLOCK = bytes.fromhex("1f8b08040000000000ff0600424302001b0003000000000000000000")
-
 
 def plan_cuts(path: str, n: int, threads: int = 0, slack: Optional[int] = None) -> List[dict]:
     """The rank boundaries (bam.find_cut dicts) that split `path` into at most n key intervals of
@@ -83,64 +84,127 @@ def windows_of(cuts) -> List[Tuple[int, int, int, int]]:
 
 
 def _run_job(r: int, eng, runner, job: dict) -> tuple:
-    """One rank's part of the file: the one-GPU stream over its window, its own keys only."""
+    """One rank's part of the file: the one-GPU stream over its window, its own keys only -- or the
+    spill's pass (job["late"]: the deferred keys to cut at)."""
     from . import bam
     st, rs = {}, {}
     t0 = time.perf_counter()
-    marks = [] if job["cuts"] else None
+    marks: list = []
     try:
         info = bam._stream_step(job["in_bam"], job["fasta"], job["out_bam"], eng, job["prefix"], job["threads"],
                                 job["level"], job["fastq"], job["tags"], job["chunk_bytes"], job["slack"],
                                 job["batch_bases"], st, job["gpu_bgzf"] and runner is None, None, rng=job["rng"],
                                 fragment=job["fragment"], runner=runner, range_stats=rs,
                                 owner=(r, job["cuts"], job["flags"]) if job["cuts"] else None, spill=job["spill"],
-                                marks=marks)
+                                marks=marks, defer=job["defer"], late_splices=job.get("late"),
+                                first_key=job.get("first_key"), read_size=job.get("read_size", 8 << 20))
     except OSError as e:
         if "foreign record" in str(e):
             return ("foreign", r, str(e))
         raise
     info["seconds"] = round(time.perf_counter() - t0, 4)
     info["marks"] = marks
+    rs.pop("spill_tail", None)
+    rs.pop("splices_tail", None)
     return ("done", r, info, st, rs)
 
 
+class _LazyEngine:
+    """An engine (or a fleet-style runner) being created on a thread of its own: attribute access
+    waits for it; load_reference before it exists is kept and applied once it does.  Lets a rank's
+    host stages start while torch loads and HIP initialises (module docstring)."""
+
+    lazy = True
+
+    def __init__(self, make):
+        self._ev = threading.Event()
+        self._lock = threading.Lock()
+        self._obj, self._err, self._ref = None, None, None
+        threading.Thread(target=self._init, args=(make,), daemon=True).start()
+
+    def _init(self, make):
+        try:
+            self._obj = make()
+        except BaseException as e:  # noqa: BLE001 -- raised to whoever needs the engine
+            self._err = e
+        finally:
+            self._ev.set()
+
+    def ready(self) -> bool:
+        return self._ev.is_set()
+
+    def get(self):
+        self._ev.wait()
+        if self._err is not None:
+            raise RuntimeError("engine creation failed: %s: %s" % (type(self._err).__name__, self._err))
+        with self._lock:
+            if self._ref is not None:
+                ref, self._ref = self._ref, None
+                self._obj.load_reference(ref)
+        return self._obj
+
+    def load_reference(self, ref):
+        with self._lock:
+            if not self._ev.is_set():
+                self._ref = ref
+                return
+        self.get().load_reference(ref)
+
+    def __getattr__(self, name):
+        if name.startswith("_"):
+            raise AttributeError(name)
+        return getattr(self.get(), name)
+
+
+def _make_engine(device: int, runner_spec: Optional[str]):
+    if runner_spec is None:
+        from .device import Engine
+        return Engine(device)
+    import importlib
+    mod, cls = runner_spec.split(":")
+    return getattr(importlib.import_module(mod), cls)(device)
+
+
 def _rank_server(i: int, device: int, runner_spec: Optional[str], tq, rq):
-    """A pool's rank process (spawned: the first thing here to touch its GPU): its engine or
-    runner once, then jobs until None."""
+    """A pool's rank process (spawned: the first thing here to touch its GPU): ready at once, its
+    engine or runner created on a thread meanwhile (_LazyEngine), then jobs until None.  Replies
+    carry the job's call id."""
     eng = runner = None
     try:
+        lazy = _LazyEngine(lambda: _make_engine(device, runner_spec))
         if runner_spec is None:
-            from .device import Engine
-            eng = Engine(device)
+            eng = lazy
         else:
-            import importlib
-            mod, cls = runner_spec.split(":")
-            runner = getattr(importlib.import_module(mod), cls)(device)
-        rq.put(("ready", i))
+            runner = lazy
+        rq.put(("ready", i, None))
         while True:
             job = tq.get()
             if job is None:
                 break
             try:
-                rq.put(_run_job(job["rank"], eng, runner, job))
+                rq.put(_run_job(job["rank"], eng, runner, job) + (job["call"],))
             except BaseException as e:  # noqa: BLE001 -- reported to the parent, which raises it
-                rq.put(("error", job["rank"], "%s: %s\n%s" % (type(e).__name__, e, traceback.format_exc())))
+                rq.put(("error", job["rank"], "%s: %s\n%s" % (type(e).__name__, e, traceback.format_exc()), job["call"]))
     except BaseException as e:  # noqa: BLE001
-        rq.put(("error", i, "%s: %s\n%s" % (type(e).__name__, e, traceback.format_exc())))
+        rq.put(("error", i, "%s: %s\n%s" % (type(e).__name__, e, traceback.format_exc()), None))
     finally:
-        if eng is not None:
-            eng.close()
-        if runner is not None and hasattr(runner, "close"):
-            runner.close()
+        try:
+            if eng is not None:
+                eng.close()
+            if runner is not None and hasattr(runner, "close"):
+                runner.close()
+        except BaseException:  # noqa: BLE001 -- (its creation failed: reported with the job)
+            pass
 
 
 class RankPool:
     """N rank processes, one per device, spawned before this process touches any GPU (spawn
     context), each holding its engine across calls of step5_ranks(pool=...): start it outside a
-    timed region, as fleet.Fleet's workers are."""
+    timed region, as fleet.Fleet's workers are.  A pool whose rank died is broken: it refuses
+    further runs (a dead rank's call may still have replies in flight)."""
 
     def __init__(self, devices: Sequence[int], runner: Optional[str] = None):
-        ctx = tmp.get_context("spawn")
+        ctx = mp.get_context("spawn")
         self.rq = ctx.Queue()
         self.tqs = [ctx.Queue() for _ in devices]
         self.procs = [ctx.Process(target=_rank_server, args=(i, int(d), runner, self.tqs[i], self.rq), daemon=True)
@@ -148,6 +212,8 @@ class RankPool:
         for p in self.procs:
             p.start()
         self.n = len(devices)
+        self.calls = 0
+        self.broken = False
         try:
             for _ in range(self.n):
                 m = self.get()
@@ -158,7 +224,7 @@ class RankPool:
             raise
 
     def get(self):
-        """The next rank message; raises if a rank died."""
+        """The next rank message; raises (and breaks the pool) if a rank died."""
         import queue
         while True:
             try:
@@ -166,16 +232,25 @@ class RankPool:
             except queue.Empty:
                 dead = [i for i, p in enumerate(self.procs) if not p.is_alive()]
                 if dead:
+                    self.broken = True
                     raise RuntimeError("rank %d exited (code %s)" % (dead[0], self.procs[dead[0]].exitcode))
 
     def run(self, jobs: Sequence[dict]) -> list:
         """Jobs 0..k-1 on ranks 0..k-1 (k <= n); their results in order.  A failing or foreign
-        rank raises after every rank has answered (the pool stays usable)."""
+        rank raises after every rank has answered (the pool stays usable); replies of an earlier
+        call (its ranks answered after it raised) are dropped by their call id."""
+        if self.broken:
+            raise RuntimeError("rank pool is broken (a rank exited); start a new one")
+        self.calls += 1
+        call = self.calls
         for r, job in enumerate(jobs):
-            self.tqs[r].put(dict(job, rank=r))
+            self.tqs[r].put(dict(job, rank=r, call=call))
         res, bad = {}, None
         while len(res) < len(jobs):
             m = self.get()
+            if m[-1] != call:
+                continue
+            m = m[:-1]
             res[m[1]] = m
             if m[0] in ("error", "foreign") and bad is None:
                 bad = m
@@ -210,73 +285,31 @@ class ForeignRecords(RuntimeError):
     """A rank met a record whose owner never reads it (step5_ranks on_foreign="raise")."""
 
 
-def _concat(dst: str, parts: Sequence[str]):
-    """The fragments in rank order, then one BGZF EOF block."""
-    import shutil
-    with open(dst, "wb") as out:
-        for p in parts:
-            with open(p, "rb") as f:
-                shutil.copyfileobj(f, out, 1 << 24)
-        out.write(EOF_BLOCK)
-
-
-def _pieces(results, frags, phase2, fr2) -> list:
-    """Every rank output's pieces between its cut points (the marks _stream_step records after the
-    header and after each chunk), as (key contig, phase, rank, index, paths, starts, ends), in
-    output order: each contig's same-contig families (phase 1, ranks in key order), then its
-    cross-key families (phase 2, the owner of the contig's end)."""
-    out = []
-    for phase, (res, fr) in enumerate(((results, frags), (phase2, fr2))):
-        for r, (inf, _, _) in enumerate(res):
-            f = fr[r]
-            ps = [f["bam"], f["fq"][0] if f["fq"] else None, f["fq"][1] if f["fq"] else None]
-            prev = [0, 0, 0]
-            for i, m in enumerate(inf.get("marks") or []):
-                end = [m[0], m[1], m[2]]
-                out.append((m[3], phase, r, i, ps, list(prev), end))
-                prev = end
-            size = [os.path.getsize(p) if p else 0 for p in ps]
-            if any(size[k] > prev[k] for k in range(3)):  # (the last mark follows the last chunk)
-                raise RuntimeError("rank %d phase %d: bytes after its last cut point" % (r, phase + 1))
-    out.sort(key=lambda x: (x[0], x[1], x[2], x[3]))
-    return out
-
-
-def _assemble(dst: str, pieces, k: int):
-    """Output file k (0 the BAM, 1 / 2 the FASTQ pair) from its pieces in order, then one EOF block."""
-    with open(dst, "wb") as out:
-        for p in pieces:
-            path, a, b = p[4][k], p[5][k], p[6][k]
-            if path is None or b <= a:
-                continue
-            with open(path, "rb") as f:
-                f.seek(a)
-                left = b - a
-                while left > 0:
-                    buf = f.read(min(left, 1 << 24))
-                    if not buf:
-                        raise RuntimeError("%s: short piece" % path)
-                    out.write(buf)
-                    left -= len(buf)
-        out.write(EOF_BLOCK)
-
-
 def step5_ranks(in_bam: str, fasta: str, out_bam: Optional[str], devices: Sequence[int], prefix: Optional[str] = None,
                 threads: int = 0, level: int = 6, fastq: Optional[Tuple[str, str]] = None, tags: bool = True,
                 chunk_bytes: Optional[int] = None, slack: Optional[int] = None, batch_bases: Optional[int] = None,
                 runner: Optional[str] = None, stats: Optional[dict] = None, gpu_bgzf: bool = False,
-                cuts: Optional[list] = None, on_foreign: str = "one", pool: Optional[RankPool] = None) -> dict:
+                cuts: Optional[list] = None, on_foreign: str = "one", pool: Optional[RankPool] = None,
+                defer: Optional[int] = None, read_size: int = 8 << 20) -> dict:
     """Rules convert_Bstrain .. callduplex (main.snake.py:121-164) on a coordinate-sorted BAM by
     len(devices) rank processes (see the module docstring); same file contract as bam.step5_stream.
     runner: "module:Class" of a fleet-style runner (the CPU stand-in of the tests) instead of the
-    GPU; cuts: the rank boundaries to use (tests; default plan_cuts).  on_foreign: what a record
-    no rank can own does -- "one": rerun the file as one range (the default), "raise":
-    ForeignRecords (the caller picks another path: cli.py runs fleet.step5_stream_multi).  pool: a
-    started RankPool of at least len(devices) ranks to run on (its devices then; default: one is
-    spawned for this call and closed after)."""
+    GPU; cuts: the rank boundaries to use (tests; default plan_cuts).  defer: the span past which a
+    template is deferred (default half the slack; 0 = off, when a record no rank can own does what
+    on_foreign says -- "one": rerun the file as one range, "raise": ForeignRecords, the caller picks
+    another path: cli.py runs fleet.step5_stream_multi).  pool: a started RankPool of at least
+    len(devices) ranks to run on (its devices then; default: one is spawned for this call and closed
+    after)."""
+    import uuid
+
+    import numpy as np
+
     from . import bam
+    if out_bam is None and fastq is None:
+        raise ValueError("step5_ranks: no output (out_bam and fastq are both None)")
     chunk_bytes = bam.DEFAULT_CHUNK_BYTES if chunk_bytes is None else chunk_bytes
     slack = bam.DEFAULT_SLACK if slack is None else slack
+    dspan = slack // 2 if defer is None else int(defer)
     t0 = time.perf_counter()
     if cuts is None:
         cuts = plan_cuts(in_bam, len(devices), threads, slack)
@@ -285,12 +318,13 @@ def step5_ranks(in_bam: str, fasta: str, out_bam: Optional[str], devices: Sequen
     pre = bam.read_name_prefix(hdr) if prefix is None else prefix
 
     tmpdir = os.path.dirname(os.path.abspath(out_bam if out_bam is not None else fastq[0]))
+    tag = "%s.rank.%s" % (os.getpid(), uuid.uuid4().hex[:12])
 
-    def paths(tag, n, spill):
-        return [dict(bam=os.path.join(tmpdir, ".%s.%d.bam" % (tag, r)) if out_bam is not None else None,
-                     fq=(os.path.join(tmpdir, ".%s.%d.r1.fq.gz" % (tag, r)), os.path.join(tmpdir, ".%s.%d.r2.fq.gz" % (tag, r)))
+    def paths(t, n, spill):
+        return [dict(bam=os.path.join(tmpdir, ".%s.%d.bam" % (t, r)) if out_bam is not None else None,
+                     fq=(os.path.join(tmpdir, ".%s.%d.r1.fq.gz" % (t, r)), os.path.join(tmpdir, ".%s.%d.r2.fq.gz" % (t, r)))
                      if fastq is not None else None,
-                     spill=os.path.join(tmpdir, ".%s.%d.spill" % (tag, r)) if spill else None) for r in range(n)]
+                     spill=os.path.join(tmpdir, ".%s.%d.spill" % (t, r)) if spill else None) for r in range(n)]
 
     def remove(fr):
         for f in fr:
@@ -299,19 +333,22 @@ def step5_ranks(in_bam: str, fasta: str, out_bam: Optional[str], devices: Sequen
                 if os.path.exists(path):
                     os.unlink(path)
 
-    def run(cuts, pl: "RankPool", in_path: str, ranges, tag: str, phase: int):
+    def first_key(r, cuts):  # the sort key of rank r's first piece (its lower boundary's)
+        return (bam.MINKEY, 0, 1) if r == 0 else (cuts[r - 1]["key"][0], cuts[r - 1]["key"][1], 1)
+
+    def run(cuts, pl: "RankPool", ranges, t: str, dsp: int):
         n = len(ranges)
-        fr = paths(tag, n, phase == 0 and len(cuts) > 0)
-        flags = (bam.OWN_STOP_FOREIGN | bam.OWN_SPILL_CROSS | bam.OWN_CONTIG_CHUNKS) if phase == 0 else \
-            bam.OWN_CONTIG_CHUNKS
-        jobs = [dict(in_bam=in_path, fasta=fasta, out_bam=fr[r]["bam"], prefix=pre, threads=threads, level=level,
+        fr = paths(t, n, dsp > 0)
+        jobs = [dict(in_bam=in_bam, fasta=fasta, out_bam=fr[r]["bam"], prefix=pre, threads=threads, level=level,
                      fastq=fr[r]["fq"], tags=tags, chunk_bytes=chunk_bytes, slack=slack, batch_bases=batch_bases,
-                     gpu_bgzf=gpu_bgzf, rng=ranges[r], cuts=cuts, flags=flags, spill=fr[r]["spill"],
-                     fragment="first" if (r == 0 and phase == 0) else "next") for r in range(n)]
+                     gpu_bgzf=gpu_bgzf, rng=ranges[r], cuts=cuts, flags=bam.OWN_STOP_FOREIGN, spill=fr[r]["spill"],
+                     fragment="first" if r == 0 else "next", defer=dsp, first_key=first_key(r, cuts),
+                     read_size=read_size)
+                for r in range(n)]
         try:
             return pl.run(jobs), fr
         except BaseException:
-            remove(fr)  # (every rank has answered: none still writes)
+            remove(fr)  # (every rank of this call has answered: none still writes)
             raise
 
     own = pool is None
@@ -323,50 +360,49 @@ def step5_ranks(in_bam: str, fasta: str, out_bam: Optional[str], devices: Sequen
         t_pool = 0.0
         if pool.n < len(cuts) + 1:
             raise ValueError("a pool of %d ranks for %d ranges" % (pool.n, len(cuts) + 1))
-    tag = "%s.rank%d" % (os.getpid(), int(time.time() * 1000) & 0xFFFFFF)
     frags, phase2, fr2, spill_bam = [], [], [], None
+    n_def = 0
     try:
         t1 = time.perf_counter()
         foreign = 0
         try:
             ranges = windows_of(cuts)
-            results, frags = run(cuts, pool, in_bam, ranges, tag, 0)
-        except ForeignRecords:  # (no fragments are left)
+            results, frags = run(cuts, pool, ranges, tag, dspan)
+        except ForeignRecords:  # (no fragments are left; only with deferral off)
             if on_foreign == "raise" or not cuts:
                 raise
             foreign = 1
             cuts, ranges = [], windows_of([])
-            results, frags = run(cuts, pool, in_bam, ranges, tag, 0)
+            results, frags = run(cuts, pool, ranges, tag, dspan)
         t2 = time.perf_counter()
-        # phase 2: the templates with a mate on another contig or unmapped, spilled by every rank
-        # from its core share, formed into families by the owners of their keys (the rank whose
-        # interval holds their contig's end), on one BAM of all the spills
-        n_cross = sum(int(x[2].get("spilled", 0)) for x in results)
-        if cuts and n_cross:
+        # phase 2: the deferred templates of every rank's core share, in file order, through one
+        # rank's stream, cut at every rank's deferred keys
+        splices = [x[0]["splices"] for x in results if len(x[0]["splices"])]
+        spilled = sum(int(x[0].get("spilled_bytes", 0)) for x in results)
+        if spilled or splices:
+            late = np.unique(np.concatenate(splices), axis=0) if splices else np.zeros((0, 2), np.int64)
             spill_bam = os.path.join(tmpdir, ".%s.spill.bam" % tag)
-            hw = bam.BamWriter(spill_bam + ".h", hdr, level, None, "first")
-            hw.close(threads)
-            with open(spill_bam, "wb") as out:
-                for part in [spill_bam + ".h"] + [f["spill"] for f in frags]:
-                    with open(part, "rb") as f:
-                        shutil.copyfileobj(f, out, 1 << 24)
-                out.write(EOF_BLOCK)
-            os.unlink(spill_bam + ".h")
-            phase2, fr2 = run(cuts, pool, spill_bam, [None] * len(ranges), tag + "x", 1)
+            n_def = bam.write_spill_bam(spill_bam, hdr, [f["spill"] for f in frags], 1, threads)
+            fr2 = paths(tag + "x", 1, False)
+            job = dict(in_bam=spill_bam, fasta=fasta, out_bam=fr2[0]["bam"], prefix=pre, threads=threads, level=level,
+                       fastq=fr2[0]["fq"], tags=tags, chunk_bytes=chunk_bytes, slack=slack, batch_bases=batch_bases,
+                       gpu_bgzf=gpu_bgzf, rng=None, cuts=[], flags=0, spill=None, fragment="next", defer=0,
+                       late=late, read_size=read_size)
+            try:
+                phase2 = pool.run([job])
+            except BaseException:
+                remove(fr2)
+                raise
         t2b = time.perf_counter()
-        if not cuts:  # one range: its fragments as they are
-            if out_bam is not None:
-                _concat(out_bam, [frags[0]["bam"]])
-            if fastq is not None:
-                for d in range(2):
-                    _concat(fastq[d], [frags[0]["fq"][d]])
-        else:
-            pieces = _pieces(results, frags, phase2, fr2)
-            if out_bam is not None:
-                _assemble(out_bam, pieces, 0)
-            if fastq is not None:
-                for d in range(2):
-                    _assemble(fastq[d], pieces, 1 + d)
+        pieces = []
+        for ph, (res, fr) in enumerate(((results, frags), (phase2, fr2))):
+            for r, (inf, _, _) in enumerate(res):
+                f = fr[r]
+                pieces += bam.pieces_of(inf["marks"], [f["bam"]] + (list(f["fq"]) if f["fq"] else [None, None]), ph, r)
+        dsts = [out_bam, fastq[0] if fastq else None, fastq[1] if fastq else None]
+        for k in range(3):
+            if dsts[k] is not None:
+                bam.assemble(dsts[k], pieces, k)
         t3 = time.perf_counter()
     except BaseException:
         if own:
@@ -380,15 +416,16 @@ def step5_ranks(in_bam: str, fasta: str, out_bam: Optional[str], devices: Sequen
             os.unlink(spill_bam)
         if own:
             pool.close()
-    info = {"ranks": len(ranges), "cuts_fallback": foreign > 0, "cross_records": n_cross, "records_in": 0,
+    info = {"ranks": len(ranges), "cuts_fallback": foreign > 0, "deferred_records": n_def, "records_in": 0,
             "families": 0, "families_emitted": 0, "records_out": 0}
     for inf, st, rs in list(results) + list(phase2):
         for k in ("records_in", "families", "families_emitted", "records_out"):
             info[k] += int(inf.get(k, 0))
     if stats is not None:
         stats.update(cut_s=round(t_cut, 4), pool_start_s=round(t_pool, 4), ranks_s=round(t2 - t1, 4),
-                     cross_s=round(t2b - t2, 4), assemble_s=round(t3 - t2b, 4),
+                     deferred_s=round(t2b - t2, 4), assemble_s=round(t3 - t2b, 4),
                      rank_records=[int(x[0].get("records_in", 0)) for x in results],
                      rank_read=[int(x[2].get("n", 0)) for x in results],
+                     rank_peak_buffered=[int(x[0].get("peak_buffered", 0)) for x in results],
                      rank_seconds=[x[0].get("seconds") for x in results], ranges=ranges)
     return info

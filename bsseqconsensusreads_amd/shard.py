@@ -17,7 +17,6 @@ import sys
 from typing import Callable, Dict, List, Optional, Sequence, Tuple
 
 import numpy as np
-import torch
 
 
 def plan_batches(fam_bases: np.ndarray, batch_bases: int) -> List[Tuple[int, int]]:
@@ -51,6 +50,7 @@ def deal(batches: Sequence[Tuple[int, int]], world: int, rank: int) -> List[int]
 
 def reduce_step(dist, elapsed_s: float, counters: Sequence[int], device) -> Tuple[float, List[int]]:
     """Bench reduction: step time MAX over ranks, counters SUM over ranks.  `dist` None = one rank."""
+    import torch
     t = torch.tensor([float(elapsed_s)], dtype=torch.float64, device=device)
     c = torch.tensor([int(x) for x in counters], dtype=torch.int64, device=device)
     if dist is not None:
@@ -128,7 +128,7 @@ def env_rank() -> Tuple[int, int, int]:
             int(os.environ.get("LOCAL_RANK", "0")))
 
 
-def init(backend: str, device: Optional[torch.device] = None):
+def init(backend: str, device=None):
     """torch.distributed over the environment's rendezvous (127.0.0.1); None for one rank."""
     rank, world, _ = env_rank()
     if world <= 1:

@@ -86,10 +86,15 @@ class SynthSet:
 
 def generate(cfg: str = "C2", n_fam: int = 1000, seed: int = 42, device=None, genome_len: int = 10_000_000,
              read_len: int = 150, chunk: int = 1 << 22, frag: Optional[Tuple[float, float, int]] = None,
-             reuse: Optional["SynthSet"] = None) -> SynthSet:
+             reuse: Optional["SynthSet"] = None, long_frac: float = 0.0, long_span: Tuple[int, int] = (20_000, 5_000_000),
+             long_giant: bool = False) -> SynthSet:
     """frag = (mean, sd, min) overrides the fragment-length model (tests use short inserts to
     exercise read-through trimming; the configs keep the survey's model).  reuse: draw the
-    families on that set's genome (one reference for a stream of chunks)."""
+    families on that set's genome (one reference for a stream of chunks).  long_frac: that
+    fraction of families get a long-span template pair -- fragments log-uniform in long_span
+    (capped at half the genome), the mates that far apart on one contig (discordant pairs of
+    whole-genome data); long_giant: family 0's fragment spans 60 % of the genome.  The other
+    families are drawn as without them."""
     if device is None:
         device = "cuda" if torch.cuda.is_available() else "cpu"
     device = torch.device(device)
@@ -114,6 +119,18 @@ def generate(cfg: str = "C2", n_fam: int = 1000, seed: int = 42, device=None, ge
         fl = fl.round().clamp(160, 600).to(torch.int64)
         fl = torch.clamp(fl, min=L + 2)
     s = (torch.rand(n_fam, generator=gen, device=device) * (genome_len - 1400)).to(torch.int64) + 700
+    if long_frac > 0 or long_giant:
+        import math
+        lf = torch.rand(n_fam, generator=gen, device=device) < long_frac
+        lo, hi = math.log(long_span[0]), math.log(max(long_span[0] + 1, min(long_span[1], genome_len // 2)))
+        u = torch.rand(n_fam, generator=gen, device=device)
+        big = torch.exp(lo + u * (hi - lo)).to(torch.int64)
+        if long_giant:
+            lf[0] = True
+            big[0] = genome_len * 6 // 10
+        fl = torch.where(lf, big, fl)
+        sl = (torch.rand(n_fam, generator=gen, device=device) * (genome_len - fl - 1400).clamp_min(1)).to(torch.int64) + 700
+        s = torch.where(lf, sl, s)
     e = s + fl
 
     # templates: family-major, AB templates first

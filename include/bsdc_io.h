@@ -17,7 +17,7 @@
 extern "C" {
 #endif
 
-#define BSDC_IO_ABI_VERSION 11
+#define BSDC_IO_ABI_VERSION 12
 #define BSDC_IO_EFORMAT (-10) /* not BGZF/BAM, truncated, bad CRC */
 #define BSDC_IO_EIO (-11)     /* open/read/write failed */
 #define BSDC_IO_EINVAL (-22)  /* bad argument */
@@ -132,27 +132,47 @@ int32_t bsdc_bam_stream_next_runs(bsdc_bam_stream *s, int64_t min_bytes, bsdc_ba
  * coordinate lies outside their owner's window [its lower coordinate - slack, its upper + slack)
  * (a mate on another contig, or unmapped: the owner never reads them; ranks.py then falls back to
  * one range); flags BSDC_OWN_STOP_FOREIGN: the first one fails the stream (BSDC_IO_EFORMAT,
- * "foreign record ..."); BSDC_OWN_SPILL_CROSS: cross-key records (below) read in the rank's core
- * coordinates [its lower bound, its upper bound) are spilled instead of streamed, the others
- * dropped; BSDC_OWN_CONTIG_CHUNKS: every chunk's families share one key contig, so the output can
- * be cut between contigs.  bsdc_bam_stream_range_stats: {records read, first coordinate, dropped,
- * foreign, spilled}. */
+ * "foreign record ...").  With bsdc_bam_stream_set_defer no record is foreign: a far record (below)
+ * is spilled by the rank whose core coordinates [its lower bound, its upper bound) hold it and its
+ * key registered by the key's owner.  bsdc_bam_stream_range_stats: {records read, first coordinate,
+ * dropped, foreign, spilled, deferred families, the most record bytes buffered at a chunk
+ * selection}. */
 int32_t bsdc_bam_find_cut(const char *path, int32_t n_threads, int64_t from, int64_t min_span, int64_t slack,
                           int64_t guard, int64_t max_bytes, int64_t *out);
 int32_t bsdc_bam_stream_open_range(const char *path, int32_t n_threads, int64_t read_size, int64_t start_block,
                                    int64_t start_off, int64_t end_block, int64_t end_off, bsdc_bam_stream **out);
 #define BSDC_OWN_STOP_FOREIGN 1   /* set_owner flags: the first foreign record fails the stream */
-#define BSDC_OWN_SPILL_CROSS 2    /* cross-key records of the core range go to bsdc_bam_stream_spill */
-#define BSDC_OWN_CONTIG_CHUNKS 4  /* no chunk holds families of two key contigs */
 int32_t bsdc_bam_stream_set_owner(bsdc_bam_stream *s, int32_t rank, const int64_t *bounds, int32_t n_bounds,
                                   int64_t slack, int32_t flags);
 void bsdc_bam_stream_range_stats(const bsdc_bam_stream *s, int64_t *st);
-/* (IO ABI 11) The cross-key records spilled so far (raw, block_size-prefixed, file order): returns
- * their bytes; with dst, copies them there and forgets them.  A cross key's contig halves differ:
- * the template's mate is on another contig or unmapped, and its key sorts at its contig's end. */
+/* (IO ABI 12) Deferred templates: bounded memory whatever the inserts.  A template whose other end
+ * lies more than `span` positions away (bsdc_bam_stream_set_defer, before the first chunk; 0 = off)
+ * or on another contig, unmapped or absent (a cross key: it sorts at its contig's end) would hold
+ * every family after its key until the stream reaches that end.  Its records (a "far" record: its
+ * own mate fields say so) leave the stream for the spill instead, unless its MI family is buffered
+ * (a molecule whose other templates are near: the record joins it), and its key is registered.  A
+ * buffered family whose coarse keys come within 3 x 4 positions of a registered key may interleave
+ * with it in TemplateCoordinate order: it is spilled too, and its keys registered.  So the chunks'
+ * families and the spill's are each whole, and the output is the chunks' outputs with the spill's
+ * families spliced in at the registered keys (bam.py: a second pass over the spill, then
+ * assembly).  A far record whose key lies at or behind the output already cut (its template's lower
+ * record is missing) fails the stream (BSDC_IO_EFORMAT).
+ * bsdc_bam_stream_spill: the spilled entries so far -- per record an int64 coordinate (contig << 32
+ * | position, unmapped last), an int64 sequence number (its place in the stream's file order), then
+ * the record (block_size-prefixed) -- returns their bytes; with dst, copies them there and forgets
+ * them.  Sorted by (coordinate, sequence) they are in file order.
+ * bsdc_bam_stream_splices: the registered keys the last chunk reported (2 int64 each, ascending;
+ * after the last chunk, at the end of the stream, every key left): its output is cut before its
+ * first family whose key exceeds each, and the spill's families of that key go there.  Returns
+ * their count; with dst, copies them there and forgets them.
+ * bsdc_bam_rec_keys: the coarse TemplateCoordinate key of every record of a chunk or file (raw or
+ * parsed), in record order: out[2k] = lower end's contig << 32 | other end's contig (0x7FFFFFFF:
+ * unmapped or absent), out[2k + 1] = the lower end's unclipped 5' position, from the input's
+ * cigar and MC; within 4 positions of the key of the records tools 1 and 2 make. */
+int32_t bsdc_bam_stream_set_defer(bsdc_bam_stream *s, int64_t span);
 int64_t bsdc_bam_stream_spill(bsdc_bam_stream *s, uint8_t *dst);
-/* The key contig (key first component >> 32) of the families of the last chunk (-1: none yet). */
-int64_t bsdc_bam_stream_chunk_contig(const bsdc_bam_stream *s);
+int64_t bsdc_bam_stream_splices(bsdc_bam_stream *s, int64_t *dst);
+int32_t bsdc_bam_rec_keys(const bsdc_bam *b, int64_t *out);
 
 /* Records to write (n_rec entries; every *_off array has n_rec + 1 entries). */
 typedef struct {

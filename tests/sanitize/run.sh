@@ -32,4 +32,4 @@ assert '$OUT/libbsdc_io.so' in maps and '$OUT/liboracle.so' in maps, 'instrument
 print('sanitizer builds loaded:', '$OUT')
 "
 python -m pytest -q -p no:cacheprovider tests/test_bam.py tests/test_families.py tests/test_oracle_golden.py \
-    tests/test_host_plan.py tests/test_bgzf.py "$@"
+    tests/test_host_plan.py tests/test_bgzf.py tests/test_stream.py tests/test_long_span.py "$@"

@@ -56,7 +56,39 @@ def test_cli_ranks_cross_contig_mates(cross_input):  # noqa: F811
                         "--gpus", "2", "--devices", "0,0"], env=env, capture_output=True, text=True, timeout=300)
     assert p.returncode == 0, p.stderr[-3000:]
     info = json.loads(p.stderr.strip().splitlines()[-1])
-    assert info["ranks"] == 2 and not info["cuts_fallback"] and info["cross_records"] > 100
+    assert info["ranks"] == 2 and not info["cuts_fallback"] and info["deferred_records"] > 100
     got = [gzip.decompress((tmp / ("x2%s" % x)).read_bytes()) for x in (".bam", "1.fq.gz", "2.fq.gz")]
     assert got == one
     assert assert_bam_matches_oracle(str(tmp / "x2.bam"), inp, fa, "cli --gpus 2 ranks, cross-contig") > 0
+
+
+@pytest.fixture(scope="module")
+def long_gpu_input(tmp_path_factory):
+    from test_long_span import _long_input
+    tmp = tmp_path_factory.mktemp("longgpu")
+    raw, p, fa, span = _long_input(tmp, n_fam=2000, cross=0.03)
+    return raw, p, fa, tmp
+
+
+def test_cli_long_span_templates(long_gpu_input):  # noqa: F811
+    """Long-span templates (mates 20 kb - 2.5 Mb away, one spanning 60% of the contig) and mates
+    on a second contig on the GPU: the one-GPU stream defers them and splices
+    their families in (with the GPU BGZF too), two ranks on GPU 0 do the same with no fallback; all
+    decompress to the same bytes and equal oracle/ on the whole file"""
+    raw, inp, fa, tmp = long_gpu_input
+    one = [gzip.decompress(b) for b in _cli(tmp, inp, fa, "L_one")]
+    gz = [gzip.decompress(b) for b in _cli(tmp, inp, fa, "L_gz", "--gpu-bgzf", "true")]
+    assert gz == one
+    assert assert_bam_matches_oracle(str(tmp / "L_one.bam"), inp, fa, "cli one GPU, long-span") > 0
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    env = {k: v for k, v in os.environ.items() if k not in ("WORLD_SIZE", "RANK", "LOCAL_RANK")}
+    env["PYTHONPATH"] = root + os.pathsep + env.get("PYTHONPATH", "")
+    p = subprocess.run([sys.executable, "-m", "bsseqconsensusreads_amd.cli", "step5", "--reference", fa, inp,
+                        str(tmp / "L2.bam"), "--fastq1", str(tmp / "L21.fq.gz"), "--fastq2", str(tmp / "L22.fq.gz"),
+                        "--threads", "4", "--batch-bases", "20000", "--chunk-mb", "0",
+                        "--gpus", "2", "--devices", "0,0"], env=env, capture_output=True, text=True, timeout=300)
+    assert p.returncode == 0, p.stderr[-3000:]
+    info = json.loads(p.stderr.strip().splitlines()[-1])
+    assert info["ranks"] == 2 and not info["cuts_fallback"] and info["deferred_records"] > 100
+    got = [gzip.decompress((tmp / ("L2%s" % x)).read_bytes()) for x in (".bam", "1.fq.gz", "2.fq.gz")]
+    assert got == one

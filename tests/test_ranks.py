@@ -235,10 +235,38 @@ def test_cross_contig_and_unmapped_mates(cross_input, n):  # noqa: F811
     info1, _, ref_bytes, _ = _run(tmp, p, fa, "x1", 1)
     info, st, got, _ = _run(tmp, p, fa, "x%d" % n, n)
     assert info["ranks"] == n and not info["cuts_fallback"]
-    assert info["cross_records"] > 100
+    assert info["deferred_records"] > 100
     assert info["records_in"] == info1["records_in"] == raw.n
     for a, b in zip(got, ref_bytes):
         assert a == b
     assert not [f for f in os.listdir(tmp) if f.startswith(".")], "pieces left behind"
     if n == 3:  # (and the records are the whole file's, against oracle/)
         assert_bam_matches_oracle(str(tmp / "x3.bam"), p, fa, "ranks, cross-contig mates") > 0
+
+
+@pytest.fixture(scope="module")
+def long_input(tmp_path_factory):
+    """Long-span templates (2% of families with mates 20 kb - 2.5 Mb away, one spanning 60% of the
+    contig) and mates on a second contig: every far template is deferred by the rank whose core
+    holds its records and spliced in at its key."""
+    from test_long_span import _long_input
+    tmp = tmp_path_factory.mktemp("long")
+    raw, p, fa, span = _long_input(tmp, n_fam=2000, cross=0.03)
+    return raw, p, fa, tmp
+
+
+@pytest.mark.parametrize("n", [2, 3])
+def test_long_span_ranks_equal_one_range(long_input, n):  # noqa: F811
+    """No rank stops on a far record (no fallback), the bytes equal the one-range run's, the records
+    equal oracle/ on the whole file, and every rank's buffered bytes stay a few chunks"""
+    raw, p, fa, tmp = long_input
+    info1, _, ref_bytes, _ = _run(tmp, p, fa, "L1", 1, read_size=16 << 10)
+    info, st, got, out = _run(tmp, p, fa, "L%d" % n, n, read_size=16 << 10)
+    assert info["ranks"] == n and not info["cuts_fallback"]
+    assert info["deferred_records"] > 100
+    for a, b in zip(got, ref_bytes):
+        assert a == b
+    assert max(st["rank_peak_buffered"]) <= 8 * 80_000, st["rank_peak_buffered"]
+    assert not [f for f in os.listdir(tmp) if f.startswith(".")], "pieces left behind"
+    if n == 3:
+        assert_bam_matches_oracle(out, p, fa, "ranks, long-span templates") > 0
