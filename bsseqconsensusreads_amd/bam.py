@@ -149,6 +149,8 @@ def _load():
     lib.bsdc_bam_stream_splices.restype = C.c_int64
     lib.bsdc_bam_rec_keys.argtypes = [_P, _P]
     lib.bsdc_bam_rec_keys.restype = C.c_int32
+    lib.bsdc_spill_sort.argtypes = [_P, C.c_int64, _P, _P]
+    lib.bsdc_spill_sort.restype = C.c_int64
     lib.bsdc_bam_writer_flush.argtypes = [_P, C.c_int32]
     lib.bsdc_bam_writer_flush.restype = C.c_int32
     lib.bsdc_bam_writer_tell.argtypes = [_P]
@@ -435,26 +437,21 @@ def _stream_splices(lib, st) -> np.ndarray:
     return out[:n]
 
 
-def spill_sorted_records(data: bytes) -> bytes:
-    """Spill entries (_stream_spill, possibly several streams' concatenated) -> their records in
-    file order: sorted by (coordinate, sequence), the stable order of the input for equal pairs."""
+def spill_sorted_records(data: bytes):
+    """Spill entries (_stream_spill, possibly several streams' concatenated) -> (their records in
+    file order -- sorted by (coordinate, sequence), the stable order of the input for equal pairs
+    (bsdc_spill_sort) --, their count)."""
     if not data:
-        return b""
+        return b"", 0
+    lib = _load()
     a = np.frombuffer(data, np.uint8)
-    offs, p = [], 0
-    n = a.shape[0]
-    while p < n:  # (entries: 16-byte key, 4-byte block_size, the rest of the record)
-        offs.append(p)
-        p += 20 + int(a[p + 16:p + 20].view(np.uint32)[0])
-    if p != n:
-        raise ValueError("truncated spill")
-    offs = np.array(offs, np.int64)
-    c = np.array([int(a[o:o + 8].view(np.int64)[0]) for o in offs], np.int64) if offs.shape[0] < 64 else \
-        a[(offs[:, None] + np.arange(8)).reshape(-1)].view(np.int64)
-    q = a[(offs[:, None] + 8 + np.arange(8)).reshape(-1)].view(np.int64)
-    order = np.lexsort((np.arange(offs.shape[0]), q, c))
-    ends = np.append(offs[1:], n)
-    return b"".join(data[int(offs[i]) + 16:int(ends[i])] for i in order)
+    cnt = np.zeros(1, np.int64)
+    n = int(lib.bsdc_spill_sort(_ptr(a), a.shape[0], None, _ptr(cnt)))
+    if n < 0:
+        raise ValueError("spill: %s" % lib.bsdc_io_last_error().decode())
+    out = np.empty(max(n, 1), np.uint8)
+    lib.bsdc_spill_sort(_ptr(a), a.shape[0], _ptr(out), None)
+    return out[:n].tobytes(), int(cnt[0])
 
 
 def stream_chunks(path: str, threads: int = 0, chunk_bytes: int = DEFAULT_CHUNK_BYTES, slack: int = DEFAULT_SLACK,
@@ -1393,17 +1390,13 @@ EOF_BLOCK = bytes.fromhex("1f8b08040000000000ff0600424302001b0003000000000000000
 def write_spill_bam(dst: str, header: "BamHeader", spills: Sequence[str], level: int = 1, threads: int = 0) -> int:
     """The spill files' records (bsdc_bam_stream_spill entries) in file order as a BAM -> records."""
     data = b"".join(open(x, "rb").read() for x in spills if x and os.path.exists(x))
-    recs = spill_sorted_records(data)
+    recs, n = spill_sorted_records(data)
+    del data
     w = BamWriter(dst, header, level)
     try:
         w.add_raw(recs, threads)
     finally:
         w.close(threads)
-    n, p = 0, 0
-    mv = memoryview(recs)
-    while p < len(recs):
-        p += 4 + int.from_bytes(mv[p:p + 4], "little")
-        n += 1
     return n
 
 

@@ -1881,6 +1881,36 @@ int32_t bsdc_bam_stream_next_runs(bsdc_bam_stream *s, int64_t min_bytes, bsdc_ba
     }
 }
 
+// Spill entries (bsdc_bam_stream_spill; several streams' concatenated) -> their records in file
+// order (see include/bsdc_io.h).
+int64_t bsdc_spill_sort(const uint8_t *data, int64_t n, uint8_t *out, int64_t *n_rec) {
+    struct E {
+        int64_t c, q, off, len;
+    };
+    std::vector<E> es;
+    int64_t p = 0, total = 0;
+    while (p < n) {
+        if (p + 20 > n) return fail(BSDC_IO_EFORMAT, "truncated spill");
+        E e;
+        memcpy(&e.c, data + p, 8);
+        memcpy(&e.q, data + p + 8, 8);
+        e.off = p + 16;
+        e.len = 4 + (int64_t)rd32(data + p + 16);
+        if (e.off + e.len > n) return fail(BSDC_IO_EFORMAT, "truncated spill");
+        es.push_back(e);
+        total += e.len;
+        p = e.off + e.len;
+    }
+    if (n_rec) *n_rec = (int64_t)es.size();
+    if (!out) return total;
+    std::stable_sort(es.begin(), es.end(), [](const E &x, const E &y) { return x.c != y.c ? x.c < y.c : x.q < y.q; });
+    std::vector<int64_t> dst(es.size() + 1, 0);
+    for (size_t i = 0; i < es.size(); i++) dst[i + 1] = dst[i] + es[i].len;
+#pragma omp parallel for schedule(dynamic, 1024)
+    for (int64_t i = 0; i < (int64_t)es.size(); i++) memcpy(out + dst[(size_t)i], data + es[(size_t)i].off, (size_t)es[(size_t)i].len);
+    return total;
+}
+
 // The coarse TemplateCoordinate key of every record of b, in record order (see include/bsdc_io.h).
 int32_t bsdc_bam_rec_keys(const bsdc_bam *b, int64_t *out) {
     const int64_t n = (int64_t)b->rec_start.size();

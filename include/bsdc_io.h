@@ -173,6 +173,11 @@ int32_t bsdc_bam_stream_set_defer(bsdc_bam_stream *s, int64_t span);
 int64_t bsdc_bam_stream_spill(bsdc_bam_stream *s, uint8_t *dst);
 int64_t bsdc_bam_stream_splices(bsdc_bam_stream *s, int64_t *dst);
 int32_t bsdc_bam_rec_keys(const bsdc_bam *b, int64_t *out);
+/* Spill entries (bsdc_bam_stream_spill's bytes, several streams' concatenated) -> their records,
+ * sorted by (coordinate, sequence) -- file order -- into out (stable for equal pairs); returns the
+ * records' bytes (out NULL: the size only) and their count in *n_rec (if not NULL), < 0 on a
+ * malformed spill. */
+int64_t bsdc_spill_sort(const uint8_t *data, int64_t n, uint8_t *out, int64_t *n_rec);
 
 /* Records to write (n_rec entries; every *_off array has n_rec + 1 entries). */
 typedef struct {

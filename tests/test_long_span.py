@@ -113,3 +113,22 @@ def test_no_far_templates_writes_in_place(standin, tmp_path):  # noqa: F811
     info = bam.step5_stream(p, fa, b, engine=standin, threads=2, level=1, chunk_bytes=CHUNK, slack=2000)
     assert info["deferred_families"] == 0 and info["splices"].shape[0] == 0
     assert open(a, "rb").read() == open(b, "rb").read()
+
+
+def test_spill_entries_sort_back_to_file_order():
+    """bsdc_spill_sort: entries {coordinate, sequence, record} from several streams, out of order,
+    come back as their records sorted by (coordinate, sequence), stably; a truncated spill fails"""
+    rng = np.random.default_rng(3)
+    ents, want = [], []
+    for k in range(300):
+        c, q = int(rng.integers(0, 50)), int(rng.integers(0, 1 << 40))
+        body = bytes(rng.integers(0, 256, int(rng.integers(32, 90)), dtype=np.uint8))
+        rec = len(body).to_bytes(4, "little") + body
+        ents.append((c, q, k, rec))
+    order = sorted(ents, key=lambda e: (e[0], e[1], e[2]))
+    data = b"".join(c.to_bytes(8, "little", signed=True) + q.to_bytes(8, "little", signed=True) + r
+                    for c, q, _, r in ents)
+    got, n = bam.spill_sorted_records(data)
+    assert n == 300 and got == b"".join(e[3] for e in order)
+    with pytest.raises(ValueError):
+        bam.spill_sorted_records(data[:-5])
