@@ -1288,8 +1288,8 @@ def step5_stream(in_bam: str, fasta: str, out_bam: Optional[str], engine=None, p
                  defer: Optional[int] = None, read_size: int = 8 << 20) -> dict:
     """step5 in bounded memory, pipelined (_stream_step); defer: the span past which a template is
     deferred (default DEFAULT_DEFER_SPAN; 0 = off); read_size: compressed bytes per refill."""
-    return _stream_step(in_bam, fasta, out_bam, engine, prefix, threads, level, fastq, tags, chunk_bytes, slack,
-                        batch_bases, stats, gpu_bgzf, None, defer=defer, read_size=read_size)
+    return _public(_stream_step(in_bam, fasta, out_bam, engine, prefix, threads, level, fastq, tags, chunk_bytes,
+                                slack, batch_bases, stats, gpu_bgzf, None, defer=defer, read_size=read_size))
 
 
 def molecular_stream(in_bam: str, out_bam: Optional[str], engine=None, prefix: Optional[str] = None, threads: int = 0,
@@ -1302,8 +1302,15 @@ def molecular_stream(in_bam: str, out_bam: Optional[str], engine=None, prefix: O
     the vote alone, --min-consensus-base-quality applied).  The output is byte-identical to
     molecular()'s whole-file path: no run straddles two chunks.  The reference's rule needs -Xmx100g
     (main.snake.py:54, README.md:83); this holds about six chunks."""
-    return _stream_step(in_bam, None, out_bam, engine, prefix, threads, level, fastq, tags, chunk_bytes, DEFAULT_SLACK,
-                        batch_bases, stats, gpu_bgzf, int(min_consensus_base_quality))
+    return _public(_stream_step(in_bam, None, out_bam, engine, prefix, threads, level, fastq, tags, chunk_bytes,
+                                DEFAULT_SLACK, batch_bases, stats, gpu_bgzf, int(min_consensus_base_quality)))
+
+
+def _public(info: dict) -> dict:
+    """The stream's info as the CLI prints it (JSON): the spliced keys become their count"""
+    sp = info.pop("splices", None)
+    info["spliced_families"] = 0 if sp is None else int(len(sp))
+    return info
 
 
 MINKEY = -(1 << 62)  # sort key of the pieces before every family (the header, a first range's start)

@@ -912,8 +912,10 @@ __device__ __forceinline__ void small_family(const KParams &P, const Tables *T, 
     const int max_len = B.max_len;
     const int stop = (P.mode >> BSDC_MODE_STOP_SHIFT) & 15;  // profiling ablation (0 = full kernel)
 
-    // list entry: family id, first record, record count | image size / 32 << 8, image base
-    const uint4 ent = reinterpret_cast<const uint4 *>(fams)[fi];
+    // list entry: family id, first record, record count | image size / 32 << 8, image base (the
+    // index made wave-uniform: one scalar load, s_load_dwordx4, instead of a vector load and five
+    // readfirstlanes)
+    const uint4 ent = reinterpret_cast<const uint4 *>(fams)[__builtin_amdgcn_readfirstlane((int)fi)];
     const uint32_t fam = __builtin_amdgcn_readfirstlane(ent.x);
     const uint32_t r0 = __builtin_amdgcn_readfirstlane(ent.y);
     const int n = (int)(__builtin_amdgcn_readfirstlane(ent.z) & 0xFF);
@@ -986,8 +988,10 @@ __device__ __forceinline__ void small_family(const KParams &P, const Tables *T, 
     const int nconv = __builtin_popcountll(conv_mask);
     const int ci = mbcnt(conv_mask);
     int cops = (int)(cinfo & 0xFFFF);
+    if (ballot(cops != 0)) {  // (most families: no complex cigar, no six-step reduction)
 #pragma unroll
-    for (int o = 32; o >= 1; o >>= 1) cops += __shfl_xor(cops, o, kWave);
+        for (int o = 32; o >= 1; o >>= 1) cops += __shfl_xor(cops, o, kWave);
+    }
     const SmallLayout Lo(n, img, nconv, cops, max_len);
     uint8_t *refw = A + Lo.ref;
     const int ws = Lo.ws;
