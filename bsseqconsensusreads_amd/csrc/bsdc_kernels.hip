@@ -1501,31 +1501,22 @@ __device__ __forceinline__ void small_family(const KParams &P, const Tables *T, 
                 // TAGS: the single-strand reads and their column statistics, fused into the vote
                 // (fgbio's per-read / per-base consensus tags).  A column whose side agrees (not
                 // slow) is that side's one base at its Q (or N / 2 below the mask), depth = its
-                // A/C/G/T reads, errors 0; a slow column's bytes are the queue's.
+                // A/C/G/T reads, errors 0.  Whole dwords: a slow column's bytes are rewritten by
+                // the queue below (the same wavefront's later store to the same address: no
+                // ordering is needed between the lanes of one wavefront), and the bytes past the
+                // set's own length (c + 3 < stride) are never read (ss_len).  Writing only the
+                // agreeing columns' bytes cost the tag leg 0.4 ms on C2 (profiles/r06/README.md).
                 if (TAGS && c < lv) {
 #pragma unroll
                     for (int side = 0; side < 2; side++) {
                         const int s = side == 0 ? sa : sb;
                         if (!(side == 0 ? hA : hB)) continue;
-                        const uint32_t wr = (side == 0 ? inA & ~slowA : inB & ~slowB);
-                        const uint32_t bb = ss[2 * side], qq = ss[2 * side + 1];
                         const uint32_t n4 = nf[side] + __builtin_bswap32(nr[side]);  // (<= 64 reads: bytes)
                         const int64_t at = (4 * (int64_t)fam + s) * stride + c;
-                        if (wr == 0xFFFFFFFFu) {
-                            *reinterpret_cast<uint32_t *>(P.O.ss_base + at) = bb;
-                            *reinterpret_cast<uint32_t *>(P.O.ss_qual + at) = qq;
-                            *reinterpret_cast<uint32_t *>(P.O.ss_depth + at) = n4;
-                            *reinterpret_cast<uint32_t *>(P.O.ss_err + at) = 0u;
-                        } else if (wr != 0u) {
-#pragma unroll
-                            for (int j = 0; j < 4; j++) {
-                                if (!((wr >> (8 * j)) & 0xFFu)) continue;
-                                P.O.ss_base[at + j] = (uint8_t)(bb >> (8 * j));
-                                P.O.ss_qual[at + j] = (uint8_t)(qq >> (8 * j));
-                                P.O.ss_depth[at + j] = (uint8_t)(n4 >> (8 * j));
-                                P.O.ss_err[at + j] = 0;
-                            }
-                        }
+                        *reinterpret_cast<uint32_t *>(P.O.ss_base + at) = ss[2 * side];
+                        *reinterpret_cast<uint32_t *>(P.O.ss_qual + at) = ss[2 * side + 1];
+                        *reinterpret_cast<uint32_t *>(P.O.ss_depth + at) = n4;
+                        *reinterpret_cast<uint32_t *>(P.O.ss_err + at) = 0u;
                     }
                 }
             }

@@ -6,6 +6,7 @@ Their tag outputs are wrong by construction; the untagged instance is untouched.
   noqueue: no single-strand stores (nor per-base counts) in the queued columns' path
   ollen:   the vote loop runs to the duplex length, not the single strands' longer one
   bare:    all three
+  st1/st2/st3: the fast path's full-dword stores cut to ss_base / + ss_qual / + ss_depth
 Usage (CPU, this container): python profiles/tag_variants.py"""
 import os
 import subprocess
@@ -18,13 +19,20 @@ OUT = os.path.join(ROOT, "profiles", "_build")
 FAST = ("if (TAGS && c < lv) {", "if (false && TAGS && c < lv) {")
 QUEUE = ("if (TAGS) {  // this side's single-strand column", "if (false) {  // this side's single-strand column")
 OLLEN = ("const int lv = TAGS ? ::max(la, lb) : ol;", "const int lv = ol;")
-VARIANTS = {"nofast": [FAST], "noqueue": [QUEUE], "ollen": [OLLEN], "bare": [FAST, QUEUE, OLLEN]}
+ST_Q = ("                            *reinterpret_cast<uint32_t *>(P.O.ss_qual + at) = qq;\n", "")
+ST_D = ("                            *reinterpret_cast<uint32_t *>(P.O.ss_depth + at) = n4;\n", "")
+ST_E = ("                            *reinterpret_cast<uint32_t *>(P.O.ss_err + at) = 0u;\n", "")
+VARIANTS = {"nofast": [FAST], "noqueue": [QUEUE], "ollen": [OLLEN], "bare": [FAST, QUEUE, OLLEN],
+            "st1": [ST_Q, ST_D, ST_E], "st2": [ST_D, ST_E], "st3": [ST_E]}
 
 
 def main():
     src = open(os.path.join(CSRC, "bsdc_kernels.hip")).read()
     os.makedirs(OUT, exist_ok=True)
+    only = sys.argv[1:]
     for name, edits in VARIANTS.items():
+        if only and name not in only:
+            continue
         s = src
         for a, b in edits:
             assert s.count(a) == 1, (name, a)
