@@ -1789,8 +1789,9 @@ __device__ void large_emit(const KParams &P, uint32_t fam, const int *cnt, const
 }
 
 // The parts' sums in scratch (include/bsdc.h split_partial_off): header [part][8] int32 (set
-// reads, set lengths), then int32x4 likelihood sums and u8x4 A/C/G/T read counts per (part, set,
-// column), the column pitch being the output stride.
+// reads, set lengths), then per (part, set) rows of the output stride's pitch: int32x4 likelihood
+// sums (slot k: the set's k-th multi-base column), u8x4 A/C/G/T read counts and int32 one-base sums
+// (or slot numbers) by column.
 
 // a[s] for a lane-varying or loop-variable s, as selects: a dynamically indexed local array goes to
 // scratch (k_large's PART instances had 32-48 B of it)
@@ -1809,7 +1810,7 @@ __device__ __forceinline__ bool multi_base(uint32_t m) {
 }
 // A part's column: its read counts per base (u8 x4; without TAGS only the OR of its A/C/G/T codes,
 // u8), and the likelihood sum of its one base when only one has reads (`one`, 4 B: most columns),
-// else the four sums (`sum`, 16 B; k_join reads them only then).
+// else the slot of its four sums (`one` = k, `sum` row slot k, 16 B; k_join reads them only then).
 struct PartSums {
     int32_t *head;
     uint4 *sum;
@@ -2355,16 +2356,17 @@ __device__ void process_large(const KParams &P, uint8_t *A, uint8_t *s_tab, cons
         }
     };
     // PART: a multi-base column's per-base sums (int32: a part holds < 255 reads a set) and counts
-    auto part_write = [&](int s, int col, long long D0, long long D1, long long D2, long long D3, uint32_t n01, uint32_t n23) {
+    // (PART) pass B's marked columns are the multi-base ones; the k-th of set s leaves its four
+    // sums in slot k of the set's row (its `one`, written in pass A, holds k)
+    auto part_write = [&](int s, int col, int k, long long D0, long long D1, long long D2, long long D3, uint32_t n01,
+                          uint32_t n23) {
         const PartSums ps(P);
-        const int64_t at = ps.at(blockIdx.x, s, col);
-        const uint32_t m = (n01 & 0xFFu) | ((n01 >> 8) & 0xFF00u) | ((n23 & 0xFFu) << 16) | ((n23 >> 16) << 24);
-        if (TAGS) ps.cnt[at] = m;
-        if (!TAGS || multi_base(m)) {  // (without TAGS pass B sees only multi-base columns; pass A wrote their OR)
-            ps.sum[at] = make_uint4((uint32_t)(int32_t)D0, (uint32_t)(int32_t)D1, (uint32_t)(int32_t)D2, (uint32_t)(int32_t)D3);
-        } else {  // (one base or none: the others' sums are 0)
-            ps.one[at] = (int32_t)(m & 0xFFu ? D0 : m & 0xFF00u ? D1 : m & 0xFF0000u ? D2 : D3);
+        if (TAGS) {
+            ps.cnt[ps.at(blockIdx.x, s, col)] =
+                (n01 & 0xFFu) | ((n01 >> 8) & 0xFF00u) | ((n23 & 0xFFu) << 16) | ((n23 >> 16) << 24);
         }
+        ps.sum[ps.at(blockIdx.x, s, k)] =
+            make_uint4((uint32_t)(int32_t)D0, (uint32_t)(int32_t)D1, (uint32_t)(int32_t)D2, (uint32_t)(int32_t)D3);
     };
     // Wavefronts by set: wave w works on set w % 4; with 8 waves (512 threads) the two waves of a
     // set split its reads (PARTS = 2).
@@ -2390,6 +2392,7 @@ __device__ void process_large(const KParams &P, uint8_t *A, uint8_t *s_tab, cons
         const uint2 *dl = desc + pick4<PART>(soff, ws);
         const int rb = wpart * na / PARTS, re = (wpart + 1) * na / PARTS;  // this wave's share of the set's reads
         const int lmax = ::max(::max(lcv[0], lcv[1]), ::max(lcv[2], lcv[3]));
+        int nmk = 0;  // (PART) the set's marked columns before this block
         for (int cb = 0; cb < lmax; cb += 4 * kWave) {  // the same trip count in every wave (barriers inside)
             const int c = cb + 4 * lane, c8 = 8 * c;
             long long T0 = 0, T1 = 0, T2 = 0, T3 = 0;
@@ -2486,6 +2489,25 @@ __device__ void process_large(const KParams &P, uint8_t *A, uint8_t *s_tab, cons
                 // several times (C4 part dispatch: 1034 -> 263 MB written, profiles/r05/README.md)
                 uint32_t or4 = 0, cnt4[4] = {0u, 0u, 0u, 0u};
                 int32_t one4[4] = {0, 0, 0, 0};
+                // PART: a multi-base column's four sums go to the slot of its rank among the set's
+                // marked columns (pass B's mlist order), and its `one` holds that rank: the join's
+                // lanes then read neighbouring columns' sums from neighbouring slots (by column, a
+                // sparse 16-B read per line cost k_join 2.2x the bytes the parts wrote)
+                uint32_t mrank = 0;
+                if (PART) {
+                    uint32_t mk4 = 0;
+#pragma unroll
+                    for (int j = 0; j < 4; j++) {
+                        uint32_t ob = (orm >> (8 * j)) & 0xFFu;
+                        if (PARTS >= 2 && c + j < lc) ob |= por[ws * ssw + c + j];
+                        if (c + j < lc && (ob & (ob - 1)) != 0) mk4 |= 1u << j;
+                    }
+#pragma unroll
+                    for (int j = 0; j < 4; j++) mrank += mbcnt(ballot((mk4 >> j) & 1u));
+                    mrank += (uint32_t)nmk;
+#pragma unroll
+                    for (int j = 0; j < 4; j++) nmk += __builtin_popcountll(ballot((mk4 >> j) & 1u));
+                }
 #pragma unroll
                 for (int j = 0; j < 4; j++) {
                     const int col = c + j;
@@ -2505,6 +2527,7 @@ __device__ void process_large(const KParams &P, uint8_t *A, uint8_t *s_tab, cons
                             cnt4[j] = ob ? nj << (8 * bi) : 0u;
                             ssq[ws * ssw + col] = 1;
                         } else {
+                            one4[j] = (int32_t)mrank++;
                             ssq[ws * ssw + col] = 0;
                         }
                         or4 |= ob << (8 * j);
@@ -2675,14 +2698,14 @@ __device__ void process_large(const KParams &P, uint8_t *A, uint8_t *s_tab, cons
                         }
                     }
                     if (PART)
-                        part_write(s, col, D0, D1, D2, D3, n01, n23);
+                        part_write(s, col, k0 + cl, D0, D1, D2, D3, n01, n23);
                     else
                         resolve(s, col, D0, D1, D2, D3, TAGS ? n01 : 0u, TAGS ? n23 : 0u);
                 }
                 __syncthreads();
             } else if (act) {
                 if (PART)
-                    part_write(s, col, D0, D1, D2, D3, n01, n23);
+                    part_write(s, col, k0 + cl, D0, D1, D2, D3, n01, n23);
                 else
                     resolve(s, col, D0, D1, D2, D3, n01, n23);
             }
@@ -2823,7 +2846,7 @@ __device__ void join_family(const KParams &P, uint4 e0, uint4 e1, uint8_t *rows,
                     m[u] = in[u] ? m[u] : 0u;
                     o[u] = in[u] ? o[u] : 0;
                     const int pc = ::min(pb + u, np - 1);
-                    sm[u] = ps.sum[multi(m[u]) ? ps.at(p0 + pc, s, c) : 0];
+                    sm[u] = ps.sum[multi(m[u]) ? ps.at(p0 + pc, s, o[u]) : 0];  // (a multi-base column's `one`: its slot)
                 }
 #pragma unroll
                 for (int u = 0; u < kJoinU; u++) add(four(m[u], o[u], sm[u]), m[u]);
@@ -2833,7 +2856,7 @@ __device__ void join_family(const KParams &P, uint4 e0, uint4 e1, uint8_t *rows,
                 if (c >= ps.head[8 * (p0 + p) + 4 + s]) continue;  // (a part whose set ends before c wrote nothing there)
                 const uint32_t x = rec(ps.at(p0 + p, s, c));
                 const int32_t o = ps.one[ps.at(p0 + p, s, c)];
-                add(four(x, o, multi(x) ? ps.sum[ps.at(p0 + p, s, c)] : make_uint4(0u, 0u, 0u, 0u)), x);
+                add(four(x, o, multi(x) ? ps.sum[ps.at(p0 + p, s, o)] : make_uint4(0u, 0u, 0u, 0u)), x);
             }
         }
         const int best = first_max4(D0, D1, D2, D3);

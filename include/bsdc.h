@@ -110,10 +110,11 @@ typedef struct {
                                     parts, fallback arena offset in scratch / 16, fallback arena bytes */
     int64_t n_split_fams;
     int64_t split_partial_off;   /* scratch offset of the parts' sums: [part][8] int32 (set reads, set
-                                    lengths), then [part][4][stride] int32x4 sums, [part][4][stride] u8x4
-                                    counts (without BSDC_MODE_TAGS: byte 0..stride-1 of each count row
-                                    holds the column's OR of one-hot A/C/G/T codes instead), [part][4]
-                                    [stride] int32 one-base sums */
+                                    lengths), then [part][4][stride] int32x4 sums (slot k: the set's
+                                    k-th multi-base column), [part][4][stride] u8x4 counts (without
+                                    BSDC_MODE_TAGS: byte 0..stride-1 of each count row holds the
+                                    column's OR of one-hot A/C/G/T codes instead), [part][4][stride]
+                                    int32 one-base sums (a multi-base column: its sums' slot k) */
 } bsdc_family_batch;
 
 /* Outputs (device pointers).  Consensus slot (f, end) holds `stride` bases. */

@@ -34,6 +34,18 @@ __global__ void wr(T *__restrict__ dst, size_t n) {
     }
 }
 
+// one byte per lane (k_join's part OR records, the tag rows' partial columns)
+__global__ void rd8(const uint8_t *__restrict__ src, size_t n, uint32_t *__restrict__ sink) {
+    uint32_t acc = 0;
+    for (size_t i = blockIdx.x * (size_t)blockDim.x + threadIdx.x; i < n; i += (size_t)gridDim.x * blockDim.x)
+        acc = acc * 0x01000193u + src[i];  // (all 32 bits live: the loads stay)
+    if (acc == 0x9E3779B9u) sink[blockIdx.x] = acc;
+}
+__global__ void wr8(uint8_t *__restrict__ dst, size_t n) {
+    for (size_t i = blockIdx.x * (size_t)blockDim.x + threadIdx.x; i < n; i += (size_t)gridDim.x * blockDim.x)
+        dst[i] = (uint8_t)i;
+}
+
 #define CHECK(x)                                                                 \
     do {                                                                         \
         hipError_t e = (x);                                                      \
@@ -55,9 +67,11 @@ int main() {
         hipLaunchKernelGGL(rd<uint4>, grid, block, 0, 0, (const uint4 *)a, kBytes / 16, sink);
         hipLaunchKernelGGL(rd<uint2>, grid, block, 0, 0, (const uint2 *)a, kBytes / 8, sink);
         hipLaunchKernelGGL(rd<uint32_t>, grid, block, 0, 0, (const uint32_t *)a, kBytes / 4, sink);
+        hipLaunchKernelGGL(rd8, grid, block, 0, 0, (const uint8_t *)a, kBytes, sink);
         hipLaunchKernelGGL(wr<uint4>, grid, block, 0, 0, (uint4 *)a, kBytes / 16);
         hipLaunchKernelGGL(wr<uint2>, grid, block, 0, 0, (uint2 *)a, kBytes / 8);
         hipLaunchKernelGGL(wr<uint32_t>, grid, block, 0, 0, (uint32_t *)a, kBytes / 4);
+        hipLaunchKernelGGL(wr8, grid, block, 0, 0, (uint8_t *)a, kBytes);
         CHECK(hipDeviceSynchronize());
     }
     CHECK(hipGetLastError());
