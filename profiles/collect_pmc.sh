@@ -15,7 +15,7 @@ for grp in \
   "SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY SQ_ACTIVE_INST_VALU SQ_LDS_BANK_CONFLICT SQ_INSTS_SMEM SQ_ACTIVE_INST_LDS GRBM_GUI_ACTIVE" \
   "FETCH_SIZE" "WRITE_SIZE"; do
   i=$((i+1))
-  timeout -s KILL 150 rocprofv3 --pmc $grp --kernel-include-regex 'k_small|k_pair|k_large|k_join|k_tie' --output-format csv \
+  timeout -s KILL 150 rocprofv3 --pmc $grp --kernel-include-regex 'k_small|k_large|k_join' --output-format csv \
       -d "$OUT/p$i" -o pmc -- python3 "$R/bench.py" $ARGS > "$OUT/p$i.log" 2>&1 || { echo "pass $i failed"; tail -5 "$OUT/p$i.log"; exit 1; }
   echo "pass $i ok"
 done

@@ -7,6 +7,9 @@ Their tag outputs are wrong by construction; the untagged instance is untouched.
   ollen:   the vote loop runs to the duplex length, not the single strands' longer one
   bare:    all three
   st1/st2/st3: the fast path's full-dword stores cut to ss_base / + ss_qual / + ss_depth
+  nocount: no per-column read counts in the fast path (depth stored as 0)
+(the st* variants edit the whole-dword stores of round 6; round 6's first ablation ran them on
+the byte-masked stores before it)
 Usage (CPU, this container): python profiles/tag_variants.py"""
 import os
 import subprocess
@@ -19,11 +22,12 @@ OUT = os.path.join(ROOT, "profiles", "_build")
 FAST = ("if (TAGS && c < lv) {", "if (false && TAGS && c < lv) {")
 QUEUE = ("if (TAGS) {  // this side's single-strand column", "if (false) {  // this side's single-strand column")
 OLLEN = ("const int lv = TAGS ? ::max(la, lb) : ol;", "const int lv = ol;")
-ST_Q = ("                            *reinterpret_cast<uint32_t *>(P.O.ss_qual + at) = qq;\n", "")
-ST_D = ("                            *reinterpret_cast<uint32_t *>(P.O.ss_depth + at) = n4;\n", "")
-ST_E = ("                            *reinterpret_cast<uint32_t *>(P.O.ss_err + at) = 0u;\n", "")
+ST_Q = ("                        *reinterpret_cast<uint32_t *>(P.O.ss_qual + at) = ss[2 * side + 1];\n", "")
+ST_D = ("                        *reinterpret_cast<uint32_t *>(P.O.ss_depth + at) = n4;\n", "")
+ST_E = ("                        *reinterpret_cast<uint32_t *>(P.O.ss_err + at) = 0u;\n", "")
+NOCOUNT = ("const uint32_t n4 = nf[side] + __builtin_bswap32(nr[side]);", "const uint32_t n4 = 0u;")
 VARIANTS = {"nofast": [FAST], "noqueue": [QUEUE], "ollen": [OLLEN], "bare": [FAST, QUEUE, OLLEN],
-            "st1": [ST_Q, ST_D, ST_E], "st2": [ST_D, ST_E], "st3": [ST_E]}
+            "st1": [ST_Q, ST_D, ST_E], "st2": [ST_D, ST_E], "st3": [ST_E], "nocount": [NOCOUNT]}
 
 
 def main():
