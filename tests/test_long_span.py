@@ -11,6 +11,7 @@ everything) byte for byte after decompression, and oracle/ on the whole file rec
 the stream's buffered bytes stay within a fixed multiple of chunk_bytes, where without deferral
 they grow to most of the file."""
 import gzip
+import json
 
 import numpy as np
 import pytest
@@ -81,6 +82,7 @@ def test_long_span_stream_is_bounded_and_exact(standin, tmp_path, cross):  # noq
     held, ref_bytes, _ = _stream(standin, tmp_path, p, fa, "held", defer=0)
     info, got, out = _stream(standin, tmp_path, p, fa, "defer", defer=1000)
     assert info["spilled_bytes"] > 0 and info["spliced_families"] > 40
+    json.dumps(info)  # (the CLI prints it: plain numbers only)
     for a, b in zip(got, ref_bytes):  # (BAM and the FASTQ pair decompress to the same bytes)
         assert a == b
     for k in ("families", "families_emitted", "records_out", "records_in"):
