@@ -5,7 +5,8 @@
 # truncated and malformed BAMs (tests/test_bam.py), family formation (tests/test_families.py, and
 # the C++ family formation bsdc_host.cpp against its numpy statement, tests/test_host_plan.py),
 # the golden fixtures (tests/test_oracle_golden.py), the BGZF restatement and the writer's
-# GPU-compressed path with its CPU stand-in (tests/test_bgzf.py) -- loaded against the instrumented builds.
+# GPU-compressed path with its CPU stand-in (tests/test_bgzf.py), the stream with deferred far templates
+# (tests/test_long_span.py) and the rank processes (tests/test_ranks.py) -- loaded against the instrumented builds.
 # CPU only (GPU sanitizers are not available on the MI355X pool).  Usage: tests/sanitize/run.sh
 set -euo pipefail
 ROOT="$(cd "$(dirname "$0")/../.." && pwd)"
@@ -32,4 +33,4 @@ assert '$OUT/libbsdc_io.so' in maps and '$OUT/liboracle.so' in maps, 'instrument
 print('sanitizer builds loaded:', '$OUT')
 "
 python -m pytest -q -p no:cacheprovider tests/test_bam.py tests/test_families.py tests/test_oracle_golden.py \
-    tests/test_host_plan.py tests/test_bgzf.py tests/test_stream.py tests/test_long_span.py "$@"
+    tests/test_host_plan.py tests/test_bgzf.py tests/test_stream.py tests/test_long_span.py tests/test_ranks.py "$@"
