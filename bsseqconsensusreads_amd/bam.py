@@ -1348,6 +1348,21 @@ def _family_cuts(cons, raw, plan, splices, strict: bool, start: int = 0):
     return out, j
 
 
+def _region_cuts(cons, raw, plan, prev: list) -> list:
+    """Output record indices where a chunk's output is cut before the first family of each new key
+    contig pair (a family's key: its first record's coarse key), keyed (pair, MINKEY); prev[0] =
+    the pair of the family before the chunk (at first: that of the range's first piece's key)."""
+    first = plan.order[plan.fam_off[:-1]]
+    k0 = raw.tc_key[first, 0]
+    em = np.zeros(k0.shape[0] + 1, np.int64)
+    em[1:] = np.cumsum((cons.status & 1) != 0)
+    before = np.empty_like(k0)
+    before[0] = k0[0] if prev[0] is None else prev[0]
+    before[1:] = k0[:-1]
+    prev[0] = int(k0[-1])
+    return [(2 * int(em[f]), (int(k0[f]), MINKEY)) for f in np.nonzero(k0 != before)[0]]
+
+
 def _slice_records(recs: "OutRecordsBam", a: int, b: int) -> "OutRecordsBam":
     """Records a..b-1 as views (the encoders index the ragged fields by absolute offsets)."""
     return OutRecordsBam(flag=recs.flag[a:b], tid=recs.tid[a:b], pos=recs.pos[a:b], mapq=recs.mapq[a:b],
@@ -1413,7 +1428,7 @@ def _stream_step(in_bam: str, fasta: Optional[str], out_bam: Optional[str], engi
                  molecular: Optional[int], rng=None, fragment: Optional[str] = None, runner=None,
                  range_stats: Optional[dict] = None, owner=None, spill: Optional[str] = None,
                  marks: Optional[list] = None, defer: Optional[int] = None, late_splices=None,
-                 first_key=None, read_size: int = 8 << 20) -> dict:
+                 first_key=None, read_size: int = 8 << 20, regions: bool = False) -> dict:
     """step5 (molecular None) or step 1 (molecular = its --min-consensus-base-quality) in bounded
     memory, pipelined: a decoder thread cuts the next chunk of the
     coordinate-sorted input (stream_bam: inflate, split where no template or MI family straddles),
@@ -1441,7 +1456,10 @@ def _stream_step(in_bam: str, fasta: Optional[str], out_bam: Optional[str], engi
     stand-in of the tests) instead of an Engine, owner = the rank's key interval (stream_chunks),
     spill = the file the deferred records go to, marks = a list that receives the output's cut
     points ((BAM offset, FASTQ offsets x 2), sort key of the piece that starts there): ranks.py
-    runs the second pass and the assembly; first_key = the sort key of the rank's first piece."""
+    runs the second pass and the assembly; first_key = the sort key of the rank's first piece;
+    regions (the ranks' passes) = also cut before the first family of every new key contig pair
+    (a piece keyed (pair, MINKEY)): a rank does not register cross keys (bsdc_io.cpp), so the
+    deferred families of a contig's cross keys go between those pieces."""
     import queue
     import threading
     import time
@@ -1467,12 +1485,14 @@ def _stream_step(in_bam: str, fasta: Optional[str], out_bam: Optional[str], engi
     dspan = 0 if molecular is not None else (DEFAULT_DEFER_SPAN if defer is None else int(defer))
     late = None if late_splices is None else np.asarray(late_splices, np.int64).reshape(-1, 2)
     lj = [0]  # (the spill's pass: the first deferred key not yet cut at)
+    rk_prev = [None]  # (regions: the key contig pair of the last family written; set with k_first)
     tie = 0 if late is not None else 1  # (a spill piece sorts before the stream's piece of its key)
     solo = marks is None and late is None  # this call runs the spill's pass and the assembly itself
     mk = [] if marks is None else marks
     frag = "first" if (solo and dspan) else fragment
     # (the spill pass's first piece, before its first key, is empty: after the header in any case)
     k_first = tuple(first_key) if first_key is not None else (MINKEY, 0, 2 if late is not None else 1)
+    rk_prev[0] = int(k_first[0])  # (a range whose first family lies in a later contig pair: cut before it)
     out0 = out_bam if out_bam is not None else fastq[0]
     spill_path = spill if spill is not None else \
         (os.path.join(os.path.dirname(os.path.abspath(out0)), ".%s.%d.%x.spill" % (os.path.basename(out0), os.getpid(),
@@ -1737,6 +1757,8 @@ def _stream_step(in_bam: str, fasta: Optional[str], out_bam: Optional[str], engi
                 elif getattr(raw, "_splices", None) is not None and raw._splices.shape[0]:
                     cuts, _ = _family_cuts(cons, raw, plan, raw._splices, True)
                     info["splices"].append(raw._splices)
+                if regions and cons.status.shape[0]:
+                    cuts = sorted(cuts + _region_cuts(cons, raw, plan, rk_prev))
                 outs.put((cons, raw, cuts))
         except BaseException:
             stop.set()

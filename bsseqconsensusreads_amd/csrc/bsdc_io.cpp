@@ -1554,8 +1554,13 @@ int32_t stream_split(bsdc_bam_stream *s) {
             f = q.mi.empty() ? -1 : find_fam(s, q.mi, q.h);
             if (f < 0) {
                 // the template's key comes with its lower record (the other one finds it registered);
-                // a record whose lower record never came registers it if still ahead of the output
-                if (owned[(size_t)k] && (q.own || !s->dreg.count(q.key))) {
+                // a record whose lower record never came registers it if still ahead of the output.
+                // A rank registers no cross key (its lower record may lie in an earlier rank's core,
+                // and the key sorts at its contig's end, past this rank's output by the time the
+                // upper record comes): a rank's output is cut at every change of the key's contig
+                // pair instead (bam._stream_step regions), which is where those families go.
+                const bool cross = (q.key.first >> 32) != (q.key.first & 0xFFFFFFFFll);
+                if (owned[(size_t)k] && !(cross && s->own_rank >= 0) && (q.own || !s->dreg.count(q.key))) {
                     const int32_t rc = defer_key(s, q.key);
                     if (rc != 0) return rc;
                     s->dreg.insert(q.key);

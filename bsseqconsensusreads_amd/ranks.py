@@ -97,7 +97,8 @@ def _run_job(r: int, eng, runner, job: dict) -> tuple:
                                 fragment=job["fragment"], runner=runner, range_stats=rs,
                                 owner=(r, job["cuts"], job["flags"]) if job["cuts"] else None, spill=job["spill"],
                                 marks=marks, defer=job["defer"], late_splices=job.get("late"),
-                                first_key=job.get("first_key"), read_size=job.get("read_size", 8 << 20))
+                                first_key=job.get("first_key"), read_size=job.get("read_size", 8 << 20),
+                                regions=True)
     except OSError as e:
         if "foreign record" in str(e):
             return ("foreign", r, str(e))

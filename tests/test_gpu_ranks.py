@@ -92,3 +92,16 @@ def test_cli_long_span_templates(long_gpu_input):  # noqa: F811
     assert info["ranks"] == 2 and not info["cuts_fallback"] and info["deferred_records"] > 100
     got = [gzip.decompress((tmp / ("L2%s" % x)).read_bytes()) for x in (".bam", "1.fq.gz", "2.fq.gz")]
     assert got == one
+
+
+def test_cli_many_contigs(tmp_path_factory):
+    """Seven contigs with mates across them and long-span templates (tests/test_many_contigs.py's
+    input) on the GPU: one GPU, and two ranks on GPU 0 whose key intervals each span several
+    contigs, decompress to the same bytes, equal to oracle/ on the whole file"""
+    from test_many_contigs import _contigs_input
+    raw, inp, fa, tmp, cross = _contigs_input(tmp_path_factory.mktemp("contigsgpu"))
+    assert cross > 20
+    one = [gzip.decompress(b) for b in _cli(tmp, inp, fa, "C_one")]
+    assert assert_bam_matches_oracle(str(tmp / "C_one.bam"), inp, fa, "cli one GPU, seven contigs") > 0
+    got = [gzip.decompress(b) for b in _cli(tmp, inp, fa, "C_two", "--gpus", "2", "--devices", "0,0")]
+    assert got == one

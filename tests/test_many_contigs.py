@@ -1,0 +1,103 @@
+"""Many contigs at once (the file path on a realistic header; VERDICT r5 "robustness of the file
+path on real inputs"): a C2 family set with 2% long-span templates, its genome cut into seven
+contigs of uneven length in gaps between reads, so that templates now also pair across contigs
+(mates on the next or a later contig) and far templates sit next to contig ends.  On the CPU with
+the oracle stand-in: the stream with deferral writes the bytes of the stream without it (which
+holds everything), those records equal oracle/ on the whole file, and three rank processes write
+the one-range bytes with no fallback."""
+import os
+
+import numpy as np
+import pytest
+
+from bsseqconsensusreads_amd import bam, synth
+from bsseqconsensusreads_amd import records as R
+from helpers import assert_bam_matches_oracle
+from test_long_span import _stream
+from test_ranks import _run
+from test_stream_pipeline import standin  # noqa: F401 -- (the fixture)
+
+READ = 16 << 10
+
+
+@pytest.fixture(scope="module")
+def contigs_input(tmp_path_factory):
+    return _contigs_input(tmp_path_factory.mktemp("contigs"))
+
+
+def _contigs_input(tmp):
+    s = synth.generate("C2", 2500, seed=31, device="cpu", genome_len=6_000_000, long_frac=0.02,
+                       long_span=(20_000, 2_500_000), long_giant=False)
+    raw = s.raw
+    glen = int(s.ref.contig_len[0])
+    # contig boundaries near these targets, moved into gaps no read covers
+    L = raw.l_seq.astype(np.int64) + 40  # (+ room for deletions)
+    cov = np.zeros(glen + 1, np.int32)
+    st = raw.pos.astype(np.int64)
+    np.add.at(cov, np.clip(st, 0, glen), 1)
+    np.add.at(cov, np.clip(st + L, 0, glen), -1)
+    covered = np.cumsum(cov)[:glen] > 0
+    bounds = [0]
+    for t in (700_000, 1_300_000, 2_900_000, 3_100_000, 4_400_000, 5_200_000):
+        g = t + int(np.argmax(~covered[t:]))
+        assert not covered[g]
+        bounds.append(g)
+    bounds.append(glen)
+    b = np.asarray(bounds, np.int64)
+    tid = np.searchsorted(b, st, side="right") - 1
+    mapped_mate = raw.next_pos.astype(np.int64) >= 0
+    ntid = np.where(mapped_mate, np.searchsorted(b, raw.next_pos.astype(np.int64), side="right") - 1, -1)
+    raw.tid = tid.astype(raw.tid.dtype)
+    raw.pos = (st - b[tid]).astype(raw.pos.dtype)
+    raw.next_tid = np.where(mapped_mate, ntid, raw.next_tid).astype(raw.next_tid.dtype)
+    raw.next_pos = np.where(mapped_mate, raw.next_pos.astype(np.int64) - b[np.maximum(ntid, 0)],
+                            raw.next_pos).astype(raw.next_pos.dtype)
+    raw.tlen = np.where(mapped_mate & (ntid != tid), 0, raw.tlen).astype(raw.tlen.dtype)
+    codes = R.unpack_nibbles(s.ref.packed, s.ref.n_nibbles)[:glen]
+    names = ["chr%d" % (i + 1) for i in range(len(b) - 1)]
+    seqs = {n: R.NT16_TO_ASCII[codes[b[i]:b[i + 1]]].tobytes() for i, n in enumerate(names)}
+    ref = R.Reference.from_contigs(names, seqs, keep_letters=False)
+    raw = R.take(raw, np.lexsort((raw.pos, raw.tid)))
+    text = "@HD\tVN:1.6\tSO:coordinate\n" + "".join("@SQ\tSN:%s\tLN:%d\n" % (n, len(seqs[n])) for n in names) \
+        + "@RG\tID:A\tSM:s\tLB:L\n"
+    hdr = bam.BamHeader(text, names, np.asarray([len(seqs[n]) for n in names], np.int64))
+    p = str(tmp / "in.bam")
+    bam.write_bam(p, hdr, bam.records_to_bam(raw), level=1, threads=4)
+    fa = str(tmp / "g.fa")
+    with open(fa, "wb") as fh:
+        for n in names:
+            fh.write((">%s\n" % n).encode() + seqs[n] + b"\n")
+    cross = int(((raw.next_tid >= 0) & (raw.next_tid != raw.tid)).sum())
+    return raw, p, fa, tmp, cross
+
+
+def test_many_contigs_stream_exact(standin, contigs_input):  # noqa: F811
+    raw, p, fa, tmp, cross = contigs_input
+    assert cross > 20  # (templates pair across the new contig boundaries)
+    held, ref_bytes, _ = _stream(standin, tmp, p, fa, "mc_held", defer=0)
+    info, got, out = _stream(standin, tmp, p, fa, "mc_defer", defer=1000)
+    assert info["spilled_bytes"] > 0
+    for a, b in zip(got, ref_bytes):
+        assert a == b
+    assert assert_bam_matches_oracle(out, p, fa, "stream, seven contigs") > 0
+
+
+@pytest.fixture(scope="module")
+def one_range_bytes(contigs_input):
+    raw, p, fa, tmp, _ = contigs_input
+    return _run(tmp, p, fa, "mc1", 1, read_size=READ)[2]
+
+
+@pytest.mark.parametrize("n", [2, 3])
+def test_many_contigs_ranks_equal_one_range(contigs_input, one_range_bytes, n):
+    """A rank whose key interval spans several contigs owns the cross keys of a contig whose lower
+    records an earlier rank read: before round 6's region cuts this failed ("lower record missing
+    or behind the output")"""
+    raw, p, fa, tmp, _ = contigs_input
+    info, st, got, out = _run(tmp, p, fa, "mc%d" % n, n, read_size=READ)
+    assert info["ranks"] == n and not info["cuts_fallback"]
+    for a, b in zip(got, one_range_bytes):
+        assert a == b
+    assert not [f for f in os.listdir(tmp) if f.startswith(".")], "pieces left behind"
+    if n == 3:
+        assert assert_bam_matches_oracle(out, p, fa, "ranks, seven contigs") > 0
