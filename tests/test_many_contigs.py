@@ -88,7 +88,7 @@ def one_range_bytes(contigs_input):
     return _run(tmp, p, fa, "mc1", 1, read_size=READ)[2]
 
 
-@pytest.mark.parametrize("n", [2, 3])
+@pytest.mark.parametrize("n", [2, 3, 5])
 def test_many_contigs_ranks_equal_one_range(contigs_input, one_range_bytes, n):
     """A rank whose key interval spans several contigs owns the cross keys of a contig whose lower
     records an earlier rank read: before round 6's region cuts this failed ("lower record missing
