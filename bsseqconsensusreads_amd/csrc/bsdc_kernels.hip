@@ -1827,11 +1827,9 @@ struct PartSums {
     }
     int32_t *one;   // the sum of a column whose reads show one base (its count byte the only one set)
     // Without TAGS the parts keep no read counts: a column's OR of the A/C/G/T codes its reads show
-    // (u8, one-hot bits) is all the join needs.  It lives at the start of the column's count row
-    // (rows keep the counts' 4 x stride spacing)
-    __device__ __forceinline__ uint8_t *orb(int64_t at, int col) const {
-        return reinterpret_cast<uint8_t *>(cnt) + 4 * at - 3 * (int64_t)col;
-    }
+    // (u8, one-hot bits) is all the join needs.  The OR rows lie back to back at the count region's
+    // start (a part's four 150-B rows in five lines: spaced like the counts, each row took two)
+    __device__ __forceinline__ uint8_t *orb(int64_t at) const { return reinterpret_cast<uint8_t *>(cnt) + at; }
     __device__ __forceinline__ int64_t at(int64_t part, int s, int col) const { return (4 * part + s) * (int64_t)pitch + col; }
 };
 
@@ -2553,7 +2551,7 @@ __device__ void process_large(const KParams &P, uint8_t *A, uint8_t *s_tab, cons
                     if (TAGS)
                         *reinterpret_cast<uint4 *>(ps.cnt + at) = make_uint4(cnt4[0], cnt4[1], cnt4[2], cnt4[3]);
                     else
-                        *reinterpret_cast<uint32_t *>(ps.orb(at, c)) = or4;
+                        *reinterpret_cast<uint32_t *>(ps.orb(at)) = or4;
                     *reinterpret_cast<int4 *>(ps.one + at) = make_int4(one4[0], one4[1], one4[2], one4[3]);
                 }
             }
@@ -2824,7 +2822,7 @@ __device__ void join_family(const KParams &P, uint4 e0, uint4 e1, uint8_t *rows,
             return make_uint4(b == 0 ? (uint32_t)o : 0u, b == 1 ? (uint32_t)o : 0u, b == 2 ? (uint32_t)o : 0u,
                               b == 3 ? (uint32_t)o : 0u);
         };
-        auto rec = [&](int64_t at) { return TAGS ? ps.cnt[at] : (uint32_t)*ps.orb(at, c); };
+        auto rec = [&](int64_t at) { return TAGS ? ps.cnt[at] : (uint32_t)*ps.orb(at); };
         if (hl_lds) {
             // kJoinU parts' loads in flight, every load unconditional (a part past the set's end,
             // or past the family's parts, reads an in-range slot and is masked after; a one-base

@@ -112,8 +112,8 @@ typedef struct {
     int64_t split_partial_off;   /* scratch offset of the parts' sums: [part][8] int32 (set reads, set
                                     lengths), then [part][4][stride] int32x4 sums (slot k: the set's
                                     k-th multi-base column), [part][4][stride] u8x4 counts (without
-                                    BSDC_MODE_TAGS: byte 0..stride-1 of each count row holds the
-                                    column's OR of one-hot A/C/G/T codes instead), [part][4][stride]
+                                    BSDC_MODE_TAGS: the region's first [part][4][stride] bytes hold
+                                    the columns' ORs of one-hot A/C/G/T codes instead), [part][4][stride]
                                     int32 one-base sums (a multi-base column: its sums' slot k) */
 } bsdc_family_batch;
 
