@@ -134,3 +134,30 @@ def test_spill_entries_sort_back_to_file_order():
     assert n == 300 and got == b"".join(e[3] for e in order)
     with pytest.raises(ValueError):
         bam.spill_sorted_records(data[:-5])
+
+
+def test_long_span_stream_c4_giant_families(standin, tmp_path):  # noqa: F811
+    """C4's skewed families (up to hundreds of templates per molecule) with 3% long-span templates:
+    a deferred template whose molecule is large joins or defers with it whole; the stream's bytes
+    equal the stream without deferral and oracle/"""
+    s = synth.generate("C4", 800, seed=11, device="cpu", genome_len=4_000_000, long_frac=0.03,
+                       long_span=(20_000, 1_500_000), long_giant=True)
+    raw = R.take(s.raw, np.lexsort((s.raw.pos, s.raw.tid)))
+    ref = s.ref
+    text = "@HD\tVN:1.6\tSO:coordinate\n" + "".join("@SQ\tSN:%s\tLN:%d\n" % (n, l) for n, l in
+                                                    zip(ref.names, ref.lengths)) + "@RG\tID:A\tSM:s\tLB:L\n"
+    hdr = bam.BamHeader(text, list(ref.names), np.asarray(ref.lengths, np.int64))
+    p = str(tmp_path / "in.bam")
+    bam.write_bam(p, hdr, bam.records_to_bam(raw), level=1, threads=4)
+    fa = str(tmp_path / "g.fa")
+    codes = R.unpack_nibbles(ref.packed, ref.n_nibbles)
+    with open(fa, "wb") as fh:
+        for i, n in enumerate(ref.names):
+            o, ln = int(ref.contig_off[i]), int(ref.contig_len[i])
+            fh.write((">%s\n" % n).encode() + R.NT16_TO_ASCII[codes[o:o + ln]].tobytes() + b"\n")
+    held, ref_bytes, _ = _stream(standin, tmp_path, p, fa, "held", defer=0)
+    info, got, out = _stream(standin, tmp_path, p, fa, "defer", defer=1000)
+    assert info["spilled_bytes"] > 0
+    for a, b in zip(got, ref_bytes):
+        assert a == b
+    assert assert_bam_matches_oracle(out, p, fa, "stream, C4 long-span") > 0
