@@ -2835,8 +2835,11 @@ __device__ void join_family(const KParams &P, uint4 e0, uint4 e1, uint8_t *rows,
                 for (int u = 0; u < kJoinU; u++) {
                     const int pc = ::min(pb + u, np - 1);
                     in[u] = pb + u < np && c < (int)hl[s * kJoinParts + pc];
-                    m[u] = rec(ps.at(p0 + pc, s, c));
-                    o[u] = ps.one[ps.at(p0 + pc, s, c)];
+                    // a lane past the part's set length reads the row's first column instead of
+                    // bytes the part never wrote (a line each: 70 MB of C4's join reads)
+                    const int cc = in[u] ? c : 0;
+                    m[u] = rec(ps.at(p0 + pc, s, cc));
+                    o[u] = ps.one[ps.at(p0 + pc, s, cc)];
                 }
                 uint4 sm[kJoinU];
 #pragma unroll
