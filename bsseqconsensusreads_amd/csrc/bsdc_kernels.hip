@@ -48,6 +48,26 @@ constexpr int kWave = 64;
 #define SMALL_STAGE_U 4  // k_small staging: image chunk loads in flight per lane
 #endif
 constexpr int kStageU = SMALL_STAGE_U;
+// Wave priority (s_setprio) while a wavefront issues its first global loads: from the kernel's table
+// loads until its family's reference-window loads are out, then back to 0 (profiles/r06/README.md,
+// prio/: C2 2.99 -> 2.93 ms, tag leg 3.39 -> 3.29).  The loads leave before other waves' LDS and VALU
+// work, so more of the HBM latency overlaps; holding the priority through the wait for the data
+// gains nothing.  1: from the family's metadata loads on (about two thirds of the gain); 0: off.
+#ifndef SMALL_PRIO
+#define SMALL_PRIO 2
+#endif
+#ifndef SMALL_PRIO_PACK
+#define SMALL_PRIO_PACK 0  // A/B arm: the output pack and stores at the raised priority too
+#endif
+#ifndef SMALL_PRIO_LEVEL
+#define SMALL_PRIO_LEVEL 3  // the raised priority (1..3: 1 measured the same)
+#endif
+#ifndef SMALL_PRIO_END
+#define SMALL_PRIO_END 1  // where it drops back to 0: 0 after the image loads (less gain), 1 after the window loads, 2 after staging (no gain)
+#endif
+#ifndef LARGE_PRIO
+#define LARGE_PRIO 1  // k_large's staging loads issue at wave priority 3 (C3 -0.3%, C4 -1%); 2: its convert's reference loads too (no further gain); 0: off
+#endif
 #ifndef SMALL_QDMA
 #define SMALL_QDMA 1  // k_small stages the quals with LDS-DMA (global_load_lds_dwordx4); 0: through VGPRs
 #endif
@@ -926,6 +946,7 @@ __device__ __forceinline__ void small_family(const KParams &P, const Tables *T, 
     // reference windows.  Metadata loads go first so the window loads (whose addresses they hold)
     // are issued while the image chunks are still in flight; up to 4 chunk loads per lane per
     // round ----
+    if (SMALL_PRIO == 1) __builtin_amdgcn_s_setprio(SMALL_PRIO_LEVEL);
     const bool has = t < n;
     uint4 rc = make_uint4(0, 0, 0, 0);
     uint2 win = make_uint2(0, 0);
@@ -975,6 +996,7 @@ __device__ __forceinline__ void small_family(const KParams &P, const Tables *T, 
     uint4 v[kStageU];
 #pragma unroll
     for (int u = 0; u < kStageU; u++) v[u] = load_img(kmap(u));
+    if (SMALL_PRIO && SMALL_PRIO_END == 0) __builtin_amdgcn_s_setprio(0);
 
     const uint32_t gslot = rc.x;
     int32_t pos = (int32_t)rc.y;
@@ -1026,6 +1048,7 @@ __device__ __forceinline__ void small_family(const KParams &P, const Tables *T, 
     uint4 wv[2];
 #pragma unroll
     for (int u = 0; u < 2; u++) wv[u] = load_win(t + 64 * u);
+    if (SMALL_PRIO && SMALL_PRIO_END == 1) __builtin_amdgcn_s_setprio(0);  // (every first-round load is issued)
 #pragma unroll
     for (int u = 0; u < kStageU; u++) store_img(kmap(u), v[u]);
     const int ub = (nch - nqc + 63) >> 6;  // rounds of base chunks
@@ -1052,6 +1075,7 @@ __device__ __forceinline__ void small_family(const KParams &P, const Tables *T, 
     }
 #endif
     wave_sync();
+    if (SMALL_PRIO && SMALL_PRIO_END == 2) __builtin_amdgcn_s_setprio(0);
     if (stop == 1) return;
 
     // ---- tool 1: every converted record at once -- 16 lanes per record, 4 positions per lane per
@@ -1604,6 +1628,7 @@ __device__ __forceinline__ void small_family(const KParams &P, const Tables *T, 
             }
         }
         wave_sync();
+        if (SMALL_PRIO_PACK) __builtin_amdgcn_s_setprio(SMALL_PRIO_LEVEL);  // (A/B arm)
         // pack and store: lanes 0-31 end 0, lanes 32-63 end 1, 8 columns per lane
         if (stop != 7 && stop != 8) {
             const int e = t >> 5;
@@ -1646,6 +1671,7 @@ __global__ __launch_bounds__(kWave *kSmallMaxWaves, kSmallMinWaves) __attribute_
     extern __shared__ __attribute__((aligned(16))) uint8_t smem[];  // the wavefronts' arenas
     __shared__ __attribute__((aligned(16))) Tables s_tab;           // static: its address folds into offsets
     if (((P.mode >> BSDC_MODE_STOP_SHIFT) & 15) == 15) return;  // profiling: launch cost alone
+    if (SMALL_PRIO == 2) __builtin_amdgcn_s_setprio(SMALL_PRIO_LEVEL);  // (from the table loads on)
     load_tables<kTabBytes>(&P.tab->t, reinterpret_cast<uint8_t *>(&s_tab));
     if (((P.mode >> BSDC_MODE_STOP_SHIFT) & 15) == 14) return;  // profiling: + the table copy
     const int w = threadIdx.x >> 6;
@@ -1884,6 +1910,7 @@ __device__ void process_large(const KParams &P, uint8_t *A, uint8_t *s_tab, cons
     auto chunk_of = [&](int i) { return i; };
     const int nreg = nch;
     uint4 v[kLStageU];
+    if (LARGE_PRIO) __builtin_amdgcn_s_setprio(3);
 #pragma unroll
     for (int u = 0; u < kLStageU; u++)
         if (tt + u * G < nreg) v[u] = load_chunk(chunk_of(tt + u * G));
@@ -1933,6 +1960,7 @@ __device__ void process_large(const KParams &P, uint8_t *A, uint8_t *s_tab, cons
     }
     int cops, maxlen_f;
     block_sum_max<G>(c, ml, red, cops, maxlen_f);  // (its barrier publishes the arena and the tables)
+    if (LARGE_PRIO) __builtin_amdgcn_s_setprio(0);
     const ArenaLayout Lo(n, 2 * (int64_t)img, maxlen_f, cops);
     uint16_t *lists = reinterpret_cast<uint16_t *>(A + Lo.lists);
     uint8_t *ssb = A + Lo.ssb;
@@ -1954,6 +1982,7 @@ __device__ void process_large(const KParams &P, uint8_t *A, uint8_t *s_tab, cons
         const int total = nc * SD;
         constexpr int kConvU = kLConvU;  // tasks per thread per round: their global loads go out together
         for (int base = 0; base < total; base += kConvU * G) {
+            if (LARGE_PRIO >= 2) __builtin_amdgcn_s_setprio(3);  // (the reference loads' issue)
             int rr[kConvU], jj[kConvU], av[kConvU];
             uint32_t w0[kConvU], w1[kConvU];
 #pragma unroll
@@ -1976,6 +2005,7 @@ __device__ void process_large(const KParams &P, uint8_t *A, uint8_t *s_tab, cons
                     }
                 }
             }
+            if (LARGE_PRIO >= 2) __builtin_amdgcn_s_setprio(0);
             uint32_t out[kConvU][H], wa[kConvU][H];
             bool ok[kConvU][H];
 #pragma unroll
