@@ -71,6 +71,10 @@ constexpr int kStageU = SMALL_STAGE_U;
 #ifndef SMALL_QDMA
 #define SMALL_QDMA 1  // k_small stages the quals with LDS-DMA (global_load_lds_dwordx4); 0: through VGPRs
 #endif
+#ifndef SMALL_TAB_DMA
+#define SMALL_TAB_DMA 0  // A/B arm: the tables by LDS-DMA, published by a barrier at the end of staging
+#endif
+static_assert(!SMALL_TAB_DMA || SMALL_QDMA, "the table barrier sits at the qual DMA's wait");
 #ifndef LARGE_THREADS
 #define LARGE_THREADS 256  // k_large workgroup size (a multiple of 64)
 #endif
@@ -1067,8 +1071,11 @@ __device__ __forceinline__ void small_family(const KParams &P, const Tables *T, 
         for (int u = 0; u < 2; u++) store_win(k0 + t + 64 * u, wv[u]);
     }
 #if SMALL_QDMA
-    __asm__ volatile("s_waitcnt vmcnt(0)" ::: "memory");  // the DMA'd quals have landed
-    wave_sync();
+    __asm__ volatile("s_waitcnt vmcnt(0)" ::: "memory");  // the DMA'd quals (and table share) have landed
+    if (SMALL_TAB_DMA)
+        __syncthreads();  // every wavefront's share of the tables (k_small; each wave reaches it once)
+    else
+        wave_sync();
     for (int k = t; k < nqc; k += 64) {
         const uint4 q = *reinterpret_cast<const uint4 *>(qimg + 16 * k);
         qor |= q.x | q.y | q.z | q.w;
@@ -1672,15 +1679,34 @@ __global__ __launch_bounds__(kWave *kSmallMaxWaves, kSmallMinWaves) __attribute_
     __shared__ __attribute__((aligned(16))) Tables s_tab;           // static: its address folds into offsets
     if (((P.mode >> BSDC_MODE_STOP_SHIFT) & 15) == 15) return;  // profiling: launch cost alone
     if (SMALL_PRIO == 2) __builtin_amdgcn_s_setprio(SMALL_PRIO_LEVEL);  // (from the table loads on)
-    load_tables<kTabBytes>(&P.tab->t, reinterpret_cast<uint8_t *>(&s_tab));
-    if (((P.mode >> BSDC_MODE_STOP_SHIFT) & 15) == 14) return;  // profiling: + the table copy
     const int w = threadIdx.x >> 6;
     const int t = threadIdx.x & 63;
     const int64_t fi = (int64_t)blockIdx.x * (blockDim.x >> 6) + w;
+#if SMALL_TAB_DMA
+    // each wavefront copies its share of the tables by LDS-DMA and goes straight on to its family's
+    // loads; the workgroup barrier that publishes the copy is at the end of staging (small_family),
+    // so the tables' latency hides under the family's own
+    {
+        constexpr int kChunks = kTabBytes / 16;
+        const int nw = (int)(blockDim.x >> 6);
+        const uint8_t *src = reinterpret_cast<const uint8_t *>(&P.tab->t);
+        uint8_t *dst = reinterpret_cast<uint8_t *>(&s_tab);
+        for (int k0 = 64 * w; k0 < kChunks; k0 += 64 * nw)
+            if (k0 + t < kChunks) glds16(src + 16 * (k0 + t), dst + 16 * k0);
+    }
+#else
+    load_tables<kTabBytes>(&P.tab->t, reinterpret_cast<uint8_t *>(&s_tab));
+#endif
+    if (((P.mode >> BSDC_MODE_STOP_SHIFT) & 15) == 14) return;  // profiling: + the table copy
     // (the arenas start kArenaGuard bytes into smem: a dword load that straddles the start of a
     // family image -- its bytes before the image masked -- stays inside the allocation)
     uint8_t *A = smem + kArenaGuard + (size_t)w * (size_t)arena;
-    if (fi < nfams) small_family<TAGS>(P, &s_tab, A, fams, fi, t);
+    if (fi < nfams) {
+        small_family<TAGS>(P, &s_tab, A, fams, fi, t);
+    } else if (SMALL_TAB_DMA) {  // (no family: the staging barrier all the same)
+        __asm__ volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        __syncthreads();
+    }
 }
 
 // ==========================================================================================
