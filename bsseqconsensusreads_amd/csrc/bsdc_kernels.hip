@@ -52,12 +52,10 @@ constexpr int kStageU = SMALL_STAGE_U;
 // loads until its family's reference-window loads are out, then back to 0 (profiles/r06/README.md,
 // prio/: C2 2.99 -> 2.93 ms, tag leg 3.39 -> 3.29).  The loads leave before other waves' LDS and VALU
 // work, so more of the HBM latency overlaps; holding the priority through the wait for the data
-// gains nothing.  1: from the family's metadata loads on (about two thirds of the gain); 0: off.
+// gains nothing, nor does the output pack at the raised priority.  1: from the family's metadata loads
+// on (about two thirds of the gain); 0: off.
 #ifndef SMALL_PRIO
 #define SMALL_PRIO 2
-#endif
-#ifndef SMALL_PRIO_PACK
-#define SMALL_PRIO_PACK 0  // A/B arm: the output pack and stores at the raised priority too
 #endif
 #ifndef SMALL_PRIO_LEVEL
 #define SMALL_PRIO_LEVEL 3  // the raised priority (1..3: 1 measured the same)
@@ -66,15 +64,11 @@ constexpr int kStageU = SMALL_STAGE_U;
 #define SMALL_PRIO_END 1  // where it drops back to 0: 0 after the image loads (less gain), 1 after the window loads, 2 after staging (no gain)
 #endif
 #ifndef LARGE_PRIO
-#define LARGE_PRIO 1  // k_large's staging loads issue at wave priority 3 (C3 -0.3%, C4 -1%); 2: its convert's reference loads too (no further gain); 0: off
+#define LARGE_PRIO 1  // k_large's staging loads issue at wave priority 3 (C3 -0.3%, C4 -1%; its convert's reference loads too: no more); 0: off
 #endif
 #ifndef SMALL_QDMA
 #define SMALL_QDMA 1  // k_small stages the quals with LDS-DMA (global_load_lds_dwordx4); 0: through VGPRs
 #endif
-#ifndef SMALL_TAB_DMA
-#define SMALL_TAB_DMA 0  // A/B arm: the tables by LDS-DMA, published by a barrier at the end of staging
-#endif
-static_assert(!SMALL_TAB_DMA || SMALL_QDMA, "the table barrier sits at the qual DMA's wait");
 #ifndef LARGE_THREADS
 #define LARGE_THREADS 256  // k_large workgroup size (a multiple of 64)
 #endif
@@ -1071,11 +1065,8 @@ __device__ __forceinline__ void small_family(const KParams &P, const Tables *T, 
         for (int u = 0; u < 2; u++) store_win(k0 + t + 64 * u, wv[u]);
     }
 #if SMALL_QDMA
-    __asm__ volatile("s_waitcnt vmcnt(0)" ::: "memory");  // the DMA'd quals (and table share) have landed
-    if (SMALL_TAB_DMA)
-        __syncthreads();  // every wavefront's share of the tables (k_small; each wave reaches it once)
-    else
-        wave_sync();
+    __asm__ volatile("s_waitcnt vmcnt(0)" ::: "memory");  // the DMA'd quals have landed
+    wave_sync();
     for (int k = t; k < nqc; k += 64) {
         const uint4 q = *reinterpret_cast<const uint4 *>(qimg + 16 * k);
         qor |= q.x | q.y | q.z | q.w;
@@ -1635,7 +1626,6 @@ __device__ __forceinline__ void small_family(const KParams &P, const Tables *T, 
             }
         }
         wave_sync();
-        if (SMALL_PRIO_PACK) __builtin_amdgcn_s_setprio(SMALL_PRIO_LEVEL);  // (A/B arm)
         // pack and store: lanes 0-31 end 0, lanes 32-63 end 1, 8 columns per lane
         if (stop != 7 && stop != 8) {
             const int e = t >> 5;
@@ -1682,31 +1672,14 @@ __global__ __launch_bounds__(kWave *kSmallMaxWaves, kSmallMinWaves) __attribute_
     const int w = threadIdx.x >> 6;
     const int t = threadIdx.x & 63;
     const int64_t fi = (int64_t)blockIdx.x * (blockDim.x >> 6) + w;
-#if SMALL_TAB_DMA
-    // each wavefront copies its share of the tables by LDS-DMA and goes straight on to its family's
-    // loads; the workgroup barrier that publishes the copy is at the end of staging (small_family),
-    // so the tables' latency hides under the family's own
-    {
-        constexpr int kChunks = kTabBytes / 16;
-        const int nw = (int)(blockDim.x >> 6);
-        const uint8_t *src = reinterpret_cast<const uint8_t *>(&P.tab->t);
-        uint8_t *dst = reinterpret_cast<uint8_t *>(&s_tab);
-        for (int k0 = 64 * w; k0 < kChunks; k0 += 64 * nw)
-            if (k0 + t < kChunks) glds16(src + 16 * (k0 + t), dst + 16 * k0);
-    }
-#else
+    // (the tables by LDS-DMA with the barrier at the end of staging measured the same, 2.937 against
+    // 2.940 ms: profiles/r06/prio/)
     load_tables<kTabBytes>(&P.tab->t, reinterpret_cast<uint8_t *>(&s_tab));
-#endif
     if (((P.mode >> BSDC_MODE_STOP_SHIFT) & 15) == 14) return;  // profiling: + the table copy
     // (the arenas start kArenaGuard bytes into smem: a dword load that straddles the start of a
     // family image -- its bytes before the image masked -- stays inside the allocation)
     uint8_t *A = smem + kArenaGuard + (size_t)w * (size_t)arena;
-    if (fi < nfams) {
-        small_family<TAGS>(P, &s_tab, A, fams, fi, t);
-    } else if (SMALL_TAB_DMA) {  // (no family: the staging barrier all the same)
-        __asm__ volatile("s_waitcnt vmcnt(0)" ::: "memory");
-        __syncthreads();
-    }
+    if (fi < nfams) small_family<TAGS>(P, &s_tab, A, fams, fi, t);
 }
 
 // ==========================================================================================
@@ -2008,7 +1981,6 @@ __device__ void process_large(const KParams &P, uint8_t *A, uint8_t *s_tab, cons
         const int total = nc * SD;
         constexpr int kConvU = kLConvU;  // tasks per thread per round: their global loads go out together
         for (int base = 0; base < total; base += kConvU * G) {
-            if (LARGE_PRIO >= 2) __builtin_amdgcn_s_setprio(3);  // (the reference loads' issue)
             int rr[kConvU], jj[kConvU], av[kConvU];
             uint32_t w0[kConvU], w1[kConvU];
 #pragma unroll
@@ -2031,7 +2003,6 @@ __device__ void process_large(const KParams &P, uint8_t *A, uint8_t *s_tab, cons
                     }
                 }
             }
-            if (LARGE_PRIO >= 2) __builtin_amdgcn_s_setprio(0);
             uint32_t out[kConvU][H], wa[kConvU][H];
             bool ok[kConvU][H];
 #pragma unroll
