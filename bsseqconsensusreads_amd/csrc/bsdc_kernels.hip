@@ -1669,13 +1669,13 @@ __global__ __launch_bounds__(kWave *kSmallMaxWaves, kSmallMinWaves) __attribute_
     __shared__ __attribute__((aligned(16))) Tables s_tab;           // static: its address folds into offsets
     if (((P.mode >> BSDC_MODE_STOP_SHIFT) & 15) == 15) return;  // profiling: launch cost alone
     if (SMALL_PRIO == 2) __builtin_amdgcn_s_setprio(SMALL_PRIO_LEVEL);  // (from the table loads on)
-    const int w = threadIdx.x >> 6;
-    const int t = threadIdx.x & 63;
-    const int64_t fi = (int64_t)blockIdx.x * (blockDim.x >> 6) + w;
     // (the tables by LDS-DMA with the barrier at the end of staging measured the same, 2.937 against
     // 2.940 ms: profiles/r06/prio/)
     load_tables<kTabBytes>(&P.tab->t, reinterpret_cast<uint8_t *>(&s_tab));
     if (((P.mode >> BSDC_MODE_STOP_SHIFT) & 15) == 14) return;  // profiling: + the table copy
+    const int w = threadIdx.x >> 6;
+    const int t = threadIdx.x & 63;
+    const int64_t fi = (int64_t)blockIdx.x * (blockDim.x >> 6) + w;
     // (the arenas start kArenaGuard bytes into smem: a dword load that straddles the start of a
     // family image -- its bytes before the image masked -- stays inside the allocation)
     uint8_t *A = smem + kArenaGuard + (size_t)w * (size_t)arena;
