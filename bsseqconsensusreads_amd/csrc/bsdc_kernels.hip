@@ -64,7 +64,7 @@ constexpr int kStageU = SMALL_STAGE_U;
 #define SMALL_PRIO_END 1  // where it drops back to 0: 0 after the image loads (less gain), 1 after the window loads, 2 after staging (no gain)
 #endif
 #ifndef LARGE_PRIO
-#define LARGE_PRIO 1  // k_large's staging loads issue at wave priority 3 (C3 -0.3%, C4 -1%; its convert's reference loads too: no more); 0: off
+#define LARGE_PRIO 1  // k_large's staging loads issue at wave priority 3 (C3 -0.3%, C4 -1%; its convert's reference loads too, or from the kernel's entry, and k_join's table loads: no more); 0: off
 #endif
 #ifndef SMALL_QDMA
 #define SMALL_QDMA 1  // k_small stages the quals with LDS-DMA (global_load_lds_dwordx4); 0: through VGPRs
